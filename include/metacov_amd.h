@@ -1,0 +1,169 @@
+/*
+ * metacov_amd — MI355X (gfx950) per-base coverage engine, C ABI.
+ *
+ * Drop-in replacement for the arithmetic under the reference's pileup path:
+ *
+ *   metacov pileup (metacov/cli.py:49-108)
+ *     -> pileup.classic(bam, ref, start, end)      (metacov/pileup.py:9-26)
+ *        -> pysam AlignmentFile.pileup()  ->  htslib bam_plp / PileupColumn.n
+ *           (called at metacov/pileup.py:13; third-party, unpinned)
+ *        -> numpy min/max/median/std/mean/sorted()/sum  (pileup.py:18-26)
+ *
+ * and of the reference's only hand-written BAM read iterator
+ * (scan.AlignmentFileIterator, metacov/scan.pyx:188-294; decl scan.pxd:6-27),
+ * whose per-record callback protocol (ReadProcessor.process_read,
+ * scan.pxd:30-36) is replaced by a batched struct-of-arrays interface.
+ *
+ * Conventions
+ *  - every function returns int: 0 = ok, < 0 = error (MC_E_*); the message
+ *    of the last error on the calling thread is mc_last_error().
+ *  - callers own all host buffers; they are copied during the call.
+ *  - the library owns device buffers, inside an opaque mc_ctx (one per GPU).
+ *    A ctx is not thread-safe; distinct ctxs may be driven from distinct
+ *    host threads.  There is no CPU fallback: a ctx needs a HIP device.
+ *  - positions are 0-based; regions are half-open [start, end).
+ */
+#ifndef METACOV_AMD_H
+#define METACOV_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MC_OK            0
+#define MC_E_INVALID    -1   /* bad argument (null pointer, range, unsorted reads, ...) */
+#define MC_E_HIP        -2   /* HIP runtime error (no device, OOM, launch failure) */
+#define MC_E_IO         -3   /* file / BGZF / BAM format error */
+#define MC_E_STATE      -4   /* call out of order (e.g. stats before depth) */
+#define MC_E_RANGE      -5   /* value outside what the engine represents exactly */
+
+/* Per-region statistics, exact integers.  Everything classic() reports
+ * (pileup.py:18-26) follows from it:
+ *   min = min, max = max, sum = sum,
+ *   avg = round(sum / n, 2), std = round(sqrt((n*sumsq - sum^2) / n^2), 2),
+ *   med = (med_lo + med_hi) / 2 truncated (np.median then int()),
+ *   q23 = round(q23_sum / q23_cnt, 2)
+ * with med_lo = sorted[(n-1)/2], med_hi = sorted[n/2] and q23_sum the sum of
+ * sorted[n/4 .. n - n/4)  (pileup.py:24).  n == 0 marks an empty region
+ * (classic raises ValueError there). */
+typedef struct mc_region_stat {
+    int64_t  n;
+    int64_t  sum;
+    uint64_t sumsq;
+    int64_t  min;
+    int64_t  max;
+    int64_t  med_lo;
+    int64_t  med_hi;
+    int64_t  q23_sum;
+    int64_t  q23_cnt;
+} mc_region_stat;
+
+/* Kernel timings of the last mc_compute_depth / mc_region_stats calls, in
+ * milliseconds, from HIP events recorded on the ctx stream. */
+typedef struct mc_timings {
+    float cigar_ms;      /* K1: CIGAR -> span (0 when spans were given) */
+    float depth_ms;      /* K2: tile depth kernel */
+    float stats_ms;      /* K3: region histogram + reduction (+ finalize) */
+    float prepare_ms;    /* ingest: sortedness check, extents, tile index */
+    int64_t depth_launches;
+    int64_t stats_launches;
+} mc_timings;
+
+typedef struct mc_ctx mc_ctx;
+
+const char* mc_last_error(void);
+const char* mc_version(void);
+
+/* ---- context ------------------------------------------------------------ */
+int mc_ctx_create(int device, mc_ctx** out);
+int mc_ctx_destroy(mc_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL = own stream. */
+int mc_ctx_set_stream(mc_ctx* ctx, void* hip_stream);
+int mc_ctx_device(const mc_ctx* ctx, int* device);
+
+/* ---- inputs ------------------------------------------------------------- */
+/* Contig table: the BAM header's @SQ lengths (pysam bam.lengths,
+ * used at util.py:64-69).  Resets reads and depth. */
+int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths);
+
+/* Append coordinate-sorted pileup intervals (host pointers): read i covers
+ * [pos[i], pos[i] + span[i]) on contig tid[i].  These are the records the
+ * pileup "all" stepper keeps (flag & 0x704 == 0), span = reference length
+ * of the CIGAR (ops M/D/N/=/X), 1 for a mapped read with none.
+ * Replaces: per-record AlignmentFileIterator.cnext()/get_tid()/get_pos()
+ * (scan.pyx:213-283) feeding ReadProcessor.process_read (scan.pxd:35). */
+int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid,
+                 const int32_t* pos, const int32_t* span);
+
+/* Same, but the three arrays are already in this ctx's device memory
+ * (e.g. torch tensors); they are copied into the ctx. */
+int mc_add_reads_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,
+                        const int32_t* d_pos, const int32_t* d_span);
+
+/* Long-read / raw-CIGAR mode: spans are computed on the GPU (K1) from the
+ * BAM-packed CIGAR words (op in low 4 bits, length << 4) of each read,
+ * read i owning cigar[cig_off[i] .. cig_off[i+1]).  Host pointers. */
+int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid,
+                       const int32_t* pos, const int64_t* cig_off,
+                       const uint32_t* cigar);
+
+/* Validates order, computes contig extents (max of length and furthest
+ * read end) and the tile index.  Called by mc_compute_depth if needed. */
+int mc_prepare(mc_ctx* ctx);
+
+/* ---- compute ------------------------------------------------------------ */
+/* Per-position depth of every contig (K1 if needed, then K2). */
+int mc_compute_depth(mc_ctx* ctx);
+
+/* Copy depth[start, end) of contig tid to host (zeros past the extent). */
+int mc_get_depth(mc_ctx* ctx, int32_t tid, int64_t start, int64_t end, int32_t* out);
+
+/* Device pointer to the concatenated depth vector and each contig's offset
+ * into it (for zero-copy consumers, e.g. torch). */
+int mc_depth_device(mc_ctx* ctx, const int32_t** d_depth, int64_t* total_len);
+int mc_contig_offset(mc_ctx* ctx, int32_t tid, int64_t* offset, int64_t* extent);
+
+/* Region statistics (K3) for R regions; rows in input order.  Regions may
+ * overlap and may run past the contig end (those positions count as 0,
+ * as in pileup.py:11-16). */
+int mc_region_stats(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                    const int64_t* start, const int64_t* end,
+                    mc_region_stat* out);
+
+/* Same, writing the R rows into device memory (for an RCCL all-gather). */
+int mc_region_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                           const int64_t* start, const int64_t* end,
+                           mc_region_stat* d_out);
+
+/* Aligned bases (sum of spans) of the reads added so far. */
+int mc_aligned_bases(mc_ctx* ctx, int64_t* out);
+int mc_max_depth(mc_ctx* ctx, int32_t* out);
+int mc_get_timings(mc_ctx* ctx, mc_timings* out);
+int mc_synchronize(mc_ctx* ctx);
+
+/* ---- host BAM decoder (C++, multi-threaded BGZF inflate) ----------------
+ * Replaces the pysam/htslib read path the reference uses: AlignmentFile
+ * header (bam.references / bam.lengths, cli.py:80, util.py:64-69),
+ * IteratorRowAll over records (scan.pyx:204), and bam_cigar2rlen /
+ * bam_endpos for the pileup interval. */
+typedef struct mc_bam mc_bam;
+
+int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter,
+                int keep_cigar, mc_bam** out);
+int mc_bam_close(mc_bam* bam);
+int mc_bam_n_targets(const mc_bam* bam, int32_t* n);
+int mc_bam_target(const mc_bam* bam, int32_t i, const char** name, int64_t* length);
+/* records in the file / records kept by the flag filter (and tid >= 0) */
+int mc_bam_counts(const mc_bam* bam, int64_t* n_records, int64_t* n_kept,
+                  int64_t* n_mapped, int64_t* n_unmapped);
+int mc_bam_intervals(const mc_bam* bam, int32_t* tid, int32_t* pos, int32_t* span);
+/* keep_cigar only: total CIGAR words, then offsets (n_kept + 1) and words */
+int mc_bam_n_cigar_words(const mc_bam* bam, int64_t* n);
+int mc_bam_cigars(const mc_bam* bam, int64_t* cig_off, uint32_t* cigar);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* METACOV_AMD_H */

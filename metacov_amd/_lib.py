@@ -1,0 +1,119 @@
+"""ctypes binding of libmetacov_amd.so (declared in include/metacov_amd.h).
+
+The shared library is built in-tree (`python -m metacov_amd.build`) and is
+the ONLY compute path: there is no CPU fallback.  A missing library raises
+`LibraryNotBuilt`; a ctx on a machine without a HIP device raises
+`MetacovError` from `mc_ctx_create`.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("METACOV_AMD_LIB", os.path.join(HERE, "libmetacov_amd.so"))
+
+MC_OK = 0
+MC_E_INVALID = -1
+MC_E_HIP = -2
+MC_E_IO = -3
+MC_E_STATE = -4
+MC_E_RANGE = -5
+
+
+class MetacovError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+class LibraryNotBuilt(ImportError):
+    pass
+
+
+class RegionStat(ctypes.Structure):
+    """mc_region_stat (72 bytes)."""
+    _fields_ = [("n", ctypes.c_int64), ("sum", ctypes.c_int64), ("sumsq", ctypes.c_uint64),
+                ("min", ctypes.c_int64), ("max", ctypes.c_int64),
+                ("med_lo", ctypes.c_int64), ("med_hi", ctypes.c_int64),
+                ("q23_sum", ctypes.c_int64), ("q23_cnt", ctypes.c_int64)]
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [("cigar_ms", ctypes.c_float), ("depth_ms", ctypes.c_float),
+                ("stats_ms", ctypes.c_float), ("prepare_ms", ctypes.c_float),
+                ("depth_launches", ctypes.c_int64), ("stats_launches", ctypes.c_int64)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U32 = ctypes.c_uint32
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+_PU32 = ctypes.POINTER(ctypes.c_uint32)
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> argtypes (all return int unless listed in _RESTYPE)
+SIGNATURES = {
+    "mc_last_error": [],
+    "mc_version": [],
+    "mc_ctx_create": [ctypes.c_int, _PP],
+    "mc_ctx_destroy": [_P],
+    "mc_ctx_set_stream": [_P, _P],
+    "mc_ctx_device": [_P, ctypes.POINTER(ctypes.c_int)],
+    "mc_set_contigs": [_P, _I32, _P],
+    "mc_add_reads": [_P, _I64, _P, _P, _P],
+    "mc_add_reads_device": [_P, _I64, _P, _P, _P],
+    "mc_add_reads_cigar": [_P, _I64, _P, _P, _P, _P],
+    "mc_prepare": [_P],
+    "mc_compute_depth": [_P],
+    "mc_get_depth": [_P, _I32, _I64, _I64, _P],
+    "mc_depth_device": [_P, _PP, _PI64],
+    "mc_contig_offset": [_P, _I32, _PI64, _PI64],
+    "mc_region_stats": [_P, _I64, _P, _P, _P, _P],
+    "mc_region_stats_device": [_P, _I64, _P, _P, _P, _P],
+    "mc_aligned_bases": [_P, _PI64],
+    "mc_max_depth": [_P, _PI32],
+    "mc_get_timings": [_P, ctypes.POINTER(Timings)],
+    "mc_synchronize": [_P],
+    "mc_bam_open": [ctypes.c_char_p, ctypes.c_int, _U32, ctypes.c_int, _PP],
+    "mc_bam_close": [_P],
+    "mc_bam_n_targets": [_P, _PI32],
+    "mc_bam_target": [_P, _I32, ctypes.POINTER(ctypes.c_char_p), _PI64],
+    "mc_bam_counts": [_P, _PI64, _PI64, _PI64, _PI64],
+    "mc_bam_intervals": [_P, _P, _P, _P],
+    "mc_bam_n_cigar_words": [_P, _PI64],
+    "mc_bam_cigars": [_P, _P, _P],
+}
+_RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p}
+
+_lib = None
+
+
+def load():
+    """Loads the library once; raises LibraryNotBuilt if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LibraryNotBuilt(
+            "%s not found: build it with `python -m metacov_amd.build` "
+            "(hipcc --offload-arch=gfx950). metacov_amd has no CPU fallback." % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != MC_OK:
+        msg = load().mc_last_error()
+        raise MetacovError(rc, msg.decode() if msg else "error")
+    return rc
+
+
+def ptr(arr):
+    """ctypes pointer of a C-contiguous numpy array."""
+    return ctypes.c_void_p(arr.ctypes.data) if arr is not None and arr.size else None

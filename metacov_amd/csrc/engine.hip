@@ -1,0 +1,608 @@
+// Host side of the coverage engine: the mc_ctx C ABI (include/metacov_amd.h).
+//
+// Device layout (one ctx = one GPU):
+//   reads   int32 tid[], pos[], span[]   SoA, coordinate-sorted, padded
+//   coff    int64 contig offset into the concatenated depth vector
+//           (each contig gets max(length, furthest read end), rounded up to
+//           64 positions)
+//   depth   int32[n_chunks * chunk_w]    all contigs back to back
+//   index   int64 chunk_first[n_chunks]  first read of each chunk (with halo)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/metacov_amd.h"
+#include "common.h"
+#include "kernels.h"
+
+using namespace mc;
+
+#define HIP_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            mc::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                          __FILE__, __LINE__);                                 \
+            return MC_E_HIP;                                                   \
+        }                                                                      \
+    } while (0)
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;   // elements
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+        }
+        hipError_t e = hipMalloc(&p, n * sizeof(T));
+        if (e != hipSuccess) {
+            cap = 0;
+            p = nullptr;
+            return e;
+        }
+        cap = n;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct mc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+
+    std::vector<int64_t> len, extent, coff;   // coff: n_contigs + 1
+    DevBuf<int64_t> d_len, d_coff;
+
+    int64_t n_reads = 0;
+    DevBuf<int32_t> d_tid, d_pos, d_span;
+    // raw-CIGAR mode
+    bool spans_pending = false;
+    DevBuf<int64_t> d_cig_off;
+    DevBuf<uint32_t> d_cigar;
+
+    bool prepared = false;
+    int32_t max_span = 0;
+    int64_t aligned_bases = 0;
+    int ring = 0;                 // LDS ring ints
+    int tiles_per_chunk = 16;
+    int64_t chunk_w = 0, n_chunks = 0, total_len = 0;
+    DevBuf<int64_t> d_chunk_first;
+    DevBuf<int32_t> d_depth;
+    bool depth_valid = false;
+    int32_t max_depth = -1;
+
+    DevBuf<unsigned long long> d_scratch;   // ingest counters
+    DevBuf<long long> d_maxend;
+    DevBuf<unsigned> d_queue;
+    DevBuf<int> d_maxdepth;
+    // K3 scratch
+    DevBuf<int64_t> d_seg_gs, d_seg_ge, d_ntot, d_nzx;
+    DevBuf<int32_t> d_seg_reg;
+    DevBuf<unsigned> d_hist;
+    DevBuf<RegionAcc> d_acc;
+    DevBuf<RegionOut> d_out;
+
+    hipEvent_t ev[8] = {};
+    mc_timings t{};
+    bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
+};
+
+static int ctx_use(mc_ctx* ctx) {
+    MC_REQUIRE(ctx, MC_E_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->device));
+    return MC_OK;
+}
+
+static void invalidate(mc_ctx* ctx) {
+    ctx->prepared = false;
+    ctx->depth_valid = false;
+    ctx->max_depth = -1;
+}
+
+extern "C" int mc_ctx_create(int device, mc_ctx** out) {
+    MC_REQUIRE(out, MC_E_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    MC_REQUIRE(e == hipSuccess && n > 0, MC_E_HIP,
+               "no HIP device available (hipGetDeviceCount: %s); metacov_amd has no CPU path",
+               hipGetErrorString(e));
+    MC_REQUIRE(device >= 0 && device < n, MC_E_INVALID, "device %d out of range [0, %d)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    mc_ctx* c = new mc_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        mc::set_error("hipStreamCreate failed");
+        return MC_E_HIP;
+    }
+    c->own_stream = true;
+    for (auto& ev : c->ev) (void)hipEventCreate(&ev);
+    if (c->d_scratch.reserve(8) != hipSuccess || c->d_queue.reserve(4) != hipSuccess ||
+        c->d_maxdepth.reserve(4) != hipSuccess) {
+        mc_ctx_destroy(c);
+        mc::set_error("hipMalloc of ctx scratch failed");
+        return MC_E_HIP;
+    }
+    *out = c;
+    return MC_OK;
+}
+
+extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
+    if (!ctx) return MC_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    ctx->d_len.release();
+    ctx->d_coff.release();
+    ctx->d_tid.release();
+    ctx->d_pos.release();
+    ctx->d_span.release();
+    ctx->d_cig_off.release();
+    ctx->d_cigar.release();
+    ctx->d_chunk_first.release();
+    ctx->d_depth.release();
+    ctx->d_scratch.release();
+    ctx->d_maxend.release();
+    ctx->d_queue.release();
+    ctx->d_maxdepth.release();
+    ctx->d_seg_gs.release();
+    ctx->d_seg_ge.release();
+    ctx->d_ntot.release();
+    ctx->d_nzx.release();
+    ctx->d_seg_reg.release();
+    ctx->d_hist.release();
+    ctx->d_acc.release();
+    ctx->d_out.release();
+    for (auto ev : ctx->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return MC_OK;
+}
+
+extern "C" int mc_ctx_set_stream(mc_ctx* ctx, void* s) {
+    if (int rc = ctx_use(ctx)) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    if (s) {
+        ctx->stream = (hipStream_t)s;
+        ctx->own_stream = false;
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+    }
+    return MC_OK;
+}
+
+extern "C" int mc_ctx_device(const mc_ctx* ctx, int* device) {
+    MC_REQUIRE(ctx && device, MC_E_INVALID, "null argument");
+    *device = ctx->device;
+    return MC_OK;
+}
+
+extern "C" int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(n >= 0 && (n == 0 || lengths), MC_E_INVALID, "bad contig table");
+    for (int32_t i = 0; i < n; ++i)
+        MC_REQUIRE(lengths[i] >= 0 && lengths[i] < (int64_t(1) << 40), MC_E_INVALID,
+                   "contig %d: bad length %lld", i, (long long)lengths[i]);
+    ctx->len.assign(lengths, lengths + n);
+    ctx->n_reads = 0;
+    ctx->spans_pending = false;
+    invalidate(ctx);
+    HIP_TRY(ctx->d_len.reserve(std::max<int64_t>(n, 1)));
+    if (n) HIP_TRY(hipMemcpy(ctx->d_len.p, lengths, n * sizeof(int64_t), hipMemcpyHostToDevice));
+    return MC_OK;
+}
+
+// grow the read arrays to hold `n_total` reads (+ one batch of padding)
+static int reserve_reads(mc_ctx* ctx, int64_t n_total, bool cigar_mode) {
+    const size_t cap = (size_t)round_up(n_total + kBatch, kBatch);
+    if (cap > ctx->d_tid.cap) {
+        size_t ncap = std::max(cap, ctx->d_tid.cap * 3 / 2);
+        ncap = (size_t)round_up((int64_t)ncap, kBatch);
+        DevBuf<int32_t> t2, p2, s2;
+        HIP_TRY(t2.reserve(ncap));
+        HIP_TRY(p2.reserve(ncap));
+        HIP_TRY(s2.reserve(ncap));
+        if (ctx->n_reads) {
+            HIP_TRY(hipMemcpyAsync(t2.p, ctx->d_tid.p, ctx->n_reads * 4, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(p2.p, ctx->d_pos.p, ctx->n_reads * 4, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(s2.p, ctx->d_span.p, ctx->n_reads * 4, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+        }
+        ctx->d_tid.release();
+        ctx->d_pos.release();
+        ctx->d_span.release();
+        ctx->d_tid = t2;
+        ctx->d_pos = p2;
+        ctx->d_span = s2;
+    }
+    (void)cigar_mode;
+    return MC_OK;
+}
+
+static int add_reads_impl(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
+                          const int32_t* span, hipMemcpyKind kind) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(n >= 0, MC_E_INVALID, "negative read count");
+    MC_REQUIRE(n == 0 || (tid && pos && span), MC_E_INVALID, "null read array");
+    MC_REQUIRE(!ctx->spans_pending, MC_E_STATE,
+               "cannot mix mc_add_reads with pending mc_add_reads_cigar reads; call mc_prepare first");
+    if (int rc = reserve_reads(ctx, ctx->n_reads + n, false)) return rc;
+    const int64_t o = ctx->n_reads;
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(ctx->d_tid.p + o, tid, n * 4, kind, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_pos.p + o, pos, n * 4, kind, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_span.p + o, span, n * 4, kind, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->n_reads += n;
+    invalidate(ctx);
+    return MC_OK;
+}
+
+extern "C" int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
+                            const int32_t* span) {
+    return add_reads_impl(ctx, n, tid, pos, span, hipMemcpyHostToDevice);
+}
+
+extern "C" int mc_add_reads_device(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
+                                   const int32_t* span) {
+    return add_reads_impl(ctx, n, tid, pos, span, hipMemcpyDeviceToDevice);
+}
+
+extern "C" int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
+                                  const int64_t* cig_off, const uint32_t* cigar) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(n >= 0, MC_E_INVALID, "negative read count");
+    MC_REQUIRE(n == 0 || (tid && pos && cig_off), MC_E_INVALID, "null read array");
+    MC_REQUIRE(ctx->n_reads == 0, MC_E_STATE,
+               "mc_add_reads_cigar must be the only read source of a ctx (call mc_set_contigs to reset)");
+    MC_REQUIRE(n == 0 || cig_off[0] == 0, MC_E_INVALID, "cig_off[0] must be 0");
+    const int64_t nw = n ? cig_off[n] : 0;
+    for (int64_t i = 0; i < n; ++i)
+        MC_REQUIRE(cig_off[i + 1] >= cig_off[i], MC_E_INVALID, "cig_off not monotone at %lld",
+                   (long long)i);
+    MC_REQUIRE(nw == 0 || cigar, MC_E_INVALID, "null cigar array");
+    if (int rc = reserve_reads(ctx, n, true)) return rc;
+    HIP_TRY(ctx->d_cig_off.reserve(n + 1));
+    HIP_TRY(ctx->d_cigar.reserve(std::max<int64_t>(nw, 1)));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(ctx->d_tid.p, tid, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_pos.p, pos, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_cig_off.p, cig_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (nw) HIP_TRY(hipMemcpyAsync(ctx->d_cigar.p, cigar, nw * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->n_reads = n;
+    ctx->spans_pending = n > 0;
+    invalidate(ctx);
+    return MC_OK;
+}
+
+static float elapsed(mc_ctx* ctx, int a, int b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]) != hipSuccess) return 0.f;
+    return ms;
+}
+
+extern "C" int mc_prepare(mc_ctx* ctx) {
+    if (int rc = ctx_use(ctx)) return rc;
+    if (ctx->prepared) return MC_OK;
+    const int32_t nc = (int32_t)ctx->len.size();
+    const int64_t n = ctx->n_reads;
+    hipStream_t s = ctx->stream;
+    ctx->t_cigar = false;
+    if (ctx->spans_pending) {
+        HIP_TRY(hipEventRecord(ctx->ev[0], s));
+        const int64_t nb = (n + kBlock - 1) / kBlock;
+        const size_t lds = (kBlock + 1) * 8 + 8 + kBlock * 4;
+        hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s,
+                           ctx->d_cig_off.p, ctx->d_cigar.p, n, ctx->d_span.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ctx->ev[1], s));
+        ctx->t_cigar = true;
+        ctx->spans_pending = false;
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    // ---- ingest: validation, aligned bases, max span, overhanging ends
+    HIP_TRY(ctx->d_maxend.reserve(std::max<int32_t>(nc, 1)));
+    HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(ctx->d_maxend.p, 0, std::max<int32_t>(nc, 1) * sizeof(long long), s));
+    if (n) {
+        const int64_t nb = std::min<int64_t>((n + kBlock - 1) / kBlock, 8192);
+        hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                           ctx->d_pos.p, ctx->d_span.p, n, ctx->d_len.p, nc, ctx->d_scratch.p,
+                           ctx->d_maxend.p);
+        HIP_TRY(hipGetLastError());
+    }
+    unsigned long long h[4];
+    std::vector<long long> maxend(std::max<int32_t>(nc, 1));
+    HIP_TRY(hipMemcpyAsync(h, ctx->d_scratch.p, sizeof h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(maxend.data(), ctx->d_maxend.p, maxend.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    MC_REQUIRE(h[0] == 0, MC_E_INVALID,
+               "%llu reads have tid outside [0, %d), negative pos or negative span", h[0], nc);
+    MC_REQUIRE(h[1] == 0, MC_E_INVALID,
+               "reads are not coordinate-sorted by (tid, pos) (%llu order violations); "
+               "the reference requires a sorted, indexed BAM (cli.py:37)", h[1]);
+    ctx->aligned_bases = (int64_t)h[2];
+    ctx->max_span = (int32_t)h[3];
+    // ---- layout: extents, contig offsets, chunk geometry
+    ctx->extent.resize(nc);
+    ctx->coff.resize(nc + 1);
+    int64_t off = 0;
+    for (int32_t i = 0; i < nc; ++i) {
+        ctx->extent[i] = std::max<int64_t>(ctx->len[i], maxend[i]);
+        ctx->coff[i] = off;
+        off += round_up(ctx->extent[i], 64);
+    }
+    ctx->coff[nc] = off;
+    ctx->total_len = off;
+    int ring = 2 * kTileW;
+    while (ring < kTileW + ctx->max_span) ring *= 2;
+    MC_REQUIRE(ring <= 32768, MC_E_RANGE,
+               "max span %d exceeds the LDS ring capacity (%d); long-read tiling is not "
+               "implemented in this build", ctx->max_span, 32768 - kTileW);
+    ctx->ring = ring;
+    ctx->tiles_per_chunk = 16;
+    ctx->chunk_w = (int64_t)ctx->tiles_per_chunk * kTileW;
+    ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
+    HIP_TRY(ctx->d_coff.reserve(nc + 1));
+    HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx->d_chunk_first.reserve(ctx->n_chunks));
+    HIP_TRY(ctx->d_depth.reserve((size_t)(ctx->n_chunks * ctx->chunk_w)));
+    if (n) {
+        const int64_t nb = (ctx->n_chunks + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                           ctx->d_pos.p, n, ctx->d_coff.p, ctx->chunk_w, (int64_t)ctx->max_span,
+                           ctx->n_chunks, ctx->d_chunk_first.p);
+        HIP_TRY(hipGetLastError());
+    } else {
+        HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, ctx->n_chunks * 8, s));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[3], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->t.prepare_ms = elapsed(ctx, 2, 3);
+    ctx->t.cigar_ms = ctx->t_cigar ? elapsed(ctx, 0, 1) : 0.f;
+    ctx->prepared = true;
+    ctx->depth_valid = false;
+    return MC_OK;
+}
+
+static int occupancy_grid(const void* kernel, size_t lds, int64_t work, int* grid) {
+    int dev = 0, ncu = 0, per = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds));
+    per = std::max(1, per);
+    *grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, (int64_t)ncu * per));
+    return MC_OK;
+}
+
+extern "C" int mc_compute_depth(mc_ctx* ctx) {
+    if (int rc = ctx_use(ctx)) return rc;
+    if (int rc = mc_prepare(ctx)) return rc;
+    hipStream_t s = ctx->stream;
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring) * 4;
+    int grid = 0;
+    if (int rc = occupancy_grid((const void*)depth_kernel, lds, ctx->n_chunks, &grid)) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
+    HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
+    HIP_TRY(hipEventRecord(ctx->ev[4], s));
+    hipLaunchKernelGGL(depth_kernel, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p, ctx->d_pos.p,
+                       ctx->d_span.p, ctx->n_reads, ctx->d_coff.p, ctx->d_chunk_first.p,
+                       ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1, ctx->d_depth.p,
+                       ctx->d_queue.p, ctx->d_maxdepth.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev[5], s));
+    ctx->t_depth = true;
+    ctx->t.depth_launches += 1;
+    ctx->depth_valid = true;
+    ctx->max_depth = -1;   // read lazily
+    return MC_OK;
+}
+
+static int fetch_max_depth(mc_ctx* ctx) {
+    if (ctx->max_depth >= 0) return MC_OK;
+    int v = 0;
+    HIP_TRY(hipMemcpyAsync(&v, ctx->d_maxdepth.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->max_depth = v;
+    return MC_OK;
+}
+
+extern "C" int mc_max_depth(mc_ctx* ctx, int32_t* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(out, MC_E_INVALID, "null out");
+    MC_REQUIRE(ctx->depth_valid, MC_E_STATE, "depth not computed");
+    if (int rc = fetch_max_depth(ctx)) return rc;
+    *out = ctx->max_depth;
+    return MC_OK;
+}
+
+extern "C" int mc_get_depth(mc_ctx* ctx, int32_t tid, int64_t start, int64_t end, int32_t* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(ctx->depth_valid, MC_E_STATE, "depth not computed (call mc_compute_depth)");
+    MC_REQUIRE(tid >= 0 && tid < (int32_t)ctx->len.size(), MC_E_INVALID, "tid %d out of range", tid);
+    MC_REQUIRE(start >= 0 && end >= start, MC_E_INVALID, "bad range [%lld, %lld)",
+               (long long)start, (long long)end);
+    MC_REQUIRE(end == start || out, MC_E_INVALID, "null out");
+    const int64_t ext = ctx->extent[tid];
+    const int64_t a = std::min(start, ext), b = std::min(end, ext);
+    if (b > a)
+        HIP_TRY(hipMemcpyAsync(out, ctx->d_depth.p + ctx->coff[tid] + a, (b - a) * 4,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (end > b) std::memset(out + (b - start), 0, (end - std::max(b, start)) * 4);
+    return MC_OK;
+}
+
+extern "C" int mc_depth_device(mc_ctx* ctx, const int32_t** d_depth, int64_t* total_len) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(d_depth && total_len, MC_E_INVALID, "null out");
+    MC_REQUIRE(ctx->depth_valid, MC_E_STATE, "depth not computed");
+    *d_depth = ctx->d_depth.p;
+    *total_len = ctx->total_len;
+    return MC_OK;
+}
+
+extern "C" int mc_contig_offset(mc_ctx* ctx, int32_t tid, int64_t* offset, int64_t* extent) {
+    MC_REQUIRE(ctx && offset && extent, MC_E_INVALID, "null argument");
+    MC_REQUIRE(ctx->prepared, MC_E_STATE, "not prepared");
+    MC_REQUIRE(tid >= 0 && tid < (int32_t)ctx->len.size(), MC_E_INVALID, "tid out of range");
+    *offset = ctx->coff[tid];
+    *extent = ctx->extent[tid];
+    return MC_OK;
+}
+
+// Region statistics: K3a over segments, K3b per region.  Writes R rows of
+// RegionOut (== mc_region_stat) to d_out (device).
+static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                             const int64_t* end, RegionOut* d_out_final) {
+    MC_REQUIRE(ctx->depth_valid, MC_E_STATE, "depth not computed (call mc_compute_depth)");
+    MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
+    const int32_t nc = (int32_t)ctx->len.size();
+    for (int64_t r = 0; r < R; ++r) {
+        MC_REQUIRE(tid[r] >= 0 && tid[r] < nc, MC_E_INVALID, "region %lld: tid %d out of range",
+                   (long long)r, tid[r]);
+        MC_REQUIRE(start[r] >= 0 && end[r] >= start[r], MC_E_INVALID,
+                   "region %lld: bad range [%lld, %lld)", (long long)r, (long long)start[r],
+                   (long long)end[r]);
+    }
+    if (R == 0) return MC_OK;
+    if (int rc = fetch_max_depth(ctx)) return rc;
+    const int nbins = ctx->max_depth + 1;
+    hipStream_t s = ctx->stream;
+    // batch regions so that the histogram stays <= 256 Mi bins
+    const int64_t max_hist = int64_t(1) << 28;
+    const int64_t rb = std::max<int64_t>(1, std::min<int64_t>(R, max_hist / nbins));
+    const bool lds_hist = nbins <= kLdsBins;
+    HIP_TRY(hipEventRecord(ctx->ev[6], s));
+    int64_t launches = 0;
+    for (int64_t r0 = 0; r0 < R; r0 += rb) {
+        const int64_t nr = std::min(rb, R - r0);
+        std::vector<int64_t> sg_gs, sg_ge, ntot(nr), nzx(nr);
+        std::vector<int32_t> sg_reg;
+        for (int64_t k = 0; k < nr; ++k) {
+            const int64_t r = r0 + k;
+            const int32_t t = tid[r];
+            const int64_t ext = ctx->extent[t];
+            const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
+            ntot[k] = end[r] - start[r];
+            nzx[k] = ntot[k] - (b - a);
+            for (int64_t p = a; p < b; p += kSeg) {
+                sg_gs.push_back(ctx->coff[t] + p);
+                sg_ge.push_back(ctx->coff[t] + std::min(b, p + kSeg));
+                sg_reg.push_back((int32_t)k);
+            }
+        }
+        const int64_t nseg = (int64_t)sg_gs.size();
+        HIP_TRY(ctx->d_seg_gs.reserve(std::max<int64_t>(nseg, 1)));
+        HIP_TRY(ctx->d_seg_ge.reserve(std::max<int64_t>(nseg, 1)));
+        HIP_TRY(ctx->d_seg_reg.reserve(std::max<int64_t>(nseg, 1)));
+        HIP_TRY(ctx->d_ntot.reserve(nr));
+        HIP_TRY(ctx->d_nzx.reserve(nr));
+        HIP_TRY(ctx->d_hist.reserve((size_t)(nr * nbins)));
+        HIP_TRY(ctx->d_acc.reserve(nr));
+        if (nseg) {
+            HIP_TRY(hipMemcpyAsync(ctx->d_seg_gs.p, sg_gs.data(), nseg * 8, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(ctx->d_seg_ge.p, sg_ge.data(), nseg * 8, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(ctx->d_seg_reg.p, sg_reg.data(), nseg * 4, hipMemcpyHostToDevice, s));
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->d_ntot.p, ntot.data(), nr * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->d_nzx.p, nzx.data(), nr * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_hist.p, 0, (size_t)(nr * nbins) * 4, s));
+        hipLaunchKernelGGL(region_init_kernel, dim3((unsigned)((nr + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, s, ctx->d_acc.p, nr);
+        HIP_TRY(hipGetLastError());
+        if (nseg) {
+            if (lds_hist)
+                hipLaunchKernelGGL(region_seg_kernel<true>, dim3((unsigned)nseg), dim3(kBlock),
+                                   (size_t)nbins * 4, s, ctx->d_depth.p, ctx->d_seg_gs.p,
+                                   ctx->d_seg_ge.p, ctx->d_seg_reg.p, nbins, ctx->d_hist.p,
+                                   ctx->d_acc.p);
+            else
+                hipLaunchKernelGGL(region_seg_kernel<false>, dim3((unsigned)nseg), dim3(kBlock), 0,
+                                   s, ctx->d_depth.p, ctx->d_seg_gs.p, ctx->d_seg_ge.p,
+                                   ctx->d_seg_reg.p, nbins, ctx->d_hist.p, ctx->d_acc.p);
+            HIP_TRY(hipGetLastError());
+            ++launches;
+        }
+        hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)nr), dim3(kBlock), 0, s,
+                           ctx->d_hist.p, nbins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p,
+                           d_out_final + r0);
+        HIP_TRY(hipGetLastError());
+        // the host vectors die at scope end: finish the copies first
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[7], s));
+    ctx->t_stats = true;
+    ctx->t.stats_launches += launches;
+    return MC_OK;
+}
+
+extern "C" int mc_region_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                                      const int64_t* start, const int64_t* end,
+                                      mc_region_stat* d_out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    static_assert(sizeof(RegionOut) == sizeof(mc_region_stat), "RegionOut layout");
+    MC_REQUIRE(R == 0 || d_out, MC_E_INVALID, "null out");
+    return region_stats_impl(ctx, R, tid, start, end, reinterpret_cast<RegionOut*>(d_out));
+}
+
+extern "C" int mc_region_stats(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                               const int64_t* end, mc_region_stat* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(R == 0 || out, MC_E_INVALID, "null out");
+    if (R == 0) return MC_OK;
+    HIP_TRY(ctx->d_out.reserve(R));
+    if (int rc = region_stats_impl(ctx, R, tid, start, end, ctx->d_out.p)) return rc;
+    HIP_TRY(hipMemcpyAsync(out, ctx->d_out.p, R * sizeof(mc_region_stat), hipMemcpyDeviceToHost,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MC_OK;
+}
+
+extern "C" int mc_aligned_bases(mc_ctx* ctx, int64_t* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(out, MC_E_INVALID, "null out");
+    if (int rc = mc_prepare(ctx)) return rc;
+    *out = ctx->aligned_bases;
+    return MC_OK;
+}
+
+extern "C" int mc_synchronize(mc_ctx* ctx) {
+    if (int rc = ctx_use(ctx)) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MC_OK;
+}
+
+extern "C" int mc_get_timings(mc_ctx* ctx, mc_timings* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(out, MC_E_INVALID, "null out");
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->t_depth) ctx->t.depth_ms = elapsed(ctx, 4, 5);
+    if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, 6, 7);
+    *out = ctx->t;
+    return MC_OK;
+}

@@ -1,0 +1,466 @@
+// gfx950 kernels of the coverage engine.  Integer work only, HBM-bound:
+// no MFMA anywhere (SURVEY.md §8 d: "integer scatter, scan and reduction").
+//
+//   ingest_kernel        validation + extents + aligned-base count (prepare)
+//   chunk_index_kernel   BAI-style linear index: first read of each chunk
+//   cigar_span_kernel    K1: packed BAM CIGAR words -> pileup span
+//   depth_kernel         K2: LDS-ring difference array + wave prefix scan
+//   region_seg_kernel    K3a: per-segment min/max/sum/sumsq + value histogram
+//   region_final_kernel  K3b: exact order statistics from the histogram
+//
+// Reference semantics being reproduced: htslib PileupColumn.n under pysam's
+// default "all" stepper (called at metacov/pileup.py:13) and the region
+// statistics of metacov/pileup.py:18-26.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mc {
+
+constexpr int kBlock = 256;            // 4 waves of 64
+constexpr int kWaves = kBlock / 64;
+constexpr int kTileW = 4096;           // positions per tile
+constexpr int kReadsPerThread = 4;     // int4 loads of tid/pos/span
+constexpr int kBatch = kBlock * kReadsPerThread;
+constexpr int kLdsHeader = 16;         // ints reserved in front of the ring
+constexpr int kSeg = 65536;            // K3 segment length (positions)
+constexpr int kLdsBins = 16384;        // K3 LDS histogram bins (64 KiB)
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+struct RegionAcc {                     // K3 per-region accumulator
+    unsigned long long sum;
+    unsigned long long sumsq;
+    int min;
+    int max;
+};
+
+// ----------------------------------------------------------------- helpers
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    return v;
+}
+
+__device__ __forceinline__ long long wave_sum64(long long v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
+// ----------------------------------------------------------------- ingest
+
+// out[0] = invalid records, out[1] = order violations, out[2] = aligned
+// bases, out[3] = max span.  maxend[t] = furthest read end past len[t].
+__global__ void __launch_bounds__(kBlock)
+ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+              const int32_t* __restrict__ span, int64_t n,
+              const int64_t* __restrict__ len, int32_t n_contigs,
+              unsigned long long* __restrict__ out, long long* __restrict__ maxend) {
+    const int lane = threadIdx.x & 63;
+    long long bad = 0, unsorted = 0, bases = 0;
+    int mspan = 0;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const int t = tid[i], p = pos[i], s = span[i];
+        if (t < 0 || t >= n_contigs || p < 0 || s < 0) {
+            ++bad;
+            continue;
+        }
+        if (i > 0) {
+            const int tp = tid[i - 1], pp = pos[i - 1];
+            if (tp > t || (tp == t && pp > p)) ++unsorted;
+        }
+        bases += s;
+        mspan = max(mspan, s);
+        const long long e = (long long)p + s;
+        if (e > len[t]) atomicMax(&maxend[t], e);
+    }
+    bad = wave_sum64(bad);
+    unsorted = wave_sum64(unsorted);
+    bases = wave_sum64(bases);
+    mspan = wave_max(mspan);
+    if (lane == 0) {
+        if (bad) atomicAdd(&out[0], (unsigned long long)bad);
+        if (unsorted) atomicAdd(&out[1], (unsigned long long)unsorted);
+        if (bases) atomicAdd(&out[2], (unsigned long long)bases);
+        atomicMax(&out[3], (unsigned long long)mspan);
+    }
+}
+
+__device__ __forceinline__ int64_t gstart_of(const int32_t* tid, const int32_t* pos,
+                                             const int64_t* coff, int64_t i) {
+    return coff[tid[i]] + pos[i];
+}
+
+// chunk_first[c] = first read index i with gstart(i) >= c * chunk_w - halo.
+__global__ void __launch_bounds__(kBlock)
+chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+                   int64_t n, const int64_t* __restrict__ coff, int64_t chunk_w,
+                   int64_t halo, int64_t n_chunks, int64_t* __restrict__ chunk_first) {
+    const int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (c >= n_chunks) return;
+    const int64_t target = c * chunk_w - halo;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = lo + ((hi - lo) >> 1);
+        if (gstart_of(tid, pos, coff, mid) < target) lo = mid + 1;
+        else hi = mid;
+    }
+    chunk_first[c] = lo;
+}
+
+// ----------------------------------------------------------------- K1
+
+// One workgroup per 256 reads; the block streams the contiguous CIGAR words
+// of its reads (coalesced) and sums the reference-consuming lengths
+// (op-type mask 0x18D = M, D, N, =, X; htslib bam_cigar2rlen).  A mapped read
+// without such an op gets span 1 (htslib bam_endpos).
+__global__ void __launch_bounds__(kBlock)
+cigar_span_kernel(const int64_t* __restrict__ cig_off, const uint32_t* __restrict__ cigar,
+                  int64_t n, int32_t* __restrict__ span) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    long long* off = reinterpret_cast<long long*>(smem_raw);          // kBlock + 1
+    int* acc = reinterpret_cast<int*>(smem_raw + (kBlock + 1) * 8 + 8);  // kBlock
+    const int64_t r0 = blockIdx.x * (int64_t)kBlock;
+    const int nr = (int)min<int64_t>(kBlock, n - r0);
+    for (int k = threadIdx.x; k <= nr; k += kBlock) off[k] = cig_off[r0 + k];
+    acc[threadIdx.x] = 0;
+    __syncthreads();
+    const long long w0 = off[0], w1 = off[nr];
+    const int lane = threadIdx.x & 63;
+    for (long long w = w0 + threadIdx.x; w - threadIdx.x < w1; w += kBlock) {
+        int r = -1, contrib = 0;
+        if (w < w1) {
+            const uint32_t c = cigar[w];
+            contrib = ((0x18Du >> (c & 0xFu)) & 1u) ? (int)(c >> 4) : 0;
+            int lo = 0, hi = nr;              // upper_bound(off, w) - 1
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (off[mid + 1] <= w) lo = mid + 1;
+                else hi = mid;
+            }
+            r = lo;
+        }
+        const int r_first = __shfl(r, 0, 64);
+        const bool uniform = __all(r == r_first) && r_first >= 0;
+        if (uniform) {
+            int s = contrib;
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+            if (lane == 0 && s) atomicAdd(&acc[r_first], s);
+        } else if (r >= 0 && contrib) {
+            atomicAdd(&acc[r], contrib);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nr) {
+        const int s = acc[threadIdx.x];
+        span[r0 + threadIdx.x] = s > 0 ? s : 1;
+    }
+}
+
+// ----------------------------------------------------------------- K2
+
+struct ReadBatch {
+    int64_t gs[kReadsPerThread];
+    int64_t ge[kReadsPerThread];
+    unsigned pending;                  // bit k: read k still to apply
+};
+
+__device__ __forceinline__ void load_batch(ReadBatch& b, int64_t base, int64_t n,
+                                           const int32_t* __restrict__ tid,
+                                           const int32_t* __restrict__ pos,
+                                           const int32_t* __restrict__ span,
+                                           const int64_t* __restrict__ coff) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
+    // arrays are padded to a multiple of kBatch past n: loads stay in bounds
+    const i32x4 t4 = *reinterpret_cast<const i32x4*>(tid + i0);
+    const i32x4 p4 = *reinterpret_cast<const i32x4*>(pos + i0);
+    const i32x4 s4 = *reinterpret_cast<const i32x4*>(span + i0);
+    const int tt[4] = {t4.x, t4.y, t4.z, t4.w};
+    const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
+    const int ss[4] = {s4.x, s4.y, s4.z, s4.w};
+    b.pending = 0;
+#pragma unroll
+    for (int k = 0; k < kReadsPerThread; ++k) {
+        if (i0 + k < n) {
+            b.gs[k] = coff[tt[k]] + pp[k];
+            b.ge[k] = b.gs[k] + ss[k];
+            b.pending |= 1u << k;
+        } else {
+            b.gs[k] = b.ge[k] = 0;
+        }
+    }
+}
+
+// One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
+// (dynamic queue).  Per chunk: the reads from chunk_first[c] (which already
+// includes the max-span halo) are applied as +1 at max(start, chunk start)
+// and -1 at end into an LDS ring of `ring` ints; each finished tile is
+// prefix-scanned (int4 per lane, wave scan, block carry) and stored to HBM
+// with 1 KiB-per-wave-instruction stores, and its ring slots are zeroed.
+// Requires ring >= kTileW + max_span, ring a power-of-two multiple of kTileW.
+__global__ void __launch_bounds__(kBlock)
+depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+             const int32_t* __restrict__ span, int64_t n,
+             const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
+             int64_t n_chunks, int tiles_per_chunk, int ring_mask,
+             int32_t* __restrict__ depth, unsigned* __restrict__ queue,
+             int* __restrict__ max_depth) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    int* hdr = lds;                       // [0] chunk id, [4..7] wave totals
+    int* ring = lds + kLdsHeader;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int ring_n = ring_mask + 1;
+    const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
+    constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
+    constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
+    int my_max = 0;
+
+    for (;;) {
+        if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
+        // zero the ring (also orders the hdr[0] write before the reads)
+        for (int k = threadIdx.x * 4; k < ring_n; k += kBlock * 4)
+            *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
+        __syncthreads();
+        const int64_t c = hdr[0];
+        if (c >= n_chunks) break;
+        const int64_t C0 = c * chunk_w;
+        int64_t base = chunk_first[c] & ~(int64_t)(kReadsPerThread - 1);
+        bool more = base < n;
+        ReadBatch b;
+        if (more) load_batch(b, base, n, tid, pos, span, coff);
+        else b.pending = 0;
+        int carry = 0;
+        for (int t = 0; t < tiles_per_chunk; ++t) {
+            const int64_t T0 = C0 + (int64_t)t * kTileW;
+            const int64_t Tend = T0 + kTileW;
+            for (;;) {
+#pragma unroll
+                for (int k = 0; k < kReadsPerThread; ++k) {
+                    if ((b.pending >> k) & 1u) {
+                        if (b.gs[k] < Tend) {
+                            const int64_t s = b.gs[k] > C0 ? b.gs[k] : C0;
+                            const int64_t e = b.ge[k];
+                            if (e > s) {
+                                atomicAdd(&ring[(int)(s & ring_mask)], 1);
+                                atomicAdd(&ring[(int)(e & ring_mask)], -1);
+                            }
+                            b.pending &= ~(1u << k);
+                        }
+                    }
+                }
+                const int all_done = __syncthreads_and(b.pending == 0);
+                if (!all_done || !more) break;
+                base += kBatch;
+                more = base < n;
+                if (!more) break;
+                load_batch(b, base, n, tid, pos, span, coff);
+            }
+            // ---- scan tile t: each wave owns kWaveSpan contiguous positions
+            const int sb = (int)(T0 & ring_mask) + wave * kWaveSpan;
+            i32x4 v[kChunks];
+            int wave_total = 0;
+#pragma unroll
+            for (int j = 0; j < kChunks; ++j) {
+                i32x4* slot = reinterpret_cast<i32x4*>(ring + sb + j * 256 + lane * 4);
+                i32x4 x = *slot;
+                *slot = i32x4{0, 0, 0, 0};
+                x.y += x.x;
+                x.z += x.y;
+                x.w += x.z;
+                const int incl = wave_incl_scan(x.w, lane);
+                const int excl = incl - x.w + wave_total;
+                x += excl;
+                v[j] = x;
+                wave_total += __shfl(incl, 63, 64);
+            }
+            if (lane == 0) hdr[4 + wave] = wave_total;
+            __syncthreads();
+            int off = carry, tile_total = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                const int tw = hdr[4 + w];
+                if (w < wave) off += tw;
+                tile_total += tw;
+            }
+            carry += tile_total;
+            int32_t* dst = depth + T0 + wave * kWaveSpan + lane * 4;
+#pragma unroll
+            for (int j = 0; j < kChunks; ++j) {
+                i32x4 x = v[j] + off;
+                my_max = max(my_max, max(max(x.x, x.y), max(x.z, x.w)));
+                __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
+            }
+        }
+        __syncthreads();   // hdr[0] / ring reuse by the next chunk
+    }
+    my_max = wave_max(my_max);
+    if (lane == 0 && my_max > 0) atomicMax(max_depth, my_max);
+}
+
+// ----------------------------------------------------------------- K3
+
+__global__ void __launch_bounds__(kBlock)
+region_init_kernel(RegionAcc* __restrict__ acc, int64_t R) {
+    const int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (r < R) {
+        acc[r].sum = 0;
+        acc[r].sumsq = 0;
+        acc[r].min = 0x7fffffff;
+        acc[r].max = 0;
+    }
+}
+
+// One workgroup per segment (<= kSeg positions of one region, clipped to
+// the contig extent).  int4 loads, masked at the unaligned ends.
+template <bool kLdsHist>
+__global__ void __launch_bounds__(kBlock)
+region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__ seg_gs,
+                  const int64_t* __restrict__ seg_ge, const int32_t* __restrict__ seg_reg,
+                  int nbins, unsigned* __restrict__ hist, RegionAcc* __restrict__ acc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned h[];
+    const int64_t sgi = blockIdx.x;
+    const int64_t gs = seg_gs[sgi], ge = seg_ge[sgi];
+    const int r = seg_reg[sgi];
+    const int lane = threadIdx.x & 63;
+    unsigned* ghist = hist + (int64_t)r * nbins;
+    if (kLdsHist) {
+        for (int k = threadIdx.x; k < nbins; k += kBlock) h[k] = 0;
+        __syncthreads();
+    }
+    long long sum = 0;
+    unsigned long long sumsq = 0;
+    int vmin = 0x7fffffff, vmax = 0;
+    const int64_t a4 = gs & ~(int64_t)3;
+    for (int64_t p = a4 + (int64_t)threadIdx.x * 4; p < ge; p += kBlock * 4) {
+        const i32x4 x4 = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(depth + p));
+        const int xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (p + k >= gs && p + k < ge) {
+                const int v = xs[k];
+                sum += v;
+                sumsq += (unsigned long long)((long long)v * v);
+                vmin = min(vmin, v);
+                vmax = max(vmax, v);
+                if (kLdsHist) atomicAdd(&h[v], 1u);
+                else atomicAdd(&ghist[v], 1u);
+            }
+        }
+    }
+    sum = wave_sum64(sum);
+    unsigned long long sq = sumsq;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) sq += __shfl_xor(sq, d, 64);
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
+    if (lane == 0) {
+        atomicAdd(&acc[r].sum, (unsigned long long)sum);
+        atomicAdd(&acc[r].sumsq, sq);
+        atomicMin(&acc[r].min, vmin);
+        atomicMax(&acc[r].max, vmax);
+    }
+    if (kLdsHist) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < nbins; k += kBlock) {
+            const unsigned c = h[k];
+            if (c) atomicAdd(&ghist[k], c);
+        }
+    }
+}
+
+struct RegionOut {                     // mirrors mc_region_stat
+    long long n, sum;
+    unsigned long long sumsq;
+    long long min, max, med_lo, med_hi, q23_sum, q23_cnt;
+};
+
+// One workgroup per region: block scan over the value histogram for the
+// ranks (n-1)/2, n/2 and the trimmed range [n/4, n - n/4) (pileup.py:21,24).
+__global__ void __launch_bounds__(kBlock)
+region_final_kernel(const unsigned* __restrict__ hist, int nbins,
+                    const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
+                    const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out) {
+    __shared__ long long s_part[kBlock];
+    __shared__ long long s_med[2];
+    const int r = blockIdx.x;
+    const unsigned* hr = hist + (int64_t)r * nbins;
+    const long long n = n_total[r];
+    const long long zx = n_zero_extra[r];
+    const int per = (nbins + kBlock - 1) / kBlock;
+    const int b0 = threadIdx.x * per;
+    const int b1 = min(nbins, b0 + per);
+    long long local = 0;
+    for (int b = b0; b < b1; ++b) local += hr[b] + (b == 0 ? zx : 0);
+    s_part[threadIdx.x] = local;
+    if (threadIdx.x < 2) s_med[threadIdx.x] = 0;
+    __syncthreads();
+    // exclusive scan of the per-thread counts (Hillis-Steele on 256 entries)
+    for (int d = 1; d < kBlock; d <<= 1) {
+        const long long y = threadIdx.x >= d ? s_part[threadIdx.x - d] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += y;
+        __syncthreads();
+    }
+    long long cum = s_part[threadIdx.x] - local;
+    const long long r_lo = (n - 1) / 2, r_hi = n / 2;
+    const long long q_lo = n / 4, q_hi = n - n / 4;
+    long long qsum = 0;
+    for (int b = b0; b < b1; ++b) {
+        const long long cnt = (long long)hr[b] + (b == 0 ? zx : 0);
+        if (cnt == 0) continue;
+        const long long e = cum + cnt;
+        if (r_lo >= cum && r_lo < e) s_med[0] = b;
+        if (r_hi >= cum && r_hi < e) s_med[1] = b;
+        const long long lo = cum > q_lo ? cum : q_lo;
+        const long long hi = e < q_hi ? e : q_hi;
+        if (hi > lo) qsum += (hi - lo) * (long long)b;
+        cum = e;
+    }
+    qsum = wave_sum64(qsum);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = qsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long q = 0;
+        for (int w = 0; w < kWaves; ++w) q += s_part[w];
+        RegionOut o;
+        o.n = n;
+        o.sum = (long long)acc[r].sum;
+        o.sumsq = acc[r].sumsq;
+        const bool any_read = n - zx > 0;
+        o.min = any_read ? acc[r].min : 0;
+        if (zx > 0 && o.min > 0) o.min = 0;
+        o.max = any_read ? acc[r].max : 0;
+        o.med_lo = s_med[0];
+        o.med_hi = s_med[1];
+        o.q23_sum = q;
+        o.q23_cnt = q_hi - q_lo;
+        if (n == 0) {
+            o.min = o.max = o.med_lo = o.med_hi = o.q23_sum = o.q23_cnt = 0;
+        }
+        out[r] = o;
+    }
+}
+
+}  // namespace mc

@@ -1,0 +1,94 @@
+"""Contig sharding across the GPUs of one node and the region-table exchange.
+
+Depth at a position depends only on the reads of its contig and every
+region lies inside one contig (metacov/cli.py:86-91), so contigs are the
+shard unit (SURVEY.md §8 e): each rank owns whole contigs, computes their
+depth and reduces the regions that lie on them with no data-path
+communication.  The only exchange is the final per-region table: one
+all-gather of a fixed-size padded int64 table over RCCL ("nccl" backend on
+ROCm, xGMI) — KB-scale and latency-bound — after which every rank holds all
+rows in input order (rank 0 writes the CSV).
+"""
+import heapq
+
+import numpy as np
+
+STAT_FIELDS = ("n", "sum", "sumsq", "min", "max", "med_lo", "med_hi", "q23_sum", "q23_cnt")
+ROW_WIDTH = len(STAT_FIELDS) + 1      # + original region index
+
+
+def lpt_shard(costs, world):
+    """Longest-processing-time greedy: contigs sorted by cost descending,
+    each to the currently least-loaded rank.  Returns a list of sorted
+    contig-id arrays, one per rank."""
+    costs = np.asarray(costs, dtype=np.float64)
+    order = np.argsort(-costs, kind="stable")
+    heap = [(0.0, r) for r in range(world)]
+    owned = [[] for _ in range(world)]
+    for c in order:
+        load, r = heapq.heappop(heap)
+        owned[r].append(int(c))
+        heapq.heappush(heap, (load + float(costs[c]), r))
+    return [np.array(sorted(o), dtype=np.int64) for o in owned]
+
+
+def contig_costs(lengths, read_counts):
+    """Cost model of K2+K3 per contig: 12 bytes per read + 8 per position
+    (depth written once, read once by the region reduction)."""
+    return 12.0 * np.asarray(read_counts, np.float64) + 8.0 * np.asarray(lengths, np.float64)
+
+
+def select_reads(tid, owned):
+    """Mask of the reads whose contig this rank owns, and the contig-id
+    remap (global tid -> local tid) for the owned contigs."""
+    n_contigs = int(max(int(tid.max()) + 1 if len(tid) else 0, int(owned.max()) + 1 if len(owned) else 0))
+    remap = np.full(n_contigs, -1, dtype=np.int32)
+    remap[owned] = np.arange(len(owned), dtype=np.int32)
+    mask = remap[tid] >= 0 if len(tid) else np.zeros(0, bool)
+    return mask, remap
+
+
+def pack_rows(rows, index):
+    """structured stat rows + original region index -> int64 [R, ROW_WIDTH]."""
+    out = np.empty((len(rows), ROW_WIDTH), dtype=np.int64)
+    for k, f in enumerate(STAT_FIELDS):
+        out[:, k] = rows[f].astype(np.int64) if f != "sumsq" else rows[f].view(np.int64)
+    out[:, -1] = index
+    return out
+
+
+def unpack_rows(table, n_regions, dtype):
+    """int64 [*, ROW_WIDTH] (rows with index < 0 are padding) -> structured
+    rows in original region order."""
+    table = np.asarray(table)
+    table = table[table[:, -1] >= 0]
+    out = np.zeros(n_regions, dtype=dtype)
+    idx = table[:, -1]
+    if len(np.unique(idx)) != len(idx) or len(idx) != n_regions:
+        raise RuntimeError("region table gather lost or duplicated rows (%d of %d)"
+                           % (len(idx), n_regions))
+    for k, f in enumerate(STAT_FIELDS):
+        col = table[:, k]
+        out[f][idx] = col.view(np.uint64) if f == "sumsq" else col
+    return out
+
+
+def all_gather_table(local, r_max, group=None, device=None):
+    """All-gather a [<= r_max, ROW_WIDTH] int64 table (numpy or torch) from
+    every rank; returns the concatenated [world * r_max, ROW_WIDTH] table as
+    numpy.  Padding rows carry index -1.  With the nccl (RCCL) backend the
+    tensors live on `device`; with gloo on the CPU."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = device if device is not None else torch.device("cpu")
+    if isinstance(local, torch.Tensor):
+        t = local
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(local, dtype=np.int64))
+    buf = torch.full((r_max, ROW_WIDTH), -1, dtype=torch.int64, device=dev)
+    if t.shape[0]:
+        buf[:t.shape[0]] = t.to(dev)
+    out = torch.empty((world * r_max, ROW_WIDTH), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return out.cpu().numpy()

@@ -1,0 +1,196 @@
+"""Python handle of one GPU coverage context (mc_ctx).
+
+    eng = CoverageEngine(device=0)
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)          # numpy (host) or torch (device)
+    eng.compute_depth()                    # K2 on the GPU
+    eng.depth(tid, start, end)             # int32 numpy
+    eng.region_stats(tids, starts, ends)   # structured numpy, exact integers
+    classic_stats(row)                     # -> the dict pileup.classic returns
+
+The statistics formatting here is the host half of the reference's
+`pileup.classic` (metacov/pileup.py:18-26): every value classic reports is a
+closed form of the exact integer row the GPU returns (see
+include/metacov_amd.h, mc_region_stat).
+"""
+import ctypes
+import math
+from fractions import Fraction
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+REGION_STAT_DTYPE = np.dtype([("n", "<i8"), ("sum", "<i8"), ("sumsq", "<u8"), ("min", "<i8"),
+                              ("max", "<i8"), ("med_lo", "<i8"), ("med_hi", "<i8"),
+                              ("q23_sum", "<i8"), ("q23_cnt", "<i8")])
+assert REGION_STAT_DTYPE.itemsize == ctypes.sizeof(_lib.RegionStat) == 72
+
+
+def _np_round2(x):
+    """round(np.float64, 2) as numpy implements it (np.round: rint(x*100)/100)."""
+    return float(np.round(np.float64(x), 2))
+
+
+def classic_stats(row):
+    """dict(min, max, med, std, avg, q23, sum) from one exact stat row.
+
+    Mirrors metacov/pileup.py:18-26 on the float64 column vector:
+      min/max/sum  int(np.amin/np.amax/np.sum)          -> exact integers
+      med          int(np.median): mean of ranks (n-1)//2 and n//2, truncated
+      avg          round(np.mean, 2): float64(sum)/n is what np.mean returns
+                   for integer-valued float64 data (its pairwise sum is exact)
+      q23          round(np.mean(sorted(c)[n//4 : n-n//4]), 2), likewise exact
+      std          round(np.std, 2) (ddof=0), from the exact variance
+    Raises ValueError for an empty region as classic does (zero-size
+    reduction in np.amin).
+    """
+    n = int(row["n"])
+    if n <= 0:
+        raise ValueError("zero-size array to reduction operation minimum which has no identity")
+    s = int(row["sum"])
+    sq = int(row["sumsq"])
+    var = Fraction(n * sq - s * s, n * n)
+    std = math.sqrt(float(var)) if var > 0 else 0.0
+    avg = float(np.float64(s) / np.float64(n))
+    q23 = float(np.float64(int(row["q23_sum"])) / np.float64(int(row["q23_cnt"])))
+    med = (int(row["med_lo"]) + int(row["med_hi"])) // 2
+    return {
+        "min": int(row["min"]),
+        "max": int(row["max"]),
+        "med": med,
+        "std": _np_round2(std),
+        "avg": _np_round2(avg),
+        "q23": _np_round2(q23),
+        "sum": s,
+    }
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+class CoverageEngine:
+    """One mc_ctx on one GPU.  Not thread-safe (one engine per thread/GPU)."""
+
+    def __init__(self, device=0):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(self._lib.mc_ctx_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self.lengths = np.zeros(0, dtype=np.int64)
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.mc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, hip_stream_ptr):
+        check(self._lib.mc_ctx_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr or None)))
+
+    # -- inputs
+    def set_contigs(self, lengths):
+        lengths = np.ascontiguousarray(lengths, dtype=np.int64)
+        check(self._lib.mc_set_contigs(self._h, len(lengths), ptr(lengths)))
+        self.lengths = lengths
+
+    def add_reads(self, tid, pos, span):
+        """Coordinate-sorted pileup intervals.  numpy arrays are copied from
+        host memory; torch tensors on this ctx's GPU are copied device-side."""
+        if _is_torch(tid):
+            import torch
+            ts = [t.contiguous().to(torch.int32) for t in (tid, pos, span)]
+            n = ts[0].numel()
+            if not all(t.is_cuda and t.numel() == n for t in ts):
+                raise ValueError("tid/pos/span must be equally sized device tensors")
+            check(self._lib.mc_add_reads_device(self._h, n, *[ctypes.c_void_p(t.data_ptr()) for t in ts]))
+            return
+        arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (tid, pos, span)]
+        n = len(arrs[0])
+        if not all(len(a) == n for a in arrs):
+            raise ValueError("tid/pos/span lengths differ")
+        check(self._lib.mc_add_reads(self._h, n, *[ptr(a) for a in arrs]))
+
+    def add_reads_cigar(self, tid, pos, cig_off, cigar):
+        tid = np.ascontiguousarray(tid, dtype=np.int32)
+        pos = np.ascontiguousarray(pos, dtype=np.int32)
+        cig_off = np.ascontiguousarray(cig_off, dtype=np.int64)
+        cigar = np.ascontiguousarray(cigar, dtype=np.uint32)
+        if len(cig_off) != len(tid) + 1:
+            raise ValueError("cig_off must have n + 1 entries")
+        check(self._lib.mc_add_reads_cigar(self._h, len(tid), ptr(tid), ptr(pos), ptr(cig_off),
+                                           ptr(cigar)))
+
+    def prepare(self):
+        check(self._lib.mc_prepare(self._h))
+
+    # -- compute
+    def compute_depth(self):
+        check(self._lib.mc_compute_depth(self._h))
+
+    def depth(self, tid, start=0, end=None):
+        if end is None:
+            end = int(self.lengths[tid])
+        out = np.empty(max(0, end - start), dtype=np.int32)
+        check(self._lib.mc_get_depth(self._h, int(tid), int(start), int(end), ptr(out)))
+        return out
+
+    def depth_device(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        check(self._lib.mc_depth_device(self._h, ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
+
+    def contig_offset(self, tid):
+        o, e = ctypes.c_int64(), ctypes.c_int64()
+        check(self._lib.mc_contig_offset(self._h, int(tid), ctypes.byref(o), ctypes.byref(e)))
+        return o.value, e.value
+
+    def region_stats(self, tids, starts, ends):
+        tids = np.ascontiguousarray(tids, dtype=np.int32)
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        out = np.zeros(len(tids), dtype=REGION_STAT_DTYPE)
+        check(self._lib.mc_region_stats(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+                                        ptr(out)))
+        return out
+
+    def region_stats_device(self, tids, starts, ends, d_out_ptr):
+        tids = np.ascontiguousarray(tids, dtype=np.int32)
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        check(self._lib.mc_region_stats_device(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+                                               ctypes.c_void_p(d_out_ptr)))
+
+    def aligned_bases(self):
+        v = ctypes.c_int64()
+        check(self._lib.mc_aligned_bases(self._h, ctypes.byref(v)))
+        return v.value
+
+    def max_depth(self):
+        v = ctypes.c_int32()
+        check(self._lib.mc_max_depth(self._h, ctypes.byref(v)))
+        return v.value
+
+    def timings(self):
+        t = _lib.Timings()
+        check(self._lib.mc_get_timings(self._h, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+    def synchronize(self):
+        check(self._lib.mc_synchronize(self._h))

@@ -1,0 +1,241 @@
+"""Synthetic coverage workloads and a minimal BAM/BGZF writer.
+
+Stands in for the reference's `metacov simulate` (`metacov/cli.py:288-414`,
+`metacov/simulate.py:31-50`), which needs the absent `art_illumina` binary.
+Configurations follow SURVEY.md §8(d) / BASELINE.json `configs`:
+
+  C1  1 contig x 100,000 bp; 10,000 x 100 bp paired reads, seed 1234
+  C2  1 contig x 5,000,000 bp; 10M x 150 bp, seed 1
+  C3  1000 contigs, lengths rng(42).integers(200_000, 1_800_001),
+      weight = length x lognormal(0,1) abundance; 100M x 150 bp
+  C5  10k contigs (50-150 kbp); 50M long reads, lognormal length (mean 10 kbp)
+
+Every config carries the SURVEY edge mix: 95% plain `150M`, 3% soft clips,
+1% I/D, 0.1% N, 0.5% =/X, 2% placed-unmapped (flag 0x4, no CIGAR) and the
+flag bits 0x100 (1%), 0x400 (0.5%), 0x200 (0.2%), 0x800 (0.5%, kept).
+
+Two forms are produced:
+* records with CIGARs (small sizes) -> `write_bam` -> BAM file, for the
+  decoder and end-to-end parity tests;
+* pileup intervals only (`interval_workload`): coordinate-sorted int32
+  (tid, pos, span) after the 0x704 filter, vectorised numpy, for the
+  device benchmark (the spans follow the same edge mix).
+"""
+import struct
+import zlib
+
+import numpy as np
+
+# CIGAR op codes (SAMv1 §4.2)
+M, I, D, N, S, H, P, EQ, X = range(9)
+REF_CONSUMING_MASK = 0x18D
+FLAG_FILTER = 0x704
+
+# category probabilities of the edge mix (SURVEY.md §8 d)
+_CATS = np.array([0.9290, 0.03, 0.005, 0.005, 0.001, 0.005, 0.02, 0.005])
+_CAT_PLAIN, _CAT_SOFT, _CAT_INS, _CAT_DEL, _CAT_SKIP, _CAT_EQX, _CAT_UNMAP, _CAT_ZERO = range(8)
+
+
+def c3_contig_lengths(n=1000, seed=42):
+    rng = np.random.default_rng(seed)
+    return rng.integers(200_000, 1_800_001, size=n).astype(np.int64)
+
+
+def _cigar_for(cat, readlen, rng):
+    """One CIGAR (list of (op, len)) for an edge-mix category."""
+    if cat == _CAT_PLAIN:
+        return [(M, readlen)]
+    if cat == _CAT_SOFT:
+        s = int(rng.integers(1, max(2, readlen // 5)))
+        return [(S, s), (M, readlen - s)] if rng.random() < 0.5 else [(M, readlen - s), (S, s)]
+    if cat == _CAT_INS:
+        a = int(rng.integers(1, readlen - 10))
+        i = int(rng.integers(1, 6))
+        return [(M, a), (I, i), (M, readlen - a - i)]
+    if cat == _CAT_DEL:
+        a = int(rng.integers(1, readlen - 1))
+        return [(M, a), (D, int(rng.integers(1, 10))), (M, readlen - a)]
+    if cat == _CAT_SKIP:
+        a = int(rng.integers(1, readlen - 1))
+        return [(M, a), (N, int(rng.integers(50, 2000))), (M, readlen - a)]
+    if cat == _CAT_EQX:
+        a = int(rng.integers(1, readlen - 1))
+        return [(EQ, a), (X, 1), (EQ, readlen - a - 1)]
+    if cat == _CAT_ZERO:
+        # mapped, but no reference-consuming op (htslib: treated as 1 bp)
+        return [(S, readlen)] if rng.random() < 0.5 else []
+    return []   # unmapped
+
+
+def ref_len(cigar):
+    return sum(ln for op, ln in cigar if (REF_CONSUMING_MASK >> op) & 1)
+
+
+class SynthRecord:
+    __slots__ = ("name", "tid", "pos", "flag", "cigar", "l_seq")
+
+    def __init__(self, name, tid, pos, flag, cigar, l_seq):
+        self.name, self.tid, self.pos, self.flag = name, tid, pos, flag
+        self.cigar, self.l_seq = cigar, l_seq
+
+
+def edge_mix_records(lengths, n_reads, readlen=150, seed=1, weights=None,
+                     overhang=False, zero_span=False, unplaced=0):
+    """Coordinate-sorted records with CIGARs and flags (small sizes).
+
+    `overhang` lets a few reads run past the end of their contig; `zero_span`
+    adds mapped reads without reference-consuming ops; `unplaced` appends
+    that many tid=-1 unmapped records at the end of the file.
+    """
+    rng = np.random.default_rng(seed)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    w = lengths.astype(np.float64) if weights is None else np.asarray(weights, np.float64)
+    tids = rng.choice(len(lengths), size=n_reads, p=w / w.sum())
+    probs = _CATS.copy()
+    if not zero_span:
+        probs[_CAT_PLAIN] += probs[_CAT_ZERO]
+        probs[_CAT_ZERO] = 0
+    cats = rng.choice(len(probs), size=n_reads, p=probs / probs.sum())
+    recs = []
+    for i in range(n_reads):
+        tid = int(tids[i])
+        L = int(lengths[tid])
+        cat = int(cats[i])
+        cigar = _cigar_for(cat, readlen, rng)
+        rl = ref_len(cigar)
+        hi = L - max(rl, 1) if not overhang else L - 1
+        pos = int(rng.integers(0, max(1, hi + 1)))
+        flag = 0x1 | (0x40 if i % 2 == 0 else 0x80)
+        if cat == _CAT_UNMAP:
+            flag |= 0x4
+        u = rng.random()
+        if u < 0.01:
+            flag |= 0x100
+        elif u < 0.015:
+            flag |= 0x400
+        elif u < 0.017:
+            flag |= 0x200
+        elif u < 0.022:
+            flag |= 0x800
+        if rng.random() < 0.5:
+            flag |= 0x10
+        recs.append(SynthRecord("r%d" % i, tid, pos, flag, cigar, readlen))
+    recs.sort(key=lambda r: (r.tid, r.pos))
+    for j in range(unplaced):
+        recs.append(SynthRecord("u%d" % j, -1, -1, 0x4, [], readlen))
+    return recs
+
+
+# ---------------------------------------------------------------- BGZF / BAM
+
+_BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def _bgzf_block(payload):
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    cdata = c.compress(payload) + c.flush()
+    bsize = len(cdata) + 25  # 18 header + 8 trailer - 1
+    hdr = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize)
+    tail = struct.pack("<II", zlib.crc32(payload) & 0xFFFFFFFF, len(payload))
+    return hdr + cdata + tail
+
+
+def _bgzf(data, block=0xff00):
+    out = bytearray()
+    for i in range(0, len(data), block):
+        out += _bgzf_block(data[i:i + block])
+    out += _BGZF_EOF
+    return bytes(out)
+
+
+def _reg2bin(beg, end):
+    end -= 1
+    if beg >> 14 == end >> 14:
+        return ((1 << 15) - 1) // 7 + (beg >> 14)
+    if beg >> 17 == end >> 17:
+        return ((1 << 12) - 1) // 7 + (beg >> 17)
+    if beg >> 20 == end >> 20:
+        return ((1 << 9) - 1) // 7 + (beg >> 20)
+    if beg >> 23 == end >> 23:
+        return ((1 << 6) - 1) // 7 + (beg >> 23)
+    if beg >> 26 == end >> 26:
+        return ((1 << 3) - 1) // 7 + (beg >> 26)
+    return 0
+
+
+def encode_record(r, long_cigar_threshold=65535):
+    """One BAM record (bytes).  CIGARs longer than the threshold are stored
+    in a CG:B,I tag behind a `<l_seq>S<rlen>N` placeholder (SAMv1 §4.2.2)."""
+    name = r.name.encode() + b"\0"
+    cig = [(ln << 4) | op for op, ln in r.cigar]
+    aux = b""
+    if len(cig) > long_cigar_threshold:
+        aux = b"CGBI" + struct.pack("<i", len(cig)) + struct.pack("<%dI" % len(cig), *cig)
+        cig = [(r.l_seq << 4) | S, (max(ref_len(r.cigar), 1) << 4) | N]
+    l_seq = r.l_seq
+    seq = bytes([0x11] * ((l_seq + 1) // 2))   # "AA..." in nt16
+    qual = bytes([30] * l_seq)
+    end = r.pos + max(ref_len(r.cigar), 1)
+    bin_ = _reg2bin(max(r.pos, 0), max(end, 1)) if r.tid >= 0 else 4680
+    core = struct.pack("<iiBBHHHiiii", r.tid, r.pos, len(name), 60, bin_, len(cig),
+                       r.flag, l_seq, r.tid, r.pos, 0)
+    body = core + name + struct.pack("<%dI" % len(cig), *cig) + seq + qual + aux
+    return struct.pack("<i", len(body)) + body
+
+
+def write_bam(path, names, lengths, records, long_cigar_threshold=65535):
+    text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join(
+        "@SQ\tSN:%s\tLN:%d\n" % (n, L) for n, L in zip(names, lengths))
+    hdr = bytearray(b"BAM\x01")
+    hdr += struct.pack("<i", len(text)) + text.encode()
+    hdr += struct.pack("<i", len(names))
+    for n, L in zip(names, lengths):
+        nb = n.encode() + b"\0"
+        hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", int(L))
+    body = bytearray(hdr)
+    for r in records:
+        body += encode_record(r, long_cigar_threshold)
+    with open(path, "wb") as fh:
+        fh.write(_bgzf(bytes(body)))
+
+
+# ------------------------------------------------------- interval workloads
+
+def interval_workload(lengths, n_reads, readlen=150, seed=1, weights=None,
+                      long_reads=False):
+    """Coordinate-sorted pileup intervals (int32 tid, pos, span) after the
+    0x704 filter, vectorised.  Spans follow the edge mix: soft clips shorten,
+    deletions / N lengthen.  `long_reads` draws lognormal lengths with mean
+    ~10 kbp clipped to the contig (config C5)."""
+    rng = np.random.default_rng(seed)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    w = lengths.astype(np.float64) if weights is None else np.asarray(weights, np.float64)
+    counts = rng.multinomial(n_reads, w / w.sum())
+    tid = np.repeat(np.arange(len(lengths), dtype=np.int32), counts)
+    if long_reads:
+        span = rng.lognormal(np.log(10_000) - 0.5 * 0.5 ** 2, 0.5, size=n_reads)
+        span = np.maximum(span.astype(np.int64), 1)
+    else:
+        u = rng.random(n_reads)
+        span = np.full(n_reads, readlen, dtype=np.int64)
+        soft = u < 0.03
+        span[soft] -= rng.integers(1, readlen // 5, size=int(soft.sum()))
+        ins = (u >= 0.03) & (u < 0.035)
+        span[ins] -= rng.integers(1, 6, size=int(ins.sum()))
+        dele = (u >= 0.035) & (u < 0.04)
+        span[dele] += rng.integers(1, 10, size=int(dele.sum()))
+        skip = (u >= 0.04) & (u < 0.041)
+        span[skip] += rng.integers(50, 2000, size=int(skip.sum()))
+    L = lengths[tid]
+    span = np.minimum(span, L)
+    pos = (rng.random(n_reads) * (L - span + 1)).astype(np.int64)
+    order = np.lexsort((pos, tid))
+    return (tid[order].astype(np.int32), pos[order].astype(np.int32),
+            span[order].astype(np.int32))
+
+
+def c3_workload(n_reads=100_000_000, n_contigs=1000, seed=42):
+    lengths = c3_contig_lengths(n_contigs, seed)
+    rng = np.random.default_rng(seed + 1)
+    weights = lengths * rng.lognormal(0.0, 1.0, size=n_contigs)
+    return lengths, weights

@@ -1,0 +1,86 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so
+(the C restatement in oracle/oracle.c).  Imported by tests/ and by bench.py's
+cpu_baseline leg only."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+STAT_DTYPE = np.dtype([("n", "<i8"), ("sum", "<i8"), ("sumsq", "<u8"), ("min", "<i8"),
+                       ("max", "<i8"), ("med_lo", "<i8"), ("med_hi", "<i8"),
+                       ("q23_sum", "<i8"), ("q23_cnt", "<i8")])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "oracle.c")):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.orc_pileup_classic.restype = ctypes.c_int64
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else None
+
+
+def layout(lengths, tid, pos, span):
+    """extents (max of length and furthest read end) and offsets."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    ext = lengths.copy()
+    if len(tid):
+        ends = pos.astype(np.int64) + span
+        np.maximum.at(ext, tid, ends)
+    coff = np.zeros(len(ext) + 1, dtype=np.int64)
+    coff[1:] = np.cumsum(ext)
+    return ext, coff
+
+
+def depth(lengths, tid, pos, span, method="interval"):
+    """Concatenated depth vector and (extent, offset) per contig."""
+    tid = np.ascontiguousarray(tid, np.int32)
+    pos = np.ascontiguousarray(pos, np.int32)
+    span = np.ascontiguousarray(span, np.int32)
+    ext, coff = layout(lengths, tid, pos, span)
+    out = np.zeros(int(coff[-1]), dtype=np.int32)
+    fn = load().orc_depth_interval if method == "interval" else load().orc_depth_columnwalk
+    fn(ctypes.c_int32(len(ext)), _p(ext), _p(coff), ctypes.c_int64(len(tid)), _p(tid), _p(pos),
+       _p(span), _p(out))
+    return out, ext, coff
+
+
+def region_stats(depth_vec, ext, coff, rtid, rstart, rend):
+    rtid = np.ascontiguousarray(rtid, np.int32)
+    rstart = np.ascontiguousarray(rstart, np.int64)
+    rend = np.ascontiguousarray(rend, np.int64)
+    out = np.zeros(len(rtid), dtype=STAT_DTYPE)
+    load().orc_region_stats(_p(depth_vec), _p(coff), _p(ext), ctypes.c_int64(len(rtid)), _p(rtid),
+                            _p(rstart), _p(rend), _p(out))
+    return out
+
+
+def pileup_classic(tid, pos, span, rtid, rstart, rend):
+    """classic() per region, end to end on one core; returns (out7, columns)."""
+    tid = np.ascontiguousarray(tid, np.int32)
+    pos = np.ascontiguousarray(pos, np.int32)
+    span = np.ascontiguousarray(span, np.int32)
+    rtid = np.ascontiguousarray(rtid, np.int32)
+    rstart = np.ascontiguousarray(rstart, np.int64)
+    rend = np.ascontiguousarray(rend, np.int64)
+    out = np.zeros((len(rtid), 7), dtype=np.float64)
+    ms = int(span.max()) if len(span) else 0
+    cols = load().orc_pileup_classic(ctypes.c_int64(len(tid)), _p(tid), _p(pos), _p(span),
+                                     ctypes.c_int32(ms), ctypes.c_int64(len(rtid)), _p(rtid),
+                                     _p(rstart), _p(rend), _p(out))
+    return out, cols

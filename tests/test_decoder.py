@@ -1,0 +1,81 @@
+"""The product's C++ BAM decoder (host code, no GPU) against the goldens."""
+import os
+
+import numpy as np
+import pytest
+
+from metacov_amd import synth
+from metacov_amd._lib import MetacovError
+from metacov_amd.bam import BamFile
+
+
+def _iv(g):
+    return [np.array(g["intervals"][k], np.int32) for k in ("tid", "pos", "span")]
+
+
+@pytest.mark.parametrize("threads", [1, 3, 0])
+def test_fixture(lib_built, fixture_golden, golden_dir, threads):
+    bf = BamFile(os.path.join(golden_dir, "bbmap.sorted.bam"), n_threads=threads)
+    assert list(bf.references) == fixture_golden["names"]
+    assert list(bf.lengths) == fixture_golden["lengths"]
+    assert bf.n_records == 4112
+    # 133 FUNMAP records (129 placed at a mate, 4 with tid -1)
+    assert bf.mapped == 4112 - 133 and bf.unmapped == 133
+    for got, want in zip((bf.tid, bf.pos, bf.span), _iv(fixture_golden)):
+        assert np.array_equal(got, want)
+    assert bf.aligned_bases() == 340526
+
+
+@pytest.mark.parametrize("tag", ["synth_edge", "synth_multi", "synth_longcigar"])
+def test_synth(lib_built, synth_golden, golden_dir, tag):
+    bf = BamFile(os.path.join(golden_dir, tag + ".bam"), n_threads=2)
+    g = synth_golden[tag]
+    assert list(bf.references) == g["names"]
+    for got, want in zip((bf.tid, bf.pos, bf.span), _iv(g)):
+        assert np.array_equal(got, want)
+
+
+def test_keep_cigar_spans(lib_built, golden_dir):
+    bf = BamFile(os.path.join(golden_dir, "synth_longcigar.bam"), keep_cigar=True)
+    assert bf.cig_off[0] == 0 and len(bf.cig_off) == len(bf.tid) + 1
+    assert bf.cig_off[1] == 140_000          # CG:B,I tag resolved
+    for i in range(len(bf.tid)):
+        w = bf.cigar[bf.cig_off[i]:bf.cig_off[i + 1]]
+        rl = sum(int(x >> 4) for x in w if (0x18D >> int(x & 0xF)) & 1)
+        assert max(rl, 1) == bf.span[i]
+
+
+def test_flag_filter_override(lib_built, golden_dir):
+    bf = BamFile(os.path.join(golden_dir, "synth_edge.bam"), flag_filter=0)
+    bf2 = BamFile(os.path.join(golden_dir, "synth_edge.bam"))
+    assert len(bf.tid) > len(bf2.tid)
+
+
+def test_many_blocks_and_threads(lib_built, tmp_path):
+    lengths = [200_000, 3_000]
+    recs = synth.edge_mix_records(lengths, 30_000, readlen=100, seed=3)
+    p = str(tmp_path / "m.bam")
+    synth.write_bam(p, ["a", "b"], lengths, recs)
+    a = BamFile(p, n_threads=1)
+    b = BamFile(p, n_threads=8)
+    for x, y in zip((a.tid, a.pos, a.span), (b.tid, b.pos, b.span)):
+        assert np.array_equal(x, y)
+    kept = [r for r in recs if r.tid >= 0 and not (r.flag & 0x704)]
+    assert len(a.tid) == len(kept)
+    assert a.span.tolist() == [max(synth.ref_len(r.cigar), 1) for r in kept]
+
+
+def test_errors(lib_built, tmp_path, golden_dir):
+    with pytest.raises(MetacovError):
+        BamFile(str(tmp_path / "missing.bam"))
+    p = tmp_path / "plain.gz"
+    import gzip
+    with gzip.open(p, "wb") as fh:
+        fh.write(b"BAM\1" + b"\0" * 100)
+    with pytest.raises(MetacovError, match="BGZF"):
+        BamFile(str(p))
+    raw = open(os.path.join(golden_dir, "bbmap.sorted.bam"), "rb").read()
+    t = tmp_path / "trunc.bam"
+    t.write_bytes(raw[: len(raw) // 2])
+    with pytest.raises(MetacovError):
+        BamFile(str(t))
