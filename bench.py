@@ -1,0 +1,268 @@
+"""Benchmark: aligned bases/s into the per-position depth vector (+ per-region
+statistics), BASELINE.json metric, on the C3 workload per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+One step = K2 (depth of every contig from device-resident (tid, pos, span)
+tuples) + K3 (whole-contig region statistics into device memory) [+ for
+N > 1 the RCCL all-gather of the region table].  Inputs are generated on the
+GPU before timing (synthetic, SURVEY.md §8 d edge mix).
+
+Default (weak scaling, as BASELINE configs[2] per GPU): every rank owns a
+full C3 workload — 1000 contigs (~1 Gbp, rng(42) lengths, lognormal(0,1)
+abundance) and 100M x ~150 bp reads; value = all ranks' aligned bases per
+second.  --strong: one C3 workload LPT-sharded by contig over the ranks
+(BASELINE configs[3]).
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--reads", type=int, default=100_000_000, help="reads per C3 workload")
+    ap.add_argument("--contigs", type=int, default=1000)
+    ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-bases", type=float, default=3.0e9,
+                    help="aligned bases in the CPU-baseline sample (~10-20 s on one core)")
+    ap.add_argument("--pcie", action="store_true", help="also time host-buffer ingest (H2D)")
+    ap.add_argument("--seed", type=int, default=1)
+    return ap.parse_args()
+
+
+def device_workload(torch, lengths, weights, n_reads, seed, dev):
+    """C3-style pileup intervals generated on the GPU: coordinate-sorted
+    int32 (tid, pos, span) with the SURVEY §8(d) span mix (3% soft clips,
+    0.5% I, 0.5% D, 0.1% N; filtered records are not part of the stream)."""
+    rng = np.random.default_rng(seed)
+    counts = rng.multinomial(n_reads, weights / weights.sum())
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    L = torch.from_numpy(lengths).to(dev)
+    tid = torch.repeat_interleave(torch.arange(len(lengths), device=dev, dtype=torch.int32),
+                                  torch.from_numpy(counts).to(dev))
+    u = torch.rand(n_reads, device=dev, generator=g)
+    r = torch.rand(n_reads, device=dev, generator=g)
+    span = torch.full((n_reads,), 150, dtype=torch.int64, device=dev)
+    span -= ((u < 0.03) * (1 + (r * 29).long()))
+    span -= (((u >= 0.03) & (u < 0.035)) * (1 + (r * 5).long()))
+    span += (((u >= 0.035) & (u < 0.04)) * (1 + (r * 9).long()))
+    span += (((u >= 0.04) & (u < 0.041)) * (50 + (r * 1950).long()))
+    Lt = L[tid.long()]
+    span = torch.minimum(span, Lt)
+    pos = (torch.rand(n_reads, device=dev, generator=g, dtype=torch.float64) *
+           (Lt - span + 1).double()).long()
+    coff = torch.zeros(len(lengths) + 1, dtype=torch.int64, device=dev)
+    coff[1:] = torch.cumsum(L, 0)
+    key = coff[tid.long()] + pos
+    order = torch.argsort(key)
+    del key, u, r
+    return (tid[order].contiguous(), pos[order].to(torch.int32).contiguous(),
+            span[order].to(torch.int32).contiguous(), counts)
+
+
+def cpu_baseline(lengths, tid, pos, span, sample_bases):
+    """The C restatement of the reference's pileup.classic path (htslib-style
+    column walk -> float64 columns -> sort-based stats) on one host core, on
+    the first contigs of this workload up to `sample_bases` aligned bases."""
+    from oracle import coracle
+    per = np.bincount(tid, weights=span.astype(np.float64), minlength=len(lengths))
+    k = int(np.searchsorted(np.cumsum(per), sample_bases)) + 1
+    k = min(k, len(lengths))
+    m = tid < k
+    t, p, s = tid[m], pos[m], span[m]
+    t0 = time.perf_counter()
+    coracle.pileup_classic(t, p, s, np.arange(k, dtype=np.int32), np.zeros(k, np.int64),
+                           lengths[:k].astype(np.int64))
+    dt = time.perf_counter() - t0
+    bases = int(s.astype(np.int64).sum())
+    return {"value": bases / dt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
+            "sample": "first %d of the rank-0 C3 contigs (%d bp, %d reads, %.3g aligned bases), "
+                      "whole-contig regions, %.2f s; oracle/oracle.c orc_pileup_classic "
+                      "(restated htslib column walk + pileup.classic stats)"
+                      % (k, int(lengths[:k].sum()), len(t), bases, dt)}
+
+
+def load_pmc_traffic(root):
+    p = os.path.join(root, "profiles", "pmc_depth_kernel.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        return json.load(fh)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from metacov_amd import synth, dist as mdist
+    from metacov_amd.engine import CoverageEngine, REGION_STAT_DTYPE
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lengths_all, weights_all = synth.c3_workload(args.reads, args.contigs)
+    if args.strong:
+        # one C3 workload, contigs LPT-sharded over the ranks
+        tid, pos, span, counts = device_workload(torch, lengths_all, weights_all, args.reads,
+                                                 args.seed, dev)
+        owned = mdist.lpt_shard(mdist.contig_costs(lengths_all, counts), world)[rank]
+        remap = torch.full((len(lengths_all),), -1, dtype=torch.int32, device=dev)
+        remap[torch.from_numpy(owned).to(dev)] = torch.arange(len(owned), dtype=torch.int32,
+                                                              device=dev)
+        lt = remap[tid.long()]
+        keep = lt >= 0
+        tid, pos, span = lt[keep].contiguous(), pos[keep].contiguous(), span[keep].contiguous()
+        lengths = lengths_all[owned]
+        region_index = owned
+    else:
+        tid, pos, span, _ = device_workload(torch, lengths_all, weights_all, args.reads,
+                                            args.seed + 1000 * rank, dev)
+        lengths = lengths_all
+        region_index = np.arange(len(lengths)) + rank * len(lengths)
+    n_regions_total = int(len(lengths_all) if args.strong else len(lengths_all) * world)
+
+    eng = CoverageEngine(local)
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+    eng.prepare()
+    prep = eng.timings()
+    bases = eng.aligned_bases()
+    R = len(lengths)
+    rt = np.arange(R, dtype=np.int32)
+    rs = np.zeros(R, np.int64)
+    re_ = lengths.astype(np.int64)
+    r_max = int(n_regions_total if args.strong else R)
+    table = torch.empty((R, 9), dtype=torch.int64, device=dev)
+    gathered = None
+
+    def step():
+        nonlocal gathered
+        eng.compute_depth()
+        eng.region_stats_device(rt, rs, re_, table.data_ptr())
+        if world > 1:
+            idx = torch.from_numpy(np.asarray(region_index, np.int64)).to(dev)
+            local_tab = torch.cat([table, idx[:, None]], 1)
+            buf = torch.full((r_max, mdist.ROW_WIDTH), -1, dtype=torch.int64, device=dev)
+            buf[:R] = local_tab
+            out = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(out, buf)
+            gathered = out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    k2, k3 = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        tm = eng.timings()            # syncs the ctx stream; HIP events around K2 / K3
+        k2.append(tm["depth_ms"])
+        k3.append(tm["stats_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_max = elapsed
+    total_bases = bases
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+        b = torch.tensor([bases], dtype=torch.int64, device=dev)
+        dist.all_reduce(b)
+        total_bases = int(b.item())
+        rows = mdist.unpack_rows(gathered.cpu().numpy(), n_regions_total, REGION_STAT_DTYPE)
+        assert int(rows["sum"].sum()) == total_bases, "gathered region table lost bases"
+    else:
+        rows = table.cpu().numpy().view(REGION_STAT_DTYPE).reshape(-1)
+        assert int(rows["sum"].sum()) == total_bases
+
+    # roofline of the dominant kernel (K2)
+    ext_sum = int(sum(eng.contig_offset(t)[1] for t in range(len(lengths))))
+    k2_bytes = 12 * len(tid) + 4 * ext_sum
+    k2_ms = float(np.mean(k2))
+    achieved = k2_bytes / (k2_ms * 1e-3) / 1e9
+    pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
+    traffic = None
+    if pmc and pmc.get("reads") == args.reads and pmc.get("contigs") == args.contigs:
+        traffic = pmc.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(lengths, tid.cpu().numpy(), pos.cpu().numpy(),
+                               span.cpu().numpy(), args.cpu_sample_bases)
+        pcie = None
+        if args.pcie and world == 1:
+            h = [x.cpu().numpy() for x in (tid, pos, span)]
+            e2 = CoverageEngine(local)
+            e2.set_contigs(lengths)
+            t1 = time.perf_counter()
+            e2.add_reads(*h)
+            e2.prepare()
+            e2.compute_depth()
+            e2.region_stats(rt, rs, re_)
+            pcie = time.perf_counter() - t1
+            e2.close()
+        value = total_bases * args.steps / t_max
+        line = {
+            "metric": "aligned bases/sec into per-position depth vector, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "aligned bases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (GPU-generated C3 intervals, SURVEY §8d span mix)",
+            "config": {
+                "workload": ("C3 LPT-sharded by contig over %d GPUs" % world) if args.strong else
+                            "C3 per GPU: %d contigs (~%.2f Gbp), %d x ~150 bp reads, whole-contig "
+                            "region stats" % (args.contigs, lengths_all.sum() / 1e9, args.reads),
+                "contigs_per_gpu": int(len(lengths)),
+                "reads_per_gpu": int(len(tid)),
+                "aligned_bases_per_step": int(total_bases),
+                "regions": n_regions_total,
+                "parallelism": "contig-shard x%d, RCCL all-gather of region table" % world
+                               if world > 1 else "single GPU",
+            },
+            "kernels_ms": {"k2_depth": k2_ms, "k3_region_stats": float(np.mean(k3)),
+                           "prepare_ingest_index": prep["prepare_ms"]},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8000.0, "traffic": traffic,
+                         "kernel": "depth_kernel (K2)",
+                         "algorithmic_bytes_per_launch": int(k2_bytes)},
+            "cpu_baseline": cpu,
+        }
+        if pcie is not None:
+            line["host_buffer_end_to_end_s"] = pcie
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

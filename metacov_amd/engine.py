@@ -115,6 +115,7 @@ class CoverageEngine:
         if _is_torch(tid):
             import torch
             ts = [t.contiguous().to(torch.int32) for t in (tid, pos, span)]
+            torch.cuda.current_stream(ts[0].device).synchronize()   # producer stream -> ctx stream
             n = ts[0].numel()
             if not all(t.is_cuda and t.numel() == n for t in ts):
                 raise ValueError("tid/pos/span must be equally sized device tensors")

@@ -1,0 +1,290 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+goldens.  Integer outputs must be bit-exact; region statistics are compared
+as exact integer rows and as the classic() dicts of the real reference.
+
+Run on an MI355X:  python -m pytest tests -m gpu
+"""
+import hashlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+from metacov_amd import synth
+from metacov_amd._lib import MetacovError, MC_E_INVALID, MC_E_RANGE
+from metacov_amd.bam import BamFile
+from metacov_amd.engine import CoverageEngine, classic_stats
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(lib_built):
+    e = CoverageEngine(0)
+    yield e
+    e.close()
+
+
+def _iv(g):
+    return [np.array(g["intervals"][k], np.int32) for k in ("tid", "pos", "span")]
+
+
+def run_engine(eng, lengths, tid, pos, span):
+    eng.set_contigs(np.asarray(lengths, np.int64))
+    eng.add_reads(tid, pos, span)
+    eng.compute_depth()
+
+
+def check_depth_vs_oracle(eng, lengths, tid, pos, span):
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    for t in range(len(lengths)):
+        got = eng.depth(t, 0, int(ext[t]))
+        assert np.array_equal(got, d[coff[t]:coff[t] + ext[t]]), "contig %d" % t
+        assert eng.contig_offset(t)[1] == ext[t]
+    return d, ext, coff
+
+
+def check_regions_vs_oracle(eng, d, ext, coff, rtid, rs, re_):
+    got = eng.region_stats(rtid, rs, re_)
+    want = coracle.region_stats(d, ext, coff, rtid, rs, re_)
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
+    return got
+
+
+def random_regions(rng, lengths, k):
+    rtid = rng.integers(0, len(lengths), size=k).astype(np.int32)
+    rs = np.array([rng.integers(0, max(1, lengths[t] + 5)) for t in rtid], np.int64)
+    re_ = rs + rng.integers(0, 3000, size=k)
+    return rtid, rs, re_
+
+
+# ------------------------------------------------------------- goldens
+
+def test_fixture_depth_and_stats(eng, fixture_golden):
+    tid, pos, span = _iv(fixture_golden)
+    run_engine(eng, fixture_golden["lengths"], tid, pos, span)
+    for t, gold in enumerate(fixture_golden["depth"]):
+        assert eng.depth(t, 0, len(gold)).tolist() == gold
+    assert eng.aligned_bases() == 340526
+    regs = fixture_golden["blast7"] + fixture_golden["whole"]
+    rows = eng.region_stats([fixture_golden["names"].index(r["sacc"]) for r in regs],
+                            [r["start"] for r in regs], [r["end"] for r in regs])
+    for row, r in zip(rows, regs):
+        assert classic_stats(row) == r["stats"]
+
+
+def test_stats_cases(eng, stats_golden):
+    """Every golden stats vector as a one-contig depth built from reads."""
+    for case in stats_golden:
+        vec = np.array(case["depth"], np.int64)
+        # reads of span 1 reproduce the vector exactly
+        pos = np.repeat(np.arange(len(vec)), vec).astype(np.int32)
+        tid = np.zeros(len(pos), np.int32)
+        span = np.ones(len(pos), np.int32)
+        run_engine(eng, [len(vec)], tid, pos, span)
+        assert np.array_equal(eng.depth(0, 0, len(vec)), vec)
+        row = eng.region_stats([0], [case["start"]], [case["end"]])[0]
+        if "error" in case["stats"]:
+            with pytest.raises(ValueError):
+                classic_stats(row)
+        else:
+            assert classic_stats(row) == case["stats"], case["tag"]
+
+
+@pytest.mark.parametrize("tag", ["synth_edge", "synth_multi"])
+def test_synth_bams(eng, synth_golden, golden_dir, tag):
+    g = synth_golden[tag]
+    bf = BamFile(os.path.join(golden_dir, tag + ".bam"))
+    run_engine(eng, bf.lengths, bf.tid, bf.pos, bf.span)
+    for t in range(len(bf.lengths)):
+        v = np.ascontiguousarray(eng.depth(t, 0, g["extents"][t]), dtype="<i4")
+        assert hashlib.sha256(v.tobytes()).hexdigest() == g["depth_sha"][t]
+        assert int(v.sum()) == g["depth_sum"][t]
+    regs = g["regions"]
+    rows = eng.region_stats([g["names"].index(r["sacc"]) for r in regs],
+                            [r["start"] for r in regs], [r["end"] for r in regs])
+    for row, r in zip(rows, regs):
+        assert classic_stats(row) == r["stats"], r
+
+
+@pytest.mark.parametrize("tag", ["synth_edge", "synth_longcigar"])
+def test_cigar_mode(eng, golden_dir, tag):
+    bf = BamFile(os.path.join(golden_dir, tag + ".bam"), keep_cigar=True)
+    eng.set_contigs(np.asarray(bf.lengths, np.int64))
+    eng.add_reads_cigar(bf.tid, bf.pos, bf.cig_off, bf.cigar)
+    eng.compute_depth()
+    got = [eng.depth(t) for t in range(len(bf.lengths))]
+    run_engine(eng, bf.lengths, bf.tid, bf.pos, bf.span)
+    for t in range(len(bf.lengths)):
+        assert np.array_equal(got[t], eng.depth(t))
+
+
+# ------------------------------------------------------------- oracle parity
+
+CASES = {
+    # name: (lengths, n_reads, span range, seed)
+    "one_contig": ([300_000], 20_000, (1, 200), 1),
+    "tiny_contigs": ([0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 65535, 65536, 65537], 3_000, (1, 30), 2),
+    "chunk_edges": ([65536 * 3 + 17, 4096 * 5], 40_000, (1, 9000), 3),
+    "long_spans": ([400_000, 90_000], 6_000, (20_000, 28_600), 4),
+    "many_contigs": (list(range(1, 2000, 7)), 50_000, (1, 150), 5),
+}
+
+
+def make_case(lengths, n, span_rng, seed, overhang=True):
+    rng = np.random.default_rng(seed)
+    lengths = np.asarray(lengths, np.int64)
+    live = np.nonzero(lengths > 0)[0]
+    tid = rng.choice(live, size=n).astype(np.int32)
+    pos = (rng.random(n) * lengths[tid]).astype(np.int32)
+    span = rng.integers(span_rng[0], span_rng[1] + 1, size=n).astype(np.int32)
+    if not overhang:
+        span = np.minimum(span, (lengths[tid] - pos)).astype(np.int32)
+    o = np.lexsort((pos, tid))
+    return lengths, tid[o], pos[o], span[o]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_random_vs_oracle(eng, name):
+    lengths, tid, pos, span = make_case(*CASES[name])
+    run_engine(eng, lengths, tid, pos, span)
+    d, ext, coff = check_depth_vs_oracle(eng, lengths, tid, pos, span)
+    assert eng.aligned_bases() == int(span.astype(np.int64).sum()) == int(d.sum())
+    assert eng.max_depth() == int(d.max())
+    rtid, rs, re_ = random_regions(np.random.default_rng(7), lengths, 300)
+    whole_t = np.arange(len(lengths), dtype=np.int32)
+    check_regions_vs_oracle(eng, d, ext, coff, np.concatenate([rtid, whole_t]),
+                            np.concatenate([rs, np.zeros(len(lengths), np.int64)]),
+                            np.concatenate([re_, lengths]))
+
+
+def test_empty_and_single(eng):
+    run_engine(eng, [1000, 5], np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int32))
+    assert eng.depth(0).sum() == 0 and eng.max_depth() == 0
+    row = eng.region_stats([0], [10], [20])[0]
+    assert classic_stats(row) == {"min": 0, "max": 0, "med": 0, "std": 0.0, "avg": 0.0,
+                                  "q23": 0.0, "sum": 0}
+    run_engine(eng, [1000], np.zeros(1, np.int32), np.array([998], np.int32), np.array([5], np.int32))
+    d = eng.depth(0, 0, 1005)
+    assert d[998:1003].tolist() == [1] * 5 and d.sum() == 5
+    assert eng.contig_offset(0)[1] == 1003          # read runs past the end
+
+
+def test_high_depth_histogram_paths(eng):
+    # LDS histogram (<= 16384 bins) and the global-histogram path beyond
+    for depth_target in (5_000, 20_000):
+        n = depth_target
+        tid = np.zeros(n, np.int32)
+        pos = np.sort(np.random.default_rng(depth_target).integers(0, 50, size=n)).astype(np.int32)
+        span = np.full(n, 100, np.int32)
+        lengths = [1000]
+        run_engine(eng, lengths, tid, pos, span)
+        d, ext, coff = check_depth_vs_oracle(eng, lengths, tid, pos, span)
+        check_regions_vs_oracle(eng, d, ext, coff, np.array([0, 0], np.int32),
+                                np.array([0, 40], np.int64), np.array([1000, 300], np.int64))
+
+
+def test_append_equals_single(eng):
+    lengths, tid, pos, span = make_case([200_000, 7000], 30_000, (1, 300), 11)
+    run_engine(eng, lengths, tid, pos, span)
+    a = [eng.depth(t) for t in range(2)]
+    eng.set_contigs(lengths)
+    for part in np.array_split(np.arange(len(tid)), 3):
+        eng.add_reads(tid[part], pos[part], span[part])
+    eng.compute_depth()
+    eng.compute_depth()          # idempotent
+    for t in range(2):
+        assert np.array_equal(a[t], eng.depth(t))
+
+
+def test_device_tensor_input(eng):
+    import torch
+    lengths, tid, pos, span = make_case([100_000], 10_000, (1, 150), 12)
+    eng.set_contigs(lengths)
+    eng.add_reads(*(torch.from_numpy(x).cuda() for x in (tid, pos, span)))
+    eng.compute_depth()
+    d, _, _ = coracle.depth(lengths, tid, pos, span)
+    assert np.array_equal(eng.depth(0, 0, len(d)), d)
+
+
+def test_errors(eng):
+    eng.set_contigs([100])
+    eng.add_reads(np.array([0, 0], np.int32), np.array([5, 3], np.int32), np.array([1, 1], np.int32))
+    with pytest.raises(MetacovError) as ei:
+        eng.compute_depth()
+    assert ei.value.code == MC_E_INVALID and "sorted" in str(ei.value)
+    eng.set_contigs([100])
+    eng.add_reads(np.array([1], np.int32), np.array([5], np.int32), np.array([1], np.int32))
+    with pytest.raises(MetacovError):
+        eng.compute_depth()
+    eng.set_contigs([100_000])
+    eng.add_reads(np.array([0], np.int32), np.array([5], np.int32), np.array([40_000], np.int32))
+    with pytest.raises(MetacovError) as ei:
+        eng.compute_depth()
+    assert ei.value.code == MC_E_RANGE
+    eng.set_contigs([100])
+    eng.add_reads(np.array([0], np.int32), np.array([5], np.int32), np.array([3], np.int32))
+    eng.compute_depth()
+    with pytest.raises(MetacovError):
+        eng.region_stats([0], [10], [5])
+    with pytest.raises(MetacovError):
+        eng.region_stats([3], [0], [5])
+
+
+# ------------------------------------------------------------- full size
+
+def test_c2_full_size(eng):
+    """BASELINE config 2: 1 contig x 5 Mbp, 10M x 150 bp: bit-exact depth."""
+    tid, pos, span = synth.interval_workload([5_000_000], 10_000_000, seed=1)
+    lengths = [5_000_000]
+    run_engine(eng, lengths, tid, pos, span)
+    d, ext, coff = check_depth_vs_oracle(eng, lengths, tid, pos, span)
+    assert eng.aligned_bases() == int(d.sum())
+    check_regions_vs_oracle(eng, d, ext, coff, np.zeros(3, np.int32),
+                            np.array([0, 1_000_000, 4_999_000], np.int64),
+                            np.array([5_000_000, 3_000_001, 5_000_100], np.int64))
+
+
+def test_c3_shape_properties(eng):
+    """C3 shape (1000 contigs, ~1 Gbp, lognormal abundance) at 20M reads:
+    depth bit-exact vs the oracle; every whole-contig stat row exact."""
+    lengths, weights = synth.c3_workload()
+    tid, pos, span = synth.interval_workload(lengths, 20_000_000, seed=3, weights=weights)
+    run_engine(eng, lengths, tid, pos, span)
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    ptr_, total = eng.depth_device()
+    got = np.concatenate([eng.depth(t, 0, int(ext[t])) for t in range(len(lengths))])
+    want = np.concatenate([d[coff[t]:coff[t] + ext[t]] for t in range(len(lengths))])
+    assert np.array_equal(got, want)
+    check_regions_vs_oracle(eng, d, ext, coff, np.arange(len(lengths), dtype=np.int32),
+                            np.zeros(len(lengths), np.int64), lengths)
+
+
+# ------------------------------------------------------------- drop-in API
+
+def test_classic_api(lib_built, fixture_golden, golden_dir):
+    from metacov_amd import pileup
+    path = os.path.join(golden_dir, "bbmap.sorted.bam")
+    for r in fixture_golden["blast7"] + fixture_golden["whole"]:
+        assert pileup.classic(path, r["sacc"], r["start"], r["end"]) == r["stats"]
+    with pytest.raises(KeyError):
+        pileup.classic(path, "nope", 0, 10)
+    with pytest.raises(ValueError):
+        pileup.classic(path, "ref1", 5, 5)
+    assert pileup.depth(path, "ref1").tolist() == fixture_golden["depth"][0]
+
+
+@pytest.mark.parametrize("mode", ["blast7", "whole"])
+def test_cli_csv_bytes(lib_built, fixture_golden, golden_dir, tmp_path, mode):
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    args = ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"), "-o", str(tmp_path / "o.csv")]
+    if mode == "blast7":
+        args += ["-rb", os.path.join(golden_dir, "regions.blast7")]
+    res = CliRunner().invoke(cli_pileup, args)
+    assert res.exit_code == 0, res.output
+    with open(tmp_path / "o.csv", newline="") as fh:
+        assert fh.read() == fixture_golden["csv_" + mode]
