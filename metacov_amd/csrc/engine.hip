@@ -85,6 +85,14 @@ struct mc_ctx {
     int tiles_per_chunk = 16;
     int64_t chunk_w = 0, n_chunks = 0, total_len = 0;
     DevBuf<int64_t> d_chunk_first;
+    // long-read path (spans > short_max)
+    bool has_long = false;
+    int short_max = 0;
+    int64_t n_long_events = 0;
+    DevBuf<unsigned> d_tile_cnt;
+    DevBuf<int64_t> d_tile_off;
+    DevBuf<int32_t> d_tile_ev;
+    DevBuf<int> d_chunk_carry;
     DevBuf<int32_t> d_depth;
     bool depth_valid = false;
     int32_t max_depth = -1;
@@ -158,6 +166,10 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_cig_off.release();
     ctx->d_cigar.release();
     ctx->d_chunk_first.release();
+    ctx->d_tile_cnt.release();
+    ctx->d_tile_off.release();
+    ctx->d_tile_ev.release();
+    ctx->d_chunk_carry.release();
     ctx->d_depth.release();
     ctx->d_scratch.release();
     ctx->d_maxend.release();
@@ -358,27 +370,71 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     }
     ctx->coff[nc] = off;
     ctx->total_len = off;
-    int ring = 2 * kTileW;
-    while (ring < kTileW + ctx->max_span) ring *= 2;
-    MC_REQUIRE(ring <= 32768, MC_E_RANGE,
-               "max span %d exceeds the LDS ring capacity (%d); long-read tiling is not "
-               "implemented in this build", ctx->max_span, 32768 - kTileW);
-    ctx->ring = ring;
+    // LDS ring of 2 tiles: reads up to short_max = ring - kTileW keep both
+    // events in LDS; longer ones take the bucketed long-read path.
+    ctx->ring = 2 * kTileW;
+    ctx->short_max = ctx->ring - kTileW;
     ctx->tiles_per_chunk = 16;
     ctx->chunk_w = (int64_t)ctx->tiles_per_chunk * kTileW;
     ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
+    const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
+    const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
     HIP_TRY(ctx->d_coff.reserve(nc + 1));
     HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(ctx->d_chunk_first.reserve(ctx->n_chunks));
-    HIP_TRY(ctx->d_depth.reserve((size_t)(ctx->n_chunks * ctx->chunk_w)));
+    HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
+    const int64_t halo = std::min<int64_t>(ctx->max_span, ctx->short_max);
     if (n) {
         const int64_t nb = (ctx->n_chunks + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, n, ctx->d_coff.p, ctx->chunk_w, (int64_t)ctx->max_span,
-                           ctx->n_chunks, ctx->d_chunk_first.p);
+                           ctx->d_pos.p, n, ctx->d_coff.p, ctx->chunk_w, halo, ctx->n_chunks,
+                           ctx->d_chunk_first.p);
         HIP_TRY(hipGetLastError());
     } else {
         HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, ctx->n_chunks * 8, s));
+    }
+    ctx->has_long = ctx->max_span > ctx->short_max;
+    ctx->n_long_events = 0;
+    if (ctx->has_long) {
+        HIP_TRY(ctx->d_tile_cnt.reserve(n_tiles + 1));
+        HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
+        HIP_TRY(ctx->d_tile_off.reserve(n_tiles + 1));
+        HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
+        const int64_t nb = std::min<int64_t>((n + kBlock - 1) / kBlock, 8192);
+        hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                           ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len,
+                           ctx->chunk_w, ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
+        HIP_TRY(hipGetLastError());
+        std::vector<unsigned> cnt(n_tiles + 1);
+        std::vector<int> cdiff(ctx->n_chunks + 1);
+        HIP_TRY(hipMemcpyAsync(cnt.data(), ctx->d_tile_cnt.p, (n_tiles + 1) * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(cdiff.data(), ctx->d_chunk_carry.p, (ctx->n_chunks + 1) * 4,
+                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int64_t> toff(n_tiles + 1);
+        int64_t acc = 0;
+        for (int64_t t = 0; t < n_tiles; ++t) {
+            toff[t] = acc;
+            acc += cnt[t];
+        }
+        toff[n_tiles] = acc;
+        int run = 0;
+        for (int64_t c = 0; c < ctx->n_chunks; ++c) {
+            run += cdiff[c];
+            cdiff[c] = run;
+        }
+        ctx->n_long_events = acc;
+        HIP_TRY(ctx->d_tile_ev.reserve(std::max<int64_t>(acc, 1)));
+        HIP_TRY(hipMemcpyAsync(ctx->d_tile_off.p, toff.data(), (n_tiles + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->d_chunk_carry.p, cdiff.data(), ctx->n_chunks * 4,
+                               hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
+        hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                           ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len,
+                           ctx->chunk_w, ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(s));   // host vectors go out of scope
     }
     HIP_TRY(hipEventRecord(ctx->ev[3], s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -411,7 +467,10 @@ extern "C" int mc_compute_depth(mc_ctx* ctx) {
     HIP_TRY(hipEventRecord(ctx->ev[4], s));
     hipLaunchKernelGGL(depth_kernel, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p, ctx->d_pos.p,
                        ctx->d_span.p, ctx->n_reads, ctx->d_coff.p, ctx->d_chunk_first.p,
-                       ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1, ctx->d_depth.p,
+                       ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1, ctx->short_max,
+                       ctx->has_long ? ctx->d_tile_off.p : nullptr,
+                       ctx->has_long ? ctx->d_tile_ev.p : nullptr,
+                       ctx->has_long ? ctx->d_chunk_carry.p : nullptr, ctx->d_depth.p,
                        ctx->d_queue.p, ctx->d_maxdepth.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[5], s));

@@ -127,6 +127,56 @@ chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ 
     chunk_first[c] = lo;
 }
 
+// ------------------------------------------------------ long reads (prepare)
+//
+// Reads longer than `short_max` (= ring - kTileW) cannot keep their -1 end
+// event in the LDS ring.  For them:
+//   * +1 is applied by K2 in-stream at the read start (its own chunk only);
+//   * -1 goes to an end-event bucket of the tile holding the end (CSR over
+//     tiles, filled here, applied by K2 at the start of that tile);
+//   * chunk_diff builds the count of long reads covering each chunk's first
+//     position that started in an earlier chunk (K2's initial carry).
+
+__global__ void __launch_bounds__(kBlock)
+long_count_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+                  const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
+                  int short_max, int64_t alloc_len, int64_t chunk_w,
+                  unsigned* __restrict__ tile_cnt, int* __restrict__ chunk_diff) {
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const int sp = span[i];
+        if (sp <= short_max) continue;
+        const int64_t gs = coff[tid[i]] + pos[i];
+        const int64_t ge = gs + sp;
+        // an end exactly on a chunk start needs no event: that chunk's carry
+        // excludes the read already
+        if (ge < alloc_len && ge % chunk_w) atomicAdd(&tile_cnt[ge / kTileW], 1u);
+        const int64_t c0 = gs / chunk_w + 1, c1 = (ge - 1) / chunk_w + 1;
+        if (c1 > c0) {
+            atomicAdd(&chunk_diff[c0], 1);
+            atomicSub(&chunk_diff[c1], 1);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+                 const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
+                 int short_max, int64_t alloc_len, int64_t chunk_w,
+                 const int64_t* __restrict__ tile_off,
+                 unsigned* __restrict__ tile_cursor, int32_t* __restrict__ ev) {
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const int sp = span[i];
+        if (sp <= short_max) continue;
+        const int64_t ge = coff[tid[i]] + pos[i] + sp;
+        if (ge >= alloc_len || ge % chunk_w == 0) continue;
+        const int64_t t = ge / kTileW;
+        const unsigned slot = atomicAdd(&tile_cursor[t], 1u);
+        ev[tile_off[t] + slot] = (int32_t)(ge - t * kTileW);
+    }
+}
+
 // ----------------------------------------------------------------- K1
 
 // One workgroup per 256 reads; the block streams the contiguous CIGAR words
@@ -217,12 +267,15 @@ __device__ __forceinline__ void load_batch(ReadBatch& b, int64_t base, int64_t n
 // and -1 at end into an LDS ring of `ring` ints; each finished tile is
 // prefix-scanned (int4 per lane, wave scan, block carry) and stored to HBM
 // with 1 KiB-per-wave-instruction stores, and its ring slots are zeroed.
-// Requires ring >= kTileW + max_span, ring a power-of-two multiple of kTileW.
+// Reads longer than short_max = ring - kTileW take the long-read path (see
+// long_count_kernel); the halo of chunk_first is min(max_span, short_max).
 __global__ void __launch_bounds__(kBlock)
 depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              const int32_t* __restrict__ span, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
-             int64_t n_chunks, int tiles_per_chunk, int ring_mask,
+             int64_t n_chunks, int tiles_per_chunk, int ring_mask, int short_max,
+             const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
+             const int* __restrict__ chunk_carry,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
              int* __restrict__ max_depth) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
@@ -250,20 +303,31 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         ReadBatch b;
         if (more) load_batch(b, base, n, tid, pos, span, coff);
         else b.pending = 0;
-        int carry = 0;
+        const bool has_long = tile_ev_off != nullptr;
+        int carry = has_long ? chunk_carry[c] : 0;
         for (int t = 0; t < tiles_per_chunk; ++t) {
             const int64_t T0 = C0 + (int64_t)t * kTileW;
             const int64_t Tend = T0 + kTileW;
+            if (has_long) {   // -1 end events of long reads ending in this tile
+                const int64_t tt = T0 / kTileW;
+                const int64_t e0 = tile_ev_off[tt], e1 = tile_ev_off[tt + 1];
+                for (int64_t k = e0 + threadIdx.x; k < e1; k += kBlock)
+                    atomicAdd(&ring[(int)((T0 + tile_ev[k]) & ring_mask)], -1);
+            }
             for (;;) {
 #pragma unroll
                 for (int k = 0; k < kReadsPerThread; ++k) {
                     if ((b.pending >> k) & 1u) {
                         if (b.gs[k] < Tend) {
-                            const int64_t s = b.gs[k] > C0 ? b.gs[k] : C0;
                             const int64_t e = b.ge[k];
-                            if (e > s) {
-                                atomicAdd(&ring[(int)(s & ring_mask)], 1);
-                                atomicAdd(&ring[(int)(e & ring_mask)], -1);
+                            if (e - b.gs[k] <= short_max) {
+                                const int64_t s = b.gs[k] > C0 ? b.gs[k] : C0;
+                                if (e > s) {
+                                    atomicAdd(&ring[(int)(s & ring_mask)], 1);
+                                    atomicAdd(&ring[(int)(e & ring_mask)], -1);
+                                }
+                            } else if (b.gs[k] >= C0) {   // long read: +1 here, -1 bucketed
+                                atomicAdd(&ring[(int)(b.gs[k] & ring_mask)], 1);
                             }
                             b.pending &= ~(1u << k);
                         }

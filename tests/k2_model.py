@@ -1,0 +1,46 @@
+"""Executable model of K2's decomposition (metacov_amd/csrc/kernels.h,
+depth_kernel + chunk_index_kernel + long_count/long_fill kernels), in numpy.
+
+TEST INFRASTRUCTURE: it checks the ALGORITHM (chunks of 16 tiles of 4096
+positions, an 8192-slot ring, the max-span halo, long-read end-event buckets
+and per-chunk carries) against the oracle on the CPU, so that decomposition
+bugs show up without a GPU.  Constants must match kernels.h.
+"""
+import numpy as np
+from oracle import coracle
+W=4096; TPC=16; CW=W*TPC; RING=8192; SM=RING-W
+def model(lengths, tid, pos, span):
+    ext, coff64 = coracle.layout(lengths, tid, pos, span)
+    coff=np.zeros(len(ext)+1,np.int64); 
+    for i in range(len(ext)): coff[i+1]=coff[i]+ (ext[i]+63)//64*64
+    G=coff[-1]; nch=max(1,(G+CW-1)//CW); alloc=nch*CW
+    gs=coff[tid]+pos; ge=gs+span
+    ms=span.max() if len(span) else 0; halo=min(ms,SM)
+    long_=span>SM
+    # events
+    ev={}
+    cdiff=np.zeros(nch+1,np.int64)
+    for a,b in zip(gs[long_],ge[long_]):
+        if b<alloc and b%CW: ev.setdefault(b//W,[]).append(b-(b//W)*W)
+        c0=a//CW+1; c1=(b-1)//CW+1
+        if c1>c0: cdiff[c0]+=1; cdiff[c1]-=1
+    carry_c=np.cumsum(cdiff)[:nch]
+    depth=np.zeros(alloc,np.int64)
+    for c in range(nch):
+        C0=c*CW
+        first=np.searchsorted(gs, C0-halo, 'left') & ~3
+        ring=np.zeros(RING,np.int64)
+        i=first; carry=carry_c[c] if long_.any() else 0
+        for t in range(TPC):
+            T0=C0+t*W; Tend=T0+W
+            for o in ev.get(T0//W,[]): ring[(T0+o)&(RING-1)]-=1
+            while i<len(gs) and gs[i]<Tend:
+                if ge[i]-gs[i]<=SM:
+                    s=max(gs[i],C0); e=ge[i]
+                    if e>s: ring[s&(RING-1)]+=1; ring[e&(RING-1)]-=1
+                elif gs[i]>=C0: ring[gs[i]&(RING-1)]+=1
+                i+=1
+            sl=np.arange(T0,Tend)&(RING-1)
+            vals=carry+np.cumsum(ring[sl]); ring[sl]=0
+            depth[T0:Tend]=vals; carry=vals[-1]
+    return depth, coff, ext
