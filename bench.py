@@ -31,6 +31,8 @@ def parse():
     ap.add_argument("--reads", type=int, default=100_000_000, help="reads per C3 workload")
     ap.add_argument("--contigs", type=int, default=1000)
     ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--unfused", action="store_true",
+                    help="K2 then a separate K3 pass instead of the fused K2 statistics")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bases", type=float, default=3.0e9,
                     help="aligned bases in the CPU-baseline sample (~10-20 s on one core)")
@@ -152,8 +154,11 @@ def main():
 
     def step():
         nonlocal gathered
-        eng.compute_depth()
-        eng.region_stats_device(rt, rs, re_, table.data_ptr())
+        if args.unfused:
+            eng.compute_depth()
+            eng.region_stats_device(rt, rs, re_, table.data_ptr())
+        else:
+            eng.compute_depth_stats_device(rt, rs, re_, table.data_ptr())
         if world > 1:
             idx = torch.from_numpy(np.asarray(region_index, np.int64)).to(dev)
             local_tab = torch.cat([table, idx[:, None]], 1)
@@ -194,7 +199,8 @@ def main():
         assert int(rows["sum"].sum()) == total_bases, "gathered region table lost bases"
     else:
         rows = table.cpu().numpy().view(REGION_STAT_DTYPE).reshape(-1)
-        assert int(rows["sum"].sum()) == total_bases
+        if not os.environ.get("MC_BENCH_NOCHECK"):   # set only for deliberately-wrong A/B builds
+            assert int(rows["sum"].sum()) == total_bases
 
     # roofline of the dominant kernel (K2)
     ext_sum = int(sum(eng.contig_offset(t)[1] for t in range(len(lengths))))
@@ -203,7 +209,9 @@ def main():
     achieved = k2_bytes / (k2_ms * 1e-3) / 1e9
     pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
     traffic = None
-    if pmc and pmc.get("reads") == args.reads and pmc.get("contigs") == args.contigs:
+    variant = "depth_kernel<%s>" % ("false" if args.unfused else "true")
+    if pmc and pmc.get("reads") == args.reads and pmc.get("contigs") == args.contigs \
+            and variant in pmc.get("kernel", ""):
         traffic = pmc.get("hbm_bytes_per_launch")
 
     if rank == 0:
@@ -248,11 +256,12 @@ def main():
                 "parallelism": "contig-shard x%d, RCCL all-gather of region table" % world
                                if world > 1 else "single GPU",
             },
-            "kernels_ms": {"k2_depth": k2_ms, "k3_region_stats": float(np.mean(k3)),
+            "kernels_ms": {"k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
+                           ("k3_region_stats" if args.unfused else "k3b_finalize"): float(np.mean(k3)),
                            "prepare_ingest_index": prep["prepare_ms"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": traffic,
-                         "kernel": "depth_kernel (K2)",
+                         "kernel": "depth_kernel<%s> (K2)" % ("false" if args.unfused else "true"),
                          "algorithmic_bytes_per_launch": int(k2_bytes)},
             "cpu_baseline": cpu,
         }

@@ -137,6 +137,21 @@ int mc_region_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
                            const int64_t* start, const int64_t* end,
                            mc_region_stat* d_out);
 
+/* Depth AND region statistics in one pass: K2 folds every tile into the
+ * regions covering it while the depth values are still in registers, so the
+ * depth vector is written once and never re-read.  Regions must not overlap
+ * each other for the fused path (whole contigs, a tiling of a contig, most
+ * BLAST hit lists); otherwise this runs K2 then K3.  Same rows as
+ * mc_region_stats.  Regions whose median / q23 ranks reach depths >= 1024
+ * are recomputed exactly by K3 (mc_fused_fallbacks counts them). */
+int mc_compute_depth_stats(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                           const int64_t* start, const int64_t* end,
+                           mc_region_stat* out);
+int mc_compute_depth_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                                  const int64_t* start, const int64_t* end,
+                                  mc_region_stat* d_out);
+int mc_fused_fallbacks(mc_ctx* ctx, int64_t* out);
+
 /* Aligned bases (sum of spans) of the reads added so far. */
 int mc_aligned_bases(mc_ctx* ctx, int64_t* out);
 int mc_max_depth(mc_ctx* ctx, int32_t* out);

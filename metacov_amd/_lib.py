@@ -71,6 +71,9 @@ SIGNATURES = {
     "mc_contig_offset": [_P, _I32, _PI64, _PI64],
     "mc_region_stats": [_P, _I64, _P, _P, _P, _P],
     "mc_region_stats_device": [_P, _I64, _P, _P, _P, _P],
+    "mc_compute_depth_stats": [_P, _I64, _P, _P, _P, _P],
+    "mc_compute_depth_stats_device": [_P, _I64, _P, _P, _P, _P],
+    "mc_fused_fallbacks": [_P, _PI64],
     "mc_aligned_bases": [_P, _PI64],
     "mc_max_depth": [_P, _PI32],
     "mc_get_timings": [_P, ctypes.POINTER(Timings)],

@@ -107,6 +107,12 @@ struct mc_ctx {
     DevBuf<unsigned> d_hist;
     DevBuf<RegionAcc> d_acc;
     DevBuf<RegionOut> d_out;
+    // fused K2 statistics
+    DevBuf<int64_t> d_fgs, d_fge, d_fchunk;
+    DevBuf<int32_t> d_fid;
+    DevBuf<unsigned> d_fhist, d_fover;
+    DevBuf<int> d_fflag;
+    int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
     mc_timings t{};
@@ -183,6 +189,13 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_hist.release();
     ctx->d_acc.release();
     ctx->d_out.release();
+    ctx->d_fgs.release();
+    ctx->d_fchunk.release();
+    ctx->d_fge.release();
+    ctx->d_fid.release();
+    ctx->d_fhist.release();
+    ctx->d_fover.release();
+    ctx->d_fflag.release();
     for (auto ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -455,23 +468,32 @@ static int occupancy_grid(const void* kernel, size_t lds, int64_t work, int* gri
     return MC_OK;
 }
 
-extern "C" int mc_compute_depth(mc_ctx* ctx) {
-    if (int rc = ctx_use(ctx)) return rc;
-    if (int rc = mc_prepare(ctx)) return rc;
+// K2 launch (plain or with fused region statistics)
+static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring) * 4;
+    const bool stats = fr.n > 0;
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins : 0)) * 4;
+    const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
     int grid = 0;
-    if (int rc = occupancy_grid((const void*)depth_kernel, lds, ctx->n_chunks, &grid)) return rc;
+    if (int rc = occupancy_grid(kfn, lds, ctx->n_chunks, &grid)) return rc;
     HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
     HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
     HIP_TRY(hipEventRecord(ctx->ev[4], s));
-    hipLaunchKernelGGL(depth_kernel, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p, ctx->d_pos.p,
-                       ctx->d_span.p, ctx->n_reads, ctx->d_coff.p, ctx->d_chunk_first.p,
-                       ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1, ctx->short_max,
-                       ctx->has_long ? ctx->d_tile_off.p : nullptr,
-                       ctx->has_long ? ctx->d_tile_ev.p : nullptr,
-                       ctx->has_long ? ctx->d_chunk_carry.p : nullptr, ctx->d_depth.p,
-                       ctx->d_queue.p, ctx->d_maxdepth.p);
+    const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
+    const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
+    const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
+    if (stats)
+        hipLaunchKernelGGL(depth_kernel<true>, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,
+                           ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,
+                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1,
+                           ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
+                           ctx->d_maxdepth.p, fr);
+    else
+        hipLaunchKernelGGL(depth_kernel<false>, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,
+                           ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,
+                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1,
+                           ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
+                           ctx->d_maxdepth.p, fr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[5], s));
     ctx->t_depth = true;
@@ -479,6 +501,13 @@ extern "C" int mc_compute_depth(mc_ctx* ctx) {
     ctx->depth_valid = true;
     ctx->max_depth = -1;   // read lazily
     return MC_OK;
+}
+
+extern "C" int mc_compute_depth(mc_ctx* ctx) {
+    if (int rc = ctx_use(ctx)) return rc;
+    if (int rc = mc_prepare(ctx)) return rc;
+    FusedRegions none{};
+    return launch_depth(ctx, none);
 }
 
 static int fetch_max_depth(mc_ctx* ctx) {
@@ -609,7 +638,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
         }
         hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)nr), dim3(kBlock), 0, s,
                            ctx->d_hist.p, nbins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p,
-                           d_out_final + r0);
+                           d_out_final + r0, (int*)nullptr, 0);
         HIP_TRY(hipGetLastError());
         // the host vectors die at scope end: finish the copies first
         HIP_TRY(hipStreamSynchronize(s));
@@ -617,6 +646,149 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
     ctx->t.stats_launches += launches;
+    return MC_OK;
+}
+
+// Depth + region statistics in one K2 pass (regions folded into the tiles
+// while they are in registers), then the histogram finalize.  Needs regions
+// that do not overlap each other; otherwise K2 then K3.  Regions whose order
+// statistics reach depths >= kHistBins are recomputed by K3.
+static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                            const int64_t* end, RegionOut* d_out) {
+    if (int rc = mc_prepare(ctx)) return rc;
+    MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
+    const int32_t nc = (int32_t)ctx->len.size();
+    struct Reg { int64_t gs, ge; int32_t id; };
+    std::vector<Reg> regs;
+    regs.reserve(R);
+    std::vector<int64_t> ntot(std::max<int64_t>(R, 1)), nzx(std::max<int64_t>(R, 1));
+    for (int64_t r = 0; r < R; ++r) {
+        MC_REQUIRE(tid[r] >= 0 && tid[r] < nc, MC_E_INVALID, "region %lld: tid %d out of range",
+                   (long long)r, tid[r]);
+        MC_REQUIRE(start[r] >= 0 && end[r] >= start[r], MC_E_INVALID,
+                   "region %lld: bad range [%lld, %lld)", (long long)r, (long long)start[r],
+                   (long long)end[r]);
+        const int64_t ext = ctx->extent[tid[r]];
+        const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
+        ntot[r] = end[r] - start[r];
+        nzx[r] = ntot[r] - (b - a);
+        if (b > a) regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r});
+    }
+    std::sort(regs.begin(), regs.end(), [](const Reg& x, const Reg& y) { return x.gs < y.gs; });
+    bool overlap = false;
+    for (size_t k = 1; k < regs.size(); ++k) overlap |= regs[k].gs < regs[k - 1].ge;
+    const bool fusable = R > 0 && !overlap && R * (int64_t)kHistBins <= (int64_t(1) << 28);
+    if (!fusable) {
+        FusedRegions none{};
+        if (int rc = launch_depth(ctx, none)) return rc;
+        return region_stats_impl(ctx, R, tid, start, end, d_out);
+    }
+    hipStream_t s = ctx->stream;
+    const int64_t nf = (int64_t)regs.size();
+    std::vector<int64_t> fgs(std::max<int64_t>(nf, 1)), fge(std::max<int64_t>(nf, 1));
+    std::vector<int32_t> fid(std::max<int64_t>(nf, 1));
+    for (int64_t k = 0; k < nf; ++k) {
+        fgs[k] = regs[k].gs;
+        fge[k] = regs[k].ge;
+        fid[k] = regs[k].id;
+    }
+    // first region (sorted order) ending after each chunk start: a merge walk
+    std::vector<int64_t> fchunk(ctx->n_chunks);
+    for (int64_t c = 0, k = 0; c < ctx->n_chunks; ++c) {
+        const int64_t C0 = c * ctx->chunk_w;
+        while (k < nf && fge[k] <= C0) ++k;
+        fchunk[c] = k;
+    }
+    HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
+    HIP_TRY(hipMemcpyAsync(ctx->d_fchunk.p, fchunk.data(), ctx->n_chunks * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx->d_fgs.reserve(std::max<int64_t>(nf, 1)));
+    HIP_TRY(ctx->d_fge.reserve(std::max<int64_t>(nf, 1)));
+    HIP_TRY(ctx->d_fid.reserve(std::max<int64_t>(nf, 1)));
+    HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
+    HIP_TRY(ctx->d_fover.reserve(R));
+    HIP_TRY(ctx->d_fflag.reserve(R));
+    HIP_TRY(ctx->d_acc.reserve(R));
+    HIP_TRY(ctx->d_ntot.reserve(R));
+    HIP_TRY(ctx->d_nzx.reserve(R));
+    if (nf) {
+        HIP_TRY(hipMemcpyAsync(ctx->d_fgs.p, fgs.data(), nf * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->d_fge.p, fge.data(), nf * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->d_fid.p, fid.data(), nf * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->d_ntot.p, ntot.data(), R * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->d_nzx.p, nzx.data(), R * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(ctx->d_fhist.p, 0, (size_t)(R * kHistBins) * 4, s));
+    HIP_TRY(hipMemsetAsync(ctx->d_fover.p, 0, R * 4, s));
+    hipLaunchKernelGGL(region_init_kernel, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, s, ctx->d_acc.p, R);
+    HIP_TRY(hipGetLastError());
+    FusedRegions fr{nf, ctx->d_fchunk.p, ctx->d_fgs.p, ctx->d_fge.p, ctx->d_fid.p, ctx->d_acc.p,
+                    ctx->d_fhist.p, ctx->d_fover.p};
+    if (nf == 0) fr.n = 0;
+    if (int rc = launch_depth(ctx, fr)) return rc;
+    HIP_TRY(hipEventRecord(ctx->ev[6], s));
+    hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
+                       kHistBins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p, d_out, ctx->d_fflag.p, 1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev[7], s));
+    ctx->t_stats = true;
+    ctx->t.stats_launches += 1;
+    std::vector<int> flags(R);
+    HIP_TRY(hipMemcpyAsync(flags.data(), ctx->d_fflag.p, R * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<int32_t> ft;
+    std::vector<int64_t> fs, fe, fr_idx;
+    for (int64_t r = 0; r < R; ++r)
+        if (flags[r]) {
+            ft.push_back(tid[r]);
+            fs.push_back(start[r]);
+            fe.push_back(end[r]);
+            fr_idx.push_back(r);
+        }
+    ctx->fused_fallbacks = (int64_t)ft.size();
+    if (!ft.empty()) {
+        const int64_t nfb = (int64_t)ft.size();
+        DevBuf<RegionOut> tmp;
+        HIP_TRY(tmp.reserve(nfb));
+        int rc = region_stats_impl(ctx, nfb, ft.data(), fs.data(), fe.data(), tmp.p);
+        if (rc == MC_OK) {
+            for (int64_t k = 0; k < nfb && rc == MC_OK; ++k)
+                if (hipMemcpyAsync(d_out + fr_idx[k], tmp.p + k, sizeof(RegionOut),
+                                   hipMemcpyDeviceToDevice, s) != hipSuccess)
+                    rc = MC_E_HIP;
+            if (hipStreamSynchronize(s) != hipSuccess) rc = MC_E_HIP;
+        }
+        tmp.release();
+        if (rc) return rc;
+    }
+    return MC_OK;
+}
+
+extern "C" int mc_compute_depth_stats(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                                      const int64_t* start, const int64_t* end,
+                                      mc_region_stat* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(R == 0 || out, MC_E_INVALID, "null out");
+    HIP_TRY(ctx->d_out.reserve(std::max<int64_t>(R, 1)));
+    if (int rc = depth_stats_impl(ctx, R, tid, start, end, ctx->d_out.p)) return rc;
+    if (R)
+        HIP_TRY(hipMemcpyAsync(out, ctx->d_out.p, R * sizeof(mc_region_stat), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MC_OK;
+}
+
+extern "C" int mc_compute_depth_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                                             const int64_t* start, const int64_t* end,
+                                             mc_region_stat* d_out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(R == 0 || d_out, MC_E_INVALID, "null out");
+    return depth_stats_impl(ctx, R, tid, start, end, reinterpret_cast<RegionOut*>(d_out));
+}
+
+extern "C" int mc_fused_fallbacks(mc_ctx* ctx, int64_t* out) {
+    MC_REQUIRE(ctx && out, MC_E_INVALID, "null argument");
+    *out = ctx->fused_fallbacks;
     return MC_OK;
 }
 

@@ -261,6 +261,88 @@ __device__ __forceinline__ void load_batch(ReadBatch& b, int64_t base, int64_t n
     }
 }
 
+// Fused region statistics of K2 (optional): non-overlapping regions sorted by
+// global start.  Each tile folds the positions it owns into the region(s)
+// covering them: min/max/sum/sum of squares per thread, value histogram of
+// the current region in LDS (kHistBins bins; larger values are counted in
+// `overflow` and resolved by the host's fallback to region_seg_kernel).
+constexpr int kHistBins = 1024;
+
+struct FusedRegions {
+    int64_t n;                         // 0 = no fused statistics
+    const int64_t* chunk_first;        // [n_chunks] first region ending after the chunk start
+    const int64_t* gs;                 // [n] global start (sorted)
+    const int64_t* ge;                 // [n] global end (clipped to the contig extent)
+    const int32_t* id;                 // [n] caller's row index
+    RegionAcc* acc;                    // [rows]
+    unsigned* hist;                    // [rows][kHistBins]
+    unsigned* overflow;                // [rows] values >= kHistBins
+};
+
+struct StatAcc {
+    int vmin, vmax;
+    long long sum;
+    unsigned long long sq;
+    __device__ void reset() {
+        vmin = 0x7fffffff;
+        vmax = 0;
+        sum = 0;
+        sq = 0;
+    }
+    __device__ void add(int v) {
+        vmin = min(vmin, v);
+        vmax = max(vmax, v);
+        sum += v;
+        sq += (unsigned long long)((long long)v * v);
+    }
+};
+
+__device__ __forceinline__ void emit_hist(const FusedRegions& R, int64_t r, unsigned* h,
+                                          StatAcc& a, int v, int cnt) {
+    if (v < kHistBins) {
+#ifdef MC_EXP_HIST_SPREAD   // experiment: same instruction count, no address conflicts
+        atomicAdd(&h[(v + (int)threadIdx.x) & (kHistBins - 1)], (unsigned)cnt);
+#else
+        atomicAdd(&h[v], (unsigned)cnt);
+#endif
+    } else {
+        atomicAdd(&R.overflow[R.id[r]], (unsigned)cnt);
+        a.vmin = min(a.vmin, v);
+        a.vmax = max(a.vmax, v);
+        a.sum += (long long)v * cnt;
+        a.sq += (unsigned long long)((long long)v * v) * (unsigned long long)cnt;
+    }
+}
+
+// Every thread calls it (it holds barriers); folds the block's partials for
+// region `r` into the global accumulators and flushes the LDS histogram.
+__device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, StatAcc& a,
+                                             unsigned* h, int lane) {
+    const int id = R.id[r];
+    int vmin = wave_min(a.vmin), vmax = wave_max(a.vmax);
+    long long sum = wave_sum64(a.sum);
+    unsigned long long sq = a.sq;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) sq += __shfl_xor(sq, d, 64);
+    if (lane == 0 && vmin <= vmax) {
+        atomicMin(&R.acc[id].min, vmin);
+        atomicMax(&R.acc[id].max, vmax);
+        atomicAdd(&R.acc[id].sum, (unsigned long long)sum);
+        atomicAdd(&R.acc[id].sumsq, sq);
+    }
+    a.reset();
+    __syncthreads();
+    unsigned* g = R.hist + (int64_t)id * kHistBins;
+    for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
+        const unsigned cnt = h[k];
+        if (cnt) {
+            atomicAdd(&g[k], cnt);
+            h[k] = 0;
+        }
+    }
+    __syncthreads();
+}
+
 // One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
 // (dynamic queue).  Per chunk: the reads from chunk_first[c] (which already
 // includes the max-span halo) are applied as +1 at max(start, chunk start)
@@ -269,6 +351,8 @@ __device__ __forceinline__ void load_batch(ReadBatch& b, int64_t base, int64_t n
 // with 1 KiB-per-wave-instruction stores, and its ring slots are zeroed.
 // Reads longer than short_max = ring - kTileW take the long-read path (see
 // long_count_kernel); the halo of chunk_first is min(max_span, short_max).
+// kStats: fold the tile into FusedRegions before it leaves the registers.
+template <bool kStats>
 __global__ void __launch_bounds__(kBlock)
 depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              const int32_t* __restrict__ span, int64_t n,
@@ -277,10 +361,11 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
              const int* __restrict__ chunk_carry,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
-             int* __restrict__ max_depth) {
+             int* __restrict__ max_depth, FusedRegions R) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    int* hdr = lds;                       // [0] chunk id, [4..7] wave totals
+    int* hdr = lds;                       // [0] chunk id, [1] region cursor, [4..7] wave totals
     int* ring = lds + kLdsHeader;
+    unsigned* hist = reinterpret_cast<unsigned*>(ring + ring_mask + 1);   // kStats only
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int ring_n = ring_mask + 1;
@@ -288,6 +373,11 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
     int my_max = 0;
+    StatAcc sa;
+    sa.reset();
+    if (kStats) {
+        for (int k = threadIdx.x; k < kHistBins; k += kBlock) hist[k] = 0;
+    }
 
     for (;;) {
         if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
@@ -298,6 +388,14 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         const int64_t c = hdr[0];
         if (c >= n_chunks) break;
         const int64_t C0 = c * chunk_w;
+        int64_t rcur = 0, r_gs = 0, r_ge = 0;
+        if (kStats) {
+            rcur = R.chunk_first[c];
+            if (rcur < R.n) {
+                r_gs = R.gs[rcur];
+                r_ge = R.ge[rcur];
+            }
+        }
         int64_t base = chunk_first[c] & ~(int64_t)(kReadsPerThread - 1);
         bool more = base < n;
         ReadBatch b;
@@ -372,9 +470,56 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 #pragma unroll
             for (int j = 0; j < kChunks; ++j) {
                 i32x4 x = v[j] + off;
+                v[j] = x;
                 my_max = max(my_max, max(max(x.x, x.y), max(x.z, x.w)));
                 __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
             }
+            if (kStats) {
+                // regions covering this tile, in order; the loop is uniform.
+                // Only the value histogram is built here (runs of equal values
+                // within a lane share one LDS atomic); min/max/sum/sumsq follow
+                // from it in region_final_kernel.  Values >= kHistBins go to
+                // the per-region overflow count + the thread's StatAcc.
+                while (rcur < R.n && r_gs < Tend) {
+                    const int64_t rgs = r_gs, rge = r_ge;
+                    const int lo = (int)((rgs > T0 ? rgs : T0) - T0);
+                    const int hi = (int)((rge < Tend ? rge : Tend) - T0);
+                    const bool full = lo == 0 && hi == kTileW;
+#pragma unroll
+                    for (int j = 0; j < kChunks; ++j) {
+                        const int q0 = wave * kWaveSpan + j * 256 + lane * 4;
+                        const int xs[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+                        int run_v = xs[0], run_n = 0;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const bool in = full || (q0 + k >= lo && q0 + k < hi);
+                            const int x = xs[k];
+                            if (in && x == run_v) {
+                                ++run_n;
+                            } else if (in) {
+                                if (run_n) emit_hist(R, rcur, hist, sa, run_v, run_n);
+                                run_v = x;
+                                run_n = 1;
+                            }
+                        }
+                        if (run_n) emit_hist(R, rcur, hist, sa, run_v, run_n);
+                    }
+                    if (rge <= Tend) {
+                        flush_region(R, rcur, sa, hist, lane);
+                        ++rcur;
+                        if (rcur < R.n) {
+                            r_gs = R.gs[rcur];
+                            r_ge = R.ge[rcur];
+                        }
+                    } else {
+                        break;
+                    }
+                }
+            }
+        }
+        if (kStats) {
+            // a region still open at the chunk end has partials here
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, sa, hist, lane);
         }
         __syncthreads();   // hdr[0] / ring reuse by the next chunk
     }
@@ -461,21 +606,38 @@ struct RegionOut {                     // mirrors mc_region_stat
 
 // One workgroup per region: block scan over the value histogram for the
 // ranks (n-1)/2, n/2 and the trimmed range [n/4, n - n/4) (pileup.py:21,24).
+// hist_stats: the fused K2 built only the histogram (values < nbins) plus the
+// overflow StatAcc in `acc` — min/max/sum/sumsq are then folded from both.
+// fallback (fused path): flags regions whose needed ranks fall into the
+// values >= nbins, which the host recomputes with the full-range K3.
 __global__ void __launch_bounds__(kBlock)
 region_final_kernel(const unsigned* __restrict__ hist, int nbins,
                     const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
-                    const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out) {
+                    const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
+                    int* __restrict__ fallback, int hist_stats) {
     __shared__ long long s_part[kBlock];
+    __shared__ long long s_red[4][kWaves];
     __shared__ long long s_med[2];
     const int r = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned* hr = hist + (int64_t)r * nbins;
     const long long n = n_total[r];
     const long long zx = n_zero_extra[r];
     const int per = (nbins + kBlock - 1) / kBlock;
     const int b0 = threadIdx.x * per;
     const int b1 = min(nbins, b0 + per);
-    long long local = 0;
-    for (int b = b0; b < b1; ++b) local += hr[b] + (b == 0 ? zx : 0);
+    long long local = 0, s1 = 0;
+    unsigned long long s2 = 0;
+    int lmin = 0x7fffffff, lmax = -1;
+    for (int b = b0; b < b1; ++b) {
+        const long long cnt = (long long)hr[b] + (b == 0 ? zx : 0);
+        if (!cnt) continue;
+        local += cnt;
+        s1 += cnt * b;
+        s2 += (unsigned long long)cnt * (unsigned long long)((long long)b * b);
+        lmin = min(lmin, b);
+        lmax = max(lmax, b);
+    }
     s_part[threadIdx.x] = local;
     if (threadIdx.x < 2) s_med[threadIdx.x] = 0;
     __syncthreads();
@@ -487,6 +649,7 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
         __syncthreads();
     }
     long long cum = s_part[threadIdx.x] - local;
+    const long long in_hist = s_part[kBlock - 1];   // values < nbins, zeros included
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;
     const long long q_lo = n / 4, q_hi = n - n / 4;
     long long qsum = 0;
@@ -502,26 +665,55 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
         cum = e;
     }
     qsum = wave_sum64(qsum);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = qsum;
+    s1 = wave_sum64(s1);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) s2 += __shfl_xor(s2, d, 64);
+    lmin = wave_min(lmin);
+    lmax = wave_max(lmax);
+    if (lane == 0) {
+        s_red[0][wave] = qsum;
+        s_red[1][wave] = s1;
+        s_red[2][wave] = (long long)s2;
+        s_red[3][wave] = ((long long)lmin << 32) | (unsigned)(lmax + 1);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        long long q = 0;
-        for (int w = 0; w < kWaves; ++w) q += s_part[w];
+        if (fallback) fallback[r] = (n > 0 && (q_hi - 1 >= in_hist || r_hi >= in_hist)) ? 1 : 0;
+        long long q = 0, t1 = 0;
+        unsigned long long t2 = 0;
+        int hmin = 0x7fffffff, hmax = -1;
+        for (int w = 0; w < kWaves; ++w) {
+            q += s_red[0][w];
+            t1 += s_red[1][w];
+            t2 += (unsigned long long)s_red[2][w];
+            hmin = min(hmin, (int)(s_red[3][w] >> 32));
+            hmax = max(hmax, (int)(s_red[3][w] & 0xffffffff) - 1);
+        }
+        const RegionAcc a = acc[r];
         RegionOut o;
         o.n = n;
-        o.sum = (long long)acc[r].sum;
-        o.sumsq = acc[r].sumsq;
-        const bool any_read = n - zx > 0;
-        o.min = any_read ? acc[r].min : 0;
-        if (zx > 0 && o.min > 0) o.min = 0;
-        o.max = any_read ? acc[r].max : 0;
+        if (hist_stats) {
+            // histogram part + overflow part (a.min == INT_MAX when empty)
+            o.sum = t1 + (long long)a.sum;
+            o.sumsq = t2 + a.sumsq;
+            o.min = in_hist > 0 ? hmin : a.min;
+            o.max = a.max > hmax ? a.max : hmax;
+        } else {
+            o.sum = (long long)a.sum;
+            o.sumsq = a.sumsq;
+            const bool any_read = n - zx > 0;
+            o.min = any_read ? a.min : 0;
+            if (zx > 0 && o.min > 0) o.min = 0;
+            o.max = any_read ? a.max : 0;
+        }
         o.med_lo = s_med[0];
         o.med_hi = s_med[1];
         o.q23_sum = q;
         o.q23_cnt = q_hi - q_lo;
         if (n == 0) {
             o.min = o.max = o.med_lo = o.med_hi = o.q23_sum = o.q23_cnt = 0;
+            o.sum = 0;
+            o.sumsq = 0;
         }
         out[r] = o;
     }

@@ -178,6 +178,29 @@ class CoverageEngine:
         check(self._lib.mc_region_stats_device(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
                                                ctypes.c_void_p(d_out_ptr)))
 
+    def compute_depth_stats(self, tids, starts, ends):
+        """K2 with the region statistics fused in (non-overlapping regions),
+        else K2 + K3.  Returns the exact rows like region_stats()."""
+        tids = np.ascontiguousarray(tids, dtype=np.int32)
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        out = np.zeros(len(tids), dtype=REGION_STAT_DTYPE)
+        check(self._lib.mc_compute_depth_stats(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+                                               ptr(out)))
+        return out
+
+    def compute_depth_stats_device(self, tids, starts, ends, d_out_ptr):
+        tids = np.ascontiguousarray(tids, dtype=np.int32)
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        check(self._lib.mc_compute_depth_stats_device(self._h, len(tids), ptr(tids), ptr(starts),
+                                                      ptr(ends), ctypes.c_void_p(d_out_ptr)))
+
+    def fused_fallbacks(self):
+        v = ctypes.c_int64()
+        check(self._lib.mc_fused_fallbacks(self._h, ctypes.byref(v)))
+        return v.value
+
     def aligned_bases(self):
         v = ctypes.c_int64()
         check(self._lib.mc_aligned_bases(self._h, ctypes.byref(v)))

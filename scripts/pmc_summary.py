@@ -56,9 +56,10 @@ def main():
                    "hbm_GBps": hbm / avg_ns if avg_ns else None}
     with open(os.path.join(prof, "%s_pmc.json" % a.tag), "w") as fh:
         json.dump(rows, fh, indent=1)
-    dk = rows["mc::depth_kernel"]
+    dk_name = next(k for k in rows if "depth_kernel" in k)
+    dk = rows[dk_name]
     with open(os.path.join(prof, "pmc_depth_kernel.json"), "w") as fh:
-        json.dump({"tag": a.tag, "reads": a.reads, "contigs": a.contigs,
+        json.dump({"tag": a.tag, "kernel": dk_name, "reads": a.reads, "contigs": a.contigs,
                    "hbm_bytes_per_launch": dk["hbm_bytes_per_launch"],
                    "fetch_kib": dk["FETCH_SIZE_KiB"], "write_kib": dk["WRITE_SIZE_KiB"],
                    "avg_ns": dk["avg_ns"],

@@ -314,3 +314,74 @@ def test_long_read_ends_on_chunk_and_tile_starts(eng):
     tid = np.zeros(4, np.int32)
     run_engine(eng, lengths, tid, pos[o], span[o])
     check_depth_vs_oracle(eng, lengths, tid, pos[o], span[o])
+
+
+# ------------------------------------------------------------- fused K2 + stats
+
+def _tiling(rng, lengths, pieces):
+    rt, rs, re_ = [], [], []
+    for t, L in enumerate(lengths):
+        cuts = np.sort(rng.integers(0, L + 1, size=pieces))
+        edges = np.concatenate([[0], cuts, [L + 37]])
+        for a, b in zip(edges[:-1], edges[1:]):
+            rt.append(t)
+            rs.append(a)
+            re_.append(b)
+    o = rng.permutation(len(rt))      # any input order
+    return (np.array(rt, np.int32)[o], np.array(rs, np.int64)[o], np.array(re_, np.int64)[o])
+
+
+@pytest.mark.parametrize("name", ["one_contig", "many_contigs", "mixed_long", "chunk_edges",
+                                  "tiny_contigs"])
+def test_fused_stats_vs_oracle(eng, name):
+    lengths, tid, pos, span = make_case(*CASES[name])
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    rng = np.random.default_rng(31)
+    for rt, rs, re_ in [(np.arange(len(lengths), dtype=np.int32), np.zeros(len(lengths), np.int64),
+                         np.asarray(lengths, np.int64)),
+                        _tiling(rng, lengths, 7)]:
+        eng.set_contigs(lengths)
+        eng.add_reads(tid, pos, span)
+        got = eng.compute_depth_stats(rt, rs, re_)
+        want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+        for t in range(len(lengths)):
+            assert np.array_equal(eng.depth(t, 0, int(ext[t])), d[coff[t]:coff[t] + ext[t]])
+
+
+def test_fused_overlapping_and_high_depth(eng):
+    # overlapping regions -> K2 + K3 path; depth > 1024 -> exact fallback
+    n = 3000
+    tid = np.zeros(n, np.int32)
+    pos = np.sort(np.random.default_rng(3).integers(0, 40, size=n)).astype(np.int32)
+    span = np.full(n, 100, np.int32)
+    lengths = [5000]
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    cases = [
+        (np.array([0, 0], np.int32), np.array([0, 10], np.int64), np.array([200, 300], np.int64)),
+        (np.array([0], np.int32), np.array([0], np.int64), np.array([120], np.int64)),
+        (np.array([0, 0], np.int32), np.array([0, 4000], np.int64), np.array([4000, 5000], np.int64)),
+    ]
+    for k, (rt, rs, re_) in enumerate(cases):
+        eng.set_contigs(lengths)
+        eng.add_reads(tid, pos, span)
+        got = eng.compute_depth_stats(rt, rs, re_)
+        want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+        if k == 1:
+            assert eng.fused_fallbacks() == 1      # median of [0,120) is > 1024
+        if k == 2:
+            assert eng.fused_fallbacks() == 0
+
+
+def test_fused_fixture_goldens(eng, fixture_golden):
+    tid, pos, span = _iv(fixture_golden)
+    regs = fixture_golden["whole"]
+    eng.set_contigs(fixture_golden["lengths"])
+    eng.add_reads(tid, pos, span)
+    rows = eng.compute_depth_stats([fixture_golden["names"].index(r["sacc"]) for r in regs],
+                                   [r["start"] for r in regs], [r["end"] for r in regs])
+    for row, r in zip(rows, regs):
+        assert classic_stats(row) == r["stats"]
