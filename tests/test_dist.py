@@ -1,0 +1,89 @@
+"""Contig sharding and the region-table exchange (CPU, gloo, world size 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from metacov_amd import dist as mdist
+from metacov_amd.engine import REGION_STAT_DTYPE
+
+
+def test_lpt_balances_and_partitions():
+    rng = np.random.default_rng(0)
+    costs = rng.lognormal(0, 1, size=1000) * 1e6
+    for world in (1, 2, 3, 8):
+        shards = mdist.lpt_shard(costs, world)
+        allc = np.sort(np.concatenate(shards))
+        assert np.array_equal(allc, np.arange(1000))
+        loads = [costs[s].sum() for s in shards]
+        # LPT bound: max load <= 4/3 OPT (+ one item); check against the mean
+        assert max(loads) <= costs.sum() / world + costs.max() + 1e-6
+
+
+def test_select_reads_remap():
+    tid = np.array([0, 0, 1, 2, 2, 3], np.int32)
+    mask, remap = mdist.select_reads(tid, np.array([1, 3]))
+    assert mask.tolist() == [False, False, True, False, False, True]
+    assert remap[tid[mask]].tolist() == [0, 1]
+
+
+def _rows(n, seed):
+    rng = np.random.default_rng(seed)
+    r = np.zeros(n, REGION_STAT_DTYPE)
+    for f in REGION_STAT_DTYPE.names:
+        r[f] = rng.integers(0, 1 << 40, size=n)
+    r["sumsq"][0] = np.uint64(1 << 63) + np.uint64(5)    # survives the int64 view
+    return r
+
+
+def test_pack_unpack_roundtrip():
+    rows = _rows(7, 1)
+    idx = np.array([6, 0, 5, 1, 4, 2, 3])
+    t = mdist.pack_rows(rows, idx)
+    pad = np.full((3, mdist.ROW_WIDTH), -1, np.int64)
+    back = mdist.unpack_rows(np.concatenate([t, pad]), 7, REGION_STAT_DTYPE)
+    for f in REGION_STAT_DTYPE.names:
+        assert np.array_equal(back[f][idx], rows[f])
+    with pytest.raises(RuntimeError):
+        mdist.unpack_rows(t[:5], 7, REGION_STAT_DTYPE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_regions, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # each rank owns an LPT shard of the "contigs" (= regions here)
+        costs = np.arange(1, n_regions + 1, dtype=np.float64)
+        owned = mdist.lpt_shard(costs, world)[rank]
+        all_rows = _rows(n_regions, 9)
+        table = mdist.pack_rows(all_rows[owned], owned)
+        out = mdist.all_gather_table(table, r_max=n_regions)
+        rows = mdist.unpack_rows(out, n_regions, REGION_STAT_DTYPE)
+        ok = all(np.array_equal(rows[f], all_rows[f]) for f in REGION_STAT_DTYPE.names)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_all_gather_world2():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, 11, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True)]
