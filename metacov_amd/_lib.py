@@ -90,29 +90,38 @@ SIGNATURES = {
 _RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p}
 
 _lib = None
+_variants = {}
 
 
-def load():
-    """Loads the library once; raises LibraryNotBuilt if it is absent."""
+def load(path=None):
+    """Loads the library once; raises LibraryNotBuilt if it is absent.
+    `path` loads another build of the same ABI side by side (A/B runs)."""
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+    if path is not None and path != LIB_PATH:
+        if path not in _variants:
+            _variants[path] = _open(path)
+        return _variants[path]
+    if _lib is None:
+        _lib = _open(LIB_PATH)
+    return _lib
+
+
+def _open(path):
+    if not os.path.exists(path):
         raise LibraryNotBuilt(
             "%s not found: build it with `python -m metacov_amd.build` "
-            "(hipcc --offload-arch=gfx950). metacov_amd has no CPU fallback." % LIB_PATH)
-    lib = ctypes.CDLL(LIB_PATH)
+            "(hipcc --offload-arch=gfx950). metacov_amd has no CPU fallback." % path)
+    lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = _RESTYPE.get(name, ctypes.c_int)
-    _lib = lib
     return lib
 
 
-def check(rc):
+def check(rc, lib=None):
     if rc != MC_OK:
-        msg = load().mc_last_error()
+        msg = (lib or load()).mc_last_error()
         raise MetacovError(rc, msg.decode() if msg else "error")
     return rc
 

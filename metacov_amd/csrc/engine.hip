@@ -349,6 +349,9 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         ctx->spans_pending = false;
     }
     HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    // K2 loads whole int4 batches past n: the tid padding must index coff
+    if (ctx->d_tid.cap > (size_t)n)
+        HIP_TRY(hipMemsetAsync(ctx->d_tid.p + n, 0, (ctx->d_tid.cap - n) * 4, s));
     // ---- ingest: validation, aligned bases, max span, overhanging ends
     HIP_TRY(ctx->d_maxend.reserve(std::max<int32_t>(nc, 1)));
     HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
@@ -385,9 +388,9 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     ctx->total_len = off;
     // LDS ring of 2 tiles: reads up to short_max = ring - kTileW keep both
     // events in LDS; longer ones take the bucketed long-read path.
-    ctx->ring = 2 * kTileW;
+    ctx->ring = kRingTiles * kTileW;
     ctx->short_max = ctx->ring - kTileW;
-    ctx->tiles_per_chunk = 16;
+    ctx->tiles_per_chunk = kTilesPerChunk;
     ctx->chunk_w = (int64_t)ctx->tiles_per_chunk * kTileW;
     ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
     const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;

@@ -18,9 +18,37 @@
 
 namespace mc {
 
+// Tuning knobs (compile-time; scripts/ab_inproc.py A/Bs builds of them).
+#ifndef MC_TILE_W
+#define MC_TILE_W 4096                 // positions per tile (multiple of 1024)
+#endif
+#ifndef MC_RING_TILES
+#define MC_RING_TILES 2                // LDS ring = tiles (power of two)
+#endif
+#ifndef MC_TILES_PER_CHUNK
+#define MC_TILES_PER_CHUNK 8
+#endif
+#ifndef MC_PREFETCH
+#define MC_PREFETCH 1                  // load read batch k+1 while applying batch k
+#endif
+#ifndef MC_PREFETCH_STATS
+#define MC_PREFETCH_STATS 0            // the same for the fused-statistics K2
+#endif
+#ifndef MC_CHUNK_PF
+#define MC_CHUNK_PF 0                  // dequeue the next chunk during the current one
+#endif
+#ifndef MC_WAVES_PLAIN
+#define MC_WAVES_PLAIN 0               // __launch_bounds__ waves/SIMD, plain K2 (0 = none)
+#endif
+#ifndef MC_WAVES_STATS
+#define MC_WAVES_STATS 4               // __launch_bounds__ waves/SIMD, fused K2 (<= 128 VGPRs)
+#endif
+
 constexpr int kBlock = 256;            // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
-constexpr int kTileW = 4096;           // positions per tile
+constexpr int kTileW = MC_TILE_W;
+constexpr int kRingTiles = MC_RING_TILES;
+constexpr int kTilesPerChunk = MC_TILES_PER_CHUNK;
 constexpr int kReadsPerThread = 4;     // int4 loads of tid/pos/span
 constexpr int kBatch = kBlock * kReadsPerThread;
 constexpr int kLdsHeader = 16;         // ints reserved in front of the ring
@@ -229,36 +257,50 @@ cigar_span_kernel(const int64_t* __restrict__ cig_off, const uint32_t* __restric
 
 // ----------------------------------------------------------------- K2
 
-struct ReadBatch {
-    int64_t gs[kReadsPerThread];
-    int64_t ge[kReadsPerThread];
+struct ReadBatch {                     // 4 reads in chunk-relative coordinates
+    int rs[kReadsPerThread];           // start - chunk start, clamped to +-2^30
+    int sp[kReadsPerThread];           // span
     unsigned pending;                  // bit k: read k still to apply
 };
 
-__device__ __forceinline__ void load_batch(ReadBatch& b, int64_t base, int64_t n,
-                                           const int32_t* __restrict__ tid,
-                                           const int32_t* __restrict__ pos,
-                                           const int32_t* __restrict__ span,
-                                           const int64_t* __restrict__ coff) {
+struct RawBatch {                      // one batch of reads as loaded (int4 per array)
+    i32x4 t, p, s;
+};
+
+// Issue the three 16-byte loads of this thread's 4 reads.  The arrays are
+// padded by one batch past n (tid padding zero-filled), so no bounds check.
+__device__ __forceinline__ void issue_raw(RawBatch& r, int64_t base,
+                                          const int32_t* __restrict__ tid,
+                                          const int32_t* __restrict__ pos,
+                                          const int32_t* __restrict__ span) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-    // arrays are padded to a multiple of kBatch past n: loads stay in bounds
-    const i32x4 t4 = *reinterpret_cast<const i32x4*>(tid + i0);
-    const i32x4 p4 = *reinterpret_cast<const i32x4*>(pos + i0);
-    const i32x4 s4 = *reinterpret_cast<const i32x4*>(span + i0);
-    const int tt[4] = {t4.x, t4.y, t4.z, t4.w};
-    const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
-    const int ss[4] = {s4.x, s4.y, s4.z, s4.w};
-    b.pending = 0;
+    r.t = *reinterpret_cast<const i32x4*>(tid + i0);
+    r.p = *reinterpret_cast<const i32x4*>(pos + i0);
+    r.s = *reinterpret_cast<const i32x4*>(span + i0);
+}
+
+// Chunk-relative start of the 4 reads: 4 independent coff lookups (small
+// table, cache-resident); reads past n are masked.  Starts far outside the
+// chunk are clamped (they are never applied: a read is applied only while
+// its start lies before the current tile end).
+__device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, int64_t base,
+                                             int64_t n, int64_t C0,
+                                             const int64_t* __restrict__ coff) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
+    const int64_t g[4] = {coff[r.t.x] + r.p.x, coff[r.t.y] + r.p.y, coff[r.t.z] + r.p.z,
+                          coff[r.t.w] + r.p.w};
+    constexpr int64_t kClamp = int64_t(1) << 30;
 #pragma unroll
-    for (int k = 0; k < kReadsPerThread; ++k) {
-        if (i0 + k < n) {
-            b.gs[k] = coff[tt[k]] + pp[k];
-            b.ge[k] = b.gs[k] + ss[k];
-            b.pending |= 1u << k;
-        } else {
-            b.gs[k] = b.ge[k] = 0;
-        }
+    for (int k = 0; k < 4; ++k) {
+        const int64_t rel = g[k] - C0;
+        b.rs[k] = (int)(rel < -kClamp ? -kClamp : rel > kClamp ? kClamp : rel);
     }
+    b.sp[0] = r.s.x;
+    b.sp[1] = r.s.y;
+    b.sp[2] = r.s.z;
+    b.sp[3] = r.s.w;
+    const int64_t left = n - i0;
+    b.pending = left >= 4 ? 0xfu : left <= 0 ? 0u : ((1u << left) - 1u);
 }
 
 // Fused region statistics of K2 (optional): non-overlapping regions sorted by
@@ -353,7 +395,9 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, S
 // long_count_kernel); the halo of chunk_first is min(max_span, short_max).
 // kStats: fold the tile into FusedRegions before it leaves the registers.
 template <bool kStats>
-__global__ void __launch_bounds__(kBlock)
+// waves/SIMD minimum per variant (0 = unconstrained -> 1)
+__global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
+                                                 : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
 depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              const int32_t* __restrict__ span, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
@@ -372,6 +416,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
+    constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
     StatAcc sa;
     sa.reset();
@@ -379,14 +424,24 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         for (int k = threadIdx.x; k < kHistBins; k += kBlock) hist[k] = 0;
     }
 
+    // chunk ids come from an atomic queue; thread 0 fetches the next id (and
+    // its chunk_first) while the current chunk is processed
+    unsigned next_c = 0;
+    int64_t next_first = 0;
+    if (threadIdx.x == 0) {
+        const unsigned c0 = atomicAdd(queue, 1u);
+        hdr[0] = (int)c0;
+        if (c0 < n_chunks) *reinterpret_cast<long long*>(hdr + 2) = chunk_first[c0];
+    }
     for (;;) {
-        if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
-        // zero the ring (also orders the hdr[0] write before the reads)
+        // zero the ring (also orders the hdr writes before the reads)
         for (int k = threadIdx.x * 4; k < ring_n; k += kBlock * 4)
             *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
         __syncthreads();
         const int64_t c = hdr[0];
         if (c >= n_chunks) break;
+        const int64_t cfirst = *reinterpret_cast<const long long*>(hdr + 2);
+        if (MC_CHUNK_PF && threadIdx.x == 0) next_c = atomicAdd(queue, 1u);
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
         if (kStats) {
@@ -396,11 +451,17 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 r_ge = R.ge[rcur];
             }
         }
-        int64_t base = chunk_first[c] & ~(int64_t)(kReadsPerThread - 1);
+        int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
         bool more = base < n;
         ReadBatch b;
-        if (more) load_batch(b, base, n, tid, pos, span, coff);
-        else b.pending = 0;
+        RawBatch nxt;
+        b.pending = 0;
+        if (more) {
+            RawBatch r0;
+            issue_raw(r0, base, tid, pos, span);
+            if (kPf && base + kBatch < n) issue_raw(nxt, base + kBatch, tid, pos, span);
+            finish_batch(b, r0, base, n, C0, coff);
+        }
         const bool has_long = tile_ev_off != nullptr;
         int carry = has_long ? chunk_carry[c] : 0;
         for (int t = 0; t < tiles_per_chunk; ++t) {
@@ -412,23 +473,23 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 for (int64_t k = e0 + threadIdx.x; k < e1; k += kBlock)
                     atomicAdd(&ring[(int)((T0 + tile_ev[k]) & ring_mask)], -1);
             }
+            const int tend_rel = (t + 1) * kTileW;   // C0 is a multiple of the ring size
             for (;;) {
 #pragma unroll
                 for (int k = 0; k < kReadsPerThread; ++k) {
-                    if ((b.pending >> k) & 1u) {
-                        if (b.gs[k] < Tend) {
-                            const int64_t e = b.ge[k];
-                            if (e - b.gs[k] <= short_max) {
-                                const int64_t s = b.gs[k] > C0 ? b.gs[k] : C0;
-                                if (e > s) {
-                                    atomicAdd(&ring[(int)(s & ring_mask)], 1);
-                                    atomicAdd(&ring[(int)(e & ring_mask)], -1);
-                                }
-                            } else if (b.gs[k] >= C0) {   // long read: +1 here, -1 bucketed
-                                atomicAdd(&ring[(int)(b.gs[k] & ring_mask)], 1);
+                    if (((b.pending >> k) & 1u) && b.rs[k] < tend_rel) {
+                        const int rs = b.rs[k], sp = b.sp[k];
+                        if (sp <= short_max) {
+                            const int s = rs > 0 ? rs : 0;
+                            const int e = rs + sp;
+                            if (e > s) {
+                                atomicAdd(&ring[s & ring_mask], 1);
+                                atomicAdd(&ring[e & ring_mask], -1);
                             }
-                            b.pending &= ~(1u << k);
+                        } else if (rs >= 0) {   // long read: +1 here, -1 bucketed
+                            atomicAdd(&ring[rs & ring_mask], 1);
                         }
+                        b.pending &= ~(1u << k);
                     }
                 }
                 const int all_done = __syncthreads_and(b.pending == 0);
@@ -436,8 +497,12 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 base += kBatch;
                 more = base < n;
                 if (!more) break;
-                load_batch(b, base, n, tid, pos, span, coff);
+                if (!kPf) issue_raw(nxt, base, tid, pos, span);
+                finish_batch(b, nxt, base, n, C0, coff);      // loaded one batch ago
+                if (kPf && base + kBatch < n) issue_raw(nxt, base + kBatch, tid, pos, span);
             }
+            if (MC_CHUNK_PF && t == 0 && threadIdx.x == 0 && next_c < n_chunks)
+                next_first = chunk_first[next_c];             // prefetch for the next chunk
             // ---- scan tile t: each wave owns kWaveSpan contiguous positions
             const int sb = (int)(T0 & ring_mask) + wave * kWaveSpan;
             i32x4 v[kChunks];
@@ -521,7 +586,15 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             // a region still open at the chunk end has partials here
             if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, sa, hist, lane);
         }
-        __syncthreads();   // hdr[0] / ring reuse by the next chunk
+        __syncthreads();   // everyone is past hdr / ring of this chunk
+        if (threadIdx.x == 0) {
+            if (!MC_CHUNK_PF) {
+                next_c = atomicAdd(queue, 1u);
+                if (next_c < n_chunks) next_first = chunk_first[next_c];
+            }
+            hdr[0] = (int)next_c;
+            *reinterpret_cast<long long*>(hdr + 2) = next_first;
+        }
     }
     my_max = wave_max(my_max);
     if (lane == 0 && my_max > 0) atomicMax(max_depth, my_max);

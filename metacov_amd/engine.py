@@ -74,10 +74,11 @@ def _is_torch(x):
 class CoverageEngine:
     """One mc_ctx on one GPU.  Not thread-safe (one engine per thread/GPU)."""
 
-    def __init__(self, device=0):
-        self._lib = _lib.load()
+    def __init__(self, device=0, lib_path=None):
+        self._lib = _lib.load(lib_path)
         h = ctypes.c_void_p()
-        check(self._lib.mc_ctx_create(int(device), ctypes.byref(h)))
+        check(self._lib.mc_ctx_create(int(device), ctypes.byref(h)), self._lib)
+        self._check = lambda rc: check(rc, self._lib)
         self._h = h
         self.device = int(device)
         self.lengths = np.zeros(0, dtype=np.int64)
@@ -101,12 +102,12 @@ class CoverageEngine:
         self.close()
 
     def set_stream(self, hip_stream_ptr):
-        check(self._lib.mc_ctx_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr or None)))
+        self._check(self._lib.mc_ctx_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr or None)))
 
     # -- inputs
     def set_contigs(self, lengths):
         lengths = np.ascontiguousarray(lengths, dtype=np.int64)
-        check(self._lib.mc_set_contigs(self._h, len(lengths), ptr(lengths)))
+        self._check(self._lib.mc_set_contigs(self._h, len(lengths), ptr(lengths)))
         self.lengths = lengths
 
     def add_reads(self, tid, pos, span):
@@ -119,13 +120,13 @@ class CoverageEngine:
             n = ts[0].numel()
             if not all(t.is_cuda and t.numel() == n for t in ts):
                 raise ValueError("tid/pos/span must be equally sized device tensors")
-            check(self._lib.mc_add_reads_device(self._h, n, *[ctypes.c_void_p(t.data_ptr()) for t in ts]))
+            self._check(self._lib.mc_add_reads_device(self._h, n, *[ctypes.c_void_p(t.data_ptr()) for t in ts]))
             return
         arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (tid, pos, span)]
         n = len(arrs[0])
         if not all(len(a) == n for a in arrs):
             raise ValueError("tid/pos/span lengths differ")
-        check(self._lib.mc_add_reads(self._h, n, *[ptr(a) for a in arrs]))
+        self._check(self._lib.mc_add_reads(self._h, n, *[ptr(a) for a in arrs]))
 
     def add_reads_cigar(self, tid, pos, cig_off, cigar):
         tid = np.ascontiguousarray(tid, dtype=np.int32)
@@ -134,32 +135,32 @@ class CoverageEngine:
         cigar = np.ascontiguousarray(cigar, dtype=np.uint32)
         if len(cig_off) != len(tid) + 1:
             raise ValueError("cig_off must have n + 1 entries")
-        check(self._lib.mc_add_reads_cigar(self._h, len(tid), ptr(tid), ptr(pos), ptr(cig_off),
+        self._check(self._lib.mc_add_reads_cigar(self._h, len(tid), ptr(tid), ptr(pos), ptr(cig_off),
                                            ptr(cigar)))
 
     def prepare(self):
-        check(self._lib.mc_prepare(self._h))
+        self._check(self._lib.mc_prepare(self._h))
 
     # -- compute
     def compute_depth(self):
-        check(self._lib.mc_compute_depth(self._h))
+        self._check(self._lib.mc_compute_depth(self._h))
 
     def depth(self, tid, start=0, end=None):
         if end is None:
             end = int(self.lengths[tid])
         out = np.empty(max(0, end - start), dtype=np.int32)
-        check(self._lib.mc_get_depth(self._h, int(tid), int(start), int(end), ptr(out)))
+        self._check(self._lib.mc_get_depth(self._h, int(tid), int(start), int(end), ptr(out)))
         return out
 
     def depth_device(self):
         p = ctypes.c_void_p()
         n = ctypes.c_int64()
-        check(self._lib.mc_depth_device(self._h, ctypes.byref(p), ctypes.byref(n)))
+        self._check(self._lib.mc_depth_device(self._h, ctypes.byref(p), ctypes.byref(n)))
         return p.value, n.value
 
     def contig_offset(self, tid):
         o, e = ctypes.c_int64(), ctypes.c_int64()
-        check(self._lib.mc_contig_offset(self._h, int(tid), ctypes.byref(o), ctypes.byref(e)))
+        self._check(self._lib.mc_contig_offset(self._h, int(tid), ctypes.byref(o), ctypes.byref(e)))
         return o.value, e.value
 
     def region_stats(self, tids, starts, ends):
@@ -167,7 +168,7 @@ class CoverageEngine:
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         ends = np.ascontiguousarray(ends, dtype=np.int64)
         out = np.zeros(len(tids), dtype=REGION_STAT_DTYPE)
-        check(self._lib.mc_region_stats(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+        self._check(self._lib.mc_region_stats(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
                                         ptr(out)))
         return out
 
@@ -175,7 +176,7 @@ class CoverageEngine:
         tids = np.ascontiguousarray(tids, dtype=np.int32)
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         ends = np.ascontiguousarray(ends, dtype=np.int64)
-        check(self._lib.mc_region_stats_device(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+        self._check(self._lib.mc_region_stats_device(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
                                                ctypes.c_void_p(d_out_ptr)))
 
     def compute_depth_stats(self, tids, starts, ends):
@@ -185,7 +186,7 @@ class CoverageEngine:
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         ends = np.ascontiguousarray(ends, dtype=np.int64)
         out = np.zeros(len(tids), dtype=REGION_STAT_DTYPE)
-        check(self._lib.mc_compute_depth_stats(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+        self._check(self._lib.mc_compute_depth_stats(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
                                                ptr(out)))
         return out
 
@@ -193,28 +194,28 @@ class CoverageEngine:
         tids = np.ascontiguousarray(tids, dtype=np.int32)
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         ends = np.ascontiguousarray(ends, dtype=np.int64)
-        check(self._lib.mc_compute_depth_stats_device(self._h, len(tids), ptr(tids), ptr(starts),
+        self._check(self._lib.mc_compute_depth_stats_device(self._h, len(tids), ptr(tids), ptr(starts),
                                                       ptr(ends), ctypes.c_void_p(d_out_ptr)))
 
     def fused_fallbacks(self):
         v = ctypes.c_int64()
-        check(self._lib.mc_fused_fallbacks(self._h, ctypes.byref(v)))
+        self._check(self._lib.mc_fused_fallbacks(self._h, ctypes.byref(v)))
         return v.value
 
     def aligned_bases(self):
         v = ctypes.c_int64()
-        check(self._lib.mc_aligned_bases(self._h, ctypes.byref(v)))
+        self._check(self._lib.mc_aligned_bases(self._h, ctypes.byref(v)))
         return v.value
 
     def max_depth(self):
         v = ctypes.c_int32()
-        check(self._lib.mc_max_depth(self._h, ctypes.byref(v)))
+        self._check(self._lib.mc_max_depth(self._h, ctypes.byref(v)))
         return v.value
 
     def timings(self):
         t = _lib.Timings()
-        check(self._lib.mc_get_timings(self._h, ctypes.byref(t)))
+        self._check(self._lib.mc_get_timings(self._h, ctypes.byref(t)))
         return {k: getattr(t, k) for k, _ in t._fields_}
 
     def synchronize(self):
-        check(self._lib.mc_synchronize(self._h))
+        self._check(self._lib.mc_synchronize(self._h))

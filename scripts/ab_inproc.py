@@ -1,0 +1,72 @@
+"""In-process A/B of library builds (same GPU, same data, interleaved rounds).
+
+    python scripts/ab_inproc.py --libs A.so B.so ... [--mode plain|fused]
+                                [--rounds 5 --steps 10 --reads 100000000]
+
+Each build gets its own mc_ctx over identical device-resident C3 reads; the
+builds run alternately, round after round (cdna_hip_programming.md rule 24),
+and their K2 times (HIP events) are reported as median / min.  Outputs are
+cross-checked: every build must produce the same region rows as the first.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--mode", default="plain", choices=["plain", "fused", "both"])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--reads", type=int, default=100_000_000)
+    a = ap.parse_args()
+    import torch
+    from bench import device_workload
+    from metacov_amd import synth
+    from metacov_amd.engine import CoverageEngine
+
+    dev = torch.device("cuda", 0)
+    lengths, weights = synth.c3_workload(a.reads, 1000)
+    tid, pos, span, _ = device_workload(torch, lengths, weights, a.reads, 1, dev)
+    R = len(lengths)
+    rt, rs, re_ = np.arange(R, dtype=np.int32), np.zeros(R, np.int64), lengths.astype(np.int64)
+    engines = []
+    for lib in a.libs:
+        e = CoverageEngine(0, lib_path=os.path.abspath(lib))
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span)
+        e.prepare()
+        engines.append(e)
+    modes = ["plain", "fused"] if a.mode == "both" else [a.mode]
+    for mode in modes:
+        times = {lib: [] for lib in a.libs}
+        ref_rows = None
+        for _ in range(a.rounds):
+            for lib, e in zip(a.libs, engines):
+                for _ in range(a.steps):
+                    if mode == "plain":
+                        e.compute_depth()
+                    else:
+                        rows = e.compute_depth_stats(rt, rs, re_)
+                    times[lib].append(e.timings()["depth_ms"])
+                if mode == "plain":
+                    rows = e.region_stats(rt, rs, re_)
+                if ref_rows is None:
+                    ref_rows = rows
+                else:
+                    for f in rows.dtype.names:
+                        assert np.array_equal(rows[f], ref_rows[f]), (lib, f)
+        for lib in a.libs:
+            t = np.array(times[lib])
+            print("%-6s %-48s K2 median %.4f ms  min %.4f ms  (n=%d)"
+                  % (mode, os.path.basename(lib), np.median(t), t.min(), len(t)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -8,7 +8,7 @@ bugs show up without a GPU.  Constants must match kernels.h.
 """
 import numpy as np
 from oracle import coracle
-W=4096; TPC=16; CW=W*TPC; RING=8192; SM=RING-W
+W=4096; TPC=8; CW=W*TPC; RING=8192; SM=RING-W
 def model(lengths, tid, pos, span):
     ext, coff64 = coracle.layout(lengths, tid, pos, span)
     coff=np.zeros(len(ext)+1,np.int64); 
