@@ -397,7 +397,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
     HIP_TRY(ctx->d_coff.reserve(nc + 1));
     HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx->d_chunk_first.reserve(ctx->n_chunks));
+    HIP_TRY(ctx->d_chunk_first.reserve(2 * ctx->n_chunks));
     HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
     const int64_t halo = std::min<int64_t>(ctx->max_span, ctx->short_max);
     if (n) {
@@ -407,7 +407,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
                            ctx->d_chunk_first.p);
         HIP_TRY(hipGetLastError());
     } else {
-        HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, ctx->n_chunks * 8, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * ctx->n_chunks * 8, s));
     }
     ctx->has_long = ctx->max_span > ctx->short_max;
     ctx->n_long_events = 0;
@@ -475,7 +475,8 @@ static int occupancy_grid(const void* kernel, size_t lds, int64_t work, int* gri
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins : 0)) * 4;
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins : 0)) * 4 +
+                       (stats ? sizeof(OverflowAcc) : 0);
     const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
     int grid = 0;
     if (int rc = occupancy_grid(kfn, lds, ctx->n_chunks, &grid)) return rc;
@@ -708,7 +709,6 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     HIP_TRY(ctx->d_fge.reserve(std::max<int64_t>(nf, 1)));
     HIP_TRY(ctx->d_fid.reserve(std::max<int64_t>(nf, 1)));
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
-    HIP_TRY(ctx->d_fover.reserve(R));
     HIP_TRY(ctx->d_fflag.reserve(R));
     HIP_TRY(ctx->d_acc.reserve(R));
     HIP_TRY(ctx->d_ntot.reserve(R));
@@ -721,12 +721,11 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     HIP_TRY(hipMemcpyAsync(ctx->d_ntot.p, ntot.data(), R * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->d_nzx.p, nzx.data(), R * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(ctx->d_fhist.p, 0, (size_t)(R * kHistBins) * 4, s));
-    HIP_TRY(hipMemsetAsync(ctx->d_fover.p, 0, R * 4, s));
     hipLaunchKernelGGL(region_init_kernel, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock),
                        0, s, ctx->d_acc.p, R);
     HIP_TRY(hipGetLastError());
     FusedRegions fr{nf, ctx->d_fchunk.p, ctx->d_fgs.p, ctx->d_fge.p, ctx->d_fid.p, ctx->d_acc.p,
-                    ctx->d_fhist.p, ctx->d_fover.p};
+                    ctx->d_fhist.p};
     if (nf == 0) fr.n = 0;
     if (int rc = launch_depth(ctx, fr)) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[6], s));

@@ -34,6 +34,9 @@ namespace mc {
 #ifndef MC_PREFETCH_STATS
 #define MC_PREFETCH_STATS 0            // the same for the fused-statistics K2
 #endif
+#ifndef MC_HIST_LDS
+#define MC_HIST_LDS 0                  // fused K2: histogram from LDS (16 positions/lane)
+#endif
 #ifndef MC_CHUNK_PF
 #define MC_CHUNK_PF 0                  // dequeue the next chunk during the current one
 #endif
@@ -138,21 +141,29 @@ __device__ __forceinline__ int64_t gstart_of(const int32_t* tid, const int32_t* 
     return coff[tid[i]] + pos[i];
 }
 
-// chunk_first[c] = first read index i with gstart(i) >= c * chunk_w - halo.
-__global__ void __launch_bounds__(kBlock)
-chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                   int64_t n, const int64_t* __restrict__ coff, int64_t chunk_w,
-                   int64_t halo, int64_t n_chunks, int64_t* __restrict__ chunk_first) {
-    const int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-    if (c >= n_chunks) return;
-    const int64_t target = c * chunk_w - halo;
+__device__ __forceinline__ int64_t lower_bound_gstart(const int32_t* tid, const int32_t* pos,
+                                                     const int64_t* coff, int64_t n,
+                                                     int64_t target) {
     int64_t lo = 0, hi = n;
     while (lo < hi) {
         const int64_t mid = lo + ((hi - lo) >> 1);
         if (gstart_of(tid, pos, coff, mid) < target) lo = mid + 1;
         else hi = mid;
     }
-    chunk_first[c] = lo;
+    return lo;
+}
+
+// chunk_index[2c]   = first read i with gstart(i) >= c * chunk_w - halo
+// chunk_index[2c+1] = first read i with gstart(i) >= (c + 1) * chunk_w
+// (the reads K2 has to load for chunk c: no batch is fetched past the end)
+__global__ void __launch_bounds__(kBlock)
+chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+                   int64_t n, const int64_t* __restrict__ coff, int64_t chunk_w,
+                   int64_t halo, int64_t n_chunks, int64_t* __restrict__ chunk_index) {
+    const int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (c >= n_chunks) return;
+    chunk_index[2 * c] = lower_bound_gstart(tid, pos, coff, n, c * chunk_w - halo);
+    chunk_index[2 * c + 1] = lower_bound_gstart(tid, pos, coff, n, (c + 1) * chunk_w);
 }
 
 // ------------------------------------------------------ long reads (prepare)
@@ -306,8 +317,9 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
 // Fused region statistics of K2 (optional): non-overlapping regions sorted by
 // global start.  Each tile folds the positions it owns into the region(s)
 // covering them: min/max/sum/sum of squares per thread, value histogram of
-// the current region in LDS (kHistBins bins; larger values are counted in
-// `overflow` and resolved by the host's fallback to region_seg_kernel).
+// the current region in LDS (kHistBins bins; larger values go to an LDS
+// overflow accumulator, and regions whose ranks reach them are recomputed by
+// the host with region_seg_kernel).
 constexpr int kHistBins = 1024;
 
 struct FusedRegions {
@@ -318,29 +330,25 @@ struct FusedRegions {
     const int32_t* id;                 // [n] caller's row index
     RegionAcc* acc;                    // [rows]
     unsigned* hist;                    // [rows][kHistBins]
-    unsigned* overflow;                // [rows] values >= kHistBins
 };
 
-struct StatAcc {
+// Statistics of the values >= kHistBins of the current region, in LDS
+// (rare; kept out of registers so the common path stays lean).
+struct OverflowAcc {
+    unsigned long long sum, sumsq;
     int vmin, vmax;
-    long long sum;
-    unsigned long long sq;
-    __device__ void reset() {
-        vmin = 0x7fffffff;
-        vmax = 0;
-        sum = 0;
-        sq = 0;
-    }
-    __device__ void add(int v) {
-        vmin = min(vmin, v);
-        vmax = max(vmax, v);
-        sum += v;
-        sq += (unsigned long long)((long long)v * v);
-    }
+    unsigned cnt, pad;
 };
 
-__device__ __forceinline__ void emit_hist(const FusedRegions& R, int64_t r, unsigned* h,
-                                          StatAcc& a, int v, int cnt) {
+__device__ __forceinline__ void emit_hist(unsigned* h, OverflowAcc* ov, int v, int cnt) {
+#ifdef MC_EXP_NO_HIST
+    asm volatile("" :: "v"(v), "v"(cnt));
+    return;
+#endif
+#ifdef MC_EXP_NO_OVF
+    atomicAdd(&h[v & (kHistBins - 1)], (unsigned)cnt);
+    return;
+#endif
     if (v < kHistBins) {
 #ifdef MC_EXP_HIST_SPREAD   // experiment: same instruction count, no address conflicts
         atomicAdd(&h[(v + (int)threadIdx.x) & (kHistBins - 1)], (unsigned)cnt);
@@ -348,41 +356,49 @@ __device__ __forceinline__ void emit_hist(const FusedRegions& R, int64_t r, unsi
         atomicAdd(&h[v], (unsigned)cnt);
 #endif
     } else {
-        atomicAdd(&R.overflow[R.id[r]], (unsigned)cnt);
-        a.vmin = min(a.vmin, v);
-        a.vmax = max(a.vmax, v);
-        a.sum += (long long)v * cnt;
-        a.sq += (unsigned long long)((long long)v * v) * (unsigned long long)cnt;
+        atomicAdd(&ov->cnt, (unsigned)cnt);
+        atomicAdd(&ov->sum, (unsigned long long)v * (unsigned long long)cnt);
+        atomicAdd(&ov->sumsq, (unsigned long long)((long long)v * v) * (unsigned long long)cnt);
+        atomicMin(&ov->vmin, v);
+        atomicMax(&ov->vmax, v);
     }
 }
 
-// Every thread calls it (it holds barriers); folds the block's partials for
-// region `r` into the global accumulators and flushes the LDS histogram.
-__device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, StatAcc& a,
-                                             unsigned* h, int lane) {
+__device__ __forceinline__ void reset_overflow(OverflowAcc* ov) {
+    ov->sum = 0;
+    ov->sumsq = 0;
+    ov->vmin = 0x7fffffff;
+    ov->vmax = 0;
+    ov->cnt = 0;
+}
+
+// Every thread calls it (it holds barriers): folds the overflow statistics
+// into the region's global accumulator and flushes the LDS histogram.
+__device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
+                                             OverflowAcc* ov) {
+#ifdef MC_EXP_NO_FLUSH
+    return;
+#endif
     const int id = R.id[r];
-    int vmin = wave_min(a.vmin), vmax = wave_max(a.vmax);
-    long long sum = wave_sum64(a.sum);
-    unsigned long long sq = a.sq;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) sq += __shfl_xor(sq, d, 64);
-    if (lane == 0 && vmin <= vmax) {
-        atomicMin(&R.acc[id].min, vmin);
-        atomicMax(&R.acc[id].max, vmax);
-        atomicAdd(&R.acc[id].sum, (unsigned long long)sum);
-        atomicAdd(&R.acc[id].sumsq, sq);
-    }
-    a.reset();
     __syncthreads();
+    if (threadIdx.x == 0 && ov->cnt) {
+        atomicMin(&R.acc[id].min, ov->vmin);
+        atomicMax(&R.acc[id].max, ov->vmax);
+        atomicAdd(&R.acc[id].sum, ov->sum);
+        atomicAdd(&R.acc[id].sumsq, ov->sumsq);
+    }
     unsigned* g = R.hist + (int64_t)id * kHistBins;
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
         const unsigned cnt = h[k];
         if (cnt) {
+#ifndef MC_EXP_NO_GATOMIC
             atomicAdd(&g[k], cnt);
+#endif
             h[k] = 0;
         }
     }
     __syncthreads();
+    if (threadIdx.x == 0) reset_overflow(ov);
 }
 
 // One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
@@ -410,6 +426,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     int* hdr = lds;                       // [0] chunk id, [1] region cursor, [4..7] wave totals
     int* ring = lds + kLdsHeader;
     unsigned* hist = reinterpret_cast<unsigned*>(ring + ring_mask + 1);   // kStats only
+    OverflowAcc* ovf = reinterpret_cast<OverflowAcc*>(hist + kHistBins);  // kStats only
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int ring_n = ring_mask + 1;
@@ -418,20 +435,22 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
-    StatAcc sa;
-    sa.reset();
     if (kStats) {
         for (int k = threadIdx.x; k < kHistBins; k += kBlock) hist[k] = 0;
+        if (threadIdx.x == 0) reset_overflow(ovf);
     }
 
     // chunk ids come from an atomic queue; thread 0 fetches the next id (and
     // its chunk_first) while the current chunk is processed
     unsigned next_c = 0;
-    int64_t next_first = 0;
+    int64_t next_first = 0, next_end = 0;
     if (threadIdx.x == 0) {
         const unsigned c0 = atomicAdd(queue, 1u);
         hdr[0] = (int)c0;
-        if (c0 < n_chunks) *reinterpret_cast<long long*>(hdr + 2) = chunk_first[c0];
+        if (c0 < n_chunks) {
+            *reinterpret_cast<long long*>(hdr + 2) = chunk_first[2 * c0];
+            *reinterpret_cast<long long*>(hdr + 8) = chunk_first[2 * c0 + 1];
+        }
     }
     for (;;) {
         // zero the ring (also orders the hdr writes before the reads)
@@ -441,6 +460,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         const int64_t c = hdr[0];
         if (c >= n_chunks) break;
         const int64_t cfirst = *reinterpret_cast<const long long*>(hdr + 2);
+        const int64_t cend = *reinterpret_cast<const long long*>(hdr + 8);   // reads of this chunk end
         if (MC_CHUNK_PF && threadIdx.x == 0) next_c = atomicAdd(queue, 1u);
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
@@ -452,14 +472,14 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             }
         }
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
-        bool more = base < n;
+        bool more = base < cend;
         ReadBatch b;
         RawBatch nxt;
         b.pending = 0;
         if (more) {
             RawBatch r0;
             issue_raw(r0, base, tid, pos, span);
-            if (kPf && base + kBatch < n) issue_raw(nxt, base + kBatch, tid, pos, span);
+            if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
             finish_batch(b, r0, base, n, C0, coff);
         }
         const bool has_long = tile_ev_off != nullptr;
@@ -495,14 +515,16 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 const int all_done = __syncthreads_and(b.pending == 0);
                 if (!all_done || !more) break;
                 base += kBatch;
-                more = base < n;
+                more = base < cend;
                 if (!more) break;
                 if (!kPf) issue_raw(nxt, base, tid, pos, span);
                 finish_batch(b, nxt, base, n, C0, coff);      // loaded one batch ago
-                if (kPf && base + kBatch < n) issue_raw(nxt, base + kBatch, tid, pos, span);
+                if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
             }
-            if (MC_CHUNK_PF && t == 0 && threadIdx.x == 0 && next_c < n_chunks)
-                next_first = chunk_first[next_c];             // prefetch for the next chunk
+            if (MC_CHUNK_PF && t == 0 && threadIdx.x == 0 && next_c < n_chunks) {
+                next_first = chunk_first[2 * next_c];         // prefetch for the next chunk
+                next_end = chunk_first[2 * next_c + 1];
+            }
             // ---- scan tile t: each wave owns kWaveSpan contiguous positions
             const int sb = (int)(T0 & ring_mask) + wave * kWaveSpan;
             i32x4 v[kChunks];
@@ -511,7 +533,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             for (int j = 0; j < kChunks; ++j) {
                 i32x4* slot = reinterpret_cast<i32x4*>(ring + sb + j * 256 + lane * 4);
                 i32x4 x = *slot;
-                *slot = i32x4{0, 0, 0, 0};
+                if (!(kStats && MC_HIST_LDS)) *slot = i32x4{0, 0, 0, 0};
                 x.y += x.x;
                 x.z += x.y;
                 x.w += x.z;
@@ -538,13 +560,65 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 v[j] = x;
                 my_max = max(my_max, max(max(x.x, x.y), max(x.z, x.w)));
                 __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
+                if (kStats && MC_HIST_LDS)
+                    *reinterpret_cast<i32x4*>(ring + sb + j * 256 + lane * 4) = x;
             }
-            if (kStats) {
+            if (kStats && MC_HIST_LDS) {
+                // final depths of the tile are in the ring: each thread takes
+                // kPer consecutive positions (long runs -> few histogram
+                // atomics) and zeroes them for the ring's next use
+                constexpr int kPer = kTileW / kBlock;
+                static_assert(kPer % 4 == 0, "tile / block must be a multiple of 4");
+                __syncthreads();
+                const int p0 = threadIdx.x * kPer;
+                const int slot0 = (int)(T0 & ring_mask) + p0;
+                int xs[kPer];
+#pragma unroll
+                for (int q = 0; q < kPer / 4; ++q) {
+                    i32x4* sl = reinterpret_cast<i32x4*>(ring + slot0 + 4 * q);
+                    const i32x4 y = *sl;
+                    *sl = i32x4{0, 0, 0, 0};
+                    xs[4 * q] = y.x;
+                    xs[4 * q + 1] = y.y;
+                    xs[4 * q + 2] = y.z;
+                    xs[4 * q + 3] = y.w;
+                }
+                while (rcur < R.n && r_gs < Tend) {
+                    const int lo = (int)((r_gs > T0 ? r_gs : T0) - T0);
+                    const int hi = (int)((r_ge < Tend ? r_ge : Tend) - T0);
+                    const bool full = lo <= p0 && hi >= p0 + kPer;
+                    int run_v = xs[0], run_n = 0;
+#pragma unroll
+                    for (int k = 0; k < kPer; ++k) {
+                        const bool in = full || (p0 + k >= lo && p0 + k < hi);
+                        const int x = xs[k];
+                        if (in && x == run_v) {
+                            ++run_n;
+                        } else if (in) {
+                            if (run_n) emit_hist(hist, ovf, run_v, run_n);
+                            run_v = x;
+                            run_n = 1;
+                        }
+                    }
+                    if (run_n) emit_hist(hist, ovf, run_v, run_n);
+                    if (r_ge <= Tend) {
+                        flush_region(R, rcur, hist, ovf);
+                        ++rcur;
+                        if (rcur < R.n) {
+                            r_gs = R.gs[rcur];
+                            r_ge = R.ge[rcur];
+                        }
+                    } else {
+                        break;
+                    }
+                }
+                __syncthreads();   // ring slots zeroed before the next tile's atomics
+            } else if (kStats) {
                 // regions covering this tile, in order; the loop is uniform.
                 // Only the value histogram is built here (runs of equal values
                 // within a lane share one LDS atomic); min/max/sum/sumsq follow
                 // from it in region_final_kernel.  Values >= kHistBins go to
-                // the per-region overflow count + the thread's StatAcc.
+                // the LDS overflow accumulator.
                 while (rcur < R.n && r_gs < Tend) {
                     const int64_t rgs = r_gs, rge = r_ge;
                     const int lo = (int)((rgs > T0 ? rgs : T0) - T0);
@@ -562,15 +636,15 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             if (in && x == run_v) {
                                 ++run_n;
                             } else if (in) {
-                                if (run_n) emit_hist(R, rcur, hist, sa, run_v, run_n);
+                                if (run_n) emit_hist(hist, ovf, run_v, run_n);
                                 run_v = x;
                                 run_n = 1;
                             }
                         }
-                        if (run_n) emit_hist(R, rcur, hist, sa, run_v, run_n);
+                        if (run_n) emit_hist(hist, ovf, run_v, run_n);
                     }
                     if (rge <= Tend) {
-                        flush_region(R, rcur, sa, hist, lane);
+                        flush_region(R, rcur, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = R.gs[rcur];
@@ -584,16 +658,20 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         }
         if (kStats) {
             // a region still open at the chunk end has partials here
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, sa, hist, lane);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, hist, ovf);
         }
         __syncthreads();   // everyone is past hdr / ring of this chunk
         if (threadIdx.x == 0) {
             if (!MC_CHUNK_PF) {
                 next_c = atomicAdd(queue, 1u);
-                if (next_c < n_chunks) next_first = chunk_first[next_c];
+                if (next_c < n_chunks) {
+                    next_first = chunk_first[2 * next_c];
+                    next_end = chunk_first[2 * next_c + 1];
+                }
             }
             hdr[0] = (int)next_c;
             *reinterpret_cast<long long*>(hdr + 2) = next_first;
+            *reinterpret_cast<long long*>(hdr + 8) = next_end;
         }
     }
     my_max = wave_max(my_max);
@@ -680,7 +758,7 @@ struct RegionOut {                     // mirrors mc_region_stat
 // One workgroup per region: block scan over the value histogram for the
 // ranks (n-1)/2, n/2 and the trimmed range [n/4, n - n/4) (pileup.py:21,24).
 // hist_stats: the fused K2 built only the histogram (values < nbins) plus the
-// overflow StatAcc in `acc` — min/max/sum/sumsq are then folded from both.
+// overflow statistics in `acc` — min/max/sum/sumsq are folded from both.
 // fallback (fused path): flags regions whose needed ranks fall into the
 // values >= nbins, which the host recomputes with the full-range K3.
 __global__ void __launch_bounds__(kBlock)
