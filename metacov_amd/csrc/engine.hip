@@ -388,7 +388,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     ctx->total_len = off;
     // LDS ring of 2 tiles: reads up to short_max = ring - kTileW keep both
     // events in LDS; longer ones take the bucketed long-read path.
-    ctx->ring = kRingTiles * kTileW;
+    ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
     ctx->tiles_per_chunk = kTilesPerChunk;
     ctx->chunk_w = (int64_t)ctx->tiles_per_chunk * kTileW;
@@ -489,14 +489,12 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     if (stats)
         hipLaunchKernelGGL(depth_kernel<true>, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,
                            ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,
-                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1,
-                           ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
+                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
                            ctx->d_maxdepth.p, fr);
     else
         hipLaunchKernelGGL(depth_kernel<false>, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,
                            ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,
-                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->ring - 1,
-                           ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
+                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
                            ctx->d_maxdepth.p, fr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[5], s));

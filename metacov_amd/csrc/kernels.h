@@ -22,8 +22,8 @@ namespace mc {
 #ifndef MC_TILE_W
 #define MC_TILE_W 4096                 // positions per tile (multiple of 1024)
 #endif
-#ifndef MC_RING_TILES
-#define MC_RING_TILES 2                // LDS ring = tiles (power of two)
+#ifndef MC_RING
+#define MC_RING (2 * MC_TILE_W)        // LDS ring ints (multiple of 256; power of two is cheapest)
 #endif
 #ifndef MC_TILES_PER_CHUNK
 #define MC_TILES_PER_CHUNK 8
@@ -50,7 +50,11 @@ namespace mc {
 constexpr int kBlock = 256;            // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
 constexpr int kTileW = MC_TILE_W;
-constexpr int kRingTiles = MC_RING_TILES;
+constexpr int kRing = MC_RING;
+static_assert(kRing % 256 == 0 && kRing > kTileW, "ring must hold a tile plus a halo");
+
+// ring slot of a chunk-relative position (the ring is re-zeroed per chunk)
+__device__ __forceinline__ int ring_slot(int rel) { return rel % kRing; }
 constexpr int kTilesPerChunk = MC_TILES_PER_CHUNK;
 constexpr int kReadsPerThread = 4;     // int4 loads of tid/pos/span
 constexpr int kBatch = kBlock * kReadsPerThread;
@@ -417,7 +421,7 @@ __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_ST
 depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              const int32_t* __restrict__ span, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
-             int64_t n_chunks, int tiles_per_chunk, int ring_mask, int short_max,
+             int64_t n_chunks, int tiles_per_chunk, int short_max,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
              const int* __restrict__ chunk_carry,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
@@ -425,11 +429,10 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     extern __shared__ __attribute__((aligned(16))) int lds[];
     int* hdr = lds;                       // [0] chunk id, [1] region cursor, [4..7] wave totals
     int* ring = lds + kLdsHeader;
-    unsigned* hist = reinterpret_cast<unsigned*>(ring + ring_mask + 1);   // kStats only
+    unsigned* hist = reinterpret_cast<unsigned*>(ring + kRing);   // kStats only
     OverflowAcc* ovf = reinterpret_cast<OverflowAcc*>(hist + kHistBins);  // kStats only
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int ring_n = ring_mask + 1;
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
@@ -454,7 +457,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     }
     for (;;) {
         // zero the ring (also orders the hdr writes before the reads)
-        for (int k = threadIdx.x * 4; k < ring_n; k += kBlock * 4)
+        for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
             *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
         __syncthreads();
         const int64_t c = hdr[0];
@@ -491,7 +494,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 const int64_t tt = T0 / kTileW;
                 const int64_t e0 = tile_ev_off[tt], e1 = tile_ev_off[tt + 1];
                 for (int64_t k = e0 + threadIdx.x; k < e1; k += kBlock)
-                    atomicAdd(&ring[(int)((T0 + tile_ev[k]) & ring_mask)], -1);
+                    atomicAdd(&ring[ring_slot(t * kTileW + tile_ev[k])], -1);
             }
             const int tend_rel = (t + 1) * kTileW;   // C0 is a multiple of the ring size
             for (;;) {
@@ -503,11 +506,11 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             const int s = rs > 0 ? rs : 0;
                             const int e = rs + sp;
                             if (e > s) {
-                                atomicAdd(&ring[s & ring_mask], 1);
-                                atomicAdd(&ring[e & ring_mask], -1);
+                                atomicAdd(&ring[ring_slot(s)], 1);
+                                atomicAdd(&ring[ring_slot(e)], -1);
                             }
                         } else if (rs >= 0) {   // long read: +1 here, -1 bucketed
-                            atomicAdd(&ring[rs & ring_mask], 1);
+                            atomicAdd(&ring[ring_slot(rs)], 1);
                         }
                         b.pending &= ~(1u << k);
                     }
@@ -526,12 +529,12 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 next_end = chunk_first[2 * next_c + 1];
             }
             // ---- scan tile t: each wave owns kWaveSpan contiguous positions
-            const int sb = (int)(T0 & ring_mask) + wave * kWaveSpan;
+            const int sb = t * kTileW + wave * kWaveSpan;   // chunk-relative start of my span
             i32x4 v[kChunks];
             int wave_total = 0;
 #pragma unroll
             for (int j = 0; j < kChunks; ++j) {
-                i32x4* slot = reinterpret_cast<i32x4*>(ring + sb + j * 256 + lane * 4);
+                i32x4* slot = reinterpret_cast<i32x4*>(ring + ring_slot(sb + j * 256) + lane * 4);
                 i32x4 x = *slot;
                 if (!(kStats && MC_HIST_LDS)) *slot = i32x4{0, 0, 0, 0};
                 x.y += x.x;
@@ -561,7 +564,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 my_max = max(my_max, max(max(x.x, x.y), max(x.z, x.w)));
                 __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
                 if (kStats && MC_HIST_LDS)
-                    *reinterpret_cast<i32x4*>(ring + sb + j * 256 + lane * 4) = x;
+                    *reinterpret_cast<i32x4*>(ring + ring_slot(sb + j * 256) + lane * 4) = x;
             }
             if (kStats && MC_HIST_LDS) {
                 // final depths of the tile are in the ring: each thread takes
@@ -571,7 +574,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 static_assert(kPer % 4 == 0, "tile / block must be a multiple of 4");
                 __syncthreads();
                 const int p0 = threadIdx.x * kPer;
-                const int slot0 = (int)(T0 & ring_mask) + p0;
+                const int slot0 = ring_slot(t * kTileW + p0);
                 int xs[kPer];
 #pragma unroll
                 for (int q = 0; q < kPer / 4; ++q) {
