@@ -210,9 +210,10 @@ def main():
     pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
     traffic = None
     variant = "depth_kernel<%s>" % ("false" if args.unfused else "true")
-    if pmc and pmc.get("reads") == args.reads and pmc.get("contigs") == args.contigs \
-            and variant in pmc.get("kernel", ""):
-        traffic = pmc.get("hbm_bytes_per_launch")
+    for v in (pmc or {}).get("variants", []):
+        if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
+                and variant in v.get("kernel", ""):
+            traffic = v.get("hbm_bytes_per_launch")
 
     if rank == 0:
         cpu = None
