@@ -28,8 +28,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--reads", type=int, default=100_000_000, help="reads per C3 workload")
-    ap.add_argument("--contigs", type=int, default=1000)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"],
+                    help="c3 (default, BASELINE configs[2]); c2: 1 x 5 Mbp, 10M x 150 bp; "
+                         "c5: 10k contigs, 50M lognormal ~10 kbp reads")
+    ap.add_argument("--reads", type=int, default=None, help="reads per workload (config default)")
+    ap.add_argument("--contigs", type=int, default=None)
     ap.add_argument("--strong", action="store_true")
     ap.add_argument("--unfused", action="store_true",
                     help="K2 then a separate K3 pass instead of the fused K2 statistics")
@@ -41,10 +44,31 @@ def parse():
     return ap.parse_args()
 
 
-def device_workload(torch, lengths, weights, n_reads, seed, dev):
+CONFIGS = {   # name: (reads, contigs, description)
+    "c2": (10_000_000, 1, "C2: 1 contig x 5 Mbp, %d x ~150 bp reads, whole-contig stats"),
+    "c3": (100_000_000, 1000, "C3 per GPU: %d contigs (~%.2f Gbp), %d x ~150 bp reads, "
+                              "whole-contig region stats"),
+    "c5": (50_000_000, 10_000, "C5 per GPU: %d contigs (~%.2f Gbp), %d lognormal ~10 kbp reads "
+                               "(long-read path), whole-contig region stats"),
+}
+
+
+def config_contigs(cfg, n_reads, n_contigs):
+    from metacov_amd import synth
+    if cfg == "c2":
+        return np.array([5_000_000], np.int64), np.ones(1)
+    if cfg == "c5":
+        rng = np.random.default_rng(5)
+        lengths = rng.integers(50_000, 150_001, size=n_contigs).astype(np.int64)
+        return lengths, lengths * rng.lognormal(0.0, 1.0, size=n_contigs)
+    return synth.c3_workload(n_reads, n_contigs)
+
+
+def device_workload(torch, lengths, weights, n_reads, seed, dev, long_reads=False):
     """C3-style pileup intervals generated on the GPU: coordinate-sorted
     int32 (tid, pos, span) with the SURVEY §8(d) span mix (3% soft clips,
-    0.5% I, 0.5% D, 0.1% N; filtered records are not part of the stream)."""
+    0.5% I, 0.5% D, 0.1% N; filtered records are not part of the stream).
+    long_reads: lognormal spans, mean ~10 kbp (C5)."""
     rng = np.random.default_rng(seed)
     counts = rng.multinomial(n_reads, weights / weights.sum())
     g = torch.Generator(device=dev)
@@ -54,11 +78,15 @@ def device_workload(torch, lengths, weights, n_reads, seed, dev):
                                   torch.from_numpy(counts).to(dev))
     u = torch.rand(n_reads, device=dev, generator=g)
     r = torch.rand(n_reads, device=dev, generator=g)
-    span = torch.full((n_reads,), 150, dtype=torch.int64, device=dev)
-    span -= ((u < 0.03) * (1 + (r * 29).long()))
-    span -= (((u >= 0.03) & (u < 0.035)) * (1 + (r * 5).long()))
-    span += (((u >= 0.035) & (u < 0.04)) * (1 + (r * 9).long()))
-    span += (((u >= 0.04) & (u < 0.041)) * (50 + (r * 1950).long()))
+    if long_reads:
+        z = torch.randn(n_reads, device=dev, generator=g, dtype=torch.float64)
+        span = torch.exp(np.log(10_000) - 0.125 + 0.5 * z).long().clamp_(min=1)
+    else:
+        span = torch.full((n_reads,), 150, dtype=torch.int64, device=dev)
+        span -= ((u < 0.03) * (1 + (r * 29).long()))
+        span -= (((u >= 0.03) & (u < 0.035)) * (1 + (r * 5).long()))
+        span += (((u >= 0.035) & (u < 0.04)) * (1 + (r * 9).long()))
+        span += (((u >= 0.04) & (u < 0.041)) * (50 + (r * 1950).long()))
     Lt = L[tid.long()]
     span = torch.minimum(span, Lt)
     pos = (torch.rand(n_reads, device=dev, generator=g, dtype=torch.float64) *
@@ -117,11 +145,15 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    lengths_all, weights_all = synth.c3_workload(args.reads, args.contigs)
+    d_reads, d_contigs, desc = CONFIGS[args.config]
+    args.reads = args.reads or d_reads
+    args.contigs = args.contigs or d_contigs
+    long_reads = args.config == "c5"
+    lengths_all, weights_all = config_contigs(args.config, args.reads, args.contigs)
     if args.strong:
         # one C3 workload, contigs LPT-sharded over the ranks
         tid, pos, span, counts = device_workload(torch, lengths_all, weights_all, args.reads,
-                                                 args.seed, dev)
+                                                 args.seed, dev, long_reads)
         owned = mdist.lpt_shard(mdist.contig_costs(lengths_all, counts), world)[rank]
         remap = torch.full((len(lengths_all),), -1, dtype=torch.int32, device=dev)
         remap[torch.from_numpy(owned).to(dev)] = torch.arange(len(owned), dtype=torch.int32,
@@ -133,7 +165,7 @@ def main():
         region_index = owned
     else:
         tid, pos, span, _ = device_workload(torch, lengths_all, weights_all, args.reads,
-                                            args.seed + 1000 * rank, dev)
+                                            args.seed + 1000 * rank, dev, long_reads)
         lengths = lengths_all
         region_index = np.arange(len(lengths)) + rank * len(lengths)
     n_regions_total = int(len(lengths_all) if args.strong else len(lengths_all) * world)
@@ -247,9 +279,11 @@ def main():
             "dtype": "int32",
             "data": "synthetic (GPU-generated C3 intervals, SURVEY §8d span mix)",
             "config": {
-                "workload": ("C3 LPT-sharded by contig over %d GPUs" % world) if args.strong else
-                            "C3 per GPU: %d contigs (~%.2f Gbp), %d x ~150 bp reads, whole-contig "
-                            "region stats" % (args.contigs, lengths_all.sum() / 1e9, args.reads),
+                "workload": ("%s LPT-sharded by contig over %d GPUs" % (args.config.upper(), world))
+                            if args.strong else
+                            (desc % args.reads if args.config == "c2" else
+                             desc % (args.contigs, lengths_all.sum() / 1e9, args.reads)),
+                "config": args.config,
                 "contigs_per_gpu": int(len(lengths)),
                 "reads_per_gpu": int(len(tid)),
                 "aligned_bases_per_step": int(total_bases),

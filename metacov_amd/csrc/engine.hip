@@ -99,6 +99,8 @@ struct mc_ctx {
 
     DevBuf<unsigned long long> d_scratch;   // ingest counters
     DevBuf<long long> d_maxend;
+    DevBuf<unsigned long long> d_cbases;
+    std::vector<unsigned long long> cbases;   // aligned bases per contig
     DevBuf<unsigned> d_queue;
     DevBuf<int> d_maxdepth;
     // K3 scratch
@@ -109,7 +111,8 @@ struct mc_ctx {
     DevBuf<RegionOut> d_out;
     // fused K2 statistics
     DevBuf<int64_t> d_fgs, d_fge, d_fchunk;
-    DevBuf<int32_t> d_fid;
+    DevBuf<int32_t> d_fid, d_fbase, d_fbase_row;
+    DevBuf<unsigned> d_flow;
     DevBuf<unsigned> d_fhist, d_fover;
     DevBuf<int> d_fflag;
     int64_t fused_fallbacks = 0;
@@ -179,6 +182,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_depth.release();
     ctx->d_scratch.release();
     ctx->d_maxend.release();
+    ctx->d_cbases.release();
     ctx->d_queue.release();
     ctx->d_maxdepth.release();
     ctx->d_seg_gs.release();
@@ -193,6 +197,9 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_fchunk.release();
     ctx->d_fge.release();
     ctx->d_fid.release();
+    ctx->d_fbase.release();
+    ctx->d_fbase_row.release();
+    ctx->d_flow.release();
     ctx->d_fhist.release();
     ctx->d_fover.release();
     ctx->d_fflag.release();
@@ -354,19 +361,24 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         HIP_TRY(hipMemsetAsync(ctx->d_tid.p + n, 0, (ctx->d_tid.cap - n) * 4, s));
     // ---- ingest: validation, aligned bases, max span, overhanging ends
     HIP_TRY(ctx->d_maxend.reserve(std::max<int32_t>(nc, 1)));
+    HIP_TRY(ctx->d_cbases.reserve(std::max<int32_t>(nc, 1)));
+    HIP_TRY(hipMemsetAsync(ctx->d_cbases.p, 0, std::max<int32_t>(nc, 1) * 8, s));
     HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(ctx->d_maxend.p, 0, std::max<int32_t>(nc, 1) * sizeof(long long), s));
     if (n) {
-        const int64_t nb = std::min<int64_t>((n + kBlock - 1) / kBlock, 8192);
+        const int64_t nb = std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock), 4096);
         hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
                            ctx->d_pos.p, ctx->d_span.p, n, ctx->d_len.p, nc, ctx->d_scratch.p,
-                           ctx->d_maxend.p);
+                           ctx->d_maxend.p, ctx->d_cbases.p);
         HIP_TRY(hipGetLastError());
     }
     unsigned long long h[4];
     std::vector<long long> maxend(std::max<int32_t>(nc, 1));
     HIP_TRY(hipMemcpyAsync(h, ctx->d_scratch.p, sizeof h, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(maxend.data(), ctx->d_maxend.p, maxend.size() * 8, hipMemcpyDeviceToHost, s));
+    ctx->cbases.assign(std::max<int32_t>(nc, 1), 0);
+    HIP_TRY(hipMemcpyAsync(ctx->cbases.data(), ctx->d_cbases.p, ctx->cbases.size() * 8,
+                           hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     MC_REQUIRE(h[0] == 0, MC_E_INVALID,
                "%llu reads have tid outside [0, %d), negative pos or negative span", h[0], nc);
@@ -390,7 +402,17 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     // events in LDS; longer ones take the bucketed long-read path.
     ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
-    ctx->tiles_per_chunk = kTilesPerChunk;
+    // chunks of kTilesPerChunk tiles; fewer (>= the tiles of one ring, so the
+    // ring divides the chunk) when the genome is too small to fill the GPU
+    {
+        const int64_t tiles = std::max<int64_t>(1, (off + kTileW - 1) / kTileW);
+        const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : kTilesPerChunk;
+        int tpc = kTilesPerChunk;
+        while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < 2048 &&
+               ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
+            tpc /= 2;
+        ctx->tiles_per_chunk = tpc;
+    }
     ctx->chunk_w = (int64_t)ctx->tiles_per_chunk * kTileW;
     ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
     const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
@@ -475,8 +497,7 @@ static int occupancy_grid(const void* kernel, size_t lds, int64_t work, int* gri
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins : 0)) * 4 +
-                       (stats ? sizeof(OverflowAcc) : 0);
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins : 0)) * 4;
     const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
     int grid = 0;
     if (int rc = occupancy_grid(kfn, lds, ctx->n_chunks, &grid)) return rc;
@@ -640,7 +661,8 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
         }
         hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)nr), dim3(kBlock), 0, s,
                            ctx->d_hist.p, nbins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p,
-                           d_out_final + r0, (int*)nullptr, 0);
+                           d_out_final + r0, (int*)nullptr, 0, (const int32_t*)nullptr,
+                           (const unsigned*)nullptr);
         HIP_TRY(hipGetLastError());
         // the host vectors die at scope end: finish the copies first
         HIP_TRY(hipStreamSynchronize(s));
@@ -660,7 +682,10 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     if (int rc = mc_prepare(ctx)) return rc;
     MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
     const int32_t nc = (int32_t)ctx->len.size();
-    struct Reg { int64_t gs, ge; int32_t id; };
+    struct Reg { int64_t gs, ge; int32_t id, base; };
+    // histogram window of each region: kHistBins values centred on its
+    // contig's mean depth (aligned bases / extent)
+    std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
     std::vector<Reg> regs;
     regs.reserve(R);
     std::vector<int64_t> ntot(std::max<int64_t>(R, 1)), nzx(std::max<int64_t>(R, 1));
@@ -674,7 +699,10 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
         ntot[r] = end[r] - start[r];
         nzx[r] = ntot[r] - (b - a);
-        if (b > a) regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r});
+        const double mean = ext > 0 ? (double)ctx->cbases[tid[r]] / (double)ext : 0.0;
+        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(mean) - kHistBins / 2);
+        if (b > a)
+            regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
     }
     std::sort(regs.begin(), regs.end(), [](const Reg& x, const Reg& y) { return x.gs < y.gs; });
     bool overlap = false;
@@ -688,11 +716,12 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     hipStream_t s = ctx->stream;
     const int64_t nf = (int64_t)regs.size();
     std::vector<int64_t> fgs(std::max<int64_t>(nf, 1)), fge(std::max<int64_t>(nf, 1));
-    std::vector<int32_t> fid(std::max<int64_t>(nf, 1));
+    std::vector<int32_t> fid(std::max<int64_t>(nf, 1)), fbase(std::max<int64_t>(nf, 1));
     for (int64_t k = 0; k < nf; ++k) {
         fgs[k] = regs[k].gs;
         fge[k] = regs[k].ge;
         fid[k] = regs[k].id;
+        fbase[k] = regs[k].base;
     }
     // first region (sorted order) ending after each chunk start: a merge walk
     std::vector<int64_t> fchunk(ctx->n_chunks);
@@ -706,6 +735,9 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     HIP_TRY(ctx->d_fgs.reserve(std::max<int64_t>(nf, 1)));
     HIP_TRY(ctx->d_fge.reserve(std::max<int64_t>(nf, 1)));
     HIP_TRY(ctx->d_fid.reserve(std::max<int64_t>(nf, 1)));
+    HIP_TRY(ctx->d_fbase.reserve(std::max<int64_t>(nf, 1)));
+    HIP_TRY(ctx->d_fbase_row.reserve(R));
+    HIP_TRY(ctx->d_flow.reserve(R));
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
     HIP_TRY(ctx->d_fflag.reserve(R));
     HIP_TRY(ctx->d_acc.reserve(R));
@@ -715,20 +747,24 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         HIP_TRY(hipMemcpyAsync(ctx->d_fgs.p, fgs.data(), nf * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(ctx->d_fge.p, fge.data(), nf * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(ctx->d_fid.p, fid.data(), nf * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ctx->d_fbase.p, fbase.data(), nf * 4, hipMemcpyHostToDevice, s));
     }
     HIP_TRY(hipMemcpyAsync(ctx->d_ntot.p, ntot.data(), R * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->d_nzx.p, nzx.data(), R * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->d_fbase_row.p, base_row.data(), R * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(ctx->d_flow.p, 0, R * 4, s));
     HIP_TRY(hipMemsetAsync(ctx->d_fhist.p, 0, (size_t)(R * kHistBins) * 4, s));
     hipLaunchKernelGGL(region_init_kernel, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock),
                        0, s, ctx->d_acc.p, R);
     HIP_TRY(hipGetLastError());
-    FusedRegions fr{nf, ctx->d_fchunk.p, ctx->d_fgs.p, ctx->d_fge.p, ctx->d_fid.p, ctx->d_acc.p,
-                    ctx->d_fhist.p};
+    FusedRegions fr{nf, ctx->d_fchunk.p, ctx->d_fgs.p, ctx->d_fge.p, ctx->d_fid.p,
+                    ctx->d_fbase.p, ctx->d_acc.p, ctx->d_fhist.p, ctx->d_flow.p};
     if (nf == 0) fr.n = 0;
     if (int rc = launch_depth(ctx, fr)) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[6], s));
     hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
-                       kHistBins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p, d_out, ctx->d_fflag.p, 1);
+                       kHistBins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p, d_out, ctx->d_fflag.p, 1,
+                       ctx->d_fbase_row.p, ctx->d_flow.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;

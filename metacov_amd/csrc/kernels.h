@@ -104,29 +104,65 @@ __device__ __forceinline__ int wave_min(int v) {
 
 // out[0] = invalid records, out[1] = order violations, out[2] = aligned
 // bases, out[3] = max span.  maxend[t] = furthest read end past len[t].
+// 4 reads per thread (int4 loads; the arrays are padded past n).
 __global__ void __launch_bounds__(kBlock)
 ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
               const int32_t* __restrict__ span, int64_t n,
               const int64_t* __restrict__ len, int32_t n_contigs,
-              unsigned long long* __restrict__ out, long long* __restrict__ maxend) {
+              unsigned long long* __restrict__ out, long long* __restrict__ maxend,
+              unsigned long long* __restrict__ cbases) {
     const int lane = threadIdx.x & 63;
-    long long bad = 0, unsorted = 0, bases = 0;
+    long long bad = 0, unsorted = 0, bases = 0, my_bases = 0;
     int mspan = 0;
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * kBlock) {
-        const int t = tid[i], p = pos[i], s = span[i];
-        if (t < 0 || t >= n_contigs || p < 0 || s < 0) {
-            ++bad;
-            continue;
+    for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q * 4 < n;
+         q += (int64_t)gridDim.x * kBlock) {
+        const int64_t i0 = q * 4;
+        const i32x4 t4 = *reinterpret_cast<const i32x4*>(tid + i0);
+        const i32x4 p4 = *reinterpret_cast<const i32x4*>(pos + i0);
+        const i32x4 s4 = *reinterpret_cast<const i32x4*>(span + i0);
+        int tp = -1, pp = 0;
+        if (i0 > 0) {
+            tp = tid[i0 - 1];
+            pp = pos[i0 - 1];
         }
-        if (i > 0) {
-            const int tp = tid[i - 1], pp = pos[i - 1];
-            if (tp > t || (tp == t && pp > p)) ++unsorted;
+        const int tt[4] = {t4.x, t4.y, t4.z, t4.w};
+        const int ps[4] = {p4.x, p4.y, p4.z, p4.w};
+        const int ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (i0 + k >= n) break;
+            const int t = tt[k], p = ps[k], sp = ss[k];
+            if (t < 0 || t >= n_contigs || p < 0 || sp < 0) {
+                ++bad;
+            } else {
+                if (tp > t || (tp == t && pp > p)) ++unsorted;
+                bases += sp;
+                mspan = max(mspan, sp);
+                my_bases += sp;
+                const long long e = (long long)p + sp;
+                if (e > len[t]) atomicMax(&maxend[t], e);
+            }
+            tp = t;
+            pp = p;
         }
-        bases += s;
-        mspan = max(mspan, s);
-        const long long e = (long long)p + s;
-        if (e > len[t]) atomicMax(&maxend[t], e);
+        // per-contig aligned bases (histogram windows of the fused statistics):
+        // the wave's 256 reads are consecutive, so usually one contig -> one
+        // atomic per wave; mixed waves add per lane
+        const int t0 = __shfl(t4.x, 0, 64);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) same &= (i0 + k >= n) || tt[k] == t0;
+        if (__all(same)) {
+            const long long wsum = wave_sum64(my_bases);
+            if (lane == 0 && wsum && t0 >= 0 && t0 < n_contigs)
+                atomicAdd(&cbases[t0], (unsigned long long)wsum);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i0 + k < n && tt[k] >= 0 && tt[k] < n_contigs && ss[k] > 0)
+                    atomicAdd(&cbases[tt[k]], (unsigned long long)ss[k]);
+        }
+        my_bases = 0;
     }
     bad = wave_sum64(bad);
     unsorted = wave_sum64(unsorted);
@@ -332,65 +368,82 @@ struct FusedRegions {
     const int64_t* gs;                 // [n] global start (sorted)
     const int64_t* ge;                 // [n] global end (clipped to the contig extent)
     const int32_t* id;                 // [n] caller's row index
-    RegionAcc* acc;                    // [rows]
+    const int32_t* base;               // [n] value of histogram bin 0 (window base)
+    RegionAcc* acc;                    // [rows] statistics of the values outside the window
     unsigned* hist;                    // [rows][kHistBins]
+    unsigned* low;                     // [rows] count of values below the window
 };
 
-// Statistics of the values >= kHistBins of the current region, in LDS
-// (rare; kept out of registers so the common path stays lean).
-struct OverflowAcc {
-    unsigned long long sum, sumsq;
+// Statistics of the values outside the histogram window of the current
+// region, per thread in registers (rare in the common case; reduced only when
+// a wave saw any).
+struct OvAcc {
+    unsigned long long sum, sq;
     int vmin, vmax;
-    unsigned cnt, pad;
+    unsigned cnt, low;                 // values outside the window / below it
+    __device__ void reset() {
+        sum = sq = 0;
+        vmin = 0x7fffffff;
+        vmax = 0;
+        cnt = low = 0;
+    }
 };
 
-__device__ __forceinline__ void emit_hist(unsigned* h, OverflowAcc* ov, int v, int cnt) {
+// One run of `cnt` positions of depth v: histogram bin v - base, or the
+// thread's overflow accumulator when v falls outside [base, base + kHistBins).
+__device__ __forceinline__ void emit_hist(unsigned* h, OvAcc& ov, int v, int cnt, int base) {
+    const int b = v - base;
 #ifdef MC_EXP_NO_HIST
-    asm volatile("" :: "v"(v), "v"(cnt));
+    asm volatile("" :: "v"(b), "v"(cnt));
     return;
 #endif
-#ifdef MC_EXP_NO_OVF
-    atomicAdd(&h[v & (kHistBins - 1)], (unsigned)cnt);
-    return;
-#endif
-    if (v < kHistBins) {
+    if ((unsigned)b < (unsigned)kHistBins) {
 #ifdef MC_EXP_HIST_SPREAD   // experiment: same instruction count, no address conflicts
-        atomicAdd(&h[(v + (int)threadIdx.x) & (kHistBins - 1)], (unsigned)cnt);
+        atomicAdd(&h[(b + (int)threadIdx.x) & (kHistBins - 1)], (unsigned)cnt);
 #else
-        atomicAdd(&h[v], (unsigned)cnt);
+        atomicAdd(&h[b], (unsigned)cnt);
 #endif
     } else {
-        atomicAdd(&ov->cnt, (unsigned)cnt);
-        atomicAdd(&ov->sum, (unsigned long long)v * (unsigned long long)cnt);
-        atomicAdd(&ov->sumsq, (unsigned long long)((long long)v * v) * (unsigned long long)cnt);
-        atomicMin(&ov->vmin, v);
-        atomicMax(&ov->vmax, v);
+        ov.cnt += cnt;
+        if (b < 0) ov.low += cnt;
+        ov.sum += (unsigned long long)v * (unsigned long long)cnt;
+        ov.sq += (unsigned long long)((long long)v * v) * (unsigned long long)cnt;
+        ov.vmin = min(ov.vmin, v);
+        ov.vmax = max(ov.vmax, v);
     }
-}
-
-__device__ __forceinline__ void reset_overflow(OverflowAcc* ov) {
-    ov->sum = 0;
-    ov->sumsq = 0;
-    ov->vmin = 0x7fffffff;
-    ov->vmax = 0;
-    ov->cnt = 0;
 }
 
 // Every thread calls it (it holds barriers): folds the overflow statistics
 // into the region's global accumulator and flushes the LDS histogram.
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
-                                             OverflowAcc* ov) {
+                                             OvAcc& ov, int lane) {
 #ifdef MC_EXP_NO_FLUSH
     return;
 #endif
     const int id = R.id[r];
-    __syncthreads();
-    if (threadIdx.x == 0 && ov->cnt) {
-        atomicMin(&R.acc[id].min, ov->vmin);
-        atomicMax(&R.acc[id].max, ov->vmax);
-        atomicAdd(&R.acc[id].sum, ov->sum);
-        atomicAdd(&R.acc[id].sumsq, ov->sumsq);
+    if (__any(ov.cnt != 0)) {
+        unsigned long long sum = ov.sum, sq = ov.sq;
+        unsigned cnt = ov.cnt, low = ov.low;
+        int vmin = ov.vmin, vmax = ov.vmax;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+            sum += __shfl_xor(sum, d, 64);
+            sq += __shfl_xor(sq, d, 64);
+            cnt += __shfl_xor(cnt, d, 64);
+            low += __shfl_xor(low, d, 64);
+            vmin = min(vmin, __shfl_xor(vmin, d, 64));
+            vmax = max(vmax, __shfl_xor(vmax, d, 64));
+        }
+        if (lane == 0 && cnt) {
+            if (low) atomicAdd(&R.low[id], low);
+            atomicMin(&R.acc[id].min, vmin);
+            atomicMax(&R.acc[id].max, vmax);
+            atomicAdd(&R.acc[id].sum, sum);
+            atomicAdd(&R.acc[id].sumsq, sq);
+        }
+        ov.reset();
     }
+    __syncthreads();
     unsigned* g = R.hist + (int64_t)id * kHistBins;
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
         const unsigned cnt = h[k];
@@ -402,7 +455,6 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) reset_overflow(ov);
 }
 
 // One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
@@ -430,7 +482,8 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     int* hdr = lds;                       // [0] chunk id, [1] region cursor, [4..7] wave totals
     int* ring = lds + kLdsHeader;
     unsigned* hist = reinterpret_cast<unsigned*>(ring + kRing);   // kStats only
-    OverflowAcc* ovf = reinterpret_cast<OverflowAcc*>(hist + kHistBins);  // kStats only
+    OvAcc ovf;
+    ovf.reset();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
@@ -440,7 +493,6 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     int my_max = 0;
     if (kStats) {
         for (int k = threadIdx.x; k < kHistBins; k += kBlock) hist[k] = 0;
-        if (threadIdx.x == 0) reset_overflow(ovf);
     }
 
     // chunk ids come from an atomic queue; thread 0 fetches the next id (and
@@ -467,11 +519,13 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (MC_CHUNK_PF && threadIdx.x == 0) next_c = atomicAdd(queue, 1u);
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
+        int r_base = 0;
         if (kStats) {
             rcur = R.chunk_first[c];
             if (rcur < R.n) {
                 r_gs = R.gs[rcur];
                 r_ge = R.ge[rcur];
+                r_base = R.base[rcur];
             }
         }
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
@@ -598,18 +652,19 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                         if (in && x == run_v) {
                             ++run_n;
                         } else if (in) {
-                            if (run_n) emit_hist(hist, ovf, run_v, run_n);
+                            if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
                             run_v = x;
                             run_n = 1;
                         }
                     }
-                    if (run_n) emit_hist(hist, ovf, run_v, run_n);
+                    if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
                     if (r_ge <= Tend) {
-                        flush_region(R, rcur, hist, ovf);
+                        flush_region(R, rcur, hist, ovf, lane);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = R.gs[rcur];
                             r_ge = R.ge[rcur];
+                            r_base = R.base[rcur];
                         }
                     } else {
                         break;
@@ -639,19 +694,20 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             if (in && x == run_v) {
                                 ++run_n;
                             } else if (in) {
-                                if (run_n) emit_hist(hist, ovf, run_v, run_n);
+                                if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
                                 run_v = x;
                                 run_n = 1;
                             }
                         }
-                        if (run_n) emit_hist(hist, ovf, run_v, run_n);
+                        if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
                     }
                     if (rge <= Tend) {
-                        flush_region(R, rcur, hist, ovf);
+                        flush_region(R, rcur, hist, ovf, lane);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = R.gs[rcur];
                             r_ge = R.ge[rcur];
+                            r_base = R.base[rcur];
                         }
                     } else {
                         break;
@@ -661,7 +717,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         }
         if (kStats) {
             // a region still open at the chunk end has partials here
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, hist, ovf);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, hist, ovf, lane);
         }
         __syncthreads();   // everyone is past hdr / ring of this chunk
         if (threadIdx.x == 0) {
@@ -760,15 +816,18 @@ struct RegionOut {                     // mirrors mc_region_stat
 
 // One workgroup per region: block scan over the value histogram for the
 // ranks (n-1)/2, n/2 and the trimmed range [n/4, n - n/4) (pileup.py:21,24).
-// hist_stats: the fused K2 built only the histogram (values < nbins) plus the
-// overflow statistics in `acc` — min/max/sum/sumsq are folded from both.
-// fallback (fused path): flags regions whose needed ranks fall into the
-// values >= nbins, which the host recomputes with the full-range K3.
+// Bin b holds the value base[r] + b (base = nullptr: 0).  Values outside the
+// window were accumulated in `acc` (count below it in low[r]); with
+// hist_stats, min/max/sum/sumsq are folded from the histogram and `acc`,
+// otherwise `acc` holds the full statistics (K3a).  fallback[r] = 1 when a
+// needed rank lies outside the window: the host recomputes that region with
+// the full-range K3.  Positions past the contig extent (zx) are zeros.
 __global__ void __launch_bounds__(kBlock)
 region_final_kernel(const unsigned* __restrict__ hist, int nbins,
                     const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
                     const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
-                    int* __restrict__ fallback, int hist_stats) {
+                    int* __restrict__ fallback, int hist_stats,
+                    const int32_t* __restrict__ base_of, const unsigned* __restrict__ low_of) {
     __shared__ long long s_part[kBlock];
     __shared__ long long s_red[4][kWaves];
     __shared__ long long s_med[2];
@@ -777,6 +836,11 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     const unsigned* hr = hist + (int64_t)r * nbins;
     const long long n = n_total[r];
     const long long zx = n_zero_extra[r];
+    const long long base = base_of ? base_of[r] : 0;
+    // zeros past the extent land in bin 0 when the window starts at 0,
+    // otherwise below the window
+    const long long zx_bin = base == 0 ? zx : 0;
+    const long long low = (low_of ? (long long)low_of[r] : 0) + (base == 0 ? 0 : zx);
     const int per = (nbins + kBlock - 1) / kBlock;
     const int b0 = threadIdx.x * per;
     const int b1 = min(nbins, b0 + per);
@@ -784,11 +848,12 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     unsigned long long s2 = 0;
     int lmin = 0x7fffffff, lmax = -1;
     for (int b = b0; b < b1; ++b) {
-        const long long cnt = (long long)hr[b] + (b == 0 ? zx : 0);
+        const long long cnt = (long long)hr[b] + (b == 0 ? zx_bin : 0);
         if (!cnt) continue;
+        const long long v = base + b;
         local += cnt;
-        s1 += cnt * b;
-        s2 += (unsigned long long)cnt * (unsigned long long)((long long)b * b);
+        s1 += cnt * v;
+        s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
         lmin = min(lmin, b);
         lmax = max(lmax, b);
     }
@@ -802,20 +867,21 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
         s_part[threadIdx.x] += y;
         __syncthreads();
     }
-    long long cum = s_part[threadIdx.x] - local;
-    const long long in_hist = s_part[kBlock - 1];   // values < nbins, zeros included
+    long long cum = low + s_part[threadIdx.x] - local;   // values below the window rank first
+    const long long in_hist = s_part[kBlock - 1];
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;
     const long long q_lo = n / 4, q_hi = n - n / 4;
     long long qsum = 0;
     for (int b = b0; b < b1; ++b) {
-        const long long cnt = (long long)hr[b] + (b == 0 ? zx : 0);
+        const long long cnt = (long long)hr[b] + (b == 0 ? zx_bin : 0);
         if (cnt == 0) continue;
+        const long long v = base + b;
         const long long e = cum + cnt;
-        if (r_lo >= cum && r_lo < e) s_med[0] = b;
-        if (r_hi >= cum && r_hi < e) s_med[1] = b;
+        if (r_lo >= cum && r_lo < e) s_med[0] = v;
+        if (r_hi >= cum && r_hi < e) s_med[1] = v;
         const long long lo = cum > q_lo ? cum : q_lo;
         const long long hi = e < q_hi ? e : q_hi;
-        if (hi > lo) qsum += (hi - lo) * (long long)b;
+        if (hi > lo) qsum += (hi - lo) * v;
         cum = e;
     }
     qsum = wave_sum64(qsum);
@@ -832,7 +898,10 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (fallback) fallback[r] = (n > 0 && (q_hi - 1 >= in_hist || r_hi >= in_hist)) ? 1 : 0;
+        const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
+        if (fallback)
+            fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo ||
+                                     q_hi - 1 >= win_hi)) ? 1 : 0;
         long long q = 0, t1 = 0;
         unsigned long long t2 = 0;
         int hmin = 0x7fffffff, hmax = -1;
@@ -847,11 +916,18 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
         RegionOut o;
         o.n = n;
         if (hist_stats) {
-            // histogram part + overflow part (a.min == INT_MAX when empty)
+            const long long high = n - win_hi;        // values above the window
             o.sum = t1 + (long long)a.sum;
             o.sumsq = t2 + a.sumsq;
-            o.min = in_hist > 0 ? hmin : a.min;
-            o.max = a.max > hmax ? a.max : hmax;
+            if (low > 0) {
+                long long m = a.min;                   // INT_MAX when only zeros are below
+                if (base > 0 && zx > 0) m = 0;
+                o.min = m;
+            } else {
+                o.min = in_hist > 0 ? base + hmin : a.min;
+            }
+            o.max = high > 0 ? (long long)a.max : (in_hist > 0 ? base + hmax : (long long)a.max);
+            if (o.max < 0) o.max = 0;
         } else {
             o.sum = (long long)a.sum;
             o.sumsq = a.sumsq;

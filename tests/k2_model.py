@@ -8,12 +8,23 @@ bugs show up without a GPU.  Constants must match kernels.h.
 """
 import numpy as np
 from oracle import coracle
-W=4096; TPC=8; CW=W*TPC; RING=8192; SM=RING-W
+W=4096; TPC_MAX=8; RING=8192; SM=RING-W
+
+
+def tiles_per_chunk(G):
+    """engine.hip mc_prepare: halve the chunk while it leaves < 2048 chunks."""
+    tiles = max(1, (G + W - 1) // W)
+    tpc = TPC_MAX
+    while tpc // 2 >= RING // W and tpc % 2 == 0 and tiles // tpc < 2048:
+        tpc //= 2
+    return tpc
+
 def model(lengths, tid, pos, span):
     ext, coff64 = coracle.layout(lengths, tid, pos, span)
     coff=np.zeros(len(ext)+1,np.int64); 
     for i in range(len(ext)): coff[i+1]=coff[i]+ (ext[i]+63)//64*64
-    G=coff[-1]; nch=max(1,(G+CW-1)//CW); alloc=nch*CW
+    G=coff[-1]; TPC=tiles_per_chunk(G); CW=W*TPC
+    nch=max(1,(G+CW-1)//CW); alloc=nch*CW
     gs=coff[tid]+pos; ge=gs+span
     ms=span.max() if len(span) else 0; halo=min(ms,SM)
     long_=span>SM

@@ -385,3 +385,25 @@ def test_fused_fixture_goldens(eng, fixture_golden):
                                    [r["start"] for r in regs], [r["end"] for r in regs])
     for row, r in zip(rows, regs):
         assert classic_stats(row) == r["stats"]
+
+
+def test_fused_window_follows_mean_depth(eng):
+    """Depth ~5000 everywhere: the fused histogram window is centred on the
+    contig's mean, so no region needs the fallback and rows stay exact."""
+    rng = np.random.default_rng(41)
+    L = 120_000
+    n = 4_000_000
+    pos = np.sort(rng.integers(0, L - 150, size=n)).astype(np.int32)
+    tid = np.zeros(n, np.int32)
+    span = np.full(n, 150, np.int32)
+    d, ext, coff = coracle.depth([L], tid, pos, span)
+    rt = np.zeros(3, np.int32)
+    rs = np.array([0, 1000, 60_000], np.int64)
+    re_ = np.array([1000, 60_000, L + 10], np.int64)
+    eng.set_contigs([L])
+    eng.add_reads(tid, pos, span)
+    got = eng.compute_depth_stats(rt, rs, re_)
+    want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
+    assert eng.fused_fallbacks() == 0

@@ -37,9 +37,10 @@ def test_model_random(args):
 
 
 def test_model_end_on_chunk_start():
-    # long reads whose end lands exactly on a chunk start (65536) or a tile start
+    # long reads whose end lands exactly on a chunk start (8192 with the small
+    # genome's 2-tile chunks; 65536 / 32768 on large ones) or a tile start
     lengths = [200_000]
-    pos = np.array([100, 5000, 60_000, 61_440], np.int32)
-    span = np.array([65436, 60536, 5536, 69632], np.int32)
+    pos = np.array([100, 5000, 60_000, 61_440, 3000, 1], np.int32)
+    span = np.array([65436, 60536, 5536, 69632, 5192, 16383], np.int32)
     o = np.argsort(pos)
-    _check(lengths, np.zeros(4, np.int32), pos[o], span[o])
+    _check(lengths, np.zeros(len(pos), np.int32), pos[o], span[o])
