@@ -178,6 +178,16 @@ int mc_bam_intervals(const mc_bam* bam, int32_t* tid, int32_t* pos, int32_t* spa
 int mc_bam_n_cigar_words(const mc_bam* bam, int64_t* n);
 int mc_bam_cigars(const mc_bam* bam, int64_t* cig_off, uint32_t* cigar);
 
+/* ---- synthetic BAM writer ------------------------------------------------
+ * Writes coordinate-sorted records from SoA arrays as BGZF-compressed BAM
+ * (blocks deflated on n_threads threads; level = zlib level).  The role of
+ * the reference's `metacov simulate` (cli.py:288-414) for the benchmarks and
+ * end-to-end tests, without ART.  Bases 'A', qualities 30, names "r<i>". */
+int mc_bam_write(const char* path, int32_t n_ref, const char* const* names,
+                 const int64_t* lengths, int64_t n, const int32_t* tid,
+                 const int32_t* pos, const uint16_t* flag, const int64_t* cig_off,
+                 const uint32_t* cigar, int32_t l_seq, int level, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,6 +86,8 @@ SIGNATURES = {
     "mc_bam_intervals": [_P, _P, _P, _P],
     "mc_bam_n_cigar_words": [_P, _PI64],
     "mc_bam_cigars": [_P, _P, _P],
+    "mc_bam_write": [ctypes.c_char_p, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _I32, ctypes.c_int,
+                     ctypes.c_int],
 }
 _RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p}
 

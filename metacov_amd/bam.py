@@ -73,16 +73,21 @@ class BamFile:
     def aligned_bases(self):
         return int(self.span.astype(np.int64).sum())
 
-    def engine(self, device=0):
-        """A CoverageEngine holding this file's depth (computed once, cached)."""
+    def engine(self, device=0, compute=True):
+        """A CoverageEngine holding this file's reads (cached per device);
+        with compute=True its depth is computed (once)."""
         eng = self._engines.get(device)
         if eng is None:
             from .engine import CoverageEngine
             eng = CoverageEngine(device)
             eng.set_contigs(np.asarray(self.lengths, dtype=np.int64))
             eng.add_reads(self.tid, self.pos, self.span)
-            eng.compute_depth()
+            eng.prepare()
+            eng._depth_ready = False
             self._engines[device] = eng
+        if compute and not eng._depth_ready:
+            eng.compute_depth()
+            eng._depth_ready = True
         return eng
 
     def close(self):

@@ -80,8 +80,14 @@ def write_rows(bam, regions, outfile, device=0):
         tids.append(bam.references.index(ref))
         starts.append(start)
         ends.append(end)
-    rows = bam.engine(device).region_stats(np.array(tids, np.int32), np.array(starts, np.int64),
-                                           np.array(ends, np.int64)) if regions else []
+    # depth and statistics in one pass (fused K2) when the regions do not
+    # overlap; the library falls back to K2 + K3 otherwise
+    rows = []
+    if regions:
+        eng = bam.engine(device, compute=False)
+        rows = eng.compute_depth_stats(np.array(tids, np.int32), np.array(starts, np.int64),
+                                       np.array(ends, np.int64))
+        eng._depth_ready = True
     writer = None
     for hit, row in zip(regions, rows):
         result = classic_stats(row)

@@ -21,6 +21,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -163,7 +167,18 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
     std::vector<Block> blocks;
     size_t total = 0;
     if (int rc = scan_blocks(mf.data, mf.size, blocks, total)) return rc;
-    std::vector<uint8_t> buf(total + 8);
+    // uninitialised: the inflate threads fault the pages in, in parallel
+    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total + 8]);
+    MC_REQUIRE(buf, MC_E_IO, "cannot allocate %zu bytes for %s", total, path);
+    const bool timing = std::getenv("MC_DECODE_TIMING") != nullptr;
+    auto t_start = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[mc_bam_open] %-10s %8.3f s\n", what,
+                     std::chrono::duration<double>(now - t_start).count());
+        t_start = now;
+    };
     int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
     nt = std::max(1, std::min<int>(nt, (int)blocks.size()));
     std::atomic<size_t> next{0};
@@ -175,7 +190,7 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
             const size_t ke = std::min(blocks.size(), k + 16);
             for (size_t j = k; j < ke; ++j) {
                 const Block& b = blocks[j];
-                if (!inflate_block(mf.data + b.cdata, b.clen, buf.data() + b.out, b.isize))
+                if (!inflate_block(mf.data + b.cdata, b.clen, buf.get() + b.out, b.isize))
                     failed = true;
             }
         }
@@ -185,8 +200,9 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
     worker();
     for (auto& th : pool) th.join();
     MC_REQUIRE(!failed, MC_E_IO, "BGZF inflate failed in %s", path);
+    lap("inflate");
 
-    const uint8_t* d = buf.data();
+    const uint8_t* d = buf.get();
     const size_t n = total;
     MC_REQUIRE(n >= 12 && std::memcmp(d, "BAM\1", 4) == 0, MC_E_IO, "%s: missing BAM magic", path);
     size_t o = 4;
@@ -213,27 +229,103 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
         bam->lens.push_back(rdi32(d + o));
         o += 4;
     }
-    if (bam->keep_cigar) bam->cig_off.push_back(0);
-    while (o < n) {
-        if (o + 4 > n) return fail("truncated record", o);
-        const int32_t block_size = rdi32(d + o);
-        if (block_size < 32 || o + 4 + (size_t)block_size > n) return fail("bad record size", o);
-        const uint8_t* r = d + o + 4;
-        const uint8_t* rend = r + block_size;
-        const int32_t tid = rdi32(r);
-        const int32_t pos = rdi32(r + 4);
+    // ---- records: the stream is cut into byte ranges; each range finds its
+    // first record start in parallel (a candidate offset must begin a chain
+    // of structurally valid records), and the ranges' walks must meet exactly
+    // (range i ends on range i+1's first record) or the split falls back to
+    // one sequential walk.  The ranges are then parsed in parallel twice
+    // (count kept records / CIGAR words, then fill exact-size outputs).
+    auto plausible = [&](size_t q) -> bool {
+        if (q + 36 > n) return false;
+        const int32_t bs = rdi32(d + q);
+        if (bs < 32 || q + 4 + (size_t)bs > n) return false;
+        const int32_t tid = rdi32(d + q + 4), pos = rdi32(d + q + 8);
+        const uint8_t lrn = d[q + 12];
+        const uint32_t ncig = rd16(d + q + 16);
+        const int32_t lseq = rdi32(d + q + 20), ntid = rdi32(d + q + 24);
+        if (tid < -1 || tid >= n_ref || ntid < -1 || ntid >= n_ref || pos < -1 || lrn == 0 ||
+            lseq < 0)
+            return false;
+        const uint64_t need = 32 + (uint64_t)lrn + 4ull * ncig + ((uint64_t)lseq + 1) / 2 + (uint64_t)lseq;
+        if (need > (uint64_t)bs) return false;
+        return d[q + 36 + lrn - 1] == 0;
+    };
+    auto sync_at = [&](size_t from, size_t limit) -> size_t {   // first chained record start
+        for (size_t q = from; q < limit; ++q) {
+            size_t z = q;
+            int k = 0;
+            for (; k < 8 && z < n && plausible(z); ++k) z += 4 + (size_t)rdi32(d + z);
+            if (k == 8 || z == n) return q;
+        }
+        return limit;
+    };
+    const size_t nseg_target = std::max<size_t>(1, std::min<size_t>((size_t)nt * 4, (n - o) / (1 << 20) + 1));
+    std::vector<size_t> seg_off(nseg_target + 1);
+    seg_off[0] = o;
+    seg_off[nseg_target] = n;
+    {
+        std::vector<size_t> cut(nseg_target + 1);
+        for (size_t i = 0; i <= nseg_target; ++i) cut[i] = o + (n - o) * i / nseg_target;
+        std::vector<std::thread> pool;
+        std::atomic<size_t> nx{1};
+        auto w = [&]() {
+            for (size_t i; (i = nx.fetch_add(1)) < nseg_target;) seg_off[i] = sync_at(cut[i], n);
+        };
+        for (int i = 1; i < nt; ++i) pool.emplace_back(w);
+        w();
+        for (auto& t : pool) t.join();
+    }
+    // verify that consecutive ranges meet; fall back to the sequential walk
+    bool chained = true;
+    {
+        std::vector<char> ok(nseg_target, 1);
+        std::vector<std::thread> pool;
+        std::atomic<size_t> nx{0};
+        auto w = [&]() {
+            for (size_t i; (i = nx.fetch_add(1)) < nseg_target;) {
+                size_t q = seg_off[i];
+                const size_t end = seg_off[i + 1];
+                if (q > end) { ok[i] = 0; continue; }
+                while (q < end) {
+                    if (q + 4 > n) { ok[i] = 0; break; }
+                    const int32_t bs = rdi32(d + q);
+                    if (bs < 32 || q + 4 + (size_t)bs > n) { ok[i] = 0; break; }
+                    q += 4 + (size_t)bs;
+                }
+                if (q != end) ok[i] = 0;
+            }
+        };
+        for (int i = 1; i < nt; ++i) pool.emplace_back(w);
+        w();
+        for (auto& t : pool) t.join();
+        for (char c : ok) chained &= c != 0;
+    }
+    if (!chained) {
+        seg_off.assign(1, o);
+        size_t q = o;
+        while (q < n) {
+            if (q + 4 > n) return fail("truncated record", q);
+            const int32_t bs = rdi32(d + q);
+            if (bs < 32 || q + 4 + (size_t)bs > n) return fail("bad record size", q);
+            q += 4 + (size_t)bs;
+        }
+        seg_off.push_back(n);
+    }
+    // drop empty ranges
+    seg_off.erase(std::unique(seg_off.begin(), seg_off.end()), seg_off.end());
+    if (seg_off.size() < 2) seg_off.push_back(n);
+    lap("boundaries");
+    const size_t nseg = seg_off.size() - 1;
+    struct SegCount { int64_t kept = 0, words = 0, mapped = 0, unmapped = 0, records = 0; int err = 0; size_t err_at = 0; };
+    std::vector<SegCount> sc(nseg);
+    // parse one record; returns false on a format error
+    auto cigar_of = [&](const uint8_t* r, const uint8_t* rend, const uint8_t** cig_out,
+                        uint32_t* n_out) -> bool {
         const uint8_t l_read_name = r[8];
         uint32_t n_cigar = rd16(r + 12);
-        const uint16_t flag = rd16(r + 14);
         const int32_t l_seq = rdi32(r + 16);
-        ++bam->n_records;
-        if (tid >= 0 && !(flag & 4)) ++bam->n_mapped;
-        else ++bam->n_unmapped;
-        o += 4 + (size_t)block_size;
-        if (tid < 0 || (flag & flag_filter)) continue;
-        if (tid >= n_ref) return fail("record tid beyond the reference list", o);
         const uint8_t* cig = r + 32 + l_read_name;
-        if (cig + (size_t)n_cigar * 4 > rend) return fail("CIGAR overruns record", o);
+        if (cig + (size_t)n_cigar * 4 > rend) return false;
         if (n_cigar == 2 && rd32(cig) == (((uint32_t)l_seq << 4) | 4u) && (rd32(cig + 4) & 0xF) == 3) {
             const uint8_t* aux = cig + 8 + ((size_t)l_seq + 1) / 2 + (size_t)l_seq;
             const uint8_t* words = nullptr;
@@ -243,21 +335,100 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
                 n_cigar = cnt;
             }
         }
-        int64_t rlen = 0;
-        for (uint32_t k = 0; k < n_cigar; ++k) {
-            const uint32_t c = rd32(cig + 4 * k);
-            if ((0x18Du >> (c & 0xF)) & 1u) rlen += c >> 4;
+        *cig_out = cig;
+        *n_out = n_cigar;
+        return true;
+    };
+    std::vector<int64_t> kept_off(nseg + 1, 0), word_off(nseg + 1, 0);
+    auto run_pass = [&](int pass) {
+        std::atomic<size_t> next_seg{0};
+        auto work = [&]() {
+            for (size_t g; (g = next_seg.fetch_add(1)) < nseg;) {
+                SegCount& c = sc[g];
+                int64_t ki = kept_off[g], wi = word_off[g];
+                for (size_t q = seg_off[g]; q < seg_off[g + 1];) {
+                    const int32_t block_size = rdi32(d + q);
+                    const uint8_t* r = d + q + 4;
+                    const uint8_t* rend = r + block_size;
+                    q += 4 + (size_t)block_size;
+                    const int32_t tid = rdi32(r);
+                    const uint16_t flag = rd16(r + 14);
+                    if (pass == 0) {
+                        ++c.records;
+                        if (tid >= 0 && !(flag & 4)) ++c.mapped;
+                        else ++c.unmapped;
+                    }
+                    if (tid < 0 || (flag & flag_filter)) continue;
+                    if (tid >= n_ref) {
+                        c.err = 1;
+                        c.err_at = q;
+                        return;
+                    }
+                    const uint8_t* cig;
+                    uint32_t n_cigar;
+                    if (!cigar_of(r, rend, &cig, &n_cigar)) {
+                        c.err = 2;
+                        c.err_at = q;
+                        return;
+                    }
+                    if (pass == 0) {
+                        ++c.kept;
+                        c.words += n_cigar;
+                        continue;
+                    }
+                    int64_t rlen = 0;
+                    for (uint32_t k = 0; k < n_cigar; ++k) {
+                        const uint32_t cw = rd32(cig + 4 * k);
+                        if ((0x18Du >> (cw & 0xF)) & 1u) rlen += cw >> 4;
+                    }
+                    if (rlen <= 0) rlen = 1;
+                    if (rlen > INT32_MAX) {
+                        c.err = 3;
+                        c.err_at = q;
+                        return;
+                    }
+                    bam->tid[ki] = tid;
+                    bam->pos[ki] = rdi32(r + 4);
+                    bam->span[ki] = (int32_t)rlen;
+                    if (bam->keep_cigar) {
+                        std::memcpy(bam->cigar.data() + wi, cig, (size_t)n_cigar * 4);
+                        wi += n_cigar;
+                        bam->cig_off[ki + 1] = wi;
+                    }
+                    ++ki;
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int i = 1; i < std::min<int>(nt, (int)nseg); ++i) pool.emplace_back(work);
+        work();
+        for (auto& t : pool) t.join();
+    };
+    run_pass(0);
+    lap("count");
+    for (size_t g = 0; g < nseg; ++g) {
+        if (sc[g].err) {
+            return fail(sc[g].err == 1 ? "record tid beyond the reference list"
+                        : sc[g].err == 2 ? "CIGAR overruns record" : "reference span exceeds int32",
+                        sc[g].err_at);
         }
-        if (rlen <= 0) rlen = 1;
-        if (rlen > INT32_MAX) return fail("reference span exceeds int32", o);
-        bam->tid.push_back(tid);
-        bam->pos.push_back(pos);
-        bam->span.push_back((int32_t)rlen);
-        if (bam->keep_cigar) {
-            for (uint32_t k = 0; k < n_cigar; ++k) bam->cigar.push_back(rd32(cig + 4 * k));
-            bam->cig_off.push_back((int64_t)bam->cigar.size());
-        }
+        kept_off[g + 1] = kept_off[g] + sc[g].kept;
+        word_off[g + 1] = word_off[g] + sc[g].words;
+        bam->n_mapped += sc[g].mapped;
+        bam->n_records += sc[g].records;
+        bam->n_unmapped += sc[g].unmapped;
     }
+    bam->tid.resize(kept_off[nseg]);
+    bam->pos.resize(kept_off[nseg]);
+    bam->span.resize(kept_off[nseg]);
+    if (bam->keep_cigar) {
+        bam->cigar.resize(word_off[nseg]);
+        bam->cig_off.assign(kept_off[nseg] + 1, 0);
+    }
+    run_pass(1);
+    lap("fill");
+    for (size_t g = 0; g < nseg; ++g)
+        if (sc[g].err) return fail("reference span exceeds int32", sc[g].err_at);
     *out = bam;
     return MC_OK;
 }

@@ -1,0 +1,152 @@
+// BAM writer for synthetic workloads (the role `metacov simulate` plays in
+// the reference, metacov/cli.py:288-414, without ART): records from SoA
+// arrays, BGZF blocks deflated in parallel (each block is independent).
+// Sequence bases are 'A', qualities 30, names "r<index>".
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/metacov_amd.h"
+#include "common.h"
+
+namespace {
+
+inline void put32(std::vector<uint8_t>& b, uint32_t v) {
+    b.push_back(v & 0xff);
+    b.push_back((v >> 8) & 0xff);
+    b.push_back((v >> 16) & 0xff);
+    b.push_back((v >> 24) & 0xff);
+}
+inline void put16(std::vector<uint8_t>& b, uint16_t v) {
+    b.push_back(v & 0xff);
+    b.push_back((v >> 8) & 0xff);
+}
+
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+// one BGZF block (header + raw deflate + crc + isize) for <= 65280 bytes
+bool bgzf_block(const uint8_t* src, size_t n, int level, std::vector<uint8_t>& out) {
+    out.resize(18 + compressBound((uLong)n) + 8 + 64);
+    z_stream zs;
+    std::memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    zs.next_in = const_cast<Bytef*>(src);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out.data() + 18;
+    zs.avail_out = (uInt)(out.size() - 26);
+    const int rc = deflate(&zs, Z_FINISH);
+    const size_t clen = zs.total_out;
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) return false;
+    const size_t bsize = clen + 26;
+    const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
+                             (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
+    std::memcpy(out.data(), hdr, 18);
+    const uint32_t crc = (uint32_t)crc32(0L, src, (uInt)n);
+    uint8_t* t = out.data() + 18 + clen;
+    for (int i = 0; i < 4; ++i) t[i] = (crc >> (8 * i)) & 0xff;
+    for (int i = 0; i < 4; ++i) t[4 + i] = ((uint32_t)n >> (8 * i)) & 0xff;
+    out.resize(bsize);
+    return true;
+}
+
+}  // namespace
+
+extern "C" int mc_bam_write(const char* path, int32_t n_ref, const char* const* names,
+                            const int64_t* lengths, int64_t n, const int32_t* tid,
+                            const int32_t* pos, const uint16_t* flag, const int64_t* cig_off,
+                            const uint32_t* cigar, int32_t l_seq, int level, int n_threads) {
+    MC_REQUIRE(path && (n_ref == 0 || (names && lengths)), MC_E_INVALID, "null argument");
+    MC_REQUIRE(n == 0 || (tid && pos && flag && cig_off), MC_E_INVALID, "null record array");
+    MC_REQUIRE(l_seq >= 0 && l_seq < (1 << 20), MC_E_INVALID, "bad l_seq");
+    // ---- serialise header + records (uncompressed stream)
+    std::vector<uint8_t> raw;
+    std::string text = "@HD\tVN:1.6\tSO:coordinate\n";
+    for (int32_t i = 0; i < n_ref; ++i)
+        text += std::string("@SQ\tSN:") + names[i] + "\tLN:" + std::to_string(lengths[i]) + "\n";
+    raw.insert(raw.end(), {'B', 'A', 'M', 1});
+    put32(raw, (uint32_t)text.size());
+    raw.insert(raw.end(), text.begin(), text.end());
+    put32(raw, (uint32_t)n_ref);
+    for (int32_t i = 0; i < n_ref; ++i) {
+        const size_t ln = std::strlen(names[i]) + 1;
+        put32(raw, (uint32_t)ln);
+        raw.insert(raw.end(), names[i], names[i] + ln);
+        put32(raw, (uint32_t)lengths[i]);
+    }
+    const size_t seq_bytes = ((size_t)l_seq + 1) / 2;
+    char name[32];
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t c0 = cig_off[i], c1 = cig_off[i + 1];
+        MC_REQUIRE(c1 >= c0 && c1 - c0 < 65536, MC_E_INVALID, "record %lld: bad CIGAR range",
+                   (long long)i);
+        const int ln = std::snprintf(name, sizeof name, "r%lld", (long long)i) + 1;
+        int64_t rlen = 0;
+        for (int64_t k = c0; k < c1; ++k)
+            if ((0x18Du >> (cigar[k] & 0xF)) & 1u) rlen += cigar[k] >> 4;
+        const int64_t end = pos[i] + std::max<int64_t>(rlen, 1);
+        const uint32_t bin = tid[i] >= 0 ? (uint32_t)reg2bin(std::max(pos[i], 0), std::max<int64_t>(end, 1))
+                                         : 4680u;
+        const uint32_t block = 32 + ln + 4 * (uint32_t)(c1 - c0) + (uint32_t)seq_bytes + (uint32_t)l_seq;
+        put32(raw, block);
+        put32(raw, (uint32_t)tid[i]);
+        put32(raw, (uint32_t)pos[i]);
+        raw.push_back((uint8_t)ln);
+        raw.push_back(60);
+        put16(raw, (uint16_t)bin);
+        put16(raw, (uint16_t)(c1 - c0));
+        put16(raw, flag[i]);
+        put32(raw, (uint32_t)l_seq);
+        put32(raw, (uint32_t)tid[i]);
+        put32(raw, (uint32_t)pos[i]);
+        put32(raw, 0);
+        raw.insert(raw.end(), name, name + ln);
+        for (int64_t k = c0; k < c1; ++k) put32(raw, cigar[k]);
+        raw.insert(raw.end(), seq_bytes, (uint8_t)0x11);
+        raw.insert(raw.end(), (size_t)l_seq, (uint8_t)30);
+    }
+    // ---- deflate 65280-byte blocks in parallel, write in order
+    const size_t kBlk = 0xff00;
+    const size_t nblk = (raw.size() + kBlk - 1) / kBlk;
+    std::vector<std::vector<uint8_t>> out(nblk);
+    std::atomic<size_t> next{0};
+    std::atomic<bool> failed{false};
+    int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = std::max(1, std::min<int>(nt, (int)std::max<size_t>(nblk, 1)));
+    auto worker = [&]() {
+        for (size_t b; (b = next.fetch_add(1)) < nblk;) {
+            const size_t o = b * kBlk;
+            if (!bgzf_block(raw.data() + o, std::min(kBlk, raw.size() - o), level, out[b]))
+                failed = true;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
+    worker();
+    for (auto& t : pool) t.join();
+    MC_REQUIRE(!failed, MC_E_IO, "deflate failed");
+    FILE* f = std::fopen(path, "wb");
+    MC_REQUIRE(f, MC_E_IO, "cannot create %s", path);
+    bool ok = true;
+    for (auto& b : out) ok &= std::fwrite(b.data(), 1, b.size(), f) == b.size();
+    static const uint8_t kEof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67,
+                                     2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    ok &= std::fwrite(kEof, 1, 28, f) == 28;
+    ok &= std::fclose(f) == 0;
+    MC_REQUIRE(ok, MC_E_IO, "write to %s failed", path);
+    return MC_OK;
+}

@@ -21,6 +21,7 @@ Two forms are produced:
   (tid, pos, span) after the 0x704 filter, vectorised numpy, for the
   device benchmark (the spans follow the same edge mix).
 """
+import os
 import struct
 import zlib
 
@@ -239,3 +240,96 @@ def c3_workload(n_reads=100_000_000, n_contigs=1000, seed=42):
     rng = np.random.default_rng(seed + 1)
     weights = lengths * rng.lognormal(0.0, 1.0, size=n_contigs)
     return lengths, weights
+
+
+# --------------------------------------------------- vectorised large BAMs
+
+def edge_mix_arrays(lengths, n_reads, readlen=150, seed=1, weights=None):
+    """Coordinate-sorted records as arrays (tid, pos, flag, cig_off, cigar)
+    with the SURVEY §8(d) edge mix — vectorised, for BAMs of millions of
+    records written by `write_bam_fast`."""
+    rng = np.random.default_rng(seed)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    w = lengths.astype(np.float64) if weights is None else np.asarray(weights, np.float64)
+    counts = rng.multinomial(n_reads, w / w.sum())
+    tid = np.repeat(np.arange(len(lengths), dtype=np.int32), counts)
+    probs = _CATS.copy()
+    probs[_CAT_PLAIN] += probs[_CAT_ZERO]
+    probs[_CAT_ZERO] = 0
+    cat = rng.choice(len(probs), size=n_reads, p=probs / probs.sum())
+    nw = np.select([cat == _CAT_PLAIN, cat == _CAT_SOFT, cat == _CAT_UNMAP], [1, 2, 0], 3)
+    cig_off = np.zeros(n_reads + 1, np.int64)
+    np.cumsum(nw, out=cig_off[1:])
+    cigar = np.zeros(int(cig_off[-1]), np.uint32)
+    a = rng.integers(1, readlen - 10, size=n_reads)
+    x = rng.integers(1, 6, size=n_reads)
+    big = rng.integers(50, 2000, size=n_reads)
+    o = cig_off[:-1]
+
+    def put(mask, k, op, ln):
+        cigar[o[mask] + k] = (np.asarray(ln)[mask] if np.ndim(ln) else ln) << 4 | op
+
+    rl = np.full(n_reads, readlen, np.int64)
+    m = cat == _CAT_PLAIN
+    put(m, 0, M, readlen)
+    m = cat == _CAT_SOFT
+    put(m, 0, S, x)
+    put(m, 1, M, readlen - x)
+    rl[m] = readlen - x[m]
+    m = cat == _CAT_INS
+    put(m, 0, M, a)
+    put(m, 1, I, x)
+    put(m, 2, M, readlen - a - x)
+    rl[m] = readlen - x[m]
+    m = cat == _CAT_DEL
+    put(m, 0, M, a)
+    put(m, 1, D, x)
+    put(m, 2, M, readlen - a)
+    rl[m] = readlen + x[m]
+    m = cat == _CAT_SKIP
+    put(m, 0, M, a)
+    put(m, 1, N, big)
+    put(m, 2, M, readlen - a)
+    rl[m] = readlen + big[m]
+    m = cat == _CAT_EQX
+    put(m, 0, EQ, a)
+    put(m, 1, X, 1)
+    put(m, 2, EQ, readlen - a - 1)
+    L = lengths[tid]
+    pos = (rng.random(n_reads) * np.maximum(L - rl + 1, 1)).astype(np.int64)
+    flag = (0x1 | np.where(np.arange(n_reads) % 2 == 0, 0x40, 0x80)).astype(np.uint16)
+    flag[cat == _CAT_UNMAP] |= 0x4
+    u = rng.random(n_reads)
+    flag[u < 0.01] |= 0x100
+    flag[(u >= 0.01) & (u < 0.015)] |= 0x400
+    flag[(u >= 0.015) & (u < 0.017)] |= 0x200
+    flag[(u >= 0.017) & (u < 0.022)] |= 0x800
+    flag[rng.random(n_reads) < 0.5] |= 0x10
+    order = np.lexsort((pos, tid))
+    new_nw = nw[order]
+    new_off = np.zeros(n_reads + 1, np.int64)
+    np.cumsum(new_nw, out=new_off[1:])
+    # gather each read's words in the new order
+    src = np.repeat(cig_off[:-1][order], new_nw) + (np.arange(int(new_off[-1])) -
+                                                    np.repeat(new_off[:-1], new_nw))
+    return (tid[order], pos[order].astype(np.int32), flag[order], new_off, cigar[src])
+
+
+def write_bam_fast(path, names, lengths, tid, pos, flag, cig_off, cigar, l_seq=150, level=1,
+                   n_threads=0):
+    """BAM from record arrays through the library's C++ writer (mc_bam_write)."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    enc = [n.encode() for n in names]
+    arr = (ctypes.c_char_p * len(enc))(*enc)
+    lengths = np.ascontiguousarray(lengths, np.int64)
+    tid = np.ascontiguousarray(tid, np.int32)
+    pos = np.ascontiguousarray(pos, np.int32)
+    flag = np.ascontiguousarray(flag, np.uint16)
+    cig_off = np.ascontiguousarray(cig_off, np.int64)
+    cigar = np.ascontiguousarray(cigar, np.uint32)
+    _lib.check(lib.mc_bam_write(os.fspath(path).encode(), len(enc), ctypes.cast(arr, ctypes.c_void_p),
+                                _lib.ptr(lengths), len(tid), _lib.ptr(tid), _lib.ptr(pos),
+                                _lib.ptr(flag), _lib.ptr(cig_off), _lib.ptr(cigar), int(l_seq),
+                                int(level), int(n_threads)))

@@ -1,0 +1,67 @@
+"""End-to-end `metacov pileup` timing on a synthetic BAM (host decode + GPU).
+
+    python scripts/e2e.py [--reads 10000000 --contigs 1 --length 5000000]
+
+Writes an edge-mix BAM with the library's writer, then times the phases of
+the CLI path: C++ decode (BGZF inflate + parse, all host threads), ingest
+(H2D + prepare), fused depth + statistics on the GPU, CSV formatting.
+Prints one JSON line.
+"""
+import argparse
+import io
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--contigs", type=int, default=1)
+    ap.add_argument("--length", type=int, default=5_000_000, help="bp per contig")
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--dir", default=None)
+    a = ap.parse_args()
+    import numpy as np
+    from metacov_amd import synth, regions as mreg
+    from metacov_amd.bam import BamFile
+    from metacov_amd.cli import write_rows
+
+    lengths = np.full(a.contigs, a.length, np.int64)
+    names = ["contig_%d" % i for i in range(a.contigs)]
+    d = a.dir or tempfile.mkdtemp()
+    path = os.path.join(d, "e2e.bam")
+    t0 = time.perf_counter()
+    arrs = synth.edge_mix_arrays(lengths, a.reads, seed=1)
+    synth.write_bam_fast(path, names, lengths, *arrs, level=6, n_threads=a.threads)
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    bam = BamFile(path, n_threads=a.threads)
+    t_dec = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    eng = bam.engine(0, compute=False)
+    t_ing = time.perf_counter() - t0
+    regs = list(mreg.get_regions_from_bam(bam))
+    t0 = time.perf_counter()
+    out = io.StringIO()
+    write_rows(bam, regs, out)
+    t_cmp = time.perf_counter() - t0
+    bases = bam.aligned_bases()
+    tot = t_dec + t_ing + t_cmp
+    print(json.dumps({
+        "bam_bytes": os.path.getsize(path), "records": bam.n_records, "kept": len(bam.tid),
+        "aligned_bases": bases, "host_threads": a.threads,
+        "decode_s": t_dec, "ingest_h2d_prepare_s": t_ing, "gpu_stats_csv_s": t_cmp,
+        "end_to_end_s": tot, "end_to_end_aligned_bases_per_s": bases / tot,
+        "decode_records_per_s": bam.n_records / t_dec, "generate_write_s": t_gen,
+        "timings": eng.timings()}))
+    os.remove(path)
+
+
+if __name__ == "__main__":
+    main()

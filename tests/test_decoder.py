@@ -79,3 +79,22 @@ def test_errors(lib_built, tmp_path, golden_dir):
     t.write_bytes(raw[: len(raw) // 2])
     with pytest.raises(MetacovError):
         BamFile(str(t))
+
+
+def test_parallel_boundaries_large(lib_built, tmp_path):
+    """2M records through the C++ writer: every thread count decodes the same
+    intervals (parallel record-boundary sync + two-pass parse)."""
+    lengths = [3_000_000, 1_000, 900_000]
+    arrs = synth.edge_mix_arrays(lengths, 2_000_000, seed=11)
+    p = str(tmp_path / "big.bam")
+    synth.write_bam_fast(p, ["x", "y", "z"], lengths, *arrs, level=1, n_threads=4)
+    ref = BamFile(p, n_threads=1)
+    assert ref.n_records == 2_000_000
+    tid, pos, flag, cig_off, cigar = arrs
+    keep = (flag & 0x704) == 0
+    assert np.array_equal(ref.tid, tid[keep]) and np.array_equal(ref.pos, pos[keep])
+    for th in (2, 7, 16):
+        b = BamFile(p, n_threads=th)
+        assert b.n_records == ref.n_records and b.mapped == ref.mapped
+        for x, y in zip((ref.tid, ref.pos, ref.span), (b.tid, b.pos, b.span)):
+            assert np.array_equal(x, y)
