@@ -37,6 +37,9 @@ namespace mc {
 #ifndef MC_HIST_LDS
 #define MC_HIST_LDS 0                  // fused K2: histogram from LDS (16 positions/lane)
 #endif
+#ifndef MC_EXP_EPILOGUE
+#define MC_EXP_EPILOGUE 2              // experiments: 0 none, 1 touch values, 2 = real epilogue
+#endif
 #ifndef MC_CHUNK_PF
 #define MC_CHUNK_PF 0                  // dequeue the next chunk during the current one
 #endif
@@ -671,6 +674,14 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     }
                 }
                 __syncthreads();   // ring slots zeroed before the next tile's atomics
+            } else if (kStats && MC_EXP_EPILOGUE == 0) {
+                // experiment: no epilogue at all (isolates occupancy/regalloc)
+            } else if (kStats && MC_EXP_EPILOGUE == 1) {
+                // experiment: keep the tile's values live, minimal work
+                int acc = 0;
+#pragma unroll
+                for (int j = 0; j < kChunks; ++j) acc += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+                asm volatile("" :: "v"(acc));
             } else if (kStats) {
                 // regions covering this tile, in order; the loop is uniform.
                 // Only the value histogram is built here (runs of equal values
