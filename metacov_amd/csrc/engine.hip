@@ -650,18 +650,17 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
             if (lds_hist)
                 hipLaunchKernelGGL(region_seg_kernel<true>, dim3((unsigned)nseg), dim3(kBlock),
                                    (size_t)nbins * 4, s, ctx->d_depth.p, ctx->d_seg_gs.p,
-                                   ctx->d_seg_ge.p, ctx->d_seg_reg.p, nbins, ctx->d_hist.p,
-                                   ctx->d_acc.p);
+                                   ctx->d_seg_ge.p, ctx->d_seg_reg.p, nbins, ctx->d_hist.p);
             else
                 hipLaunchKernelGGL(region_seg_kernel<false>, dim3((unsigned)nseg), dim3(kBlock), 0,
                                    s, ctx->d_depth.p, ctx->d_seg_gs.p, ctx->d_seg_ge.p,
-                                   ctx->d_seg_reg.p, nbins, ctx->d_hist.p, ctx->d_acc.p);
+                                   ctx->d_seg_reg.p, nbins, ctx->d_hist.p);
             HIP_TRY(hipGetLastError());
             ++launches;
         }
         hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)nr), dim3(kBlock), 0, s,
                            ctx->d_hist.p, nbins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p,
-                           d_out_final + r0, (int*)nullptr, 0, (const int32_t*)nullptr,
+                           d_out_final + r0, (int*)nullptr, 1, (const int32_t*)nullptr,
                            (const unsigned*)nullptr);
         HIP_TRY(hipGetLastError());
         // the host vectors die at scope end: finish the copies first

@@ -762,53 +762,52 @@ region_init_kernel(RegionAcc* __restrict__ acc, int64_t R) {
 }
 
 // One workgroup per segment (<= kSeg positions of one region, clipped to
-// the contig extent).  int4 loads, masked at the unaligned ends.
+// the contig extent).  Builds the value histogram only (bins 0..nbins-1 cover
+// every depth: nbins = max depth + 1); region_final_kernel derives min, max,
+// sum and sum of squares from it.  Each thread keeps 4 int4 loads in flight;
+// runs of equal values within an int4 share one atomic.
 template <bool kLdsHist>
 __global__ void __launch_bounds__(kBlock)
 region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__ seg_gs,
                   const int64_t* __restrict__ seg_ge, const int32_t* __restrict__ seg_reg,
-                  int nbins, unsigned* __restrict__ hist, RegionAcc* __restrict__ acc) {
+                  int nbins, unsigned* __restrict__ hist) {
     extern __shared__ __attribute__((aligned(16))) unsigned h[];
     const int64_t sgi = blockIdx.x;
     const int64_t gs = seg_gs[sgi], ge = seg_ge[sgi];
     const int r = seg_reg[sgi];
-    const int lane = threadIdx.x & 63;
     unsigned* ghist = hist + (int64_t)r * nbins;
+    unsigned* hh = kLdsHist ? h : ghist;
     if (kLdsHist) {
         for (int k = threadIdx.x; k < nbins; k += kBlock) h[k] = 0;
         __syncthreads();
     }
-    long long sum = 0;
-    unsigned long long sumsq = 0;
-    int vmin = 0x7fffffff, vmax = 0;
+    constexpr int kU = 4;                                // int4 loads in flight per thread
     const int64_t a4 = gs & ~(int64_t)3;
-    for (int64_t p = a4 + (int64_t)threadIdx.x * 4; p < ge; p += kBlock * 4) {
-        const i32x4 x4 = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(depth + p));
-        const int xs[4] = {x4.x, x4.y, x4.z, x4.w};
+    for (int64_t p0 = a4 + (int64_t)threadIdx.x * 4; p0 < ge; p0 += (int64_t)kBlock * 4 * kU) {
+        i32x4 x[kU];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (p + k >= gs && p + k < ge) {
-                const int v = xs[k];
-                sum += v;
-                sumsq += (unsigned long long)((long long)v * v);
-                vmin = min(vmin, v);
-                vmax = max(vmax, v);
-                if (kLdsHist) atomicAdd(&h[v], 1u);
-                else atomicAdd(&ghist[v], 1u);
-            }
+        for (int u = 0; u < kU; ++u) {
+            const int64_t p = p0 + (int64_t)u * kBlock * 4;
+            x[u] = p < ge ? __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(depth + p))
+                          : i32x4{-1, -1, -1, -1};
         }
-    }
-    sum = wave_sum64(sum);
-    unsigned long long sq = sumsq;
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) sq += __shfl_xor(sq, d, 64);
-    vmin = wave_min(vmin);
-    vmax = wave_max(vmax);
-    if (lane == 0) {
-        atomicAdd(&acc[r].sum, (unsigned long long)sum);
-        atomicAdd(&acc[r].sumsq, sq);
-        atomicMin(&acc[r].min, vmin);
-        atomicMax(&acc[r].max, vmax);
+        for (int u = 0; u < kU; ++u) {
+            const int64_t p = p0 + (int64_t)u * kBlock * 4;
+            // positions outside [gs, ge) become -1 and are skipped
+            const int y0 = (p >= gs && p < ge) ? x[u].x : -1;
+            const int y1 = (p + 1 >= gs && p + 1 < ge) ? x[u].y : -1;
+            const int y2 = (p + 2 >= gs && p + 2 < ge) ? x[u].z : -1;
+            const int y3 = (p + 3 >= gs && p + 3 < ge) ? x[u].w : -1;
+            const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
+            const int l2 = s3 ? 1 : 2;
+            const int l1 = s2 ? 1 : l2 + 1;
+            const int l0 = s1 ? 1 : l1 + 1;
+            if (y0 >= 0) atomicAdd(&hh[y0], (unsigned)l0);
+            if (s1 && y1 >= 0) atomicAdd(&hh[y1], (unsigned)l1);
+            if (s2 && y2 >= 0) atomicAdd(&hh[y2], (unsigned)l2);
+            if (s3 && y3 >= 0) atomicAdd(&hh[y3], 1u);
+        }
     }
     if (kLdsHist) {
         __syncthreads();
