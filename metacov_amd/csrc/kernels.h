@@ -37,6 +37,9 @@ namespace mc {
 #ifndef MC_HIST_LDS
 #define MC_HIST_LDS 0                  // fused K2: histogram from LDS (16 positions/lane)
 #endif
+#ifndef MC_NT_STORE
+#define MC_NT_STORE 1                  // non-temporal depth stores (written once, not re-read soon)
+#endif
 #ifndef MC_EXP_EPILOGUE
 #define MC_EXP_EPILOGUE 2              // experiments: 0 none, 1 touch values, 2 = real epilogue
 #endif
@@ -619,7 +622,10 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 i32x4 x = v[j] + off;
                 v[j] = x;
                 my_max = max(my_max, max(max(x.x, x.y), max(x.z, x.w)));
-                __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
+                if (MC_NT_STORE)
+                    __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
+                else
+                    *reinterpret_cast<i32x4*>(dst + j * 256) = x;
                 if (kStats && MC_HIST_LDS)
                     *reinterpret_cast<i32x4*>(ring + ring_slot(sb + j * 256) + lane * 4) = x;
             }

@@ -407,3 +407,42 @@ def test_fused_window_follows_mean_depth(eng):
     for f in want.dtype.names:
         assert np.array_equal(got[f], want[f]), f
     assert eng.fused_fallbacks() == 0
+
+
+def test_cli_csv_regions_and_batch_api(lib_built, fixture_golden, golden_dir, tmp_path):
+    """-rc CSV regions (values stay strings, util.py:61) and classic_batch."""
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    from metacov_amd import pileup
+    bam = os.path.join(golden_dir, "bbmap.sorted.bam")
+    rc = tmp_path / "r.csv"
+    rc.write_text("sequence_id,start,stop\nref1,1,425\nref2,575,1\n")
+    res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rc", str(rc), "-o", str(tmp_path / "o.csv")])
+    assert res.exit_code == 0, res.output
+    lines = open(tmp_path / "o.csv", newline="").read().split("\r\n")
+    b7 = {(r["sacc"], r["start"], r["end"]): r["stats"] for r in fixture_golden["blast7"]}
+    s = b7[("ref1", 1, 425)]
+    assert lines[1] == "ref1,1,425,%r,%d,%d,%d,%r,%r,%d" % (s["avg"], s["max"], s["med"], s["min"],
+                                                             s["q23"], s["std"], s["sum"])
+    assert lines[2].startswith("ref2,575,1,")          # raw (unsorted) start/end echoed
+    regs = [("ref1", 1, 425), ("ref2", 1, 575), ("ref2", 1, 300), ("ref2", 301, 575)]
+    got = pileup.classic_batch(bam, regs)
+    assert got == [b7[r] for r in regs]
+    with pytest.raises(KeyError):
+        pileup.classic_batch(bam, [("nope", 0, 5)])
+
+
+def test_external_stream(lib_built):
+    """mc_ctx_set_stream: the ctx runs on torch's current stream."""
+    import torch
+    eng = CoverageEngine(0)
+    s = torch.cuda.Stream()
+    eng.set_stream(s.cuda_stream)
+    lengths, tid, pos, span = make_case([70_000], 5_000, (1, 150), 13)
+    run_engine(eng, lengths, tid, pos, span)
+    d, _, _ = coracle.depth(lengths, tid, pos, span)
+    assert np.array_equal(eng.depth(0, 0, len(d)), d)
+    eng.set_stream(None)
+    eng.compute_depth()
+    assert np.array_equal(eng.depth(0, 0, len(d)), d)
+    eng.close()

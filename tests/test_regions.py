@@ -46,3 +46,15 @@ def test_whole_contigs_and_exclusive():
     import click
     with pytest.raises(click.BadParameter):
         regions.make_region_iterator(io.StringIO(""), io.StringIO(""), B())
+
+
+def test_cli_rejects_kmer_histogram(tmp_path, golden_dir):
+    """-k (pileup.experimental) is outside this build: a usage error, before
+    any GPU work (runs on CPU)."""
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup
+    k = tmp_path / "k.csv"
+    k.write_text("kmer,n\n")
+    res = CliRunner().invoke(pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
+                                      "-k", str(k), "-o", str(tmp_path / "o.csv")])
+    assert res.exit_code == 2 and "kmer-histogram" in res.output
