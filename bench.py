@@ -41,6 +41,9 @@ def parse():
                     help="aligned bases in the CPU-baseline sample (~10-20 s on one core)")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer ingest (H2D)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -140,10 +143,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
     d_reads, d_contigs, desc = CONFIGS[args.config]
     args.reads = args.reads or d_reads
@@ -196,7 +204,8 @@ def main():
             local_tab = torch.cat([table, idx[:, None]], 1)
             buf = torch.full((r_max, mdist.ROW_WIDTH), -1, dtype=torch.int64, device=dev)
             buf[:R] = local_tab
-            out = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=dev)
+            buf = buf.to(coll_dev)
+            out = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=coll_dev)
             dist.all_gather_into_tensor(out, buf)
             gathered = out
 
@@ -221,10 +230,10 @@ def main():
     t_max = elapsed
     total_bases = bases
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
-        b = torch.tensor([bases], dtype=torch.int64, device=dev)
+        b = torch.tensor([bases], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(b)
         total_bases = int(b.item())
         rows = mdist.unpack_rows(gathered.cpu().numpy(), n_regions_total, REGION_STAT_DTYPE)
@@ -242,7 +251,7 @@ def main():
     pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
     traffic = None
     variant = "depth_kernel<%s>" % ("false" if args.unfused else "true")
-    for v in (pmc or {}).get("variants", []):
+    for v in ([] if args.strong else (pmc or {}).get("variants", [])):   # PMC of the per-GPU workload
         if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
                 and variant in v.get("kernel", ""):
             traffic = v.get("hbm_bytes_per_launch")
@@ -288,7 +297,8 @@ def main():
                 "reads_per_gpu": int(len(tid)),
                 "aligned_bases_per_step": int(total_bases),
                 "regions": n_regions_total,
-                "parallelism": "contig-shard x%d, RCCL all-gather of region table" % world
+                "parallelism": ("contig-shard x%d, %s all-gather of region table"
+                                % (world, "RCCL" if args.backend == "nccl" else "gloo"))
                                if world > 1 else "single GPU",
             },
             "kernels_ms": {"k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
