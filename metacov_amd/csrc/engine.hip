@@ -61,6 +61,35 @@ struct DevBuf {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Per-call host arrays go up in ONE copy from a pinned buffer (a pageable
+// hipMemcpyAsync per array costs a staging round trip each).  The caller
+// synchronises the stream before the next reuse.
+struct Stage {
+    void* h = nullptr;
+    size_t cap = 0;
+    DevBuf<unsigned char> d;
+    hipError_t reserve(size_t n) {
+        if (n > cap) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+            cap = 0;
+            hipError_t e = hipHostMalloc(&h, n, hipHostMallocDefault);
+            if (e != hipSuccess) return e;
+            cap = n;
+        }
+        return d.reserve(n);
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = nullptr;
+        cap = 0;
+        d.release();
+    }
+    unsigned char* host() const { return static_cast<unsigned char*>(h); }
+};
+
+inline size_t stage_align(size_t x) { return (x + 255) & ~size_t(255); }
+
 }  // namespace
 
 struct mc_ctx {
@@ -104,16 +133,15 @@ struct mc_ctx {
     DevBuf<unsigned> d_queue;
     DevBuf<int> d_maxdepth;
     // K3 scratch
-    DevBuf<int64_t> d_seg_gs, d_seg_ge, d_ntot, d_nzx;
-    DevBuf<int32_t> d_seg_reg;
+    Stage k3_stage;                       // segments + per-region counts
     DevBuf<unsigned> d_hist;
     DevBuf<RegionAcc> d_acc;
     DevBuf<RegionOut> d_out;
     // fused K2 statistics
-    DevBuf<int64_t> d_fgs, d_fge, d_fchunk;
-    DevBuf<int32_t> d_fid, d_fbase, d_fbase_row;
+    DevBuf<int64_t> d_fchunk;
+    Stage fstage;                         // per-call region arrays + returned flags
     DevBuf<unsigned> d_flow;
-    DevBuf<unsigned> d_fhist, d_fover;
+    DevBuf<unsigned> d_fhist;
     DevBuf<int> d_fflag;
     int64_t fused_fallbacks = 0;
 
@@ -185,23 +213,14 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_cbases.release();
     ctx->d_queue.release();
     ctx->d_maxdepth.release();
-    ctx->d_seg_gs.release();
-    ctx->d_seg_ge.release();
-    ctx->d_ntot.release();
-    ctx->d_nzx.release();
-    ctx->d_seg_reg.release();
+    ctx->k3_stage.release();
     ctx->d_hist.release();
     ctx->d_acc.release();
     ctx->d_out.release();
-    ctx->d_fgs.release();
     ctx->d_fchunk.release();
-    ctx->d_fge.release();
-    ctx->d_fid.release();
-    ctx->d_fbase.release();
-    ctx->d_fbase_row.release();
+    ctx->fstage.release();
     ctx->d_flow.release();
     ctx->d_fhist.release();
-    ctx->d_fover.release();
     ctx->d_fflag.release();
     for (auto ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -628,42 +647,53 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
             }
         }
         const int64_t nseg = (int64_t)sg_gs.size();
-        HIP_TRY(ctx->d_seg_gs.reserve(std::max<int64_t>(nseg, 1)));
-        HIP_TRY(ctx->d_seg_ge.reserve(std::max<int64_t>(nseg, 1)));
-        HIP_TRY(ctx->d_seg_reg.reserve(std::max<int64_t>(nseg, 1)));
-        HIP_TRY(ctx->d_ntot.reserve(nr));
-        HIP_TRY(ctx->d_nzx.reserve(nr));
-        HIP_TRY(ctx->d_hist.reserve((size_t)(nr * nbins)));
+        const size_t o_gs = 0, o_ge = o_gs + stage_align(nseg * 8),
+                     o_reg = o_ge + stage_align(nseg * 8), o_ntot = o_reg + stage_align(nseg * 4),
+                     o_nzx = o_ntot + stage_align(nr * 8), total = o_nzx + stage_align(nr * 8);
+        HIP_TRY(ctx->k3_stage.reserve(total));
+        unsigned char* h = ctx->k3_stage.host();
+        std::memcpy(h + o_gs, sg_gs.data(), nseg * 8);
+        std::memcpy(h + o_ge, sg_ge.data(), nseg * 8);
+        std::memcpy(h + o_reg, sg_reg.data(), nseg * 4);
+        std::memcpy(h + o_ntot, ntot.data(), nr * 8);
+        std::memcpy(h + o_nzx, nzx.data(), nr * 8);
+        unsigned char* d = ctx->k3_stage.d.p;
+        const int64_t* d_seg_gs = reinterpret_cast<const int64_t*>(d + o_gs);
+        const int64_t* d_seg_ge = reinterpret_cast<const int64_t*>(d + o_ge);
+        const int32_t* d_seg_reg = reinterpret_cast<const int32_t*>(d + o_reg);
+        HIP_TRY(ctx->d_hist.reserve((size_t)round_up(nr * nbins, 4)));
         HIP_TRY(ctx->d_acc.reserve(nr));
-        if (nseg) {
-            HIP_TRY(hipMemcpyAsync(ctx->d_seg_gs.p, sg_gs.data(), nseg * 8, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipMemcpyAsync(ctx->d_seg_ge.p, sg_ge.data(), nseg * 8, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipMemcpyAsync(ctx->d_seg_reg.p, sg_reg.data(), nseg * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s));
+        {
+            const int64_t hw = round_up(nr * nbins, 4);
+            const int64_t work = std::max<int64_t>(hw / 4, nr);
+            const unsigned g = (unsigned)std::min<int64_t>(4096, (work + kBlock - 1) / kBlock);
+            hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
+                               ctx->d_hist.p, hw, (unsigned*)nullptr, ctx->d_acc.p, nr,
+                               (const int64_t*)nullptr, (int64_t)0, (int64_t)1, (int64_t)0,
+                               (int64_t*)nullptr);
+            HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipMemcpyAsync(ctx->d_ntot.p, ntot.data(), nr * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(ctx->d_nzx.p, nzx.data(), nr * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(ctx->d_hist.p, 0, (size_t)(nr * nbins) * 4, s));
-        hipLaunchKernelGGL(region_init_kernel, dim3((unsigned)((nr + kBlock - 1) / kBlock)),
-                           dim3(kBlock), 0, s, ctx->d_acc.p, nr);
-        HIP_TRY(hipGetLastError());
         if (nseg) {
             if (lds_hist)
                 hipLaunchKernelGGL(region_seg_kernel<true>, dim3((unsigned)nseg), dim3(kBlock),
-                                   (size_t)nbins * 4, s, ctx->d_depth.p, ctx->d_seg_gs.p,
-                                   ctx->d_seg_ge.p, ctx->d_seg_reg.p, nbins, ctx->d_hist.p);
+                                   (size_t)nbins * 4, s, ctx->d_depth.p, d_seg_gs, d_seg_ge,
+                                   d_seg_reg, nbins, ctx->d_hist.p);
             else
                 hipLaunchKernelGGL(region_seg_kernel<false>, dim3((unsigned)nseg), dim3(kBlock), 0,
-                                   s, ctx->d_depth.p, ctx->d_seg_gs.p, ctx->d_seg_ge.p,
-                                   ctx->d_seg_reg.p, nbins, ctx->d_hist.p);
+                                   s, ctx->d_depth.p, d_seg_gs, d_seg_ge, d_seg_reg, nbins,
+                                   ctx->d_hist.p);
             HIP_TRY(hipGetLastError());
             ++launches;
         }
         hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)nr), dim3(kBlock), 0, s,
-                           ctx->d_hist.p, nbins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p,
+                           ctx->d_hist.p, nbins, ctx->d_acc.p,
+                           reinterpret_cast<const int64_t*>(d + o_ntot),
+                           reinterpret_cast<const int64_t*>(d + o_nzx),
                            d_out_final + r0, (int*)nullptr, 1, (const int32_t*)nullptr,
                            (const unsigned*)nullptr);
         HIP_TRY(hipGetLastError());
-        // the host vectors die at scope end: finish the copies first
+        // the staging buffer is reused by the next batch / call
         HIP_TRY(hipStreamSynchronize(s));
     }
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
@@ -714,62 +744,62 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     }
     hipStream_t s = ctx->stream;
     const int64_t nf = (int64_t)regs.size();
-    std::vector<int64_t> fgs(std::max<int64_t>(nf, 1)), fge(std::max<int64_t>(nf, 1));
-    std::vector<int32_t> fid(std::max<int64_t>(nf, 1)), fbase(std::max<int64_t>(nf, 1));
+    // every per-call array in one pinned buffer -> one H2D copy; the region
+    // flags come back through the same buffer
+    auto al = stage_align;
+    const size_t o_gs = 0, o_ge = o_gs + al(nf * 8), o_id = o_ge + al(nf * 8),
+                 o_base = o_id + al(nf * 4), o_ntot = o_base + al(nf * 4),
+                 o_nzx = o_ntot + al(R * 8), o_brow = o_nzx + al(R * 8), up = o_brow + al(R * 4),
+                 o_flag = up, total = up + al(R * 4);
+    HIP_TRY(ctx->fstage.reserve(total));
+    unsigned char* h = ctx->fstage.host();
     for (int64_t k = 0; k < nf; ++k) {
-        fgs[k] = regs[k].gs;
-        fge[k] = regs[k].ge;
-        fid[k] = regs[k].id;
-        fbase[k] = regs[k].base;
+        reinterpret_cast<int64_t*>(h + o_gs)[k] = regs[k].gs;
+        reinterpret_cast<int64_t*>(h + o_ge)[k] = regs[k].ge;
+        reinterpret_cast<int32_t*>(h + o_id)[k] = regs[k].id;
+        reinterpret_cast<int32_t*>(h + o_base)[k] = regs[k].base;
     }
-    // first region (sorted order) ending after each chunk start: a merge walk
-    std::vector<int64_t> fchunk(ctx->n_chunks);
-    for (int64_t c = 0, k = 0; c < ctx->n_chunks; ++c) {
-        const int64_t C0 = c * ctx->chunk_w;
-        while (k < nf && fge[k] <= C0) ++k;
-        fchunk[c] = k;
-    }
+    std::memcpy(h + o_ntot, ntot.data(), R * 8);
+    std::memcpy(h + o_nzx, nzx.data(), R * 8);
+    std::memcpy(h + o_brow, base_row.data(), R * 4);
     HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
-    HIP_TRY(hipMemcpyAsync(ctx->d_fchunk.p, fchunk.data(), ctx->n_chunks * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx->d_fgs.reserve(std::max<int64_t>(nf, 1)));
-    HIP_TRY(ctx->d_fge.reserve(std::max<int64_t>(nf, 1)));
-    HIP_TRY(ctx->d_fid.reserve(std::max<int64_t>(nf, 1)));
-    HIP_TRY(ctx->d_fbase.reserve(std::max<int64_t>(nf, 1)));
-    HIP_TRY(ctx->d_fbase_row.reserve(R));
     HIP_TRY(ctx->d_flow.reserve(R));
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
     HIP_TRY(ctx->d_fflag.reserve(R));
     HIP_TRY(ctx->d_acc.reserve(R));
-    HIP_TRY(ctx->d_ntot.reserve(R));
-    HIP_TRY(ctx->d_nzx.reserve(R));
-    if (nf) {
-        HIP_TRY(hipMemcpyAsync(ctx->d_fgs.p, fgs.data(), nf * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(ctx->d_fge.p, fge.data(), nf * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(ctx->d_fid.p, fid.data(), nf * 4, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(ctx->d_fbase.p, fbase.data(), nf * 4, hipMemcpyHostToDevice, s));
+    unsigned char* d = ctx->fstage.d.p;
+    HIP_TRY(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, s));
+    const int64_t* d_fge = reinterpret_cast<const int64_t*>(d + o_ge);
+    {
+        const int64_t work = std::max<int64_t>({R * kHistBins / 4, R, ctx->n_chunks});
+        const unsigned g = (unsigned)std::min<int64_t>(4096, (work + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
+                           ctx->d_fhist.p, R * kHistBins, ctx->d_flow.p, ctx->d_acc.p, R, d_fge, nf,
+                           ctx->chunk_w, ctx->n_chunks, ctx->d_fchunk.p);
+        HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipMemcpyAsync(ctx->d_ntot.p, ntot.data(), R * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->d_nzx.p, nzx.data(), R * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->d_fbase_row.p, base_row.data(), R * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(ctx->d_flow.p, 0, R * 4, s));
-    HIP_TRY(hipMemsetAsync(ctx->d_fhist.p, 0, (size_t)(R * kHistBins) * 4, s));
-    hipLaunchKernelGGL(region_init_kernel, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, s, ctx->d_acc.p, R);
-    HIP_TRY(hipGetLastError());
-    FusedRegions fr{nf, ctx->d_fchunk.p, ctx->d_fgs.p, ctx->d_fge.p, ctx->d_fid.p,
-                    ctx->d_fbase.p, ctx->d_acc.p, ctx->d_fhist.p, ctx->d_flow.p};
+    FusedRegions fr{nf,
+                    ctx->d_fchunk.p,
+                    reinterpret_cast<const int64_t*>(d + o_gs),
+                    d_fge,
+                    reinterpret_cast<const int32_t*>(d + o_id),
+                    reinterpret_cast<const int32_t*>(d + o_base),
+                    ctx->d_acc.p,
+                    ctx->d_fhist.p,
+                    ctx->d_flow.p};
     if (nf == 0) fr.n = 0;
     if (int rc = launch_depth(ctx, fr)) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[6], s));
     hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
-                       kHistBins, ctx->d_acc.p, ctx->d_ntot.p, ctx->d_nzx.p, d_out, ctx->d_fflag.p, 1,
-                       ctx->d_fbase_row.p, ctx->d_flow.p);
+                       kHistBins, ctx->d_acc.p, reinterpret_cast<const int64_t*>(d + o_ntot),
+                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->d_fflag.p, 1,
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
     ctx->t.stats_launches += 1;
-    std::vector<int> flags(R);
-    HIP_TRY(hipMemcpyAsync(flags.data(), ctx->d_fflag.p, R * 4, hipMemcpyDeviceToHost, s));
+    int* flags = reinterpret_cast<int*>(h + o_flag);
+    HIP_TRY(hipMemcpyAsync(flags, ctx->d_fflag.p, R * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::vector<int32_t> ft;
     std::vector<int64_t> fs, fe, fr_idx;

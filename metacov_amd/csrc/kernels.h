@@ -491,7 +491,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     OvAcc ovf;
     ovf.reset();
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform per wave
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
@@ -756,14 +756,34 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 
 // ----------------------------------------------------------------- K3
 
+// Statistics setup in one launch: zero the per-region histograms and
+// below-window counts (low may be null), initialise the accumulators, and build
+// chunk_first[c] = first region (sorted, non-overlapping: ge increasing)
+// whose end lies past the chunk start c * chunk_w.
 __global__ void __launch_bounds__(kBlock)
-region_init_kernel(RegionAcc* __restrict__ acc, int64_t R) {
-    const int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-    if (r < R) {
+fused_init_kernel(unsigned* __restrict__ hist, int64_t hist_words, unsigned* __restrict__ low,
+                  RegionAcc* __restrict__ acc, int64_t R, const int64_t* __restrict__ fge,
+                  int64_t nf, int64_t chunk_w, int64_t n_chunks, int64_t* __restrict__ chunk_first) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    for (int64_t q = i0; q * 4 < hist_words; q += stride)   // hist_words % 4 == 0
+        *reinterpret_cast<i32x4*>(hist + q * 4) = i32x4{0, 0, 0, 0};
+    for (int64_t r = i0; r < R; r += stride) {
+        if (low) low[r] = 0;
         acc[r].sum = 0;
         acc[r].sumsq = 0;
         acc[r].min = 0x7fffffff;
         acc[r].max = 0;
+    }
+    for (int64_t c = i0; c < n_chunks; c += stride) {
+        const int64_t C0 = c * chunk_w;
+        int64_t lo = 0, hi = nf;                  // upper_bound(fge, C0)
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (fge[mid] <= C0) lo = mid + 1;
+            else hi = mid;
+        }
+        chunk_first[c] = lo;
     }
 }
 
