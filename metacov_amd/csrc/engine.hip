@@ -516,7 +516,7 @@ static int occupancy_grid(const void* kernel, size_t lds, int64_t work, int* gri
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins : 0)) * 4;
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins + kOvInts : 0)) * 4;
     const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
     int grid = 0;
     if (int rc = occupancy_grid(kfn, lds, ctx->n_chunks, &grid)) return rc;

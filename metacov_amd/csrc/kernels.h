@@ -32,7 +32,7 @@ namespace mc {
 #define MC_PREFETCH 1                  // load read batch k+1 while applying batch k
 #endif
 #ifndef MC_PREFETCH_STATS
-#define MC_PREFETCH_STATS 0            // the same for the fused-statistics K2
+#define MC_PREFETCH_STATS 1            // the same for the fused-statistics K2
 #endif
 #ifndef MC_HIST_LDS
 #define MC_HIST_LDS 0                  // fused K2: histogram from LDS (16 positions/lane)
@@ -381,23 +381,35 @@ struct FusedRegions {
 };
 
 // Statistics of the values outside the histogram window of the current
-// region, per thread in registers (rare in the common case; reduced only when
-// a wave saw any).
-struct OvAcc {
+// region: one LDS record per workgroup behind the histogram, updated with LDS
+// atomics on the rare out-of-window path (no registers held for it).
+struct OvLds {
     unsigned long long sum, sq;
     int vmin, vmax;
     unsigned cnt, low;                 // values outside the window / below it
-    __device__ void reset() {
-        sum = sq = 0;
-        vmin = 0x7fffffff;
-        vmax = 0;
-        cnt = low = 0;
-    }
 };
+constexpr int kOvInts = sizeof(OvLds) / 4;
+
+__device__ __forceinline__ void ov_reset(OvLds* ov) {
+    ov->sum = ov->sq = 0;
+    ov->vmin = 0x7fffffff;
+    ov->vmax = 0;
+    ov->cnt = ov->low = 0;
+}
+
+// Statistics of one run of `cnt` positions of value v outside the window.
+__device__ __forceinline__ void ov_add(OvLds* ov, int v, int cnt, int base) {
+    atomicAdd(&ov->cnt, (unsigned)cnt);
+    if (v < base) atomicAdd(&ov->low, (unsigned)cnt);
+    atomicAdd(&ov->sum, (unsigned long long)v * (unsigned long long)cnt);
+    atomicAdd(&ov->sq, (unsigned long long)((long long)v * v) * (unsigned long long)cnt);
+    atomicMin(&ov->vmin, v);
+    atomicMax(&ov->vmax, v);
+}
 
 // One run of `cnt` positions of depth v: histogram bin v - base, or the
-// thread's overflow accumulator when v falls outside [base, base + kHistBins).
-__device__ __forceinline__ void emit_hist(unsigned* h, OvAcc& ov, int v, int cnt, int base) {
+// overflow record when v falls outside [base, base + kHistBins).
+__device__ __forceinline__ void emit_hist(unsigned* h, OvLds* ov, int v, int cnt, int base) {
     const int b = v - base;
 #ifdef MC_EXP_NO_HIST
     asm volatile("" :: "v"(b), "v"(cnt));
@@ -410,46 +422,57 @@ __device__ __forceinline__ void emit_hist(unsigned* h, OvAcc& ov, int v, int cnt
         atomicAdd(&h[b], (unsigned)cnt);
 #endif
     } else {
-        ov.cnt += cnt;
-        if (b < 0) ov.low += cnt;
-        ov.sum += (unsigned long long)v * (unsigned long long)cnt;
-        ov.sq += (unsigned long long)((long long)v * v) * (unsigned long long)cnt;
-        ov.vmin = min(ov.vmin, v);
-        ov.vmax = max(ov.vmax, v);
+        ov_add(ov, v, cnt, base);
+    }
+}
+
+// Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
+// one predicated LDS atomic per run of equal values, no branches except the
+// rare out-of-window path (same run arithmetic as region_seg_kernel).
+__device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1, int y2, int y3,
+                                          int base) {
+    const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
+    const int l2 = s3 ? 1 : 2;
+    const int l1 = s2 ? 1 : l2 + 1;
+    const int l0 = s1 ? 1 : l1 + 1;
+    const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
+    const unsigned b0 = (unsigned)(y0 - base), b1 = (unsigned)(y1 - base),
+                   b2 = (unsigned)(y2 - base), b3 = (unsigned)(y3 - base);
+    const bool w0 = e0 && b0 < (unsigned)kHistBins, w1 = e1 && b1 < (unsigned)kHistBins,
+               w2 = e2 && b2 < (unsigned)kHistBins, w3 = e3 && b3 < (unsigned)kHistBins;
+#ifdef MC_EXP_NO_HIST
+    asm volatile("" :: "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(l0), "v"(l1), "v"(l2));
+#else
+    if (w0) atomicAdd(&h[b0], (unsigned)l0);
+    if (w1) atomicAdd(&h[b1], (unsigned)l1);
+    if (w2) atomicAdd(&h[b2], (unsigned)l2);
+    if (w3) atomicAdd(&h[b3], 1u);
+#endif
+    if (__builtin_expect((e0 && !w0) || (e1 && !w1) || (e2 && !w2) || (e3 && !w3), 0)) {
+        if (e0 && !w0) ov_add(ov, y0, l0, base);
+        if (e1 && !w1) ov_add(ov, y1, l1, base);
+        if (e2 && !w2) ov_add(ov, y2, l2, base);
+        if (e3 && !w3) ov_add(ov, y3, 1, base);
     }
 }
 
 // Every thread calls it (it holds barriers): folds the overflow statistics
 // into the region's global accumulator and flushes the LDS histogram.
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
-                                             OvAcc& ov, int lane) {
+                                             OvLds* ov) {
 #ifdef MC_EXP_NO_FLUSH
     return;
 #endif
     const int id = R.id[r];
-    if (__any(ov.cnt != 0)) {
-        unsigned long long sum = ov.sum, sq = ov.sq;
-        unsigned cnt = ov.cnt, low = ov.low;
-        int vmin = ov.vmin, vmax = ov.vmax;
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) {
-            sum += __shfl_xor(sum, d, 64);
-            sq += __shfl_xor(sq, d, 64);
-            cnt += __shfl_xor(cnt, d, 64);
-            low += __shfl_xor(low, d, 64);
-            vmin = min(vmin, __shfl_xor(vmin, d, 64));
-            vmax = max(vmax, __shfl_xor(vmax, d, 64));
-        }
-        if (lane == 0 && cnt) {
-            if (low) atomicAdd(&R.low[id], low);
-            atomicMin(&R.acc[id].min, vmin);
-            atomicMax(&R.acc[id].max, vmax);
-            atomicAdd(&R.acc[id].sum, sum);
-            atomicAdd(&R.acc[id].sumsq, sq);
-        }
-        ov.reset();
+    __syncthreads();   // every wave's histogram and overflow atomics are in
+    if (threadIdx.x == 0 && ov->cnt) {
+        if (ov->low) atomicAdd(&R.low[id], ov->low);
+        atomicMin(&R.acc[id].min, ov->vmin);
+        atomicMax(&R.acc[id].max, ov->vmax);
+        atomicAdd(&R.acc[id].sum, ov->sum);
+        atomicAdd(&R.acc[id].sumsq, ov->sq);
+        ov_reset(ov);
     }
-    __syncthreads();
     unsigned* g = R.hist + (int64_t)id * kHistBins;
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
         const unsigned cnt = h[k];
@@ -488,8 +511,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     int* hdr = lds;                       // [0] chunk id, [1] region cursor, [4..7] wave totals
     int* ring = lds + kLdsHeader;
     unsigned* hist = reinterpret_cast<unsigned*>(ring + kRing);   // kStats only
-    OvAcc ovf;
-    ovf.reset();
+    OvLds* ovf = reinterpret_cast<OvLds*>(hist + kHistBins);           // kStats only
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform per wave
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
@@ -499,6 +521,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     int my_max = 0;
     if (kStats) {
         for (int k = threadIdx.x; k < kHistBins; k += kBlock) hist[k] = 0;
+        if (threadIdx.x == 0) ov_reset(ovf);   // ordered by the first barrier
     }
 
     // chunk ids come from an atomic queue; thread 0 fetches the next id (and
@@ -668,7 +691,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     }
                     if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
                     if (r_ge <= Tend) {
-                        flush_region(R, rcur, hist, ovf, lane);
+                        flush_region(R, rcur, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = R.gs[rcur];
@@ -701,25 +724,18 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     const bool full = lo == 0 && hi == kTileW;
 #pragma unroll
                     for (int j = 0; j < kChunks; ++j) {
-                        const int q0 = wave * kWaveSpan + j * 256 + lane * 4;
-                        const int xs[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-                        int run_v = xs[0], run_n = 0;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const bool in = full || (q0 + k >= lo && q0 + k < hi);
-                            const int x = xs[k];
-                            if (in && x == run_v) {
-                                ++run_n;
-                            } else if (in) {
-                                if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
-                                run_v = x;
-                                run_n = 1;
-                            }
+                        int y0 = v[j].x, y1 = v[j].y, y2 = v[j].z, y3 = v[j].w;
+                        if (!full) {   // positions outside [lo, hi) -> -1
+                            const int q0 = wave * kWaveSpan + j * 256 + lane * 4;
+                            y0 = (q0 >= lo && q0 < hi) ? y0 : -1;
+                            y1 = (q0 + 1 >= lo && q0 + 1 < hi) ? y1 : -1;
+                            y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
+                            y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
+                        hist_int4(hist, ovf, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
-                        flush_region(R, rcur, hist, ovf, lane);
+                        flush_region(R, rcur, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = R.gs[rcur];
@@ -734,7 +750,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         }
         if (kStats) {
             // a region still open at the chunk end has partials here
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, hist, ovf, lane);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, hist, ovf);
         }
         __syncthreads();   // everyone is past hdr / ring of this chunk
         if (threadIdx.x == 0) {
