@@ -178,6 +178,24 @@ int mc_bam_intervals(const mc_bam* bam, int32_t* tid, int32_t* pos, int32_t* spa
 int mc_bam_n_cigar_words(const mc_bam* bam, int64_t* n);
 int mc_bam_cigars(const mc_bam* bam, int64_t* cig_off, uint32_t* cigar);
 
+/* ---- BAI index ------------------------------------------------------------
+ * The reference opens an indexed BAM (`metacov pileup` needs `samtools
+ * index`: pysam AlignmentFile.pileup(ref, start, end) at pileup.py:13 is an
+ * indexed query; AlignmentFile.mapped / .unmapped at cli.py:58-66 read the
+ * index pseudo-bins).  mc_bam_index_build writes <bam>.bai (bai_path NULL)
+ * the way htslib's hts_idx_push / hts_idx_finish do.  mc_bam_open_contigs
+ * decodes only the records of the chosen contigs (one rank's shard) through
+ * the index: same intervals as mc_bam_open restricted to those tids (global
+ * tid values), whole-file mapped / unmapped counts from the index.
+ * mc_bam_index_stats: per-reference mapped / unmapped counts and the records
+ * without coordinates (sharding costs without a decode). */
+int mc_bam_index_build(const char* bam_path, const char* bai_path, int n_threads);
+int mc_bam_index_stats(const char* bai_path, int32_t n_ref, int64_t* n_mapped,
+                       int64_t* n_unmapped, int64_t* n_no_coor);
+int mc_bam_open_contigs(const char* path, const char* bai_path, int n_threads,
+                        uint32_t flag_filter, int keep_cigar, int32_t n_sel,
+                        const int32_t* sel, mc_bam** out);
+
 /* ---- synthetic BAM writer ------------------------------------------------
  * Writes coordinate-sorted records from SoA arrays as BGZF-compressed BAM
  * (blocks deflated on n_threads threads; level = zlib level).  The role of

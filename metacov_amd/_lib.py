@@ -86,6 +86,10 @@ SIGNATURES = {
     "mc_bam_intervals": [_P, _P, _P, _P],
     "mc_bam_n_cigar_words": [_P, _PI64],
     "mc_bam_cigars": [_P, _P, _P],
+    "mc_bam_index_build": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int],
+    "mc_bam_index_stats": [ctypes.c_char_p, _I32, _P, _P, _PI64],
+    "mc_bam_open_contigs": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _U32, ctypes.c_int, _I32,
+                            _P, _PP],
     "mc_bam_write": [ctypes.c_char_p, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _I32, ctypes.c_int,
                      ctypes.c_int],
 }

@@ -5,6 +5,11 @@ into coordinate-sorted pileup intervals and keeps the header.  It offers the
 parts of `pysam.AlignmentFile` the reference's pileup path touches:
 `references` / `lengths` (metacov/cli.py:80, metacov/util.py:64-69),
 `mapped` / `unmapped` (cli.py:67-76) and `filename`.
+
+`BamFile(path, contigs=[...])` decodes only those contigs' records through
+the BAI index (`<path>.bai`, or `index=`), the way one rank of a multi-GPU
+run reads its shard; `contigs=[]` reads the header and the index counts only.
+Its engine holds just those contigs (`local_tid` maps header ids to them).
 """
 import ctypes
 import os
@@ -17,17 +22,49 @@ from ._lib import check
 FLAG_FILTER = 0x704   # pysam pileup stepper "all": UNMAP|SECONDARY|QCFAIL|DUP
 
 
+def build_index(path, index=None, n_threads=0):
+    """Writes the BAI of a coordinate-sorted BAM (`samtools index`), by
+    default next to it as <path>.bai."""
+    lib = _lib.load()
+    check(lib.mc_bam_index_build(os.fspath(path).encode(),
+                                 os.fspath(index).encode() if index else None, int(n_threads)))
+    return os.fspath(index) if index else os.fspath(path) + ".bai"
+
+
+def index_stats(index, n_ref):
+    """Per-reference (mapped, unmapped) record counts and the records without
+    coordinates, from a BAI's pseudo-bins."""
+    lib = _lib.load()
+    m = np.zeros(n_ref, np.int64)
+    u = np.zeros(n_ref, np.int64)
+    nc = ctypes.c_int64()
+    check(lib.mc_bam_index_stats(os.fspath(index).encode(), int(n_ref), _lib.ptr(m), _lib.ptr(u),
+                                 ctypes.byref(nc)))
+    return m, u, nc.value
+
+
 class BamFile:
-    def __init__(self, path, n_threads=0, flag_filter=FLAG_FILTER, keep_cigar=False):
+    def __init__(self, path, n_threads=0, flag_filter=FLAG_FILTER, keep_cigar=False,
+                 contigs=None, index=None):
         if hasattr(path, "filename"):          # pysam.AlignmentFile
             path = path.filename
         if isinstance(path, bytes):
             path = path.decode()
         self.filename = os.fspath(path)
+        self.index = os.fspath(index) if index else None
         lib = _lib.load()
         h = ctypes.c_void_p()
-        check(lib.mc_bam_open(self.filename.encode(), int(n_threads), int(flag_filter),
-                              1 if keep_cigar else 0, ctypes.byref(h)))
+        if contigs is None:
+            self.contigs = None
+            check(lib.mc_bam_open(self.filename.encode(), int(n_threads), int(flag_filter),
+                                  1 if keep_cigar else 0, ctypes.byref(h)))
+        else:
+            self.contigs = np.unique(np.asarray(contigs, dtype=np.int32))
+            check(lib.mc_bam_open_contigs(self.filename.encode(),
+                                          self.index.encode() if self.index else None,
+                                          int(n_threads), int(flag_filter), 1 if keep_cigar else 0,
+                                          len(self.contigs), _lib.ptr(self.contigs),
+                                          ctypes.byref(h)))
         try:
             n = ctypes.c_int32()
             check(lib.mc_bam_n_targets(h, ctypes.byref(n)))
@@ -73,15 +110,50 @@ class BamFile:
     def aligned_bases(self):
         return int(self.span.astype(np.int64).sum())
 
+    def restrict(self, contigs):
+        """This file's records of `contigs` only, as a contig-shard BamFile
+        (the no-index fallback of a multi-GPU run: decode all, keep a shard)."""
+        out = object.__new__(BamFile)
+        out.__dict__.update(self.__dict__)
+        out.contigs = np.unique(np.asarray(contigs, dtype=np.int32))
+        keep = np.isin(self.tid, out.contigs)
+        out.tid, out.pos, out.span = self.tid[keep], self.pos[keep], self.span[keep]
+        if self.cig_off is not None:
+            idx = np.nonzero(keep)[0]
+            lens = (self.cig_off[idx + 1] - self.cig_off[idx]).astype(np.int64)
+            out.cig_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+            sel = np.concatenate([np.arange(self.cig_off[i], self.cig_off[i + 1]) for i in idx]) \
+                if len(idx) else np.zeros(0, np.int64)
+            out.cigar = self.cigar[sel]
+        out._engines = {}
+        return out
+
+    def local_tid(self, tid):
+        """Engine contig id of header contig id(s) `tid` (identity for a
+        whole-file BamFile; KeyError for a contig outside the shard)."""
+        if self.contigs is None:
+            return tid
+        t = np.asarray(tid, dtype=np.int64)
+        k = np.searchsorted(self.contigs, t)
+        if np.any(k >= len(self.contigs)) or np.any(self.contigs[np.minimum(k, len(self.contigs) - 1)] != t):
+            raise KeyError("contig outside this shard: %r" % (tid,))
+        return k.astype(np.int32) if t.ndim else int(k)
+
     def engine(self, device=0, compute=True):
         """A CoverageEngine holding this file's reads (cached per device);
-        with compute=True its depth is computed (once)."""
+        with compute=True its depth is computed (once).  A contig shard's
+        engine holds only its contigs (ids from local_tid)."""
         eng = self._engines.get(device)
         if eng is None:
             from .engine import CoverageEngine
             eng = CoverageEngine(device)
-            eng.set_contigs(np.asarray(self.lengths, dtype=np.int64))
-            eng.add_reads(self.tid, self.pos, self.span)
+            lengths = np.asarray(self.lengths, dtype=np.int64)
+            tid = self.tid
+            if self.contigs is not None:
+                lengths = lengths[self.contigs]
+                tid = np.searchsorted(self.contigs, self.tid).astype(np.int32)
+            eng.set_contigs(lengths)
+            eng.add_reads(tid, self.pos, self.span)
             eng.prepare()
             eng._depth_ready = False
             self._engines[device] = eng

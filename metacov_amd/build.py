@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmetacov_amd.so")
-SOURCES = ["engine.hip", "bam_decode.cpp", "bam_write.cpp", "common.cpp"]
+SOURCES = ["engine.hip", "bam_decode.cpp", "bam_index.cpp", "bam_write.cpp", "common.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

@@ -98,3 +98,88 @@ def test_parallel_boundaries_large(lib_built, tmp_path):
         assert b.n_records == ref.n_records and b.mapped == ref.mapped
         for x, y in zip((ref.tid, ref.pos, ref.span), (b.tid, b.pos, b.span)):
             assert np.array_equal(x, y)
+
+
+# ---- BAI index (mc_bam_index_build) and indexed contig decode ------------
+
+def _parse_bai(path):
+    """Test-side reader: {bin: chunks} (sorted; the pseudo-bin as stored),
+    the linear index per reference, and the no-coordinate count."""
+    import struct
+    d = open(path, "rb").read()
+    assert d[:4] == b"BAI\1"
+    o = 8
+    refs = []
+    for _ in range(struct.unpack_from("<i", d, 4)[0]):
+        n_bin, = struct.unpack_from("<i", d, o)
+        o += 4
+        bins = {}
+        for _ in range(n_bin):
+            b, nc = struct.unpack_from("<Ii", d, o)
+            o += 8
+            ch = [struct.unpack_from("<QQ", d, o + 16 * k) for k in range(nc)]
+            o += 16 * nc
+            bins[b] = ch if b == 37450 else sorted(ch)
+        n_intv, = struct.unpack_from("<i", d, o)
+        o += 4
+        refs.append((bins, list(struct.unpack_from("<%dQ" % n_intv, d, o))))
+        o += 8 * n_intv
+    return refs, struct.unpack_from("<Q", d, o)[0]
+
+
+def test_index_matches_reference_fixture(lib_built, golden_dir, tmp_path):
+    """Our index of the reference's test BAM equals the .bai its authors
+    shipped beside it (tests/data/bbmap.sorted.bam.bai, made by samtools)."""
+    import shutil
+    from metacov_amd.bam import build_index, index_stats
+    p = tmp_path / "f.bam"
+    shutil.copy(os.path.join(golden_dir, "bbmap.sorted.bam"), p)
+    ours = build_index(str(p))
+    assert _parse_bai(ours) == _parse_bai(os.path.join(golden_dir, "bbmap.sorted.bam.bai"))
+    m, u, nc = index_stats(os.path.join(golden_dir, "bbmap.sorted.bam.bai"), 2)
+    assert m.tolist() == [1694, 2285] and u.tolist() == [38, 91] and nc == 4
+
+
+def test_indexed_contig_decode(lib_built, tmp_path):
+    """BamFile(contigs=...) through the index == the full decode restricted to
+    those contigs; counts come from the index (pysam .mapped / .unmapped)."""
+    from metacov_amd.bam import build_index, index_stats
+    lengths = [3_000_000, 1_000, 900_000, 50_000, 2_000_000, 7]
+    arrs = synth.edge_mix_arrays(lengths, 600_000, seed=5)
+    p = str(tmp_path / "m.bam")
+    synth.write_bam_fast(p, ["c%d" % i for i in range(len(lengths))], lengths, *arrs, level=1,
+                         n_threads=4)
+    build_index(p)
+    full = BamFile(p, keep_cigar=True)
+    m, u, nc = index_stats(p + ".bai", len(lengths))
+    assert m.sum() == full.mapped and u.sum() + nc == full.unmapped
+    for sel in ([0], [4, 2], [5], [1, 3, 5], list(range(6)), []):
+        bf = BamFile(p, contigs=sel, n_threads=3, keep_cigar=True)
+        keep = np.isin(full.tid, sel)
+        for a, b in ((bf.tid, full.tid), (bf.pos, full.pos), (bf.span, full.span)):
+            assert np.array_equal(a, b[keep])
+        assert (bf.mapped, bf.unmapped, bf.references) == (full.mapped, full.unmapped,
+                                                            full.references)
+        r = full.restrict(sel)
+        assert np.array_equal(r.cigar, bf.cigar) and np.array_equal(r.cig_off, bf.cig_off)
+        if len(sel):
+            assert bf.local_tid(sorted(sel)[-1]) == len(set(sel)) - 1
+    with pytest.raises(KeyError):
+        BamFile(p, contigs=[1]).local_tid(0)
+
+
+def test_index_errors(lib_built, tmp_path, golden_dir):
+    with pytest.raises(MetacovError, match="bai"):
+        BamFile(os.path.join(golden_dir, "synth_multi.bam"), contigs=[0],
+                index=str(tmp_path / "none.bai"))
+    lengths = [10_000]
+    tid = np.zeros(3, np.int32)
+    pos = np.array([500, 100, 900], np.int32)          # not coordinate-sorted
+    flag = np.zeros(3, np.uint16)
+    cig_off = np.arange(4, dtype=np.int64)
+    cigar = np.full(3, (50 << 4) | 0, np.uint32)
+    p = str(tmp_path / "u.bam")
+    synth.write_bam_fast(p, ["a"], lengths, tid, pos, flag, cig_off, cigar, l_seq=50)
+    from metacov_amd.bam import build_index
+    with pytest.raises(MetacovError, match="coordinate-sorted"):
+        build_index(p)

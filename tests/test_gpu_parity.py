@@ -446,3 +446,41 @@ def test_external_stream(lib_built):
     eng.compute_depth()
     assert np.array_equal(eng.depth(0, 0, len(d)), d)
     eng.close()
+
+
+@pytest.mark.parametrize("indexed", [True, False])
+def test_cli_two_ranks(lib_built, golden_dir, tmp_path, indexed):
+    """`metacov pileup` on 2 ranks (torch.distributed.run, contig shards,
+    region-table all-gather; gloo so both ranks can share the box's one GPU)
+    writes byte-for-byte the CSV of one process — with the index (each rank
+    decodes only its contigs) and without (decode all, keep the shard)."""
+    import shutil
+    import socket
+    import subprocess
+    import sys
+    from click.testing import CliRunner
+    from metacov_amd.bam import build_index
+    from metacov_amd.cli import pileup as cli_pileup
+    bam = str(tmp_path / "m.bam")
+    shutil.copy(os.path.join(golden_dir, "synth_multi.bam"), bam)
+    if indexed:
+        build_index(bam)
+    rc = tmp_path / "r.csv"
+    rc.write_text("sequence_id,start,stop\ncontig_5,100,39000\ncontig_0,0,5000\ncontig_6,7000,10\n"
+                  "contig_2,5,6\ncontig_3,0,1\ncontig_5,0,40000\ncontig_1,0,300\n")
+    one = tmp_path / "one.csv"
+    res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rc", str(rc), "-o", str(one)])
+    assert res.exit_code == 0, res.output
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    two = tmp_path / "two.csv"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MC_DIST_BACKEND="gloo",
+               PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, "-m", "metacov_amd.cli", "pileup",
+           "-b", bam, "-rc", str(rc), "-o", str(two)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert open(two, newline="").read() == open(one, newline="").read()
