@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bases", type=float, default=3.0e9,
                     help="aligned bases in the CPU-baseline sample (~10-20 s on one core)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the contig-parallel CPU baseline (the box's CPU share)")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer ingest (H2D)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -103,7 +105,7 @@ def device_workload(torch, lengths, weights, n_reads, seed, dev, long_reads=Fals
             span[order].to(torch.int32).contiguous(), counts)
 
 
-def cpu_baseline(lengths, tid, pos, span, sample_bases):
+def cpu_baseline(lengths, tid, pos, span, sample_bases, label="C3"):
     """The C restatement of the reference's pileup.classic path (htslib-style
     column walk -> float64 columns -> sort-based stats) on one host core, on
     the first contigs of this workload up to `sample_bases` aligned bases."""
@@ -119,10 +121,28 @@ def cpu_baseline(lengths, tid, pos, span, sample_bases):
     dt = time.perf_counter() - t0
     bases = int(s.astype(np.int64).sum())
     return {"value": bases / dt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
-            "sample": "first %d of the rank-0 C3 contigs (%d bp, %d reads, %.3g aligned bases), "
+            "sample": "first %d of the rank-0 %s contigs (%d bp, %d reads, %.3g aligned bases), "
                       "whole-contig regions, %.2f s; oracle/oracle.c orc_pileup_classic "
                       "(restated htslib column walk + pileup.classic stats)"
-                      % (k, int(lengths[:k].sum()), len(t), bases, dt)}
+                      % (k, label, int(lengths[:k].sum()), len(t), bases, dt)}
+
+
+def cpu_baseline_parallel(lengths, tid, pos, span, sample_bases, threads):
+    """The same restatement and sample, contig-parallel on `threads` host
+    threads (SURVEY.md §8 d: the one-core and all-cores CPU baselines)."""
+    from oracle import coracle
+    per = np.bincount(tid, weights=span.astype(np.float64), minlength=len(lengths))
+    k = min(int(np.searchsorted(np.cumsum(per), sample_bases)) + 1, len(lengths))
+    m = tid < k
+    t, p, s = tid[m], pos[m], span[m]
+    t0 = time.perf_counter()
+    coracle.pileup_classic_parallel(t, p, s, np.arange(k, dtype=np.int32), np.zeros(k, np.int64),
+                                    lengths[:k].astype(np.int64), threads)
+    dt = time.perf_counter() - t0
+    bases = int(s.astype(np.int64).sum())
+    return {"value": bases / dt, "unit": "aligned bases/s", "cores": threads, "kind": "port",
+            "sample": "same %d contigs as cpu_baseline, contig-parallel on %d threads, %.2f s"
+                      % (k, threads, dt)}
 
 
 def load_pmc_traffic(root):
@@ -257,10 +277,13 @@ def main():
             traffic = v.get("hbm_bytes_per_launch")
 
     if rank == 0:
-        cpu = None
+        cpu = cpu_par = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(lengths, tid.cpu().numpy(), pos.cpu().numpy(),
-                               span.cpu().numpy(), args.cpu_sample_bases)
+            h = [x.cpu().numpy() for x in (tid, pos, span)]
+            cpu = cpu_baseline(lengths, *h, args.cpu_sample_bases, args.config.upper())
+            threads = min(args.cpu_threads, os.cpu_count() or 1)
+            cpu_par = cpu_baseline_parallel(lengths, *h, args.cpu_sample_bases, threads)
+            del h
         pcie = None
         if args.pcie and world == 1:
             h = [x.cpu().numpy() for x in (tid, pos, span)]
@@ -309,6 +332,7 @@ def main():
                          "kernel": "depth_kernel<%s> (K2)" % ("false" if args.unfused else "true"),
                          "algorithmic_bytes_per_launch": int(k2_bytes)},
             "cpu_baseline": cpu,
+            "cpu_baseline_parallel": cpu_par,
         }
         if pcie is not None:
             line["host_buffer_end_to_end_s"] = pcie

@@ -426,6 +426,47 @@ __device__ __forceinline__ void emit_hist(unsigned* h, OvLds* ov, int v, int cnt
     }
 }
 
+// The wave's runs outside the histogram window (contig ends, depth far from
+// the mean): reduced across the wave, then one lane updates the LDS record.
+// Out of line: its temporaries stay off the hot loop's register budget.
+// v < 0: no run in that slot.
+__device__ __attribute__((noinline, cold)) void ov_add_wave(OvLds* ov, int v0, int n0, int v1, int n1,
+                                                       int v2, int n2, int v3, int base) {
+    unsigned long long s = 0, q = 0;
+    unsigned c = 0, lo = 0;
+    int mn = 0x7fffffff, mx = 0;
+    auto take = [&](int v, int n) {
+        if (v < 0) return;
+        s += (unsigned long long)v * (unsigned long long)n;
+        q += (unsigned long long)((long long)v * v) * (unsigned long long)n;
+        c += n;
+        if (v < base) lo += n;
+        mn = min(mn, v);
+        mx = max(mx, v);
+    };
+    take(v0, n0);
+    take(v1, n1);
+    take(v2, n2);
+    take(v3, 1);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        s += __shfl_xor(s, d, 64);
+        q += __shfl_xor(q, d, 64);
+        c += __shfl_xor(c, d, 64);
+        lo += __shfl_xor(lo, d, 64);
+        mn = min(mn, __shfl_xor(mn, d, 64));
+        mx = max(mx, __shfl_xor(mx, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&ov->cnt, c);
+        if (lo) atomicAdd(&ov->low, lo);
+        atomicAdd(&ov->sum, s);
+        atomicAdd(&ov->sq, q);
+        atomicMin(&ov->vmin, mn);
+        atomicMax(&ov->vmax, mx);
+    }
+}
+
 // Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
 // one predicated LDS atomic per run of equal values, no branches except the
 // rare out-of-window path (same run arithmetic as region_seg_kernel).
@@ -448,12 +489,9 @@ __device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1
     if (w2) atomicAdd(&h[b2], (unsigned)l2);
     if (w3) atomicAdd(&h[b3], 1u);
 #endif
-    if (__builtin_expect((e0 && !w0) || (e1 && !w1) || (e2 && !w2) || (e3 && !w3), 0)) {
-        if (e0 && !w0) ov_add(ov, y0, l0, base);
-        if (e1 && !w1) ov_add(ov, y1, l1, base);
-        if (e2 && !w2) ov_add(ov, y2, l2, base);
-        if (e3 && !w3) ov_add(ov, y3, 1, base);
-    }
+    const bool o0 = e0 && !w0, o1 = e1 && !w1, o2 = e2 && !w2, o3 = e3 && !w3;
+    if (__builtin_expect(__any(o0 || o1 || o2 || o3), 0))
+        ov_add_wave(ov, o0 ? y0 : -1, l0, o1 ? y1 : -1, l1, o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
 }
 
 // Every thread calls it (it holds barriers): folds the overflow statistics

@@ -26,15 +26,17 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reads", type=int, default=100_000_000)
     ap.add_argument("--nocheck", action="store_true", help="deliberately-wrong experiment builds")
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"])
     a = ap.parse_args()
     import torch
-    from bench import device_workload
-    from metacov_amd import synth
+    from bench import CONFIGS, config_contigs, device_workload
     from metacov_amd.engine import CoverageEngine
 
     dev = torch.device("cuda", 0)
-    lengths, weights = synth.c3_workload(a.reads, 1000)
-    tid, pos, span, _ = device_workload(torch, lengths, weights, a.reads, 1, dev)
+    reads = a.reads if a.config == "c3" else CONFIGS[a.config][0]
+    lengths, weights = config_contigs(a.config, reads, CONFIGS[a.config][1])
+    tid, pos, span, _ = device_workload(torch, lengths, weights, reads, 1, dev,
+                                        long_reads=a.config == "c5")
     R = len(lengths)
     rt, rs, re_ = np.arange(R, dtype=np.int32), np.zeros(R, np.int64), lengths.astype(np.int64)
     engines = []

@@ -68,7 +68,8 @@ def main():
     path = os.path.join(prof, "pmc_depth_kernel.json")
     variants = []
     if os.path.exists(path):
-        variants = [v for v in json.load(open(path)).get("variants", []) if v["kernel"] != dk_name]
+        variants = [v for v in json.load(open(path)).get("variants", [])
+                    if (v["kernel"], v.get("reads"), v.get("contigs")) != (dk_name, a.reads, a.contigs)]
     with open(path, "w") as fh:
         json.dump({"variants": variants + [entry]}, fh, indent=1)
     for k, v in rows.items():

@@ -119,3 +119,21 @@ def test_pileup_classic_cpu_path(fixture_golden):
         assert (int(o[0]), int(o[1]), int(o[2]), int(o[6])) == (s["min"], s["max"], s["med"], s["sum"])
         for k, key in ((3, "std"), (4, "avg"), (5, "q23")):
             assert round(float(o[k]), 2) == s[key]
+
+
+def test_parallel_classic_equals_one_core():
+    """bench.py's contig-parallel CPU baseline computes the same rows."""
+    rng = np.random.default_rng(7)
+    lengths = rng.integers(1_000, 20_000, 12).astype(np.int64)
+    tid, pos, span = [], [], []
+    for t, L in enumerate(lengths):
+        n = int(L // 10)
+        pos.append(np.sort(rng.integers(0, L, n)).astype(np.int32))
+        tid.append(np.full(n, t, np.int32))
+        span.append(rng.integers(1, 300, n).astype(np.int32))
+    tid, pos, span = map(np.concatenate, (tid, pos, span))
+    R = len(lengths)
+    args = (tid, pos, span, np.arange(R, dtype=np.int32), np.zeros(R, np.int64), lengths)
+    a, ca = coracle.pileup_classic(*args)
+    b, cb = coracle.pileup_classic_parallel(*args, threads=5)
+    assert np.array_equal(a, b) and ca == cb
