@@ -678,11 +678,11 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
             if (lds_hist)
                 hipLaunchKernelGGL(region_seg_kernel<true>, dim3((unsigned)nseg), dim3(kBlock),
                                    (size_t)nbins * 4, s, ctx->d_depth.p, d_seg_gs, d_seg_ge,
-                                   d_seg_reg, nbins, ctx->d_hist.p);
+                                   d_seg_reg, nbins, ctx->d_hist.p, ctx->d_acc.p);
             else
                 hipLaunchKernelGGL(region_seg_kernel<false>, dim3((unsigned)nseg), dim3(kBlock), 0,
                                    s, ctx->d_depth.p, d_seg_gs, d_seg_ge, d_seg_reg, nbins,
-                                   ctx->d_hist.p);
+                                   ctx->d_hist.p, ctx->d_acc.p);
             HIP_TRY(hipGetLastError());
             ++launches;
         }
@@ -691,7 +691,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
                            reinterpret_cast<const int64_t*>(d + o_ntot),
                            reinterpret_cast<const int64_t*>(d + o_nzx),
                            d_out_final + r0, (int*)nullptr, 1, (const int32_t*)nullptr,
-                           (const unsigned*)nullptr);
+                           (const unsigned*)nullptr, 1);
         HIP_TRY(hipGetLastError());
         // the staging buffer is reused by the next batch / call
         HIP_TRY(hipStreamSynchronize(s));
@@ -793,7 +793,7 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
                        kHistBins, ctx->d_acc.p, reinterpret_cast<const int64_t*>(d + o_ntot),
                        reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->d_fflag.p, 1,
-                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p);
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p, 0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;

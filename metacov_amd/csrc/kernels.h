@@ -850,7 +850,7 @@ template <bool kLdsHist>
 __global__ void __launch_bounds__(kBlock)
 region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__ seg_gs,
                   const int64_t* __restrict__ seg_ge, const int32_t* __restrict__ seg_reg,
-                  int nbins, unsigned* __restrict__ hist) {
+                  int nbins, unsigned* __restrict__ hist, RegionAcc* __restrict__ acc) {
     extern __shared__ __attribute__((aligned(16))) unsigned h[];
     const int64_t sgi = blockIdx.x;
     const int64_t gs = seg_gs[sgi], ge = seg_ge[sgi];
@@ -862,6 +862,7 @@ region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__
         __syncthreads();
     }
     constexpr int kU = 4;                                // int4 loads in flight per thread
+    int vmax = 0;
     const int64_t a4 = gs & ~(int64_t)3;
     for (int64_t p0 = a4 + (int64_t)threadIdx.x * 4; p0 < ge; p0 += (int64_t)kBlock * 4 * kU) {
         i32x4 x[kU];
@@ -887,8 +888,11 @@ region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__
             if (s1 && y1 >= 0) atomicAdd(&hh[y1], (unsigned)l1);
             if (s2 && y2 >= 0) atomicAdd(&hh[y2], (unsigned)l2);
             if (s3 && y3 >= 0) atomicAdd(&hh[y3], 1u);
+            vmax = max(vmax, max(max(y0, y1), max(y2, y3)));
         }
     }
+    vmax = wave_max(vmax);                   // bounds K3b's scan of this region's bins
+    if ((threadIdx.x & 63) == 0 && vmax > 0) atomicMax(&acc[r].max, vmax);
     if (kLdsHist) {
         __syncthreads();
         for (int k = threadIdx.x; k < nbins; k += kBlock) {
@@ -904,21 +908,25 @@ struct RegionOut {                     // mirrors mc_region_stat
     long long min, max, med_lo, med_hi, q23_sum, q23_cnt;
 };
 
-// One workgroup per region: block scan over the value histogram for the
-// ranks (n-1)/2, n/2 and the trimmed range [n/4, n - n/4) (pileup.py:21,24).
-// Bin b holds the value base[r] + b (base = nullptr: 0).  Values outside the
-// window were accumulated in `acc` (count below it in low[r]); with
-// hist_stats, min/max/sum/sumsq are folded from the histogram and `acc`,
-// otherwise `acc` holds the full statistics (K3a).  fallback[r] = 1 when a
-// needed rank lies outside the window: the host recomputes that region with
-// the full-range K3.  Positions past the contig extent (zx) are zeros.
+// One workgroup per region: the value histogram is walked in coalesced tiles
+// of kBlock x 4 bins (a 64-bit block scan per tile gives every bin its rank
+// range) for the ranks (n-1)/2, n/2 and the trimmed range [n/4, n - n/4)
+// (pileup.py:21,24), and for min / max / sum / sum of squares.  Bin b holds
+// the value base[r] + b (base = nullptr: 0).  Values outside the window were
+// accumulated in `acc` (count below it in low[r]); with hist_stats,
+// min/max/sum/sumsq are folded from the histogram and `acc`, otherwise `acc`
+// holds the full statistics.  bound_by_max (K3: no window): acc[r].max, the
+// region's largest depth from K3a, bounds the bins scanned.  fallback[r] = 1
+// when a needed rank lies outside the window: the host recomputes that region
+// with the full-range K3.  Positions past the contig extent (zx) are zeros.
 __global__ void __launch_bounds__(kBlock)
 region_final_kernel(const unsigned* __restrict__ hist, int nbins,
                     const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
                     const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
                     int* __restrict__ fallback, int hist_stats,
-                    const int32_t* __restrict__ base_of, const unsigned* __restrict__ low_of) {
-    __shared__ long long s_part[kBlock];
+                    const int32_t* __restrict__ base_of, const unsigned* __restrict__ low_of,
+                    int bound_by_max) {
+    __shared__ long long s_tot[2][kWaves];
     __shared__ long long s_red[4][kWaves];
     __shared__ long long s_med[2];
     const int r = blockIdx.x;
@@ -931,49 +939,57 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     // otherwise below the window
     const long long zx_bin = base == 0 ? zx : 0;
     const long long low = (low_of ? (long long)low_of[r] : 0) + (base == 0 ? 0 : zx);
-    const int per = (nbins + kBlock - 1) / kBlock;
-    const int b0 = threadIdx.x * per;
-    const int b1 = min(nbins, b0 + per);
-    long long local = 0, s1 = 0;
-    unsigned long long s2 = 0;
-    int lmin = 0x7fffffff, lmax = -1;
-    for (int b = b0; b < b1; ++b) {
-        const long long cnt = (long long)hr[b] + (b == 0 ? zx_bin : 0);
-        if (!cnt) continue;
-        const long long v = base + b;
-        local += cnt;
-        s1 += cnt * v;
-        s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
-        lmin = min(lmin, b);
-        lmax = max(lmax, b);
-    }
-    s_part[threadIdx.x] = local;
-    if (threadIdx.x < 2) s_med[threadIdx.x] = 0;
-    __syncthreads();
-    // exclusive scan of the per-thread counts (Hillis-Steele on 256 entries)
-    for (int d = 1; d < kBlock; d <<= 1) {
-        const long long y = threadIdx.x >= d ? s_part[threadIdx.x - d] : 0;
-        __syncthreads();
-        s_part[threadIdx.x] += y;
-        __syncthreads();
-    }
-    long long cum = low + s_part[threadIdx.x] - local;   // values below the window rank first
-    const long long in_hist = s_part[kBlock - 1];
+    const int nb = bound_by_max ? min(nbins, max(acc[r].max, 0) + 1) : nbins;
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;
     const long long q_lo = n / 4, q_hi = n - n / 4;
-    long long qsum = 0;
-    for (int b = b0; b < b1; ++b) {
-        const long long cnt = (long long)hr[b] + (b == 0 ? zx_bin : 0);
-        if (cnt == 0) continue;
-        const long long v = base + b;
-        const long long e = cum + cnt;
-        if (r_lo >= cum && r_lo < e) s_med[0] = v;
-        if (r_hi >= cum && r_hi < e) s_med[1] = v;
-        const long long lo = cum > q_lo ? cum : q_lo;
-        const long long hi = e < q_hi ? e : q_hi;
-        if (hi > lo) qsum += (hi - lo) * v;
-        cum = e;
+    if (threadIdx.x < 2) s_med[threadIdx.x] = 0;
+    long long running = low;                 // values below the window rank first
+    long long qsum = 0, s1 = 0;
+    unsigned long long s2 = 0;
+    int lmin = 0x7fffffff, lmax = -1;
+    int buf = 0;
+    for (int t0 = 0; t0 < nb; t0 += kBlock * 4, buf ^= 1) {
+        const int b = t0 + (int)threadIdx.x * 4;
+        long long c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            c[k] = b + k < nb ? (long long)hr[b + k] + (b + k == 0 ? zx_bin : 0) : 0;
+        const long long mine = c[0] + c[1] + c[2] + c[3];
+        long long incl = mine;               // 64-bit wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const long long y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_tot[buf][wave] = incl;
+        __syncthreads();                     // (double-buffered: one barrier per tile)
+        long long cum = running + incl - mine, tile = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            const long long tw = s_tot[buf][w];
+            if (w < wave) cum += tw;
+            tile += tw;
+        }
+        running += tile;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long long cnt = c[k];
+            if (cnt == 0) continue;
+            const long long v = base + b + k;
+            const long long e = cum + cnt;
+            if (r_lo >= cum && r_lo < e) s_med[0] = v;
+            if (r_hi >= cum && r_hi < e) s_med[1] = v;
+            const long long lo = cum > q_lo ? cum : q_lo;
+            const long long hi = e < q_hi ? e : q_hi;
+            if (hi > lo) qsum += (hi - lo) * v;
+            s1 += cnt * v;
+            s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
+            lmin = min(lmin, b + k);
+            lmax = max(lmax, b + k);
+            cum = e;
+        }
     }
+    const long long in_hist = running - low;
     qsum = wave_sum64(qsum);
     s1 = wave_sum64(s1);
 #pragma unroll
