@@ -327,6 +327,7 @@ def main():
             "kernels_ms": {"k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
                            ("k3_region_stats" if args.unfused else "k3b_finalize"): float(np.mean(k3)),
                            "prepare_ingest_index": prep["prepare_ms"]},
+            "fused_fallback_regions": None if args.unfused else eng.fused_fallbacks(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": traffic,
                          "kernel": "depth_kernel<%s> (K2)" % ("false" if args.unfused else "true"),

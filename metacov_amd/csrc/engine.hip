@@ -607,8 +607,11 @@ extern "C" int mc_contig_offset(mc_ctx* ctx, int32_t tid, int64_t* offset, int64
 
 // Region statistics: K3a over segments, K3b per region.  Writes R rows of
 // RegionOut (== mc_region_stat) to d_out (device).
+// out_rows (host, optional): region r's row goes to d_out_final[out_rows[r]]
+// instead of d_out_final[r] (the fused path's fallback regions).
 static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
-                             const int64_t* end, RegionOut* d_out_final) {
+                             const int64_t* end, RegionOut* d_out_final,
+                             const int64_t* out_rows = nullptr) {
     MC_REQUIRE(ctx->depth_valid, MC_E_STATE, "depth not computed (call mc_compute_depth)");
     MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
     const int32_t nc = (int32_t)ctx->len.size();
@@ -627,7 +630,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
     const int64_t max_hist = int64_t(1) << 28;
     const int64_t rb = std::max<int64_t>(1, std::min<int64_t>(R, max_hist / nbins));
     const bool lds_hist = nbins <= kLdsBins;
-    HIP_TRY(hipEventRecord(ctx->ev[6], s));
+    if (!out_rows) HIP_TRY(hipEventRecord(ctx->ev[6], s));   // a fallback extends the fused K3b span
     int64_t launches = 0;
     for (int64_t r0 = 0; r0 < R; r0 += rb) {
         const int64_t nr = std::min(rb, R - r0);
@@ -649,7 +652,8 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
         const int64_t nseg = (int64_t)sg_gs.size();
         const size_t o_gs = 0, o_ge = o_gs + stage_align(nseg * 8),
                      o_reg = o_ge + stage_align(nseg * 8), o_ntot = o_reg + stage_align(nseg * 4),
-                     o_nzx = o_ntot + stage_align(nr * 8), total = o_nzx + stage_align(nr * 8);
+                     o_nzx = o_ntot + stage_align(nr * 8), o_rows = o_nzx + stage_align(nr * 8),
+                     total = o_rows + (out_rows ? stage_align(nr * 8) : 0);
         HIP_TRY(ctx->k3_stage.reserve(total));
         unsigned char* h = ctx->k3_stage.host();
         std::memcpy(h + o_gs, sg_gs.data(), nseg * 8);
@@ -657,6 +661,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
         std::memcpy(h + o_reg, sg_reg.data(), nseg * 4);
         std::memcpy(h + o_ntot, ntot.data(), nr * 8);
         std::memcpy(h + o_nzx, nzx.data(), nr * 8);
+        if (out_rows) std::memcpy(h + o_rows, out_rows + r0, nr * 8);
         unsigned char* d = ctx->k3_stage.d.p;
         const int64_t* d_seg_gs = reinterpret_cast<const int64_t*>(d + o_gs);
         const int64_t* d_seg_ge = reinterpret_cast<const int64_t*>(d + o_ge);
@@ -690,8 +695,9 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
                            ctx->d_hist.p, nbins, ctx->d_acc.p,
                            reinterpret_cast<const int64_t*>(d + o_ntot),
                            reinterpret_cast<const int64_t*>(d + o_nzx),
-                           d_out_final + r0, (int*)nullptr, 1, (const int32_t*)nullptr,
-                           (const unsigned*)nullptr, 1);
+                           out_rows ? d_out_final : d_out_final + r0, (int*)nullptr, 1,
+                           (const int32_t*)nullptr, (const unsigned*)nullptr, 1,
+                           out_rows ? reinterpret_cast<const int64_t*>(d + o_rows) : nullptr);
         HIP_TRY(hipGetLastError());
         // the staging buffer is reused by the next batch / call
         HIP_TRY(hipStreamSynchronize(s));
@@ -793,7 +799,8 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
                        kHistBins, ctx->d_acc.p, reinterpret_cast<const int64_t*>(d + o_ntot),
                        reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->d_fflag.p, 1,
-                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p, 0);
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p, 0,
+                       (const int64_t*)nullptr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
@@ -811,20 +818,10 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
             fr_idx.push_back(r);
         }
     ctx->fused_fallbacks = (int64_t)ft.size();
-    if (!ft.empty()) {
-        const int64_t nfb = (int64_t)ft.size();
-        DevBuf<RegionOut> tmp;
-        HIP_TRY(tmp.reserve(nfb));
-        int rc = region_stats_impl(ctx, nfb, ft.data(), fs.data(), fe.data(), tmp.p);
-        if (rc == MC_OK) {
-            for (int64_t k = 0; k < nfb && rc == MC_OK; ++k)
-                if (hipMemcpyAsync(d_out + fr_idx[k], tmp.p + k, sizeof(RegionOut),
-                                   hipMemcpyDeviceToDevice, s) != hipSuccess)
-                    rc = MC_E_HIP;
-            if (hipStreamSynchronize(s) != hipSuccess) rc = MC_E_HIP;
-        }
-        tmp.release();
-        if (rc) return rc;
+    if (!ft.empty()) {   // exact recompute, rows written in place
+        if (int rc = region_stats_impl(ctx, (int64_t)ft.size(), ft.data(), fs.data(), fe.data(),
+                                       d_out, fr_idx.data()))
+            return rc;
     }
     return MC_OK;
 }

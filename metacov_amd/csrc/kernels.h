@@ -222,25 +222,79 @@ chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ 
 //   * chunk_diff builds the count of long reads covering each chunk's first
 //     position that started in an earlier chunk (K2's initial carry).
 
+// Wave-aggregated counter increments: lanes with equal keys (key < 0: none)
+// share one atomic (reads are position-sorted, so a wave's 64 reads touch a
+// handful of tiles / chunks).  Returns each lane's slot: the counter value
+// before the group's add plus the lane's rank within its group.
+__device__ __forceinline__ unsigned wave_key_add(unsigned* arr, long long key, int lane) {
+    unsigned slot = 0;
+    unsigned long long pending = __ballot(key >= 0);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const long long k = __shfl(key, leader, 64);
+        const unsigned long long m = __ballot(key == k) & pending;
+        unsigned b = 0;
+        if (lane == leader) b = atomicAdd(&arr[k], (unsigned)__popcll(m));
+        b = __shfl(b, leader, 64);
+        if ((m >> lane) & 1ull) slot = b + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+        pending &= ~m;
+    }
+    return slot;
+}
+
+__device__ __forceinline__ void wave_key_add_signed(int* arr, long long key, int sign, int lane) {
+    unsigned long long pending = __ballot(key >= 0);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const long long k = __shfl(key, leader, 64);
+        const unsigned long long m = __ballot(key == k) & pending;
+        if (lane == leader) atomicAdd(&arr[k], sign * (int)__popcll(m));
+        pending &= ~m;
+    }
+}
+
+// Long-read events of read i (short_max < span): the tile of its end event
+// (or -1: past the allocation, or exactly on a chunk start, where the next
+// chunk's carry already excludes it) and its chunk-carry range [c0, c1).
+struct LongEv {
+    long long tile, c0, c1;
+};
+
+__device__ __forceinline__ LongEv long_events(const int32_t* tid, const int32_t* pos,
+                                              const int32_t* span, int64_t i, int64_t n,
+                                              const int64_t* coff, int short_max,
+                                              int64_t alloc_len, int64_t chunk_w, int64_t* ge_out) {
+    LongEv e{-1, -1, -1};
+    if (i >= n) return e;
+    const int sp = span[i];
+    if (sp <= short_max) return e;
+    const int64_t gs = coff[tid[i]] + pos[i];
+    const int64_t ge = gs + sp;
+    *ge_out = ge;
+    if (ge < alloc_len && ge % chunk_w) e.tile = ge / kTileW;
+    const int64_t c0 = gs / chunk_w + 1, c1 = (ge - 1) / chunk_w + 1;
+    if (c1 > c0) {
+        e.c0 = c0;
+        e.c1 = c1;
+    }
+    return e;
+}
+
 __global__ void __launch_bounds__(kBlock)
 long_count_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                   const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
                   int short_max, int64_t alloc_len, int64_t chunk_w,
                   unsigned* __restrict__ tile_cnt, int* __restrict__ chunk_diff) {
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * kBlock) {
-        const int sp = span[i];
-        if (sp <= short_max) continue;
-        const int64_t gs = coff[tid[i]] + pos[i];
-        const int64_t ge = gs + sp;
-        // an end exactly on a chunk start needs no event: that chunk's carry
-        // excludes the read already
-        if (ge < alloc_len && ge % chunk_w) atomicAdd(&tile_cnt[ge / kTileW], 1u);
-        const int64_t c0 = gs / chunk_w + 1, c1 = (ge - 1) / chunk_w + 1;
-        if (c1 > c0) {
-            atomicAdd(&chunk_diff[c0], 1);
-            atomicSub(&chunk_diff[c1], 1);
-        }
+    const int lane = threadIdx.x & 63;
+    // whole waves stride together (the aggregation loops are wave-wide)
+    for (int64_t w0 = blockIdx.x * (int64_t)kBlock + (threadIdx.x & ~63); w0 < n;
+         w0 += (int64_t)gridDim.x * kBlock) {
+        int64_t ge = 0;
+        const LongEv e = long_events(tid, pos, span, w0 + lane, n, coff, short_max, alloc_len,
+                                     chunk_w, &ge);
+        (void)wave_key_add(tile_cnt, e.tile, lane);
+        wave_key_add_signed(chunk_diff, e.c0, 1, lane);
+        wave_key_add_signed(chunk_diff, e.c1, -1, lane);
     }
 }
 
@@ -250,15 +304,14 @@ long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ po
                  int short_max, int64_t alloc_len, int64_t chunk_w,
                  const int64_t* __restrict__ tile_off,
                  unsigned* __restrict__ tile_cursor, int32_t* __restrict__ ev) {
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * kBlock) {
-        const int sp = span[i];
-        if (sp <= short_max) continue;
-        const int64_t ge = coff[tid[i]] + pos[i] + sp;
-        if (ge >= alloc_len || ge % chunk_w == 0) continue;
-        const int64_t t = ge / kTileW;
-        const unsigned slot = atomicAdd(&tile_cursor[t], 1u);
-        ev[tile_off[t] + slot] = (int32_t)(ge - t * kTileW);
+    const int lane = threadIdx.x & 63;
+    for (int64_t w0 = blockIdx.x * (int64_t)kBlock + (threadIdx.x & ~63); w0 < n;
+         w0 += (int64_t)gridDim.x * kBlock) {
+        int64_t ge = 0;
+        const LongEv e = long_events(tid, pos, span, w0 + lane, n, coff, short_max, alloc_len,
+                                     chunk_w, &ge);
+        const unsigned slot = wave_key_add(tile_cursor, e.tile, lane);
+        if (e.tile >= 0) ev[tile_off[e.tile] + slot] = (int32_t)(ge - e.tile * kTileW);
     }
 }
 
@@ -916,7 +969,8 @@ struct RegionOut {                     // mirrors mc_region_stat
 // accumulated in `acc` (count below it in low[r]); with hist_stats,
 // min/max/sum/sumsq are folded from the histogram and `acc`, otherwise `acc`
 // holds the full statistics.  bound_by_max (K3: no window): acc[r].max, the
-// region's largest depth from K3a, bounds the bins scanned.  fallback[r] = 1
+// region's largest depth from K3a, bounds the bins scanned.  out_row: row r
+// is written to out[out_row[r]] (scattered fallback rows).  fallback[r] = 1
 // when a needed rank lies outside the window: the host recomputes that region
 // with the full-range K3.  Positions past the contig extent (zx) are zeros.
 __global__ void __launch_bounds__(kBlock)
@@ -925,7 +979,7 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
                     const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
                     int* __restrict__ fallback, int hist_stats,
                     const int32_t* __restrict__ base_of, const unsigned* __restrict__ low_of,
-                    int bound_by_max) {
+                    int bound_by_max, const int64_t* __restrict__ out_row) {
     __shared__ long long s_tot[2][kWaves];
     __shared__ long long s_red[4][kWaves];
     __shared__ long long s_med[2];
@@ -1051,7 +1105,7 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
             o.sum = 0;
             o.sumsq = 0;
         }
-        out[r] = o;
+        out[out_row ? out_row[r] : r] = o;
     }
 }
 
