@@ -36,6 +36,10 @@ def parse():
     ap.add_argument("--strong", action="store_true")
     ap.add_argument("--unfused", action="store_true",
                     help="K2 then a separate K3 pass instead of the fused K2 statistics")
+    ap.add_argument("--cigar", action="store_true",
+                    help="raw-CIGAR input: ~Poisson(--cigar-ops) BAM CIGAR words per read resident "
+                         "in HBM; each step runs K1 (CIGAR -> span) + prepare + K2 + K3b")
+    ap.add_argument("--cigar-ops", type=float, default=200.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bases", type=float, default=3.0e9,
                     help="aligned bases in the CPU-baseline sample (~10-20 s on one core)")
@@ -200,10 +204,18 @@ def main():
 
     eng = CoverageEngine(local)
     eng.set_contigs(lengths)
-    eng.add_reads(tid, pos, span)
+    cig_off = cigar = None
+    if args.cigar:
+        cig_off, cigar = synth.device_cigars(torch, span, args.cigar_ops, args.seed + 7)
+        torch.cuda.synchronize()
+        eng.add_reads_cigar_device(tid, pos, cig_off, cigar)
+    else:
+        eng.add_reads(tid, pos, span)
     eng.prepare()
     prep = eng.timings()
     bases = eng.aligned_bases()
+    if args.cigar:   # K1 re-derived exactly the generator's spans
+        assert bases == int(span.to(torch.int64).sum()), "K1 spans differ from the generator"
     R = len(lengths)
     rt = np.arange(R, dtype=np.int32)
     rs = np.zeros(R, np.int64)
@@ -214,6 +226,9 @@ def main():
 
     def step():
         nonlocal gathered
+        if args.cigar:   # a fresh raw-CIGAR batch: K1 + prepare run inside this step
+            eng.clear_reads()
+            eng.add_reads_cigar_device(tid, pos, cig_off, cigar)
         if args.unfused:
             eng.compute_depth()
             eng.region_stats_device(rt, rs, re_, table.data_ptr())
@@ -235,13 +250,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    k2, k3 = [], []
+    k2, k3, k1, kp = [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         tm = eng.timings()            # syncs the ctx stream; HIP events around K2 / K3
         k2.append(tm["depth_ms"])
         k3.append(tm["stats_ms"])
+        k1.append(tm["cigar_ms"])
+        kp.append(tm["prepare_ms"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -268,6 +285,11 @@ def main():
     k2_bytes = 12 * len(tid) + 4 * ext_sum
     k2_ms = float(np.mean(k2))
     achieved = k2_bytes / (k2_ms * 1e-3) / 1e9
+    k1_ms = float(np.mean(k1)) if args.cigar else 0.0
+    if args.cigar and k1_ms > k2_ms:   # K1 streams the CIGAR words: the dominant kernel
+        n_words = int(cigar.numel())
+        k1_bytes = 4 * n_words + 8 * (len(tid) + 1) + 4 * len(tid)
+        achieved_k1 = k1_bytes / (k1_ms * 1e-3) / 1e9
     pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
     traffic = None
     variant = "depth_kernel<%s>" % ("false" if args.unfused else "true")
@@ -275,6 +297,19 @@ def main():
         if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
                 and variant in v.get("kernel", ""):
             traffic = v.get("hbm_bytes_per_launch")
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                "frac": achieved / 8000.0, "traffic": traffic,
+                "kernel": "depth_kernel<%s> (K2)" % ("false" if args.unfused else "true"),
+                "algorithmic_bytes_per_launch": int(k2_bytes)}
+    if args.cigar and k1_ms > k2_ms:
+        k1_traffic = None
+        for v in ([] if args.strong else (pmc or {}).get("variants", [])):
+            if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
+                    and "cigar_span_kernel" in v.get("kernel", ""):
+                k1_traffic = v.get("hbm_bytes_per_launch")
+        roofline = {"bound": "hbm", "achieved": achieved_k1, "peak": 8000.0, "unit": "GB/s",
+                    "frac": achieved_k1 / 8000.0, "traffic": k1_traffic,
+                    "kernel": "cigar_span_kernel (K1)", "algorithmic_bytes_per_launch": int(k1_bytes)}
 
     if rank == 0:
         cpu = cpu_par = None
@@ -320,18 +355,21 @@ def main():
                 "reads_per_gpu": int(len(tid)),
                 "aligned_bases_per_step": int(total_bases),
                 "regions": n_regions_total,
+                "input": ("raw BAM CIGAR words in HBM (%d words, %.1f GB, ~%g ops/read); per step "
+                          "K1 CIGAR->span + prepare + K2 + K3b" % (cigar.numel(), cigar.numel() * 4e-9,
+                                                                    args.cigar_ops))
+                         if args.cigar else "(tid, pos, span) tuples in HBM; prepared index reused",
                 "parallelism": ("contig-shard x%d, %s all-gather of region table"
                                 % (world, "RCCL" if args.backend == "nccl" else "gloo"))
                                if world > 1 else "single GPU",
             },
-            "kernels_ms": {"k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
+            "kernels_ms": {**({"k1_cigar_span": k1_ms} if args.cigar else {}),
+                           "k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
                            ("k3_region_stats" if args.unfused else "k3b_finalize"): float(np.mean(k3)),
-                           "prepare_ingest_index": prep["prepare_ms"]},
+                           "prepare_ingest_index": float(np.mean(kp)) if args.cigar
+                           else prep["prepare_ms"]},
             "fused_fallback_regions": None if args.unfused else eng.fused_fallbacks(),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": achieved / 8000.0, "traffic": traffic,
-                         "kernel": "depth_kernel<%s> (K2)" % ("false" if args.unfused else "true"),
-                         "algorithmic_bytes_per_launch": int(k2_bytes)},
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
         }

@@ -109,6 +109,17 @@ int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid,
                        const int32_t* pos, const int64_t* cig_off,
                        const uint32_t* cigar);
 
+/* Same with device pointers (a batch already in HBM, e.g. torch tensors).
+ * tid / pos are copied into the ctx; cig_off and cigar are BORROWED: they
+ * must stay valid until the next mc_prepare (K1 reads them there), so a
+ * 40 GB CIGAR batch is never duplicated.  cig_off[0] must be 0. */
+int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,
+                              const int32_t* d_pos, const int64_t* d_cig_off,
+                              const uint32_t* d_cigar);
+
+/* Drops the ctx's reads (the contigs stay): the next batch starts empty. */
+int mc_clear_reads(mc_ctx* ctx);
+
 /* Validates order, computes contig extents (max of length and furthest
  * read end) and the tile index.  Called by mc_compute_depth if needed. */
 int mc_prepare(mc_ctx* ctx);

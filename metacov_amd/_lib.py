@@ -64,6 +64,8 @@ SIGNATURES = {
     "mc_add_reads": [_P, _I64, _P, _P, _P],
     "mc_add_reads_device": [_P, _I64, _P, _P, _P],
     "mc_add_reads_cigar": [_P, _I64, _P, _P, _P, _P],
+    "mc_add_reads_cigar_device": [_P, _I64, _P, _P, _P, _P],
+    "mc_clear_reads": [_P],
     "mc_prepare": [_P],
     "mc_compute_depth": [_P],
     "mc_get_depth": [_P, _I32, _I64, _I64, _P],
@@ -105,20 +107,23 @@ def load(path=None):
     global _lib
     if path is not None and path != LIB_PATH:
         if path not in _variants:
-            _variants[path] = _open(path)
+            _variants[path] = _open(path, partial=True)
         return _variants[path]
     if _lib is None:
         _lib = _open(LIB_PATH)
     return _lib
 
 
-def _open(path):
+def _open(path, partial=False):
+    """partial: an A/B build of an older revision may lack newer entry points."""
     if not os.path.exists(path):
         raise LibraryNotBuilt(
             "%s not found: build it with `python -m metacov_amd.build` "
             "(hipcc --offload-arch=gfx950). metacov_amd has no CPU fallback." % path)
     lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
+        if partial and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = _RESTYPE.get(name, ctypes.c_int)

@@ -106,6 +106,8 @@ struct mc_ctx {
     bool spans_pending = false;
     DevBuf<int64_t> d_cig_off;
     DevBuf<uint32_t> d_cigar;
+    const int64_t* cig_off_ext = nullptr;   // borrowed (mc_add_reads_cigar_device)
+    const uint32_t* cigar_ext = nullptr;
 
     bool prepared = false;
     int32_t max_span = 0;
@@ -258,6 +260,8 @@ extern "C" int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths) {
     ctx->len.assign(lengths, lengths + n);
     ctx->n_reads = 0;
     ctx->spans_pending = false;
+    ctx->cig_off_ext = nullptr;
+    ctx->cigar_ext = nullptr;
     invalidate(ctx);
     HIP_TRY(ctx->d_len.reserve(std::max<int64_t>(n, 1)));
     if (n) HIP_TRY(hipMemcpy(ctx->d_len.p, lengths, n * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -346,6 +350,41 @@ extern "C" int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid, co
     }
     ctx->n_reads = n;
     ctx->spans_pending = n > 0;
+    ctx->cig_off_ext = nullptr;
+    ctx->cigar_ext = nullptr;
+    invalidate(ctx);
+    return MC_OK;
+}
+
+extern "C" int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* tid,
+                                         const int32_t* pos, const int64_t* cig_off,
+                                         const uint32_t* cigar) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(n >= 0, MC_E_INVALID, "negative read count");
+    MC_REQUIRE(n == 0 || (tid && pos && cig_off && cigar), MC_E_INVALID, "null read array");
+    MC_REQUIRE(ctx->n_reads == 0, MC_E_STATE,
+               "mc_add_reads_cigar_device must be the only read source of a ctx "
+               "(call mc_clear_reads to start a new batch)");
+    if (int rc = reserve_reads(ctx, n, true)) return rc;
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(ctx->d_tid.p, tid, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->d_pos.p, pos, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    ctx->cig_off_ext = cig_off;
+    ctx->cigar_ext = cigar;
+    ctx->n_reads = n;
+    ctx->spans_pending = n > 0;
+    invalidate(ctx);
+    return MC_OK;
+}
+
+extern "C" int mc_clear_reads(mc_ctx* ctx) {
+    if (int rc = ctx_use(ctx)) return rc;
+    ctx->n_reads = 0;
+    ctx->spans_pending = false;
+    ctx->cig_off_ext = nullptr;
+    ctx->cigar_ext = nullptr;
+    ctx->fused_fallbacks = 0;
     invalidate(ctx);
     return MC_OK;
 }
@@ -366,13 +405,17 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     if (ctx->spans_pending) {
         HIP_TRY(hipEventRecord(ctx->ev[0], s));
         const int64_t nb = (n + kBlock - 1) / kBlock;
-        const size_t lds = (kBlock + 1) * 8 + 8 + kBlock * 4;
-        hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s,
-                           ctx->d_cig_off.p, ctx->d_cigar.p, n, ctx->d_span.p);
+        const size_t lds = (kBlock + 1) * 8 + 8 + kBlock * 4 + kOwnerBuckets;
+        const int64_t* co = ctx->cig_off_ext ? ctx->cig_off_ext : ctx->d_cig_off.p;
+        const uint32_t* cw = ctx->cigar_ext ? ctx->cigar_ext : ctx->d_cigar.p;
+        hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s, co, cw, n,
+                           ctx->d_span.p);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ctx->ev[1], s));
         ctx->t_cigar = true;
         ctx->spans_pending = false;
+        ctx->cig_off_ext = nullptr;   // borrowed until this prepare's stream sync
+        ctx->cigar_ext = nullptr;
     }
     HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // K2 loads whole int4 batches past n: the tid padding must index coff

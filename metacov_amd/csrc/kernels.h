@@ -79,13 +79,24 @@ struct RegionAcc {                     // K3 per-region accumulator
 
 // ----------------------------------------------------------------- helpers
 
+// Inclusive wave scan on DPP (VALU lane moves, no LDS round trips):
+// row_shr 1/2/4/8 scans each row of 16 lanes, row_bcast:15 / :31 carry the
+// row totals into the following rows (gfx9 DPP; lanes without a source add
+// the `old` operand, 0).
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        int y = __shfl_up(v, d, 64);
-        if (lane >= d) v += y;
-    }
+    (void)lane;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
     return v;
+}
+
+// Sum over the wave, uniform result (DPP scan, then lane 63).
+__device__ __forceinline__ int wave_sum_i32(int v) {
+    return __builtin_amdgcn_readlane(wave_incl_scan(v, 0), 63);
 }
 
 __device__ __forceinline__ long long wave_sum64(long long v) {
@@ -317,46 +328,128 @@ long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ po
 
 // ----------------------------------------------------------------- K1
 
-// One workgroup per 256 reads; the block streams the contiguous CIGAR words
-// of its reads (coalesced) and sums the reference-consuming lengths
-// (op-type mask 0x18D = M, D, N, =, X; htslib bam_cigar2rlen).  A mapped read
-// without such an op gets span 1 (htslib bam_endpos).
+// One workgroup per 256 reads: the block streams the contiguous CIGAR words
+// of its reads as int4 (kU loads in flight per thread) and sums the
+// reference-consuming lengths per read (op-type mask 0x18D = M, D, N, =, X;
+// htslib bam_cigar2rlen).  A mapped read without such an op gets span 1
+// (htslib bam_endpos).  Each lane splits its 4 words into runs by read (one
+// LDS binary search per int4, then forward steps); a wave whose runs touch few
+// reads (long CIGARs) reduces them with shuffles before one LDS atomic per
+// read, otherwise (short CIGARs, low contention) each run adds directly.
+constexpr int kCigarLoads = 4;
+constexpr int kOwnerBuckets = 2048;       // K1 word -> read lookup buckets (bytes of LDS)
+
+__device__ __forceinline__ int cigar_ref_len(uint32_t c) {
+    return ((0x18Du >> (c & 0xFu)) & 1u) ? (int)(c >> 4) : 0;
+}
+
 __global__ void __launch_bounds__(kBlock)
 cigar_span_kernel(const int64_t* __restrict__ cig_off, const uint32_t* __restrict__ cigar,
                   int64_t n, int32_t* __restrict__ span) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    long long* off = reinterpret_cast<long long*>(smem_raw);          // kBlock + 1
-    int* acc = reinterpret_cast<int*>(smem_raw + (kBlock + 1) * 8 + 8);  // kBlock
+    long long* off = reinterpret_cast<long long*>(smem_raw);                 // kBlock + 1
+    int* acc = reinterpret_cast<int*>(smem_raw + (kBlock + 1) * 8 + 8);      // kBlock
+    unsigned char* owner = smem_raw + (kBlock + 1) * 8 + 8 + kBlock * 4;     // kOwnerBuckets
     const int64_t r0 = blockIdx.x * (int64_t)kBlock;
     const int nr = (int)min<int64_t>(kBlock, n - r0);
     for (int k = threadIdx.x; k <= nr; k += kBlock) off[k] = cig_off[r0 + k];
     acc[threadIdx.x] = 0;
     __syncthreads();
     const long long w0 = off[0], w1 = off[nr];
+    // owner[k]: the read holding word w0 + (k << sh) (2^sh words per bucket,
+    // kOwnerBuckets buckets cover the block's words): a lookup plus a step or
+    // two replaces a binary search per int4
+    int sh = 0;
+    while (((long long)kOwnerBuckets << sh) < w1 - w0) ++sh;
+    if ((int)threadIdx.x < nr) {                       // each read claims its buckets
+        const long long lo = off[threadIdx.x] - w0, hi = off[threadIdx.x + 1] - w0;
+        for (long long k = (lo + (1ll << sh) - 1) >> sh; (k << sh) < hi; ++k)
+            owner[k] = (unsigned char)threadIdx.x;
+    }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
-    for (long long w = w0 + threadIdx.x; w - threadIdx.x < w1; w += kBlock) {
-        int r = -1, contrib = 0;
-        if (w < w1) {
-            const uint32_t c = cigar[w];
-            contrib = ((0x18Du >> (c & 0xFu)) & 1u) ? (int)(c >> 4) : 0;
-            int lo = 0, hi = nr;              // upper_bound(off, w) - 1
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (off[mid + 1] <= w) lo = mid + 1;
-                else hi = mid;
-            }
-            r = lo;
-        }
-        const int r_first = __shfl(r, 0, 64);
-        const bool uniform = __all(r == r_first) && r_first >= 0;
-        if (uniform) {
-            int s = contrib;
+    const long long a4 = w0 & ~3ll;
+    constexpr long long kStep = 4ll * kBlock;
+    auto load = [&](uint32_t (&wd)[kCigarLoads][4], long long base) {
 #pragma unroll
-            for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
-            if (lane == 0 && s) atomicAdd(&acc[r_first], s);
-        } else if (r >= 0 && contrib) {
-            atomicAdd(&acc[r], contrib);
+        for (int u = 0; u < kCigarLoads; ++u) {
+            const long long p = base + u * kStep + 4ll * threadIdx.x;
+            if (p + 3 < w1 && p >= w0) {
+                const uint4 x = *reinterpret_cast<const uint4*>(cigar + p);
+                wd[u][0] = x.x;
+                wd[u][1] = x.y;
+                wd[u][2] = x.z;
+                wd[u][3] = x.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    wd[u][k] = (p + k >= w0 && p + k < w1) ? cigar[p + k] : 0u;
+            }
         }
+    };
+    uint32_t cur[kCigarLoads][4], nxt[kCigarLoads][4];
+    if (a4 < w1) load(cur, a4);
+    for (long long base = a4; base < w1; base += kStep * kCigarLoads) {
+        const long long nbase = base + kStep * kCigarLoads;
+        if (nbase < w1) load(nxt, nbase);            // next batch in flight meanwhile
+#pragma unroll
+        for (int u = 0; u < kCigarLoads; ++u) {
+            const long long p = base + u * kStep + 4ll * threadIdx.x;
+            // runs of this lane's words by read: (ra, sa) first, (rb, sb) last
+            int ra = -1, rb = -1, sa = 0, sb = 0;
+            const long long first = p > w0 ? p : w0;
+            if (first < w1 && first < p + 4) {
+                int r = owner[(first - w0) >> sh];
+                long long next = off[r + 1];               // first word of read r + 1
+                ra = -2;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const long long w = p + k;
+                    if (w < first || w >= w1) continue;
+                    while (next <= w) {                    // w < w1 = off[nr]: stops at r < nr
+                        ++r;
+                        next = off[r + 1];
+                    }
+                    const int c = cigar_ref_len(cur[u][k]);
+                    if (ra == -2) ra = r;
+                    if (r == ra) {
+                        sa += c;
+                    } else if (r == rb) {
+                        sb += c;
+                    } else {
+                        if (rb >= 0 && sb) atomicAdd(&acc[rb], sb);   // a short read in the middle
+                        rb = r;
+                        sb = c;
+                    }
+                }
+            }
+            // few distinct reads in the wave: shuffle-reduce per read
+            const int prev_b = __shfl_up(rb >= 0 ? rb : ra, 1, 64);
+            const bool head = ra >= 0 && (lane == 0 || prev_b != ra);
+            if (__popcll(__ballot(head)) <= 4) {
+#pragma unroll
+                for (int pass = 0; pass < 2; ++pass) {
+                    const int key = pass == 0 ? ra : rb;
+                    const int val = pass == 0 ? sa : sb;
+                    unsigned long long pending = __ballot(key >= 0);
+                    while (pending) {
+                        const int leader = __ffsll((long long)pending) - 1;
+                        const int k = __shfl(key, leader, 64);
+                        const unsigned long long m = __ballot(key == k) & pending;
+                        const int v = wave_sum_i32(((m >> lane) & 1ull) ? val : 0);
+                        if (lane == leader && v) atomicAdd(&acc[k], v);
+                        pending &= ~m;
+                    }
+                }
+            } else {
+                if (ra >= 0 && sa) atomicAdd(&acc[ra], sa);
+                if (rb >= 0 && sb) atomicAdd(&acc[rb], sb);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCigarLoads; ++u)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[u][k] = nxt[u][k];
     }
     __syncthreads();
     if (threadIdx.x < nr) {
@@ -718,7 +811,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 const int excl = incl - x.w + wave_total;
                 x += excl;
                 v[j] = x;
-                wave_total += __shfl(incl, 63, 64);
+                wave_total += __builtin_amdgcn_readlane(incl, 63);
             }
             if (lane == 0) hdr[4 + wave] = wave_total;
             __syncthreads();

@@ -138,6 +138,31 @@ class CoverageEngine:
         self._check(self._lib.mc_add_reads_cigar(self._h, len(tid), ptr(tid), ptr(pos), ptr(cig_off),
                                            ptr(cigar)))
 
+    def add_reads_cigar_device(self, tid, pos, cig_off, cigar):
+        """Raw-CIGAR batch already in this GPU's memory (torch tensors: int32
+        tid/pos, int64 cig_off with n + 1 entries starting at 0, int32/uint32
+        cigar words).  tid/pos are copied; cig_off/cigar are borrowed until
+        the next prepare() (K1 reads them there) — keep them alive."""
+        import torch
+        tid = tid.contiguous().to(torch.int32)
+        pos = pos.contiguous().to(torch.int32)
+        if not (cig_off.is_contiguous() and cig_off.dtype == torch.int64 and cigar.is_contiguous()
+                and cigar.dtype in (torch.int32, torch.uint32)):
+            raise ValueError("cig_off must be contiguous int64 and cigar contiguous 32-bit")
+        n = tid.numel()
+        if pos.numel() != n or cig_off.numel() != n + 1:
+            raise ValueError("need n tid/pos and n + 1 cig_off entries")
+        torch.cuda.current_stream(tid.device).synchronize()
+        self._borrowed = (cig_off, cigar)
+        self._check(self._lib.mc_add_reads_cigar_device(
+            self._h, n, ctypes.c_void_p(tid.data_ptr()), ctypes.c_void_p(pos.data_ptr()),
+            ctypes.c_void_p(cig_off.data_ptr()), ctypes.c_void_p(cigar.data_ptr())))
+
+    def clear_reads(self):
+        """Drop the reads (contigs stay): the next batch starts empty."""
+        self._check(self._lib.mc_clear_reads(self._h))
+        self._borrowed = None
+
     def prepare(self):
         self._check(self._lib.mc_prepare(self._h))
 

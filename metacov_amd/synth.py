@@ -333,3 +333,42 @@ def write_bam_fast(path, names, lengths, tid, pos, flag, cig_off, cigar, l_seq=1
                                 _lib.ptr(lengths), len(tid), _lib.ptr(tid), _lib.ptr(pos),
                                 _lib.ptr(flag), _lib.ptr(cig_off), _lib.ptr(cigar), int(l_seq),
                                 int(level), int(n_threads)))
+
+
+def device_cigars(torch, span, mean_ops=200, seed=1, batch_reads=2_000_000):
+    """BAM-packed CIGAR words on the GPU whose reference-consuming lengths sum
+    to `span` (int32 device tensor): read i gets m_i ~ Poisson(mean_ops / 2)
+    reference blocks (M mostly; D, N, =, X mixed in) separated by 1-3 bp
+    insertions, i.e. 2 m_i - 1 ops (SURVEY §8 d C5: ~Poisson(200) ops per
+    read).  Built in read batches; returns (cig_off int64 [n + 1], cigar
+    int32 [W])."""
+    dev = span.device
+    n = span.numel()
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    m = torch.poisson(torch.full((n,), mean_ops / 2.0, device=dev), generator=g).to(torch.int64)
+    m.clamp_(min=1)
+    ops = 2 * m - 1
+    cig_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    cig_off[1:] = torch.cumsum(ops, 0)
+    total = int(cig_off[-1])
+    cigar = torch.empty(total, dtype=torch.int32, device=dev)
+    lut = torch.tensor([0] * 12 + [2, 3, 7, 8], dtype=torch.int64, device=dev)   # M x12, D, N, =, X
+    for r0 in range(0, n, batch_reads):
+        r1 = min(n, r0 + batch_reads)
+        w0, w1 = int(cig_off[r0]), int(cig_off[r1])
+        rid = torch.repeat_interleave(torch.arange(r0, r1, device=dev), ops[r0:r1])
+        k = torch.arange(w0, w1, device=dev) - cig_off[rid]
+        is_ref = (k & 1) == 0
+        j = k >> 1
+        s = span[rid].to(torch.int64)
+        mm = m[rid]
+        ref_len = (s * (j + 1)) // mm - (s * j) // mm
+        del s, mm, j, k
+        ins_len = torch.randint(1, 4, (w1 - w0,), generator=g, device=dev)
+        code = torch.randint(0, 16, (w1 - w0,), generator=g, device=dev)
+        op = torch.where(is_ref, lut[code], torch.ones_like(code))          # I = 1
+        length = torch.where(is_ref, ref_len, ins_len)
+        cigar[w0:w1] = ((length << 4) | op).to(torch.int32)
+        del rid, is_ref, ref_len, ins_len, code, op, length
+    return cig_off, cigar

@@ -484,3 +484,38 @@ def test_cli_two_ranks(lib_built, golden_dir, tmp_path, indexed):
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     assert open(two, newline="").read() == open(one, newline="").read()
+
+
+def test_cigar_device_batches(lib_built):
+    """Raw-CIGAR batches from device memory (borrowed cig_off / cigar, K1 in
+    prepare), cleared and re-added: depth and region rows equal the
+    interval path's and the oracle's."""
+    import torch
+    lengths, tid, pos, span = make_case([60_000, 7, 25_000, 9_000], 4_000, (1, 12_000), 21)
+    dev = torch.device("cuda", 0)
+    t_span = torch.from_numpy(span).to(dev)
+    cig_off, cigar = synth.device_cigars(torch, t_span, mean_ops=30, seed=3, batch_reads=1_000)
+    t_tid, t_pos = torch.from_numpy(tid).to(dev), torch.from_numpy(pos).to(dev)
+    a = CoverageEngine(0)
+    a.set_contigs(lengths)
+    b = CoverageEngine(0)
+    b.set_contigs(lengths)
+    b.add_reads(tid, pos, span)
+    rt = np.array([0, 2, 3, 0], np.int32)
+    rs = np.array([0, 100, 0, 59_000], np.int64)
+    re_ = np.array([60_000, 24_000, 9_000, 61_000], np.int64)
+    want = b.compute_depth_stats(rt, rs, re_)
+    for _ in range(2):
+        a.clear_reads()
+        a.add_reads_cigar_device(t_tid, t_pos, cig_off, cigar)
+        got = a.compute_depth_stats(rt, rs, re_)
+        assert a.timings()["cigar_ms"] > 0
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+        for t in range(len(lengths)):
+            assert np.array_equal(a.depth(t), b.depth(t))
+    check_depth_vs_oracle(a, lengths, tid, pos, span)
+    with pytest.raises(MetacovError):
+        a.add_reads_cigar_device(t_tid, t_pos, cig_off, cigar)   # reads already present
+    a.close()
+    b.close()
