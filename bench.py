@@ -344,7 +344,10 @@ def main():
             "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (GPU-generated C3 intervals, SURVEY §8d span mix)",
+            "data": ("synthetic (GPU-generated %s intervals, %s%s)"
+                     % (args.config.upper(),
+                        "lognormal ~10 kbp spans" if args.config == "c5" else "SURVEY §8d span mix",
+                        ", BAM CIGAR words generated on the GPU" if args.cigar else "")),
             "config": {
                 "workload": ("%s LPT-sharded by contig over %d GPUs" % (args.config.upper(), world))
                             if args.strong else
