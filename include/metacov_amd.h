@@ -97,6 +97,14 @@ int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths);
 int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid,
                  const int32_t* pos, const int32_t* span);
 
+/* Same, but the copy is only enqueued on the ctx stream: with pinned host
+ * buffers (hipHostMalloc / torch pin_memory) the DMA overlaps the caller's
+ * next decode.  The buffers must stay unchanged until mc_synchronize(ctx)
+ * (double-buffered streaming ingest: fill B, mc_synchronize, add A's
+ * successor ...). */
+int mc_add_reads_async(mc_ctx* ctx, int64_t n, const int32_t* tid,
+                       const int32_t* pos, const int32_t* span);
+
 /* Same, but the three arrays are already in this ctx's device memory
  * (e.g. torch tensors); they are copied into the ctx. */
 int mc_add_reads_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,
@@ -188,6 +196,22 @@ int mc_bam_intervals(const mc_bam* bam, int32_t* tid, int32_t* pos, int32_t* spa
 /* keep_cigar only: total CIGAR words, then offsets (n_kept + 1) and words */
 int mc_bam_n_cigar_words(const mc_bam* bam, int64_t* n);
 int mc_bam_cigars(const mc_bam* bam, int64_t* cig_off, uint32_t* cigar);
+
+/* ---- streaming decode -----------------------------------------------------
+ * Bounded-memory variant of mc_bam_open for BAMs larger than host memory:
+ * BGZF blocks are inflated a window (window_bytes inflated, 0 = 256 MiB) at
+ * a time on n_threads threads and the kept records' intervals come out in
+ * order, up to `cap` per mc_bam_stream_next call (*n_out = 0 at the end).
+ * mc_bam_stream_header exposes the header and the running record counts
+ * through the mc_bam accessors (mc_bam_n_targets, mc_bam_target,
+ * mc_bam_counts); the handle stays owned by the stream. */
+typedef struct mc_bam_stream mc_bam_stream;
+int mc_bam_stream_open(const char* path, int n_threads, uint32_t flag_filter,
+                       int64_t window_bytes, mc_bam_stream** out);
+int mc_bam_stream_next(mc_bam_stream* s, int64_t cap, int32_t* tid, int32_t* pos,
+                       int32_t* span, int64_t* n_out);
+int mc_bam_stream_header(const mc_bam_stream* s, const mc_bam** header);
+int mc_bam_stream_close(mc_bam_stream* s);
 
 /* ---- BAI index ------------------------------------------------------------
  * The reference opens an indexed BAM (`metacov pileup` needs `samtools

@@ -63,6 +63,7 @@ SIGNATURES = {
     "mc_set_contigs": [_P, _I32, _P],
     "mc_add_reads": [_P, _I64, _P, _P, _P],
     "mc_add_reads_device": [_P, _I64, _P, _P, _P],
+    "mc_add_reads_async": [_P, _I64, _P, _P, _P],
     "mc_add_reads_cigar": [_P, _I64, _P, _P, _P, _P],
     "mc_add_reads_cigar_device": [_P, _I64, _P, _P, _P, _P],
     "mc_clear_reads": [_P],
@@ -88,6 +89,10 @@ SIGNATURES = {
     "mc_bam_intervals": [_P, _P, _P, _P],
     "mc_bam_n_cigar_words": [_P, _PI64],
     "mc_bam_cigars": [_P, _P, _P],
+    "mc_bam_stream_open": [ctypes.c_char_p, ctypes.c_int, _U32, _I64, _PP],
+    "mc_bam_stream_next": [_P, _I64, _P, _P, _P, _PI64],
+    "mc_bam_stream_header": [_P, _PP],
+    "mc_bam_stream_close": [_P],
     "mc_bam_index_build": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int],
     "mc_bam_index_stats": [ctypes.c_char_p, _I32, _P, _P, _PI64],
     "mc_bam_open_contigs": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, _U32, ctypes.c_int, _I32,

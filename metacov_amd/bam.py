@@ -172,3 +172,118 @@ class BamFile:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class BamStream:
+    """Bounded-memory decode (mc_bam_stream_*): the BGZF blocks are inflated a
+    window at a time and the kept records' intervals are read out in batches,
+    in file order.  references / lengths come from the header; record counts
+    grow as the file is consumed."""
+
+    def __init__(self, path, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0):
+        self.filename = os.fspath(getattr(path, "filename", path))
+        self._lib = _lib.load()
+        self._h = ctypes.c_void_p()
+        check(self._lib.mc_bam_stream_open(self.filename.encode(), int(n_threads), int(flag_filter),
+                                           int(window_bytes), ctypes.byref(self._h)))
+        hdr = ctypes.c_void_p()
+        check(self._lib.mc_bam_stream_header(self._h, ctypes.byref(hdr)))
+        self._hdr = hdr
+        n = ctypes.c_int32()
+        check(self._lib.mc_bam_n_targets(hdr, ctypes.byref(n)))
+        names, lengths = [], []
+        for i in range(n.value):
+            nm = ctypes.c_char_p()
+            ln = ctypes.c_int64()
+            check(self._lib.mc_bam_target(hdr, i, ctypes.byref(nm), ctypes.byref(ln)))
+            names.append(nm.value.decode())
+            lengths.append(ln.value)
+        self.references = tuple(names)
+        self.lengths = tuple(lengths)
+
+    def counts(self):
+        """(records, mapped, unmapped) decoded so far."""
+        c = [ctypes.c_int64() for _ in range(4)]
+        check(self._lib.mc_bam_counts(self._hdr, *[ctypes.byref(x) for x in c]))
+        return c[0].value, c[2].value, c[3].value
+
+    def read(self, cap, out=None):
+        """Up to `cap` intervals into `out` = (tid, pos, span) int32 arrays
+        (allocated if None); returns (k, out); k = 0 at the end."""
+        if out is None:
+            out = tuple(np.empty(cap, np.int32) for _ in range(3))
+        k = ctypes.c_int64()
+        check(self._lib.mc_bam_stream_next(self._h, int(cap), *[_lib.ptr(a) for a in out],
+                                           ctypes.byref(k)))
+        return k.value, out
+
+    def close(self):
+        if self._h:
+            self._lib.mc_bam_stream_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+
+def _host_batch(n, pinned):
+    if pinned:
+        import torch
+        ts = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(3)]
+        return tuple(t.numpy() for t in ts), ts
+    return tuple(np.empty(n, np.int32) for _ in range(3)), None
+
+
+class StreamedBam:
+    """The pileup path over a BAM of any size: the file is decoded in windows
+    and fed to the GPU through two pinned host batches (the H2D copy of one
+    overlaps the decode of the next), so host memory stays bounded.  Offers
+    what the CLI uses of BamFile: references, lengths, mapped, unmapped,
+    engine(), local_tid()."""
+
+    def __init__(self, path, device=0, n_threads=0, flag_filter=FLAG_FILTER,
+                 batch_reads=1 << 22, window_bytes=0, pinned=True):
+        from .engine import CoverageEngine
+        self.filename = os.fspath(getattr(path, "filename", path))
+        self.contigs = None
+        with BamStream(self.filename, n_threads, flag_filter, window_bytes) as st:
+            self.references, self.lengths = st.references, st.lengths
+            eng = CoverageEngine(device)
+            eng.set_contigs(np.asarray(self.lengths, dtype=np.int64))
+            bufs = [_host_batch(batch_reads, pinned) for _ in range(2)]
+            k, _ = st.read(batch_reads, bufs[0][0])
+            if k:
+                eng.add_reads_async(*[a[:k] for a in bufs[0][0]])
+            i = 1
+            while True:
+                k, _ = st.read(batch_reads, bufs[i][0])     # overlaps the other batch's copy
+                eng.synchronize()
+                if k == 0:
+                    break
+                eng.add_reads_async(*[a[:k] for a in bufs[i][0]])
+                i ^= 1
+            eng.synchronize()
+            self.n_records, self.mapped, self.unmapped = st.counts()
+        eng.prepare()
+        eng._depth_ready = False
+        self._eng, self._device = eng, device
+
+    def local_tid(self, tid):
+        return tid
+
+    def engine(self, device=0, compute=True):
+        if device != self._device:
+            raise ValueError("a StreamedBam's reads live on device %d" % self._device)
+        if compute and not self._eng._depth_ready:
+            self._eng.compute_depth()
+            self._eng._depth_ready = True
+        return self._eng
+
+    def close(self):
+        self._eng.close()

@@ -28,7 +28,7 @@ import click
 import numpy as np
 
 from . import regions as _regions
-from .bam import BamFile, index_stats
+from .bam import BamFile, StreamedBam, index_stats
 from .engine import REGION_STAT_DTYPE, classic_stats
 
 logging.basicConfig(level=logging.INFO,
@@ -60,8 +60,11 @@ def main():
 @click.option('--outfile', '-o', type=click.File('w'), default="-",
               help="Output CSV (default STDOUT)")
 @click.option('--device', type=int, default=0, help="HIP device ordinal")
+@click.option('--stream/--no-stream', default=None,
+              help="Decode in bounded-memory windows, feeding the GPU through pinned double "
+                   "buffers (default: when the BAM is larger than 2 GiB)")
 def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
-           kmer_histogram, kmer_length, outfile, device):
+           kmer_histogram, kmer_length, outfile, device, stream):
     """
     Compute fold coverage values
     """
@@ -70,7 +73,9 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
                                "the metacov_amd engine")
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile)
-    bam = BamFile(bamfile.name)
+    if stream is None:
+        stream = os.path.getsize(bamfile.name) > (2 << 30)
+    bam = StreamedBam(bamfile.name, device=device) if stream else BamFile(bamfile.name)
     regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam))
     log_counts(bam)
     write_rows(bam, regions, outfile, device=device)

@@ -14,6 +14,7 @@
 // tag behind a `<l_seq>S<rlen>N` placeholder (SAMv1 §4.2.2), as htslib's
 // bam_read1 resolves it.
 #include <chrono>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -22,49 +23,24 @@
 
 using namespace mc::bgzf;
 
-extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter, int keep_cigar,
-                           mc_bam** out) {
-    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
-    *out = nullptr;
-    MappedFile mf;
-    if (int rc = mf.open(path)) return rc;
+namespace {
 
-    std::vector<Block> blocks;
-    size_t total = 0;
-    if (int rc = scan_blocks(mf.data, mf.size, 0, SIZE_MAX, blocks, total)) return rc;
-    // uninitialised: the inflate threads fault the pages in, in parallel
-    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total + 8]);
-    MC_REQUIRE(buf, MC_E_IO, "cannot allocate %zu bytes for %s", total, path);
-    const bool timing = std::getenv("MC_DECODE_TIMING") != nullptr;
-    auto t_start = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!timing) return;
-        const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[mc_bam_open] %-10s %8.3f s\n", what,
-                     std::chrono::duration<double>(now - t_start).count());
-        t_start = now;
-    };
-    int nt = n_threads_or_all(n_threads);
-    nt = std::max(1, std::min<int>(nt, (int)blocks.size()));
-    MC_REQUIRE(inflate_blocks(mf.data, blocks, buf.get(), nt), MC_E_IO, "BGZF inflate failed in %s",
-               path);
-    lap("inflate");
-
-    const uint8_t* d = buf.get();
-    const size_t n = total;
-    std::vector<std::string> names;
-    std::vector<int64_t> lens;
-    size_t o = 0;
-    if (int rc = parse_header(d, n, path, names, lens, &o)) return rc;
-    const int32_t n_ref = (int32_t)names.size();
-    mc_bam* bam = new mc_bam();
-    bam->keep_cigar = keep_cigar != 0;
-    bam->names = std::move(names);
-    bam->lens = std::move(lens);
+// Parses the BAM records in d[o, n) and appends the kept ones to `bam`.
+// partial: d may end inside a record (a streaming window); parsing stops
+// before it and *consumed is its offset.  Otherwise the records must tile
+// [o, n) exactly.
+int parse_records(const uint8_t* d, size_t o, size_t n, bool partial, int32_t n_ref,
+                  uint32_t flag_filter, int nt, mc_bam* bam, size_t* consumed, const char* path,
+                  const std::function<void(const char*)>& lap) {
     auto fail = [&](const char* msg, size_t at) {
-        delete bam;
         mc::set_error("%s: %s at byte %zu of the inflated stream", path, msg, at);
         return MC_E_IO;
+    };
+    // a complete record starts at q
+    auto complete = [&](size_t q) -> bool {
+        if (q + 4 > n) return false;
+        const int32_t bs = rdi32(d + q);
+        return bs >= 32 && q + 4 + (size_t)bs <= n;
     };
     // ---- records: the stream is cut into byte ranges; each range finds its
     // first record start in parallel (a candidate offset must begin a chain
@@ -96,6 +72,10 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
         }
         return limit;
     };
+    if (o >= n) {
+        *consumed = n;
+        return MC_OK;
+    }
     const size_t nseg_target = std::max<size_t>(1, std::min<size_t>((size_t)nt * 4, (n - o) / (1 << 20) + 1));
     std::vector<size_t> seg_off(nseg_target + 1);
     seg_off[0] = o;
@@ -114,6 +94,7 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
     }
     // verify that consecutive ranges meet; fall back to the sequential walk
     bool chained = true;
+    size_t tail_end = n;
     {
         std::vector<char> ok(nseg_target, 1);
         std::vector<std::thread> pool;
@@ -121,15 +102,18 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
         auto w = [&]() {
             for (size_t i; (i = nx.fetch_add(1)) < nseg_target;) {
                 size_t q = seg_off[i];
+                const bool last = i + 1 == nseg_target;
                 const size_t end = seg_off[i + 1];
                 if (q > end) { ok[i] = 0; continue; }
                 while (q < end) {
-                    if (q + 4 > n) { ok[i] = 0; break; }
-                    const int32_t bs = rdi32(d + q);
-                    if (bs < 32 || q + 4 + (size_t)bs > n) { ok[i] = 0; break; }
-                    q += 4 + (size_t)bs;
+                    if (!complete(q)) {
+                        if (!(last && partial)) ok[i] = 0;
+                        break;
+                    }
+                    q += 4 + (size_t)rdi32(d + q);
                 }
-                if (q != end) ok[i] = 0;
+                if (last && partial) tail_end = q;     // the window's last complete record ends here
+                else if (q != end) ok[i] = 0;
             }
         };
         for (int i = 1; i < nt; ++i) pool.emplace_back(w);
@@ -141,21 +125,30 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
         seg_off.assign(1, o);
         size_t q = o;
         while (q < n) {
-            if (q + 4 > n) return fail("truncated record", q);
-            const int32_t bs = rdi32(d + q);
-            if (bs < 32 || q + 4 + (size_t)bs > n) return fail("bad record size", q);
-            q += 4 + (size_t)bs;
+            if (!complete(q)) {
+                if (partial) break;
+                return fail(q + 4 > n ? "truncated record" : "bad record size", q);
+            }
+            q += 4 + (size_t)rdi32(d + q);
         }
-        seg_off.push_back(n);
+        tail_end = q;
+        seg_off.push_back(q);
+    } else {
+        seg_off.back() = tail_end;
     }
+    *consumed = tail_end;
     // drop empty ranges
     seg_off.erase(std::unique(seg_off.begin(), seg_off.end()), seg_off.end());
-    if (seg_off.size() < 2) seg_off.push_back(n);
+    if (seg_off.size() < 2) seg_off.push_back(tail_end);
     lap("boundaries");
     const size_t nseg = seg_off.size() - 1;
     struct SegCount { int64_t kept = 0, words = 0, mapped = 0, unmapped = 0, records = 0; int err = 0; size_t err_at = 0; };
     std::vector<SegCount> sc(nseg);
     std::vector<int64_t> kept_off(nseg + 1, 0), word_off(nseg + 1, 0);
+    // append after what `bam` already holds
+    kept_off[0] = (int64_t)bam->tid.size();
+    word_off[0] = bam->keep_cigar ? (int64_t)bam->cigar.size() : 0;
+    if (bam->keep_cigar && bam->cig_off.empty()) bam->cig_off.push_back(0);
     auto run_pass = [&](int pass) {
         std::atomic<size_t> next_seg{0};
         auto work = [&]() {
@@ -235,12 +228,61 @@ extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter
     bam->span.resize(kept_off[nseg]);
     if (bam->keep_cigar) {
         bam->cigar.resize(word_off[nseg]);
-        bam->cig_off.assign(kept_off[nseg] + 1, 0);
+        bam->cig_off.resize(kept_off[nseg] + 1, 0);
     }
     run_pass(1);
     lap("fill");
     for (size_t g = 0; g < nseg; ++g)
         if (sc[g].err) return fail("reference span exceeds int32", sc[g].err_at);
+    return MC_OK;
+}
+
+}  // namespace
+
+extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter, int keep_cigar,
+                           mc_bam** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    MappedFile mf;
+    if (int rc = mf.open(path)) return rc;
+
+    std::vector<Block> blocks;
+    size_t total = 0;
+    if (int rc = scan_blocks(mf.data, mf.size, 0, SIZE_MAX, blocks, total)) return rc;
+    // uninitialised: the inflate threads fault the pages in, in parallel
+    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total + 8]);
+    MC_REQUIRE(buf, MC_E_IO, "cannot allocate %zu bytes for %s", total, path);
+    const bool timing = std::getenv("MC_DECODE_TIMING") != nullptr;
+    auto t_start = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[mc_bam_open] %-10s %8.3f s\n", what,
+                     std::chrono::duration<double>(now - t_start).count());
+        t_start = now;
+    };
+    int nt = n_threads_or_all(n_threads);
+    nt = std::max(1, std::min<int>(nt, (int)blocks.size()));
+    MC_REQUIRE(inflate_blocks(mf.data, blocks, buf.get(), nt), MC_E_IO, "BGZF inflate failed in %s",
+               path);
+    lap("inflate");
+
+    const uint8_t* d = buf.get();
+    const size_t n = total;
+    std::vector<std::string> names;
+    std::vector<int64_t> lens;
+    size_t o = 0;
+    if (int rc = parse_header(d, n, path, names, lens, &o)) return rc;
+    const int32_t n_ref = (int32_t)names.size();
+    mc_bam* bam = new mc_bam();
+    bam->keep_cigar = keep_cigar != 0;
+    bam->names = std::move(names);
+    bam->lens = std::move(lens);
+    size_t consumed = 0;
+    if (int rc = parse_records(d, o, n, false, n_ref, flag_filter, nt, bam, &consumed, path, lap)) {
+        delete bam;
+        return rc;
+    }
     *out = bam;
     return MC_OK;
 }
@@ -300,5 +342,139 @@ extern "C" int mc_bam_cigars(const mc_bam* bam, int64_t* cig_off, uint32_t* ciga
         MC_REQUIRE(cigar, MC_E_INVALID, "null cigar");
         std::memcpy(cigar, bam->cigar.data(), bam->cigar.size() * 4);
     }
+    return MC_OK;
+}
+
+// ---- streaming decode ------------------------------------------------------
+//
+// Bounded memory: BGZF blocks are inflated a window at a time (on all
+// threads), the window's complete records are parsed (the parallel parse
+// above, in partial mode) and a record cut by the window end is carried into
+// the next window.  Intervals are handed out in caller-sized batches.
+struct mc_bam_stream {
+    MappedFile mf;
+    std::string path;
+    int nt = 1;
+    uint32_t flag_filter = 0;
+    size_t window = 0;                // inflated bytes per window
+    size_t next_off = 0;              // file offset of the next BGZF block
+    std::vector<uint8_t> buf;         // carried bytes + the current window
+    size_t carry = 0;
+    int32_t n_ref = 0;
+    mc_bam out;                       // header, counters, parsed intervals not yet handed out
+    size_t out_pos = 0;
+    bool eof = false;
+};
+
+namespace {
+
+// Inflates the next window of blocks after the carried bytes; returns the
+// number of new bytes (0 at the end of the file).
+int stream_fill(mc_bam_stream* s, size_t* added) {
+    std::vector<Block> blocks;
+    size_t total = 0;
+    while (s->next_off < s->mf.size && total < s->window) {
+        const size_t first = blocks.size();
+        if (int rc = scan_blocks(s->mf.data, s->mf.size, s->next_off, s->next_off, blocks, total))
+            return rc;
+        const Block& b = blocks[first];
+        s->next_off = b.cdata + b.clen + 8;
+    }
+    s->buf.resize(s->carry + total + 8);
+    MC_REQUIRE(blocks.empty() || inflate_blocks(s->mf.data, blocks, s->buf.data() + s->carry, s->nt),
+               MC_E_IO, "BGZF inflate failed in %s", s->path.c_str());
+    *added = total;
+    return MC_OK;
+}
+
+// Parses buf[from, carry + added) (partial unless the file is done) and
+// keeps the unparsed tail as the next carry.
+int stream_parse(mc_bam_stream* s, size_t from, size_t added) {
+    const size_t n = s->carry + added;
+    const bool last = s->next_off >= s->mf.size;
+    if (s->out_pos) {                 // drop what was already handed out
+        s->out.tid.erase(s->out.tid.begin(), s->out.tid.begin() + s->out_pos);
+        s->out.pos.erase(s->out.pos.begin(), s->out.pos.begin() + s->out_pos);
+        s->out.span.erase(s->out.span.begin(), s->out.span.begin() + s->out_pos);
+        s->out_pos = 0;
+    }
+    size_t consumed = from;
+    const std::function<void(const char*)> nolap = [](const char*) {};
+    if (int rc = parse_records(s->buf.data(), from, n, !last, s->n_ref, s->flag_filter, s->nt,
+                               &s->out, &consumed, s->path.c_str(), nolap))
+        return rc;
+    s->carry = n - consumed;
+    if (s->carry) std::memmove(s->buf.data(), s->buf.data() + consumed, s->carry);
+    if (last) {
+        MC_REQUIRE(s->carry == 0, MC_E_IO, "%s: truncated record at the end of the file",
+                   s->path.c_str());
+        s->eof = true;
+    }
+    return MC_OK;
+}
+
+}  // namespace
+
+extern "C" int mc_bam_stream_open(const char* path, int n_threads, uint32_t flag_filter,
+                                  int64_t window_bytes, mc_bam_stream** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<mc_bam_stream> s(new mc_bam_stream());
+    if (int rc = s->mf.open(path)) return rc;
+    s->path = path;
+    s->nt = n_threads_or_all(n_threads);
+    s->flag_filter = flag_filter;
+    s->window = (size_t)std::max<int64_t>(window_bytes > 0 ? window_bytes : (256ll << 20), 1 << 16);
+    // header: windows until the reference list parses, then the first records
+    size_t o = 0;
+    for (;;) {
+        size_t added = 0;
+        if (int rc = stream_fill(s.get(), &added)) return rc;
+        s->carry += added;
+        std::vector<std::string> names;
+        std::vector<int64_t> lens;
+        if (parse_header(s->buf.data(), s->carry, path, names, lens, &o) == MC_OK) {
+            s->out.names = std::move(names);
+            s->out.lens = std::move(lens);
+            break;
+        }
+        MC_REQUIRE(s->next_off < s->mf.size, MC_E_IO, "%s: no valid BAM header", path);
+    }
+    s->n_ref = (int32_t)s->out.names.size();
+    const size_t have = s->carry;
+    s->carry = 0;
+    if (int rc = stream_parse(s.get(), o, have)) return rc;
+    *out = s.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_stream_next(mc_bam_stream* s, int64_t cap, int32_t* tid, int32_t* pos,
+                                  int32_t* span, int64_t* n_out) {
+    MC_REQUIRE(s && n_out && cap >= 0 && (cap == 0 || (tid && pos && span)), MC_E_INVALID,
+               "bad argument");
+    while ((int64_t)(s->out.tid.size() - s->out_pos) < cap && !s->eof) {
+        size_t added = 0;
+        if (int rc = stream_fill(s, &added)) return rc;
+        if (int rc = stream_parse(s, 0, added)) return rc;
+    }
+    const int64_t k = std::min<int64_t>(cap, (int64_t)(s->out.tid.size() - s->out_pos));
+    if (k) {
+        std::memcpy(tid, s->out.tid.data() + s->out_pos, k * 4);
+        std::memcpy(pos, s->out.pos.data() + s->out_pos, k * 4);
+        std::memcpy(span, s->out.span.data() + s->out_pos, k * 4);
+        s->out_pos += (size_t)k;
+    }
+    *n_out = k;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_stream_header(const mc_bam_stream* s, const mc_bam** header) {
+    MC_REQUIRE(s && header, MC_E_INVALID, "null argument");
+    *header = &s->out;      // names, lengths and (so far) counts via the mc_bam accessors
+    return MC_OK;
+}
+
+extern "C" int mc_bam_stream_close(mc_bam_stream* s) {
+    delete s;
     return MC_OK;
 }

@@ -296,7 +296,7 @@ static int reserve_reads(mc_ctx* ctx, int64_t n_total, bool cigar_mode) {
 }
 
 static int add_reads_impl(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
-                          const int32_t* span, hipMemcpyKind kind) {
+                          const int32_t* span, hipMemcpyKind kind, bool wait = true) {
     if (int rc = ctx_use(ctx)) return rc;
     MC_REQUIRE(n >= 0, MC_E_INVALID, "negative read count");
     MC_REQUIRE(n == 0 || (tid && pos && span), MC_E_INVALID, "null read array");
@@ -308,7 +308,7 @@ static int add_reads_impl(mc_ctx* ctx, int64_t n, const int32_t* tid, const int3
         HIP_TRY(hipMemcpyAsync(ctx->d_tid.p + o, tid, n * 4, kind, ctx->stream));
         HIP_TRY(hipMemcpyAsync(ctx->d_pos.p + o, pos, n * 4, kind, ctx->stream));
         HIP_TRY(hipMemcpyAsync(ctx->d_span.p + o, span, n * 4, kind, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (wait) HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     ctx->n_reads += n;
     invalidate(ctx);
@@ -318,6 +318,14 @@ static int add_reads_impl(mc_ctx* ctx, int64_t n, const int32_t* tid, const int3
 extern "C" int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
                             const int32_t* span) {
     return add_reads_impl(ctx, n, tid, pos, span, hipMemcpyHostToDevice);
+}
+
+// Host batch copied asynchronously on the ctx stream (pinned buffers: DMA
+// overlapped with the caller's next decode); the buffers must stay unchanged
+// until mc_synchronize.
+extern "C" int mc_add_reads_async(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,
+                                  const int32_t* span) {
+    return add_reads_impl(ctx, n, tid, pos, span, hipMemcpyHostToDevice, false);
 }
 
 extern "C" int mc_add_reads_device(mc_ctx* ctx, int64_t n, const int32_t* tid, const int32_t* pos,

@@ -128,6 +128,15 @@ class CoverageEngine:
             raise ValueError("tid/pos/span lengths differ")
         self._check(self._lib.mc_add_reads(self._h, n, *[ptr(a) for a in arrs]))
 
+    def add_reads_async(self, tid, pos, span):
+        """Host int32 arrays (pinned for a real overlap) copied asynchronously
+        on the ctx stream; keep them unchanged until synchronize()."""
+        arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (tid, pos, span)]
+        if any(a.ctypes.data != np.asarray(b).ctypes.data for a, b in zip(arrs, (tid, pos, span))):
+            raise ValueError("add_reads_async needs contiguous int32 arrays (no copies)")
+        n = len(arrs[0])
+        self._check(self._lib.mc_add_reads_async(self._h, n, *[ptr(a) for a in arrs]))
+
     def add_reads_cigar(self, tid, pos, cig_off, cigar):
         tid = np.ascontiguousarray(tid, dtype=np.int32)
         pos = np.ascontiguousarray(pos, dtype=np.int32)

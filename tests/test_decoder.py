@@ -183,3 +183,47 @@ def test_index_errors(lib_built, tmp_path, golden_dir):
     from metacov_amd.bam import build_index
     with pytest.raises(MetacovError, match="coordinate-sorted"):
         build_index(p)
+
+
+# ---- streaming decode (mc_bam_stream_*) ------------------------------------
+
+def _drain(st, cap):
+    parts = []
+    while True:
+        k, out = st.read(cap)
+        if k == 0:
+            break
+        parts.append([a[:k].copy() for a in out])
+    if not parts:
+        return [np.zeros(0, np.int32)] * 3
+    return [np.concatenate([x[i] for x in parts]) for i in range(3)]
+
+
+@pytest.mark.parametrize("window", [1 << 16, 1 << 20, 0])
+def test_stream_equals_full_decode(lib_built, golden_dir, tmp_path, window):
+    """Windows far smaller than one record (the 140 000-op CG record) and
+    batch sizes that cut windows: the same intervals and counts."""
+    from metacov_amd.bam import BamStream
+    lengths = [2_000_000, 700, 300_000]
+    arrs = synth.edge_mix_arrays(lengths, 300_000, seed=4)
+    p = str(tmp_path / "s.bam")
+    synth.write_bam_fast(p, ["a", "b", "c"], lengths, *arrs, level=1, n_threads=4)
+    for path in (p, os.path.join(golden_dir, "bbmap.sorted.bam"),
+                 os.path.join(golden_dir, "synth_longcigar.bam")):
+        full = BamFile(path)
+        with BamStream(path, n_threads=3, window_bytes=window) as st:
+            assert st.references == full.references and st.lengths == full.lengths
+            got = _drain(st, 12_345)
+            assert st.counts() == (full.n_records, full.mapped, full.unmapped)
+        for g, w in zip(got, (full.tid, full.pos, full.span)):
+            assert np.array_equal(g, w)
+
+
+def test_stream_truncated(lib_built, golden_dir, tmp_path):
+    from metacov_amd.bam import BamStream
+    raw = open(os.path.join(golden_dir, "bbmap.sorted.bam"), "rb").read()
+    t = tmp_path / "trunc.bam"
+    t.write_bytes(raw[: len(raw) // 2])
+    with pytest.raises(MetacovError):
+        with BamStream(str(t), window_bytes=1 << 16) as st:
+            _drain(st, 1000)

@@ -519,3 +519,35 @@ def test_cigar_device_batches(lib_built):
         a.add_reads_cigar_device(t_tid, t_pos, cig_off, cigar)   # reads already present
     a.close()
     b.close()
+
+
+def test_streamed_ingest_and_cli(lib_built, golden_dir, tmp_path):
+    """StreamedBam (windowed decode, pinned double-buffered async H2D) gives
+    the rows of the whole-file decode; the CLI's --stream CSV is identical."""
+    from click.testing import CliRunner
+    from metacov_amd.bam import StreamedBam
+    from metacov_amd.cli import pileup as cli_pileup
+    lengths = [1_500_000, 800, 600_000]
+    arrs = synth.edge_mix_arrays(lengths, 400_000, seed=8)
+    p = str(tmp_path / "s.bam")
+    synth.write_bam_fast(p, ["a", "b", "c"], lengths, *arrs, level=1, n_threads=4)
+    full = BamFile(p)
+    sb = StreamedBam(p, batch_reads=50_000, window_bytes=1 << 20)
+    assert (sb.mapped, sb.unmapped) == (full.mapped, full.unmapped)
+    rt = np.array([0, 2, 1, 0], np.int32)
+    rs = np.array([0, 10, 0, 999_000], np.int64)
+    re_ = np.array([1_500_000, 600_000, 900, 1_600_000], np.int64)
+    a = full.engine(0, compute=False).compute_depth_stats(rt, rs, re_)
+    b = sb.engine(0, compute=False).compute_depth_stats(rt, rs, re_)
+    for f in a.dtype.names:
+        assert np.array_equal(a[f], b[f]), f
+    sb.close()
+    full.close()
+    outs = []
+    for flag in ("--stream", "--no-stream"):
+        o = tmp_path / ("o%s.csv" % flag)
+        res = CliRunner().invoke(cli_pileup, ["-b", os.path.join(golden_dir, "synth_multi.bam"),
+                                              flag, "-o", str(o)])
+        assert res.exit_code == 0, res.output
+        outs.append(open(o, newline="").read())
+    assert outs[0] == outs[1] and outs[0].count("\n") == 8
