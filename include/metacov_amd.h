@@ -105,6 +105,10 @@ int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid,
 int mc_add_reads_async(mc_ctx* ctx, int64_t n, const int32_t* tid,
                        const int32_t* pos, const int32_t* span);
 
+/* Page-locked host buffers for mc_add_reads_async (hipHostMalloc). */
+int mc_pinned_alloc(int64_t bytes, void** out);
+int mc_pinned_free(void* p);
+
 /* Same, but the three arrays are already in this ctx's device memory
  * (e.g. torch tensors); they are copied into the ctx. */
 int mc_add_reads_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,

@@ -64,6 +64,8 @@ SIGNATURES = {
     "mc_add_reads": [_P, _I64, _P, _P, _P],
     "mc_add_reads_device": [_P, _I64, _P, _P, _P],
     "mc_add_reads_async": [_P, _I64, _P, _P, _P],
+    "mc_pinned_alloc": [_I64, _PP],
+    "mc_pinned_free": [_P],
     "mc_add_reads_cigar": [_P, _I64, _P, _P, _P, _P],
     "mc_add_reads_cigar_device": [_P, _I64, _P, _P, _P, _P],
     "mc_clear_reads": [_P],

@@ -232,11 +232,30 @@ class BamStream:
         self.close()
 
 
+class PinnedInt32:
+    """int32 numpy array over page-locked host memory (mc_pinned_alloc), so
+    mc_add_reads_async's DMA overlaps the host's next decode."""
+
+    def __init__(self, n):
+        self._lib = _lib.load()
+        self._p = ctypes.c_void_p()
+        check(self._lib.mc_pinned_alloc(int(n) * 4, ctypes.byref(self._p)))
+        self.array = np.ctypeslib.as_array((ctypes.c_int32 * int(n)).from_address(self._p.value))
+
+    def free(self):
+        if self._p:
+            self.array = None
+            self._lib.mc_pinned_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.free()
+
+
 def _host_batch(n, pinned):
     if pinned:
-        import torch
-        ts = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(3)]
-        return tuple(t.numpy() for t in ts), ts
+        bufs = [PinnedInt32(n) for _ in range(3)]
+        return tuple(b.array for b in bufs), bufs
     return tuple(np.empty(n, np.int32) for _ in range(3)), None
 
 

@@ -320,6 +320,19 @@ extern "C" int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid, const in
     return add_reads_impl(ctx, n, tid, pos, span, hipMemcpyHostToDevice);
 }
 
+// Page-locked host memory for async ingest batches (hipHostMalloc).
+extern "C" int mc_pinned_alloc(int64_t bytes, void** out) {
+    MC_REQUIRE(out && bytes > 0, MC_E_INVALID, "bad argument");
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    return MC_OK;
+}
+
+extern "C" int mc_pinned_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return MC_OK;
+}
+
 // Host batch copied asynchronously on the ctx stream (pinned buffers: DMA
 // overlapped with the caller's next decode); the buffers must stay unchanged
 // until mc_synchronize.
