@@ -60,9 +60,9 @@ def main():
 @click.option('--outfile', '-o', type=click.File('w'), default="-",
               help="Output CSV (default STDOUT)")
 @click.option('--device', type=int, default=0, help="HIP device ordinal")
-@click.option('--stream/--no-stream', default=None,
+@click.option('--stream/--no-stream', default=True,
               help="Decode in bounded-memory windows, feeding the GPU through pinned double "
-                   "buffers (default: when the BAM is larger than 2 GiB)")
+                   "buffers (default; --no-stream decodes the whole file into host memory first)")
 def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
            kmer_histogram, kmer_length, outfile, device, stream):
     """
@@ -73,8 +73,6 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
                                "the metacov_amd engine")
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile)
-    if stream is None:
-        stream = os.path.getsize(bamfile.name) > (2 << 30)
     bam = StreamedBam(bamfile.name, device=device) if stream else BamFile(bamfile.name)
     regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam))
     log_counts(bam)
