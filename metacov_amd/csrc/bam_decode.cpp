@@ -239,54 +239,6 @@ int parse_records(const uint8_t* d, size_t o, size_t n, bool partial, int32_t n_
 
 }  // namespace
 
-extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter, int keep_cigar,
-                           mc_bam** out) {
-    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
-    *out = nullptr;
-    MappedFile mf;
-    if (int rc = mf.open(path)) return rc;
-
-    std::vector<Block> blocks;
-    size_t total = 0;
-    if (int rc = scan_blocks(mf.data, mf.size, 0, SIZE_MAX, blocks, total)) return rc;
-    // uninitialised: the inflate threads fault the pages in, in parallel
-    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total + 8]);
-    MC_REQUIRE(buf, MC_E_IO, "cannot allocate %zu bytes for %s", total, path);
-    const bool timing = std::getenv("MC_DECODE_TIMING") != nullptr;
-    auto t_start = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!timing) return;
-        const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[mc_bam_open] %-10s %8.3f s\n", what,
-                     std::chrono::duration<double>(now - t_start).count());
-        t_start = now;
-    };
-    int nt = n_threads_or_all(n_threads);
-    nt = std::max(1, std::min<int>(nt, (int)blocks.size()));
-    MC_REQUIRE(inflate_blocks(mf.data, blocks, buf.get(), nt), MC_E_IO, "BGZF inflate failed in %s",
-               path);
-    lap("inflate");
-
-    const uint8_t* d = buf.get();
-    const size_t n = total;
-    std::vector<std::string> names;
-    std::vector<int64_t> lens;
-    size_t o = 0;
-    if (int rc = parse_header(d, n, path, names, lens, &o)) return rc;
-    const int32_t n_ref = (int32_t)names.size();
-    mc_bam* bam = new mc_bam();
-    bam->keep_cigar = keep_cigar != 0;
-    bam->names = std::move(names);
-    bam->lens = std::move(lens);
-    size_t consumed = 0;
-    if (int rc = parse_records(d, o, n, false, n_ref, flag_filter, nt, bam, &consumed, path, lap)) {
-        delete bam;
-        return rc;
-    }
-    *out = bam;
-    return MC_OK;
-}
-
 extern "C" int mc_bam_close(mc_bam* bam) {
     delete bam;
     return MC_OK;
@@ -415,16 +367,17 @@ int stream_parse(mc_bam_stream* s, size_t from, size_t added) {
 
 }  // namespace
 
-extern "C" int mc_bam_stream_open(const char* path, int n_threads, uint32_t flag_filter,
-                                  int64_t window_bytes, mc_bam_stream** out) {
-    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
-    *out = nullptr;
-    std::unique_ptr<mc_bam_stream> s(new mc_bam_stream());
+namespace {
+
+int stream_open(const char* path, int n_threads, uint32_t flag_filter, int64_t window_bytes,
+                bool keep_cigar, std::unique_ptr<mc_bam_stream>& s) {
+    s.reset(new mc_bam_stream());
     if (int rc = s->mf.open(path)) return rc;
     s->path = path;
     s->nt = n_threads_or_all(n_threads);
     s->flag_filter = flag_filter;
     s->window = (size_t)std::max<int64_t>(window_bytes > 0 ? window_bytes : (256ll << 20), 1 << 16);
+    s->out.keep_cigar = keep_cigar;
     // header: windows until the reference list parses, then the first records
     size_t o = 0;
     for (;;) {
@@ -443,8 +396,35 @@ extern "C" int mc_bam_stream_open(const char* path, int n_threads, uint32_t flag
     s->n_ref = (int32_t)s->out.names.size();
     const size_t have = s->carry;
     s->carry = 0;
-    if (int rc = stream_parse(s.get(), o, have)) return rc;
+    return stream_parse(s.get(), o, have);
+}
+
+}  // namespace
+
+extern "C" int mc_bam_stream_open(const char* path, int n_threads, uint32_t flag_filter,
+                                  int64_t window_bytes, mc_bam_stream** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<mc_bam_stream> s;
+    if (int rc = stream_open(path, n_threads, flag_filter, window_bytes, false, s)) return rc;
     *out = s.release();
+    return MC_OK;
+}
+
+// The whole file: the same windows (the buffer stays warm instead of faulting
+// in the entire inflated file), every kept interval accumulated.
+extern "C" int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter, int keep_cigar,
+                           mc_bam** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<mc_bam_stream> s;
+    if (int rc = stream_open(path, n_threads, flag_filter, 0, keep_cigar != 0, s)) return rc;
+    while (!s->eof) {
+        size_t added = 0;
+        if (int rc = stream_fill(s.get(), &added)) return rc;
+        if (int rc = stream_parse(s.get(), 0, added)) return rc;
+    }
+    *out = new mc_bam(std::move(s->out));
     return MC_OK;
 }
 
