@@ -25,7 +25,7 @@ def build(verbose=True, extra_flags=()):
         return LIB
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", *extra_flags,
-           "-o", LIB + ".tmp", *srcs, "-lz", "-lpthread"]
+           "-o", LIB + ".tmp", *srcs, "-lz", "-lpthread", "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

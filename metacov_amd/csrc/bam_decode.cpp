@@ -310,19 +310,33 @@ struct mc_bam_stream {
     uint32_t flag_filter = 0;
     size_t window = 0;                // inflated bytes per window
     size_t next_off = 0;              // file offset of the next BGZF block
-    std::vector<uint8_t> buf;         // carried bytes + the current window
+    std::unique_ptr<uint8_t[]> buf;   // carried bytes + the current window (uninitialised)
+    size_t cap = 0;
     size_t carry = 0;
     int32_t n_ref = 0;
     mc_bam out;                       // header, counters, parsed intervals not yet handed out
     size_t out_pos = 0;
     bool eof = false;
+    double t_scan = 0, t_inflate = 0, t_parse = 0;   // MC_DECODE_TIMING
+    ~mc_bam_stream() {
+        if (std::getenv("MC_DECODE_TIMING"))
+            std::fprintf(stderr, "[bam stream] scan %.3f s  inflate %.3f s  parse %.3f s\n", t_scan,
+                         t_inflate, t_parse);
+    }
 };
+
+namespace {
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
 
 namespace {
 
 // Inflates the next window of blocks after the carried bytes; returns the
 // number of new bytes (0 at the end of the file).
 int stream_fill(mc_bam_stream* s, size_t* added) {
+    const double t0 = now_s();
     std::vector<Block> blocks;
     size_t total = 0;
     while (s->next_off < s->mf.size && total < s->window) {
@@ -332,9 +346,20 @@ int stream_fill(mc_bam_stream* s, size_t* added) {
         const Block& b = blocks[first];
         s->next_off = b.cdata + b.clen + 8;
     }
-    s->buf.resize(s->carry + total + 8);
-    MC_REQUIRE(blocks.empty() || inflate_blocks(s->mf.data, blocks, s->buf.data() + s->carry, s->nt),
+    const size_t need = s->carry + total + 8;
+    if (need > s->cap) {              // grow without zero-filling; keep the carried bytes
+        const size_t ncap = std::max(need, s->cap + s->cap / 4);
+        std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[ncap]);
+        MC_REQUIRE(nb, MC_E_IO, "cannot allocate %zu bytes for %s", ncap, s->path.c_str());
+        if (s->carry) std::memcpy(nb.get(), s->buf.get(), s->carry);
+        s->buf = std::move(nb);
+        s->cap = ncap;
+    }
+    const double t1 = now_s();
+    MC_REQUIRE(blocks.empty() || inflate_blocks(s->mf.data, blocks, s->buf.get() + s->carry, s->nt),
                MC_E_IO, "BGZF inflate failed in %s", s->path.c_str());
+    s->t_scan += t1 - t0;
+    s->t_inflate += now_s() - t1;
     *added = total;
     return MC_OK;
 }
@@ -351,12 +376,14 @@ int stream_parse(mc_bam_stream* s, size_t from, size_t added) {
         s->out_pos = 0;
     }
     size_t consumed = from;
+    const double t0 = now_s();
     const std::function<void(const char*)> nolap = [](const char*) {};
-    if (int rc = parse_records(s->buf.data(), from, n, !last, s->n_ref, s->flag_filter, s->nt,
+    if (int rc = parse_records(s->buf.get(), from, n, !last, s->n_ref, s->flag_filter, s->nt,
                                &s->out, &consumed, s->path.c_str(), nolap))
         return rc;
     s->carry = n - consumed;
-    if (s->carry) std::memmove(s->buf.data(), s->buf.data() + consumed, s->carry);
+    if (s->carry) std::memmove(s->buf.get(), s->buf.get() + consumed, s->carry);
+    s->t_parse += now_s() - t0;
     if (last) {
         MC_REQUIRE(s->carry == 0, MC_E_IO, "%s: truncated record at the end of the file",
                    s->path.c_str());
@@ -386,7 +413,7 @@ int stream_open(const char* path, int n_threads, uint32_t flag_filter, int64_t w
         s->carry += added;
         std::vector<std::string> names;
         std::vector<int64_t> lens;
-        if (parse_header(s->buf.data(), s->carry, path, names, lens, &o) == MC_OK) {
+        if (parse_header(s->buf.get(), s->carry, path, names, lens, &o) == MC_OK) {
             s->out.names = std::move(names);
             s->out.lens = std::move(lens);
             break;

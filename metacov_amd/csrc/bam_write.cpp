@@ -1,12 +1,16 @@
 // BAM writer for synthetic workloads (the role `metacov simulate` plays in
 // the reference, metacov/cli.py:288-414, without ART): records from SoA
 // arrays, BGZF blocks deflated in parallel (each block is independent).
-// Sequence bases are 'A', qualities 30, names "r<index>".
+// Bases and qualities are pseudo-random per record (uniform ACGT, Phred 2-40)
+// so the files compress like real BAMs (~3x), names are "r<index>".  Blocks
+// are deflated with libdeflate when the image has it (dlopen), else zlib.
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -38,20 +42,65 @@ int reg2bin(int64_t beg, int64_t end) {
     return 0;
 }
 
-// one BGZF block (header + raw deflate + crc + isize) for <= 65280 bytes
-bool bgzf_block(const uint8_t* src, size_t n, int level, std::vector<uint8_t>& out) {
-    out.resize(18 + compressBound((uLong)n) + 8 + 64);
+struct LibdeflateC {
+    void* (*alloc)(int) = nullptr;
+    size_t (*compress)(void*, const void*, size_t, void*, size_t) = nullptr;
+    void (*free_c)(void*) = nullptr;
+    bool ok = false;
+    LibdeflateC() {
+        if (std::getenv("MC_NO_LIBDEFLATE")) return;
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = reinterpret_cast<void* (*)(int)>(dlsym(h, "libdeflate_alloc_compressor"));
+        compress = reinterpret_cast<size_t (*)(void*, const void*, size_t, void*, size_t)>(
+            dlsym(h, "libdeflate_deflate_compress"));
+        free_c = reinterpret_cast<void (*)(void*)>(dlsym(h, "libdeflate_free_compressor"));
+        ok = alloc && compress && free_c;
+    }
+};
+
+const LibdeflateC& libdeflate_c() {
+    static const LibdeflateC ld;
+    return ld;
+}
+
+// raw deflate of src[0, n) into dst (capacity cap); returns the size, 0 on failure
+size_t deflate_raw(const uint8_t* src, size_t n, int level, uint8_t* dst, size_t cap) {
+    const LibdeflateC& ld = libdeflate_c();
+    if (ld.ok) {
+        struct State {
+            void* c = nullptr;
+            int level = -1;
+            ~State() {
+                if (c) libdeflate_c().free_c(c);
+            }
+        };
+        thread_local State st;
+        if (st.level != level) {
+            if (st.c) ld.free_c(st.c);
+            st.c = ld.alloc(level);
+            st.level = level;
+        }
+        if (st.c) return ld.compress(st.c, src, n, dst, cap);
+    }
     z_stream zs;
     std::memset(&zs, 0, sizeof zs);
-    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return 0;
     zs.next_in = const_cast<Bytef*>(src);
     zs.avail_in = (uInt)n;
-    zs.next_out = out.data() + 18;
-    zs.avail_out = (uInt)(out.size() - 26);
+    zs.next_out = dst;
+    zs.avail_out = (uInt)cap;
     const int rc = deflate(&zs, Z_FINISH);
     const size_t clen = zs.total_out;
     deflateEnd(&zs);
-    if (rc != Z_STREAM_END) return false;
+    return rc == Z_STREAM_END ? clen : 0;
+}
+
+// one BGZF block (header + raw deflate + crc + isize) for <= 65280 bytes
+bool bgzf_block(const uint8_t* src, size_t n, int level, std::vector<uint8_t>& out) {
+    out.resize(18 + compressBound((uLong)n) + 8 + 64);
+    const size_t clen = deflate_raw(src, n, level, out.data() + 18, out.size() - 26);
+    if (clen == 0 && n > 0) return false;
     const size_t bsize = clen + 26;
     const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
                              (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
@@ -116,8 +165,29 @@ extern "C" int mc_bam_write(const char* path, int32_t n_ref, const char* const* 
         put32(raw, 0);
         raw.insert(raw.end(), name, name + ln);
         for (int64_t k = c0; k < c1; ++k) put32(raw, cigar[k]);
-        raw.insert(raw.end(), seq_bytes, (uint8_t)0x11);
-        raw.insert(raw.end(), (size_t)l_seq, (uint8_t)30);
+        uint64_t h = (uint64_t)i + 0x632BE59BD9B4E019ull;   // per-record stream start:
+        h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;          // hashed, so records do not
+        h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;          // share shifted streams
+        h ^= h >> 31;
+        auto rnd = [&h]() {       // splitmix64 step
+            uint64_t z = (h += 0x9E3779B97F4A7C15ull);
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            return z ^ (z >> 31);
+        };
+        static const uint8_t kNt16[4] = {1, 2, 4, 8};      // A C G T
+        uint64_t bits = 0;
+        for (size_t k = 0; k < seq_bytes; ++k) {
+            if ((k & 15) == 0) bits = rnd();
+            const uint8_t b = (uint8_t)((kNt16[bits & 3] << 4) | kNt16[(bits >> 2) & 3]);
+            bits >>= 4;
+            raw.push_back(b);
+        }
+        for (int32_t k = 0; k < l_seq; ++k) {
+            if ((k & 7) == 0) bits = rnd();
+            raw.push_back((uint8_t)(2 + (bits & 0xff) % 39));
+            bits >>= 8;
+        }
     }
     // ---- deflate 65280-byte blocks in parallel, write in order
     const size_t kBlk = 0xff00;

@@ -2,6 +2,7 @@
 // index builder / indexed range reader (bam_index.cpp).  Host code only.
 #pragma once
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -11,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -70,6 +72,7 @@ struct MappedFile {
         void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
         MC_REQUIRE(m != MAP_FAILED, MC_E_IO, "mmap %s failed", path);
         data = (const uint8_t*)m;
+        (void)madvise(m, size, MADV_SEQUENTIAL);   // read ahead: blocks are visited in order
         return MC_OK;
     }
 };
@@ -105,8 +108,50 @@ inline int scan_blocks(const uint8_t* d, size_t n, size_t from, size_t last,
     return MC_OK;
 }
 
+// libdeflate (the image's libdeflate.so.0, Debian libdeflate0 1.10) inflates a
+// BGZF block 2-3x faster than zlib.  It has no header in the image, so its
+// stable C entry points are bound with dlopen / dlsym; without the library
+// (or with MC_NO_LIBDEFLATE set) zlib does the work.
+struct Libdeflate {
+    void* (*alloc)() = nullptr;
+    int (*decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+    void (*free_d)(void*) = nullptr;
+    bool ok = false;
+    Libdeflate() {
+        if (std::getenv("MC_NO_LIBDEFLATE")) return;
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = reinterpret_cast<void* (*)()>(dlsym(h, "libdeflate_alloc_decompressor"));
+        decompress = reinterpret_cast<int (*)(void*, const void*, size_t, void*, size_t, size_t*)>(
+            dlsym(h, "libdeflate_deflate_decompress"));
+        free_d = reinterpret_cast<void (*)(void*)>(dlsym(h, "libdeflate_free_decompressor"));
+        ok = alloc && decompress && free_d;
+    }
+};
+
+inline const Libdeflate& libdeflate() {
+    static const Libdeflate ld;
+    return ld;
+}
+
+struct LibdeflateState {   // one decompressor per thread
+    void* d = nullptr;
+    ~LibdeflateState() {
+        if (d) libdeflate().free_d(d);
+    }
+};
+
 inline bool inflate_block(const uint8_t* src, size_t clen, uint8_t* dst, size_t isize) {
     if (isize == 0) return true;
+    const Libdeflate& ld = libdeflate();
+    if (ld.ok) {
+        thread_local LibdeflateState st;
+        if (!st.d) st.d = ld.alloc();
+        if (st.d) {
+            size_t got = 0;
+            return ld.decompress(st.d, src, clen, dst, isize, &got) == 0 && got == isize;
+        }
+    }
     z_stream zs;
     std::memset(&zs, 0, sizeof zs);
     if (inflateInit2(&zs, -15) != Z_OK) return false;
