@@ -142,19 +142,27 @@ int parse_records(const uint8_t* d, size_t o, size_t n, bool partial, int32_t n_
     if (seg_off.size() < 2) seg_off.push_back(tail_end);
     lap("boundaries");
     const size_t nseg = seg_off.size() - 1;
-    struct SegCount { int64_t kept = 0, words = 0, mapped = 0, unmapped = 0, records = 0; int err = 0; size_t err_at = 0; };
-    std::vector<SegCount> sc(nseg);
-    std::vector<int64_t> kept_off(nseg + 1, 0), word_off(nseg + 1, 0);
-    // append after what `bam` already holds
-    kept_off[0] = (int64_t)bam->tid.size();
-    word_off[0] = bam->keep_cigar ? (int64_t)bam->cigar.size() : 0;
-    if (bam->keep_cigar && bam->cig_off.empty()) bam->cig_off.push_back(0);
-    auto run_pass = [&](int pass) {
+    // one pass: each range fills its own buffers, then they are concatenated
+    // in parallel after what `bam` already holds
+    struct Seg {
+        int64_t mapped = 0, unmapped = 0, records = 0;
+        int err = 0;
+        size_t err_at = 0;
+        std::vector<int32_t> tid, pos, span;
+        std::vector<uint32_t> cigar;
+        std::vector<int64_t> nw;
+    };
+    std::vector<Seg> sg(nseg);
+    const bool keep_cigar = bam->keep_cigar;
+    {
         std::atomic<size_t> next_seg{0};
         auto work = [&]() {
             for (size_t g; (g = next_seg.fetch_add(1)) < nseg;) {
-                SegCount& c = sc[g];
-                int64_t ki = kept_off[g], wi = word_off[g];
+                Seg& c = sg[g];
+                const size_t guess = (seg_off[g + 1] - seg_off[g]) / 200 + 16;
+                c.tid.reserve(guess);
+                c.pos.reserve(guess);
+                c.span.reserve(guess);
                 for (size_t q = seg_off[g]; q < seg_off[g + 1];) {
                     const int32_t block_size = rdi32(d + q);
                     const uint8_t* r = d + q + 4;
@@ -162,45 +170,37 @@ int parse_records(const uint8_t* d, size_t o, size_t n, bool partial, int32_t n_
                     q += 4 + (size_t)block_size;
                     const int32_t tid = rdi32(r);
                     const uint16_t flag = rd16(r + 14);
-                    if (pass == 0) {
-                        ++c.records;
-                        if (tid >= 0 && !(flag & 4)) ++c.mapped;
-                        else ++c.unmapped;
-                    }
+                    ++c.records;
+                    if (tid >= 0 && !(flag & 4)) ++c.mapped;
+                    else ++c.unmapped;
                     if (tid < 0 || (flag & flag_filter)) continue;
                     if (tid >= n_ref) {
                         c.err = 1;
                         c.err_at = q;
-                        return;
+                        break;
                     }
                     const uint8_t* cig;
                     uint32_t n_cigar;
                     if (!cigar_of(r, rend, &cig, &n_cigar)) {
                         c.err = 2;
                         c.err_at = q;
-                        return;
-                    }
-                    if (pass == 0) {
-                        ++c.kept;
-                        c.words += n_cigar;
-                        continue;
+                        break;
                     }
                     int64_t rlen = cigar_rlen(cig, n_cigar);
                     if (rlen <= 0) rlen = 1;
                     if (rlen > INT32_MAX) {
                         c.err = 3;
                         c.err_at = q;
-                        return;
+                        break;
                     }
-                    bam->tid[ki] = tid;
-                    bam->pos[ki] = rdi32(r + 4);
-                    bam->span[ki] = (int32_t)rlen;
-                    if (bam->keep_cigar) {
-                        std::memcpy(bam->cigar.data() + wi, cig, (size_t)n_cigar * 4);
-                        wi += n_cigar;
-                        bam->cig_off[ki + 1] = wi;
+                    c.tid.push_back(tid);
+                    c.pos.push_back(rdi32(r + 4));
+                    c.span.push_back((int32_t)rlen);
+                    if (keep_cigar) {
+                        c.cigar.insert(c.cigar.end(), reinterpret_cast<const uint32_t*>(cig),
+                                       reinterpret_cast<const uint32_t*>(cig) + n_cigar);
+                        c.nw.push_back(n_cigar);
                     }
-                    ++ki;
                 }
             }
         };
@@ -208,32 +208,58 @@ int parse_records(const uint8_t* d, size_t o, size_t n, bool partial, int32_t n_
         for (int i = 1; i < std::min<int>(nt, (int)nseg); ++i) pool.emplace_back(work);
         work();
         for (auto& t : pool) t.join();
-    };
-    run_pass(0);
-    lap("count");
+    }
+    lap("parse");
+    std::vector<int64_t> kept_off(nseg + 1, 0), word_off(nseg + 1, 0);
+    kept_off[0] = (int64_t)bam->tid.size();
+    word_off[0] = keep_cigar ? (int64_t)bam->cigar.size() : 0;
+    if (keep_cigar && bam->cig_off.empty()) bam->cig_off.push_back(0);
     for (size_t g = 0; g < nseg; ++g) {
-        if (sc[g].err) {
-            return fail(sc[g].err == 1 ? "record tid beyond the reference list"
-                        : sc[g].err == 2 ? "CIGAR overruns record" : "reference span exceeds int32",
-                        sc[g].err_at);
+        if (sg[g].err) {
+            return fail(sg[g].err == 1 ? "record tid beyond the reference list"
+                        : sg[g].err == 2 ? "CIGAR overruns record" : "reference span exceeds int32",
+                        sg[g].err_at);
         }
-        kept_off[g + 1] = kept_off[g] + sc[g].kept;
-        word_off[g + 1] = word_off[g] + sc[g].words;
-        bam->n_mapped += sc[g].mapped;
-        bam->n_records += sc[g].records;
-        bam->n_unmapped += sc[g].unmapped;
+        kept_off[g + 1] = kept_off[g] + (int64_t)sg[g].tid.size();
+        word_off[g + 1] = word_off[g] + (int64_t)sg[g].cigar.size();
+        bam->n_mapped += sg[g].mapped;
+        bam->n_records += sg[g].records;
+        bam->n_unmapped += sg[g].unmapped;
     }
     bam->tid.resize(kept_off[nseg]);
     bam->pos.resize(kept_off[nseg]);
     bam->span.resize(kept_off[nseg]);
-    if (bam->keep_cigar) {
+    if (keep_cigar) {
         bam->cigar.resize(word_off[nseg]);
         bam->cig_off.resize(kept_off[nseg] + 1, 0);
     }
-    run_pass(1);
-    lap("fill");
-    for (size_t g = 0; g < nseg; ++g)
-        if (sc[g].err) return fail("reference span exceeds int32", sc[g].err_at);
+    {
+        std::atomic<size_t> next_seg{0};
+        auto copy = [&]() {
+            for (size_t g; (g = next_seg.fetch_add(1)) < nseg;) {
+                const Seg& c = sg[g];
+                const size_t k = c.tid.size();
+                if (k) {
+                    std::memcpy(bam->tid.data() + kept_off[g], c.tid.data(), k * 4);
+                    std::memcpy(bam->pos.data() + kept_off[g], c.pos.data(), k * 4);
+                    std::memcpy(bam->span.data() + kept_off[g], c.span.data(), k * 4);
+                }
+                if (keep_cigar) {
+                    if (!c.cigar.empty())
+                        std::memcpy(bam->cigar.data() + word_off[g], c.cigar.data(), c.cigar.size() * 4);
+                    int64_t w = word_off[g];
+                    for (size_t i = 0; i < k; ++i) {
+                        w += c.nw[i];
+                        bam->cig_off[kept_off[g] + i + 1] = w;
+                    }
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int i = 1; i < std::min<int>(nt, (int)nseg); ++i) pool.emplace_back(copy);
+        copy();
+        for (auto& t : pool) t.join();
+    }
     return MC_OK;
 }
 
