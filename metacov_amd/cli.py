@@ -112,7 +112,21 @@ def compute_rows(bam, tids, starts, ends, device=0):
     eng = bam.engine(device, compute=False)
     rows = eng.compute_depth_stats(np.asarray(bam.local_tid(tids), np.int32), starts, ends)
     eng._depth_ready = True
+    warn_depth_cap(eng.max_depth())
     return rows
+
+
+HTSLIB_MAX_DEPTH = 8000   # pysam pileup's default max_depth (the htslib read-pool cap)
+
+
+def warn_depth_cap(max_depth):
+    """The reference's pysam pileup stops adding reads to a column's pool past
+    max_depth=8000 (version-dependent); this engine never caps.
+    Above the cap the two disagree, so say so."""
+    if max_depth > HTSLIB_MAX_DEPTH:
+        log.warning("maximum depth %d exceeds pysam's pileup cap of %d: the reference would "
+                    "report capped depths there; these values are exact", max_depth,
+                    HTSLIB_MAX_DEPTH)
 
 
 def write_csv(regions, rows, outfile):
