@@ -121,7 +121,20 @@ __device__ __forceinline__ int wave_min(int v) {
 
 // out[0] = invalid records, out[1] = order violations, out[2] = aligned
 // bases, out[3] = max span.  maxend[t] = furthest read end past len[t].
-// 4 reads per thread (int4 loads; the arrays are padded past n).
+// Each wave owns a contiguous range of int4 read groups (the arrays are
+// padded past n), so its per-contig aligned bases accumulate in registers
+// while the wave's reads stay on one contig and are reduced only when the
+// contig changes.
+__device__ __forceinline__ void flush_cbases(unsigned long long* cbases, long long& acc, int& cur_t,
+                                             int lane) {
+    if (cur_t >= 0) {
+        const long long w = wave_sum64(acc);
+        if (lane == 0 && w) atomicAdd(&cbases[cur_t], (unsigned long long)w);
+    }
+    acc = 0;
+    cur_t = -1;
+}
+
 __global__ void __launch_bounds__(kBlock)
 ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
               const int32_t* __restrict__ span, int64_t n,
@@ -129,26 +142,42 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
               unsigned long long* __restrict__ out, long long* __restrict__ maxend,
               unsigned long long* __restrict__ cbases) {
     const int lane = threadIdx.x & 63;
-    long long bad = 0, unsorted = 0, bases = 0, my_bases = 0;
+    const int64_t n4 = (n + 3) / 4;
+    const int64_t n_waves = (int64_t)gridDim.x * kWaves;
+    const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int64_t per = (n4 + n_waves - 1) / n_waves;
+    const int64_t g0 = gw * per, g1 = min(n4, g0 + per);
+    long long bad = 0, unsorted = 0, bases = 0;
     int mspan = 0;
-    for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q * 4 < n;
-         q += (int64_t)gridDim.x * kBlock) {
+    long long acc = 0;   // aligned bases of contig cur_t (wave-uniform) not yet added
+    int cur_t = -1;
+    for (int64_t gb = g0; gb < g1; gb += 64) {
+        const int64_t q = gb + lane;
+        const bool mine = q < g1;
         const int64_t i0 = q * 4;
-        const i32x4 t4 = *reinterpret_cast<const i32x4*>(tid + i0);
-        const i32x4 p4 = *reinterpret_cast<const i32x4*>(pos + i0);
-        const i32x4 s4 = *reinterpret_cast<const i32x4*>(span + i0);
+        i32x4 t4 = {0, 0, 0, 0}, p4 = {0, 0, 0, 0}, s4 = {0, 0, 0, 0};
         int tp = -1, pp = 0;
-        if (i0 > 0) {
-            tp = tid[i0 - 1];
-            pp = pos[i0 - 1];
+        if (mine) {
+            t4 = *reinterpret_cast<const i32x4*>(tid + i0);
+            p4 = *reinterpret_cast<const i32x4*>(pos + i0);
+            s4 = *reinterpret_cast<const i32x4*>(span + i0);
+            if (i0 > 0) {
+                tp = tid[i0 - 1];
+                pp = pos[i0 - 1];
+            }
         }
         const int tt[4] = {t4.x, t4.y, t4.z, t4.w};
         const int ps[4] = {p4.x, p4.y, p4.z, p4.w};
         const int ss[4] = {s4.x, s4.y, s4.z, s4.w};
+        long long my_bases = 0;
+        bool same = true;
+        const int t0 = __builtin_amdgcn_readfirstlane(t4.x);   // lane 0 always holds a read
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (i0 + k >= n) break;
+            const bool live = mine && i0 + k < n;
+            if (!live) continue;
             const int t = tt[k], p = ps[k], sp = ss[k];
+            same &= t == t0;
             if (t < 0 || t >= n_contigs || p < 0 || sp < 0) {
                 ++bad;
             } else {
@@ -162,25 +191,21 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             tp = t;
             pp = p;
         }
-        // per-contig aligned bases (histogram windows of the fused statistics):
-        // the wave's 256 reads are consecutive, so usually one contig -> one
-        // atomic per wave; mixed waves add per lane
-        const int t0 = __shfl(t4.x, 0, 64);
-        bool same = true;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) same &= (i0 + k >= n) || tt[k] == t0;
-        if (__all(same)) {
-            const long long wsum = wave_sum64(my_bases);
-            if (lane == 0 && wsum && t0 >= 0 && t0 < n_contigs)
-                atomicAdd(&cbases[t0], (unsigned long long)wsum);
-        } else {
+        if (__all(same) && t0 >= 0 && t0 < n_contigs) {
+            if (t0 != cur_t) {
+                flush_cbases(cbases, acc, cur_t, lane);
+                cur_t = t0;
+            }
+            acc += my_bases;
+        } else {                                   // a contig boundary inside the wave
+            flush_cbases(cbases, acc, cur_t, lane);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (i0 + k < n && tt[k] >= 0 && tt[k] < n_contigs && ss[k] > 0)
+                if (mine && i0 + k < n && tt[k] >= 0 && tt[k] < n_contigs && ss[k] > 0)
                     atomicAdd(&cbases[tt[k]], (unsigned long long)ss[k]);
         }
-        my_bases = 0;
     }
+    flush_cbases(cbases, acc, cur_t, lane);
     bad = wave_sum64(bad);
     unsorted = wave_sum64(unsorted);
     bases = wave_sum64(bases);
@@ -237,27 +262,29 @@ chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ 
 // share one atomic (reads are position-sorted, so a wave's 64 reads touch a
 // handful of tiles / chunks).  Returns each lane's slot: the counter value
 // before the group's add plus the lane's rank within its group.
-__device__ __forceinline__ unsigned wave_key_add(unsigned* arr, long long key, int lane) {
+// (keys are tile / chunk indices < 2^31; readlane with the uniform leader,
+// no LDS round trips)
+__device__ __forceinline__ unsigned wave_key_add(unsigned* arr, int key, int lane) {
     unsigned slot = 0;
     unsigned long long pending = __ballot(key >= 0);
     while (pending) {
         const int leader = __ffsll((long long)pending) - 1;
-        const long long k = __shfl(key, leader, 64);
+        const int k = __builtin_amdgcn_readlane(key, leader);
         const unsigned long long m = __ballot(key == k) & pending;
         unsigned b = 0;
         if (lane == leader) b = atomicAdd(&arr[k], (unsigned)__popcll(m));
-        b = __shfl(b, leader, 64);
+        b = (unsigned)__builtin_amdgcn_readlane((int)b, leader);
         if ((m >> lane) & 1ull) slot = b + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
         pending &= ~m;
     }
     return slot;
 }
 
-__device__ __forceinline__ void wave_key_add_signed(int* arr, long long key, int sign, int lane) {
+__device__ __forceinline__ void wave_key_add_signed(int* arr, int key, int sign, int lane) {
     unsigned long long pending = __ballot(key >= 0);
     while (pending) {
         const int leader = __ffsll((long long)pending) - 1;
-        const long long k = __shfl(key, leader, 64);
+        const int k = __builtin_amdgcn_readlane(key, leader);
         const unsigned long long m = __ballot(key == k) & pending;
         if (lane == leader) atomicAdd(&arr[k], sign * (int)__popcll(m));
         pending &= ~m;
@@ -268,7 +295,7 @@ __device__ __forceinline__ void wave_key_add_signed(int* arr, long long key, int
 // (or -1: past the allocation, or exactly on a chunk start, where the next
 // chunk's carry already excludes it) and its chunk-carry range [c0, c1).
 struct LongEv {
-    long long tile, c0, c1;
+    int tile, c0, c1;
 };
 
 __device__ __forceinline__ LongEv long_events(const int32_t* tid, const int32_t* pos,
@@ -282,11 +309,11 @@ __device__ __forceinline__ LongEv long_events(const int32_t* tid, const int32_t*
     const int64_t gs = coff[tid[i]] + pos[i];
     const int64_t ge = gs + sp;
     *ge_out = ge;
-    if (ge < alloc_len && ge % chunk_w) e.tile = ge / kTileW;
+    if (ge < alloc_len && ge % chunk_w) e.tile = (int)(ge / kTileW);
     const int64_t c0 = gs / chunk_w + 1, c1 = (ge - 1) / chunk_w + 1;
     if (c1 > c0) {
-        e.c0 = c0;
-        e.c1 = c1;
+        e.c0 = (int)c0;
+        e.c1 = (int)c1;
     }
     return e;
 }
@@ -322,7 +349,7 @@ long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ po
         const LongEv e = long_events(tid, pos, span, w0 + lane, n, coff, short_max, alloc_len,
                                      chunk_w, &ge);
         const unsigned slot = wave_key_add(tile_cursor, e.tile, lane);
-        if (e.tile >= 0) ev[tile_off[e.tile] + slot] = (int32_t)(ge - e.tile * kTileW);
+        if (e.tile >= 0) ev[tile_off[e.tile] + slot] = (int32_t)(ge - (int64_t)e.tile * kTileW);
     }
 }
 
