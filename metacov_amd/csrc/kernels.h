@@ -394,89 +394,59 @@ cigar_span_kernel(const int64_t* __restrict__ cig_off, const uint32_t* __restric
             owner[k] = (unsigned char)threadIdx.x;
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
+    // each lane sums kLaneWords consecutive words per step (4 int4 loads,
+    // the next step's in flight), so a long CIGAR's words stay in one lane's
+    // registers and a lane adds at most a few per-read partial sums to LDS
+    constexpr int kLaneWords = 4 * kCigarLoads;
+    constexpr long long kStep = (long long)kLaneWords * kBlock;
     const long long a4 = w0 & ~3ll;
-    constexpr long long kStep = 4ll * kBlock;
-    auto load = [&](uint32_t (&wd)[kCigarLoads][4], long long base) {
+    auto load = [&](uint32_t (&wd)[kLaneWords], long long base) {
+        const long long p0 = base + (long long)kLaneWords * threadIdx.x;
 #pragma unroll
         for (int u = 0; u < kCigarLoads; ++u) {
-            const long long p = base + u * kStep + 4ll * threadIdx.x;
+            const long long p = p0 + 4 * u;
             if (p + 3 < w1 && p >= w0) {
                 const uint4 x = *reinterpret_cast<const uint4*>(cigar + p);
-                wd[u][0] = x.x;
-                wd[u][1] = x.y;
-                wd[u][2] = x.z;
-                wd[u][3] = x.w;
+                wd[4 * u] = x.x;
+                wd[4 * u + 1] = x.y;
+                wd[4 * u + 2] = x.z;
+                wd[4 * u + 3] = x.w;
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    wd[u][k] = (p + k >= w0 && p + k < w1) ? cigar[p + k] : 0u;
+                    wd[4 * u + k] = (p + k >= w0 && p + k < w1) ? cigar[p + k] : 0u;
             }
         }
     };
-    uint32_t cur[kCigarLoads][4], nxt[kCigarLoads][4];
+    uint32_t cur[kLaneWords], nxt[kLaneWords];
     if (a4 < w1) load(cur, a4);
-    for (long long base = a4; base < w1; base += kStep * kCigarLoads) {
-        const long long nbase = base + kStep * kCigarLoads;
-        if (nbase < w1) load(nxt, nbase);            // next batch in flight meanwhile
+    for (long long base = a4; base < w1; base += kStep) {
+        if (base + kStep < w1) load(nxt, base + kStep);   // next step in flight meanwhile
+        const long long p = base + (long long)kLaneWords * threadIdx.x;
+        const long long first = p > w0 ? p : w0;
+        if (first < w1 && first < p + kLaneWords) {
+            int r = owner[(first - w0) >> sh];
+            long long next = off[r + 1];                   // first word of read r + 1
+            int run = 0, s = 0;
 #pragma unroll
-        for (int u = 0; u < kCigarLoads; ++u) {
-            const long long p = base + u * kStep + 4ll * threadIdx.x;
-            // runs of this lane's words by read: (ra, sa) first, (rb, sb) last
-            int ra = -1, rb = -1, sa = 0, sb = 0;
-            const long long first = p > w0 ? p : w0;
-            if (first < w1 && first < p + 4) {
-                int r = owner[(first - w0) >> sh];
-                long long next = off[r + 1];               // first word of read r + 1
-                ra = -2;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const long long w = p + k;
-                    if (w < first || w >= w1) continue;
-                    while (next <= w) {                    // w < w1 = off[nr]: stops at r < nr
+            for (int k = 0; k < kLaneWords; ++k) {
+                const long long w = p + k;
+                if (w < first || w >= w1) continue;
+                if (next <= w) {                           // a new read: flush the run
+                    if (s) atomicAdd(&acc[run], s);
+                    do {
                         ++r;
                         next = off[r + 1];
-                    }
-                    const int c = cigar_ref_len(cur[u][k]);
-                    if (ra == -2) ra = r;
-                    if (r == ra) {
-                        sa += c;
-                    } else if (r == rb) {
-                        sb += c;
-                    } else {
-                        if (rb >= 0 && sb) atomicAdd(&acc[rb], sb);   // a short read in the middle
-                        rb = r;
-                        sb = c;
-                    }
+                    } while (next <= w);
+                    s = 0;
                 }
+                run = r;
+                s += cigar_ref_len(cur[k]);
             }
-            // few distinct reads in the wave: shuffle-reduce per read
-            const int prev_b = __shfl_up(rb >= 0 ? rb : ra, 1, 64);
-            const bool head = ra >= 0 && (lane == 0 || prev_b != ra);
-            if (__popcll(__ballot(head)) <= 4) {
-#pragma unroll
-                for (int pass = 0; pass < 2; ++pass) {
-                    const int key = pass == 0 ? ra : rb;
-                    const int val = pass == 0 ? sa : sb;
-                    unsigned long long pending = __ballot(key >= 0);
-                    while (pending) {
-                        const int leader = __ffsll((long long)pending) - 1;
-                        const int k = __shfl(key, leader, 64);
-                        const unsigned long long m = __ballot(key == k) & pending;
-                        const int v = wave_sum_i32(((m >> lane) & 1ull) ? val : 0);
-                        if (lane == leader && v) atomicAdd(&acc[k], v);
-                        pending &= ~m;
-                    }
-                }
-            } else {
-                if (ra >= 0 && sa) atomicAdd(&acc[ra], sa);
-                if (rb >= 0 && sb) atomicAdd(&acc[rb], sb);
-            }
+            if (s) atomicAdd(&acc[run], s);
         }
 #pragma unroll
-        for (int u = 0; u < kCigarLoads; ++u)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur[u][k] = nxt[u][k];
+        for (int k = 0; k < kLaneWords; ++k) cur[k] = nxt[k];
     }
     __syncthreads();
     if (threadIdx.x < nr) {
