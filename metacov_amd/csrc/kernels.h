@@ -363,7 +363,10 @@ long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ po
 // LDS binary search per int4, then forward steps); a wave whose runs touch few
 // reads (long CIGARs) reduces them with shuffles before one LDS atomic per
 // read, otherwise (short CIGARs, low contention) each run adds directly.
-constexpr int kCigarLoads = 4;
+#ifndef MC_K1_LOADS
+#define MC_K1_LOADS 2                  // K1: int4 loads per lane per step (sweep: 1/2/4/8)
+#endif
+constexpr int kCigarLoads = MC_K1_LOADS;
 constexpr int kOwnerBuckets = 2048;       // K1 word -> read lookup buckets (bytes of LDS)
 
 __device__ __forceinline__ int cigar_ref_len(uint32_t c) {
