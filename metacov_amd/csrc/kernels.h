@@ -169,7 +169,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         const int tt[4] = {t4.x, t4.y, t4.z, t4.w};
         const int ps[4] = {p4.x, p4.y, p4.z, p4.w};
         const int ss[4] = {s4.x, s4.y, s4.z, s4.w};
-        long long my_bases = 0;
+        long long my_bases = 0, my_end = 0;   // my_end: furthest end past its contig
         bool same = true;
         const int t0 = __builtin_amdgcn_readfirstlane(t4.x);   // lane 0 always holds a read
 #pragma unroll
@@ -186,7 +186,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 mspan = max(mspan, sp);
                 my_bases += sp;
                 const long long e = (long long)p + sp;
-                if (e > len[t]) atomicMax(&maxend[t], e);
+                if (e > len[t]) my_end = max(my_end, e);
             }
             tp = t;
             pp = p;
@@ -197,12 +197,20 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 cur_t = t0;
             }
             acc += my_bases;
+            if (__any(my_end > 0)) {               // one atomic per wave for the overhangs
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) my_end = max(my_end, (long long)__shfl_xor(my_end, d, 64));
+                if (lane == 0) atomicMax(&maxend[t0], my_end);
+            }
         } else {                                   // a contig boundary inside the wave
             flush_cbases(cbases, acc, cur_t, lane);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (mine && i0 + k < n && tt[k] >= 0 && tt[k] < n_contigs && ss[k] > 0)
-                    atomicAdd(&cbases[tt[k]], (unsigned long long)ss[k]);
+            for (int k = 0; k < 4; ++k) {
+                const bool live = mine && i0 + k < n && tt[k] >= 0 && tt[k] < n_contigs;
+                if (live && ss[k] > 0) atomicAdd(&cbases[tt[k]], (unsigned long long)ss[k]);
+                if (live && ps[k] >= 0 && ss[k] >= 0 && (long long)ps[k] + ss[k] > len[tt[k]])
+                    atomicMax(&maxend[tt[k]], (long long)ps[k] + ss[k]);
+            }
         }
     }
     flush_cbases(cbases, acc, cur_t, lane);
@@ -265,19 +273,26 @@ chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ 
 // (keys are tile / chunk indices < 2^31; readlane with the uniform leader,
 // no LDS round trips)
 __device__ __forceinline__ unsigned wave_key_add(unsigned* arr, int key, int lane) {
-    unsigned slot = 0;
+    // group the lanes by key (ballots only), then every group's leader adds
+    // its count in one atomic instruction: one round trip per wave
+    unsigned rank = 0, count = 0;
+    int leader_of = lane;
     unsigned long long pending = __ballot(key >= 0);
     while (pending) {
         const int leader = __ffsll((long long)pending) - 1;
         const int k = __builtin_amdgcn_readlane(key, leader);
         const unsigned long long m = __ballot(key == k) & pending;
-        unsigned b = 0;
-        if (lane == leader) b = atomicAdd(&arr[k], (unsigned)__popcll(m));
-        b = (unsigned)__builtin_amdgcn_readlane((int)b, leader);
-        if ((m >> lane) & 1ull) slot = b + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+        if (lane == leader) count = (unsigned)__popcll(m);
+        if ((m >> lane) & 1ull) {
+            leader_of = leader;
+            rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+        }
         pending &= ~m;
     }
-    return slot;
+    unsigned base = 0;
+    if (count) base = atomicAdd(&arr[key], count);
+    base = (unsigned)__shfl((int)base, leader_of, 64);
+    return base + rank;
 }
 
 __device__ __forceinline__ void wave_key_add_signed(int* arr, int key, int sign, int lane) {
