@@ -34,17 +34,8 @@ namespace mc {
 #ifndef MC_PREFETCH_STATS
 #define MC_PREFETCH_STATS 1            // the same for the fused-statistics K2
 #endif
-#ifndef MC_HIST_LDS
-#define MC_HIST_LDS 0                  // fused K2: histogram from LDS (16 positions/lane)
-#endif
 #ifndef MC_NT_STORE
 #define MC_NT_STORE 1                  // non-temporal depth stores (written once, not re-read soon)
-#endif
-#ifndef MC_EXP_EPILOGUE
-#define MC_EXP_EPILOGUE 2              // experiments: 0 none, 1 touch values, 2 = real epilogue
-#endif
-#ifndef MC_CHUNK_PF
-#define MC_CHUNK_PF 0                  // dequeue the next chunk during the current one
 #endif
 #ifndef MC_WAVES_PLAIN
 #define MC_WAVES_PLAIN 0               // __launch_bounds__ waves/SIMD, plain K2 (0 = none)
@@ -568,25 +559,6 @@ __device__ __forceinline__ void ov_add(OvLds* ov, int v, int cnt, int base) {
     atomicMax(&ov->vmax, v);
 }
 
-// One run of `cnt` positions of depth v: histogram bin v - base, or the
-// overflow record when v falls outside [base, base + kHistBins).
-__device__ __forceinline__ void emit_hist(unsigned* h, OvLds* ov, int v, int cnt, int base) {
-    const int b = v - base;
-#ifdef MC_EXP_NO_HIST
-    asm volatile("" :: "v"(b), "v"(cnt));
-    return;
-#endif
-    if ((unsigned)b < (unsigned)kHistBins) {
-#ifdef MC_EXP_HIST_SPREAD   // experiment: same instruction count, no address conflicts
-        atomicAdd(&h[(b + (int)threadIdx.x) & (kHistBins - 1)], (unsigned)cnt);
-#else
-        atomicAdd(&h[b], (unsigned)cnt);
-#endif
-    } else {
-        ov_add(ov, v, cnt, base);
-    }
-}
-
 // The wave's runs outside the histogram window (contig ends, depth far from
 // the mean): reduced across the wave, then one lane updates the LDS record.
 // Out of line: its temporaries stay off the hot loop's register budget.
@@ -744,7 +716,6 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (c >= n_chunks) break;
         const int64_t cfirst = *reinterpret_cast<const long long*>(hdr + 2);
         const int64_t cend = *reinterpret_cast<const long long*>(hdr + 8);   // reads of this chunk end
-        if (MC_CHUNK_PF && threadIdx.x == 0) next_c = atomicAdd(queue, 1u);
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
         int r_base = 0;
@@ -806,10 +777,6 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 finish_batch(b, nxt, base, n, C0, coff);      // loaded one batch ago
                 if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
             }
-            if (MC_CHUNK_PF && t == 0 && threadIdx.x == 0 && next_c < n_chunks) {
-                next_first = chunk_first[2 * next_c];         // prefetch for the next chunk
-                next_end = chunk_first[2 * next_c + 1];
-            }
             // ---- scan tile t: each wave owns kWaveSpan contiguous positions
             const int sb = t * kTileW + wave * kWaveSpan;   // chunk-relative start of my span
             i32x4 v[kChunks];
@@ -818,7 +785,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             for (int j = 0; j < kChunks; ++j) {
                 i32x4* slot = reinterpret_cast<i32x4*>(ring + ring_slot(sb + j * 256) + lane * 4);
                 i32x4 x = *slot;
-                if (!(kStats && MC_HIST_LDS)) *slot = i32x4{0, 0, 0, 0};
+                *slot = i32x4{0, 0, 0, 0};
                 x.y += x.x;
                 x.z += x.y;
                 x.w += x.z;
@@ -848,74 +815,13 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
                 else
                     *reinterpret_cast<i32x4*>(dst + j * 256) = x;
-                if (kStats && MC_HIST_LDS)
-                    *reinterpret_cast<i32x4*>(ring + ring_slot(sb + j * 256) + lane * 4) = x;
             }
-            if (kStats && MC_HIST_LDS) {
-                // final depths of the tile are in the ring: each thread takes
-                // kPer consecutive positions (long runs -> few histogram
-                // atomics) and zeroes them for the ring's next use
-                constexpr int kPer = kTileW / kBlock;
-                static_assert(kPer % 4 == 0, "tile / block must be a multiple of 4");
-                __syncthreads();
-                const int p0 = threadIdx.x * kPer;
-                const int slot0 = ring_slot(t * kTileW + p0);
-                int xs[kPer];
-#pragma unroll
-                for (int q = 0; q < kPer / 4; ++q) {
-                    i32x4* sl = reinterpret_cast<i32x4*>(ring + slot0 + 4 * q);
-                    const i32x4 y = *sl;
-                    *sl = i32x4{0, 0, 0, 0};
-                    xs[4 * q] = y.x;
-                    xs[4 * q + 1] = y.y;
-                    xs[4 * q + 2] = y.z;
-                    xs[4 * q + 3] = y.w;
-                }
-                while (rcur < R.n && r_gs < Tend) {
-                    const int lo = (int)((r_gs > T0 ? r_gs : T0) - T0);
-                    const int hi = (int)((r_ge < Tend ? r_ge : Tend) - T0);
-                    const bool full = lo <= p0 && hi >= p0 + kPer;
-                    int run_v = xs[0], run_n = 0;
-#pragma unroll
-                    for (int k = 0; k < kPer; ++k) {
-                        const bool in = full || (p0 + k >= lo && p0 + k < hi);
-                        const int x = xs[k];
-                        if (in && x == run_v) {
-                            ++run_n;
-                        } else if (in) {
-                            if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
-                            run_v = x;
-                            run_n = 1;
-                        }
-                    }
-                    if (run_n) emit_hist(hist, ovf, run_v, run_n, r_base);
-                    if (r_ge <= Tend) {
-                        flush_region(R, rcur, hist, ovf);
-                        ++rcur;
-                        if (rcur < R.n) {
-                            r_gs = R.gs[rcur];
-                            r_ge = R.ge[rcur];
-                            r_base = R.base[rcur];
-                        }
-                    } else {
-                        break;
-                    }
-                }
-                __syncthreads();   // ring slots zeroed before the next tile's atomics
-            } else if (kStats && MC_EXP_EPILOGUE == 0) {
-                // experiment: no epilogue at all (isolates occupancy/regalloc)
-            } else if (kStats && MC_EXP_EPILOGUE == 1) {
-                // experiment: keep the tile's values live, minimal work
-                int acc = 0;
-#pragma unroll
-                for (int j = 0; j < kChunks; ++j) acc += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-                asm volatile("" :: "v"(acc));
-            } else if (kStats) {
+            if (kStats) {
                 // regions covering this tile, in order; the loop is uniform.
                 // Only the value histogram is built here (runs of equal values
                 // within a lane share one LDS atomic); min/max/sum/sumsq follow
-                // from it in region_final_kernel.  Values >= kHistBins go to
-                // the LDS overflow accumulator.
+                // from it in region_final_kernel.  Values outside the window
+                // go to the wave-reduced LDS overflow record (hist_int4).
                 while (rcur < R.n && r_gs < Tend) {
                     const int64_t rgs = r_gs, rge = r_ge;
                     const int lo = (int)((rgs > T0 ? rgs : T0) - T0);
@@ -953,12 +859,10 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         }
         __syncthreads();   // everyone is past hdr / ring of this chunk
         if (threadIdx.x == 0) {
-            if (!MC_CHUNK_PF) {
-                next_c = atomicAdd(queue, 1u);
-                if (next_c < n_chunks) {
-                    next_first = chunk_first[2 * next_c];
-                    next_end = chunk_first[2 * next_c + 1];
-                }
+            next_c = atomicAdd(queue, 1u);
+            if (next_c < n_chunks) {
+                next_first = chunk_first[2 * next_c];
+                next_end = chunk_first[2 * next_c + 1];
             }
             hdr[0] = (int)next_c;
             *reinterpret_cast<long long*>(hdr + 2) = next_first;
