@@ -224,6 +224,13 @@ def main():
     table = torch.empty((R, 9), dtype=torch.int64, device=dev)
     gathered = None
 
+    gbuf = coll_buf = gout = None
+    if world > 1:   # exchange buffers, allocated once: [r_max, 9 stats + region index]
+        gbuf = torch.full((r_max, mdist.ROW_WIDTH), -1, dtype=torch.int64, device=dev)
+        gbuf[:R, 9] = torch.from_numpy(np.asarray(region_index, np.int64)).to(dev)
+        coll_buf = gbuf if coll_dev == dev else gbuf.to(coll_dev)
+        gout = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=coll_dev)
+
     def step():
         nonlocal gathered
         if args.cigar:   # a fresh raw-CIGAR batch: K1 + prepare run inside this step
@@ -234,15 +241,12 @@ def main():
             eng.region_stats_device(rt, rs, re_, table.data_ptr())
         else:
             eng.compute_depth_stats_device(rt, rs, re_, table.data_ptr())
-        if world > 1:
-            idx = torch.from_numpy(np.asarray(region_index, np.int64)).to(dev)
-            local_tab = torch.cat([table, idx[:, None]], 1)
-            buf = torch.full((r_max, mdist.ROW_WIDTH), -1, dtype=torch.int64, device=dev)
-            buf[:R] = local_tab
-            buf = buf.to(coll_dev)
-            out = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=coll_dev)
-            dist.all_gather_into_tensor(out, buf)
-            gathered = out
+        if world > 1:   # rows into the padded exchange table (index column preset), one all-gather
+            gbuf[:R, :9].copy_(table)
+            if coll_buf is not gbuf:
+                coll_buf.copy_(gbuf)
+            dist.all_gather_into_tensor(gout, coll_buf)
+            gathered = gout
 
     for _ in range(args.warmup):
         step()
