@@ -148,6 +148,8 @@ struct mc_ctx {
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
+    int k2_resident[2] = {0, 0};          // resident K2 workgroups (plain, fused)
+    size_t k2_resident_lds[2] = {0, 0};
     mc_timings t{};
     bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
 };
@@ -566,13 +568,19 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     return MC_OK;
 }
 
-static int occupancy_grid(const void* kernel, size_t lds, int64_t work, int* grid) {
-    int dev = 0, ncu = 0, per = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds));
-    per = std::max(1, per);
-    *grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, (int64_t)ncu * per));
+// Resident workgroups of a K2 variant (queried once per ctx and LDS size).
+static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t lds, int64_t work,
+                          int* grid) {
+    int& cached = ctx->k2_resident[variant];
+    if (cached <= 0 || ctx->k2_resident_lds[variant] != lds) {
+        int dev = 0, ncu = 0, per = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds));
+        cached = ncu * std::max(1, per);
+        ctx->k2_resident_lds[variant] = lds;
+    }
+    *grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, (int64_t)cached));
     return MC_OK;
 }
 
@@ -583,9 +591,11 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins + kOvInts : 0)) * 4;
     const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
     int grid = 0;
-    if (int rc = occupancy_grid(kfn, lds, ctx->n_chunks, &grid)) return rc;
-    HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
-    HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
+    if (int rc = occupancy_grid(ctx, stats ? 1 : 0, kfn, lds, ctx->n_chunks, &grid)) return rc;
+    if (!stats) {   // the fused path's fused_init_kernel zeroes them
+        HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
+    }
     HIP_TRY(hipEventRecord(ctx->ev[4], s));
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
@@ -740,7 +750,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
             hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
                                ctx->d_hist.p, hw, (unsigned*)nullptr, ctx->d_acc.p, nr,
                                (const int64_t*)nullptr, (int64_t)0, (int64_t)1, (int64_t)0,
-                               (int64_t*)nullptr);
+                               (int64_t*)nullptr, (unsigned*)nullptr, (int*)nullptr);
             HIP_TRY(hipGetLastError());
         }
         if (nseg) {
@@ -845,7 +855,8 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         const unsigned g = (unsigned)std::min<int64_t>(4096, (work + kBlock - 1) / kBlock);
         hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
                            ctx->d_fhist.p, R * kHistBins, ctx->d_flow.p, ctx->d_acc.p, R, d_fge, nf,
-                           ctx->chunk_w, ctx->n_chunks, ctx->d_fchunk.p);
+                           ctx->chunk_w, ctx->n_chunks, ctx->d_fchunk.p, ctx->d_queue.p,
+                           ctx->d_maxdepth.p);
         HIP_TRY(hipGetLastError());
     }
     FusedRegions fr{nf,

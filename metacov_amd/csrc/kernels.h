@@ -882,7 +882,12 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 __global__ void __launch_bounds__(kBlock)
 fused_init_kernel(unsigned* __restrict__ hist, int64_t hist_words, unsigned* __restrict__ low,
                   RegionAcc* __restrict__ acc, int64_t R, const int64_t* __restrict__ fge,
-                  int64_t nf, int64_t chunk_w, int64_t n_chunks, int64_t* __restrict__ chunk_first) {
+                  int64_t nf, int64_t chunk_w, int64_t n_chunks, int64_t* __restrict__ chunk_first,
+                  unsigned* __restrict__ queue, int* __restrict__ max_depth) {
+    if (blockIdx.x == 0 && threadIdx.x < 4) {   // K2's chunk queue and max depth (may be null)
+        if (queue) queue[threadIdx.x] = 0;
+        if (max_depth) max_depth[threadIdx.x] = 0;
+    }
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
     for (int64_t q = i0; q * 4 < hist_words; q += stride)   // hist_words % 4 == 0
