@@ -149,6 +149,26 @@ def cpu_baseline_parallel(lengths, tid, pos, span, sample_bases, threads):
                       % (k, threads, dt)}
 
 
+def cpu_baseline_interval(lengths, tid, pos, span, sample_bases):
+    """The simple interval-count CPU path on one core (difference array +
+    exact counting-sort statistics: oracle orc_depth_interval +
+    orc_region_stats), same sample (BASELINE.md CPU-baseline plan)."""
+    from oracle import coracle
+    per = np.bincount(tid, weights=span.astype(np.float64), minlength=len(lengths))
+    k = min(int(np.searchsorted(np.cumsum(per), sample_bases)) + 1, len(lengths))
+    m = tid < k
+    t, p, s = tid[m], pos[m], span[m]
+    t0 = time.perf_counter()
+    d, ext, coff = coracle.depth(lengths[:k], t, p, s, method="interval")
+    coracle.region_stats(d, ext, coff, np.arange(k, dtype=np.int32), np.zeros(k, np.int64),
+                         lengths[:k].astype(np.int64))
+    dt = time.perf_counter() - t0
+    bases = int(s.astype(np.int64).sum())
+    return {"value": bases / dt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
+            "sample": "same %d contigs as cpu_baseline, difference array + counting-sort "
+                      "statistics (not the reference algorithm), %.2f s" % (k, dt)}
+
+
 def load_pmc_traffic(root):
     p = os.path.join(root, "profiles", "pmc_depth_kernel.json")
     if not os.path.exists(p):
@@ -316,12 +336,13 @@ def main():
                     "kernel": "cigar_span_kernel (K1)", "algorithmic_bytes_per_launch": int(k1_bytes)}
 
     if rank == 0:
-        cpu = cpu_par = None
+        cpu = cpu_par = cpu_int = None
         if world == 1 and not args.no_cpu_baseline:
             h = [x.cpu().numpy() for x in (tid, pos, span)]
             cpu = cpu_baseline(lengths, *h, args.cpu_sample_bases, args.config.upper())
             threads = min(args.cpu_threads, os.cpu_count() or 1)
             cpu_par = cpu_baseline_parallel(lengths, *h, args.cpu_sample_bases, threads)
+            cpu_int = cpu_baseline_interval(lengths, *h, args.cpu_sample_bases)
             del h
         pcie = None
         if args.pcie and world == 1:
@@ -379,6 +400,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
+            "cpu_interval_count": cpu_int,
         }
         if pcie is not None:
             line["host_buffer_end_to_end_s"] = pcie
