@@ -245,6 +245,56 @@ int mc_bam_write(const char* path, int32_t n_ref, const char* const* names,
                  const int32_t* pos, const uint16_t* flag, const int64_t* cig_off,
                  const uint32_t* cigar, int32_t l_seq, int level, int n_threads);
 
+/* ---- pileup.experimental (metacov/pileup.py:38-173, SURVEY.md §8 f) --------
+ * The reference's experimental estimator, called by `metacov pileup -k`
+ * (cli.py:81, :93-95) after classic() for every region.
+ *
+ * Read side (host C++): mc_reads_open decodes every placed record of a
+ * coordinate-sorted BAM into the fields experimental() reads from pysam
+ * (flags, query_name, reference_start, reference_length, the first K bases
+ * of query_alignment_sequence as a 2-bit A/C/G/T code).  It replaces
+ * bam.fetch(ref, start, end) at pileup.py:101.  mc_experimental_reads runs
+ * the per-read loop (pileup.py:101-151) for R regions on n_threads threads:
+ *   counts[8*q + 0..7] = status (0 ok, 1 read without SEQ, 2 read without
+ *       reference_length, 3 k_cor None with a mate pair -- the reference
+ *       raises TypeError for 1-3), secondary, improper, nreads,
+ *       sum(cov), #distinct starts, sum(cov2), #"RCOR is ZERO" events
+ *   sums[4*q + 0..3] = sum(cov_cor) (summation order differs from the
+ *       reference), builtin sum(cor) and np.add.reduce(cor) (both exact),
+ *       wnf (exact, pairing order)
+ * K-mer tables: val/has [4^K] per read number (k_cor[0], k_cor[1]); pass
+ * NULL tables for k_cor = None.  Events of region q (readno << 32 | code):
+ * mc_experimental_events. */
+typedef struct mc_reads mc_reads;
+int mc_reads_open(const char* path, int n_threads, int k_len, mc_reads** out);
+int mc_reads_close(mc_reads* r);
+int mc_reads_header(const mc_reads* r, int32_t* n_ref, int64_t* n_records, int64_t* n_placed);
+int mc_reads_target(const mc_reads* r, int32_t i, const char** name, int64_t* length);
+int mc_experimental_reads(mc_reads* r, int k_len, const double* val1, const uint8_t* has1,
+                          const double* val2, const uint8_t* has2, int64_t R,
+                          const int32_t* tid, const int64_t* start, const int64_t* end,
+                          int n_threads, int64_t* counts, double* sums);
+int mc_experimental_events(const mc_reads* r, int64_t region, int64_t cap, uint64_t* events,
+                           int64_t* n);
+
+/* Sequence side (GPU, fp64): the k-mer correction correlation of
+ * pileup.py:63-88 -- fwd / rev k-mer weights over the region's bases, the
+ * 900-tap normal-pdf correlation of rev and inner(fwd, revsum) -- plus the
+ * G+C / A+T counts of pileup.py:64-66.  seq = all contigs' bases back to
+ * back (as in the FASTA, any case); a region is (base offset of its first
+ * base, bases available n <= length, length = end - start).  fwd / rev:
+ * dense [4^K] tables, 0 for missing keys; taps = norm[0 .. n_taps).
+ * inner[q] is ecor * length.  kernel_ms: HIP-event time of the kernel. */
+typedef struct mc_ecor mc_ecor;
+int mc_ecor_create(int device, mc_ecor** out);
+int mc_ecor_destroy(mc_ecor* e);
+int mc_ecor_set_sequence(mc_ecor* e, int64_t n_bytes, const uint8_t* seq);
+int mc_ecor_set_tables(mc_ecor* e, int k_len, const double* fwd, const double* rev,
+                       int n_taps, const double* taps);
+int mc_ecor_run(mc_ecor* e, int64_t R, const int64_t* base, const int64_t* n_avail,
+                const int64_t* length, double* inner, int64_t* gc, int64_t* at,
+                float* kernel_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,6 +101,19 @@ SIGNATURES = {
                             _P, _PP],
     "mc_bam_write": [ctypes.c_char_p, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _I32, ctypes.c_int,
                      ctypes.c_int],
+    # pileup.experimental: read side (host) and sequence side (GPU)
+    "mc_reads_open": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _PP],
+    "mc_reads_close": [_P],
+    "mc_reads_header": [_P, _PI32, _PI64, _PI64],
+    "mc_reads_target": [_P, _I32, ctypes.POINTER(ctypes.c_char_p), _PI64],
+    "mc_experimental_reads": [_P, ctypes.c_int, _P, _P, _P, _P, _I64, _P, _P, _P, ctypes.c_int,
+                              _P, _P],
+    "mc_experimental_events": [_P, _I64, _I64, _P, _PI64],
+    "mc_ecor_create": [ctypes.c_int, _PP],
+    "mc_ecor_destroy": [_P],
+    "mc_ecor_set_sequence": [_P, _I64, _P],
+    "mc_ecor_set_tables": [_P, ctypes.c_int, _P, _P, ctypes.c_int, _P],
+    "mc_ecor_run": [_P, _I64, _P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float)],
 }
 _RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p}
 

@@ -12,13 +12,15 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmetacov_amd.so")
-SOURCES = ["engine.hip", "bam_decode.cpp", "bam_index.cpp", "bam_write.cpp", "common.cpp"]
+SOURCES = ["engine.hip", "ecor.hip", "bam_decode.cpp", "bam_index.cpp", "bam_write.cpp",
+           "exp_reads.cpp", "common.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
 def build(verbose=True, extra_flags=()):
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "common.h"),
+            os.path.join(CSRC, "bgzf.h"),
                    os.path.join(os.path.dirname(HERE), "include", "metacov_amd.h")]
     if os.path.exists(LIB) and not extra_flags and \
             os.path.getmtime(LIB) > max(os.path.getmtime(d) for d in deps):

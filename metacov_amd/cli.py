@@ -5,9 +5,10 @@ reference command (metacov/cli.py:35-108).
 
 Differences from the reference, all outside the CSV: the BAM need not be
 indexed (it is decoded whole by the library's C++ decoder); all regions are
-reduced in one batched GPU call; `-k/--kmer-histogram` (pileup.experimental,
-SURVEY.md §8 f rank 2) is not part of this build and is rejected with a
-usage error.
+reduced in one batched GPU call.  With `-k/--kmer-histogram` every row also
+carries pileup.experimental's 13 columns (cli.py:81, :93-95; SURVEY.md §8 f):
+the read side runs on host threads, the k-mer correlation against `-f` on
+the GPU (metacov_amd/experimental.py).
 
 Multi-GPU (one process per GPU, SURVEY.md §8 e):
 
@@ -27,6 +28,7 @@ import sys
 import click
 import numpy as np
 
+from . import experimental as _experimental
 from . import regions as _regions
 from .bam import BamFile, StreamedBam, index_stats
 from .engine import REGION_STAT_DTYPE, classic_stats
@@ -54,7 +56,7 @@ def main():
 @click.option('--regionfile-csv', '-rc', type=click.File('r'),
               help="Input Region file in CSV format")
 @click.option('--kmer-histogram', '-k', type=click.File('r'),
-              help="Kmer Histogram produced with metacov scan (not supported by this build)")
+              help="Kmer Histogram produced with metacov scan")
 @click.option('--kmer-length', '-K', type=int, default=7,
               help="Length of k-mer")
 @click.option('--outfile', '-o', type=click.File('w'), default="-",
@@ -68,15 +70,16 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     """
     Compute fold coverage values
     """
-    if kmer_histogram is not None:
-        raise click.UsageError("--kmer-histogram (pileup.experimental) is not supported by "
-                               "the metacov_amd engine")
+    fasta = reference_fasta.name if reference_fasta else None
+    # cli.py:81: the histogram is read with load_kmerhist's default k_len (7)
+    k_cor = _experimental.load_kmerhist(kmer_histogram) if kmer_histogram else None
+    exp = (k_cor, kmer_length, fasta) if k_cor is not None else None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile)
+        return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp)
     bam = StreamedBam(bamfile.name, device=device) if stream else BamFile(bamfile.name)
     regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam))
     log_counts(bam)
-    write_rows(bam, regions, outfile, device=device)
+    write_rows(bam, regions, outfile, device=device, exp=exp)
 
 
 def log_counts(bam):
@@ -129,11 +132,24 @@ def warn_depth_cap(max_depth):
                     HTSLIB_MAX_DEPTH)
 
 
-def write_csv(regions, rows, outfile):
-    """Rows in input order exactly as cli.py:97-108 writes them."""
+def experimental_results(path, exp, references, tids, starts, ends, device=0):
+    """pileup.experimental for every region (cli.py:93-95), or None without -k."""
+    if exp is None:
+        return None
+    k_cor, k_len, fasta = exp
+    regs = [(references[t], int(a), int(b)) for t, a, b in zip(tids, starts, ends)]
+    return _experimental.experimental_batch(path, k_cor, k_len, fasta, regs, device=device)
+
+
+def write_csv(regions, rows, outfile, extra=None):
+    """Rows in input order exactly as cli.py:97-108 writes them; `extra`
+    (experimental_batch results) adds the -k columns, its "RCOR is ZERO"
+    lines and its errors at the region where the reference meets them."""
     writer = None
-    for hit, row in zip(regions, rows):
+    for i, (hit, row) in enumerate(zip(regions, rows)):
         result = classic_stats(row)
+        if extra is not None:
+            result.update(extra[i].emit(out=sys.stdout))
         if writer is None:
             writer = csv.DictWriter(outfile, fieldnames=['sacc', 'start', 'end'] + sorted(result))
             writer.writeheader()
@@ -141,15 +157,19 @@ def write_csv(regions, rows, outfile):
         writer.writerow(result)
 
 
-def write_rows(bam, regions, outfile, device=0):
+def write_rows(bam, regions, outfile, device=0, exp=None):
     """Resolves names like cli.py:80-91, reduces all regions in one GPU call,
     then writes rows in input order exactly as cli.py:97-108 does."""
     tids, starts, ends = resolve_regions(bam, regions)
-    write_csv(regions, compute_rows(bam, tids, starts, ends, device), outfile)
+    rows = compute_rows(bam, tids, starts, ends, device)
+    extra = experimental_results(bam.filename, exp, bam.references, tids, starts, ends, device)
+    write_csv(regions, rows, outfile, extra)
 
 
-def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile):
-    """One rank of a multi-GPU `pileup` (launched by torch.distributed.run)."""
+def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None):
+    """One rank of a multi-GPU `pileup` (launched by torch.distributed.run).
+    With -k, rank 0 adds the experimental columns for all regions after the
+    gather (their read side is host work over the whole file)."""
     import torch
     import torch.distributed as dist
     from . import dist as mdist
@@ -187,7 +207,9 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile):
         table = mdist.all_gather_table(mdist.pack_rows(rows, mine), r_max, device=coll_dev)
         if rank == 0:
             log_counts(head)
-            write_csv(regions, mdist.unpack_rows(table, len(regions), REGION_STAT_DTYPE), outfile)
+            extra = experimental_results(path, exp, head.references, tids, starts, ends, device)
+            write_csv(regions, mdist.unpack_rows(table, len(regions), REGION_STAT_DTYPE), outfile,
+                      extra)
     finally:
         dist.destroy_process_group()
 

@@ -10,11 +10,15 @@ classic(): positions are 0-based half-open [start, end); positions the reads
 do not cover (or past the contig end) count as 0 (pileup.py:11-16); an empty
 region raises ValueError (pileup.py:19 on a zero-size vector); an unknown
 `ref` raises KeyError.
+
+`experimental` and `load_kmerhist` (pileup.py:29-173) are re-exported from
+`metacov_amd.experimental`, so `pileup.<name>` resolves as in the reference.
 """
 import numpy as np
 
 from .bam import BamFile
 from .engine import classic_stats
+from .experimental import experimental, load_kmerhist  # noqa: F401  (pileup.py:29-173)
 
 _open_files = {}
 

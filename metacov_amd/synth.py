@@ -73,11 +73,11 @@ def ref_len(cigar):
 
 
 class SynthRecord:
-    __slots__ = ("name", "tid", "pos", "flag", "cigar", "l_seq")
+    __slots__ = ("name", "tid", "pos", "flag", "cigar", "l_seq", "seq")
 
-    def __init__(self, name, tid, pos, flag, cigar, l_seq):
+    def __init__(self, name, tid, pos, flag, cigar, l_seq, seq=None):
         self.name, self.tid, self.pos, self.flag = name, tid, pos, flag
-        self.cigar, self.l_seq = cigar, l_seq
+        self.cigar, self.l_seq, self.seq = cigar, l_seq, seq
 
 
 def edge_mix_records(lengths, n_reads, readlen=150, seed=1, weights=None,
@@ -129,6 +129,8 @@ def edge_mix_records(lengths, n_reads, readlen=150, seed=1, weights=None,
 
 # ---------------------------------------------------------------- BGZF / BAM
 
+NT16 = "=ACMGRSVTWYHKDBN"
+
 _BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 
 
@@ -173,8 +175,13 @@ def encode_record(r, long_cigar_threshold=65535):
     if len(cig) > long_cigar_threshold:
         aux = b"CGBI" + struct.pack("<i", len(cig)) + struct.pack("<%dI" % len(cig), *cig)
         cig = [(r.l_seq << 4) | S, (max(ref_len(r.cigar), 1) << 4) | N]
-    l_seq = r.l_seq
-    seq = bytes([0x11] * ((l_seq + 1) // 2))   # "AA..." in nt16
+    if r.seq is None:
+        l_seq = r.l_seq
+        seq = bytes([0x11] * ((l_seq + 1) // 2))   # "AA..." in nt16
+    else:                                          # given bases (SAMv1 §4.2.3)
+        l_seq = len(r.seq)
+        codes = [NT16.index(c) for c in r.seq.upper()] + [0]
+        seq = bytes((codes[i] << 4) | codes[i + 1] for i in range(0, l_seq, 2))
     qual = bytes([30] * l_seq)
     end = r.pos + max(ref_len(r.cigar), 1)
     bin_ = _reg2bin(max(r.pos, 0), max(end, 1)) if r.tid >= 0 else 4680

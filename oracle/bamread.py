@@ -29,12 +29,15 @@ FLAG_FILTER = 0x704          # BAM_FUNMAP | BAM_FSECONDARY | BAM_FQCFAIL | BAM_F
 REF_CONSUMING_MASK = 0x18D   # bits for M(0) D(2) N(3) =(7) X(8)
 
 
-class Record:
-    __slots__ = ("tid", "pos", "flag", "cigar", "l_seq", "name")
+NT16 = "=ACMGRSVTWYHKDBN"   # BAM 4-bit base codes (SAMv1 §4.2.3)
 
-    def __init__(self, tid, pos, flag, cigar, l_seq, name):
+
+class Record:
+    __slots__ = ("tid", "pos", "flag", "cigar", "l_seq", "name", "seq")
+
+    def __init__(self, tid, pos, flag, cigar, l_seq, name, seq=""):
         self.tid, self.pos, self.flag = tid, pos, flag
-        self.cigar, self.l_seq, self.name = cigar, l_seq, name
+        self.cigar, self.l_seq, self.name, self.seq = cigar, l_seq, name, seq
 
     def ref_len(self):
         """htslib bam_cigar2rlen: sum of lengths of reference-consuming ops."""
@@ -82,11 +85,13 @@ def read_bam(path):
         cig = struct.unpack_from("<%dI" % n_cigar, data, p)
         cigar = [(c & 0xF, c >> 4) for c in cig]
         p += 4 * n_cigar
+        packed = data[p:p + (l_seq + 1) // 2]
+        seq = "".join(NT16[(packed[i >> 1] >> (4 * (1 - (i & 1)))) & 0xF] for i in range(l_seq))
         # CG:B,I long-CIGAR convention (SAMv1 §4.2.2): placeholder kSmN
         if (n_cigar == 2 and cigar[0] == (4, l_seq) and cigar[1][0] == 3):
             aux = p + (l_seq + 1) // 2 + l_seq
             cigar = _find_cg(data, aux, rec_end) or cigar
-        recs.append(Record(tid, pos, flag, cigar, l_seq, name))
+        recs.append(Record(tid, pos, flag, cigar, l_seq, name, seq))
         off = rec_end
     return names, lengths, recs
 

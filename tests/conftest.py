@@ -34,6 +34,11 @@ def synth_golden():
 
 
 @pytest.fixture(scope="session")
+def experimental_golden():
+    return load_golden("experimental.json")
+
+
+@pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
 

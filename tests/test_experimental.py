@@ -1,0 +1,339 @@
+"""pileup.experimental / load_kmerhist (reference metacov/pileup.py:29-173,
+SURVEY.md §8 f).
+
+Goldens (tests/golden/experimental.json) are the real reference function's
+outputs (make_experimental_golden.py).  Bar: every field bit-exact with the
+reference's value type, except `covc` (re-associated float sum: relative
+1e-12) and `ecor` / `cov3` (the reference's np.inner is a BLAS dot; the
+GPU correlation sums in another order: the unrounded ecor*L agrees to
+relative 1e-12, and the 3-decimal rounded values are equal unless the
+reference's value lies within 1e-9 of a rounding tie).
+
+CPU tests: the oracle against the goldens, the host read side (no FASTA) of
+the product against the goldens and the oracle, load_kmerhist, the taps.
+GPU tests: everything with a FASTA (the ecor kernel), the CLI's -k columns.
+"""
+import contextlib
+import io
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import experimental as ox
+from metacov_amd import experimental as mx
+from metacov_amd import synth
+
+EXACT_FP = {"covc": 1e-12}
+NEAR_TIE = ("ecor", "cov3")
+
+
+@pytest.fixture(scope="module")
+def gold(experimental_golden):
+    return experimental_golden
+
+
+def _same(key, want, got, tie_ok=False):
+    if isinstance(want, float) and math.isnan(want):
+        return isinstance(got, (float, np.floating)) and math.isnan(got)
+    if key in EXACT_FP:
+        return abs(got - want) <= EXACT_FP[key] * max(1.0, abs(want))
+    if want == got:
+        return True
+    if tie_ok and key in NEAR_TIE:
+        # a rounding tie the re-associated sum may fall either side of
+        return abs(got - want) <= 1.0001e-3
+    return False
+
+
+def check_result(case, res, tie_ok=False):
+    if "error" in case:
+        assert res.error is not None, case["region"]
+        assert type(res.error).__name__ == case["error"], (case["region"], res.error)
+        return
+    assert res.error is None, (case["region"], res.error)
+    assert set(res.row) == set(case["row"])
+    for key, want in case["row"].items():
+        got = res.row[key]
+        assert _same(key, want, got, tie_ok), (case["bam"], case["kcor"], case["region"], key,
+                                               want, got)
+        assert type(got).__name__ == case["types"][key], (key, type(got).__name__)
+    assert res.zero_lines == case["stdout"].splitlines()
+
+
+def _kcor(gold, case):
+    return gold["kcor"][case["kcor"]] if case["kcor"] else None
+
+
+# ------------------------------------------------------------------ CPU
+
+def test_oracle_matches_reference_goldens(gold, golden_dir):
+    """The restatement, run on duck-typed pysam objects, reproduces every
+    golden exactly (values, types, printed lines, errors)."""
+    bams, fastas = {}, {}
+    for case in gold["cases"]:
+        bam = bams.setdefault(case["bam"], ox.DuckBam(os.path.join(golden_dir, case["bam"])))
+        fa = None
+        if case["fasta"]:
+            fa = fastas.setdefault(case["fasta"],
+                                   ox.DuckFasta(os.path.join(golden_dir, case["fasta"])))
+        buf = io.StringIO()
+        try:
+            with contextlib.redirect_stdout(buf):
+                row = ox.experimental(bam, _kcor(gold, case), case["k"], fa, *case["region"])
+            err = None
+        except Exception as e:  # noqa: BLE001
+            row, err = None, e
+        res = mx.RegionResult(row=row, error=err, zero_lines=buf.getvalue().splitlines())
+        check_result(case, res)
+
+
+def test_read_side_matches_goldens(gold, golden_dir, lib_built):
+    """Host C++ read pass (mc_experimental_reads) + the Python finish, for the
+    cases without a FASTA (no GPU needed)."""
+    n = 0
+    for case in gold["cases"]:
+        if case["fasta"]:
+            continue
+        res = mx.experimental_batch(os.path.join(golden_dir, case["bam"]), _kcor(gold, case),
+                                    case["k"], None, [tuple(case["region"])])[0]
+        check_result(case, res)
+        n += 1
+    assert n >= 10
+
+
+def test_taps_equal_scipy():
+    ref = ox.norm_taps()
+    assert np.array_equal(mx.norm_taps(), ref)
+    sps = pytest.importorskip("scipy.stats")
+    assert np.array_equal(sps.norm(450, 150).pdf(range(0, 901)).ravel(), ref)
+
+
+def test_load_kmerhist(tmp_path):
+    csv = tmp_path / "k.csv"
+    csv.write_text(
+        "kmer,n0,n1,n2,R,Mapped\n"
+        "AAAAAAA,4,2,6,R1,Mapped\n"
+        "NNNNNNN,9,9,9,R1,Mapped\n"
+        "CCCCCCC,3,1,2,R2,Mapped\n"
+        "GGGGGGG,5,5,5,R1,Unmapped\n"
+        "TTTTTTT,0,0,0,R2,Mapped\n"
+        "ACGTACG,1,0,0,R1,Mapped\n")
+    got = mx.load_kmerhist(str(csv))
+    want = ox.load_kmerhist(str(csv))
+    assert got[0].keys() == want[0].keys() and got[1].keys() == want[1].keys()
+    assert got[0]["AAAAAAA"] == 4 / 4 and got[1]["CCCCCCC"] == 3 / 1.5
+    assert "NNNNNNN" not in got[0] and "GGGGGGG" not in got[0]
+    assert math.isnan(got[1]["TTTTTTT"]) and math.isinf(got[0]["ACGTACG"])
+    # file objects, as the CLI passes them (cli.py:81)
+    with open(csv) as fh:
+        assert mx.load_kmerhist(fh)[1].keys() == got[1].keys()
+
+
+def test_kmer_tables_drop_foreign_keys(caplog):
+    t = mx.KmerTables([{"ACGT": 2.0, "ACG": 1.0, "ACNT": 3.0}, {"TTTT": 0.5}], 4)
+    assert t.has.sum() == 2
+    assert t.val[0, 0b00011011] == 2.0 and t.val[1, 255] == 0.5
+    assert t.decode(0b00011011) == "ACGT"
+    assert "dropped" in caplog.text
+
+
+def _long_bam(path, seed, L=60_000, pairs=2_500):
+    """One long contig, paired reads with real bases: regions longer than
+    numpy's 8192-element reduction chunk, many starts and mates."""
+    rng = np.random.default_rng(seed)
+    ref = "".join(rng.choice(list("ACGT"), size=L))
+    recs = []
+    for q in range(pairs):
+        rl = int(rng.integers(50, 150))
+        p1 = int(rng.integers(0, L - rl))
+        p2 = int(min(L - rl, p1 + rng.integers(0, 600)))
+        for mate, (p, rev) in enumerate(((p1, False), (p2, True))):
+            seq = ref[p:p + rl]
+            if rng.random() < 0.05:
+                seq = "N" + seq[1:]
+            flag = 0x1 | (0x40 if mate == 0 else 0x80) | (0x10 if rev else 0)
+            u = rng.random()
+            flag |= 0x2 if u < 0.9 else (0x102 if u < 0.95 else 0)
+            recs.append(synth.SynthRecord("p%d" % q, 0, p, flag, [(0, rl)], rl, seq))
+    recs.sort(key=lambda r: r.pos)
+    synth.write_bam(path, ["chr"], [L], recs)
+    return ref
+
+
+def test_read_side_long_regions_vs_oracle(tmp_path, lib_built):
+    path = str(tmp_path / "long.bam")
+    _long_bam(path, 5)
+    k = 5
+    rng = np.random.default_rng(6)
+    keys = ["".join(p) for p in __import__("itertools").product("ACGT", repeat=k)]
+    kc = [{x: float(rng.uniform(0.3, 3)) for x in keys if rng.random() < 0.8} for _ in range(2)]
+    kc[0][keys[7]] = 0.0
+    regions = [("chr", 0, 60_000), ("chr", 123, 41_000), ("chr", 8_191, 16_385),
+               ("chr", 59_000, 70_000), ("chr", 30_000, 30_017)]
+    bam = ox.DuckBam(path)
+    with mx.ReadTable(path, k) as table:
+        got = mx.experimental_batch(table, kc, k, None, regions)
+    for (ref, s, e), res in zip(regions, got):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            want = ox.experimental(bam, kc, k, None, ref, s, e)
+        case = {"row": {a: (float(b) if isinstance(b, np.floating) else b) for a, b in want.items()},
+                "types": {a: type(b).__name__ for a, b in want.items()},
+                "stdout": buf.getvalue(), "bam": "long", "kcor": "k5", "region": [ref, s, e]}
+        check_result(case, res)
+
+
+def test_unsorted_bam_rejected(tmp_path, lib_built):
+    from metacov_amd._lib import MetacovError
+    path = str(tmp_path / "u.bam")
+    synth.write_bam(path, ["c"], [1000], [
+        synth.SynthRecord("a", 0, 500, 0x3, [(0, 10)], 10, "ACGTACGTAC"),
+        synth.SynthRecord("b", 0, 100, 0x3, [(0, 10)], 10, "ACGTACGTAC")])
+    with pytest.raises(MetacovError):
+        mx.ReadTable(path, 4)
+
+
+def test_region_errors_without_gpu(golden_dir, lib_built):
+    bam = os.path.join(golden_dir, "bbmap.sorted.bam")
+    res = mx.experimental_batch(bam, [{}, {}], 7, None,
+                                [("ref1", 5, 5), ("nope", 0, 10), ("ref1", 0, 300),
+                                 ("ref1", 0, 10)])
+    assert type(res[0].error) is Exception and str(res[0].error) == "Length must be > 0"
+    assert isinstance(res[1].error, ValueError)
+    assert res[2].error is None
+    # every position of ref1[0:10] has a read start: nzef = 0, and without a
+    # FASTA (ecor = -1, a Python int) cov3 divides a Python float by 0.0
+    assert isinstance(res[3].error, ZeroDivisionError)
+    with pytest.raises(ZeroDivisionError):
+        ox.experimental(ox.DuckBam(bam), [{}, {}], 7, None, "ref1", 0, 10)
+    with pytest.raises(Exception, match="Length must be > 0"):
+        mx.experimental(bam, [{}, {}], 7, None, "ref1", 3, 3)
+
+
+# ------------------------------------------------------------------ GPU
+
+@pytest.mark.gpu
+def test_goldens_with_fasta_gpu(gold, golden_dir, lib_built):
+    """Every golden case through the product, FASTA cases on the GPU kernel."""
+    reads = {}
+    for case in gold["cases"]:
+        key = (case["bam"], case["k"])
+        if key not in reads:
+            reads[key] = mx.ReadTable(os.path.join(golden_dir, case["bam"]), case["k"])
+        fasta = os.path.join(golden_dir, case["fasta"]) if case["fasta"] else None
+        res = mx.experimental_batch(reads[key], _kcor(gold, case), case["k"], fasta,
+                                    [tuple(case["region"])])[0]
+        check_result(case, res, tie_ok=True)
+    for r in reads.values():
+        r.close()
+
+
+@pytest.mark.gpu
+def test_goldens_batched_gpu(gold, golden_dir, lib_built):
+    """All regions of one (bam, fasta, k_cor) in one batch: same rows."""
+    groups = {}
+    for case in gold["cases"]:
+        groups.setdefault((case["bam"], case["fasta"], case["kcor"], case["k"]), []).append(case)
+    for (bam, fasta, kc, k), cases in groups.items():
+        got = mx.experimental_batch(os.path.join(golden_dir, bam),
+                                    gold["kcor"][kc] if kc else None, k,
+                                    os.path.join(golden_dir, fasta) if fasta else None,
+                                    [tuple(c["region"]) for c in cases])
+        for case, res in zip(cases, got):
+            check_result(case, res, tie_ok=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 4, 7, 11])
+def test_ecor_kernel_vs_oracle_gpu(k, lib_built, tmp_path):
+    """mc_ecor_run against the oracle's per-position arrays (np.inner) on
+    random sequence with lower case and N runs, multi-tile regions, regions
+    cut short by the sequence end and a table with zero / inf weights."""
+    rng = np.random.default_rng(100 + k)
+    seqs = []
+    for L in (70_000, 5_000, 900, 3):
+        s = rng.choice(list("ACGTacgtN"), size=L, p=[.22, .22, .22, .22, .02, .02, .02, .02, .04])
+        seqs.append("".join(s))
+    fa = tmp_path / "r.fa"
+    fa.write_text("".join(">s%d extra\n%s\n" % (i, s) for i, s in enumerate(seqs)))
+    n = 4 ** k
+    vals = [rng.uniform(0.2, 3.0, size=n) for _ in range(2)]
+    for v in vals:
+        v[rng.random(n) < 0.2] = 0.0
+    vals[1][rng.integers(0, n)] = np.inf if k == 4 else vals[1][0]
+    codes = ["".join(p) for p in __import__("itertools").product("ACGT", repeat=k)] if k <= 7 \
+        else None
+    if codes is None:    # large k: keep a random subset of keys
+        idx = rng.choice(n, size=5000, replace=False)
+        to_s = lambda c: "".join("ACGT"[(c >> (2 * (k - 1 - m))) & 3] for m in range(k))  # noqa: E731
+        kc = [{to_s(int(c)): float(v[c]) for c in idx} for v in vals]
+    else:
+        kc = [{codes[c]: float(v[c]) for c in range(n)} for v in vals]
+    fasta = mx.FastaFile(str(fa))
+    regions = [("s0", 0, 70_000), ("s0", 10, 2058), ("s0", 4095, 4096 + 2048 * 3 + 5),
+               ("s0", 69_500, 71_000), ("s1", 0, 5000), ("s1", 4990, 6000), ("s2", 0, 900),
+               ("s3", 0, 3), ("s3", 5, 50), ("s0", 3, 4)]
+    tables = mx.KmerTables(kc, k)
+    eng = mx.EcorEngine(0)
+    eng.set_sequence(fasta)
+    eng.set_tables(tables)
+    spans = [fasta.span(*r) for r in regions]
+    inner, gc, at = eng.run([s[0] for s in spans], [s[1] for s in spans],
+                            [r[2] - r[1] for r in regions])
+    eng.close()
+    for q, (ref, s, e) in enumerate(regions):
+        region = fasta.fetch(ref, s, e).upper()
+        want = ox.raw_ecor(kc, k, region, e - s)
+        if np.isnan(want):
+            assert np.isnan(inner[q])
+        else:
+            assert abs(inner[q] - want) <= 1e-12 * max(1.0, abs(want)), (ref, s, e, inner[q], want)
+        assert gc[q] == region.count("G") + region.count("C")
+        assert at[q] == region.count("A") + region.count("T")
+
+
+@pytest.mark.gpu
+def test_cli_kmer_histogram_gpu(golden_dir, fixture_golden, lib_built, tmp_path):
+    """`metacov pileup -k H -f F`: classic + experimental columns per region
+    (cli.py:81, :93-108), against the reference's classic goldens and the
+    oracle's experimental on the same k_cor."""
+    import csv as _csv
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    rng = np.random.default_rng(11)
+    keys = ["".join(p) for p in __import__("itertools").product("ACGT", repeat=7)]
+    rows = ["kmer,n0,n1,n2,R,Mapped"]
+    for r in ("R1", "R2"):
+        for x in keys:
+            if rng.random() < 0.7:
+                rows.append("%s,%d,%d,%d,%s,Mapped" % (x, rng.integers(1, 50), rng.integers(1, 50),
+                                                       rng.integers(1, 50), r))
+    rows.append("NNNNNNN,1,1,1,R1,Mapped")
+    hist = tmp_path / "k.csv"
+    hist.write_text("\n".join(rows) + "\n")
+    fasta = os.path.join(golden_dir, "reference_1K.fa.gz")
+    bam = os.path.join(golden_dir, "bbmap.sorted.bam")
+    out = tmp_path / "o.csv"
+    res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"),
+                                          "-k", str(hist), "-f", fasta, "-o", str(out)])
+    assert res.exit_code == 0, res.output
+    got = list(_csv.DictReader(open(out, newline="")))
+    kc = ox.load_kmerhist(str(hist))
+    obam, ofa = ox.DuckBam(bam), ox.DuckFasta(fasta)
+    b7 = fixture_golden["blast7"]
+    assert len(got) == len(b7)
+    assert list(got[0].keys()) == ["sacc", "start", "end"] + sorted(
+        list(b7[0]["stats"]) + ["cov", "covc", "den", "denc", "cov2", "cf", "ambig", "improper",
+                                "nzef", "gc", "ecor", "wnf", "cov3"])
+    for g, w in zip(got, b7):
+        for key, v in w["stats"].items():
+            assert g[key] == str(v), key
+        s, e = sorted((int(w["start"]), int(w["end"])))
+        want = ox.experimental(obam, kc, 7, ofa, w["sacc"], s, e)
+        for key, v in want.items():
+            if key in ("covc", "ecor", "cov3"):
+                assert abs(float(g[key]) - float(v)) <= 1.0001e-3 * max(1.0, abs(float(v))), key
+            else:
+                assert g[key] == str(v), (key, g[key], v)

@@ -48,8 +48,9 @@ def test_whole_contigs_and_exclusive():
         regions.make_region_iterator(io.StringIO(""), io.StringIO(""), B())
 
 
-def test_cli_rejects_kmer_histogram(tmp_path, golden_dir):
-    """-k (pileup.experimental) is outside this build: a usage error, before
+def test_cli_kmer_histogram_without_columns(tmp_path, golden_dir):
+    """-k with a histogram lacking the Mapped / R columns fails in
+    load_kmerhist with the reference's AttributeError (pileup.py:31), before
     any GPU work (runs on CPU)."""
     from click.testing import CliRunner
     from metacov_amd.cli import pileup
@@ -57,4 +58,4 @@ def test_cli_rejects_kmer_histogram(tmp_path, golden_dir):
     k.write_text("kmer,n\n")
     res = CliRunner().invoke(pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
                                       "-k", str(k), "-o", str(tmp_path / "o.csv")])
-    assert res.exit_code == 2 and "kmer-histogram" in res.output
+    assert res.exit_code == 1 and isinstance(res.exception, AttributeError)
