@@ -295,6 +295,71 @@ int mc_ecor_run(mc_ecor* e, int64_t R, const int64_t* base, const int64_t* n_ava
                 const int64_t* length, double* inner, int64_t* gc, int64_t* at,
                 float* kernel_ms);
 
+/* ---- metacov scan: read histograms (SURVEY.md §8 f ranks 3-4) --------------
+ * Replaces scan.scan_reads + the ReadProcessor plugins (metacov/scan.pyx:
+ * 345-376 ReadProcessor / ReadProcessorList, 380-419 ByFlag, 422-476
+ * BaseHist, 479-511 KmerHist, 514-552 MirrorHist, 555-588 IsizeHist,
+ * 623-672 scan_reads) and the read iterators they are fed by
+ * (AlignmentFileIterator scan.pyx:188-294, FastQFileIterator :297-340 over
+ * pyfq.FastQFile / FastQFilePair, pyfq.pyx:60-270).
+ *
+ * Sources (host C++): every record of a BAM (file order, placed and unplaced)
+ * or of one FASTQ / a FASTQ pair (plain or gzip), handed out in SoA batches
+ * of the ReadIterator accessors: rlen = get_len, flag = get_flags, gpos =
+ * get_pos, gisize = get_isize, tid = get_tid (int32 each), packed nt16 bases
+ * (2 per byte, high nibble first; seq_off[n + 1] byte offsets).  Batch
+ * arrays are borrowed until the next mc_scan_src_next. */
+typedef struct mc_scan_src mc_scan_src;
+int mc_scan_src_open_bam(const char* path, int n_threads, mc_scan_src** out);
+int mc_scan_src_open_fastq(const char* path1, const char* path2, mc_scan_src** out);
+int mc_scan_src_close(mc_scan_src* s);
+int mc_scan_src_n_targets(const mc_scan_src* s, int32_t* n);
+int mc_scan_src_target(const mc_scan_src* s, int32_t i, const char** name, int64_t* length);
+int mc_scan_src_next(mc_scan_src* s, int64_t max_reads, int64_t max_seq_bytes, int64_t* n_out);
+int mc_scan_src_batch(const mc_scan_src* s, const int32_t** rlen, const int32_t** flag,
+                      const int32_t** gpos, const int32_t** gisize, const int32_t** tid,
+                      const int64_t** seq_off, const uint8_t** seq, int64_t* seq_bytes);
+int mc_scan_src_records(const mc_scan_src* s, int64_t* n_records);
+
+/* Histograms (GPU).  The processor tree the CLI builds (cli.py:247-257):
+ * ByFlag over any of BaseHist(base_start), KmerHist(k, nk, step, offset),
+ * MirrorHist(offset, n), IsizeHist, grouped by the flag masks in order
+ * (2^n_flags groups, the first flag the most significant group bit).
+ * mc_scan_set_reference: FASTA sequences (ASCII) for BaseHist / MirrorHist;
+ * a batch's ref_id selects one per read (-1: none; reads as N).
+ * mc_scan_run drives a source through the kernel (max_reads 0 = all), with
+ * tid_to_ref mapping source tids to reference sequences.  Results come back
+ * group-major in the reference's layouts: base [G][rows][5] with rows =
+ * max(50, longest read) + base_start, kmer [G][4^K+1][NK], mirror
+ * [G][N+1][2], isize [G][isize_cap] and isize_max [G]. */
+typedef struct mc_scan_config {
+    int32_t n_flags;
+    uint32_t flags[16];
+    int32_t base_on, base_start;
+    int32_t kmer_on, kmer_k, kmer_nk, kmer_step, kmer_offset;
+    int32_t mirror_on, mirror_offset, mirror_n;
+    int32_t isize_on;
+} mc_scan_config;
+typedef struct mc_scan mc_scan;
+int mc_scan_create(int device, const mc_scan_config* cfg, mc_scan** out);
+int mc_scan_destroy(mc_scan* s);
+int mc_scan_set_reference(mc_scan* s, int32_t n_seq, const int64_t* off, const int64_t* len,
+                          int64_t n_bytes, const uint8_t* ascii);
+int mc_scan_add_batch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag,
+                      const int32_t* gpos, const int32_t* gisize, const int32_t* ref_id,
+                      const int64_t* seq_off, const uint8_t* seq);
+int mc_scan_add_batch_device(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag,
+                             const int32_t* gpos, const int32_t* gisize, const int32_t* ref_id,
+                             const int64_t* seq_off, const uint8_t* seq, int32_t max_rlen,
+                             int64_t max_abs_isize, float* kernel_ms);
+int mc_scan_run(mc_scan* s, mc_scan_src* src, int32_t n_map, const int32_t* tid_to_ref,
+                int64_t max_reads, int64_t batch_reads, int64_t* n_done);
+int mc_scan_dims(mc_scan* s, int32_t* groups, int64_t* base_rows, int64_t* isize_cap,
+                 int32_t* max_rlen, int64_t* n_reads);
+int mc_scan_results(mc_scan* s, uint32_t* base, uint32_t* kmer, uint32_t* mirror,
+                    uint32_t* isize, int32_t* isize_max);
+int mc_scan_timing(mc_scan* s, float* last_kernel_ms, int64_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,17 @@ class RegionStat(ctypes.Structure):
                 ("q23_sum", ctypes.c_int64), ("q23_cnt", ctypes.c_int64)]
 
 
+class ScanConfig(ctypes.Structure):
+    """mc_scan_config."""
+    _fields_ = [("n_flags", ctypes.c_int32), ("flags", ctypes.c_uint32 * 16),
+                ("base_on", ctypes.c_int32), ("base_start", ctypes.c_int32),
+                ("kmer_on", ctypes.c_int32), ("kmer_k", ctypes.c_int32),
+                ("kmer_nk", ctypes.c_int32), ("kmer_step", ctypes.c_int32),
+                ("kmer_offset", ctypes.c_int32),
+                ("mirror_on", ctypes.c_int32), ("mirror_offset", ctypes.c_int32),
+                ("mirror_n", ctypes.c_int32), ("isize_on", ctypes.c_int32)]
+
+
 class Timings(ctypes.Structure):
     _fields_ = [("cigar_ms", ctypes.c_float), ("depth_ms", ctypes.c_float),
                 ("stats_ms", ctypes.c_float), ("prepare_ms", ctypes.c_float),
@@ -114,6 +125,25 @@ SIGNATURES = {
     "mc_ecor_set_sequence": [_P, _I64, _P],
     "mc_ecor_set_tables": [_P, ctypes.c_int, _P, _P, ctypes.c_int, _P],
     "mc_ecor_run": [_P, _I64, _P, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_float)],
+    # metacov scan: read sources (host) and histograms (GPU)
+    "mc_scan_src_open_bam": [ctypes.c_char_p, ctypes.c_int, _PP],
+    "mc_scan_src_open_fastq": [ctypes.c_char_p, ctypes.c_char_p, _PP],
+    "mc_scan_src_close": [_P],
+    "mc_scan_src_n_targets": [_P, _PI32],
+    "mc_scan_src_target": [_P, _I32, ctypes.POINTER(ctypes.c_char_p), _PI64],
+    "mc_scan_src_next": [_P, _I64, _I64, _PI64],
+    "mc_scan_src_batch": [_P, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PI64],
+    "mc_scan_src_records": [_P, _PI64],
+    "mc_scan_create": [ctypes.c_int, _P, _PP],
+    "mc_scan_destroy": [_P],
+    "mc_scan_set_reference": [_P, _I32, _P, _P, _I64, _P],
+    "mc_scan_add_batch": [_P, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "mc_scan_add_batch_device": [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _I64,
+                                 ctypes.POINTER(ctypes.c_float)],
+    "mc_scan_run": [_P, _P, _I32, _P, _I64, _I64, _PI64],
+    "mc_scan_dims": [_P, _PI32, _PI64, _PI64, _PI32, _PI64],
+    "mc_scan_results": [_P, _P, _P, _P, _P, _P],
+    "mc_scan_timing": [_P, ctypes.POINTER(ctypes.c_float), _PI64],
 }
 _RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p}
 

@@ -12,8 +12,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmetacov_amd.so")
-SOURCES = ["engine.hip", "ecor.hip", "bam_decode.cpp", "bam_index.cpp", "bam_write.cpp",
-           "exp_reads.cpp", "common.cpp"]
+SOURCES = ["engine.hip", "ecor.hip", "scan.hip", "bam_decode.cpp", "bam_index.cpp",
+           "bam_write.cpp", "exp_reads.cpp", "scan_src.cpp", "common.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

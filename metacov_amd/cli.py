@@ -30,6 +30,7 @@ import numpy as np
 
 from . import experimental as _experimental
 from . import regions as _regions
+from . import scan as _scan
 from .bam import BamFile, StreamedBam, index_stats
 from .engine import REGION_STAT_DTYPE, classic_stats
 
@@ -212,6 +213,127 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
                       extra)
     finally:
         dist.destroy_process_group()
+
+
+@main.command()
+@click.option("--readfile-type", "-t",
+              type=click.Choice(['bam', 'fq']),
+              help="Override filename based detection of readfile type.")
+@click.option("--max-reads", "-m",
+              type=click.IntRange(1), metavar="N",
+              help="Only consider the first N reads.")
+@click.option("--group-by", "-g",
+              type=click.Choice(_scan.Flags.keys()), multiple=True, metavar="FLAG",
+              help="Group output by BAM flag. May be specified multiple times. "
+              "FLAG can be one of {}".format(list(_scan.Flags.keys())))
+@click.option('--reference-fasta', '-f',
+              type=click.File('rb'), metavar="FILE",
+              help="Fasta file reads where mapped to. Required for boffset."
+              " File may be bgzip'ed, but not gzip'ed.")
+@click.option("--out-basehist", "-b",
+              type=click.File("w", lazy=False), metavar="FILE",
+              help="Compute histogram of base counts by position in read.")
+@click.option('--boffset', '-bo',
+              type=click.IntRange(0, 200), default=0, metavar="N", show_default=True,
+              help="Include N bases prior to read start in base histogram. "
+              "Requires reference fasta file.")
+@click.option("--out-kmerhist", "-o",
+              type=click.File("w", lazy=False), metavar="FILE",
+              help="Compute histogram of kmers in reads")
+@click.option("-k",
+              type=click.IntRange(2, 12), default=7, metavar="N", show_default=True,
+              help="Length of kmers")
+@click.option("--step", "-s",
+              type=click.IntRange(1, 100), default=7, metavar="N", show_default=True,
+              help="Step between sampled kmers")
+@click.option("--offset", "-O",
+              type=click.IntRange(-100, 100), default=0, metavar="N", show_default=True,
+              help="Offset of first sampled kmer")
+@click.option("--number", "-n",
+              type=click.IntRange(1, 100), default=8, metavar="N", show_default=True,
+              help="Numer of sampled kmers")
+@click.option('--out-mirrorhist', '-M',
+              type=click.File('w', lazy=False), metavar="FILE",
+              help="Compute histogram of mismatches against palindrome")
+@click.option('--mirror-offset', '-MO',
+              type=click.IntRange(-100, 100), default=4, metavar="N", show_default=True,
+              help="Offset of palindrome center from read start")
+@click.option('--mirror-length', '-Ml',
+              type=click.IntRange(1, 50), default=10, metavar="N", show_default=True,
+              help="Palindrome length is 2N+1")
+@click.option('--out-isizehist', '-I',
+              type=click.File('w', lazy=False), metavar="FILE",
+              help="Compute histogram of insert sizes.")
+@click.option('--device', type=int, default=0, help="HIP device ordinal")
+@click.argument("readfile", nargs=-1, required=True)
+def scan(readfile, readfile_type, out_basehist, boffset, out_kmerhist,
+         k, number, step, offset, max_reads, reference_fasta,
+         out_mirrorhist, mirror_offset, mirror_length,
+         out_isizehist, group_by, device):
+    """
+    Gather read statistics
+    """
+    # reference metacov/cli.py:162-285: same options, checks and CSV files;
+    # the histograms run on the GPU (metacov_amd/scan.py)
+    if not readfile_type:
+        for ext, ft in {'.bam': 'bam', '.sam': 'bam', '.fq': 'fq', '.fq.gz': 'fq',
+                        '.fastq': 'fq', '.fastq.gz': 'fq'}.items():
+            if readfile[0].endswith(ext):
+                readfile_type = ft
+                break
+    if not readfile_type:
+        raise click.UsageError("Couldn't guess input format. Please supply -t")
+    if readfile_type != 'fq' and len(readfile) > 1:
+        raise click.UsageError("Multiple input files only supported for fastq")
+    if len(readfile) > 2:
+        raise click.UsageError("At most two fastq files allowed (fwd and rev)")
+    if readfile_type != 'bam' and reference_fasta:
+        raise click.UsageError("Reference fasta can only be used with mapped (bam/sam) reads")
+
+    from . import pyfq
+    fasta = None
+    if readfile_type == 'bam':
+        infile = readfile[0]
+        if os.path.exists(infile + ".bai"):
+            head = BamFile(infile, contigs=[])
+            mapped, unmapped, nocoor = index_stats(infile + ".bai", len(head.lengths))
+            mapped, unmapped = int(mapped.sum()), int(unmapped.sum()) + nocoor
+            log.info("mapped = {}, unmapped = {}, total = {}".format(
+                mapped, unmapped, mapped + unmapped))
+        if reference_fasta:
+            fasta = reference_fasta.name
+    else:
+        infile = (pyfq.FastQFilePair(readfile[0], readfile[1]) if len(readfile) > 1
+                  else pyfq.FastQFile(readfile[0]))
+
+    counters = []
+    if out_basehist:
+        counters.append(_scan.BaseHist(boffset))
+    if out_kmerhist:
+        counters.append(_scan.KmerHist(k, number, step, offset))
+    if out_mirrorhist:
+        counters.append(_scan.MirrorHist(mirror_offset, mirror_length))
+    if out_isizehist:
+        counters.append(_scan.IsizeHist())
+    counters = _scan.ByFlag(counters, [_scan.Flags[flag] for flag in group_by])
+
+    nreads = _scan.scan_reads(infile, fasta, counters, maxreads=max_reads or 0, device=device)
+    log.info("Processed {} reads".format(nreads))
+
+    # the reference's output index sequence, including the missing
+    # `n = n + 1` after the k-mer table (cli.py:266-285)
+    n = 0
+    if out_basehist:
+        csv.writer(out_basehist).writerows(counters.get_rows(n))
+        n = n + 1
+    if out_kmerhist:
+        csv.writer(out_kmerhist).writerows(counters.get_rows(n))
+    if out_mirrorhist:
+        csv.writer(out_mirrorhist).writerows(counters.get_rows(n))
+        n = n + 1
+    if out_isizehist:
+        csv.writer(out_isizehist).writerows(counters.get_rows(n))
+        n = n + 1
 
 
 if __name__ == "__main__":

@@ -73,11 +73,11 @@ def ref_len(cigar):
 
 
 class SynthRecord:
-    __slots__ = ("name", "tid", "pos", "flag", "cigar", "l_seq", "seq")
+    __slots__ = ("name", "tid", "pos", "flag", "cigar", "l_seq", "seq", "tlen")
 
-    def __init__(self, name, tid, pos, flag, cigar, l_seq, seq=None):
+    def __init__(self, name, tid, pos, flag, cigar, l_seq, seq=None, tlen=0):
         self.name, self.tid, self.pos, self.flag = name, tid, pos, flag
-        self.cigar, self.l_seq, self.seq = cigar, l_seq, seq
+        self.cigar, self.l_seq, self.seq, self.tlen = cigar, l_seq, seq, tlen
 
 
 def edge_mix_records(lengths, n_reads, readlen=150, seed=1, weights=None,
@@ -125,6 +125,77 @@ def edge_mix_records(lengths, n_reads, readlen=150, seed=1, weights=None,
     for j in range(unplaced):
         recs.append(SynthRecord("u%d" % j, -1, -1, 0x4, [], readlen))
     return recs
+
+
+def scan_mix(n_reads=800, n_contigs=4, contig_len=3000, seed=7, long_reads=4):
+    """(names, lengths, records, fasta) for `scan` tests: reads whose bases
+    come from their contig (BaseHist's match test passes for most), a few
+    percent mutated, N bases, lower-case and IUPAC letters in the FASTA, a
+    contig the FASTA lacks, reads running off either contig end, reverse
+    strand, proper pairs with +/- insert sizes, unmapped-but-placed and
+    unplaced records, empty SEQ, and `long_reads` reads of 1-3 kbp."""
+    rng = np.random.default_rng(seed)
+    names = ["c%d" % i for i in range(n_contigs)]
+    lengths = [contig_len + 37 * i for i in range(n_contigs)]
+    alphabet = np.array(list("ACGT"))
+    contigs = []
+    for L in lengths:
+        s = alphabet[rng.integers(0, 4, L)]
+        s[rng.random(L) < 0.01] = "N"
+        low = rng.random(L) < 0.05
+        s[low] = np.char.lower(s[low])
+        s[rng.random(L) < 0.002] = "R"
+        contigs.append("".join(s))
+    fasta = {n: c for n, c in zip(names[:-1], contigs[:-1])}   # the last contig is missing
+    recs = []
+    for i in range(n_reads):
+        tid = int(rng.integers(0, n_contigs))
+        L = lengths[tid]
+        rlen = int(rng.integers(20, 160)) if i >= long_reads else int(rng.integers(1000, 3000))
+        pos = int(rng.integers(-20, L - rlen + 40))
+        pos = max(pos, 0)
+        ref = contigs[tid].upper()
+        bases = list(ref[pos:pos + rlen].ljust(rlen, "A"))
+        for j in np.nonzero(rng.random(rlen) < (0.2 if i % 17 == 0 else 0.01))[0]:
+            bases[j] = "ACGTN"[int(rng.integers(0, 5))]
+        bases = ["N" if b not in "ACGT" else b for b in bases]
+        flag = 0
+        if rng.random() < 0.8:
+            flag |= 0x1 | (0x40 if i % 2 == 0 else 0x80)
+            if rng.random() < 0.7:
+                flag |= 0x2
+            if rng.random() < 0.5:
+                flag |= 0x20
+            if rng.random() < 0.05:
+                flag |= 0x8
+        if rng.random() < 0.5:
+            flag |= 0x10
+        if rng.random() < 0.03:
+            flag |= 0x4
+        if rng.random() < 0.03:
+            flag |= 0x100
+        if rng.random() < 0.02:
+            flag |= 0x400
+        tlen = int(rng.integers(100, 700)) * (1 if rng.random() < 0.5 else -1)
+        if rng.random() < 0.1:
+            tlen = 0
+        seq = "" if i % 97 == 5 else "".join(bases)
+        recs.append(SynthRecord("s%d" % i, tid, pos, flag, [(0, max(len(seq), 1))], len(seq),
+                                seq=seq, tlen=tlen))
+    recs.sort(key=lambda r: (r.tid, r.pos))
+    for j in range(6):
+        seq = "".join(alphabet[rng.integers(0, 4, 60)])
+        recs.append(SynthRecord("u%d" % j, -1, -1, 0x4 | 0x1 | 0x2, [], 60, seq=seq,
+                                tlen=int(rng.integers(-500, 500))))
+    return names, lengths, recs, fasta
+
+
+def write_fasta(path, seqs, width=60):
+    with open(path, "w") as fh:
+        for name, s in seqs.items():
+            fh.write(">%s description\n" % name)
+            for i in range(0, len(s), width):
+                fh.write(s[i:i + width] + "\n")
 
 
 # ---------------------------------------------------------------- BGZF / BAM
@@ -186,7 +257,7 @@ def encode_record(r, long_cigar_threshold=65535):
     end = r.pos + max(ref_len(r.cigar), 1)
     bin_ = _reg2bin(max(r.pos, 0), max(end, 1)) if r.tid >= 0 else 4680
     core = struct.pack("<iiBBHHHiiii", r.tid, r.pos, len(name), 60, bin_, len(cig),
-                       r.flag, l_seq, r.tid, r.pos, 0)
+                       r.flag, l_seq, r.tid, r.pos, getattr(r, "tlen", 0))
     body = core + name + struct.pack("<%dI" % len(cig), *cig) + seq + qual + aux
     return struct.pack("<i", len(body)) + body
 

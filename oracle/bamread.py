@@ -33,11 +33,12 @@ NT16 = "=ACMGRSVTWYHKDBN"   # BAM 4-bit base codes (SAMv1 §4.2.3)
 
 
 class Record:
-    __slots__ = ("tid", "pos", "flag", "cigar", "l_seq", "name", "seq")
+    __slots__ = ("tid", "pos", "flag", "cigar", "l_seq", "name", "seq", "tlen")
 
-    def __init__(self, tid, pos, flag, cigar, l_seq, name, seq=""):
+    def __init__(self, tid, pos, flag, cigar, l_seq, name, seq="", tlen=0):
         self.tid, self.pos, self.flag = tid, pos, flag
         self.cigar, self.l_seq, self.name, self.seq = cigar, l_seq, name, seq
+        self.tlen = tlen
 
     def ref_len(self):
         """htslib bam_cigar2rlen: sum of lengths of reference-consuming ops."""
@@ -78,7 +79,7 @@ def read_bam(path):
         (block_size,) = struct.unpack_from("<i", data, off)
         rec_end = off + 4 + block_size
         (tid, pos, l_read_name, _mapq, _bin, n_cigar, flag, l_seq,
-         _ntid, _npos, _tlen) = struct.unpack_from("<iiBBHHHiiii", data, off + 4)
+         _ntid, _npos, tlen) = struct.unpack_from("<iiBBHHHiiii", data, off + 4)
         p = off + 36
         name = data[p:p + l_read_name - 1].decode()
         p += l_read_name
@@ -91,7 +92,7 @@ def read_bam(path):
         if (n_cigar == 2 and cigar[0] == (4, l_seq) and cigar[1][0] == 3):
             aux = p + (l_seq + 1) // 2 + l_seq
             cigar = _find_cg(data, aux, rec_end) or cigar
-        recs.append(Record(tid, pos, flag, cigar, l_seq, name, seq))
+        recs.append(Record(tid, pos, flag, cigar, l_seq, name, seq, tlen))
         off = rec_end
     return names, lengths, recs
 

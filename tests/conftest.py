@@ -48,3 +48,19 @@ def lib_built():
     from metacov_amd import build
     build.build(verbose=False)
     return build.LIB
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """torch ships its own HIP runtime (torch/lib/libamdhip64.so) beside the
+    /opt/rocm one libmetacov_amd links; torch only finds the GPU when its
+    runtime initialises first.  GPU runs therefore touch torch's device
+    before any test creates a library context."""
+    expr = request.config.getoption("-m") or ""
+    if "gpu" in expr and "not gpu" not in expr:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.zeros(1, device="cuda")
+        except Exception:   # a test that needs torch reports it itself
+            pass

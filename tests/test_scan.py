@@ -1,0 +1,445 @@
+"""`metacov scan` (reference metacov/cli.py:112-285, metacov/scan.pyx,
+metacov/pyfq.pyx; SURVEY.md §8 f ranks 3-4).
+
+Pinned: the FASTQ readers (the oracle's, the product's Python pyfq mirror
+and the C++ batch source the GPU path reads through) against the known
+answers of the reference's tests/test_pyfq.py (tests/golden/pyfq.json).
+Histograms: parity unpinned beyond oracle/scan.py, the line-by-line
+restatement of scan.pyx (the Cython cannot be built here: SURVEY.md §8 c);
+the GPU path must reproduce its CSV files byte for byte.  Bar: bit-exact
+(integer histograms).
+"""
+import ctypes
+import gzip
+import os
+
+import numpy as np
+import pytest
+from click.testing import CliRunner
+
+from oracle import bamread
+from oracle import scan as oscan
+from metacov_amd import synth
+
+
+@pytest.fixture(scope="module")
+def pyfq_golden(golden_dir):
+    import json
+    with open(os.path.join(golden_dir, "pyfq.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def mix(tmp_path_factory):
+    d = tmp_path_factory.mktemp("scanmix")
+    names, lengths, recs, fasta = synth.scan_mix()
+    bam = str(d / "mix.bam")
+    synth.write_bam(bam, names, lengths, recs)
+    fa = str(d / "mix.fa")
+    synth.write_fasta(fa, fasta)
+    return bam, fa
+
+
+def _paths(golden_dir, files):
+    return [os.path.join(golden_dir, f) for f in files]
+
+
+# ------------------------------------------------------------ FASTQ (pinned)
+
+def _hist(reads):
+    lengths, freq, n = [0] * 11, [0] * 5, 0
+    for rlen, seq in reads:
+        lengths[int(rlen / 10)] += 1
+        for b in seq:
+            freq[b] += 1
+        n += 1
+    return lengths, freq, n
+
+
+def test_oracle_fastq_matches_reference_known_answers(pyfq_golden, golden_dir):
+    for case in pyfq_golden["cases"]:
+        paths = _paths(golden_dir, case["files"])
+        f = oscan.FastQFile(*paths) if len(paths) == 1 else oscan.FastQFilePair(*paths)
+        assert f.size == case["size_kb"]
+        lengths, freq, _ = _hist((r.rlen, r.seq) for r in f.reads())
+        assert lengths == case["lengths_by_10"]
+        assert freq == case["base_freq"]
+
+
+def test_pyfq_matches_reference_known_answers(pyfq_golden, golden_dir):
+    """reference tests/test_pyfq.py:12-45 against metacov_amd.pyfq."""
+    from metacov_amd import pyfq
+    for case in pyfq_golden["cases"]:
+        paths = _paths(golden_dir, case["files"])
+        fq = pyfq.FastQFile(*paths) if len(paths) == 1 else pyfq.FastQFilePair(*paths)
+        with fq as infile:
+            assert infile.size == case["size_kb"]
+            assert infile.pos == 0
+            lengths, freq = [0] * 11, [0] * 5
+            for read in infile:
+                lengths[int(read.rlen / 10)] += 1
+                assert read.pos <= infile.size
+                for base in read.seq:
+                    assert 0 <= base < 5
+                    freq[base] += 1
+        assert freq == case["base_freq"]
+        assert lengths == case["lengths_by_10"]
+
+
+def test_pyfq_writer_round_trip(pyfq_golden, golden_dir, tmp_path):
+    """reference tests/test_pyfq.py:48-64."""
+    from metacov_amd import pyfq
+    src = os.path.join(golden_dir, "ecoli_1K_1.fq.gz")
+    out = str(tmp_path / "out.fq.gz")
+    n1 = 0
+    with pyfq.FastQFile(src) as infile, pyfq.FastQWriter(out) as outfile:
+        for read in infile:
+            outfile.write(read)
+            n1 += 1
+    n2 = 0
+    with pyfq.FastQFile(out) as a, pyfq.FastQFile(src) as b:
+        for r1, r2 in zip(a, b):
+            assert r1.rlen == r2.rlen and r1.seq == r2.seq
+            n2 += 1
+    assert n1 == n2 == pyfq_golden["writer_records"]
+
+
+def _src_batches(lib, h, cap=997):
+    from metacov_amd import _lib
+    P = ctypes.c_void_p
+    while True:
+        n = ctypes.c_int64()
+        _lib.check(lib.mc_scan_src_next(h, cap, 1 << 20, ctypes.byref(n)), lib)
+        if n.value == 0:
+            return
+        ptrs = [P() for _ in range(7)]
+        nb = ctypes.c_int64()
+        _lib.check(lib.mc_scan_src_batch(h, *[ctypes.byref(p) for p in ptrs], ctypes.byref(nb)), lib)
+        k = n.value
+
+        def arr(p, dt, m):
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(dt)), shape=(m,)).copy() \
+                if m else np.zeros(0, np.dtype(dt))
+        cols = [arr(ptrs[i], ctypes.c_int32, k) for i in range(5)]
+        off = arr(ptrs[5], ctypes.c_int64, k + 1)
+        seq = arr(ptrs[6], ctypes.c_uint8, nb.value)
+        yield cols, off, seq
+
+
+def _unpack(seq, off, rlen):
+    nib = np.empty(2 * len(seq), np.uint8)
+    nib[0::2] = seq >> 4
+    nib[1::2] = seq & 15
+    t = np.array(oscan.NT16_NT4, np.uint8)
+    return [t[nib[2 * off[i]:2 * off[i] + rlen[i]]] for i in range(len(rlen))]
+
+
+def test_cpp_fastq_source_matches_reference_known_answers(pyfq_golden, golden_dir, lib_built):
+    from metacov_amd import _lib
+    lib = _lib.load()
+    for case in pyfq_golden["cases"]:
+        paths = _paths(golden_dir, case["files"])
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_src_open_fastq(paths[0].encode(),
+                                              paths[1].encode() if len(paths) > 1 else None,
+                                              ctypes.byref(h)), lib)
+        try:
+            reads, flags = [], []
+            for (rlen, flag, gpos, gisize, tid), off, seq in _src_batches(lib, h):
+                assert (gpos == -1).all() and (gisize == -1).all() and (tid == -1).all()
+                flags += flag.tolist()
+                reads += list(zip(rlen.tolist(), _unpack(seq, off, rlen)))
+        finally:
+            lib.mc_scan_src_close(h)
+        lengths, freq, n = _hist(reads)
+        assert lengths == case["lengths_by_10"]
+        assert freq == case["base_freq"]
+        if len(paths) == 2:   # FastQFilePair: second file first
+            assert flags[:4] == [0x81, 0x41, 0x81, 0x41]
+        else:
+            assert set(flags) == {0}
+        # record by record against the oracle iterator
+        want = list(oscan.fastq_reads(*paths))
+        assert [(r.rlen, list(r.seq), r.flags) for r in want] == \
+               [(a, list(s), f) for (a, s), f in zip(reads, flags)]
+
+
+def test_cpp_fastq_source_truncated_and_plain(tmp_path, lib_built):
+    """A file ending inside a record ends the stream (pyfq.pyx:166-175); the
+    last quality line may lack its newline; plain files read as-is."""
+    from metacov_amd import _lib
+    lib = _lib.load()
+    text = b"@a\nACGTN\n+\nIIIII\n@b\nacgtx\n+\nIIIII"   # no final newline
+    for name, data in (("t.fq", text), ("t2.fq", text + b"\n@c\nAC\n+\n")):
+        p = tmp_path / name
+        p.write_bytes(data)
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_src_open_fastq(str(p).encode(), None, ctypes.byref(h)), lib)
+        got = []
+        for (rlen, *_), off, seq in _src_batches(lib, h):
+            got += [(int(a), s.tolist()) for a, s in zip(rlen, _unpack(seq, off, rlen))]
+        lib.mc_scan_src_close(h)
+        assert got == [(6, [0, 1, 2, 3, 4, 4]), (6, [0, 1, 2, 3, 4, 4])]
+        want = [(r.rlen, r.seq) for r in oscan.fastq_reads(str(p))]
+        assert got == want
+
+
+def test_cpp_bam_source_matches_oracle(mix, golden_dir, lib_built):
+    """Every record in file order, with the ReadIterator accessor values."""
+    from metacov_amd import _lib
+    lib = _lib.load()
+    for path in (mix[0], os.path.join(golden_dir, "bbmap.sorted.bam"),
+                 os.path.join(golden_dir, "synth_edge.bam")):
+        _names, _lengths, recs = bamread.read_bam(path)
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_src_open_bam(path.encode(), 2, ctypes.byref(h)), lib)
+        rows = []
+        for (rlen, flag, gpos, gisize, tid), off, seq in _src_batches(lib, h, cap=301):
+            codes = []
+            for i in range(len(rlen)):
+                b = seq[off[i]:off[i + 1]]
+                nib = np.empty(2 * len(b), np.uint8)
+                nib[0::2], nib[1::2] = b >> 4, b & 15
+                codes.append("".join(bamread.NT16[c] for c in nib[:rlen[i]]))
+            rows += list(zip(rlen.tolist(), flag.tolist(), gpos.tolist(), gisize.tolist(),
+                             tid.tolist(), codes))
+        n = ctypes.c_int64()
+        lib.mc_scan_src_records(h, ctypes.byref(n))
+        lib.mc_scan_src_close(h)
+        assert n.value == len(recs)
+        want = [(r.l_seq, r.flag, r.pos + r.l_seq if r.flag & 0x10 else r.pos,
+                 r.tlen if r.flag & 2 else 0, r.tid, r.seq) for r in recs]
+        assert rows == want
+
+
+# ----------------------------------------------------- processors (no GPU)
+
+def test_byflag_rows_layout():
+    """ByFlag.get_rows: header + group columns in reverse -g order, groups
+    in bit order (scan.pyx:395-405) -- same rows as the oracle's."""
+    from metacov_amd import scan as mscan
+    pf = [mscan.Flags["Mapped"], mscan.Flags["Readdir"]]
+    of = [oscan.Flags["Mapped"], oscan.Flags["Readdir"]]
+    m = mscan.ByFlag([mscan.MirrorHist(4, 3), mscan.IsizeHist()], pf)
+    o = oscan.ByFlag([oscan.MirrorHist(4, 3), oscan.IsizeHist()], of)
+    rng = np.random.default_rng(0)
+    for g in range(4):
+        c = rng.integers(0, 9, (4, 2)).astype(np.uint32)
+        m.processors[g].processors[0]._add(c)
+        o.processors[g].processors[0].counts = c.tolist()
+        isz = rng.integers(0, 5, 9).astype(np.uint32)
+        m.processors[g].processors[1]._add(isz, 3 + g)
+        o.processors[g].processors[1].counts = dict(enumerate(isz.tolist()))
+        o.processors[g].processors[1].max_isize = 3 + g
+    for i in range(2):
+        got = [[str(v) for v in row] for row in m.get_rows(i)]
+        want = [[str(v) for v in row] for row in o.get_rows(i)]
+        assert got == want
+    assert got[0] == ["n", "count", "Readdir", "Mapped"]
+    assert got[1][-2:] == ["Forward", "Mapped"]
+
+
+@pytest.mark.parametrize("args,msg", [
+    (["x.txt", "-o", "o.csv"], "Couldn't guess input format"),
+    (["a.bam", "b.bam", "-o", "o.csv"], "Multiple input files only supported for fastq"),
+    (["a.fq", "b.fq", "c.fq", "-o", "o.csv"], "At most two fastq files allowed"),
+])
+def test_cli_scan_usage_errors(tmp_path, args, msg):
+    from metacov_amd.cli import scan
+    with CliRunner().isolated_filesystem(temp_dir=tmp_path):
+        r = CliRunner().invoke(scan, args)
+    assert r.exit_code == 2 and msg in r.output
+
+
+def test_cli_scan_fasta_with_fastq_rejected(tmp_path, golden_dir):
+    from metacov_amd.cli import scan
+    fq = os.path.join(golden_dir, "ecoli_1K_1.fq.gz")
+    fa = tmp_path / "r.fa"
+    fa.write_text(">x\nACGT\n")
+    r = CliRunner().invoke(scan, [fq, "-f", str(fa), "-o", str(tmp_path / "o.csv")])
+    assert r.exit_code == 2
+    assert "Reference fasta can only be used with mapped (bam/sam) reads" in r.output
+
+
+# ----------------------------------------------------------- GPU parity
+
+def _cli_scan(tmp_path, readfile, out, extra=()):
+    from metacov_amd.cli import scan
+    files = {"base": "-b", "kmer": "-o", "mirror": "-M", "isize": "-I"}
+    args = list(readfile)
+    for name in out:
+        args += [files[name], str(tmp_path / (name + ".csv"))]
+    r = CliRunner().invoke(scan, args + list(extra))
+    assert r.exit_code == 0, (r.output, r.exception)
+    texts = {}
+    for name in out:
+        with open(tmp_path / (name + ".csv"), newline="") as fh:
+            texts[name] = fh.read()
+    return texts
+
+
+def _oracle_kwargs(extra):
+    kw, it = {}, iter(extra)
+    keys = {"-f": "fasta", "-bo": "boffset", "-k": "k", "-n": "number", "-s": "step",
+            "-O": "offset", "-MO": "mirror_offset", "-Ml": "mirror_length", "-m": "max_reads"}
+    groups = []
+    for a in it:
+        v = next(it)
+        if a == "-g":
+            groups.append(v)
+        else:
+            kw[keys[a]] = v if a == "-f" else int(v)
+    kw["group_by"] = groups
+    return kw
+
+
+ALL = ("base", "kmer", "mirror", "isize")
+
+BAM_CASES = [
+    ("bbmap", ALL, ("-f", "@fa")),
+    ("bbmap", ("base", "kmer"), ()),                                   # no FASTA
+    ("bbmap", ALL, ("-f", "@fa", "-g", "Mapped", "-g", "Readdir", "-bo", "5")),
+    ("mix", ALL, ("-f", "@mixfa")),
+    ("mix", ALL, ("-f", "@mixfa", "-g", "IsRead1", "-g", "PairedProperly", "-g", "Readdir",
+                  "-bo", "7", "-k", "3", "-n", "5", "-s", "2", "-O", "-3", "-MO", "-2",
+                  "-Ml", "6")),
+    ("mix", ("kmer", "isize"), ("-k", "9", "-n", "3", "-s", "40", "-O", "2")),
+    ("mix", ("mirror", "base"), ("-f", "@mixfa", "-MO", "30", "-Ml", "3", "-m", "300")),
+    # 6 flags -> 64 groups: BaseHist no longer fits in LDS (global atomics)
+    ("mix", ("base", "isize"), ("-f", "@mixfa", "-g", "Paired", "-g", "PairedProperly",
+                                "-g", "Mapped", "-g", "Readdir", "-g", "IsRead1",
+                                "-g", "MateReaddir")),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(BAM_CASES)))
+def test_scan_bam_cli_vs_oracle_gpu(case, mix, golden_dir, lib_built, tmp_path):
+    which, out, extra = BAM_CASES[case]
+    bam = mix[0] if which == "mix" else os.path.join(golden_dir, "bbmap.sorted.bam")
+    subst = {"@fa": os.path.join(golden_dir, "reference_1K.fa.gz"), "@mixfa": mix[1]}
+    extra = [subst.get(a, a) for a in extra]
+    got = _cli_scan(tmp_path, [bam], out, extra)
+    want = oscan.scan_csv([bam], out, **_oracle_kwargs(extra))
+    for name in out:
+        assert got[name] == want[name], name
+
+
+FQ_CASES = [
+    (["ecoli_1K_1.fq.gz"], ("kmer", "base"), ()),                       # reference test_scan
+    (["ecoli_1K_2.fq.gz"], ALL, ("-k", "5", "-n", "12", "-s", "8", "-O", "1")),
+    (["ecoli_1K_1.fq.gz", "ecoli_1K_2.fq.gz"], ("kmer", "isize"), ("-g", "IsRead1")),
+    (["ecoli_1K_1.fq.gz", "ecoli_1K_2.fq.gz"], ("kmer", "mirror"), ("-m", "777", "-g", "IsRead2",
+                                                                    "-g", "Paired")),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(FQ_CASES)))
+def test_scan_fastq_cli_vs_oracle_gpu(case, golden_dir, lib_built, tmp_path):
+    files, out, extra = FQ_CASES[case]
+    paths = _paths(golden_dir, files)
+    got = _cli_scan(tmp_path, paths, out, extra)
+    want = oscan.scan_csv(paths, out, **_oracle_kwargs(extra))
+    for name in out:
+        assert got[name] == want[name], name
+
+
+@pytest.mark.gpu
+def test_scan_reads_api_accumulates_gpu(mix, lib_built):
+    """scan_reads twice into the same counters: counts add up, BaseHist is
+    cut back to 50 + start_pos rows at each call's set_max_readlen(50)."""
+    from metacov_amd import scan as mscan
+    bam, fa = mix
+    m = mscan.ByFlag([mscan.BaseHist(2), mscan.KmerHist(4, 3, 5, 1), mscan.IsizeHist()],
+                     [mscan.Flags["Readdir"]])
+    o = oscan.ByFlag([oscan.BaseHist(2), oscan.KmerHist(4, 3, 5, 1), oscan.IsizeHist()],
+                     [oscan.Flags["Readdir"]])
+    fasta = oscan.read_fasta(fa)
+    for maxreads in (0, 50):
+        assert mscan.scan_reads(bam, fa, m, maxreads=maxreads) == \
+               oscan.scan_reads(oscan.bam_reads(bam, fasta), o, maxreads)
+    for i in range(3):
+        assert [[str(v) for v in r] for r in m.get_rows(i)] == \
+               [[str(v) for v in r] for r in o.get_rows(i)]
+
+
+@pytest.mark.gpu
+def test_scan_large_isize_and_long_reads_gpu(tmp_path, lib_built):
+    """Insert sizes beyond the LDS arena (global IsizeHist) and 20 kbp reads
+    (BaseHist rows beyond the arena), against the oracle."""
+    rng = np.random.default_rng(3)
+    L = 60000
+    ref = "".join(np.array(list("ACGT"))[rng.integers(0, 4, L)])
+    recs = []
+    for i in range(40):
+        rl = int(rng.integers(15000, 20000)) if i < 6 else 120
+        pos = int(rng.integers(0, L - rl))
+        recs.append(synth.SynthRecord("q%d" % i, 0, pos, 0x3 | (0x10 if i % 3 else 0),
+                                      [(0, rl)], rl, seq=ref[pos:pos + rl],
+                                      tlen=int(rng.integers(-90000, 90000))))
+    recs.sort(key=lambda r: r.pos)
+    bam = str(tmp_path / "long.bam")
+    synth.write_bam(bam, ["big"], [L], recs)
+    fa = str(tmp_path / "big.fa")
+    synth.write_fasta(fa, {"big": ref})
+    got = _cli_scan(tmp_path, [bam], ("base", "isize", "mirror"), ["-f", fa, "-bo", "3"])
+    want = oscan.scan_csv([bam], ("base", "isize", "mirror"), fasta=fa, boffset=3)
+    assert got == want
+
+
+@pytest.mark.gpu
+def test_scan_kernel_device_batch_gpu(lib_built):
+    """mc_scan_add_batch_device (the bench path) equals mc_scan_add_batch."""
+    import torch
+    from metacov_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    n = 5000
+    rlen = rng.integers(0, 200, n).astype(np.int32)
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum((rlen + 1) // 2)
+    seq = rng.integers(0, 256, int(off[-1])).astype(np.uint8)
+    flag = rng.integers(0, 0x800, n).astype(np.int32)
+    gpos = rng.integers(-5, 3000, n).astype(np.int32)
+    gis = rng.integers(-900, 900, n).astype(np.int32)
+    rid = rng.integers(-1, 2, n).astype(np.int32)
+    refs = rng.choice(list(b"ACGTNacgt"), 5000).astype(np.uint8)
+    roff = np.array([0, 2500], np.int64)
+    rlen_ref = np.array([2500, 2500], np.int64)
+    cfg = _lib.ScanConfig()
+    cfg.n_flags = 2
+    cfg.flags[0], cfg.flags[1] = 0x10, 0x40
+    cfg.base_on, cfg.base_start = 1, 4
+    cfg.kmer_on, cfg.kmer_k, cfg.kmer_nk, cfg.kmer_step, cfg.kmer_offset = 1, 6, 9, 5, 2
+    cfg.mirror_on, cfg.mirror_offset, cfg.mirror_n = 1, 4, 10
+    cfg.isize_on = 1
+    outs = []
+    for mode in ("host", "device"):
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_create(0, ctypes.byref(cfg), ctypes.byref(h)), lib)
+        _lib.check(lib.mc_scan_set_reference(h, 2, _lib.ptr(roff), _lib.ptr(rlen_ref), refs.size,
+                                             _lib.ptr(refs)), lib)
+        arrs = [rlen, flag, gpos, gis, rid, off, seq]
+        if mode == "host":
+            _lib.check(lib.mc_scan_add_batch(h, n, *[_lib.ptr(a) for a in arrs]), lib)
+        else:
+            dev = [torch.from_numpy(a).cuda() for a in arrs]
+            ms = ctypes.c_float()
+            _lib.check(lib.mc_scan_add_batch_device(h, n, *[ctypes.c_void_p(t.data_ptr()) for t in dev],
+                                                    int(rlen.max()), int(np.abs(gis).max()),
+                                                    ctypes.byref(ms)), lib)
+            assert ms.value > 0
+        G, rows, cap = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        lib.mc_scan_dims(h, ctypes.byref(G), ctypes.byref(rows), ctypes.byref(cap), None, None)
+        base = np.zeros((4, rows.value, 5), np.uint32)
+        kmer = np.zeros((4, 4 ** 6 + 1, 9), np.uint32)
+        mir = np.zeros((4, 11, 2), np.uint32)
+        isz = np.zeros((4, cap.value), np.uint32)
+        mx = np.zeros(4, np.int32)
+        _lib.check(lib.mc_scan_results(h, *[_lib.ptr(a) for a in (base, kmer, mir, isz, mx)]), lib)
+        lib.mc_scan_destroy(h)
+        outs.append((base, kmer, mir, isz, mx))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    assert outs[0][0].sum() > 0 and outs[0][1].sum() > 0 and outs[0][3].sum() == n
