@@ -64,8 +64,14 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kLdsWords = 12288;   // 48 KiB: 3 workgroups per CU
+constexpr int kWaves = kThreads / 64;
+constexpr int kLdsWords = 8192;     // histogram arena: 32 KiB
+constexpr int kSeqStage = 6144;     // per wave: packed bases of the batch
+constexpr int kRefStage = 2048;     // per wave: reference window of the batch
+constexpr int kStagePad = 16;
+constexpr int kStageBytes = kSeqStage + kRefStage + 2 * kStagePad;
 constexpr int kMaxFlags = 16;
+constexpr int kRefPad = 64;         // zero bytes before and after the device reference
 
 struct ScanArgs {
     const int32_t* rlen;
@@ -76,7 +82,8 @@ struct ScanArgs {
     const int64_t* seq_off;
     const uint8_t* seq;
     int64_t n;
-    const uint8_t* ref;       // nt4 codes, all sequences back to back
+    int64_t per_wave;         // reads per wave (a multiple of 64)
+    const uint8_t* ref;       // nt4 codes, all sequences back to back (padded both ends)
     const int64_t* ref_off;
     const int64_t* ref_len;
     int32_t n_ref;
@@ -86,9 +93,13 @@ struct ScanArgs {
     // BaseHist: [row][G][5]
     int32_t base_on, base_start, base_rows, base_lds;
     uint32_t* base;
-    // KmerHist: [G][4^K + 1][NK]
+    // KmerHist: [G][NK][4^K + 1] (slot-major on the device).  kcodes != null:
+    // the codes go to kcodes[slot][read] (u16, 0xFFFF = no k-mer) and
+    // kmer_count_kernel counts them; else global atomics here.
     int32_t kmer_on, K, NK, STEP, OFF;
     uint32_t* kmer;
+    uint16_t* kcodes;
+    uint16_t* kgroup;         // per read group (G > 1 with kcodes)
     // MirrorHist: [G][N + 1][2]
     int32_t mir_on, MOFF, MN, mir_lds;
     uint32_t* mir;
@@ -96,76 +107,102 @@ struct ScanArgs {
     int32_t isz_on, isz_cap, isz_lds;
     uint32_t* isz;
     int32_t* isz_max;
-    // LDS arena (words)
-    int32_t lds_base, lds_mir, lds_isz, lds_isz_max, lds_words;
+    // LDS arena (words) and the staging area after it
+    int32_t lds_base, lds_mir, lds_isz, lds_isz_max, lds_words, stage_off;
+    int32_t* error;           // set when a read's bases are not 4-byte aligned
 };
 
-__device__ __forceinline__ int nt16_nt4(uint32_t v) {
-    return (v != 0 && (v & (v - 1)) == 0) ? __builtin_ctz(v) : 4;
-}
+// LDS pointers carry their address space explicitly: generic pointers into
+// LDS compile to flat instructions (vector-memory path, several times
+// slower than ds_* for the atomics and byte reads this kernel lives on).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+
+// nt16 code -> nt4 (scan.pyx:26-29): 1/2/4/8 -> 0..3, anything else -> 4
+constexpr uint64_t kNt4 = 0x4444444344424104ull;   // nibble v holds nt4(v)
+
+__device__ __forceinline__ int nt4_of(uint32_t v) { return (int)((kNt4 >> (4 * v)) & 15); }
 
 __device__ __forceinline__ int comp4(int n) { return n < 4 ? 3 - n : 4; }
 
-// nt16 nibble of base j of the read whose packed bases start at s
-__device__ __forceinline__ uint32_t nib(const uint8_t* s, int64_t j) {
-    const uint32_t b = s[j >> 1];
-    return (j & 1) ? (b & 15u) : (b >> 4);
+// base j (0 = high nibble of byte 0) of a dword holding 8 packed bases
+__device__ __forceinline__ uint32_t nib8(uint32_t w, int j) {
+    return (w >> (8 * (j >> 1) + 4 * (1 - (j & 1)))) & 15u;
 }
 
-struct Ref {
-    const uint8_t* p;
+// The read's reference sequence: a staged LDS window [wlo, whi) of it (the
+// batch's span) and the global copy for everything else.  Cython indexing:
+// one negative wrap; outside [0, L) reads N.
+struct RefWin {
+    const uint8_t* g;     // global nt4, sequence start (nullptr: no sequence)
     int64_t L;
+    lds_cu8* w;           // LDS: position wlo
+    int64_t wlo, whi;
     __device__ __forceinline__ int at(int64_t i) const {
+        if (!g) return 4;
         if (i < 0) i += L;
-        return (i < 0 || i >= L) ? 4 : (int)p[i];
+        if (i < 0 || i >= L) return 4;
+        return (i >= wlo && i < whi) ? (int)w[i - wlo] : (int)g[i];
+    }
+    // 8 consecutive positions p..p+7, all inside [wlo, whi + 8) (window
+    // padding covers the overhang): nt4 bytes little-endian in two dwords
+    __device__ __forceinline__ void at8(int64_t p, uint32_t& lo, uint32_t& hi) const {
+        const uint32_t a = (uint32_t)(uintptr_t)(w + (p - wlo));   // LDS byte address
+        lds_cu32* q = (lds_cu32*)(uintptr_t)(a & ~3u);
+        const uint32_t sh = a & 3u;
+        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+        lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
     }
 };
 
-__device__ __forceinline__ void inc(uint32_t* lds_or_null, uint32_t* g, int64_t i, bool in_lds) {
+__device__ __forceinline__ void inc(lds_u32* lds_base, uint32_t* g, int64_t i, bool in_lds) {
     if (in_lds)
-        atomicAdd(lds_or_null + i, 1u);
+        __hip_atomic_fetch_add(lds_base + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     else
         atomicAdd(g + i, 1u);
 }
 
-__global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
-    extern __shared__ uint32_t lds[];
-    for (int i = threadIdx.x; i < a.lds_words; i += kThreads) lds[i] = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * kThreads;
-    for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += stride) {
-        const int32_t rlen = a.rlen[r], flag = a.flag[r], gpos = a.gpos[r];
-        const int64_t so = a.seq_off[r];
-        const uint8_t* s = a.seq + so;
-        const bool rev = (flag & 0x10) != 0;
-        int g = 0;
-        for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((flag & a.fmask[f]) ? 1 : 0);
-        Ref ref{nullptr, 0};
-        const int32_t rid = a.ref_id[r];
-        if (rid >= 0 && rid < a.n_ref) ref = Ref{a.ref + a.ref_off[rid], a.ref_len[rid]};
+// Per-read rules (see the header): s = the read's packed bases (LDS or
+// global, 4-byte aligned), rw = its reference.
+// Returns true when the read passed BaseHist's match test and `defer` left
+// the counting of its bases to the caller.
+template <typename P8, typename P32>
+__device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s, P32 s32,
+                                             const RefWin& rw, lds_u32* lds, bool defer,
+                                             bool isize_done) {
+    const int32_t rlen = a.rlen[r], flag = a.flag[r], gpos = a.gpos[r];
+    const bool rev = (flag & 0x10) != 0;
+    int g = 0;
+    for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((flag & a.fmask[f]) ? 1 : 0);
 
-        if (a.isz_on) {
-            int32_t v = a.gisize[r];
-            v = v < 0 ? -v : v;
-            const int64_t bin = (int64_t)v * a.G + g;
-            inc(lds + a.lds_isz, a.isz, bin, a.isz_lds);
-            if (a.isz_lds)
-                atomicMax(reinterpret_cast<int32_t*>(lds + a.lds_isz_max) + g, v);
-            else
-                atomicMax(a.isz_max + g, v);
-        }
+    if (a.isz_on && !isize_done) {
+        int32_t v = a.gisize[r];
+        v = v < 0 ? -v : v;
+        inc(lds + a.lds_isz, a.isz, (int64_t)v * a.G + g, a.isz_lds);
+        if (a.isz_lds)
+            __hip_atomic_fetch_max((__attribute__((address_space(3))) int32_t*)(lds + a.lds_isz_max) + g,
+                                   v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            atomicMax(a.isz_max + g, v);
+    }
 
-        if (a.kmer_on && rlen >= a.OFF + a.STEP * a.NK) {
-            const uint32_t nbucket = 1u << (2 * a.K);
-            uint32_t* kg = a.kmer + (int64_t)g * (nbucket + 1) * a.NK;
-            for (int i = 0; i < a.NK; ++i) {
-                uint32_t k = 0;
+    if (a.kmer_on) {
+        const uint32_t nbucket = 1u << (2 * a.K);
+        const bool ok = rlen >= a.OFF + a.STEP * a.NK;
+        if (a.kcodes && a.G > 1) a.kgroup[r] = (uint16_t)g;
+        for (int i = 0; i < a.NK; ++i) {
+            uint32_t k = 0xFFFFu;
+            if (ok) {
+                k = 0;
                 for (int j = 0; j < a.K; ++j) {
-                    const int64_t x = (int64_t)a.OFF + (int64_t)i * a.STEP + j;
+                    const int x = a.OFF + i * a.STEP + j;
                     int c = 4;
                     if (x >= 0 && x < rlen) {
-                        c = nt16_nt4(nib(s, rev ? rlen - 1 - x : x));
+                        const int b = rev ? rlen - 1 - x : x;
+                        const uint32_t byte = s[b >> 1];
+                        c = nt4_of((b & 1) ? (byte & 15u) : (byte >> 4));
                         if (rev) c = comp4(c);
                     }
                     if (c > 3) {
@@ -174,67 +211,300 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
                     }
                     k |= (uint32_t)c << (2 * j);
                 }
-                atomicAdd(kg + (int64_t)k * a.NK + i, 1u);
             }
+            if (a.kcodes)
+                a.kcodes[(int64_t)i * a.n + r] = (uint16_t)k;
+            else if (ok)
+                atomicAdd(a.kmer + ((int64_t)g * a.NK + i) * (nbucket + 1) + k, 1u);
         }
+    }
 
-        if (a.mir_on) {
-            const int64_t p = (int64_t)gpos + a.MOFF;
-            if (p >= (int64_t)a.MN - a.MOFF) {
-                int plain = 0, cmp = 0;
-                for (int i = 0; i < a.MN; ++i) {
-                    const int x = ref.at(p + i + 1), y = ref.at(p - i - 1);
-                    plain += x != y;
-                    cmp += x != comp4(y);
+    if (a.mir_on) {
+        const int64_t p = (int64_t)gpos + a.MOFF;
+        if (p >= (int64_t)a.MN - a.MOFF) {
+            int plain = 0, cmp = 0;
+            for (int i = 0; i < a.MN; ++i) {
+                const int x = rw.at(p + i + 1), y = rw.at(p - i - 1);
+                plain += x != y;
+                cmp += x != comp4(y);
+            }
+            const int64_t b = ((int64_t)g * (a.MN + 1)) * 2;
+            inc(lds + a.lds_mir, a.mir, b + plain * 2, a.mir_lds);
+            inc(lds + a.lds_mir, a.mir, b + cmp * 2 + 1, a.mir_lds);
+        }
+    }
+
+    if (a.base_on && gpos >= a.base_start) {
+        // mismatches in BAM orientation: base j against position b0 + j
+        // (the reverse strand's comparison mapped back; comp is a bijection)
+        const int64_t b0 = rev ? (int64_t)gpos - rlen : (int64_t)gpos;
+        const int nw = (rlen + 7) >> 3;
+        const bool fast = rw.g && b0 >= rw.wlo && b0 + rlen <= rw.whi;
+        int mism = 0;
+        bool reject = false;
+        for (int k = 0; k < nw && !reject; ++k) {
+            const uint32_t w = s32[k];
+            const int n8 = min(8, rlen - 8 * k);
+            if (fast) {
+                uint32_t lo, hi;
+                rw.at8(b0 + 8 * k, lo, hi);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int rv = (int)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 255u);
+                    mism += (j < n8) & (nt4_of(nib8(w, j)) != rv);
                 }
-                const int64_t b = ((int64_t)g * (a.MN + 1)) * 2;
-                inc(lds + a.lds_mir, a.mir, b + plain * 2, a.mir_lds);
-                inc(lds + a.lds_mir, a.mir, b + cmp * 2 + 1, a.mir_lds);
+            } else {
+                for (int j = 0; j < n8; ++j) mism += nt4_of(nib8(w, j)) != rw.at(b0 + 8 * k + j);
             }
+            reject = mism * 32 > rlen;
         }
-
-        if (a.base_on && gpos >= a.base_start) {
-            // mismatches in BAM orientation: read[x] vs the reference, reverse
-            // strand mapped back (comp is a bijection on 0..4)
-            const int64_t b0 = rev ? (int64_t)gpos - rlen : (int64_t)gpos;
-            int mism = 0;
-            bool reject = false;
+        if (!reject) {
+            const int64_t rowstride = (int64_t)a.G * 5;
+            for (int x = 0; x < a.base_start; ++x) {
+                const int v = rev ? comp4(rw.at((int64_t)gpos - x - 1 + a.base_start))
+                                  : rw.at((int64_t)gpos + x - a.base_start);
+                inc(lds + a.lds_base, a.base, x * rowstride + g * 5 + v, a.base_lds);
+            }
+            if (defer) return true;   // the wave counts the read's bases (count_bases)
             for (int j = 0; j < rlen; ++j) {
-                mism += nt16_nt4(nib(s, j)) != ref.at(b0 + j);
-                if (mism * 32 > rlen) {
-                    reject = true;
-                    break;
+                const uint32_t byte = s[j >> 1];
+                int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
+                int x = j;
+                if (rev) {
+                    v = comp4(v);
+                    x = rlen - 1 - j;
                 }
-            }
-            if (!reject) {
-                const int64_t rowstride = (int64_t)a.G * 5;
-                for (int x = 0; x < a.base_start; ++x) {
-                    const int v = rev ? comp4(ref.at((int64_t)gpos - x - 1 + a.base_start))
-                                      : ref.at((int64_t)gpos + x - a.base_start);
-                    inc(lds + a.lds_base, a.base, x * rowstride + g * 5 + v, a.base_lds);
-                }
-                // lane-rotated walk: the wave's lanes hit different rows
-                int j = rlen > 0 ? lane % rlen : 0;
-                for (int t = 0; t < rlen; ++t) {
-                    int v = nt16_nt4(nib(s, j));
-                    int x = j;
-                    if (rev) {
-                        v = comp4(v);
-                        x = rlen - 1 - j;
-                    }
-                    inc(lds + a.lds_base, a.base, (int64_t)(x + a.base_start) * rowstride + g * 5 + v,
-                        a.base_lds);
-                    if (++j == rlen) j = 0;
-                }
+                inc(lds + a.lds_base, a.base, (int64_t)(x + a.base_start) * rowstride + g * 5 + v,
+                    a.base_lds);
             }
         }
+    }
+    return false;
+}
+
+// BaseHist counts of the batch's passing reads, position-parallel: lane L
+// owns read positions L, L+64, L+128, L+192 and keeps 5 packed 12-bit
+// counters per position in a 64-bit register while the wave walks the
+// reads one by one (broadcast LDS reads of each read's bytes); one LDS add
+// per non-zero counter at the end.  Positions from 256 on, and batches
+// whose passing reads are in several groups, are counted per lane.
+__device__ __forceinline__ void count_bases(const ScanArgs& a, int64_t r, bool pending, bool act,
+                                            int soff, lds_u32* sseq, lds_u32* lds, int lane) {
+    uint64_t pend = __ballot(pending);
+    if (!pend) return;
+    const int32_t rlen = act ? a.rlen[r] : 0;
+    const int32_t fl = act ? a.flag[r] : 0;
+    int g = 0;
+    for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
+    const int first = __builtin_ctzll(pend);
+    const int g0 = __builtin_amdgcn_readlane(g, first);
+    const int rowstride = a.G * 5;
+    if (!a.base_lds || __ballot(pending && g != g0)) {
+        if (pending) {
+            lds_cu8* s = (lds_cu8*)(sseq + soff);
+            const bool rev = (fl & 0x10) != 0;
+            for (int j = 0; j < rlen; ++j) {
+                const uint32_t byte = s[j >> 1];
+                int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
+                int x = j;
+                if (rev) {
+                    v = comp4(v);
+                    x = rlen - 1 - j;
+                }
+                inc(lds + a.lds_base, a.base, (int64_t)(x + a.base_start) * rowstride + g * 5 + v,
+                    a.base_lds);
+            }
+        }
+        return;
+    }
+    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    while (pend) {
+        const int l = __builtin_ctzll(pend);
+        pend &= pend - 1;
+        const int rl = __builtin_amdgcn_readlane(rlen, l);
+        const int rv = __builtin_amdgcn_readlane(fl, l) & 0x10;
+        const int so = __builtin_amdgcn_readlane(soff, l);
+        lds_cu8* s = (lds_cu8*)(sseq + so);
+#define MC_COUNT_POS(q, c)                                                     \
+        {                                                                      \
+            const int x = lane + 64 * (q);                                     \
+            if (x < rl) {                                                      \
+                const int j = rv ? rl - 1 - x : x;                             \
+                const uint32_t byte = s[j >> 1];                               \
+                int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));          \
+                if (rv) v = comp4(v);                                          \
+                c += 1ull << (12 * v);                                         \
+            }                                                                  \
+        }
+        MC_COUNT_POS(0, c0)
+        MC_COUNT_POS(1, c1)
+        MC_COUNT_POS(2, c2)
+        MC_COUNT_POS(3, c3)
+#undef MC_COUNT_POS
+        for (int x = 256 + lane; x < rl; x += 64) {
+            const int j = rv ? rl - 1 - x : x;
+            const uint32_t byte = s[j >> 1];
+            int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
+            if (rv) v = comp4(v);
+            __hip_atomic_fetch_add(lds + a.lds_base + (x + a.base_start) * rowstride + g0 * 5 + v, 1u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    const uint64_t cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (!cs[q]) continue;
+        lds_u32* row = lds + a.lds_base + (lane + 64 * q + a.base_start) * rowstride + g0 * 5;
+#pragma unroll
+        for (int v = 0; v < 5; ++v) {
+            const uint32_t c = (uint32_t)(cs[q] >> (12 * v)) & 0xFFFu;
+            if (c) __hip_atomic_fetch_add(row + v, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// Reference positions a read's BaseHist / MirrorHist may read: [lo, hi).
+__device__ __forceinline__ void ref_span(const ScanArgs& a, int64_t r, int64_t& lo, int64_t& hi) {
+    const int32_t rlen = a.rlen[r], gpos = a.gpos[r];
+    const bool rev = (a.flag[r] & 0x10) != 0;
+    lo = INT64_MAX;
+    hi = INT64_MIN;
+    if (a.base_on && gpos >= a.base_start) {
+        const int64_t b0 = rev ? (int64_t)gpos - rlen : (int64_t)gpos;
+        lo = min(lo, b0);
+        hi = max(hi, b0 + rlen);
+        if (a.base_start) {
+            lo = min(lo, rev ? (int64_t)gpos : (int64_t)gpos - a.base_start);
+            hi = max(hi, rev ? (int64_t)gpos + a.base_start : (int64_t)gpos);
+        }
+    }
+    if (a.mir_on) {
+        const int64_t p = (int64_t)gpos + a.MOFF;
+        if (p >= (int64_t)a.MN - a.MOFF) {
+            lo = min(lo, p - a.MN);
+            hi = max(hi, p + a.MN + 1);
+        }
+    }
+}
+
+__device__ __forceinline__ int64_t wave_min(int64_t v) {
+    for (int d = 32; d > 0; d >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, d, 64));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_max(int64_t v) {
+    for (int d = 32; d > 0; d >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, d, 64));
+    return v;
+}
+
+// One wave walks its slice of reads in batches of up to 64 consecutive
+// reads (one lane each) whose packed bases fit the wave's staging buffer:
+// the batch's bases (contiguous in HBM) and, when the batch shares one
+// reference sequence, the reference window it touches are copied to LDS
+// with coalesced dword loads; every per-read access after that is LDS.
+// A read too long to stage is processed from global memory.
+__global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
+    extern __shared__ uint32_t lds_[];
+    lds_u32* lds = (lds_u32*)lds_;
+    for (int i = threadIdx.x; i < a.lds_words; i += kThreads) lds[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    lds_u32* sseq = lds + a.stage_off + wave * (kStageBytes / 4);
+    lds_u32* sref = sseq + (kSeqStage + kStagePad) / 4;
+    const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
+    int64_t r0 = gw * a.per_wave;
+    const int64_t rend = min(a.n, r0 + a.per_wave);
+    while (r0 < rend) {
+        const int64_t r = r0 + lane;
+        const bool valid = r < rend;
+        const int64_t so = valid ? a.seq_off[r] : 0, se = valid ? a.seq_off[r + 1] : 0;
+        if (valid && (so & 3)) atomicOr(a.error, 1);
+        const int64_t base = __shfl((long long)so, 0, 64);
+        const uint64_t fit = __ballot(valid && se - base <= kSeqStage);
+        const int m = fit == ~0ull ? 64 : __builtin_ctzll(~fit);
+        if (m == 0) {   // the first read alone exceeds the stage: global path
+            if (lane == 0) {
+                const int32_t rid = a.ref_id[r];
+                RefWin rw{nullptr, 0, nullptr, 0, 0};
+                if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
+                process_read(a, r, a.seq + so, reinterpret_cast<const uint32_t*>(a.seq + so), rw,
+                             lds, false, false);
+            }
+            r0 += 1;
+            continue;
+        }
+        const bool act = lane < m;
+        const int64_t end = __shfl((long long)se, m - 1, 64);
+        // stage the batch's bases
+        const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.seq + (base & ~int64_t(3)));
+        const int nwd = (int)((end - (base & ~int64_t(3)) + 3) >> 2);
+        for (int i = lane; i < nwd; i += 64) sseq[i] = g32[i];
+        // the reference window, when the batch shares one sequence
+        const int32_t rid = act ? a.ref_id[r] : -1;
+        const int32_t rid0 = __shfl(rid, 0, 64);
+        const bool one_ref = __ballot(act && rid != rid0) == 0 && rid0 >= 0 && rid0 < a.n_ref;
+        RefWin rw{nullptr, 0, nullptr, 0, 0};
+        if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
+        if (one_ref) {
+            int64_t lo, hi;
+            if (act) {
+                ref_span(a, r, lo, hi);
+            } else {
+                lo = INT64_MAX;
+                hi = INT64_MIN;
+            }
+            const int64_t L = a.ref_len[rid0];
+            int64_t wlo = max<int64_t>(wave_min(lo), 0), whi = min<int64_t>(wave_max(hi), L);
+            if (whi > wlo && whi - wlo <= kRefStage) {
+                const uint8_t* gref = a.ref + a.ref_off[rid0];
+                const uintptr_t ga = reinterpret_cast<uintptr_t>(gref + wlo);
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(ga & ~uintptr_t(3));
+                const int nrw = (int)((whi - wlo + (int64_t)(ga & 3) + 3) >> 2);
+                for (int i = lane; i < nrw; i += 64) sref[i] = q[i];
+                rw.w = (lds_cu8*)sref + (ga & 3);
+                rw.wlo = wlo;
+                rw.whi = whi;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // IsizeHist max, aggregated when the batch is one group
+        bool isize_done = false;
+        if (a.isz_on && a.isz_lds) {
+            int g = 0;
+            const int32_t fl = act ? a.flag[r] : 0;
+            for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
+            const int g0 = __shfl(g, 0, 64);
+            if (__ballot(act && g != g0) == 0) {
+                int32_t v = act ? a.gisize[r] : 0;
+                v = v < 0 ? -v : v;
+                if (act)
+                    __hip_atomic_fetch_add(lds + a.lds_isz + (int64_t)v * a.G + g, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int64_t mx = wave_max(act ? (int64_t)v : 0);
+                if (lane == 0)
+                    __hip_atomic_fetch_max((__attribute__((address_space(3))) int32_t*)(lds + a.lds_isz_max) + g0,
+                                           (int32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                isize_done = true;
+            }
+        }
+        const int soff = (int)((so - (base & ~int64_t(3))) >> 2);   // the read's first dword
+        bool pending = false;
+        if (act) {
+            lds_cu32* rs32 = sseq + soff;
+            pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done);
+        }
+        if (a.base_on) count_bases(a, r, pending, act, soff, sseq, lds, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        r0 += m;
     }
     __syncthreads();
     // flush the workgroup's private bins
     for (int i = threadIdx.x; i < a.lds_words; i += kThreads) {
         const uint32_t v = lds[i];
         if (!v) continue;
-        if (i >= a.lds_isz_max && a.isz_lds && i < a.lds_isz_max + a.G) {
+        if (a.isz_lds && i >= a.lds_isz_max && i < a.lds_isz_max + a.G) {
             atomicMax(a.isz_max + (i - a.lds_isz_max), (int32_t)v);
         } else if (a.base_lds && i >= a.lds_base && i < a.lds_base + a.base_rows * a.G * 5) {
             atomicAdd(a.base + (i - a.lds_base), v);
@@ -243,6 +513,42 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
         } else if (a.isz_lds && i >= a.lds_isz && i < a.lds_isz + a.isz_cap * a.G) {
             atomicAdd(a.isz + (i - a.lds_isz), v);
         }
+    }
+}
+
+// KmerHist counts from the per-read codes scan_kernel wrote (u16,
+// kcodes[slot][read], 0xFFFF = read too short).  The table of 4^K+1 bins
+// for `spp` slots of one group sits in LDS (u32; K = 7: two slots, 128 KiB),
+// so the random-key increments are LDS atomics; blockIdx.y picks the slots,
+// blockIdx.z the group.  Each workgroup adds its table into the device's
+// slot-major [G][NK][4^K+1] table once: consecutive bins, coalesced.
+constexpr int kKmerThreads = 512;
+constexpr int kKmerLdsBytes = 160 * 1024;
+
+__global__ __launch_bounds__(kKmerThreads) void kmer_count_kernel(
+    const uint16_t* __restrict__ kcodes, const uint16_t* __restrict__ kgroup, int64_t n, int NK,
+    int nbins, int spp, int G, uint32_t* __restrict__ kmer) {
+    extern __shared__ uint32_t t_[];
+    lds_u32* t = (lds_u32*)t_;
+    const int s0 = blockIdx.y * spp, ns = min(spp, NK - s0), g = blockIdx.z;
+    const int words = ns * nbins;
+    for (int i = threadIdx.x; i < words; i += kKmerThreads) t[i] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kKmerThreads;
+    for (int64_t r = (int64_t)blockIdx.x * kKmerThreads + threadIdx.x; r < n; r += stride) {
+        if (G > 1 && kgroup[r] != g) continue;
+        for (int q = 0; q < ns; ++q) {
+            const uint32_t c = kcodes[(int64_t)(s0 + q) * n + r];
+            if (c != 0xFFFFu)
+                __hip_atomic_fetch_add(t + q * nbins + c, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = kmer + ((int64_t)g * NK + s0) * nbins;
+    for (int i = threadIdx.x; i < words; i += kKmerThreads) {
+        const uint32_t v = t[i];
+        if (v) atomicAdd(out + i, v);
     }
 }
 
@@ -315,6 +621,9 @@ struct mc_scan {
     Dev<int32_t> isz_max;
     Dev<uint8_t> ref;
     Dev<int64_t> ref_off, ref_len;
+    Dev<int32_t> error;
+    Dev<uint16_t> kcodes, kgroup;
+    int cus = 1;
     int32_t n_ref = 0;
     Slot slot[2];
     int next_slot = 0;
@@ -381,7 +690,7 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
     a.seq_off = seq_off;
     a.seq = seq;
     a.n = n;
-    a.ref = s->ref.p;
+    a.ref = s->ref.p ? s->ref.p + kRefPad : nullptr;
     a.ref_off = s->ref_off.p;
     a.ref_len = s->ref_len.p;
     a.n_ref = s->n_ref;
@@ -426,12 +735,38 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
     a.STEP = c.kmer_step;
     a.OFF = c.kmer_offset;
     a.kmer = s->kmer.p;
+    const int nbins = (1 << (2 * c.kmer_k)) + 1;
+    const int spp = c.kmer_on ? std::min(c.kmer_nk, kKmerLdsBytes / (nbins * 4)) : 0;
+    if (c.kmer_on && spp >= 1) {       // K <= 7: codes + LDS counting kernel
+        HIP_TRY(s->kcodes.reserve((size_t)(n * c.kmer_nk)));
+        a.kcodes = s->kcodes.p;
+        if (s->G > 1) {
+            HIP_TRY(s->kgroup.reserve((size_t)n));
+            a.kgroup = s->kgroup.p;
+        }
+    }
     a.lds_words = words;
     if (!a.isz_lds) a.lds_isz_max = kLdsWords;   // outside the arena: never matched by the flush
-    const int64_t want = (n + kThreads - 1) / kThreads;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, s->grid));
-    hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kThreads), (size_t)words * 4, s->stream, a);
+    a.stage_off = (words + 3) & ~3;
+    a.error = s->error.p;
+    // one slice of whole 64-read batches per wave
+    const int64_t batches = (n + 63) / 64;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((batches + kWaves - 1) / kWaves,
+                                                                  s->grid));
+    const int64_t waves = (int64_t)grid * kWaves;
+    a.per_wave = (batches + waves - 1) / waves * 64;
+    const size_t lds_bytes = (size_t)a.stage_off * 4 + (size_t)kWaves * kStageBytes;
+    hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kThreads), lds_bytes, s->stream, a);
     HIP_TRY(hipGetLastError());
+    if (a.kcodes) {
+        const int passes = (c.kmer_nk + spp - 1) / spp;
+        const int64_t wantb = (n + kKmerThreads - 1) / kKmerThreads;
+        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(wantb, s->cus));
+        hipLaunchKernelGGL(kmer_count_kernel, dim3(gx, passes, s->G), dim3(kKmerThreads),
+                           (size_t)spp * nbins * 4, s->stream, a.kcodes, a.kgroup, n, c.kmer_nk,
+                           nbins, spp, s->G, s->kmer.p);
+        HIP_TRY(hipGetLastError());
+    }
     ++s->launches;
     return MC_OK;
 }
@@ -467,7 +802,12 @@ extern "C" int mc_scan_create(int device, const mc_scan_config* cfg, mc_scan** o
     for (auto& sl : s->slot) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    s->grid = std::max(1, cus) * 4;
+    s->cus = std::max(1, cus);
+    s->grid = s->cus * 3;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(kmer_count_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kKmerLdsBytes));
+    HIP_TRY(s->error.reserve(1));
+    HIP_TRY(hipMemsetAsync(s->error.p, 0, 4, s->stream));
     if (cfg->base_on) {
         s->base_rows = (int64_t)s->max_rlen + cfg->base_start;   // set_max_readlen(50)
         HIP_TRY(s->base.reserve((size_t)(s->base_rows * s->G * 5)));
@@ -514,13 +854,14 @@ extern "C" int mc_scan_set_reference(mc_scan* s, int32_t n_seq, const int64_t* o
                    (long long)len[i], (long long)n_bytes);
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    HIP_TRY(s->ref.reserve((size_t)std::max<int64_t>(n_bytes, 1)));
+    HIP_TRY(s->ref.reserve((size_t)n_bytes + 2 * kRefPad));
     HIP_TRY(s->ref_off.reserve((size_t)std::max(n_seq, 1)));
     HIP_TRY(s->ref_len.reserve((size_t)std::max(n_seq, 1)));
+    HIP_TRY(hipMemset(s->ref.p, 4, (size_t)n_bytes + 2 * kRefPad));
     if (n_bytes) {
-        HIP_TRY(hipMemcpy(s->ref.p, ascii, (size_t)n_bytes, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(s->ref.p + kRefPad, ascii, (size_t)n_bytes, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(ascii_nt4_kernel, dim3((unsigned)((n_bytes + 255) / 256)), dim3(256), 0,
-                           s->stream, s->ref.p, n_bytes);
+                           s->stream, s->ref.p + kRefPad, n_bytes);
         HIP_TRY(hipGetLastError());
     }
     if (n_seq) {
@@ -555,8 +896,15 @@ extern "C" int mc_scan_add_batch(mc_scan* s, int64_t n, const int32_t* rlen, con
     MC_REQUIRE(mi < (int64_t(1) << 28), MC_E_RANGE,
                "insert size %lld too large for a dense histogram", (long long)mi);
     if (int rc = ensure_shape(s, mr, s->cfg.isize_on ? mi : 0)) return rc;
-    const int64_t nbytes = seq_off[n];
-    // staging layout: 5 int32 columns, seq_off (n+1 int64, rebased), seq
+    // the kernel stages bases in dwords: every read's bases start on a
+    // 4-byte boundary (the sources emit that; anything else is repacked)
+    bool aligned = true;
+    int64_t packed = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        aligned &= (seq_off[i] - seq_off[0]) % 4 == 0;
+        packed += (seq_off[i + 1] - seq_off[i] + 3) & ~int64_t(3);
+    }
+    const int64_t nbytes = aligned ? seq_off[n] - seq_off[0] : packed;
     const size_t cols = (size_t)n * 4, offb = (size_t)(n + 1) * 8;
     const size_t total = 5 * cols + offb + (size_t)nbytes + 16;
     Slot& sl = s->slot[s->next_slot];
@@ -567,21 +915,37 @@ extern "C" int mc_scan_add_batch(mc_scan* s, int64_t n, const int32_t* rlen, con
     }
     HIP_TRY(sl.host.reserve(total));
     HIP_TRY(sl.dev.reserve(total));
+    // staging layout: seq_off (n+1 int64, rebased), 5 int32 columns, bases
     uint8_t* h = static_cast<uint8_t*>(sl.host.p);
-    std::memcpy(h, rlen, cols);
-    std::memcpy(h + cols, flag, cols);
-    std::memcpy(h + 2 * cols, gpos, cols);
-    std::memcpy(h + 3 * cols, gisize, cols);
-    std::memcpy(h + 4 * cols, ref_id, cols);
-    std::memcpy(h + 5 * cols, seq_off, offb);
-    std::memcpy(h + 5 * cols + offb, seq, (size_t)nbytes);
+    int64_t* ho = reinterpret_cast<int64_t*>(h);
+    uint8_t* hc = h + offb;
+    std::memcpy(hc, rlen, cols);
+    std::memcpy(hc + cols, flag, cols);
+    std::memcpy(hc + 2 * cols, gpos, cols);
+    std::memcpy(hc + 3 * cols, gisize, cols);
+    std::memcpy(hc + 4 * cols, ref_id, cols);
+    uint8_t* hs = hc + 5 * cols;
+    if (aligned) {
+        for (int64_t i = 0; i <= n; ++i) ho[i] = seq_off[i] - seq_off[0];
+        std::memcpy(hs, seq + seq_off[0], (size_t)nbytes);
+    } else {
+        int64_t o = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            ho[i] = o;
+            const int64_t k = seq_off[i + 1] - seq_off[i];
+            std::memcpy(hs + o, seq + seq_off[i], (size_t)k);
+            std::memset(hs + o + k, 0, (size_t)(((k + 3) & ~int64_t(3)) - k));
+            o += (k + 3) & ~int64_t(3);
+        }
+        ho[n] = o;
+    }
+    std::memset(hs + nbytes, 0, 16);
     HIP_TRY(hipMemcpyAsync(sl.dev.p, h, total, hipMemcpyHostToDevice, s->stream));
-    uint8_t* d = sl.dev.p;
+    const uint8_t* d = sl.dev.p + offb;
     HIP_TRY(hipEventRecord(s->t0, s->stream));
     if (int rc = launch(s, n, (const int32_t*)d, (const int32_t*)(d + cols),
                         (const int32_t*)(d + 2 * cols), (const int32_t*)(d + 3 * cols),
-                        (const int32_t*)(d + 4 * cols), (const int64_t*)(d + 5 * cols),
-                        d + 5 * cols + offb))
+                        (const int32_t*)(d + 4 * cols), (const int64_t*)sl.dev.p, d + 5 * cols))
         return rc;
     HIP_TRY(hipEventRecord(s->t1, s->stream));
     HIP_TRY(hipEventRecord(sl.done, s->stream));
@@ -673,6 +1037,10 @@ extern "C" int mc_scan_results(mc_scan* s, uint32_t* base, uint32_t* kmer, uint3
     MC_REQUIRE(s, MC_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    int32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, s->error.p, 4, hipMemcpyDeviceToHost));
+    MC_REQUIRE(err == 0, MC_E_INVALID,
+               "a device batch had read bases that do not start on a 4-byte boundary");
     const int G = s->G;
     if (base && s->cfg.base_on) {
         std::vector<uint32_t> t((size_t)(s->base_rows * G * 5));
@@ -681,8 +1049,15 @@ extern "C" int mc_scan_results(mc_scan* s, uint32_t* base, uint32_t* kmer, uint3
             for (int g = 0; g < G; ++g)
                 std::memcpy(base + ((int64_t)g * s->base_rows + r) * 5, &t[(r * G + g) * 5], 20);
     }
-    if (kmer && s->cfg.kmer_on)
-        HIP_TRY(hipMemcpy(kmer, s->kmer.p, (size_t)s->kmer_bins * 4, hipMemcpyDeviceToHost));
+    if (kmer && s->cfg.kmer_on) {   // device [G][NK][bins] -> [G][bins][NK]
+        const int64_t nb = (int64_t(1) << (2 * s->cfg.kmer_k)) + 1, NK = s->cfg.kmer_nk;
+        std::vector<uint32_t> t((size_t)s->kmer_bins);
+        HIP_TRY(hipMemcpy(t.data(), s->kmer.p, t.size() * 4, hipMemcpyDeviceToHost));
+        for (int64_t g = 0; g < G; ++g)
+            for (int64_t i = 0; i < NK; ++i)
+                for (int64_t k = 0; k < nb; ++k)
+                    kmer[(g * nb + k) * NK + i] = t[(size_t)((g * NK + i) * nb + k)];
+    }
     if (mirror && s->cfg.mirror_on)
         HIP_TRY(hipMemcpy(mirror, s->mir.p, (size_t)G * (s->cfg.mirror_n + 1) * 2 * 4,
                           hipMemcpyDeviceToHost));

@@ -15,7 +15,8 @@
 //                      (:267-271, is_paired :291-292); FASTQ -1 (:322-323)
 //   tid     get_tid    BAM refID (:282-283); FASTQ -1
 //   seq     get_seq    the BAM nt16 nibbles as stored (2 per byte, high
-//                      nibble first); FASTQ bytes mapped to the same code
+//                      nibble first; each read's bytes start on a 4-byte
+//                      boundary, zero padded); FASTQ bytes mapped to the same code
 //                      (A/C/G/T either case -> 1/2/4/8, anything else -> 15,
 //                      which the kernel's nt16 -> nt4 makes 4 exactly like
 //                      iupac_to_nt4, pyfq.pyx:26-49).  The kernel undoes the
@@ -211,6 +212,7 @@ int bam_next(mc_scan_src* s, int64_t max_reads, int64_t max_bytes) {
         s->gisize.push_back((flag & 0x2) ? tlen : 0);
         s->tid.push_back(tid);
         s->seq.insert(s->seq.end(), r + seq_at, r + seq_at + nbytes);
+        s->seq.resize((s->seq.size() + 3) & ~size_t(3), 0);   // 4-byte aligned starts
         s->seq_off.push_back((int64_t)s->seq.size());
         s->o += 4 + (size_t)bs;
         ++s->n_records;
@@ -230,7 +232,7 @@ int fq_record(mc_scan_src* s, int f, int32_t flag, bool* got) {
     const size_t L = q.size();
     MC_REQUIRE(L <= (size_t)INT32_MAX, MC_E_RANGE, "FASTQ sequence line too long");
     const size_t at = s->seq.size();
-    s->seq.resize(at + (L + 1) / 2);
+    s->seq.resize(at + (((L + 1) / 2 + 3) & ~size_t(3)), 0);   // 4-byte aligned starts
     uint8_t* o = s->seq.data() + at;
     const uint8_t* c = reinterpret_cast<const uint8_t*>(q.data());
     for (size_t i = 0; i + 1 < L; i += 2) o[i >> 1] = (uint8_t)(kAscii16.t[c[i]] << 4 | kAscii16.t[c[i + 1]]);

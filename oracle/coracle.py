@@ -24,10 +24,12 @@ def build():
 def load():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "oracle.c")):
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+                os.path.getmtime(os.path.join(HERE, f)) for f in ("oracle.c", "scan_oracle.c")):
             build()
         _lib = ctypes.CDLL(LIB)
         _lib.orc_pileup_classic.restype = ctypes.c_int64
+        _lib.orc_scan.restype = ctypes.c_int64
     return _lib
 
 
@@ -116,3 +118,27 @@ def pileup_classic_parallel(tid, pos, span, rtid, rstart, rend, threads):
     with ThreadPoolExecutor(threads) as ex:
         cols = sum(ex.map(run, [g for g in groups if len(g)]))
     return out, cols
+
+
+def scan(cfg, batch, ref=None, ref_off=None, ref_len=None, base_rows=0, isize_cap=128):
+    """orc_scan over one SoA batch (rlen, flag, gpos, gisize, ref_id, seq_off,
+    seq); cfg is a metacov_amd._lib.ScanConfig (same layout).  Returns the
+    group-major tables (base, kmer, mirror, isize, isize_max) and the read
+    count."""
+    lib = load()
+    G = 1 << cfg.n_flags
+    rlen, flag, gpos, gisize, ref_id, seq_off, seq = batch
+    base = np.zeros((G, base_rows, 5), np.uint32)
+    kmer = np.zeros((G, (4 ** cfg.kmer_k + 1) if cfg.kmer_on else 0, cfg.kmer_nk), np.uint32)
+    mirror = np.zeros((G, cfg.mirror_n + 1, 2), np.uint32)
+    isize = np.zeros((G, isize_cap), np.uint32)
+    isize_max = np.zeros(G, np.int32)
+    ref = np.zeros(1, np.uint8) if ref is None else ref
+    ref_off = np.zeros(1, np.int64) if ref_off is None else ref_off
+    n_ref = 0 if ref_len is None else len(ref_len)
+    ref_len = np.zeros(1, np.int64) if ref_len is None else ref_len
+    done = lib.orc_scan(ctypes.byref(cfg), ctypes.c_int64(len(rlen)), *[_p(a) for a in (
+        rlen, flag, gpos, gisize, ref_id, seq_off, seq, ref, ref_off, ref_len)],
+        ctypes.c_int32(n_ref), ctypes.c_int64(base_rows), _p(base), _p(kmer), _p(mirror),
+        ctypes.c_int64(isize_cap), _p(isize), _p(isize_max))
+    return (base, kmer, mirror, isize, isize_max), done

@@ -390,16 +390,24 @@ def test_scan_large_isize_and_long_reads_gpu(tmp_path, lib_built):
 
 @pytest.mark.gpu
 def test_scan_kernel_device_batch_gpu(lib_built):
-    """mc_scan_add_batch_device (the bench path) equals mc_scan_add_batch."""
+    """mc_scan_add_batch_device (the bench path, 4-byte aligned read starts)
+    equals mc_scan_add_batch on a tightly packed batch (repacked on the
+    host)."""
     import torch
     from metacov_amd import _lib
     lib = _lib.load()
     rng = np.random.default_rng(5)
     n = 5000
     rlen = rng.integers(0, 200, n).astype(np.int32)
-    off = np.zeros(n + 1, np.int64)
-    off[1:] = np.cumsum((rlen + 1) // 2)
+    nbytes = (rlen + 1) // 2
+    off = np.zeros(n + 1, np.int64)            # tight: the host path repacks it
+    off[1:] = np.cumsum(nbytes)
     seq = rng.integers(0, 256, int(off[-1])).astype(np.uint8)
+    aoff = np.zeros(n + 1, np.int64)           # 4-byte aligned starts (device path contract)
+    aoff[1:] = np.cumsum((nbytes + 3) // 4 * 4)
+    aseq = np.zeros(int(aoff[-1]), np.uint8)
+    for i in range(n):
+        aseq[aoff[i]:aoff[i] + nbytes[i]] = seq[off[i]:off[i + 1]]
     flag = rng.integers(0, 0x800, n).astype(np.int32)
     gpos = rng.integers(-5, 3000, n).astype(np.int32)
     gis = rng.integers(-900, 900, n).astype(np.int32)
@@ -420,7 +428,8 @@ def test_scan_kernel_device_batch_gpu(lib_built):
         _lib.check(lib.mc_scan_create(0, ctypes.byref(cfg), ctypes.byref(h)), lib)
         _lib.check(lib.mc_scan_set_reference(h, 2, _lib.ptr(roff), _lib.ptr(rlen_ref), refs.size,
                                              _lib.ptr(refs)), lib)
-        arrs = [rlen, flag, gpos, gis, rid, off, seq]
+        arrs = [rlen, flag, gpos, gis, rid, off, seq] if mode == "host" else \
+            [rlen, flag, gpos, gis, rid, aoff, aseq]
         if mode == "host":
             _lib.check(lib.mc_scan_add_batch(h, n, *[_lib.ptr(a) for a in arrs]), lib)
         else:
@@ -443,3 +452,105 @@ def test_scan_kernel_device_batch_gpu(lib_built):
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
     assert outs[0][0].sum() > 0 and outs[0][1].sum() > 0 and outs[0][3].sum() == n
+
+
+def _mix_batch(lib, bam, fasta_path):
+    """The whole BAM as one SoA batch through the C++ source, with ref_id
+    forward-filled as mc_scan_run does; plus the FASTA as nt4."""
+    from metacov_amd import _lib
+    from metacov_amd.experimental import FastaFile
+    fa = FastaFile(fasta_path)
+    h = ctypes.c_void_p()
+    _lib.check(lib.mc_scan_src_open_bam(bam.encode(), 1, ctypes.byref(h)), lib)
+    names = []
+    nt = ctypes.c_int32()
+    lib.mc_scan_src_n_targets(h, ctypes.byref(nt))
+    for t in range(nt.value):
+        nm = ctypes.c_char_p()
+        lib.mc_scan_src_target(h, t, ctypes.byref(nm), None)
+        names.append(nm.value.decode())
+    parts = list(_src_batches(lib, h, cap=10 ** 7))
+    lib.mc_scan_src_close(h)
+    (rlen, flag, gpos, gisize, tid), off, seq = parts[0]
+    tmap = np.array([fa._index.get(n, -1) for n in names], np.int32)
+    rid, last = np.empty_like(tid), -1
+    for i, t in enumerate(tid):
+        if t >= 0 and tmap[t] >= 0:
+            last = tmap[t]
+        rid[i] = last
+    t4 = np.full(256, 4, np.uint8)
+    for ch, v in zip(b"ACGTacgt", (0, 1, 2, 3, 0, 1, 2, 3)):
+        t4[ch] = v
+    ref = t4[np.asarray(fa.buffer)]
+    return [rlen, flag, gpos, gisize, rid, off, seq], ref, np.asarray(fa._off, np.int64), \
+        np.asarray(fa.lengths, np.int64)
+
+
+def test_c_port_matches_python_oracle(mix, lib_built):
+    """The two restatements (oracle/scan.py per read, oracle/scan_oracle.c
+    over the C++ source's batch) agree: the C port is the bench's CPU
+    baseline and the GPU check at scale."""
+    from metacov_amd import _lib
+    from oracle import coracle
+    lib = _lib.load()
+    bam, fa = mix
+    batch, ref, roff, rlen_ref = _mix_batch(lib, bam, fa)
+    cfg = _lib.ScanConfig()
+    cfg.n_flags = 2
+    cfg.flags[0], cfg.flags[1] = 0x40, 0x10
+    cfg.base_on, cfg.base_start = 1, 3
+    cfg.kmer_on, cfg.kmer_k, cfg.kmer_nk, cfg.kmer_step, cfg.kmer_offset = 1, 4, 6, 3, -2
+    cfg.mirror_on, cfg.mirror_offset, cfg.mirror_n = 1, 4, 10
+    cfg.isize_on = 1
+    rows = max(50, int(batch[0].max())) + 3
+    (base, kmer, mirror, isize, isize_max), done = coracle.scan(cfg, batch, ref, roff, rlen_ref,
+                                                               rows, 1024)
+    o = oscan.ByFlag([oscan.BaseHist(3), oscan.KmerHist(4, 6, 3, -2), oscan.MirrorHist(4, 10),
+                      oscan.IsizeHist()], [oscan.Flags["IsRead1"], oscan.Flags["Readdir"]])
+    assert oscan.scan_reads(oscan.bam_reads(bam, oscan.read_fasta(fa)), o) == done
+    for g in range(4):
+        b, k, m, i = o.processors[g].processors
+        assert np.array_equal(base[g], np.array(b.counts, np.uint32))
+        assert np.array_equal(kmer[g], np.array(k.counts, np.uint32))
+        assert np.array_equal(mirror[g], np.array(m.counts, np.uint32))
+        assert isize_max[g] == i.max_isize
+        assert all(isize[g][a] == c for a, c in i.counts.items())
+        assert isize[g].sum() == sum(i.counts.values())
+
+
+@pytest.mark.gpu
+def test_scan_kernel_vs_c_port_gpu(mix, lib_built):
+    """mc_scan_add_batch on the mix BAM's batch equals the C port."""
+    from metacov_amd import _lib
+    from oracle import coracle
+    lib = _lib.load()
+    bam, fa = mix
+    batch, ref, roff, rlen_ref = _mix_batch(lib, bam, fa)
+    for nflags, flags in ((0, ()), (3, (0x2, 0x10, 0x80))):
+        cfg = _lib.ScanConfig()
+        cfg.n_flags = nflags
+        for i, f in enumerate(flags):
+            cfg.flags[i] = f
+        cfg.base_on, cfg.base_start = 1, 11
+        cfg.kmer_on, cfg.kmer_k, cfg.kmer_nk, cfg.kmer_step, cfg.kmer_offset = 1, 7, 8, 7, 0
+        cfg.mirror_on, cfg.mirror_offset, cfg.mirror_n = 1, -3, 25
+        cfg.isize_on = 1
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_create(0, ctypes.byref(cfg), ctypes.byref(h)), lib)
+        from metacov_amd.experimental import FastaFile
+        f = FastaFile(fa)
+        buf = np.ascontiguousarray(f.buffer)
+        _lib.check(lib.mc_scan_set_reference(h, len(rlen_ref), _lib.ptr(roff), _lib.ptr(rlen_ref),
+                                             buf.size, _lib.ptr(buf)), lib)
+        _lib.check(lib.mc_scan_add_batch(h, len(batch[0]), *[_lib.ptr(a) for a in batch]), lib)
+        G, rows, cap = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        lib.mc_scan_dims(h, ctypes.byref(G), ctypes.byref(rows), ctypes.byref(cap), None, None)
+        got = (np.zeros((G.value, rows.value, 5), np.uint32),
+               np.zeros((G.value, 4 ** 7 + 1, 8), np.uint32),
+               np.zeros((G.value, 26, 2), np.uint32), np.zeros((G.value, cap.value), np.uint32),
+               np.zeros(G.value, np.int32))
+        _lib.check(lib.mc_scan_results(h, *[_lib.ptr(x) for x in got]), lib)
+        lib.mc_scan_destroy(h)
+        want, _ = coracle.scan(cfg, batch, ref, roff, rlen_ref, rows.value, cap.value)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)
