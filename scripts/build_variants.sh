@@ -8,7 +8,7 @@ cd "$R/metacov_amd/csrc"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags \
-      -o "$R/metacov_amd/variants/lib_$name.so" engine.hip ecor.hip bam_decode.cpp bam_index.cpp bam_write.cpp exp_reads.cpp common.cpp -lz -lpthread -ldl &
+      -o "$R/metacov_amd/variants/lib_$name.so" engine.hip ecor.hip scan.hip bam_decode.cpp bam_index.cpp bam_write.cpp exp_reads.cpp scan_src.cpp common.cpp -lz -lpthread -ldl &
 done
 wait
 ls -la "$R/metacov_amd/variants"
