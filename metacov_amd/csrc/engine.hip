@@ -142,6 +142,16 @@ struct mc_ctx {
     // fused K2 statistics
     DevBuf<int64_t> d_fchunk;
     Stage fstage;                         // per-call region arrays + returned flags
+    // the last fused call's regions: a repeated call with the same regions on
+    // the same prepared reads reuses the staged (sorted) arrays on the device
+    uint64_t prep_gen = 0;
+    struct {
+        bool valid = false;
+        uint64_t gen = 0;
+        std::vector<int32_t> tid;
+        std::vector<int64_t> start, end;
+        int64_t nf = 0;
+    } fcache;
     DevBuf<unsigned> d_flow;
     DevBuf<unsigned> d_fhist;
     DevBuf<int> d_fflag;
@@ -223,6 +233,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_out.release();
     ctx->d_fchunk.release();
     ctx->fstage.release();
+    ctx->fcache.valid = false;
     ctx->d_flow.release();
     ctx->d_fhist.release();
     ctx->d_fflag.release();
@@ -565,6 +576,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     ctx->t.cigar_ms = ctx->t_cigar ? elapsed(ctx, 0, 1) : 0.f;
     ctx->prepared = true;
     ctx->depth_valid = false;
+    ++ctx->prep_gen;
     return MC_OK;
 }
 
@@ -786,69 +798,43 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
 // while they are in registers), then the histogram finalize.  Needs regions
 // that do not overlap each other; otherwise K2 then K3.  Regions whose order
 // statistics reach depths >= kHistBins are recomputed by K3.
-static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
-                            const int64_t* end, RegionOut* d_out) {
-    if (int rc = mc_prepare(ctx)) return rc;
-    MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
-    const int32_t nc = (int32_t)ctx->len.size();
-    struct Reg { int64_t gs, ge; int32_t id, base; };
-    // histogram window of each region: kHistBins values centred on its
-    // contig's mean depth (aligned bases / extent)
-    std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
-    std::vector<Reg> regs;
-    regs.reserve(R);
-    std::vector<int64_t> ntot(std::max<int64_t>(R, 1)), nzx(std::max<int64_t>(R, 1));
-    for (int64_t r = 0; r < R; ++r) {
-        MC_REQUIRE(tid[r] >= 0 && tid[r] < nc, MC_E_INVALID, "region %lld: tid %d out of range",
-                   (long long)r, tid[r]);
-        MC_REQUIRE(start[r] >= 0 && end[r] >= start[r], MC_E_INVALID,
-                   "region %lld: bad range [%lld, %lld)", (long long)r, (long long)start[r],
-                   (long long)end[r]);
-        const int64_t ext = ctx->extent[tid[r]];
-        const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
-        ntot[r] = end[r] - start[r];
-        nzx[r] = ntot[r] - (b - a);
-        const double mean = ext > 0 ? (double)ctx->cbases[tid[r]] / (double)ext : 0.0;
-        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(mean) - kHistBins / 2);
-        if (b > a)
-            regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
-    }
-    std::sort(regs.begin(), regs.end(), [](const Reg& x, const Reg& y) { return x.gs < y.gs; });
-    bool overlap = false;
-    for (size_t k = 1; k < regs.size(); ++k) overlap |= regs[k].gs < regs[k - 1].ge;
-    const bool fusable = R > 0 && !overlap && R * (int64_t)kHistBins <= (int64_t(1) << 28);
-    if (!fusable) {
-        FusedRegions none{};
-        if (int rc = launch_depth(ctx, none)) return rc;
-        return region_stats_impl(ctx, R, tid, start, end, d_out);
-    }
-    hipStream_t s = ctx->stream;
-    const int64_t nf = (int64_t)regs.size();
-    // every per-call array in one pinned buffer -> one H2D copy; the region
-    // flags come back through the same buffer
+// Staging layout of a fused call: sorted region arrays (nf), per-region
+// arrays (R), then the returned flags.
+struct FusedLayout {
+    size_t gs, ge, id, base, ntot, nzx, brow, up, flag, total;
+};
+static FusedLayout fused_layout(int64_t nf, int64_t R) {
     auto al = stage_align;
-    const size_t o_gs = 0, o_ge = o_gs + al(nf * 8), o_id = o_ge + al(nf * 8),
-                 o_base = o_id + al(nf * 4), o_ntot = o_base + al(nf * 4),
-                 o_nzx = o_ntot + al(R * 8), o_brow = o_nzx + al(R * 8), up = o_brow + al(R * 4),
-                 o_flag = up, total = up + al(R * 4);
-    HIP_TRY(ctx->fstage.reserve(total));
-    unsigned char* h = ctx->fstage.host();
-    for (int64_t k = 0; k < nf; ++k) {
-        reinterpret_cast<int64_t*>(h + o_gs)[k] = regs[k].gs;
-        reinterpret_cast<int64_t*>(h + o_ge)[k] = regs[k].ge;
-        reinterpret_cast<int32_t*>(h + o_id)[k] = regs[k].id;
-        reinterpret_cast<int32_t*>(h + o_base)[k] = regs[k].base;
-    }
-    std::memcpy(h + o_ntot, ntot.data(), R * 8);
-    std::memcpy(h + o_nzx, nzx.data(), R * 8);
-    std::memcpy(h + o_brow, base_row.data(), R * 4);
+    FusedLayout L;
+    L.gs = 0;
+    L.ge = L.gs + al(nf * 8);
+    L.id = L.ge + al(nf * 8);
+    L.base = L.id + al(nf * 4);
+    L.ntot = L.base + al(nf * 4);
+    L.nzx = L.ntot + al(R * 8);
+    L.brow = L.nzx + al(R * 8);
+    L.up = L.brow + al(R * 4);
+    L.flag = L.up;
+    L.total = L.up + al(R * 4);
+    return L;
+}
+
+// The launches of a fused call whose region arrays are staged in
+// ctx->fstage (just now, or by an identical earlier call).
+static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                              const int64_t* end, RegionOut* d_out, int64_t nf) {
+    hipStream_t s = ctx->stream;
+    const FusedLayout L = fused_layout(nf, R);
+    const size_t o_gs = L.gs, o_ge = L.ge, o_id = L.id, o_base = L.base, o_ntot = L.ntot,
+                 o_nzx = L.nzx, o_brow = L.brow, o_flag = L.flag;
+    (void)o_brow;
     HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
     HIP_TRY(ctx->d_fflag.reserve(R));
     HIP_TRY(ctx->d_acc.reserve(R));
     unsigned char* d = ctx->fstage.d.p;
-    HIP_TRY(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, s));
+    unsigned char* h = ctx->fstage.host();
     const int64_t* d_fge = reinterpret_cast<const int64_t*>(d + o_ge);
     {
         const int64_t work = std::max<int64_t>({R * kHistBins / 4, R, ctx->n_chunks});
@@ -900,6 +886,73 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     }
     return MC_OK;
 }
+
+static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                            const int64_t* end, RegionOut* d_out) {
+    if (int rc = mc_prepare(ctx)) return rc;
+    MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
+    auto& fc = ctx->fcache;
+    const bool hit = R > 0 && fc.valid && fc.gen == ctx->prep_gen && (int64_t)fc.tid.size() == R &&
+                     std::memcmp(fc.tid.data(), tid, R * 4) == 0 &&
+                     std::memcmp(fc.start.data(), start, R * 8) == 0 &&
+                     std::memcmp(fc.end.data(), end, R * 8) == 0;
+    if (hit) return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
+    fc.valid = false;
+    const int32_t nc = (int32_t)ctx->len.size();
+    struct Reg { int64_t gs, ge; int32_t id, base; };
+    // histogram window of each region: kHistBins values centred on its
+    // contig's mean depth (aligned bases / extent)
+    std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
+    std::vector<Reg> regs;
+    regs.reserve(R);
+    std::vector<int64_t> ntot(std::max<int64_t>(R, 1)), nzx(std::max<int64_t>(R, 1));
+    for (int64_t r = 0; r < R; ++r) {
+        MC_REQUIRE(tid[r] >= 0 && tid[r] < nc, MC_E_INVALID, "region %lld: tid %d out of range",
+                   (long long)r, tid[r]);
+        MC_REQUIRE(start[r] >= 0 && end[r] >= start[r], MC_E_INVALID,
+                   "region %lld: bad range [%lld, %lld)", (long long)r, (long long)start[r],
+                   (long long)end[r]);
+        const int64_t ext = ctx->extent[tid[r]];
+        const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
+        ntot[r] = end[r] - start[r];
+        nzx[r] = ntot[r] - (b - a);
+        const double mean = ext > 0 ? (double)ctx->cbases[tid[r]] / (double)ext : 0.0;
+        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(mean) - kHistBins / 2);
+        if (b > a)
+            regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
+    }
+    std::sort(regs.begin(), regs.end(), [](const Reg& x, const Reg& y) { return x.gs < y.gs; });
+    bool overlap = false;
+    for (size_t k = 1; k < regs.size(); ++k) overlap |= regs[k].gs < regs[k - 1].ge;
+    const bool fusable = R > 0 && !overlap && R * (int64_t)kHistBins <= (int64_t(1) << 28);
+    if (!fusable) {
+        FusedRegions none{};
+        if (int rc = launch_depth(ctx, none)) return rc;
+        return region_stats_impl(ctx, R, tid, start, end, d_out);
+    }
+    const int64_t nf = (int64_t)regs.size();
+    const FusedLayout L = fused_layout(nf, R);
+    HIP_TRY(ctx->fstage.reserve(L.total));
+    unsigned char* h = ctx->fstage.host();
+    for (int64_t k = 0; k < nf; ++k) {
+        reinterpret_cast<int64_t*>(h + L.gs)[k] = regs[k].gs;
+        reinterpret_cast<int64_t*>(h + L.ge)[k] = regs[k].ge;
+        reinterpret_cast<int32_t*>(h + L.id)[k] = regs[k].id;
+        reinterpret_cast<int32_t*>(h + L.base)[k] = regs[k].base;
+    }
+    std::memcpy(h + L.ntot, ntot.data(), R * 8);
+    std::memcpy(h + L.nzx, nzx.data(), R * 8);
+    std::memcpy(h + L.brow, base_row.data(), R * 4);
+    HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p, h, L.up, hipMemcpyHostToDevice, ctx->stream));
+    fc.tid.assign(tid, tid + R);
+    fc.start.assign(start, start + R);
+    fc.end.assign(end, end + R);
+    fc.nf = nf;
+    fc.gen = ctx->prep_gen;
+    fc.valid = true;
+    return depth_stats_launch(ctx, R, tid, start, end, d_out, nf);
+}
+
 
 extern "C" int mc_compute_depth_stats(mc_ctx* ctx, int64_t R, const int32_t* tid,
                                       const int64_t* start, const int64_t* end,

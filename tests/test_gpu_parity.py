@@ -551,3 +551,30 @@ def test_streamed_ingest_and_cli(lib_built, golden_dir, tmp_path):
         assert res.exit_code == 0, res.output
         outs.append(open(o, newline="").read())
     assert outs[0] == outs[1] and outs[0].count("\n") == 8
+
+
+def test_fused_repeated_calls_reuse_and_invalidate(eng):
+    """A repeated fused call with the same regions reuses the staged region
+    arrays; other regions, or new reads (a new prepare), restage them."""
+    lengths, tid, pos, span = make_case([60_000, 90_000, 30_000], 30_000, (1, 300), 17)
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    whole = (np.arange(3, dtype=np.int32), np.zeros(3, np.int64), np.asarray(lengths, np.int64))
+    tiles = _tiling(np.random.default_rng(5), lengths, 9)
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+
+    def check(regs, d, ext, coff):
+        got = eng.compute_depth_stats(*regs)
+        want = coracle.region_stats(d, ext, coff, *regs)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+
+    for regs in (whole, whole, tiles, tiles, whole):
+        check(regs, d, ext, coff)
+    # new reads: the staged window bases (per-contig mean depth) change
+    lengths2, tid2, pos2, span2 = make_case([60_000, 90_000, 30_000], 90_000, (1, 300), 18)
+    d2, ext2, coff2 = coracle.depth(lengths2, tid2, pos2, span2)
+    eng.set_contigs(lengths2)
+    eng.add_reads(tid2, pos2, span2)
+    check(whole, d2, ext2, coff2)
+    check(whole, d2, ext2, coff2)
