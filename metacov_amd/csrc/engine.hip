@@ -600,7 +600,7 @@ static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t l
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistBins + kOvInts : 0)) * 4;
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistLds + kOvInts : 0)) * 4;
     const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
     int grid = 0;
     if (int rc = occupancy_grid(ctx, stats ? 1 : 0, kfn, lds, ctx->n_chunks, &grid)) return rc;

@@ -43,6 +43,12 @@ namespace mc {
 #ifndef MC_WAVES_STATS
 #define MC_WAVES_STATS 4               // __launch_bounds__ waves/SIMD, fused K2 (<= 128 VGPRs)
 #endif
+#ifndef MC_SCALAR_COFF
+#define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
+#endif
+#ifndef MC_CHEAP_AND
+#define MC_CHEAP_AND 1                 // block-wide AND: one barrier (not __syncthreads_and's three)
+#endif
 
 constexpr int kBlock = 256;            // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
@@ -496,8 +502,33 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
                                              int64_t n, int64_t C0,
                                              const int64_t* __restrict__ coff) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
+#if MC_SCALAR_COFF
+    // The wave's distinct contigs (one or two per batch unless contigs are
+    // tiny) one at a time: a uniform index, so coff comes in on the scalar
+    // path (lgkmcnt).  Per-lane vector loads here would need a vmcnt(0),
+    // which on gfx9 also waits for every depth store still in flight.
+    const int tt[4] = {r.t.x, r.t.y, r.t.z, r.t.w};
+    const int pp[4] = {r.p.x, r.p.y, r.p.z, r.p.w};
+    int64_t g[4] = {0, 0, 0, 0};
+    unsigned todo = 0xfu;   // tids are >= 0 (validated by ingest; padding is 0)
+    for (;;) {
+        const int cand = (todo & 1u) ? tt[0] : (todo & 2u) ? tt[1] : (todo & 4u) ? tt[2]
+                       : (todo & 8u) ? tt[3] : -1;
+        const unsigned long long act = __ballot(cand >= 0);
+        if (!act) break;
+        const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
+        const int64_t c = coff[t0];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (((todo >> k) & 1u) && tt[k] == t0) {
+                g[k] = c + pp[k];
+                todo &= ~(1u << k);
+            }
+    }
+#else
     const int64_t g[4] = {coff[r.t.x] + r.p.x, coff[r.t.y] + r.p.y, coff[r.t.z] + r.p.z,
                           coff[r.t.w] + r.p.w};
+#endif
     constexpr int64_t kClamp = int64_t(1) << 30;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -518,7 +549,30 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
 // the current region in LDS (kHistBins bins; larger values go to an LDS
 // overflow accumulator, and regions whose ranks reach them are recomputed by
 // the host with region_seg_kernel).
-constexpr int kHistBins = 1024;
+//
+// The LDS histogram is kept in kHistCopies lane-striped copies (lane L adds
+// into copy L % kHistCopies).  Neighbouring lanes hold neighbouring positions,
+// which mostly have the same depth: with one copy, the 32 lanes of an LDS
+// atomic group pile onto a handful of bins (same-address lanes serialise; the
+// fused K2 showed 8x the plain kernel's SQ_LDS_BANK_CONFLICT cycles).  Copies
+// start 32 / kHistCopies banks apart, and the flush sums them.  Budget: ring +
+// copies stay at or below 40,672 B so 4 workgroups fit a CU (2 copies of 992
+// bins, 40,928 B, ran at 3: +11 % K2 time).  Measured on C3 / C5 fused K2
+// (scripts/ab_inproc.py): 1 copy 1.195 / 1.600 ms, 2 x 960 1.094 / 1.514,
+// 4 x 480 1.102 / 1.559, 8 x 224 1.096 / 1.723 (narrow windows: fallbacks).
+#ifndef MC_HIST_COPIES
+#define MC_HIST_COPIES 2
+#endif
+#ifndef MC_HIST_BINS
+#define MC_HIST_BINS (MC_HIST_COPIES == 1 ? 1024 : MC_HIST_COPIES == 2 ? 960 \
+                      : MC_HIST_COPIES == 4 ? 480 : MC_HIST_COPIES == 8 ? 224 : 96)
+#endif
+constexpr int kHistBins = MC_HIST_BINS;
+constexpr int kHistCopies = MC_HIST_COPIES;
+static_assert(kHistBins % 32 == 0 && (kHistCopies & (kHistCopies - 1)) == 0 && kHistCopies <= 32,
+              "histogram bins: multiple of 32; copies: power of two");
+constexpr int kHistStride = kHistBins + (kHistCopies > 1 ? 32 / kHistCopies : 0);
+constexpr int kHistLds = kHistCopies * kHistStride;   // ints of LDS
 
 struct FusedRegions {
     int64_t n;                         // 0 = no fused statistics
@@ -627,6 +681,20 @@ __device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1
         ov_add_wave(ov, o0 ? y0 : -1, l0, o1 ? y1 : -1, l1, o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
 }
 
+// Block-wide AND of `pred` with one barrier: each wave's vote is a byte of a
+// double-buffered LDS word (flip = which word; the next call uses the other,
+// so a wave running ahead never overwrites a word another wave still reads).
+// __syncthreads_and compiles to three barriers and an LDS atomic.
+__device__ __forceinline__ bool block_all(int* words, int& flip, bool pred, int wave, int lane) {
+    const bool w = __all(pred);
+    if (lane == 0) reinterpret_cast<unsigned char*>(words + flip)[wave] = w ? 1 : 0;
+    __syncthreads();
+    const bool all = words[flip] == 0x01010101;
+    flip ^= 1;
+    return all;
+}
+static_assert(kWaves == 4, "block_all packs one byte per wave into a word");
+
 // Every thread calls it (it holds barriers): folds the overflow statistics
 // into the region's global accumulator and flushes the LDS histogram.
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
@@ -646,12 +714,15 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
     }
     unsigned* g = R.hist + (int64_t)id * kHistBins;
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
-        const unsigned cnt = h[k];
+        unsigned cnt = 0;
+#pragma unroll
+        for (int c = 0; c < kHistCopies; ++c) cnt += h[c * kHistStride + k];
         if (cnt) {
 #ifndef MC_EXP_NO_GATOMIC
             atomicAdd(&g[k], cnt);
 #endif
-            h[k] = 0;
+#pragma unroll
+            for (int c = 0; c < kHistCopies; ++c) h[c * kHistStride + k] = 0;
         }
     }
     __syncthreads();
@@ -679,11 +750,14 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
              int* __restrict__ max_depth, FusedRegions R) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    int* hdr = lds;                       // [0] chunk id, [1] region cursor, [4..7] wave totals
+    // [0] chunk id, [2..3] first read, [4..7] wave totals, [8..9] read end, [12..13] block_all votes
+    int* hdr = lds;
+    int and_flip = 0;
     int* ring = lds + kLdsHeader;
     unsigned* hist = reinterpret_cast<unsigned*>(ring + kRing);   // kStats only
-    OvLds* ovf = reinterpret_cast<OvLds*>(hist + kHistBins);           // kStats only
+    OvLds* ovf = reinterpret_cast<OvLds*>(hist + kHistLds);            // kStats only
     const int lane = threadIdx.x & 63;
+    unsigned* hist_lane = hist + (lane & (kHistCopies - 1)) * kHistStride;   // this lane's copy
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform per wave
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
@@ -691,7 +765,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
     if (kStats) {
-        for (int k = threadIdx.x; k < kHistBins; k += kBlock) hist[k] = 0;
+        for (int k = threadIdx.x; k < kHistLds; k += kBlock) hist[k] = 0;
         if (threadIdx.x == 0) ov_reset(ovf);   // ordered by the first barrier
     }
 
@@ -768,7 +842,11 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                         b.pending &= ~(1u << k);
                     }
                 }
+#if MC_CHEAP_AND
+                const bool all_done = block_all(hdr + 12, and_flip, b.pending == 0, wave, lane);
+#else
                 const int all_done = __syncthreads_and(b.pending == 0);
+#endif
                 if (!all_done || !more) break;
                 base += kBatch;
                 more = base < cend;
@@ -837,7 +915,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
                             y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        hist_int4(hist, ovf, y0, y1, y2, y3, r_base);
+                        hist_int4(hist_lane, ovf, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
                         flush_region(R, rcur, hist, ovf);
