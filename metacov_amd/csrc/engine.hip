@@ -61,6 +61,37 @@ struct DevBuf {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Host memory a kernel writes directly (coherent, mapped): the fused call's
+// fallback flags land here without a device-to-host copy command.
+template <typename T>
+struct HostMapped {
+    T* h = nullptr;
+    T* d = nullptr;       // device address of h
+    size_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        release();
+        void* p = nullptr;
+        hipError_t e = hipHostMalloc(&p, n * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return e;
+        void* dp = nullptr;
+        e = hipHostGetDevicePointer(&dp, p, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(p);
+            return e;
+        }
+        h = static_cast<T*>(p);
+        d = static_cast<T*>(dp);
+        cap = n;
+        return hipSuccess;
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = d = nullptr;
+        cap = 0;
+    }
+};
+
 // Per-call host arrays go up in ONE copy from a pinned buffer (a pageable
 // hipMemcpyAsync per array costs a staging round trip each).  The caller
 // synchronises the stream before the next reuse.
@@ -151,10 +182,11 @@ struct mc_ctx {
         std::vector<int32_t> tid;
         std::vector<int64_t> start, end;
         int64_t nf = 0;
+        bool chunk_first = false;   // d_fchunk holds this region set's chunk -> region index
     } fcache;
     DevBuf<unsigned> d_flow;
     DevBuf<unsigned> d_fhist;
-    DevBuf<int> d_fflag;
+    HostMapped<int> h_fflag;              // fallback flags, written by region_final_kernel
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
@@ -162,6 +194,7 @@ struct mc_ctx {
     size_t k2_resident_lds[2] = {0, 0};
     mc_timings t{};
     bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
+    bool stats_after_depth = false;       // the statistics span starts at ev[5] (fused call)
 };
 
 static int ctx_use(mc_ctx* ctx) {
@@ -232,11 +265,12 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_acc.release();
     ctx->d_out.release();
     ctx->d_fchunk.release();
+    ctx->h_fflag.release();
     ctx->fstage.release();
     ctx->fcache.valid = false;
+    ctx->fcache.chunk_first = false;
     ctx->d_flow.release();
     ctx->d_fhist.release();
-    ctx->d_fflag.release();
     for (auto ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -716,7 +750,10 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
     const int64_t max_hist = int64_t(1) << 28;
     const int64_t rb = std::max<int64_t>(1, std::min<int64_t>(R, max_hist / nbins));
     const bool lds_hist = nbins <= kLdsBins;
-    if (!out_rows) HIP_TRY(hipEventRecord(ctx->ev[6], s));   // a fallback extends the fused K3b span
+    if (!out_rows) {   // (a fallback extends the fused K3b span)
+        HIP_TRY(hipEventRecord(ctx->ev[6], s));
+        ctx->stats_after_depth = false;
+    }
     int64_t launches = 0;
     for (int64_t r0 = 0; r0 < R; r0 += rb) {
         const int64_t nr = std::min(rb, R - r0);
@@ -798,10 +835,10 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
 // while they are in registers), then the histogram finalize.  Needs regions
 // that do not overlap each other; otherwise K2 then K3.  Regions whose order
 // statistics reach depths >= kHistBins are recomputed by K3.
-// Staging layout of a fused call: sorted region arrays (nf), per-region
-// arrays (R), then the returned flags.
+// Staging layout of a fused call: sorted region arrays (nf), then per-region
+// arrays (R).  The fallback flags come back through ctx->h_fflag.
 struct FusedLayout {
-    size_t gs, ge, id, base, ntot, nzx, brow, up, flag, total;
+    size_t gs, ge, id, base, ntot, nzx, brow, up, total;
 };
 static FusedLayout fused_layout(int64_t nf, int64_t R) {
     auto al = stage_align;
@@ -814,8 +851,7 @@ static FusedLayout fused_layout(int64_t nf, int64_t R) {
     L.nzx = L.ntot + al(R * 8);
     L.brow = L.nzx + al(R * 8);
     L.up = L.brow + al(R * 4);
-    L.flag = L.up;
-    L.total = L.up + al(R * 4);
+    L.total = L.up;
     return L;
 }
 
@@ -826,24 +862,27 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     hipStream_t s = ctx->stream;
     const FusedLayout L = fused_layout(nf, R);
     const size_t o_gs = L.gs, o_ge = L.ge, o_id = L.id, o_base = L.base, o_ntot = L.ntot,
-                 o_nzx = L.nzx, o_brow = L.brow, o_flag = L.flag;
-    (void)o_brow;
+                 o_nzx = L.nzx, o_brow = L.brow;
     HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
-    HIP_TRY(ctx->d_fflag.reserve(R));
+    HIP_TRY(ctx->h_fflag.reserve(R));
     HIP_TRY(ctx->d_acc.reserve(R));
     unsigned char* d = ctx->fstage.d.p;
-    unsigned char* h = ctx->fstage.host();
     const int64_t* d_fge = reinterpret_cast<const int64_t*>(d + o_ge);
     {
-        const int64_t work = std::max<int64_t>({R * kHistBins / 4, R, ctx->n_chunks});
+        // the chunk -> first region index depends only on the staged region
+        // set: built once per set (the binary searches are most of this
+        // launch), reused by repeated calls
+        const int64_t idx_chunks = ctx->fcache.chunk_first ? 0 : ctx->n_chunks;
+        const int64_t work = std::max<int64_t>({R * kHistBins / 4, R, idx_chunks});
         const unsigned g = (unsigned)std::min<int64_t>(4096, (work + kBlock - 1) / kBlock);
         hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
                            ctx->d_fhist.p, R * kHistBins, ctx->d_flow.p, ctx->d_acc.p, R, d_fge, nf,
-                           ctx->chunk_w, ctx->n_chunks, ctx->d_fchunk.p, ctx->d_queue.p,
+                           ctx->chunk_w, idx_chunks, ctx->d_fchunk.p, ctx->d_queue.p,
                            ctx->d_maxdepth.p);
         HIP_TRY(hipGetLastError());
+        ctx->fcache.chunk_first = true;
     }
     FusedRegions fr{nf,
                     ctx->d_fchunk.p,
@@ -856,19 +895,20 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                     ctx->d_flow.p};
     if (nf == 0) fr.n = 0;
     if (int rc = launch_depth(ctx, fr)) return rc;
-    HIP_TRY(hipEventRecord(ctx->ev[6], s));
+    // K3b: its span is timed from K2's end event (one event fewer per call)
+    ctx->stats_after_depth = true;
     hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
                        kHistBins, ctx->d_acc.p, reinterpret_cast<const int64_t*>(d + o_ntot),
-                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->d_fflag.p, 1,
+                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d, 1,
                        reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p, 0,
                        (const int64_t*)nullptr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
     ctx->t.stats_launches += 1;
-    int* flags = reinterpret_cast<int*>(h + o_flag);
-    HIP_TRY(hipMemcpyAsync(flags, ctx->d_fflag.p, R * 4, hipMemcpyDeviceToHost, s));
+    // the flags are in host memory once the stream has drained (no copy command)
     HIP_TRY(hipStreamSynchronize(s));
+    const int* flags = ctx->h_fflag.h;
     std::vector<int32_t> ft;
     std::vector<int64_t> fs, fe, fr_idx;
     for (int64_t r = 0; r < R; ++r)
@@ -898,6 +938,7 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
                      std::memcmp(fc.end.data(), end, R * 8) == 0;
     if (hit) return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
     fc.valid = false;
+    fc.chunk_first = false;
     const int32_t nc = (int32_t)ctx->len.size();
     struct Reg { int64_t gs, ge; int32_t id, base; };
     // histogram window of each region: kHistBins values centred on its
@@ -1023,7 +1064,7 @@ extern "C" int mc_get_timings(mc_ctx* ctx, mc_timings* out) {
     MC_REQUIRE(out, MC_E_INVALID, "null out");
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (ctx->t_depth) ctx->t.depth_ms = elapsed(ctx, 4, 5);
-    if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, 6, 7);
+    if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, ctx->stats_after_depth ? 5 : 6, 7);
     *out = ctx->t;
     return MC_OK;
 }
