@@ -697,13 +697,16 @@ static_assert(kWaves == 4, "block_all packs one byte per wave into a word");
 
 // Every thread calls it (it holds barriers): folds the overflow statistics
 // into the region's global accumulator and flushes the LDS histogram.
+// kBarriers = false: the caller has just passed a barrier after the last
+// atomics, and a barrier follows before the histogram is used again.
+template <bool kBarriers = true>
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
                                              OvLds* ov) {
 #ifdef MC_EXP_NO_FLUSH
     return;
 #endif
     const int id = R.id[r];
-    __syncthreads();   // every wave's histogram and overflow atomics are in
+    if (kBarriers) __syncthreads();   // every wave's histogram and overflow atomics are in
     if (threadIdx.x == 0 && ov->cnt) {
         if (ov->low) atomicAdd(&R.low[id], ov->low);
         atomicMin(&R.acc[id].min, ov->vmin);
@@ -725,7 +728,7 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
             for (int c = 0; c < kHistCopies; ++c) h[c * kHistStride + k] = 0;
         }
     }
-    __syncthreads();
+    if (kBarriers) __syncthreads();
 }
 
 // One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
@@ -931,11 +934,12 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 }
             }
         }
+        __syncthreads();   // everyone is past hdr / ring of this chunk (and its atomics)
         if (kStats) {
-            // a region still open at the chunk end has partials here
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region(R, rcur, hist, ovf);
+            // a region still open at the chunk end has partials here; the
+            // barrier above and the one after the ring zeroing bracket it
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false>(R, rcur, hist, ovf);
         }
-        __syncthreads();   // everyone is past hdr / ring of this chunk
         if (threadIdx.x == 0) {
             next_c = atomicAdd(queue, 1u);
             if (next_c < n_chunks) {
