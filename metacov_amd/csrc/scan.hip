@@ -240,12 +240,16 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
         const int64_t b0 = rev ? (int64_t)gpos - rlen : (int64_t)gpos;
         const int nw = (rlen + 7) >> 3;
         const bool fast = rw.g && b0 >= rw.wlo && b0 + rlen <= rw.whi;
+        // The mismatch count only grows, so testing it once at the end
+        // rejects exactly the reads the reference's early exit does; without
+        // the exit the staged-window loop has no loop-carried branch and its
+        // LDS reads of several words are in flight together.
         int mism = 0;
-        bool reject = false;
-        for (int k = 0; k < nw && !reject; ++k) {
-            const uint32_t w = s32[k];
-            const int n8 = min(8, rlen - 8 * k);
-            if (fast) {
+        if (fast) {
+#pragma unroll 4
+            for (int k = 0; k < nw; ++k) {
+                const uint32_t w = s32[k];
+                const int n8 = min(8, rlen - 8 * k);
                 uint32_t lo, hi;
                 rw.at8(b0 + 8 * k, lo, hi);
 #pragma unroll
@@ -253,11 +257,15 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
                     const int rv = (int)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 255u);
                     mism += (j < n8) & (nt4_of(nib8(w, j)) != rv);
                 }
-            } else {
+            }
+        } else {
+            for (int k = 0; k < nw && mism * 32 <= rlen; ++k) {
+                const uint32_t w = s32[k];
+                const int n8 = min(8, rlen - 8 * k);
                 for (int j = 0; j < n8; ++j) mism += nt4_of(nib8(w, j)) != rw.at(b0 + 8 * k + j);
             }
-            reject = mism * 32 > rlen;
         }
+        const bool reject = mism * 32 > rlen;
         if (!reject) {
             const int64_t rowstride = (int64_t)a.G * 5;
             for (int x = 0; x < a.base_start; ++x) {
@@ -318,36 +326,54 @@ __device__ __forceinline__ void count_bases(const ScanArgs& a, int64_t r, bool p
         return;
     }
     uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    // two reads per step, branch-free (a position past the read end reads
+    // the read's first byte and adds 0), so both reads' LDS loads are in
+    // flight together instead of one read's latency at a time
     while (pend) {
         const int l = __builtin_ctzll(pend);
         pend &= pend - 1;
+        const bool two = pend != 0;
+        const int l2 = two ? __builtin_ctzll(pend) : l;
+        if (two) pend &= pend - 1;
         const int rl = __builtin_amdgcn_readlane(rlen, l);
         const int rv = __builtin_amdgcn_readlane(fl, l) & 0x10;
         const int so = __builtin_amdgcn_readlane(soff, l);
+        const int rl2 = two ? __builtin_amdgcn_readlane(rlen, l2) : 0;
+        const int rv2 = __builtin_amdgcn_readlane(fl, l2) & 0x10;
+        const int so2 = __builtin_amdgcn_readlane(soff, l2);
         lds_cu8* s = (lds_cu8*)(sseq + so);
-#define MC_COUNT_POS(q, c)                                                     \
-        {                                                                      \
-            const int x = lane + 64 * (q);                                     \
-            if (x < rl) {                                                      \
-                const int j = rv ? rl - 1 - x : x;                             \
-                const uint32_t byte = s[j >> 1];                               \
-                int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));          \
-                if (rv) v = comp4(v);                                          \
-                c += 1ull << (12 * v);                                         \
-            }                                                                  \
-        }
-        MC_COUNT_POS(0, c0)
-        MC_COUNT_POS(1, c1)
-        MC_COUNT_POS(2, c2)
-        MC_COUNT_POS(3, c3)
-#undef MC_COUNT_POS
-        for (int x = 256 + lane; x < rl; x += 64) {
-            const int j = rv ? rl - 1 - x : x;
-            const uint32_t byte = s[j >> 1];
+        lds_cu8* s2 = (lds_cu8*)(sseq + so2);
+        auto count_pos = [](lds_cu8* sp, int len, int rev, int x, uint64_t& c) {
+            const bool ok = x < len;
+            const int j = ok ? (rev ? len - 1 - x : x) : 0;
+            const uint32_t byte = sp[j >> 1];
             int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
-            if (rv) v = comp4(v);
-            __hip_atomic_fetch_add(lds + a.lds_base + (x + a.base_start) * rowstride + g0 * 5 + v, 1u,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (rev) v = comp4(v);
+            c += ok ? (1ull << (12 * v)) : 0ull;
+        };
+        count_pos(s, rl, rv, lane, c0);
+        count_pos(s2, rl2, rv2, lane, c0);
+        count_pos(s, rl, rv, lane + 64, c1);
+        count_pos(s2, rl2, rv2, lane + 64, c1);
+        if (max(rl, rl2) > 128) {
+            count_pos(s, rl, rv, lane + 128, c2);
+            count_pos(s2, rl2, rv2, lane + 128, c2);
+        }
+        if (max(rl, rl2) > 192) {
+            count_pos(s, rl, rv, lane + 192, c3);
+            count_pos(s2, rl2, rv2, lane + 192, c3);
+        }
+        for (int k = 0; k < 2; ++k) {
+            const int len = k ? rl2 : rl, rev = k ? rv2 : rv;
+            lds_cu8* sp = k ? s2 : s;
+            for (int x = 256 + lane; x < len; x += 64) {
+                const int j = rev ? len - 1 - x : x;
+                const uint32_t byte = sp[j >> 1];
+                int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
+                if (rev) v = comp4(v);
+                __hip_atomic_fetch_add(lds + a.lds_base + (x + a.base_start) * rowstride + g0 * 5 + v,
+                                       1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
     }
     const uint64_t cs[4] = {c0, c1, c2, c3};
