@@ -835,6 +835,11 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
 // while they are in registers), then the histogram finalize.  Needs regions
 // that do not overlap each other; otherwise K2 then K3.  Regions whose order
 // statistics reach depths >= kHistBins are recomputed by K3.
+#ifndef MC_WIN_BELOW
+#define MC_WIN_BELOW (3 * kHistBins / 4)
+#endif
+constexpr int kWinBelow = MC_WIN_BELOW;   // window bins below the estimated body depth
+
 // Staging layout of a fused call: sorted region arrays (nf), then per-region
 // arrays (R).  The fallback flags come back through ctx->h_fflag.
 struct FusedLayout {
@@ -941,9 +946,10 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     fc.chunk_first = false;
     const int32_t nc = (int32_t)ctx->len.size();
     struct Reg { int64_t gs, ge; int32_t id, base; };
-    // histogram window of each region: kHistBins values centred on its
-    // contig's mean depth (aligned bases / extent)
+    // histogram window of each region: kHistBins values, kWinBelow of them
+    // below its contig's estimated body depth
     std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
+    const double span_mean = ctx->n_reads ? (double)ctx->aligned_bases / (double)ctx->n_reads : 0.0;
     std::vector<Reg> regs;
     regs.reserve(R);
     std::vector<int64_t> ntot(std::max<int64_t>(R, 1)), nzx(std::max<int64_t>(R, 1));
@@ -957,8 +963,14 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
         ntot[r] = end[r] - start[r];
         nzx[r] = ntot[r] - (b - a);
-        const double mean = ext > 0 ? (double)ctx->cbases[tid[r]] / (double)ext : 0.0;
-        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(mean) - kHistBins / 2);
+        // the contig's body depth: its aligned bases over its length less one
+        // mean read span (the two end ramps hold about half a span of depth
+        // each); the window sits mostly below it, where the quartile ranks
+        // of a contig with long-read ramps fall (C5 fallbacks: 259 at kHistBins / 2
+        // below, 123 at 3 / 4)
+        const double body = ext > 2 * span_mean ? (double)ext - span_mean : (double)ext;
+        const double depth_est = ext > 0 ? (double)ctx->cbases[tid[r]] / body : 0.0;
+        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(depth_est) - kWinBelow);
         if (b > a)
             regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
     }

@@ -556,15 +556,17 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
 // atomic group pile onto a handful of bins (same-address lanes serialise; the
 // fused K2 showed 8x the plain kernel's SQ_LDS_BANK_CONFLICT cycles).  Copies
 // start 32 / kHistCopies banks apart, and the flush sums them.  Budget: ring +
-// copies stay at or below 40,672 B so 4 workgroups fit a CU (2 copies of 992
-// bins, 40,928 B, ran at 3: +11 % K2 time).  Measured on C3 / C5 fused K2
-// (scripts/ab_inproc.py): 1 copy 1.195 / 1.600 ms, 2 x 960 1.094 / 1.514,
-// 4 x 480 1.102 / 1.559, 8 x 224 1.096 / 1.723 (narrow windows: fallbacks).
+// copies + overflow records stay at or below 40,672 B so 4 workgroups fit a
+// CU (2 copies of 992 bins, 40,928 B in all, ran at 3: +11 % K2 time).
+// Measured on C3 / C5 fused K2 (scripts/ab_inproc.py, one 32-byte overflow
+// record): 1 copy 1.195 / 1.600 ms, 2 x 960 1.094 / 1.514, 4 x 480 1.102 /
+// 1.559, 8 x 224 1.096 / 1.723 (narrow windows: fallbacks).  With the 16
+// overflow records (640 B) the 2 copies hold 864 bins (40,512 B).
 #ifndef MC_HIST_COPIES
 #define MC_HIST_COPIES 2
 #endif
 #ifndef MC_HIST_BINS
-#define MC_HIST_BINS (MC_HIST_COPIES == 1 ? 1024 : MC_HIST_COPIES == 2 ? 960 \
+#define MC_HIST_BINS (MC_HIST_COPIES == 1 ? 1024 : MC_HIST_COPIES == 2 ? 864 \
                       : MC_HIST_COPIES == 4 ? 480 : MC_HIST_COPIES == 8 ? 224 : 96)
 #endif
 constexpr int kHistBins = MC_HIST_BINS;
@@ -587,14 +589,21 @@ struct FusedRegions {
 };
 
 // Statistics of the values outside the histogram window of the current
-// region: one LDS record per workgroup behind the histogram, updated with LDS
-// atomics on the rare out-of-window path (no registers held for it).
+// region: kOvRecs LDS records per workgroup behind the histogram (lane L
+// updates record L % kOvRecs with LDS atomics), folded at the flush.  The
+// out-of-window path is cold on C3 but not at C5, where the ramps at the ends
+// of deep contigs fall below the window: a wave-wide reduction per int4 there
+// cost 0.1 ms a launch.  40-byte records start 10 banks apart, so the 16
+// records' fields sit in distinct banks (lanes L and L + 16 share one).
 struct OvLds {
     unsigned long long sum, sq;
     int vmin, vmax;
     unsigned cnt, low;                 // values outside the window / below it
+    unsigned pad[2];
 };
-constexpr int kOvInts = sizeof(OvLds) / 4;
+constexpr int kOvRecs = 16;
+static_assert(sizeof(OvLds) == 40, "record stride: 10 banks");
+constexpr int kOvInts = kOvRecs * (int)sizeof(OvLds) / 4;
 
 __device__ __forceinline__ void ov_reset(OvLds* ov) {
     ov->sum = ov->sq = 0;
@@ -603,21 +612,11 @@ __device__ __forceinline__ void ov_reset(OvLds* ov) {
     ov->cnt = ov->low = 0;
 }
 
-// Statistics of one run of `cnt` positions of value v outside the window.
-__device__ __forceinline__ void ov_add(OvLds* ov, int v, int cnt, int base) {
-    atomicAdd(&ov->cnt, (unsigned)cnt);
-    if (v < base) atomicAdd(&ov->low, (unsigned)cnt);
-    atomicAdd(&ov->sum, (unsigned long long)v * (unsigned long long)cnt);
-    atomicAdd(&ov->sq, (unsigned long long)((long long)v * v) * (unsigned long long)cnt);
-    atomicMin(&ov->vmin, v);
-    atomicMax(&ov->vmax, v);
-}
-
-// The wave's runs outside the histogram window (contig ends, depth far from
-// the mean): reduced across the wave, then one lane updates the LDS record.
+// A lane's runs outside the histogram window (contig ends, depth far from
+// the mean), summed in the lane, then added to its record (ov = the record).
 // Out of line: its temporaries stay off the hot loop's register budget.
 // v < 0: no run in that slot.
-__device__ __attribute__((noinline, cold)) void ov_add_wave(OvLds* ov, int v0, int n0, int v1, int n1,
+__device__ __attribute__((noinline, cold)) void ov_add_lane(OvLds* ov, int v0, int n0, int v1, int n1,
                                                        int v2, int n2, int v3, int base) {
     unsigned long long s = 0, q = 0;
     unsigned c = 0, lo = 0;
@@ -635,16 +634,7 @@ __device__ __attribute__((noinline, cold)) void ov_add_wave(OvLds* ov, int v0, i
     take(v1, n1);
     take(v2, n2);
     take(v3, 1);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        s += __shfl_xor(s, d, 64);
-        q += __shfl_xor(q, d, 64);
-        c += __shfl_xor(c, d, 64);
-        lo += __shfl_xor(lo, d, 64);
-        mn = min(mn, __shfl_xor(mn, d, 64));
-        mx = max(mx, __shfl_xor(mx, d, 64));
-    }
-    if ((threadIdx.x & 63) == 0) {
+    if (c) {
         atomicAdd(&ov->cnt, c);
         if (lo) atomicAdd(&ov->low, lo);
         atomicAdd(&ov->sum, s);
@@ -677,8 +667,13 @@ __device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1
     if (w3) atomicAdd(&h[b3], 1u);
 #endif
     const bool o0 = e0 && !w0, o1 = e1 && !w1, o2 = e2 && !w2, o3 = e3 && !w3;
+#ifndef MC_EXP_NO_OV
     if (__builtin_expect(__any(o0 || o1 || o2 || o3), 0))
-        ov_add_wave(ov, o0 ? y0 : -1, l0, o1 ? y1 : -1, l1, o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
+#else
+    if (false)
+#endif
+        ov_add_lane(ov + (threadIdx.x & (kOvRecs - 1)), o0 ? y0 : -1, l0, o1 ? y1 : -1, l1,
+                    o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
 }
 
 // Block-wide AND of `pred` with one barrier: each wave's vote is a byte of a
@@ -707,13 +702,16 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
 #endif
     const int id = R.id[r];
     if (kBarriers) __syncthreads();   // every wave's histogram and overflow atomics are in
-    if (threadIdx.x == 0 && ov->cnt) {
-        if (ov->low) atomicAdd(&R.low[id], ov->low);
-        atomicMin(&R.acc[id].min, ov->vmin);
-        atomicMax(&R.acc[id].max, ov->vmax);
-        atomicAdd(&R.acc[id].sum, ov->sum);
-        atomicAdd(&R.acc[id].sumsq, ov->sq);
-        ov_reset(ov);
+    if (threadIdx.x < kOvRecs) {
+        OvLds* o = ov + threadIdx.x;
+        if (o->cnt) {
+            if (o->low) atomicAdd(&R.low[id], o->low);
+            atomicMin(&R.acc[id].min, o->vmin);
+            atomicMax(&R.acc[id].max, o->vmax);
+            atomicAdd(&R.acc[id].sum, o->sum);
+            atomicAdd(&R.acc[id].sumsq, o->sq);
+            ov_reset(o);
+        }
     }
     unsigned* g = R.hist + (int64_t)id * kHistBins;
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
@@ -769,7 +767,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     int my_max = 0;
     if (kStats) {
         for (int k = threadIdx.x; k < kHistLds; k += kBlock) hist[k] = 0;
-        if (threadIdx.x == 0) ov_reset(ovf);   // ordered by the first barrier
+        if (threadIdx.x < kOvRecs) ov_reset(ovf + threadIdx.x);   // ordered by the first barrier
     }
 
     // chunk ids come from an atomic queue; thread 0 fetches the next id (and
