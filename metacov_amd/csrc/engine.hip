@@ -759,6 +759,15 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
         const int64_t nr = std::min(rb, R - r0);
         std::vector<int64_t> sg_gs, sg_ge, ntot(nr), nzx(nr);
         std::vector<int32_t> sg_reg;
+        // segment length: kSeg, halved (down to 16 Ki) while a small job
+        // (the fused path's fallback regions) would leave the CUs idle
+        int64_t covered = 0;
+        for (int64_t k = 0; k < nr; ++k) {
+            const int64_t ext = ctx->extent[tid[r0 + k]];
+            covered += std::min(end[r0 + k], ext) - std::min(start[r0 + k], ext);
+        }
+        int64_t seg = kSeg;
+        while (seg > 16384 && covered / seg < 2048) seg >>= 1;
         for (int64_t k = 0; k < nr; ++k) {
             const int64_t r = r0 + k;
             const int32_t t = tid[r];
@@ -766,9 +775,9 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
             const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
             ntot[k] = end[r] - start[r];
             nzx[k] = ntot[k] - (b - a);
-            for (int64_t p = a; p < b; p += kSeg) {
+            for (int64_t p = a; p < b; p += seg) {
                 sg_gs.push_back(ctx->coff[t] + p);
-                sg_ge.push_back(ctx->coff[t] + std::min(b, p + kSeg));
+                sg_ge.push_back(ctx->coff[t] + std::min(b, p + seg));
                 sg_reg.push_back((int32_t)k);
             }
         }
@@ -871,7 +880,7 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
-    HIP_TRY(ctx->h_fflag.reserve(R));
+    HIP_TRY(ctx->h_fflag.reserve(R + 1));
     HIP_TRY(ctx->d_acc.reserve(R));
     unsigned char* d = ctx->fstage.d.p;
     const int64_t* d_fge = reinterpret_cast<const int64_t*>(d + o_ge);
@@ -902,11 +911,13 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     if (int rc = launch_depth(ctx, fr)) return rc;
     // K3b: its span is timed from K2's end event (one event fewer per call)
     ctx->stats_after_depth = true;
-    hipLaunchKernelGGL(region_final_kernel, dim3((unsigned)R), dim3(kBlock), 0, s, ctx->d_fhist.p,
-                       kHistBins, ctx->d_acc.p, reinterpret_cast<const int64_t*>(d + o_ntot),
-                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d, 1,
-                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p, 0,
-                       (const int64_t*)nullptr);
+    // one wave per region; flags [0, R) and K2's max depth [R] land in mapped host memory
+    hipLaunchKernelGGL(region_final_wave_kernel, dim3((unsigned)((R + kWaves - 1) / kWaves)),
+                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,
+                       reinterpret_cast<const int64_t*>(d + o_ntot),
+                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,
+                       ctx->d_maxdepth.p, ctx->h_fflag.d + R);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
@@ -914,6 +925,7 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     // the flags are in host memory once the stream has drained (no copy command)
     HIP_TRY(hipStreamSynchronize(s));
     const int* flags = ctx->h_fflag.h;
+    ctx->max_depth = flags[R];   // a fallback's K3 sizes its histogram by it
     std::vector<int32_t> ft;
     std::vector<int64_t> fs, fe, fr_idx;
     for (int64_t r = 0; r < R; ++r)

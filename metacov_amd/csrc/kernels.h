@@ -1206,4 +1206,110 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     }
 }
 
+// The fused path's finalize: one wave per region (4 per workgroup) over its
+// kHistBins-bin window, the same rules as region_final_kernel with base_of,
+// low_of and hist_stats set and no row scatter.  A 256-thread block per
+// region spent most of its time being dispatched (C5: 10,000 regions,
+// 40 us).  Lane L owns bins [L * kFinPer, L * kFinPer + kFinPer).  Block 0
+// also copies K2's max depth to max_out (mapped host memory: the fallback
+// path needs it without a device-to-host copy).
+constexpr int kFinPer = (kHistBins + 63) / 64;
+
+__global__ void __launch_bounds__(kBlock)
+region_final_wave_kernel(const unsigned* __restrict__ hist, int64_t R,
+                         const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
+                         const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
+                         int* __restrict__ fallback, const int32_t* __restrict__ base_of,
+                         const unsigned* __restrict__ low_of, const int* __restrict__ max_depth,
+                         int* __restrict__ max_out) {
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && max_out) *max_out = *max_depth;
+    const int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const unsigned* hr = hist + r * kHistBins;
+    const long long n = n_total[r];
+    const long long zx = n_zero_extra[r];
+    const long long base = base_of[r];
+    const long long zx_bin = base == 0 ? zx : 0;
+    const long long low = (long long)low_of[r] + (base == 0 ? 0 : zx);
+    const long long r_lo = (n - 1) / 2, r_hi = n / 2;
+    const long long q_lo = n / 4, q_hi = n - n / 4;
+    const int b0 = lane * kFinPer;
+    long long c[kFinPer];
+    long long mine = 0;
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+        const int b = b0 + k;
+        c[k] = b < kHistBins ? (long long)hr[b] + (b == 0 ? zx_bin : 0) : 0;
+        mine += c[k];
+    }
+    long long incl = mine;                   // 64-bit wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const long long in_hist = __shfl(incl, 63, 64);
+    long long cum = low + incl - mine;
+    long long qsum = 0, s1 = 0, med_lo = -1, med_hi = -1;
+    unsigned long long s2 = 0;
+    int lmin = 0x7fffffff, lmax = -1;
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+        const long long cnt = c[k];
+        if (cnt == 0) continue;
+        const long long v = base + b0 + k;
+        const long long e = cum + cnt;
+        if (r_lo >= cum && r_lo < e) med_lo = v;
+        if (r_hi >= cum && r_hi < e) med_hi = v;
+        const long long lo = cum > q_lo ? cum : q_lo;
+        const long long hi = e < q_hi ? e : q_hi;
+        if (hi > lo) qsum += (hi - lo) * v;
+        s1 += cnt * v;
+        s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
+        lmin = min(lmin, b0 + k);
+        lmax = max(lmax, b0 + k);
+        cum = e;
+    }
+    qsum = wave_sum64(qsum);
+    s1 = wave_sum64(s1);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        s2 += __shfl_xor(s2, d, 64);
+        med_lo = max(med_lo, (long long)__shfl_xor(med_lo, d, 64));
+        med_hi = max(med_hi, (long long)__shfl_xor(med_hi, d, 64));
+    }
+    lmin = wave_min(lmin);
+    lmax = wave_max(lmax);
+    if (lane != 0) return;
+    const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
+    fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi))
+                      ? 1 : 0;
+    const RegionAcc a = acc[r];
+    RegionOut o;
+    o.n = n;
+    const long long high = n - win_hi;       // values above the window
+    o.sum = s1 + (long long)a.sum;
+    o.sumsq = s2 + a.sumsq;
+    if (low > 0) {
+        long long m = a.min;                 // INT_MAX when only zeros are below
+        if (base > 0 && zx > 0) m = 0;
+        o.min = m;
+    } else {
+        o.min = in_hist > 0 ? base + lmin : a.min;
+    }
+    o.max = high > 0 ? (long long)a.max : (in_hist > 0 ? base + lmax : (long long)a.max);
+    if (o.max < 0) o.max = 0;
+    o.med_lo = med_lo < 0 ? 0 : med_lo;
+    o.med_hi = med_hi < 0 ? 0 : med_hi;
+    o.q23_sum = qsum;
+    o.q23_cnt = q_hi - q_lo;
+    if (n == 0) {
+        o.min = o.max = o.med_lo = o.med_hi = o.q23_sum = o.q23_cnt = 0;
+        o.sum = 0;
+        o.sumsq = 0;
+    }
+    out[r] = o;
+}
+
 }  // namespace mc
