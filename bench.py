@@ -316,14 +316,17 @@ def main():
         achieved_k1 = k1_bytes / (k1_ms * 1e-3) / 1e9
     pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
     traffic = None
-    variant = "depth_kernel<%s>" % ("false" if args.unfused else "true")
+    # depth_kernel<kStats, kLong>: the long-read variant runs when a span exceeds the LDS ring
+    long_path = args.config == "c5"
+    variant = "depth_kernel<%s, %s>" % ("false" if args.unfused else "true",
+                                         "true" if long_path else "false")
     for v in ([] if args.strong else (pmc or {}).get("variants", [])):   # PMC of the per-GPU workload
         if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
                 and variant in v.get("kernel", ""):
             traffic = v.get("hbm_bytes_per_launch")
     roofline = {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                 "frac": achieved / 8000.0, "traffic": traffic,
-                "kernel": "depth_kernel<%s> (K2)" % ("false" if args.unfused else "true"),
+                "kernel": "%s (K2)" % variant,
                 "algorithmic_bytes_per_launch": int(k2_bytes)}
     if args.cigar and k1_ms > k2_ms:
         k1_traffic = None

@@ -190,8 +190,8 @@ struct mc_ctx {
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
-    int k2_resident[2] = {0, 0};          // resident K2 workgroups (plain, fused)
-    size_t k2_resident_lds[2] = {0, 0};
+    int k2_resident[4] = {0, 0, 0, 0};    // resident K2 workgroups (plain, fused) x (short, long)
+    size_t k2_resident_lds[4] = {0, 0, 0, 0};
     mc_timings t{};
     bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
     bool stats_after_depth = false;       // the statistics span starts at ev[5] (fused call)
@@ -593,7 +593,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             cdiff[c] = run;
         }
         ctx->n_long_events = acc;
-        HIP_TRY(ctx->d_tile_ev.reserve(std::max<int64_t>(acc, 1)));
+        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(acc + kBatch)));   // K2 loads whole int4 batches
         HIP_TRY(hipMemcpyAsync(ctx->d_tile_off.p, toff.data(), (n_tiles + 1) * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(ctx->d_chunk_carry.p, cdiff.data(), ctx->n_chunks * 4,
                                hipMemcpyHostToDevice, s));
@@ -635,9 +635,12 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
     const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistLds + kOvInts : 0)) * 4;
-    const void* kfn = stats ? (const void*)depth_kernel<true> : (const void*)depth_kernel<false>;
+    const bool lng = ctx->has_long;
+    const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
+                            : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);
     int grid = 0;
-    if (int rc = occupancy_grid(ctx, stats ? 1 : 0, kfn, lds, ctx->n_chunks, &grid)) return rc;
+    if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, ctx->n_chunks, &grid))
+        return rc;
     if (!stats) {   // the fused path's fused_init_kernel zeroes them
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
         HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
@@ -646,16 +649,19 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
-    if (stats)
-        hipLaunchKernelGGL(depth_kernel<true>, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,
-                           ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,
-                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
-                           ctx->d_maxdepth.p, fr);
-    else
-        hipLaunchKernelGGL(depth_kernel<false>, dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,
-                           ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,
-                           ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->short_max, toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p,
-                           ctx->d_maxdepth.p, fr);
+#define MC_LAUNCH_K2(S, L)                                                                     \
+    hipLaunchKernelGGL((depth_kernel<S, L>), dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,     \
+                       ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,                  \
+                       ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->short_max, \
+                       toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr)
+    if (stats) {
+        if (lng) MC_LAUNCH_K2(true, true);
+        else MC_LAUNCH_K2(true, false);
+    } else {
+        if (lng) MC_LAUNCH_K2(false, true);
+        else MC_LAUNCH_K2(false, false);
+    }
+#undef MC_LAUNCH_K2
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[5], s));
     ctx->t_depth = true;

@@ -46,9 +46,6 @@ namespace mc {
 #ifndef MC_SCALAR_COFF
 #define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
 #endif
-#ifndef MC_CHEAP_AND
-#define MC_CHEAP_AND 1                 // block-wide AND: one barrier (not __syncthreads_and's three)
-#endif
 
 constexpr int kBlock = 256;            // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
@@ -61,7 +58,7 @@ __device__ __forceinline__ int ring_slot(int rel) { return rel % kRing; }
 constexpr int kTilesPerChunk = MC_TILES_PER_CHUNK;
 constexpr int kReadsPerThread = 4;     // int4 loads of tid/pos/span
 constexpr int kBatch = kBlock * kReadsPerThread;
-constexpr int kLdsHeader = 16;         // ints reserved in front of the ring
+constexpr int kLdsHeader = 20;         // ints reserved in front of the ring (K2: see depth_kernel)
 constexpr int kSeg = 65536;            // K3 segment length (positions)
 constexpr int kLdsBins = 16384;        // K3 LDS histogram bins (64 KiB)
 
@@ -361,7 +358,8 @@ long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ po
         const LongEv e = long_events(tid, pos, span, w0 + lane, n, coff, short_max, alloc_len,
                                      chunk_w, &ge);
         const unsigned slot = wave_key_add(tile_cursor, e.tile, lane);
-        if (e.tile >= 0) ev[tile_off[e.tile] + slot] = (int32_t)(ge - (int64_t)e.tile * kTileW);
+        // chunk-relative end (grouped by tile, so a chunk's events stream in tile order)
+        if (e.tile >= 0) ev[tile_off[e.tile] + slot] = (int32_t)(ge - ge / chunk_w * chunk_w);
     }
 }
 
@@ -676,19 +674,45 @@ __device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1
                     o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
 }
 
-// Block-wide AND of `pred` with one barrier: each wave's vote is a byte of a
-// double-buffered LDS word (flip = which word; the next call uses the other,
-// so a wave running ahead never overwrites a word another wave still reads).
-// __syncthreads_and compiles to three barriers and an LDS atomic.
-__device__ __forceinline__ bool block_all(int* words, int& flip, bool pred, int wave, int lane) {
-    const bool w = __all(pred);
-    if (lane == 0) reinterpret_cast<unsigned char*>(words + flip)[wave] = w ? 1 : 0;
+// Block-wide AND of two predicates with one barrier: each wave's votes are
+// bits 0 / 1 of a byte of a double-buffered LDS word (flip = which word; the
+// next call uses the other, so a wave running ahead never overwrites a word
+// another wave still reads).  __syncthreads_and compiled to three barriers
+// and an LDS atomic for one predicate.
+static_assert(kWaves == 4, "block_all2 packs one byte per wave into a word");
+__device__ __forceinline__ void block_all2(int* words, int& flip, bool p0, bool p1, int wave, int lane,
+                                           bool& all0, bool& all1) {
+    const int v = (__all(p0) ? 1 : 0) | (__all(p1) ? 2 : 0);
+    if (lane == 0) reinterpret_cast<unsigned char*>(words + flip)[wave] = (unsigned char)v;
     __syncthreads();
-    const bool all = words[flip] == 0x01010101;
+    const int w = words[flip];
+    all0 = (w & 0x01010101) == 0x01010101;
+    all1 = (w & 0x02020202) == 0x02020202;
     flip ^= 1;
-    return all;
 }
-static_assert(kWaves == 4, "block_all packs one byte per wave into a word");
+
+// A batch of the chunk's long-read end events: 4 consecutive events per
+// thread (chunk-relative positions), indices [e_lo, e_hi) only.
+struct EvBatch {
+    int rel[4];
+    unsigned pending;
+};
+
+__device__ __forceinline__ void load_events(EvBatch& e, const int32_t* __restrict__ ev, int64_t base,
+                                            int64_t e_lo, int64_t e_hi) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * 4;
+    e.pending = 0;
+    if (i0 < e_hi && i0 + 4 > e_lo) {   // ev is padded by one batch past its end
+        const i32x4 x = *reinterpret_cast<const i32x4*>(ev + i0);
+        e.rel[0] = x.x;
+        e.rel[1] = x.y;
+        e.rel[2] = x.z;
+        e.rel[3] = x.w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k >= e_lo && i0 + k < e_hi) e.pending |= 1u << k;
+    }
+}
 
 // Every thread calls it (it holds barriers): folds the overflow statistics
 // into the region's global accumulator and flushes the LDS histogram.
@@ -738,7 +762,10 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
 // Reads longer than short_max = ring - kTileW take the long-read path (see
 // long_count_kernel); the halo of chunk_first is min(max_span, short_max).
 // kStats: fold the tile into FusedRegions before it leaves the registers.
-template <bool kStats>
+// kLong: the long-read path is compiled in (spans > short_max exist); without
+// it the event stream's registers are not held (the fused variant is at its
+// 128-VGPR budget).
+template <bool kStats, bool kLong>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
 __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
                                                  : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
@@ -751,7 +778,8 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
              int* __restrict__ max_depth, FusedRegions R) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    // [0] chunk id, [2..3] first read, [4..7] wave totals, [8..9] read end, [12..13] block_all votes
+    // [0] chunk id, [2..3] first read, [4..7] wave totals, [8..9] read end, [12..13] block_all votes,
+    // [16..19] the chunk's long-read event range
     int* hdr = lds;
     int and_flip = 0;
     int* ring = lds + kLdsHeader;
@@ -774,6 +802,14 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     // its chunk_first) while the current chunk is processed
     unsigned next_c = 0;
     int64_t next_first = 0, next_end = 0;
+    // [16..19]: the chunk's range of long-read end events
+    auto load_event_range = [&](int64_t c) {
+        if (tile_ev_off && c < n_chunks) {
+            long long* o = reinterpret_cast<long long*>(hdr + 16);
+            o[0] = tile_ev_off[c * tiles_per_chunk];
+            o[1] = tile_ev_off[(c + 1) * tiles_per_chunk];
+        }
+    };
     if (threadIdx.x == 0) {
         const unsigned c0 = atomicAdd(queue, 1u);
         hdr[0] = (int)c0;
@@ -781,6 +817,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             *reinterpret_cast<long long*>(hdr + 2) = chunk_first[2 * c0];
             *reinterpret_cast<long long*>(hdr + 8) = chunk_first[2 * c0 + 1];
         }
+        load_event_range(c0);
     }
     for (;;) {
         // zero the ring (also orders the hdr writes before the reads)
@@ -813,19 +850,36 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
             finish_batch(b, r0, base, n, C0, coff);
         }
-        const bool has_long = tile_ev_off != nullptr;
+        constexpr bool has_long = kLong;
         int carry = has_long ? chunk_carry[c] : 0;
+        // -1 end events of long reads (chunk-relative, in tile order): a
+        // second stream of 1024-event batches, applied like the reads while
+        // they lie before the current tile end (a dependent load chain per
+        // tile was 0.24 ms of a C5 launch)
+        EvBatch eb;
+        eb.pending = 0;
+        int64_t ev_lo = 0, ev_hi = 0, ev_base = 0;
+        bool ev_more = false;
+        if (has_long) {
+            ev_lo = *reinterpret_cast<const long long*>(hdr + 16);
+            ev_hi = *reinterpret_cast<const long long*>(hdr + 18);
+            ev_base = ev_lo & ~(int64_t)3;
+            ev_more = ev_base < ev_hi;
+            if (ev_more) load_events(eb, tile_ev, ev_base, ev_lo, ev_hi);
+        }
         for (int t = 0; t < tiles_per_chunk; ++t) {
             const int64_t T0 = C0 + (int64_t)t * kTileW;
             const int64_t Tend = T0 + kTileW;
-            if (has_long) {   // -1 end events of long reads ending in this tile
-                const int64_t tt = T0 / kTileW;
-                const int64_t e0 = tile_ev_off[tt], e1 = tile_ev_off[tt + 1];
-                for (int64_t k = e0 + threadIdx.x; k < e1; k += kBlock)
-                    atomicAdd(&ring[ring_slot(t * kTileW + tile_ev[k])], -1);
-            }
             const int tend_rel = (t + 1) * kTileW;   // C0 is a multiple of the ring size
             for (;;) {
+                if (has_long) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (((eb.pending >> k) & 1u) && eb.rel[k] < tend_rel) {
+                            atomicAdd(&ring[ring_slot(eb.rel[k])], -1);
+                            eb.pending &= ~(1u << k);
+                        }
+                }
 #pragma unroll
                 for (int k = 0; k < kReadsPerThread; ++k) {
                     if (((b.pending >> k) & 1u) && b.rs[k] < tend_rel) {
@@ -843,18 +897,26 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                         b.pending &= ~(1u << k);
                     }
                 }
-#if MC_CHEAP_AND
-                const bool all_done = block_all(hdr + 12, and_flip, b.pending == 0, wave, lane);
-#else
-                const int all_done = __syncthreads_and(b.pending == 0);
-#endif
-                if (!all_done || !more) break;
-                base += kBatch;
-                more = base < cend;
-                if (!more) break;
-                if (!kPf) issue_raw(nxt, base, tid, pos, span);
-                finish_batch(b, nxt, base, n, C0, coff);      // loaded one batch ago
-                if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
+                bool all_done, ev_done;
+                block_all2(hdr + 12, and_flip, b.pending == 0, eb.pending == 0, wave, lane, all_done,
+                           ev_done);
+                const bool adv_reads = all_done && more;
+                const bool adv_events = ev_done && ev_more;
+                if (!adv_reads && !adv_events) break;
+                if (adv_events) {
+                    ev_base += kBatch;
+                    ev_more = ev_base < ev_hi;
+                    if (ev_more) load_events(eb, tile_ev, ev_base, ev_lo, ev_hi);
+                }
+                if (adv_reads) {
+                    base += kBatch;
+                    more = base < cend;
+                    if (more) {
+                        if (!kPf) issue_raw(nxt, base, tid, pos, span);
+                        finish_batch(b, nxt, base, n, C0, coff);      // loaded one batch ago
+                        if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
+                    }
+                }
             }
             // ---- scan tile t: each wave owns kWaveSpan contiguous positions
             const int sb = t * kTileW + wave * kWaveSpan;   // chunk-relative start of my span
@@ -947,6 +1009,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             hdr[0] = (int)next_c;
             *reinterpret_cast<long long*>(hdr + 2) = next_first;
             *reinterpret_cast<long long*>(hdr + 8) = next_end;
+            load_event_range(next_c);
         }
     }
     my_max = wave_max(my_max);
