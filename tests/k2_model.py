@@ -2,8 +2,9 @@
 depth_kernel + chunk_index_kernel + long_count/long_fill kernels), in numpy.
 
 TEST INFRASTRUCTURE: it checks the ALGORITHM (chunks of 16 tiles of 4096
-positions, an 8192-slot ring, the max-span halo, long-read end-event buckets
-and per-chunk carries) against the oracle on the CPU, so that decomposition
+positions, an 8192-slot ring, the max-span halo, long-read end events as a
+chunk-relative stream in tile order, and per-chunk carries) against the
+oracle on the CPU, so that decomposition
 bugs show up without a GPU.  Constants must match kernels.h.
 """
 import numpy as np
@@ -28,11 +29,11 @@ def model(lengths, tid, pos, span):
     gs=coff[tid]+pos; ge=gs+span
     ms=span.max() if len(span) else 0; halo=min(ms,SM)
     long_=span>SM
-    # events
+    # events: chunk-relative end positions, grouped by tile (long_fill_kernel)
     ev={}
     cdiff=np.zeros(nch+1,np.int64)
     for a,b in zip(gs[long_],ge[long_]):
-        if b<alloc and b%CW: ev.setdefault(b//W,[]).append(b-(b//W)*W)
+        if b<alloc and b%CW: ev.setdefault(b//CW,[]).append((b//W, b-(b//CW)*CW))
         c0=a//CW+1; c1=(b-1)//CW+1
         if c1>c0: cdiff[c0]+=1; cdiff[c1]-=1
     carry_c=np.cumsum(cdiff)[:nch]
@@ -42,9 +43,12 @@ def model(lengths, tid, pos, span):
         first=np.searchsorted(gs, C0-halo, 'left') & ~3
         ring=np.zeros(RING,np.int64)
         i=first; carry=carry_c[c] if long_.any() else 0
+        stream=[r for _, r in sorted(ev.get(c, []), key=lambda e: e[0])]   # tile order
+        k=0
         for t in range(TPC):
             T0=C0+t*W; Tend=T0+W
-            for o in ev.get(T0//W,[]): ring[(T0+o)&(RING-1)]-=1
+            while k<len(stream) and stream[k]<(t+1)*W:   # applied while before the tile end
+                ring[(C0+stream[k])&(RING-1)]-=1; k+=1
             while i<len(gs) and gs[i]<Tend:
                 if ge[i]-gs[i]<=SM:
                     s=max(gs[i],C0); e=ge[i]
