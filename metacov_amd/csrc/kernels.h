@@ -7,6 +7,7 @@
 //   depth_kernel         K2: LDS-ring difference array + wave prefix scan
 //   region_seg_kernel    K3a: per-segment min/max/sum/sumsq + value histogram
 //   region_final_kernel  K3b: exact order statistics from the histogram
+//   region_final_wave_kernel  K3b of the fused path: one wave per region
 //
 // Reference semantics being reproduced: htslib PileupColumn.n under pysam's
 // default "all" stepper (called at metacov/pileup.py:13) and the region
