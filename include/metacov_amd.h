@@ -69,6 +69,12 @@ typedef struct mc_timings {
     float prepare_ms;    /* ingest: sortedness check, extents, tile index */
     int64_t depth_launches;
     int64_t stats_launches;
+    /* Sums over every mc_compute_depth_stats[_device] call of this ctx (each
+     * read once its stream has drained inside the call), so a caller can
+     * average many calls without a timing query between them. */
+    double fused_depth_ms_total;   /* K2 */
+    double fused_stats_ms_total;   /* K3b (+ fallback K3) */
+    int64_t fused_calls;
 } mc_timings;
 
 typedef struct mc_ctx mc_ctx;

@@ -51,7 +51,9 @@ class ScanConfig(ctypes.Structure):
 class Timings(ctypes.Structure):
     _fields_ = [("cigar_ms", ctypes.c_float), ("depth_ms", ctypes.c_float),
                 ("stats_ms", ctypes.c_float), ("prepare_ms", ctypes.c_float),
-                ("depth_launches", ctypes.c_int64), ("stats_launches", ctypes.c_int64)]
+                ("depth_launches", ctypes.c_int64), ("stats_launches", ctypes.c_int64),
+                ("fused_depth_ms_total", ctypes.c_double), ("fused_stats_ms_total", ctypes.c_double),
+                ("fused_calls", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

@@ -947,6 +947,12 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                                        d_out, fr_idx.data()))
             return rc;
     }
+    // the stream has drained up to the flags; a fallback recorded ev[7] after
+    // its own last sync
+    if (!ft.empty()) HIP_TRY(hipEventSynchronize(ctx->ev[7]));
+    ctx->t.fused_depth_ms_total += elapsed(ctx, 4, 5);
+    ctx->t.fused_stats_ms_total += elapsed(ctx, 5, 7);
+    ctx->t.fused_calls += 1;
     return MC_OK;
 }
 
