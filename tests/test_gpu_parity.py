@@ -578,3 +578,21 @@ def test_fused_repeated_calls_reuse_and_invalidate(eng):
     eng.add_reads(tid2, pos2, span2)
     check(whole, d2, ext2, coff2)
     check(whole, d2, ext2, coff2)
+
+
+def test_fused_timing_totals(eng):
+    """mc_timings.fused_*_total: each fused call adds its K2 and K3b event
+    times (what bench.py averages over the timed steps)."""
+    lengths, tid, pos, span = make_case([60_000, 90_000], 20_000, (1, 300), 23)
+    regs = (np.arange(2, dtype=np.int32), np.zeros(2, np.int64), np.asarray(lengths, np.int64))
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+    t0 = eng.timings()
+    for _ in range(3):
+        eng.compute_depth_stats(*regs)
+    t1 = eng.timings()
+    assert t1["fused_calls"] - t0["fused_calls"] == 3
+    dk2 = t1["fused_depth_ms_total"] - t0["fused_depth_ms_total"]
+    dk3 = t1["fused_stats_ms_total"] - t0["fused_stats_ms_total"]
+    assert dk2 > 0 and dk3 > 0
+    assert dk2 >= t1["depth_ms"] * 0.99   # three launches, the last one among them
