@@ -296,7 +296,14 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
 // reads one by one (broadcast LDS reads of each read's bytes); one LDS add
 // per non-zero counter at the end.  Positions from 256 on, and batches
 // whose passing reads are in several groups, are counted per lane.
-__device__ __forceinline__ void count_bases(const ScanArgs& a, int64_t r, bool pending, bool act,
+#ifndef MC_SCAN_INC_TAB
+#define MC_SCAN_INC_TAB 1
+#endif
+typedef __attribute__((address_space(3))) const uint64_t lds_cu64;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+constexpr int kIncTabWords = 64;   // 32 u64: nibble -> packed-counter increment, forward then reverse
+
+__device__ __forceinline__ void count_bases(lds_cu64* inc_tab, const ScanArgs& a, int64_t r, bool pending, bool act,
                                             int soff, lds_u32* sseq, lds_u32* lds, int lane) {
     uint64_t pend = __ballot(pending);
     if (!pend) return;
@@ -343,13 +350,18 @@ __device__ __forceinline__ void count_bases(const ScanArgs& a, int64_t r, bool p
         const int so2 = __builtin_amdgcn_readlane(soff, l2);
         lds_cu8* s = (lds_cu8*)(sseq + so);
         lds_cu8* s2 = (lds_cu8*)(sseq + so2);
-        auto count_pos = [](lds_cu8* sp, int len, int rev, int x, uint64_t& c) {
+        auto count_pos = [inc_tab](lds_cu8* sp, int len, int rev, int x, uint64_t& c) {
             const bool ok = x < len;
             const int j = ok ? (rev ? len - 1 - x : x) : 0;
             const uint32_t byte = sp[j >> 1];
-            int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
+            const uint32_t nib = (j & 1) ? (byte & 15u) : (byte >> 4);
+#if MC_SCAN_INC_TAB
+            c += ok ? inc_tab[(rev ? 16 : 0) + nib] : 0ull;   // the packed counter's increment
+#else
+            int v = nt4_of(nib);
             if (rev) v = comp4(v);
             c += ok ? (1ull << (12 * v)) : 0ull;
+#endif
         };
         count_pos(s, rl, rv, lane, c0);
         count_pos(s2, rl2, rv2, lane, c0);
@@ -432,6 +444,13 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
     extern __shared__ uint32_t lds_[];
     lds_u32* lds = (lds_u32*)lds_;
     for (int i = threadIdx.x; i < a.lds_words; i += kThreads) lds[i] = 0;
+    // BaseHist's per-base increment of the packed counters (1 << 12 * nt4,
+    // complemented on the reverse strand), after the staging buffers
+    lds_u64* inc_tab = (lds_u64*)(lds + a.stage_off + kWaves * (kStageBytes / 4));
+    if (threadIdx.x < 32) {
+        const int v = nt4_of(threadIdx.x & 15u);
+        inc_tab[threadIdx.x] = 1ull << (12 * (threadIdx.x < 16 ? v : comp4(v)));
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     lds_u32* sseq = lds + a.stage_off + wave * (kStageBytes / 4);
@@ -520,7 +539,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
             lds_cu32* rs32 = sseq + soff;
             pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done);
         }
-        if (a.base_on) count_bases(a, r, pending, act, soff, sseq, lds, lane);
+        if (a.base_on) count_bases(inc_tab, a, r, pending, act, soff, sseq, lds, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         r0 += m;
@@ -781,7 +800,7 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
                                                                   s->grid));
     const int64_t waves = (int64_t)grid * kWaves;
     a.per_wave = (batches + waves - 1) / waves * 64;
-    const size_t lds_bytes = (size_t)a.stage_off * 4 + (size_t)kWaves * kStageBytes;
+    const size_t lds_bytes = (size_t)a.stage_off * 4 + (size_t)kWaves * kStageBytes + kIncTabWords * 4;
     hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kThreads), lds_bytes, s->stream, a);
     HIP_TRY(hipGetLastError());
     if (a.kcodes) {
