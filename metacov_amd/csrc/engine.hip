@@ -20,6 +20,11 @@
 
 using namespace mc;
 
+#ifndef MC_PLAIN_TILES_PER_CHUNK
+#define MC_PLAIN_TILES_PER_CHUNK 4
+#endif
+constexpr int kPlainTilesPerChunk = MC_PLAIN_TILES_PER_CHUNK;   // plain K2, short reads
+
 #define HIP_TRY(expr)                                                          \
     do {                                                                       \
         hipError_t e_ = (expr);                                                \
@@ -147,6 +152,10 @@ struct mc_ctx {
     int tiles_per_chunk = 16;
     int64_t chunk_w = 0, n_chunks = 0, total_len = 0;
     DevBuf<int64_t> d_chunk_first;
+    // the plain K2's chunk geometry (half-size chunks for short reads)
+    int tpc_plain = 0;
+    int64_t n_chunks_plain = 0;
+    DevBuf<int64_t> d_chunk_first_plain;
     // long-read path (spans > short_max)
     bool has_long = false;
     int short_max = 0;
@@ -250,6 +259,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_cig_off.release();
     ctx->d_cigar.release();
     ctx->d_chunk_first.release();
+    ctx->d_chunk_first_plain.release();
     ctx->d_tile_cnt.release();
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
@@ -561,6 +571,25 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     } else {
         HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * ctx->n_chunks * 8, s));
     }
+    // The plain K2 balances better on half-size chunks (C3: 0.995 -> 0.936 ms),
+    // the fused one is faster on full ones (its chunk-end flushes double):
+    // short-read batches get a second chunk index for the plain kernel.
+    // (Long reads' end-event buckets and carries are per chunk geometry, so
+    // they keep one.)
+    ctx->tpc_plain = ctx->tiles_per_chunk;
+    ctx->n_chunks_plain = ctx->n_chunks;
+    if (ctx->max_span <= ctx->short_max && ctx->tiles_per_chunk > kPlainTilesPerChunk &&
+        ((int64_t)kPlainTilesPerChunk * kTileW) % ctx->ring == 0 && n) {
+        ctx->tpc_plain = kPlainTilesPerChunk;
+        const int64_t cw = (int64_t)kPlainTilesPerChunk * kTileW;
+        ctx->n_chunks_plain = std::max<int64_t>(1, (off + cw - 1) / cw);
+        HIP_TRY(ctx->d_chunk_first_plain.reserve(2 * ctx->n_chunks_plain));
+        const int64_t nb = (ctx->n_chunks_plain + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                           ctx->d_pos.p, n, ctx->d_coff.p, cw, halo, ctx->n_chunks_plain,
+                           ctx->d_chunk_first_plain.p);
+        HIP_TRY(hipGetLastError());
+    }
     ctx->has_long = ctx->max_span > ctx->short_max;
     ctx->n_long_events = 0;
     if (ctx->has_long) {
@@ -638,8 +667,13 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const bool lng = ctx->has_long;
     const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
                             : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);
+    // the plain kernel's own chunk geometry when prepare built one (short reads)
+    const bool own_geo = !stats && ctx->tpc_plain > 0 && ctx->tpc_plain != ctx->tiles_per_chunk;
+    const int tpc = own_geo ? ctx->tpc_plain : ctx->tiles_per_chunk;
+    const int64_t nch = own_geo ? ctx->n_chunks_plain : ctx->n_chunks;
+    const int64_t* cfirst = own_geo ? ctx->d_chunk_first_plain.p : ctx->d_chunk_first.p;
     int grid = 0;
-    if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, ctx->n_chunks, &grid))
+    if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))
         return rc;
     if (!stats) {   // the fused path's fused_init_kernel zeroes them
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
@@ -652,7 +686,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
 #define MC_LAUNCH_K2(S, L)                                                                     \
     hipLaunchKernelGGL((depth_kernel<S, L>), dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,     \
                        ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,                  \
-                       ctx->d_chunk_first.p, ctx->n_chunks, ctx->tiles_per_chunk, ctx->short_max, \
+                       cfirst, nch, tpc, ctx->short_max,                                         \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr)
     if (stats) {
         if (lng) MC_LAUNCH_K2(true, true);
