@@ -169,12 +169,28 @@ def cpu_baseline_interval(lengths, tid, pos, span, sample_bases):
                       "statistics (not the reference algorithm), %.2f s" % (k, dt)}
 
 
+def kernel_source_id(root):
+    """Fingerprint of the K1/K2 sources (kernels.h + engine.hip): a PMC record
+    measured on other kernel code is stale and is not reported."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("kernels.h", "engine.hip"):
+        with open(os.path.join(root, "metacov_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_pmc_traffic(root):
+    """PMC records of profiles/pmc_depth_kernel.json measured on the current
+    kernel sources (scripts/pmc_summary.py stamps each with kernel_source_id)."""
     p = os.path.join(root, "profiles", "pmc_depth_kernel.json")
     if not os.path.exists(p):
         return None
     with open(p) as fh:
-        return json.load(fh)
+        d = json.load(fh)
+    sid = kernel_source_id(root)
+    d["variants"] = [v for v in d.get("variants", []) if v.get("source_id") == sid]
+    return d
 
 
 def main():

@@ -128,7 +128,8 @@ int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid,
                        const uint32_t* cigar);
 
 /* Same with device pointers (a batch already in HBM, e.g. torch tensors).
- * tid / pos are copied into the ctx; cig_off and cigar are BORROWED: they
+ * tid / pos are copied into the ctx before the call returns (the caller may
+ * free or overwrite them afterwards); cig_off and cigar are BORROWED: they
  * must stay valid until the next mc_prepare (K1 reads them there), so a
  * 40 GB CIGAR batch is never duplicated.  cig_off[0] must be 0. */
 int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,

@@ -95,13 +95,16 @@ def resolve_regions(bam, regions):
     """Header contig id and sorted 0-based half-open range per region, as
     cli.py:80-91 (KeyError for an unknown name, as cli.py:86)."""
     name2ref = {w.split()[0]: w for w in bam.references}
+    ref2tid = {}
+    for t, w in enumerate(bam.references):
+        ref2tid.setdefault(w, t)      # first header entry, as list.index
     tids, starts, ends = [], [], []
     for hit in regions:
         ref = name2ref[hit.sacc]
         start, end = sorted((int(hit.sstart), int(hit.send)))
         if start < 0:
             raise ValueError("region start %d < 0" % start)
-        tids.append(bam.references.index(ref))
+        tids.append(ref2tid[ref])
         starts.append(start)
         ends.append(end)
     return (np.array(tids, np.int32), np.array(starts, np.int64), np.array(ends, np.int64))
@@ -182,29 +185,15 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
     if backend == "nccl":
         torch.cuda.set_device(device)
     dist.init_process_group(backend)
+    coll_dev = torch.device("cuda", device) if backend == "nccl" else None
     try:
-        index = path + ".bai"
-        have_index = os.path.exists(index)
-        if have_index:       # header + per-contig counts from the index, no decode
-            head = BamFile(path, contigs=[])
-            reads_per, _, _ = index_stats(index, len(head.lengths))
-        else:
-            head = BamFile(path)
-            reads_per = np.bincount(head.tid, minlength=len(head.lengths))
-        regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, head))
-        tids, starts, ends = resolve_regions(head, regions)
-        shards = mdist.lpt_shard(mdist.contig_costs(head.lengths, reads_per), world)
-        owner = np.zeros(len(head.lengths), np.int64)
-        for r, sh in enumerate(shards):
-            owner[sh] = r
-        region_rank = owner[tids] if len(tids) else np.zeros(0, np.int64)
-        mine = np.nonzero(region_rank == rank)[0]
-        r_max = max(1, int(np.bincount(region_rank, minlength=world).max()) if len(tids) else 1)
-        rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
-        if len(mine):
-            bam = BamFile(path, contigs=shards[rank]) if have_index else head.restrict(shards[rank])
-            rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device)
-        coll_dev = torch.device("cuda", device) if backend == "nccl" else None
+        err = None
+        try:
+            table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device)
+        except Exception as e:   # every rank learns of it before the table gather
+            err = e
+        mdist.agree_on_error(err, device=coll_dev)
+        head, regions, tids, starts, ends, rows, mine, r_max = table_args
         table = mdist.all_gather_table(mdist.pack_rows(rows, mine), r_max, device=coll_dev)
         if rank == 0:
             log_counts(head)
@@ -213,6 +202,34 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
                       extra)
     finally:
         dist.destroy_process_group()
+
+
+def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device):
+    """This rank's part of a distributed pileup: header and regions (every
+    rank), LPT contig shards, and the rows of the regions on its contigs."""
+    from . import dist as mdist
+    index = path + ".bai"
+    have_index = os.path.exists(index)
+    if have_index:       # header + per-contig counts from the index, no decode
+        head = BamFile(path, contigs=[])
+        reads_per, _, _ = index_stats(index, len(head.lengths))
+    else:
+        head = BamFile(path)
+        reads_per = np.bincount(head.tid, minlength=len(head.lengths))
+    regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, head))
+    tids, starts, ends = resolve_regions(head, regions)
+    shards = mdist.lpt_shard(mdist.contig_costs(head.lengths, reads_per), world)
+    owner = np.zeros(len(head.lengths), np.int64)
+    for r, sh in enumerate(shards):
+        owner[sh] = r
+    region_rank = owner[tids] if len(tids) else np.zeros(0, np.int64)
+    mine = np.nonzero(region_rank == rank)[0]
+    r_max = max(1, int(np.bincount(region_rank, minlength=world).max()) if len(tids) else 1)
+    rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
+    if len(mine):
+        bam = BamFile(path, contigs=shards[rank]) if have_index else head.restrict(shards[rank])
+        rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device)
+    return head, regions, tids, starts, ends, rows, mine, r_max
 
 
 @main.command()

@@ -447,6 +447,9 @@ extern "C" int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* 
     if (n) {
         HIP_TRY(hipMemcpyAsync(ctx->d_tid.p, tid, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
         HIP_TRY(hipMemcpyAsync(ctx->d_pos.p, pos, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        // tid/pos are the caller's (often temporaries of a dtype cast): they may be freed
+        // or reused on another stream as soon as this returns, so the copies finish here.
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     ctx->cig_off_ext = cig_off;
     ctx->cigar_ext = cigar;

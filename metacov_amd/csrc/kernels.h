@@ -44,6 +44,9 @@ namespace mc {
 #ifndef MC_WAVES_STATS
 #define MC_WAVES_STATS 4               // __launch_bounds__ waves/SIMD, fused K2 (<= 128 VGPRs)
 #endif
+#ifndef MC_SP_COPY
+#define MC_SP_COPY 1                   // spans waited for at the batch advance, not in the apply loop
+#endif
 #ifndef MC_SCALAR_COFF
 #define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
 #endif
@@ -110,6 +113,22 @@ __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
     return v;
+}
+
+// Load at a wave-uniform index through the scalar cache (s_load, counted by
+// lgkmcnt).  A per-lane vector load of the same value would need a
+// vmcnt wait, which on gfx9 also waits for every store still in flight (K2's
+// depth stores).  Only for data no kernel of the launch writes.
+template <class T>
+__device__ __forceinline__ T uload(const T* p, int64_t i) {
+    return ((const __attribute__((address_space(4))) T*)(p))[i];
+}
+
+// An LDS value every lane reads alike, made wave-uniform (SGPR) for the compiler.
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
 // ----------------------------------------------------------------- ingest
@@ -534,10 +553,21 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
         const int64_t rel = g[k] - C0;
         b.rs[k] = (int)(rel < -kClamp ? -kClamp : rel > kClamp ? kClamp : rel);
     }
+    // The spans are copied into registers of their own here: used straight from
+    // the load's destination, their first use inside the apply loop carried a
+    // vmcnt(0) that ran every tile and drained the previous tile's depth stores
+    // (in-order vmcnt); here the wait runs once per batch.
+#if MC_SP_COPY
+    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[0]) : "v"(r.s.x));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[1]) : "v"(r.s.y));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[2]) : "v"(r.s.z));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[3]) : "v"(r.s.w));
+#else
     b.sp[0] = r.s.x;
     b.sp[1] = r.s.y;
     b.sp[2] = r.s.z;
     b.sp[3] = r.s.w;
+#endif
     const int64_t left = n - i0;
     b.pending = left >= 4 ? 0xfu : left <= 0 ? 0u : ((1u << left) - 1u);
 }
@@ -725,7 +755,7 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
 #ifdef MC_EXP_NO_FLUSH
     return;
 #endif
-    const int id = R.id[r];
+    const int id = uload(R.id, r);
     if (kBarriers) __syncthreads();   // every wave's histogram and overflow atomics are in
     if (threadIdx.x < kOvRecs) {
         OvLds* o = ov + threadIdx.x;
@@ -779,8 +809,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
              int* __restrict__ max_depth, FusedRegions R) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    // [0] chunk id, [2..3] first read, [4..7] wave totals, [8..9] read end, [12..13] block_all votes,
-    // [16..19] the chunk's long-read event range
+    // [0] chunk id, [4..7] wave totals, [12..13] block_all votes
     int* hdr = lds;
     int and_flip = 0;
     int* ring = lds + kLdsHeader;
@@ -799,45 +828,27 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (threadIdx.x < kOvRecs) ov_reset(ovf + threadIdx.x);   // ordered by the first barrier
     }
 
-    // chunk ids come from an atomic queue; thread 0 fetches the next id (and
-    // its chunk_first) while the current chunk is processed
-    unsigned next_c = 0;
-    int64_t next_first = 0, next_end = 0;
-    // [16..19]: the chunk's range of long-read end events
-    auto load_event_range = [&](int64_t c) {
-        if (tile_ev_off && c < n_chunks) {
-            long long* o = reinterpret_cast<long long*>(hdr + 16);
-            o[0] = tile_ev_off[c * tiles_per_chunk];
-            o[1] = tile_ev_off[(c + 1) * tiles_per_chunk];
-        }
-    };
-    if (threadIdx.x == 0) {
-        const unsigned c0 = atomicAdd(queue, 1u);
-        hdr[0] = (int)c0;
-        if (c0 < n_chunks) {
-            *reinterpret_cast<long long*>(hdr + 2) = chunk_first[2 * c0];
-            *reinterpret_cast<long long*>(hdr + 8) = chunk_first[2 * c0 + 1];
-        }
-        load_event_range(c0);
-    }
+    // chunk ids come from an atomic queue (thread 0); everything indexed by
+    // the chunk id is then loaded by every wave at a uniform index (uload)
+    if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
     for (;;) {
-        // zero the ring (also orders the hdr writes before the reads)
+        // zero the ring (also orders the hdr write before the reads)
         for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
             *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
         __syncthreads();
-        const int64_t c = hdr[0];
+        const int64_t c = (unsigned)__builtin_amdgcn_readfirstlane(hdr[0]);
         if (c >= n_chunks) break;
-        const int64_t cfirst = *reinterpret_cast<const long long*>(hdr + 2);
-        const int64_t cend = *reinterpret_cast<const long long*>(hdr + 8);   // reads of this chunk end
+        const int64_t cfirst = uload(chunk_first, 2 * c);
+        const int64_t cend = uload(chunk_first, 2 * c + 1);   // reads of this chunk end
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
         int r_base = 0;
         if (kStats) {
-            rcur = R.chunk_first[c];
+            rcur = uload(R.chunk_first, c);
             if (rcur < R.n) {
-                r_gs = R.gs[rcur];
-                r_ge = R.ge[rcur];
-                r_base = R.base[rcur];
+                r_gs = uload(R.gs, rcur);
+                r_ge = uload(R.ge, rcur);
+                r_base = uload(R.base, rcur);
             }
         }
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
@@ -852,7 +863,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             finish_batch(b, r0, base, n, C0, coff);
         }
         constexpr bool has_long = kLong;
-        int carry = has_long ? chunk_carry[c] : 0;
+        int carry = has_long ? uload(chunk_carry, c) : 0;
         // -1 end events of long reads (chunk-relative, in tile order): a
         // second stream of 1024-event batches, applied like the reads while
         // they lie before the current tile end (a dependent load chain per
@@ -861,9 +872,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         eb.pending = 0;
         int64_t ev_lo = 0, ev_hi = 0, ev_base = 0;
         bool ev_more = false;
-        if (has_long) {
-            ev_lo = *reinterpret_cast<const long long*>(hdr + 16);
-            ev_hi = *reinterpret_cast<const long long*>(hdr + 18);
+        if (has_long) {   // the chunk's range of long-read end events
+            ev_lo = uload(tile_ev_off, c * tiles_per_chunk);
+            ev_hi = uload(tile_ev_off, (c + 1) * tiles_per_chunk);
             ev_base = ev_lo & ~(int64_t)3;
             ev_more = ev_base < ev_hi;
             if (ev_more) load_events(eb, tile_ev, ev_base, ev_lo, ev_hi);
@@ -985,9 +996,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                         flush_region(R, rcur, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
-                            r_gs = R.gs[rcur];
-                            r_ge = R.ge[rcur];
-                            r_base = R.base[rcur];
+                            r_gs = uload(R.gs, rcur);
+                            r_ge = uload(R.ge, rcur);
+                            r_base = uload(R.base, rcur);
                         }
                     } else {
                         break;
@@ -1001,17 +1012,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             // barrier above and the one after the ring zeroing bracket it
             if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false>(R, rcur, hist, ovf);
         }
-        if (threadIdx.x == 0) {
-            next_c = atomicAdd(queue, 1u);
-            if (next_c < n_chunks) {
-                next_first = chunk_first[2 * next_c];
-                next_end = chunk_first[2 * next_c + 1];
-            }
-            hdr[0] = (int)next_c;
-            *reinterpret_cast<long long*>(hdr + 2) = next_first;
-            *reinterpret_cast<long long*>(hdr + 8) = next_end;
-            load_event_range(next_c);
-        }
+        if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
     }
     my_max = wave_max(my_max);
     if (lane == 0 && my_max > 0) atomicMax(max_depth, my_max);

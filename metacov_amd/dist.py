@@ -92,3 +92,24 @@ def all_gather_table(local, r_max, group=None, device=None):
     out = torch.empty((world * r_max, ROW_WIDTH), dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(out, buf, group=group)
     return out.cpu().numpy()
+
+
+class PeerRankError(RuntimeError):
+    """Raised on the ranks whose own work succeeded when another rank failed."""
+
+
+def agree_on_error(err, group=None, device=None):
+    """Collective: every rank passes the exception its local work raised (or
+    None).  If any rank failed, every rank raises — its own exception, or
+    PeerRankError — so no rank is left blocked in a later collective waiting
+    for a peer that has already given up."""
+    import torch
+    import torch.distributed as dist
+    dev = device if device is not None else torch.device("cpu")
+    flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.SUM, group=group)
+    failed = int(flag.item())
+    if err is not None:
+        raise err
+    if failed:
+        raise PeerRankError("%d rank(s) failed; see their logs" % failed)

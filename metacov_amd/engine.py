@@ -150,8 +150,9 @@ class CoverageEngine:
     def add_reads_cigar_device(self, tid, pos, cig_off, cigar):
         """Raw-CIGAR batch already in this GPU's memory (torch tensors: int32
         tid/pos, int64 cig_off with n + 1 entries starting at 0, int32/uint32
-        cigar words).  tid/pos are copied; cig_off/cigar are borrowed until
-        the next prepare() (K1 reads them there) — keep them alive."""
+        cigar words).  tid/pos (any integer dtype) are copied before this
+        returns; cig_off/cigar are borrowed until the next prepare() (K1 reads
+        them there) — this engine keeps references to them until then."""
         import torch
         tid = tid.contiguous().to(torch.int32)
         pos = pos.contiguous().to(torch.int32)

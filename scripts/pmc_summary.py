@@ -16,8 +16,11 @@ import csv
 import json
 import os
 import shutil
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_source_id  # noqa: E402
 
 
 def per_kernel(path, counter):
@@ -62,6 +65,7 @@ def main():
     for dk_name in [k for k in rows if "depth_kernel" in k or "cigar_span_kernel" in k]:
         dk = rows[dk_name]
         entry = {"tag": a.tag, "kernel": dk_name, "reads": a.reads, "contigs": a.contigs,
+                 "source_id": kernel_source_id(ROOT),
                  "hbm_bytes_per_launch": dk["hbm_bytes_per_launch"],
                  "fetch_kib": dk["FETCH_SIZE_KiB"], "write_kib": dk["WRITE_SIZE_KiB"],
                  "avg_ns": dk["avg_ns"],

@@ -1,22 +1,31 @@
 #!/bin/bash
-# rocprofv3 passes over a short bench run: kernel trace + stats, then one
-# PMC pass per TCC counter (FETCH_SIZE and WRITE_SIZE cannot share a pass).
+# rocprofv3 passes over the bench, for scripts/pmc_summary.py <TAG>:
+#   trace  --kernel-trace --stats (per-kernel average durations)
+#   fetch  --pmc FETCH_SIZE        write  --pmc WRITE_SIZE
+# (separate passes: FETCH_SIZE uses 3 TCC counters, WRITE_SIZE 2).
+# Extra bench flags in BENCH_ARGS (e.g. --unfused, --config c5).  Each pass
+# has its own time limit; the first failure ends the script.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r01}
-ARGS=${PROF_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline"}
-mkdir -p "$R/gpurun_out"
+TAG=${TAG:?set TAG}
+O=$R/gpurun_out
+mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-python3 -m metacov_amd.build >/dev/null 2>&1 || (cd "$R" && python3 -m metacov_amd.build)
-run() {   # $1 = name, rest = rocprofv3 options
-  local name=$1; shift
-  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$R/gpurun_out/prof_${TAG}_${name}" -o run \
-      -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof_${TAG}_${name}.log" 2>&1
-  local s=$?
-  tail -3 "$R/gpurun_out/prof_${TAG}_${name}.log"
-  if [ $s -ne 0 ]; then echo "step $name failed with $s"; exit $s; fi
-}
-run trace --kernel-trace --stats
-run fetch --pmc FETCH_SIZE
-run write --pmc WRITE_SIZE
+B="$R/bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_${TAG}_trace" -o run \
+    -- python3 $B > "$O/prof_${TAG}_trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$O/prof_${TAG}_trace.log"; exit 1; }
+tail -1 "$O/prof_${TAG}_trace.log"
+for c in FETCH_SIZE WRITE_SIZE; do
+  d=fetch; [ $c = WRITE_SIZE ] && d=write
+  timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$O/prof_${TAG}_$d" -o run \
+      -- python3 $B > "$O/prof_${TAG}_$d.log" 2>&1 || { echo "$c pass failed"; tail -5 "$O/prof_${TAG}_$d.log"; exit 1; }
+done
+for p in ${SQ_PASSES:-}; do   # SQ_PASSES="A B": SQ counter sets below
+  case $p in
+    A) C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY" ;;
+    B) C="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SMEM" ;;
+  esac
+  timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$O/prof_${TAG}_sq$p" -o run \
+      -- python3 $B > "$O/prof_${TAG}_sq$p.log" 2>&1 || { echo "SQ pass $p failed"; tail -5 "$O/prof_${TAG}_sq$p.log"; exit 1; }
+done
 exit 0

@@ -87,3 +87,42 @@ def test_gloo_all_gather_world2():
     for p in ps:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def _err_worker(rank, world, port, bad_rank, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        err = OSError("shard unreadable") if rank == bad_rank else None
+        try:
+            mdist.agree_on_error(err)
+            q.put((rank, "none"))
+        except mdist.PeerRankError:
+            q.put((rank, "peer"))
+        except OSError:
+            q.put((rank, "own"))
+        # everyone is still in step: a later collective completes
+        out = mdist.all_gather_table(np.zeros((0, mdist.ROW_WIDTH), np.int64), r_max=1)
+        assert out.shape == (world, mdist.ROW_WIDTH)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_error_agreement_world2():
+    """One rank's failure (cli.pileup_distributed's per-rank work) reaches
+    every rank through one all-reduce: the failing rank re-raises its own
+    error, the others raise PeerRankError, none blocks in the table gather."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    for bad in (1, None):
+        q = ctx.Queue()
+        port = _free_port()
+        ps = [ctx.Process(target=_err_worker, args=(r, 2, port, bad, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        res = sorted(q.get(timeout=120) for _ in ps)
+        for p in ps:
+            p.join(timeout=60)
+        want = [(0, "peer"), (1, "own")] if bad == 1 else [(0, "none"), (1, "none")]
+        assert res == want

@@ -517,6 +517,16 @@ def test_cigar_device_batches(lib_built):
     check_depth_vs_oracle(a, lengths, tid, pos, span)
     with pytest.raises(MetacovError):
         a.add_reads_cigar_device(t_tid, t_pos, cig_off, cigar)   # reads already present
+    # int64 tid/pos: the int32 casts are temporaries freed when the call
+    # returns; the caching allocator hands their memory straight to the
+    # scribble below, on torch's stream, so a pending copy would read garbage
+    a.clear_reads()
+    a.add_reads_cigar_device(t_tid.to(torch.int64), t_pos.to(torch.int64), cig_off, cigar)
+    scribble = torch.full((2 * len(tid),), -7, dtype=torch.int32, device=dev)
+    got = a.compute_depth_stats(rt, rs, re_)
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
+    del scribble
     a.close()
     b.close()
 
