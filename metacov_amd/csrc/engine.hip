@@ -666,7 +666,10 @@ static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t l
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistLds + kOvInts : 0)) * 4;
+#ifndef MC_EXTRA_LDS
+#define MC_EXTRA_LDS 0   // experiment knob: bytes of unused LDS per workgroup (occupancy sweeps)
+#endif
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistLds + kOvInts : 0)) * 4 + MC_EXTRA_LDS;
     const bool lng = ctx->has_long;
     const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
                             : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);

@@ -602,7 +602,11 @@ constexpr int kHistBins = MC_HIST_BINS;
 constexpr int kHistCopies = MC_HIST_COPIES;
 static_assert(kHistBins % 32 == 0 && (kHistCopies & (kHistCopies - 1)) == 0 && kHistCopies <= 32,
               "histogram bins: multiple of 32; copies: power of two");
-constexpr int kHistStride = kHistBins + (kHistCopies > 1 ? 32 / kHistCopies : 0);
+// Each copy is followed by a pad of kHistPad ints: it offsets the next copy by
+// 32 / kHistCopies banks, and holds the per-lane dummy slots the branch-free
+// histogram adds 0 into (hist_int4).
+constexpr int kHistPad = kHistCopies > 1 ? 32 / kHistCopies : 32;
+constexpr int kHistStride = kHistBins + kHistPad;
 constexpr int kHistLds = kHistCopies * kHistStride;   // ints of LDS
 
 struct FusedRegions {
@@ -676,8 +680,15 @@ __device__ __attribute__((noinline, cold)) void ov_add_lane(OvLds* ov, int v0, i
 // Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
 // one predicated LDS atomic per run of equal values, no branches except the
 // rare out-of-window path (same run arithmetic as region_seg_kernel).
-__device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1, int y2, int y3,
-                                          int base) {
+#ifndef MC_HIST_BRANCHLESS
+#define MC_HIST_BRANCHLESS 1
+#endif
+// dummy: this lane's pad slot (index into h).  MC_HIST_BRANCHLESS: every slot
+// issues its atomic, lanes with nothing to add put 0 into their own pad slot;
+// the predicated form cost ~6 SALU exec-mask instructions per atomic, and the
+// fused K2 is bound by instruction issue, not by LDS (SQ counters, r02a).
+__device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, int y0, int y1, int y2,
+                                          int y3, int base) {
     const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
     const int l2 = s3 ? 1 : 2;
     const int l1 = s2 ? 1 : l2 + 1;
@@ -689,7 +700,13 @@ __device__ __forceinline__ void hist_int4(unsigned* h, OvLds* ov, int y0, int y1
                w2 = e2 && b2 < (unsigned)kHistBins, w3 = e3 && b3 < (unsigned)kHistBins;
 #ifdef MC_EXP_NO_HIST
     asm volatile("" :: "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(l0), "v"(l1), "v"(l2));
+#elif MC_HIST_BRANCHLESS
+    atomicAdd(&h[w0 ? (int)b0 : dummy], w0 ? (unsigned)l0 : 0u);
+    atomicAdd(&h[w1 ? (int)b1 : dummy], w1 ? (unsigned)l1 : 0u);
+    atomicAdd(&h[w2 ? (int)b2 : dummy], w2 ? (unsigned)l2 : 0u);
+    atomicAdd(&h[w3 ? (int)b3 : dummy], w3 ? 1u : 0u);
 #else
+    (void)dummy;
     if (w0) atomicAdd(&h[b0], (unsigned)l0);
     if (w1) atomicAdd(&h[b1], (unsigned)l1);
     if (w2) atomicAdd(&h[b2], (unsigned)l2);
@@ -817,6 +834,8 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     OvLds* ovf = reinterpret_cast<OvLds*>(hist + kHistLds);            // kStats only
     const int lane = threadIdx.x & 63;
     unsigned* hist_lane = hist + (lane & (kHistCopies - 1)) * kHistStride;   // this lane's copy
+    // this lane's pad slot: distinct among the lanes of its copy in a half-wave
+    const int hist_dummy = kHistBins + (lane / kHistCopies) % kHistPad;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform per wave
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
@@ -990,7 +1009,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
                             y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        hist_int4(hist_lane, ovf, y0, y1, y2, y3, r_base);
+                        hist_int4(hist_lane, hist_dummy, ovf, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
                         flush_region(R, rcur, hist, ovf);

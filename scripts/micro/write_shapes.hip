@@ -41,6 +41,26 @@ __global__ void __launch_bounds__(256) chunked(i32x4* __restrict__ d, int64_t n4
     }
 }
 
+// like chunked<0, CW>, but lane L of wave w writes the 64 contiguous bytes
+// [w*4096 + 64L, +64) of the tile as 4 dwordx4 (lane stride 64 B per instruction)
+template <int CW>
+__global__ void __launch_bounds__(256) chunked_lane64(i32x4* __restrict__ d, int64_t n4, unsigned* q) {
+    __shared__ unsigned c_s;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (;;) {
+        if (threadIdx.x == 0) c_s = atomicAdd(q, 1u);
+        __syncthreads();
+        const int64_t c = c_s;
+        __syncthreads();
+        if (c * CW >= n4) break;
+        for (int t = 0; t < CW / 1024; ++t) {
+            i32x4* base = d + c * CW + t * 1024 + wave * 256 + lane * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) base[j] = i32x4{t, j, lane, 3};
+        }
+    }
+}
+
 int main() {
     const int64_t wbytes = 4020000000LL / (1 << 17) * (1 << 17);
     const int64_t n4 = wbytes / 16;
@@ -65,6 +85,11 @@ int main() {
         char nm[64];
         snprintf(nm, 64, "grid-stride plain g%d", g); run(nm, [&] { hipLaunchKernelGGL(grid_stride<0>, dim3(g), dim3(256), 0, 0, d, n4); });
         snprintf(nm, 64, "grid-stride nt g%d", g); run(nm, [&] { hipLaunchKernelGGL(grid_stride<1>, dim3(g), dim3(256), 0, 0, d, n4); });
+    }
+    for (int g : {512, 1024}) {
+        char nm[64];
+        snprintf(nm, 64, "chunk128K lane64B plain g%d", g); run(nm, [&] { hipLaunchKernelGGL((chunked_lane64<8192>), dim3(g), dim3(256), 0, 0, d, n4, q); });
+        snprintf(nm, 64, "chunk128K coalesced plain g%d", g); run(nm, [&] { hipLaunchKernelGGL((chunked<0, 8192>), dim3(g), dim3(256), 0, 0, d, n4, q); });
     }
     for (int g : {512, 1024, 2048, 4096}) {
         char nm[64];
