@@ -47,6 +47,9 @@ namespace mc {
 #ifndef MC_SP_COPY
 #define MC_SP_COPY 1                   // spans waited for at the batch advance, not in the apply loop
 #endif
+#ifndef MC_DEFER_STORE
+#define MC_DEFER_STORE 1               // a tile's depth stores wait until the next tile's reads are applied
+#endif
 #ifndef MC_SCALAR_COFF
 #define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
 #endif
@@ -840,6 +843,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
+    // deferred tile stores: not in the fused long-read variant, which is at its
+    // register budget (C5 fused +0.9 %; plain C3 -2.4 %, C5 -4.9 %, fused C3 -1.2 %)
+    constexpr bool kDefer = MC_DEFER_STORE && !(kStats && kLong);
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
     if (kStats) {
@@ -898,6 +904,18 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             ev_more = ev_base < ev_hi;
             if (ev_more) load_events(eb, tile_ev, ev_base, ev_lo, ev_hi);
         }
+        i32x4 v[kChunks];          // the scanned tile (this wave's span)
+        int64_t pend_T0 = -1;      // MC_DEFER_STORE: tile whose depth in v is not stored yet
+        auto store_tile = [&](int64_t tile0) {
+            int32_t* dst = depth + tile0 + wave * kWaveSpan + lane * 4;
+#pragma unroll
+            for (int j = 0; j < kChunks; ++j) {
+                if (MC_NT_STORE)
+                    __builtin_nontemporal_store(v[j], reinterpret_cast<i32x4*>(dst + j * 256));
+                else
+                    *reinterpret_cast<i32x4*>(dst + j * 256) = v[j];
+            }
+        };
         for (int t = 0; t < tiles_per_chunk; ++t) {
             const int64_t T0 = C0 + (int64_t)t * kTileW;
             const int64_t Tend = T0 + kTileW;
@@ -949,9 +967,15 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     }
                 }
             }
+            // the previous tile's depth, held in v since its scan: its stores go
+            // out only now, so a vmcnt wait in the apply loop above (batch
+            // advance) found them a whole tile phase old instead of just issued
+            if (kDefer && pend_T0 >= 0) {
+                store_tile(pend_T0);
+                pend_T0 = -1;
+            }
             // ---- scan tile t: each wave owns kWaveSpan contiguous positions
             const int sb = t * kTileW + wave * kWaveSpan;   // chunk-relative start of my span
-            i32x4 v[kChunks];
             int wave_total = 0;
 #pragma unroll
             for (int j = 0; j < kChunks; ++j) {
@@ -977,16 +1001,16 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 tile_total += tw;
             }
             carry += tile_total;
-            int32_t* dst = depth + T0 + wave * kWaveSpan + lane * 4;
 #pragma unroll
             for (int j = 0; j < kChunks; ++j) {
                 i32x4 x = v[j] + off;
                 v[j] = x;
                 my_max = max(my_max, max(max(x.x, x.y), max(x.z, x.w)));
-                if (MC_NT_STORE)
-                    __builtin_nontemporal_store(x, reinterpret_cast<i32x4*>(dst + j * 256));
-                else
-                    *reinterpret_cast<i32x4*>(dst + j * 256) = x;
+            }
+            if (kDefer) {
+                pend_T0 = T0;   // stored after the next tile's apply loop (or at the chunk end)
+            } else {
+                store_tile(T0);
             }
             if (kStats) {
                 // regions covering this tile, in order; the loop is uniform.
@@ -1025,6 +1049,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 }
             }
         }
+        if (kDefer && pend_T0 >= 0) store_tile(pend_T0);   // the chunk's last tile
         __syncthreads();   // everyone is past hdr / ring of this chunk (and its atomics)
         if (kStats) {
             // a region still open at the chunk end has partials here; the
