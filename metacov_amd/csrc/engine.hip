@@ -571,6 +571,11 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
                            ctx->d_pos.p, n, ctx->d_coff.p, ctx->chunk_w, halo, ctx->n_chunks,
                            ctx->d_chunk_first.p);
         HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(chunk_halo_kernel, dim3((unsigned)((ctx->n_chunks + kWaves - 1) / kWaves)),
+                           dim3(kBlock), 0, s, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n,
+                           ctx->d_coff.p, ctx->chunk_w, ctx->short_max, ctx->n_chunks,
+                           ctx->d_chunk_first.p);
+        HIP_TRY(hipGetLastError());
     } else {
         HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * ctx->n_chunks * 8, s));
     }
@@ -590,6 +595,11 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         const int64_t nb = (ctx->n_chunks_plain + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
                            ctx->d_pos.p, n, ctx->d_coff.p, cw, halo, ctx->n_chunks_plain,
+                           ctx->d_chunk_first_plain.p);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(chunk_halo_kernel, dim3((unsigned)((ctx->n_chunks_plain + kWaves - 1) / kWaves)),
+                           dim3(kBlock), 0, s, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n,
+                           ctx->d_coff.p, cw, ctx->short_max, ctx->n_chunks_plain,
                            ctx->d_chunk_first_plain.p);
         HIP_TRY(hipGetLastError());
     }

@@ -273,6 +273,37 @@ chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ 
     chunk_index[2 * c + 1] = lower_bound_gstart(tid, pos, coff, n, (c + 1) * chunk_w);
 }
 
+// Tighten chunk_index[2c] (one wave per chunk): of the reads the halo brought
+// in (gstart in [C0 - halo, C0)), only those that cross the chunk start
+// (end > C0, short reads; long reads are the carry's) contribute to the
+// chunk.  The first such read becomes the chunk's first read, or the first
+// read starting at or after C0 when none crosses.  With C3's rare 2,150-bp
+// N-spans the halo is 2,150 positions (~215 reads, 2.6 KB per chunk) where
+// ~15 reads actually cross.
+__global__ void __launch_bounds__(kBlock)
+chunk_halo_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+                  const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
+                  int64_t chunk_w, int short_max, int64_t n_chunks, int64_t* __restrict__ chunk_index) {
+    const int lane = threadIdx.x & 63;
+    const int64_t c = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6);
+    if (c >= n_chunks) return;
+    const int64_t C0 = c * chunk_w;
+    const int64_t i0 = chunk_index[2 * c];
+    int64_t first = -1;
+    for (int64_t j0 = i0; first < 0; j0 += 64) {
+        const int64_t j = j0 + lane;
+        bool stop = j >= n;   // every read before j ends at or before C0
+        if (!stop) {
+            const int64_t gs = coff[tid[j]] + pos[j];
+            const int sp = span[j];
+            stop = gs >= C0 || (sp <= short_max && gs + sp > C0);
+        }
+        const unsigned long long m = __ballot(stop);
+        if (m) first = j0 + __ffsll((long long)m) - 1;
+    }
+    if (lane == 0) chunk_index[2 * c] = first < n ? first : n;
+}
+
 // ------------------------------------------------------ long reads (prepare)
 //
 // Reads longer than `short_max` (= ring - kTileW) cannot keep their -1 end
@@ -505,18 +536,26 @@ struct RawBatch {                      // one batch of reads as loaded (int4 per
 
 // Issue the three 16-byte loads of this thread's 4 reads.  The arrays are
 // padded by one batch past n (tid padding zero-filled), so no bounds check.
+// Lanes whose 4 reads all lie at or past `cend` (the chunk's last batch runs
+// past the chunk) load nothing: those are the next chunk's reads, which
+// another workgroup, usually on another XCD, fetches again (PMC: the
+// overshoot was most of K2's 21-39 % fetch excess over 12 B/read).
 __device__ __forceinline__ void issue_raw(RawBatch& r, int64_t base,
                                           const int32_t* __restrict__ tid,
                                           const int32_t* __restrict__ pos,
-                                          const int32_t* __restrict__ span) {
+                                          const int32_t* __restrict__ span, int64_t cend) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-    r.t = *reinterpret_cast<const i32x4*>(tid + i0);
-    r.p = *reinterpret_cast<const i32x4*>(pos + i0);
-    r.s = *reinterpret_cast<const i32x4*>(span + i0);
+    if (i0 < cend) {
+        r.t = *reinterpret_cast<const i32x4*>(tid + i0);
+        r.p = *reinterpret_cast<const i32x4*>(pos + i0);
+        r.s = *reinterpret_cast<const i32x4*>(span + i0);
+    } else {
+        r.t = r.p = r.s = i32x4{0, 0, 0, 0};
+    }
 }
 
 // Chunk-relative start of the 4 reads: 4 independent coff lookups (small
-// table, cache-resident); reads past n are masked.  Starts far outside the
+// table, cache-resident); reads at or past n (the chunk's read end) are masked.  Starts far outside the
 // chunk are clamped (they are never applied: a read is applied only while
 // its start lies before the current tile end).
 __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, int64_t base,
@@ -883,9 +922,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         b.pending = 0;
         if (more) {
             RawBatch r0;
-            issue_raw(r0, base, tid, pos, span);
-            if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
-            finish_batch(b, r0, base, n, C0, coff);
+            issue_raw(r0, base, tid, pos, span, cend);
+            if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span, cend);
+            finish_batch(b, r0, base, cend, C0, coff);
         }
         constexpr bool has_long = kLong;
         int carry = has_long ? uload(chunk_carry, c) : 0;
@@ -961,9 +1000,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     base += kBatch;
                     more = base < cend;
                     if (more) {
-                        if (!kPf) issue_raw(nxt, base, tid, pos, span);
-                        finish_batch(b, nxt, base, n, C0, coff);      // loaded one batch ago
-                        if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span);
+                        if (!kPf) issue_raw(nxt, base, tid, pos, span, cend);
+                        finish_batch(b, nxt, base, cend, C0, coff);   // loaded one batch ago
+                        if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span, cend);
                     }
                 }
             }

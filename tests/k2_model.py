@@ -3,7 +3,8 @@ depth_kernel + chunk_index_kernel + long_count/long_fill kernels), in numpy.
 
 TEST INFRASTRUCTURE: it checks the ALGORITHM (chunks of 16 tiles of 4096
 positions, an 8192-slot ring, the max-span halo, long-read end events as a
-chunk-relative stream in tile order, and per-chunk carries) against the
+chunk-relative stream in tile order, per-chunk carries and the halo
+tightened to the first crossing read) against the
 oracle on the CPU, so that decomposition
 bugs show up without a GPU.  Constants must match kernels.h.
 """
@@ -40,7 +41,12 @@ def model(lengths, tid, pos, span):
     depth=np.zeros(alloc,np.int64)
     for c in range(nch):
         C0=c*CW
-        first=np.searchsorted(gs, C0-halo, 'left') & ~3
+        first=np.searchsorted(gs, C0-halo, 'left')
+        # chunk_halo_kernel: the first halo read that crosses C0 (short reads),
+        # else the first read starting at or after C0
+        while first<len(gs) and not (gs[first]>=C0 or (span[first]<=SM and ge[first]>C0)):
+            first+=1
+        first&=~3
         ring=np.zeros(RING,np.int64)
         i=first; carry=carry_c[c] if long_.any() else 0
         stream=[r for _, r in sorted(ev.get(c, []), key=lambda e: e[0])]   # tile order
