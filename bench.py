@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the contig-parallel CPU baseline (the box's CPU share)")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer ingest (H2D)")
+    ap.add_argument("--prepare-steps", type=int, default=None,
+                    help="steps of the second timed loop that re-prepares the batch every step "
+                         "(default: --steps; 0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
@@ -213,6 +216,8 @@ def main():
             dist.init_process_group("gloo")
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
 
+    if args.prepare_steps is None:
+        args.prepare_steps = args.steps
     d_reads, d_contigs, desc = CONFIGS[args.config]
     args.reads = args.reads or d_reads
     args.contigs = args.contigs or d_contigs
@@ -316,12 +321,37 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # The same steps on a fresh batch each time: every step first drops the
+    # prepared index (mc_invalidate), so it re-runs mc_prepare (ingest:
+    # validation, aligned bases, extents; the chunk index; long-read
+    # buckets) on the resident reads before K2 + K3b.  (--cigar steps
+    # already re-add and re-prepare their batch.)
+    elapsed_prep, prep_ms = None, []
+    if not args.cigar and args.prepare_steps > 0:
+        eng.invalidate()
+        step()                       # warm: the first re-prepare after the timed loop
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.prepare_steps):
+            eng.invalidate()
+            step()
+            prep_ms.append(eng.timings()["prepare_ms"])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed_prep = time.perf_counter() - t1
     t_max = elapsed
+    t_max_prep = elapsed_prep
     total_bases = bases
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([elapsed, elapsed_prep or 0.0], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
+        t_max = float(t[0].item())
+        t_max_prep = float(t[1].item()) if elapsed_prep is not None else None
         b = torch.tensor([bases], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(b)
         total_bases = int(b.item())
@@ -433,6 +463,15 @@ def main():
             "cpu_baseline_parallel": cpu_par,
             "cpu_interval_count": cpu_int,
         }
+        if t_max_prep is not None:
+            line["with_prepare"] = {
+                "value": total_bases * args.prepare_steps / t_max_prep,
+                "ms_per_step": t_max_prep / args.prepare_steps * 1e3,
+                "steps": args.prepare_steps,
+                "prepare_ms": float(np.median(prep_ms)),
+                "step": "mc_invalidate + the same step: mc_prepare (ingest, validation, extents, "
+                        "chunk index) re-runs on the resident batch before K2 + K3b",
+            }
         if pcie is not None:
             line["host_buffer_end_to_end_s"] = pcie
         print(json.dumps(line), flush=True)

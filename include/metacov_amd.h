@@ -143,6 +143,11 @@ int mc_clear_reads(mc_ctx* ctx);
  * read end) and the tile index.  Called by mc_compute_depth if needed. */
 int mc_prepare(mc_ctx* ctx);
 
+/* Drops the prepared index and depth (the reads stay): the next compute call
+ * re-runs mc_prepare over the same device reads, as for a fresh batch (what
+ * the benchmark's per-batch step times). */
+int mc_invalidate(mc_ctx* ctx);
+
 /* ---- compute ------------------------------------------------------------ */
 /* Per-position depth of every contig (K1 if needed, then K2). */
 int mc_compute_depth(mc_ctx* ctx);

@@ -82,6 +82,7 @@ SIGNATURES = {
     "mc_add_reads_cigar": [_P, _I64, _P, _P, _P, _P],
     "mc_add_reads_cigar_device": [_P, _I64, _P, _P, _P, _P],
     "mc_clear_reads": [_P],
+    "mc_invalidate": [_P],
     "mc_prepare": [_P],
     "mc_compute_depth": [_P],
     "mc_get_depth": [_P, _I32, _I64, _I64, _P],

@@ -151,11 +151,13 @@ struct mc_ctx {
     int ring = 0;                 // LDS ring ints
     int tiles_per_chunk = 16;
     int64_t chunk_w = 0, n_chunks = 0, total_len = 0;
-    DevBuf<int64_t> d_chunk_first;
-    // the plain K2's chunk geometry (half-size chunks for short reads)
+    DevBuf<int64_t> d_chunk_first;        // [2 * base chunks] (see mc_prepare)
+    DevBuf<uint64_t> d_chunk_keys;        // (tid, pos) key of each base chunk start
+    // the plain K2's chunk geometry = the index's base chunks (half-size
+    // chunks for short reads); a fused chunk is cstride base chunks
     int tpc_plain = 0;
+    int cstride = 1;
     int64_t n_chunks_plain = 0;
-    DevBuf<int64_t> d_chunk_first_plain;
     // long-read path (spans > short_max)
     bool has_long = false;
     int short_max = 0;
@@ -199,6 +201,7 @@ struct mc_ctx {
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
+    int ingest_grid = 0;                  // resident ingest workgroups
     int k2_resident[4] = {0, 0, 0, 0};    // resident K2 workgroups (plain, fused) x (short, long)
     size_t k2_resident_lds[4] = {0, 0, 0, 0};
     mc_timings t{};
@@ -259,7 +262,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_cig_off.release();
     ctx->d_cigar.release();
     ctx->d_chunk_first.release();
-    ctx->d_chunk_first_plain.release();
+    ctx->d_chunk_keys.release();
     ctx->d_tile_cnt.release();
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
@@ -459,6 +462,12 @@ extern "C" int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* 
     return MC_OK;
 }
 
+extern "C" int mc_invalidate(mc_ctx* ctx) {
+    if (int rc = ctx_use(ctx)) return rc;
+    invalidate(ctx);
+    return MC_OK;
+}
+
 extern "C" int mc_clear_reads(mc_ctx* ctx) {
     if (int rc = ctx_use(ctx)) return rc;
     ctx->n_reads = 0;
@@ -509,9 +518,19 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(ctx->d_maxend.p, 0, std::max<int32_t>(nc, 1) * sizeof(long long), s));
     if (n) {
-        const int64_t nb = std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock), 4096);
+        // one resident wave per range: a second round of waves would start
+        // its ranges only when the first finished
+        if (ctx->ingest_grid <= 0) {
+            int dev = 0, ncu = 0, per = 0;
+            HIP_TRY(hipGetDevice(&dev));
+            HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ingest_kernel, kBlock, 0));
+            ctx->ingest_grid = ncu * std::max(1, per);
+        }
+        const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
+                                                                  ctx->ingest_grid));
         hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, ctx->d_span.p, n, ctx->d_len.p, nc, ctx->d_scratch.p,
+                           ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
                            ctx->d_maxend.p, ctx->d_cbases.p);
         HIP_TRY(hipGetLastError());
     }
@@ -562,46 +581,38 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
     HIP_TRY(ctx->d_coff.reserve(nc + 1));
     HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(ctx->d_chunk_first.reserve(2 * ctx->n_chunks));
     HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
     const int64_t halo = std::min<int64_t>(ctx->max_span, ctx->short_max);
+    // One chunk index serves both K2 variants.  Its base chunks are the plain
+    // K2's: half-size (kPlainTilesPerChunk tiles) for short-read batches,
+    // where the plain kernel balances better (C3: 0.995 -> 0.936 ms), while
+    // the fused one is faster on full chunks (its chunk-end flushes double)
+    // and reads its chunk c as base chunks [c*s, c*s + s).  Long reads' end
+    // buckets and carries are per fused chunk, so with long reads both use
+    // the fused geometry.
+    int tpc_base = ctx->tiles_per_chunk;
+    if (ctx->max_span <= ctx->short_max && ctx->tiles_per_chunk > kPlainTilesPerChunk &&
+        ((int64_t)kPlainTilesPerChunk * kTileW) % ctx->ring == 0 &&
+        ctx->tiles_per_chunk % kPlainTilesPerChunk == 0)
+        tpc_base = kPlainTilesPerChunk;
+    ctx->tpc_plain = tpc_base;
+    ctx->cstride = ctx->tiles_per_chunk / tpc_base;
+    const int64_t wb = (int64_t)tpc_base * kTileW;
+    ctx->n_chunks_plain = std::max<int64_t>(1, (off + wb - 1) / wb);
+    const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every fused chunk's base chunks
+    HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
+    HIP_TRY(ctx->d_chunk_keys.reserve(n_base + 1));
     if (n) {
-        const int64_t nb = (ctx->n_chunks + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, n, ctx->d_coff.p, ctx->chunk_w, halo, ctx->n_chunks,
-                           ctx->d_chunk_first.p);
+        hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)((n_base + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, ctx->d_tid.p, ctx->d_pos.p, n, ctx->d_coff.p, nc, wb, halo, n_base,
+                           ctx->d_chunk_first.p, ctx->d_chunk_keys.p);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(chunk_halo_kernel, dim3((unsigned)((ctx->n_chunks + kWaves - 1) / kWaves)),
-                           dim3(kBlock), 0, s, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n,
-                           ctx->d_coff.p, ctx->chunk_w, ctx->short_max, ctx->n_chunks,
-                           ctx->d_chunk_first.p);
+        hipLaunchKernelGGL(chunk_halo_kernel, dim3((unsigned)((n_base + kWaves - 1) / kWaves)), dim3(kBlock),
+                           0, s, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, ctx->short_max, n_base,
+                           ctx->d_chunk_keys.p, ctx->d_chunk_first.p);
         HIP_TRY(hipGetLastError());
     } else {
-        HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * ctx->n_chunks * 8, s));
-    }
-    // The plain K2 balances better on half-size chunks (C3: 0.995 -> 0.936 ms),
-    // the fused one is faster on full ones (its chunk-end flushes double):
-    // short-read batches get a second chunk index for the plain kernel.
-    // (Long reads' end-event buckets and carries are per chunk geometry, so
-    // they keep one.)
-    ctx->tpc_plain = ctx->tiles_per_chunk;
-    ctx->n_chunks_plain = ctx->n_chunks;
-    if (ctx->max_span <= ctx->short_max && ctx->tiles_per_chunk > kPlainTilesPerChunk &&
-        ((int64_t)kPlainTilesPerChunk * kTileW) % ctx->ring == 0 && n) {
-        ctx->tpc_plain = kPlainTilesPerChunk;
-        const int64_t cw = (int64_t)kPlainTilesPerChunk * kTileW;
-        ctx->n_chunks_plain = std::max<int64_t>(1, (off + cw - 1) / cw);
-        HIP_TRY(ctx->d_chunk_first_plain.reserve(2 * ctx->n_chunks_plain));
-        const int64_t nb = (ctx->n_chunks_plain + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, n, ctx->d_coff.p, cw, halo, ctx->n_chunks_plain,
-                           ctx->d_chunk_first_plain.p);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(chunk_halo_kernel, dim3((unsigned)((ctx->n_chunks_plain + kWaves - 1) / kWaves)),
-                           dim3(kBlock), 0, s, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n,
-                           ctx->d_coff.p, cw, ctx->short_max, ctx->n_chunks_plain,
-                           ctx->d_chunk_first_plain.p);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * n_base * 8, s));
     }
     ctx->has_long = ctx->max_span > ctx->short_max;
     ctx->n_long_events = 0;
@@ -684,10 +695,10 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
                             : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);
     // the plain kernel's own chunk geometry when prepare built one (short reads)
-    const bool own_geo = !stats && ctx->tpc_plain > 0 && ctx->tpc_plain != ctx->tiles_per_chunk;
-    const int tpc = own_geo ? ctx->tpc_plain : ctx->tiles_per_chunk;
-    const int64_t nch = own_geo ? ctx->n_chunks_plain : ctx->n_chunks;
-    const int64_t* cfirst = own_geo ? ctx->d_chunk_first_plain.p : ctx->d_chunk_first.p;
+    const int tpc = stats ? ctx->tiles_per_chunk : ctx->tpc_plain;
+    const int64_t nch = stats ? ctx->n_chunks : ctx->n_chunks_plain;
+    const int cstride = stats ? ctx->cstride : 1;
+    const int64_t* cfirst = ctx->d_chunk_first.p;
     int grid = 0;
     if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))
         return rc;
@@ -702,7 +713,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
 #define MC_LAUNCH_K2(S, L)                                                                     \
     hipLaunchKernelGGL((depth_kernel<S, L>), dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,     \
                        ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,                  \
-                       cfirst, nch, tpc, ctx->short_max,                                         \
+                       cfirst, cstride, nch, tpc, ctx->short_max,                                \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr)
     if (stats) {
         if (lng) MC_LAUNCH_K2(true, true);

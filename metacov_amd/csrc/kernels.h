@@ -137,100 +137,153 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 // ----------------------------------------------------------------- ingest
 
 // out[0] = invalid records, out[1] = order violations, out[2] = aligned
-// bases, out[3] = max span.  maxend[t] = furthest read end past len[t].
+// bases, out[3] = max span.  maxend[t] = furthest read end of contig t
+// (the host takes max(len, maxend) as the extent); cbases[t] = aligned
+// bases of contig t.
+//
 // Each wave owns a contiguous range of int4 read groups (the arrays are
-// padded past n), so its per-contig aligned bases accumulate in registers
-// while the wave's reads stay on one contig and are reduced only when the
-// contig changes.
-__device__ __forceinline__ void flush_cbases(unsigned long long* cbases, long long& acc, int& cur_t,
-                                             int lane) {
-    if (cur_t >= 0) {
-        const long long w = wave_sum64(acc);
-        if (lane == 0 && w) atomicAdd(&cbases[cur_t], (unsigned long long)w);
+// padded past n) and walks it kIngestU groups per lane at a time (lane L,
+// slot u: group gb + 64u + L, so every load instruction is 1 KiB
+// contiguous), the next step's 3 x kIngestU loads in flight while the
+// current one is checked.  Nothing is loaded that depends on a load: the
+// predecessor of a group's first read comes from the neighbouring lane (or
+// the previous slot / step), and per-contig sums and ends accumulate in
+// wave-uniform registers while the wave stays on one contig, one atomic each
+// when it moves on.  (The first version gathered len[tid] per read and
+// re-loaded each group's predecessor: 0.57 ms per 100 M reads, 2.1 TB/s.)
+constexpr int kIngestU = 2;
+
+struct IngestAcc {                     // running record of contig cur (wave-uniform)
+    int cur = -1;
+    long long bases = 0, end = 0;      // per lane, reduced at the flush
+};
+
+// every lane calls it (cur is uniform)
+__device__ __forceinline__ void ingest_flush(IngestAcc& a, unsigned long long* cbases,
+                                             long long* maxend, int lane) {
+    if (a.cur >= 0) {
+        const long long b = wave_sum64(a.bases);
+        long long e = a.end;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) e = max(e, (long long)__shfl_xor(e, d, 64));
+        if (lane == 0) {
+            if (b) atomicAdd(&cbases[a.cur], (unsigned long long)b);
+            atomicMax(&maxend[a.cur], e);
+        }
     }
-    acc = 0;
-    cur_t = -1;
+    a.bases = a.end = 0;
 }
 
 __global__ void __launch_bounds__(kBlock)
 ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-              const int32_t* __restrict__ span, int64_t n,
-              const int64_t* __restrict__ len, int32_t n_contigs,
+              const int32_t* __restrict__ span, int64_t n, int32_t n_contigs,
               unsigned long long* __restrict__ out, long long* __restrict__ maxend,
               unsigned long long* __restrict__ cbases) {
+    constexpr int U = kIngestU;
     const int lane = threadIdx.x & 63;
     const int64_t n4 = (n + 3) / 4;
     const int64_t n_waves = (int64_t)gridDim.x * kWaves;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-    const int64_t per = (n4 + n_waves - 1) / n_waves;
+    const int64_t per = ((n4 + n_waves - 1) / n_waves + 63) & ~(int64_t)63;
     const int64_t g0 = gw * per, g1 = min(n4, g0 + per);
     long long bad = 0, unsorted = 0, bases = 0;
     int mspan = 0;
-    long long acc = 0;   // aligned bases of contig cur_t (wave-uniform) not yet added
-    int cur_t = -1;
-    for (int64_t gb = g0; gb < g1; gb += 64) {
-        const int64_t q = gb + lane;
-        const bool mine = q < g1;
-        const int64_t i0 = q * 4;
-        i32x4 t4 = {0, 0, 0, 0}, p4 = {0, 0, 0, 0}, s4 = {0, 0, 0, 0};
-        int tp = -1, pp = 0;
-        if (mine) {
-            t4 = *reinterpret_cast<const i32x4*>(tid + i0);
-            p4 = *reinterpret_cast<const i32x4*>(pos + i0);
-            s4 = *reinterpret_cast<const i32x4*>(span + i0);
-            if (i0 > 0) {
-                tp = tid[i0 - 1];
-                pp = pos[i0 - 1];
-            }
-        }
-        const int tt[4] = {t4.x, t4.y, t4.z, t4.w};
-        const int ps[4] = {p4.x, p4.y, p4.z, p4.w};
-        const int ss[4] = {s4.x, s4.y, s4.z, s4.w};
-        long long my_bases = 0, my_end = 0;   // my_end: furthest end past its contig
-        bool same = true;
-        const int t0 = __builtin_amdgcn_readfirstlane(t4.x);   // lane 0 always holds a read
+    IngestAcc acc;
+    // the read before the wave's range (every wave checks its first read too)
+    int carry_t = -1, carry_p = 0;
+    if (g0 < g1 && g0 > 0) {
+        carry_t = uload(tid, g0 * 4 - 1);
+        carry_p = uload(pos, g0 * 4 - 1);
+    }
+    i32x4 ct[U], cp[U], cs[U], nt[U], np[U], ns[U];
+#define MC_INGEST_LOAD(T, P, S, GB)                                                  \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                  \
+        const int64_t q_ = (GB) + 64 * u + lane;                                     \
+        const bool in_ = q_ < g1;                                                    \
+        const int64_t o_ = in_ ? q_ * 4 : 0;                                         \
+        T[u] = *reinterpret_cast<const i32x4*>(tid + o_);                            \
+        P[u] = *reinterpret_cast<const i32x4*>(pos + o_);                            \
+        S[u] = *reinterpret_cast<const i32x4*>(span + o_);                           \
+    }
+    constexpr int64_t kStep = 64 * U;
+    if (g0 < g1) { MC_INGEST_LOAD(ct, cp, cs, g0) }
+    for (int64_t gb = g0; gb < g1; gb += kStep) {
+        if (gb + kStep < g1) { MC_INGEST_LOAD(nt, np, ns, gb + kStep) }
+        int tt[4 * U], ps[4 * U], ss[4 * U], tprev[U], pprev[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool live = mine && i0 + k < n;
-            if (!live) continue;
-            const int t = tt[k], p = ps[k], sp = ss[k];
-            same &= t == t0;
-            if (t < 0 || t >= n_contigs || p < 0 || sp < 0) {
-                ++bad;
-            } else {
-                if (tp > t || (tp == t && pp > p)) ++unsorted;
-                bases += sp;
-                mspan = max(mspan, sp);
-                my_bases += sp;
-                const long long e = (long long)p + sp;
-                if (e > len[t]) my_end = max(my_end, e);
-            }
-            tp = t;
-            pp = p;
+        for (int u = 0; u < U; ++u) {
+            tt[4 * u] = ct[u].x; tt[4 * u + 1] = ct[u].y; tt[4 * u + 2] = ct[u].z; tt[4 * u + 3] = ct[u].w;
+            ps[4 * u] = cp[u].x; ps[4 * u + 1] = cp[u].y; ps[4 * u + 2] = cp[u].z; ps[4 * u + 3] = cp[u].w;
+            ss[4 * u] = cs[u].x; ss[4 * u + 1] = cs[u].y; ss[4 * u + 2] = cs[u].z; ss[4 * u + 3] = cs[u].w;
+            // predecessor of this group's first read: lane L-1's last read; lane 0
+            // takes the previous slot's lane 63 (or the previous step's)
+            const int up_t = __shfl_up(ct[u].w, 1, 64), up_p = __shfl_up(cp[u].w, 1, 64);
+            const int l0_t = u ? __builtin_amdgcn_readlane(ct[u - 1].w, 63) : carry_t;
+            const int l0_p = u ? __builtin_amdgcn_readlane(cp[u - 1].w, 63) : carry_p;
+            tprev[u] = lane ? up_t : l0_t;
+            pprev[u] = lane ? up_p : l0_p;
         }
-        if (__all(same) && t0 >= 0 && t0 < n_contigs) {
-            if (t0 != cur_t) {
-                flush_cbases(cbases, acc, cur_t, lane);
-                cur_t = t0;
-            }
-            acc += my_bases;
-            if (__any(my_end > 0)) {               // one atomic per wave for the overhangs
+        carry_t = __builtin_amdgcn_readlane(ct[U - 1].w, 63);
+        carry_p = __builtin_amdgcn_readlane(cp[U - 1].w, 63);
+        unsigned todo = 0;   // bit 4u+k: valid live read
 #pragma unroll
-                for (int d = 32; d > 0; d >>= 1) my_end = max(my_end, (long long)__shfl_xor(my_end, d, 64));
-                if (lane == 0) atomicMax(&maxend[t0], my_end);
-            }
-        } else {                                   // a contig boundary inside the wave
-            flush_cbases(cbases, acc, cur_t, lane);
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = gb + 64 * u + lane;
+            int tp = tprev[u], pp = pprev[u];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const bool live = mine && i0 + k < n && tt[k] >= 0 && tt[k] < n_contigs;
-                if (live && ss[k] > 0) atomicAdd(&cbases[tt[k]], (unsigned long long)ss[k]);
-                if (live && ps[k] >= 0 && ss[k] >= 0 && (long long)ps[k] + ss[k] > len[tt[k]])
-                    atomicMax(&maxend[tt[k]], (long long)ps[k] + ss[k]);
+                const int j = 4 * u + k;
+                const bool live = q < g1 && q * 4 + k < n;
+                if (!live) continue;
+                const int t = tt[j], p = ps[j], sp = ss[j];
+                if (t < 0 || t >= n_contigs || p < 0 || sp < 0) {
+                    ++bad;
+                } else {
+                    if (tp > t || (tp == t && pp > p)) ++unsorted;
+                    todo |= 1u << j;
+                }
+                tp = t;
+                pp = p;
             }
         }
+        // per contig of this step (one, unless the wave crosses a boundary):
+        // wave sums of bases / max end / max span, added to the running record
+        for (;;) {
+            int cand = -1;
+#pragma unroll
+            for (int j = 4 * U - 1; j >= 0; --j)
+                if ((todo >> j) & 1u) cand = tt[j];
+            const unsigned long long act = __ballot(cand >= 0);
+            if (!act) break;
+            const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
+            long long b = 0, e = 0;
+            int m = 0;
+#pragma unroll
+            for (int j = 0; j < 4 * U; ++j)
+                if (((todo >> j) & 1u) && tt[j] == t0) {
+                    b += ss[j];
+                    e = max(e, (long long)ps[j] + ss[j]);
+                    m = max(m, ss[j]);
+                    todo &= ~(1u << j);
+                }
+            mspan = max(mspan, m);
+            bases += b;
+            if (t0 != acc.cur) {
+                ingest_flush(acc, cbases, maxend, lane);
+                acc.cur = t0;
+            }
+            acc.bases += b;
+            acc.end = max(acc.end, e);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ct[u] = nt[u];
+            cp[u] = np[u];
+            cs[u] = ns[u];
+        }
     }
-    flush_cbases(cbases, acc, cur_t, lane);
+#undef MC_INGEST_LOAD
+    ingest_flush(acc, cbases, maxend, lane);
     bad = wave_sum64(bad);
     unsorted = wave_sum64(unsorted);
     bases = wave_sum64(bases);
@@ -243,65 +296,105 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     }
 }
 
-__device__ __forceinline__ int64_t gstart_of(const int32_t* tid, const int32_t* pos,
-                                             const int64_t* coff, int64_t i) {
-    return coff[tid[i]] + pos[i];
-}
+// The chunk index (prepare): for base chunk k of width w (the plain K2's
+// chunk; the fused K2's chunks are `s` consecutive base chunks),
+//   chunk_index[2k]   = first read K2 has to load for the chunk: of the reads
+//                       starting in [k*w - halo, k*w), the first that crosses
+//                       k*w (a short read; long reads are the carry's), else the
+//                       first read starting at or after k*w
+//   chunk_index[2k+1] = first read starting at or after (k+1)*w
+// Searches run in (tid, pos) key space: a global position X maps to the key
+// (t, X - coff[t]) of the contig whose range holds it, and read i lies before
+// X exactly when its key is lexicographically smaller (reads are clipped to
+// their contig's extent, coff is increasing).  A probe then needs tid[i] and
+// pos[i] side by side, not the dependent coff[tid[i]] a global start needs.
+struct PosKey {
+    int t;
+    int64_t l;
+};
 
-__device__ __forceinline__ int64_t lower_bound_gstart(const int32_t* tid, const int32_t* pos,
-                                                     const int64_t* coff, int64_t n,
-                                                     int64_t target) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = lo + ((hi - lo) >> 1);
-        if (gstart_of(tid, pos, coff, mid) < target) lo = mid + 1;
+// key of global position X (X <= 0: the smallest key; X >= coff[nc]: past all reads)
+__device__ __forceinline__ PosKey pos_key(const int64_t* __restrict__ coff, int nc, int64_t X) {
+    if (X <= 0) return PosKey{0, 0};
+    int lo = 0, hi = nc;                       // last t with coff[t] <= X
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (coff[mid] <= X) lo = mid;
         else hi = mid;
     }
-    return lo;
+    if (X >= coff[nc]) return PosKey{nc, 0};
+    return PosKey{lo, X - coff[lo]};
 }
 
-// chunk_index[2c]   = first read i with gstart(i) >= c * chunk_w - halo
-// chunk_index[2c+1] = first read i with gstart(i) >= (c + 1) * chunk_w
-// (the reads K2 has to load for chunk c: no batch is fetched past the end)
+__device__ __forceinline__ bool key_before(int t, int p, const PosKey& k) {
+    return t < k.t || (t == k.t && (int64_t)p < k.l);
+}
+
+// One thread per base chunk: lower bounds of both targets in lockstep (the
+// probes of the two searches go out together: one memory round trip per
+// level).  key_out[k+1] = the key of (k+1)*w, packed (t << 32 | l clamped to
+// 32 bits: a larger l only makes the halo scan stop early), for the halo scan.
 __global__ void __launch_bounds__(kBlock)
-chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                   int64_t n, const int64_t* __restrict__ coff, int64_t chunk_w,
-                   int64_t halo, int64_t n_chunks, int64_t* __restrict__ chunk_index) {
-    const int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-    if (c >= n_chunks) return;
-    chunk_index[2 * c] = lower_bound_gstart(tid, pos, coff, n, c * chunk_w - halo);
-    chunk_index[2 * c + 1] = lower_bound_gstart(tid, pos, coff, n, (c + 1) * chunk_w);
+chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos, int64_t n,
+                   const int64_t* __restrict__ coff, int nc, int64_t w, int64_t halo,
+                   int64_t n_chunks, int64_t* __restrict__ chunk_index,
+                   uint64_t* __restrict__ key_out) {
+    const int64_t k = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (k >= n_chunks) return;
+    const PosKey ka = pos_key(coff, nc, k * w - halo), kb = pos_key(coff, nc, (k + 1) * w);
+    int64_t la = 0, ha = n, lb = 0, hb = n;
+    while (la < ha || lb < hb) {
+        const int64_t ma = la + ((ha - la) >> 1), mb = lb + ((hb - lb) >> 1);
+        const bool ga = la < ha, gb = lb < hb;
+        const int ta = ga ? tid[ma] : 0, pa = ga ? pos[ma] : 0;
+        const int tb = gb ? tid[mb] : 0, pb = gb ? pos[mb] : 0;
+        if (ga) {
+            if (key_before(ta, pa, ka)) la = ma + 1;
+            else ha = ma;
+        }
+        if (gb) {
+            if (key_before(tb, pb, kb)) lb = mb + 1;
+            else hb = mb;
+        }
+    }
+    chunk_index[2 * k] = la;
+    chunk_index[2 * k + 1] = lb;
+    const uint64_t lc = kb.l > 0xffffffffll ? 0xffffffffull : (uint64_t)kb.l;
+    key_out[k + 1] = ((uint64_t)(uint32_t)kb.t << 32) | lc;
+    if (k == 0) key_out[0] = 0;
 }
 
-// Tighten chunk_index[2c] (one wave per chunk): of the reads the halo brought
-// in (gstart in [C0 - halo, C0)), only those that cross the chunk start
-// (end > C0, short reads; long reads are the carry's) contribute to the
-// chunk.  The first such read becomes the chunk's first read, or the first
-// read starting at or after C0 when none crosses.  With C3's rare 2,150-bp
-// N-spans the halo is 2,150 positions (~215 reads, 2.6 KB per chunk) where
-// ~15 reads actually cross.
+// Tighten chunk_index[2k] (one wave per base chunk): of the reads the halo
+// brought in, only those that cross the chunk start C0 = k*w contribute; the
+// first of them becomes the chunk's first read, or chunk_index[2k-1] (the
+// first read starting at C0) when none crosses.  A read crosses C0 only on
+// C0's contig (t, l): pos + span > l.  With C3's rare 2,150-bp N-spans the
+// halo is 2,150 positions (~215 reads, 2.6 KB per chunk) where ~15 reads
+// actually cross.
 __global__ void __launch_bounds__(kBlock)
 chunk_halo_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                  const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
-                  int64_t chunk_w, int short_max, int64_t n_chunks, int64_t* __restrict__ chunk_index) {
+                  const int32_t* __restrict__ span, int short_max, int64_t n_chunks,
+                  const uint64_t* __restrict__ keys, int64_t* __restrict__ chunk_index) {
     const int lane = threadIdx.x & 63;
-    const int64_t c = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;
-    const int64_t C0 = c * chunk_w;
-    const int64_t i0 = chunk_index[2 * c];
+    const int64_t k = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6);
+    if (k >= n_chunks || k == 0) return;      // chunk 0 starts at read 0
+    const int64_t i0 = chunk_index[2 * k];
+    const int64_t bound = chunk_index[2 * k - 1];
+    const uint64_t key = keys[k];
+    const int tc = (int)(key >> 32);
+    const int64_t lc = (int64_t)(key & 0xffffffffull);
     int64_t first = -1;
     for (int64_t j0 = i0; first < 0; j0 += 64) {
         const int64_t j = j0 + lane;
-        bool stop = j >= n;   // every read before j ends at or before C0
+        bool stop = j >= bound;               // every read before j ends at or before C0
         if (!stop) {
-            const int64_t gs = coff[tid[j]] + pos[j];
-            const int sp = span[j];
-            stop = gs >= C0 || (sp <= short_max && gs + sp > C0);
+            const int t = tid[j], p = pos[j], sp = span[j];
+            stop = sp <= short_max && t == tc && (int64_t)p + sp > lc;
         }
         const unsigned long long m = __ballot(stop);
         if (m) first = j0 + __ffsll((long long)m) - 1;
     }
-    if (lane == 0) chunk_index[2 * c] = first < n ? first : n;
+    if (lane == 0) chunk_index[2 * k] = first < bound ? first : bound;
 }
 
 // ------------------------------------------------------ long reads (prepare)
@@ -862,7 +955,7 @@ __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_ST
 depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
              const int32_t* __restrict__ span, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
-             int64_t n_chunks, int tiles_per_chunk, int short_max,
+             int cstride, int64_t n_chunks, int tiles_per_chunk, int short_max,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
              const int* __restrict__ chunk_carry,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
@@ -902,8 +995,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         __syncthreads();
         const int64_t c = (unsigned)__builtin_amdgcn_readfirstlane(hdr[0]);
         if (c >= n_chunks) break;
-        const int64_t cfirst = uload(chunk_first, 2 * c);
-        const int64_t cend = uload(chunk_first, 2 * c + 1);   // reads of this chunk end
+        // chunk c = base chunks [c * cstride, (c + 1) * cstride) of the index
+        const int64_t cfirst = uload(chunk_first, 2 * c * cstride);
+        const int64_t cend = uload(chunk_first, 2 * (c + 1) * cstride - 1);   // reads of this chunk end
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
         int r_base = 0;

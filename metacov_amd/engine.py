@@ -176,6 +176,11 @@ class CoverageEngine:
     def prepare(self):
         self._check(self._lib.mc_prepare(self._h))
 
+    def invalidate(self):
+        """Drop the prepared index: the next compute call re-prepares the
+        same device reads, as for a fresh batch."""
+        self._check(self._lib.mc_invalidate(self._h))
+
     # -- compute
     def compute_depth(self):
         self._check(self._lib.mc_compute_depth(self._h))
