@@ -240,7 +240,7 @@ extern "C" int mc_ctx_create(int device, mc_ctx** out) {
     }
     c->own_stream = true;
     for (auto& ev : c->ev) (void)hipEventCreate(&ev);
-    if (c->d_scratch.reserve(8) != hipSuccess || c->d_queue.reserve(4) != hipSuccess ||
+    if (c->d_scratch.reserve(8) != hipSuccess || c->d_queue.reserve(8) != hipSuccess ||
         c->d_maxdepth.reserve(4) != hipSuccess) {
         mc_ctx_destroy(c);
         mc::set_error("hipMalloc of ctx scratch failed");
@@ -703,7 +703,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))
         return rc;
     if (!stats) {   // the fused path's fused_init_kernel zeroes them
-        HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 16, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 32, s));
         HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
     }
     HIP_TRY(hipEventRecord(ctx->ev[4], s));

@@ -50,6 +50,22 @@ namespace mc {
 #ifndef MC_DEFER_STORE
 #define MC_DEFER_STORE 1               // a tile's depth stores wait until the next tile's reads are applied
 #endif
+#ifndef MC_QUEUE_AHEAD
+// K2: reserve the next chunk at the start of the current one (in-process A/B:
+// C3 plain +6.7 %, fused +3.0 %, C5 plain +3.5 %, C5 fused -3.6 %): only the
+// fused long-read variant does
+#define MC_QUEUE_AHEAD 0
+#endif
+#ifndef MC_QUEUE_AHEAD_FUSED_LONG
+#define MC_QUEUE_AHEAD_FUSED_LONG 1
+#endif
+#ifndef MC_XCD_QUEUES
+// K2: 8 chunk queues over contiguous chunk ranges, one per blockIdx % 8 group
+// (an XCD), stealing when empty.  In-process A/B: C3 plain +0.8 %, fused
+// +2.0 %, C5 fused +1.0 % (K2's HBM traffic is within 5 % of its algorithmic
+// bytes, so there is little L2 reuse to win, and one queue is not the limit)
+#define MC_XCD_QUEUES 0
+#endif
 #ifndef MC_SCALAR_COFF
 #define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
 #endif
@@ -151,7 +167,13 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 // wave-uniform registers while the wave stays on one contig, one atomic each
 // when it moves on.  (The first version gathered len[tid] per read and
 // re-loaded each group's predecessor: 0.57 ms per 100 M reads, 2.1 TB/s.)
-constexpr int kIngestU = 2;
+#ifndef MC_INGEST_U
+#define MC_INGEST_U 4                  // sweep (C3 prepare): 1 0.544, 2 0.507, 4 0.480 ms
+#endif
+#ifndef MC_INGEST_STRIDE
+#define MC_INGEST_STRIDE 0             // 1: steps of all waves side by side (grid stride)
+#endif
+constexpr int kIngestU = MC_INGEST_U;
 
 struct IngestAcc {                     // running record of contig cur (wave-uniform)
     int cur = -1;
@@ -184,13 +206,18 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     const int64_t n4 = (n + 3) / 4;
     const int64_t n_waves = (int64_t)gridDim.x * kWaves;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-    const int64_t per = ((n4 + n_waves - 1) / n_waves + 63) & ~(int64_t)63;
-    const int64_t g0 = gw * per, g1 = min(n4, g0 + per);
+    constexpr int64_t kStep = 64 * U;
+#if MC_INGEST_STRIDE
+    const int64_t g0 = gw * kStep, g1 = n4, gstride = n_waves * kStep;
+#else
+    const int64_t per = ((n4 + n_waves - 1) / n_waves + kStep - 1) / kStep * kStep;
+    const int64_t g0 = gw * per, g1 = min(n4, g0 + per), gstride = kStep;
+#endif
     long long bad = 0, unsorted = 0, bases = 0;
     int mspan = 0;
     IngestAcc acc;
     // the read before the wave's range (every wave checks its first read too)
-    int carry_t = -1, carry_p = 0;
+    int carry_t = -1, carry_p = 0, ncarry_t = -1, ncarry_p = 0;
     if (g0 < g1 && g0 > 0) {
         carry_t = uload(tid, g0 * 4 - 1);
         carry_p = uload(pos, g0 * 4 - 1);
@@ -205,10 +232,15 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         P[u] = *reinterpret_cast<const i32x4*>(pos + o_);                            \
         S[u] = *reinterpret_cast<const i32x4*>(span + o_);                           \
     }
-    constexpr int64_t kStep = 64 * U;
     if (g0 < g1) { MC_INGEST_LOAD(ct, cp, cs, g0) }
-    for (int64_t gb = g0; gb < g1; gb += kStep) {
-        if (gb + kStep < g1) { MC_INGEST_LOAD(nt, np, ns, gb + kStep) }
+    for (int64_t gb = g0; gb < g1; gb += gstride) {
+        if (gb + gstride < g1) {
+            MC_INGEST_LOAD(nt, np, ns, gb + gstride)
+            if (MC_INGEST_STRIDE) {
+                ncarry_t = uload(tid, (gb + gstride) * 4 - 1);
+                ncarry_p = uload(pos, (gb + gstride) * 4 - 1);
+            }
+        }
         int tt[4 * U], ps[4 * U], ss[4 * U], tprev[U], pprev[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -223,8 +255,13 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             tprev[u] = lane ? up_t : l0_t;
             pprev[u] = lane ? up_p : l0_p;
         }
-        carry_t = __builtin_amdgcn_readlane(ct[U - 1].w, 63);
-        carry_p = __builtin_amdgcn_readlane(cp[U - 1].w, 63);
+        if (MC_INGEST_STRIDE) {
+            carry_t = ncarry_t;
+            carry_p = ncarry_p;
+        } else {
+            carry_t = __builtin_amdgcn_readlane(ct[U - 1].w, 63);
+            carry_p = __builtin_amdgcn_readlane(cp[U - 1].w, 63);
+        }
         unsigned todo = 0;   // bit 4u+k: valid live read
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -284,15 +321,28 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     }
 #undef MC_INGEST_LOAD
     ingest_flush(acc, cbases, maxend, lane);
+    // one atomic per workgroup and counter: same-address atomics from every
+    // wave of the grid serialise at the end of the launch
+    __shared__ long long red[4][kWaves];
+    const int wave = threadIdx.x >> 6;
     bad = wave_sum64(bad);
     unsorted = wave_sum64(unsorted);
     bases = wave_sum64(bases);
     mspan = wave_max(mspan);
     if (lane == 0) {
-        if (bad) atomicAdd(&out[0], (unsigned long long)bad);
-        if (unsorted) atomicAdd(&out[1], (unsigned long long)unsorted);
-        if (bases) atomicAdd(&out[2], (unsigned long long)bases);
-        atomicMax(&out[3], (unsigned long long)mspan);
+        red[0][wave] = bad;
+        red[1][wave] = unsorted;
+        red[2][wave] = bases;
+        red[3][wave] = mspan;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        long long v = red[threadIdx.x][0];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w)
+            v = threadIdx.x == 3 ? max(v, red[3][w]) : v + red[threadIdx.x][w];
+        if (threadIdx.x == 3) atomicMax(&out[3], (unsigned long long)v);
+        else if (v) atomicAdd(&out[threadIdx.x], (unsigned long long)v);
     }
 }
 
@@ -936,6 +986,30 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
     if (kBarriers) __syncthreads();
 }
 
+// K2's chunk queue (thread 0).  MC_XCD_QUEUES: queue q hands out the chunks
+// [n * q / 8, n * (q + 1) / 8); workgroup b starts on queue b % 8 (the blocks
+// the dispatcher places on one XCD, so neighbouring chunks, which share read
+// cache lines, meet in one L2; 8 counters instead of one contended address)
+// and moves on to the next queue when its own is empty.  Placement only
+// changes speed: every chunk is taken exactly once either way.
+__device__ __forceinline__ int take_chunk(unsigned* queue, int64_t n_chunks, int& qk) {
+#if MC_XCD_QUEUES
+    const int xq = blockIdx.x & 7;
+    while (qk < 8) {
+        const int q = (xq + qk) & 7;
+        const int64_t lo = n_chunks * q / 8, hi = n_chunks * (q + 1) / 8;
+        const unsigned t = atomicAdd(&queue[q], 1u);
+        if (lo + (int64_t)t < hi) return (int)(lo + t);
+        ++qk;
+    }
+    return (int)n_chunks;
+#else
+    (void)qk;
+    const unsigned t = atomicAdd(queue, 1u);
+    return t < (unsigned)n_chunks ? (int)t : (int)n_chunks;
+#endif
+}
+
 // One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
 // (dynamic queue).  Per chunk: the reads from chunk_first[c] (which already
 // includes the max-span halo) are applied as +1 at max(start, chunk start)
@@ -987,7 +1061,13 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 
     // chunk ids come from an atomic queue (thread 0); everything indexed by
     // the chunk id is then loaded by every wave at a uniform index (uload)
-    if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
+    // kAhead: the next chunk is reserved at the start of the current one,
+    // together with its first read batch, so the queue atomic's round trip
+    // overlaps that load instead of following the chunk's end (the WG then
+    // holds a chunk others cannot take: the tail balances worse).
+    constexpr bool kAhead = MC_QUEUE_AHEAD || (MC_QUEUE_AHEAD_FUSED_LONG && kStats && kLong);
+    int ticket = 0, qk = 0;
+    if (threadIdx.x == 0) hdr[0] = take_chunk(queue, n_chunks, qk);
     for (;;) {
         // zero the ring (also orders the hdr write before the reads)
         for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
@@ -995,6 +1075,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         __syncthreads();
         const int64_t c = (unsigned)__builtin_amdgcn_readfirstlane(hdr[0]);
         if (c >= n_chunks) break;
+        if (kAhead && threadIdx.x == 0) ticket = take_chunk(queue, n_chunks, qk);
         // chunk c = base chunks [c * cstride, (c + 1) * cstride) of the index
         const int64_t cfirst = uload(chunk_first, 2 * c * cstride);
         const int64_t cend = uload(chunk_first, 2 * (c + 1) * cstride - 1);   // reads of this chunk end
@@ -1189,10 +1270,17 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             // barrier above and the one after the ring zeroing bracket it
             if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false>(R, rcur, hist, ovf);
         }
-        if (threadIdx.x == 0) hdr[0] = (int)atomicAdd(queue, 1u);
+        if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks, qk);
     }
+    // one atomic per workgroup (same-address atomics of every wave at the end of
+    // the launch serialise); hdr[8..11] are free once the queue is drained
     my_max = wave_max(my_max);
-    if (lane == 0 && my_max > 0) atomicMax(max_depth, my_max);
+    if (lane == 0) hdr[8 + wave] = my_max;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int m = max(max(hdr[8], hdr[9]), max(hdr[10], hdr[11]));
+        if (m > 0) atomicMax(max_depth, m);
+    }
 }
 
 // ----------------------------------------------------------------- K3
@@ -1206,9 +1294,9 @@ fused_init_kernel(unsigned* __restrict__ hist, int64_t hist_words, unsigned* __r
                   RegionAcc* __restrict__ acc, int64_t R, const int64_t* __restrict__ fge,
                   int64_t nf, int64_t chunk_w, int64_t n_chunks, int64_t* __restrict__ chunk_first,
                   unsigned* __restrict__ queue, int* __restrict__ max_depth) {
-    if (blockIdx.x == 0 && threadIdx.x < 4) {   // K2's chunk queue and max depth (may be null)
+    if (blockIdx.x == 0 && threadIdx.x < 8) {   // K2's chunk queues and max depth (may be null)
         if (queue) queue[threadIdx.x] = 0;
-        if (max_depth) max_depth[threadIdx.x] = 0;
+        if (max_depth && threadIdx.x < 4) max_depth[threadIdx.x] = 0;
     }
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     const int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
