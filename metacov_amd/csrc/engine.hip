@@ -151,13 +151,12 @@ struct mc_ctx {
     int ring = 0;                 // LDS ring ints
     int tiles_per_chunk = 16;
     int64_t chunk_w = 0, n_chunks = 0, total_len = 0;
-    DevBuf<int64_t> d_chunk_first;        // [2 * base chunks] (see mc_prepare)
-    DevBuf<uint64_t> d_chunk_keys;        // (tid, pos) key of each base chunk start
+    DevBuf<int64_t> d_chunk_first;        // [2 * base chunks] (ingest_kernel)
     // the plain K2's chunk geometry = the index's base chunks (half-size
     // chunks for short reads); a fused chunk is cstride base chunks
-    int tpc_plain = 0;
+    int tpc_base = 0;
     int cstride = 1;
-    int64_t n_chunks_plain = 0;
+    int64_t n_chunks_base = 0;
     // long-read path (spans > short_max)
     bool has_long = false;
     int short_max = 0;
@@ -262,7 +261,6 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_cig_off.release();
     ctx->d_cigar.release();
     ctx->d_chunk_first.release();
-    ctx->d_chunk_keys.release();
     ctx->d_tile_cnt.release();
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
@@ -511,62 +509,41 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     // K2 loads whole int4 batches past n: the tid padding must index coff
     if (ctx->d_tid.cap > (size_t)n)
         HIP_TRY(hipMemsetAsync(ctx->d_tid.p + n, 0, (ctx->d_tid.cap - n) * 4, s));
-    // ---- ingest: validation, aligned bases, max span, overhanging ends
-    HIP_TRY(ctx->d_maxend.reserve(std::max<int32_t>(nc, 1)));
-    HIP_TRY(ctx->d_cbases.reserve(std::max<int32_t>(nc, 1)));
-    HIP_TRY(hipMemsetAsync(ctx->d_cbases.p, 0, std::max<int32_t>(nc, 1) * 8, s));
-    HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
-    HIP_TRY(hipMemsetAsync(ctx->d_maxend.p, 0, std::max<int32_t>(nc, 1) * sizeof(long long), s));
-    if (n) {
-        // one resident wave per range: a second round of waves would start
-        // its ranges only when the first finished
-        if (ctx->ingest_grid <= 0) {
-            int dev = 0, ncu = 0, per = 0;
-            HIP_TRY(hipGetDevice(&dev));
-            HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ingest_kernel, kBlock, 0));
-            ctx->ingest_grid = ncu * std::max(1, per);
-        }
-        const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
-                                                                  ctx->ingest_grid));
-        hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
-                           ctx->d_maxend.p, ctx->d_cbases.p);
-        HIP_TRY(hipGetLastError());
-    }
-    unsigned long long h[4];
-    std::vector<long long> maxend(std::max<int32_t>(nc, 1));
-    HIP_TRY(hipMemcpyAsync(h, ctx->d_scratch.p, sizeof h, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(maxend.data(), ctx->d_maxend.p, maxend.size() * 8, hipMemcpyDeviceToHost, s));
-    ctx->cbases.assign(std::max<int32_t>(nc, 1), 0);
-    HIP_TRY(hipMemcpyAsync(ctx->cbases.data(), ctx->d_cbases.p, ctx->cbases.size() * 8,
-                           hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    MC_REQUIRE(h[0] == 0, MC_E_INVALID,
-               "%llu reads have tid outside [0, %d), negative pos or negative span", h[0], nc);
-    MC_REQUIRE(h[1] == 0, MC_E_INVALID,
-               "reads are not coordinate-sorted by (tid, pos) (%llu order violations); "
-               "the reference requires a sorted, indexed BAM (cli.py:37)", h[1]);
-    ctx->aligned_bases = (int64_t)h[2];
-    ctx->max_span = (int32_t)h[3];
-    // ---- layout: extents, contig offsets, chunk geometry
-    ctx->extent.resize(nc);
-    ctx->coff.resize(nc + 1);
-    int64_t off = 0;
-    for (int32_t i = 0; i < nc; ++i) {
-        ctx->extent[i] = std::max<int64_t>(ctx->len[i], maxend[i]);
-        ctx->coff[i] = off;
-        off += round_up(ctx->extent[i], 64);
-    }
-    ctx->coff[nc] = off;
-    ctx->total_len = off;
     // LDS ring of 2 tiles: reads up to short_max = ring - kTileW keep both
     // events in LDS; longer ones take the bucketed long-read path.
     ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
-    // chunks of kTilesPerChunk tiles; fewer (>= the tiles of one ring, so the
-    // ring divides the chunk) when the genome is too small to fill the GPU
-    {
+    HIP_TRY(ctx->d_maxend.reserve(std::max<int32_t>(nc, 1)));
+    HIP_TRY(ctx->d_cbases.reserve(std::max<int32_t>(nc, 1)));
+    HIP_TRY(ctx->d_coff.reserve(nc + 1));
+    if (n && ctx->ingest_grid <= 0) {
+        // one resident wave per range: a second round of waves would start
+        // its ranges only when the first finished
+        int dev = 0, ncu = 0, per = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ingest_kernel, kBlock, 0));
+        ctx->ingest_grid = ncu * std::max(1, per);
+    }
+    // ---- layout for given extents: contig offsets and chunk geometry.  One
+    // chunk index serves both K2 variants: its base chunks are the plain K2's,
+    // half-size (kPlainTilesPerChunk tiles), where the plain kernel balances
+    // better (C3: 0.995 -> 0.936 ms); the fused one is faster on full chunks
+    // (its chunk-end flushes double) and reads its chunk c as base chunks
+    // [c*s, c*s + s).  Long reads' end buckets and carries are per full
+    // chunk, so with long reads the plain K2 runs on full chunks too.
+    auto layout = [&](const std::vector<int64_t>& ext) {
+        ctx->extent = ext;
+        ctx->coff.resize(nc + 1);
+        int64_t off = 0;
+        for (int32_t i = 0; i < nc; ++i) {
+            ctx->coff[i] = off;
+            off += round_up(ext[i], 64);
+        }
+        ctx->coff[nc] = off;
+        ctx->total_len = off;
+        // chunks of kTilesPerChunk tiles; fewer (>= the tiles of one ring, so
+        // the ring divides the chunk) when the genome is too small to fill the GPU
         const int64_t tiles = std::max<int64_t>(1, (off + kTileW - 1) / kTileW);
         const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : kTilesPerChunk;
         int tpc = kTilesPerChunk;
@@ -574,46 +551,72 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
                ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
             tpc /= 2;
         ctx->tiles_per_chunk = tpc;
+        ctx->chunk_w = (int64_t)tpc * kTileW;
+        ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
+        int tpc_base = tpc;
+        if (tpc > kPlainTilesPerChunk && tpc % kPlainTilesPerChunk == 0 &&
+            ((int64_t)kPlainTilesPerChunk * kTileW) % ctx->ring == 0)
+            tpc_base = kPlainTilesPerChunk;
+        ctx->tpc_base = tpc_base;
+        ctx->cstride = tpc / tpc_base;
+        const int64_t wb = (int64_t)tpc_base * kTileW;
+        ctx->n_chunks_base = std::max<int64_t>(1, (off + wb - 1) / wb);
+    };
+    // ---- ingest + chunk index in one pass over the reads, on the layout the
+    // contig lengths give; a read past its contig's end grows the extent, and
+    // the pass runs again on the final layout
+    std::vector<int64_t> ext(ctx->len);
+    layout(ext);
+    unsigned long long h[4];
+    std::vector<long long> maxend(std::max<int32_t>(nc, 1));
+    ctx->cbases.assign(std::max<int32_t>(nc, 1), 0);
+    for (int pass = 0;; ++pass) {
+        const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every full chunk's base chunks
+        HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
+        HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_cbases.p, 0, std::max<int32_t>(nc, 1) * 8, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
+        HIP_TRY(hipMemsetAsync(ctx->d_maxend.p, 0, std::max<int32_t>(nc, 1) * sizeof(long long), s));
+        if (n) {
+            HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0xff, 2 * n_base * 8, s));   // no crossing read
+            IngestIndex ix{ctx->d_coff.p, 0, ctx->short_max, n_base, ctx->d_chunk_first.p};
+            while (((int64_t)1 << ix.lw) < (int64_t)ctx->tpc_base * kTileW) ++ix.lw;
+            const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
+                                                                      ctx->ingest_grid));
+            hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                               ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
+                               ctx->d_maxend.p, ctx->d_cbases.p, ix);
+            HIP_TRY(hipGetLastError());
+        } else {
+            HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * n_base * 8, s));
+        }
+        HIP_TRY(hipMemcpyAsync(h, ctx->d_scratch.p, sizeof h, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(maxend.data(), ctx->d_maxend.p, maxend.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(ctx->cbases.data(), ctx->d_cbases.p, ctx->cbases.size() * 8,
+                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        MC_REQUIRE(h[0] == 0, MC_E_INVALID,
+                   "%llu reads have tid outside [0, %d), negative pos or negative span", h[0], nc);
+        MC_REQUIRE(h[1] == 0, MC_E_INVALID,
+                   "reads are not coordinate-sorted by (tid, pos) (%llu order violations); "
+                   "the reference requires a sorted, indexed BAM (cli.py:37)", h[1]);
+        bool grew = false;
+        for (int32_t i = 0; i < nc; ++i)
+            if (maxend[i] > ext[i]) {
+                ext[i] = maxend[i];
+                grew = true;
+            }
+        if (!grew) break;
+        MC_REQUIRE(pass == 0, MC_E_STATE, "contig extents changed on the second ingest pass");
+        layout(ext);
     }
-    ctx->chunk_w = (int64_t)ctx->tiles_per_chunk * kTileW;
-    ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
+    ctx->aligned_bases = (int64_t)h[2];
+    ctx->max_span = (int32_t)h[3];
+    const int64_t off = ctx->total_len;
     const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
     const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
-    HIP_TRY(ctx->d_coff.reserve(nc + 1));
-    HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
-    const int64_t halo = std::min<int64_t>(ctx->max_span, ctx->short_max);
-    // One chunk index serves both K2 variants.  Its base chunks are the plain
-    // K2's: half-size (kPlainTilesPerChunk tiles) for short-read batches,
-    // where the plain kernel balances better (C3: 0.995 -> 0.936 ms), while
-    // the fused one is faster on full chunks (its chunk-end flushes double)
-    // and reads its chunk c as base chunks [c*s, c*s + s).  Long reads' end
-    // buckets and carries are per fused chunk, so with long reads both use
-    // the fused geometry.
-    int tpc_base = ctx->tiles_per_chunk;
-    if (ctx->max_span <= ctx->short_max && ctx->tiles_per_chunk > kPlainTilesPerChunk &&
-        ((int64_t)kPlainTilesPerChunk * kTileW) % ctx->ring == 0 &&
-        ctx->tiles_per_chunk % kPlainTilesPerChunk == 0)
-        tpc_base = kPlainTilesPerChunk;
-    ctx->tpc_plain = tpc_base;
-    ctx->cstride = ctx->tiles_per_chunk / tpc_base;
-    const int64_t wb = (int64_t)tpc_base * kTileW;
-    ctx->n_chunks_plain = std::max<int64_t>(1, (off + wb - 1) / wb);
-    const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every fused chunk's base chunks
-    HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
-    HIP_TRY(ctx->d_chunk_keys.reserve(n_base + 1));
-    if (n) {
-        hipLaunchKernelGGL(chunk_index_kernel, dim3((unsigned)((n_base + kBlock - 1) / kBlock)), dim3(kBlock),
-                           0, s, ctx->d_tid.p, ctx->d_pos.p, n, ctx->d_coff.p, nc, wb, halo, n_base,
-                           ctx->d_chunk_first.p, ctx->d_chunk_keys.p);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(chunk_halo_kernel, dim3((unsigned)((n_base + kWaves - 1) / kWaves)), dim3(kBlock),
-                           0, s, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, ctx->short_max, n_base,
-                           ctx->d_chunk_keys.p, ctx->d_chunk_first.p);
-        HIP_TRY(hipGetLastError());
-    } else {
-        HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * n_base * 8, s));
-    }
+    (void)off;
     ctx->has_long = ctx->max_span > ctx->short_max;
     ctx->n_long_events = 0;
     if (ctx->has_long) {
@@ -695,9 +698,11 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
                             : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);
     // the plain kernel's own chunk geometry when prepare built one (short reads)
-    const int tpc = stats ? ctx->tiles_per_chunk : ctx->tpc_plain;
-    const int64_t nch = stats ? ctx->n_chunks : ctx->n_chunks_plain;
-    const int cstride = stats ? ctx->cstride : 1;
+    // the plain K2 runs on the base chunks unless long reads need full ones
+    const bool full = stats || ctx->has_long;
+    const int tpc = full ? ctx->tiles_per_chunk : ctx->tpc_base;
+    const int64_t nch = full ? ctx->n_chunks : ctx->n_chunks_base;
+    const int cstride = full ? ctx->cstride : 1;
     const int64_t* cfirst = ctx->d_chunk_first.p;
     int grid = 0;
     if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))

@@ -2,7 +2,7 @@
 // no MFMA anywhere (SURVEY.md §8 d: "integer scatter, scan and reduction").
 //
 //   ingest_kernel        validation + extents + aligned-base count (prepare)
-//   chunk_index_kernel   BAI-style linear index: first read of each chunk
+//                        + the BAI-style chunk index (first read of each chunk)
 //   cigar_span_kernel    K1: packed BAM CIGAR words -> pileup span
 //   depth_kernel         K2: LDS-ring difference array + wave prefix scan
 //   region_seg_kernel    K3a: per-segment min/max/sum/sumsq + value histogram
@@ -152,26 +152,39 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 
 // ----------------------------------------------------------------- ingest
 
-// out[0] = invalid records, out[1] = order violations, out[2] = aligned
-// bases, out[3] = max span.  maxend[t] = furthest read end of contig t
-// (the host takes max(len, maxend) as the extent); cbases[t] = aligned
-// bases of contig t.
+// One streaming pass over the reads (prepare) computes everything K2 needs
+// from them besides the long-read buckets:
+//   out[0] = invalid records, out[1] = order violations, out[2] = aligned
+//   bases, out[3] = max span; maxend[t] = furthest read end of contig t (the
+//   host takes max(len, maxend) as the extent); cbases[t] = aligned bases of
+//   contig t;
+//   the chunk index, for base chunks of width w = 2^lw in the layout coff:
+//     index[2k]   = first short read (span <= short_max) crossing k*w, i.e.
+//                   starting before it and ending after it (UINT64_MAX: none)
+//     index[2k+1] = first read starting at or after (k+1)*w
+//   so base chunk k's reads start at min(index[2k], index[2k-1]) (0 for
+//   k = 0) and end at index[2k+1].  The fused K2's chunk c is base chunks
+//   [c*s, c*s + s).  Reads longer than short_max are the long-read path's.
+// The layout is the one prepare expects (extents = contig lengths); when a
+// read runs past its contig (maxend > len), the extents grow and prepare runs
+// the pass again with the final layout.
 //
 // Each wave owns a contiguous range of int4 read groups (the arrays are
 // padded past n) and walks it kIngestU groups per lane at a time (lane L,
 // slot u: group gb + 64u + L, so every load instruction is 1 KiB
 // contiguous), the next step's 3 x kIngestU loads in flight while the
-// current one is checked.  Nothing is loaded that depends on a load: the
-// predecessor of a group's first read comes from the neighbouring lane (or
-// the previous slot / step), and per-contig sums and ends accumulate in
-// wave-uniform registers while the wave stays on one contig, one atomic each
-// when it moves on.  (The first version gathered len[tid] per read and
-// re-loaded each group's predecessor: 0.57 ms per 100 M reads, 2.1 TB/s.)
+// current one is checked.  Nothing is loaded that depends on a load: a
+// read's predecessor comes from the neighbouring lane (or the previous slot /
+// step), the contig offset of the step's contig(s) by a scalar load, and
+// per-contig sums and ends accumulate in registers while the wave stays on
+// one contig, one atomic each when it moves on.  Index entries are stores at
+// the reads where a chunk boundary falls between two starts (every entry has
+// exactly one writer), and one atomicMin per boundary and slot for the first
+// crossing read.  (The first ingest gathered len[tid] per read and re-loaded
+// each group's predecessor: 0.57 ms per 100 M reads; the index then took two
+// more kernels of binary searches and halo scans: 0.24 ms.)
 #ifndef MC_INGEST_U
-#define MC_INGEST_U 4                  // sweep (C3 prepare): 1 0.544, 2 0.507, 4 0.480 ms
-#endif
-#ifndef MC_INGEST_STRIDE
-#define MC_INGEST_STRIDE 0             // 1: steps of all waves side by side (grid stride)
+#define MC_INGEST_U 1                  // C3 prepare: 1 0.406, 2 0.426, 4 0.82 ms (VGPR-bound occupancy)
 #endif
 constexpr int kIngestU = MC_INGEST_U;
 
@@ -196,31 +209,50 @@ __device__ __forceinline__ void ingest_flush(IngestAcc& a, unsigned long long* c
     a.bases = a.end = 0;
 }
 
+struct IngestIndex {
+    const int64_t* coff;               // [n_contigs + 1] layout of the pass
+    int lw;                            // base chunk width 2^lw
+    int short_max;
+    int64_t n_base;                    // base chunks
+    int64_t* index;                    // [2 * n_base]
+};
+
+__device__ __forceinline__ int64_t shfl_up_i64(int64_t v) {
+    const int lo = __shfl_up((int)(v & 0xffffffff), 1, 64), hi = __shfl_up((int)(v >> 32), 1, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 __global__ void __launch_bounds__(kBlock)
 ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
               const int32_t* __restrict__ span, int64_t n, int32_t n_contigs,
               unsigned long long* __restrict__ out, long long* __restrict__ maxend,
-              unsigned long long* __restrict__ cbases) {
+              unsigned long long* __restrict__ cbases, IngestIndex X) {
     constexpr int U = kIngestU;
     const int lane = threadIdx.x & 63;
     const int64_t n4 = (n + 3) / 4;
     const int64_t n_waves = (int64_t)gridDim.x * kWaves;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
     constexpr int64_t kStep = 64 * U;
-#if MC_INGEST_STRIDE
-    const int64_t g0 = gw * kStep, g1 = n4, gstride = n_waves * kStep;
-#else
     const int64_t per = ((n4 + n_waves - 1) / n_waves + kStep - 1) / kStep * kStep;
-    const int64_t g0 = gw * per, g1 = min(n4, g0 + per), gstride = kStep;
-#endif
+    const int64_t g0 = gw * per, g1 = min(n4, g0 + per);
     long long bad = 0, unsorted = 0, bases = 0;
     int mspan = 0;
     IngestAcc acc;
-    // the read before the wave's range (every wave checks its first read too)
-    int carry_t = -1, carry_p = 0, ncarry_t = -1, ncarry_p = 0;
+    // the read before the wave's range (every wave checks its first read too);
+    // carry_g = -1: none (the first read of all: boundaries from 1 on)
+    int carry_t = -1, carry_p = 0;
+    int64_t carry_g = -1;
     if (g0 < g1 && g0 > 0) {
         carry_t = uload(tid, g0 * 4 - 1);
         carry_p = uload(pos, g0 * 4 - 1);
+        if (carry_t >= 0 && carry_t < n_contigs && carry_p >= 0)
+            carry_g = uload(X.coff, carry_t) + carry_p;
     }
     i32x4 ct[U], cp[U], cs[U], nt[U], np[U], ns[U];
 #define MC_INGEST_LOAD(T, P, S, GB)                                                  \
@@ -233,14 +265,8 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         S[u] = *reinterpret_cast<const i32x4*>(span + o_);                           \
     }
     if (g0 < g1) { MC_INGEST_LOAD(ct, cp, cs, g0) }
-    for (int64_t gb = g0; gb < g1; gb += gstride) {
-        if (gb + gstride < g1) {
-            MC_INGEST_LOAD(nt, np, ns, gb + gstride)
-            if (MC_INGEST_STRIDE) {
-                ncarry_t = uload(tid, (gb + gstride) * 4 - 1);
-                ncarry_p = uload(pos, (gb + gstride) * 4 - 1);
-            }
-        }
+    for (int64_t gb = g0; gb < g1; gb += kStep) {
+        if (gb + kStep < g1) { MC_INGEST_LOAD(nt, np, ns, gb + kStep) }
         int tt[4 * U], ps[4 * U], ss[4 * U], tprev[U], pprev[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -255,13 +281,8 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             tprev[u] = lane ? up_t : l0_t;
             pprev[u] = lane ? up_p : l0_p;
         }
-        if (MC_INGEST_STRIDE) {
-            carry_t = ncarry_t;
-            carry_p = ncarry_p;
-        } else {
-            carry_t = __builtin_amdgcn_readlane(ct[U - 1].w, 63);
-            carry_p = __builtin_amdgcn_readlane(cp[U - 1].w, 63);
-        }
+        carry_t = __builtin_amdgcn_readlane(ct[U - 1].w, 63);
+        carry_p = __builtin_amdgcn_readlane(cp[U - 1].w, 63);
         unsigned todo = 0;   // bit 4u+k: valid live read
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -283,8 +304,12 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 pp = p;
             }
         }
+        const unsigned valid = todo;
         // per contig of this step (one, unless the wave crosses a boundary):
-        // wave sums of bases / max end / max span, added to the running record
+        // global starts, bases / max end / max span into the running record
+        int64_t g[4 * U];
+#pragma unroll
+        for (int j = 0; j < 4 * U; ++j) g[j] = -1;
         for (;;) {
             int cand = -1;
 #pragma unroll
@@ -293,6 +318,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             const unsigned long long act = __ballot(cand >= 0);
             if (!act) break;
             const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
+            const int64_t c0 = uload(X.coff, t0);
             long long b = 0, e = 0;
             int m = 0;
 #pragma unroll
@@ -301,6 +327,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     b += ss[j];
                     e = max(e, (long long)ps[j] + ss[j]);
                     m = max(m, ss[j]);
+                    g[j] = c0 + ps[j];
                     todo &= ~(1u << j);
                 }
             mspan = max(mspan, m);
@@ -311,6 +338,94 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             }
             acc.bases += b;
             acc.end = max(acc.end, e);
+        }
+        // chunk index: boundaries m*w with prev < m*w <= g get "first read at
+        // or after" = i (usually none between two neighbouring starts); the
+        // last read of all also closes every boundary after it with n
+        int64_t gprev[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t up = shfl_up_i64(g[4 * u + 3]);
+            const int64_t l0 = u ? readlane_i64(g[4 * u - 1], 63) : carry_g;
+            gprev[u] = lane ? up : l0;
+        }
+        carry_g = readlane_i64(g[4 * U - 1], 63);
+        // bit j of bnd: a base chunk boundary lies in (prev start, start]
+        // (rare: one read in ~1,600 at C3); bit j of cross: a short read
+        // crossing the boundary after its start
+        unsigned bnd = 0, cross = 0;
+        int mc[4 * U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int cp_id = gprev[u] < 0 ? -1 : (int)(gprev[u] >> X.lw);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 4 * u + k;
+                const int cid = (int)(g[j] >> X.lw);
+                const int sp = ss[j];
+                const bool ok = (valid >> j) & 1u;
+                if (ok && cid > cp_id) bnd |= 1u << j;
+                mc[j] = cid + 1;
+                if (ok && sp > 0 && sp <= X.short_max && cid + 1 < X.n_base &&
+                    (int)((g[j] + sp - 1) >> X.lw) > cid)
+                    cross |= 1u << j;
+                cp_id = ok ? cid : -1;
+            }
+        }
+        if (__builtin_expect(__any(bnd != 0), 0)) {
+            // boundaries m with prev < m*w <= start get "first read at or after" = i
+            while (bnd) {
+                const int j = __ffs(bnd) - 1;
+                bnd &= bnd - 1;
+                const int u = j >> 2, k = j & 3;
+                const int64_t i = (gb + 64 * u + lane) * 4 + k;
+                int64_t gp = -1;
+#pragma unroll
+                for (int jj = 0; jj < 4 * U; ++jj)
+                    if (jj == j) gp = (k == 0) ? gprev[u] : (((valid >> (jj - 1)) & 1u) ? g[jj - 1] : -1);
+                const int64_t m_lo = (gp < 0 ? 0 : (gp >> X.lw)) + 1;
+                int64_t m_hi = 0;
+#pragma unroll
+                for (int jj = 0; jj < 4 * U; ++jj)
+                    if (jj == j) m_hi = g[jj] >> X.lw;
+                if (m_hi > X.n_base) m_hi = X.n_base;
+                for (int64_t mm = m_lo; mm <= m_hi; ++mm) X.index[2 * mm - 1] = i;
+            }
+        }
+        // the last read of all closes every boundary after its start with n
+        if (__builtin_expect((gb + kStep) * 4 >= n && gb * 4 < n, 0)) {
+#pragma unroll
+            for (int j = 0; j < 4 * U; ++j) {
+                const int64_t i = (gb + 64 * (j >> 2) + lane) * 4 + (j & 3);
+                if (i == n - 1 && ((valid >> j) & 1u))
+                    for (int64_t mm = (g[j] >> X.lw) + 1; mm <= X.n_base; ++mm) X.index[2 * mm - 1] = n;
+            }
+        }
+        // first crossing read per boundary: per slot, the wave's earliest
+        // pending crossing read takes an atomicMin, every later read of the
+        // same boundary in the slot is dropped
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            unsigned pend = (cross >> (4 * u)) & 0xfu;
+            for (;;) {
+                int cm = -1, ck = 0;
+#pragma unroll
+                for (int k = 3; k >= 0; --k)
+                    if ((pend >> k) & 1u) {
+                        cm = mc[4 * u + k];
+                        ck = k;
+                    }
+                const unsigned long long act = __ballot(cm >= 0);
+                if (!act) break;
+                const int leader = __ffsll((long long)act) - 1;
+                const int m0 = __builtin_amdgcn_readlane(cm, leader);
+                if (lane == leader)
+                    atomicMin(reinterpret_cast<unsigned long long*>(&X.index[2 * (int64_t)m0]),
+                              (unsigned long long)((gb + 64 * u + lane) * 4 + ck));
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (((pend >> k) & 1u) && mc[4 * u + k] == m0) pend &= ~(1u << k);
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -344,107 +459,6 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (threadIdx.x == 3) atomicMax(&out[3], (unsigned long long)v);
         else if (v) atomicAdd(&out[threadIdx.x], (unsigned long long)v);
     }
-}
-
-// The chunk index (prepare): for base chunk k of width w (the plain K2's
-// chunk; the fused K2's chunks are `s` consecutive base chunks),
-//   chunk_index[2k]   = first read K2 has to load for the chunk: of the reads
-//                       starting in [k*w - halo, k*w), the first that crosses
-//                       k*w (a short read; long reads are the carry's), else the
-//                       first read starting at or after k*w
-//   chunk_index[2k+1] = first read starting at or after (k+1)*w
-// Searches run in (tid, pos) key space: a global position X maps to the key
-// (t, X - coff[t]) of the contig whose range holds it, and read i lies before
-// X exactly when its key is lexicographically smaller (reads are clipped to
-// their contig's extent, coff is increasing).  A probe then needs tid[i] and
-// pos[i] side by side, not the dependent coff[tid[i]] a global start needs.
-struct PosKey {
-    int t;
-    int64_t l;
-};
-
-// key of global position X (X <= 0: the smallest key; X >= coff[nc]: past all reads)
-__device__ __forceinline__ PosKey pos_key(const int64_t* __restrict__ coff, int nc, int64_t X) {
-    if (X <= 0) return PosKey{0, 0};
-    int lo = 0, hi = nc;                       // last t with coff[t] <= X
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (coff[mid] <= X) lo = mid;
-        else hi = mid;
-    }
-    if (X >= coff[nc]) return PosKey{nc, 0};
-    return PosKey{lo, X - coff[lo]};
-}
-
-__device__ __forceinline__ bool key_before(int t, int p, const PosKey& k) {
-    return t < k.t || (t == k.t && (int64_t)p < k.l);
-}
-
-// One thread per base chunk: lower bounds of both targets in lockstep (the
-// probes of the two searches go out together: one memory round trip per
-// level).  key_out[k+1] = the key of (k+1)*w, packed (t << 32 | l clamped to
-// 32 bits: a larger l only makes the halo scan stop early), for the halo scan.
-__global__ void __launch_bounds__(kBlock)
-chunk_index_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos, int64_t n,
-                   const int64_t* __restrict__ coff, int nc, int64_t w, int64_t halo,
-                   int64_t n_chunks, int64_t* __restrict__ chunk_index,
-                   uint64_t* __restrict__ key_out) {
-    const int64_t k = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-    if (k >= n_chunks) return;
-    const PosKey ka = pos_key(coff, nc, k * w - halo), kb = pos_key(coff, nc, (k + 1) * w);
-    int64_t la = 0, ha = n, lb = 0, hb = n;
-    while (la < ha || lb < hb) {
-        const int64_t ma = la + ((ha - la) >> 1), mb = lb + ((hb - lb) >> 1);
-        const bool ga = la < ha, gb = lb < hb;
-        const int ta = ga ? tid[ma] : 0, pa = ga ? pos[ma] : 0;
-        const int tb = gb ? tid[mb] : 0, pb = gb ? pos[mb] : 0;
-        if (ga) {
-            if (key_before(ta, pa, ka)) la = ma + 1;
-            else ha = ma;
-        }
-        if (gb) {
-            if (key_before(tb, pb, kb)) lb = mb + 1;
-            else hb = mb;
-        }
-    }
-    chunk_index[2 * k] = la;
-    chunk_index[2 * k + 1] = lb;
-    const uint64_t lc = kb.l > 0xffffffffll ? 0xffffffffull : (uint64_t)kb.l;
-    key_out[k + 1] = ((uint64_t)(uint32_t)kb.t << 32) | lc;
-    if (k == 0) key_out[0] = 0;
-}
-
-// Tighten chunk_index[2k] (one wave per base chunk): of the reads the halo
-// brought in, only those that cross the chunk start C0 = k*w contribute; the
-// first of them becomes the chunk's first read, or chunk_index[2k-1] (the
-// first read starting at C0) when none crosses.  A read crosses C0 only on
-// C0's contig (t, l): pos + span > l.  With C3's rare 2,150-bp N-spans the
-// halo is 2,150 positions (~215 reads, 2.6 KB per chunk) where ~15 reads
-// actually cross.
-__global__ void __launch_bounds__(kBlock)
-chunk_halo_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                  const int32_t* __restrict__ span, int short_max, int64_t n_chunks,
-                  const uint64_t* __restrict__ keys, int64_t* __restrict__ chunk_index) {
-    const int lane = threadIdx.x & 63;
-    const int64_t k = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6);
-    if (k >= n_chunks || k == 0) return;      // chunk 0 starts at read 0
-    const int64_t i0 = chunk_index[2 * k];
-    const int64_t bound = chunk_index[2 * k - 1];
-    const uint64_t key = keys[k];
-    const int tc = (int)(key >> 32);
-    const int64_t lc = (int64_t)(key & 0xffffffffull);
-    int64_t first = -1;
-    for (int64_t j0 = i0; first < 0; j0 += 64) {
-        const int64_t j = j0 + lane;
-        bool stop = j >= bound;               // every read before j ends at or before C0
-        if (!stop) {
-            const int t = tid[j], p = pos[j], sp = span[j];
-            stop = sp <= short_max && t == tc && (int64_t)p + sp > lc;
-        }
-        const unsigned long long m = __ballot(stop);
-        if (m) first = j0 + __ffsll((long long)m) - 1;
-    }
-    if (lane == 0) chunk_index[2 * k] = first < bound ? first : bound;
 }
 
 // ------------------------------------------------------ long reads (prepare)
@@ -1077,7 +1091,11 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (c >= n_chunks) break;
         if (kAhead && threadIdx.x == 0) ticket = take_chunk(queue, n_chunks, qk);
         // chunk c = base chunks [c * cstride, (c + 1) * cstride) of the index
-        const int64_t cfirst = uload(chunk_first, 2 * c * cstride);
+        // (ingest_kernel): its reads start at the first short read crossing
+        // its start, else at the first read starting in it
+        const int64_t b0 = c * cstride;
+        const int64_t cfirst = b0 ? (int64_t)min((uint64_t)uload(chunk_first, 2 * b0),
+                                                 (uint64_t)uload(chunk_first, 2 * b0 - 1)) : 0;
         const int64_t cend = uload(chunk_first, 2 * (c + 1) * cstride - 1);   // reads of this chunk end
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;

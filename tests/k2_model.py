@@ -1,5 +1,5 @@
 """Executable model of K2's decomposition (metacov_amd/csrc/kernels.h,
-depth_kernel + chunk_index_kernel + long_count/long_fill kernels), in numpy.
+depth_kernel + ingest_kernel's chunk index + long_count/long_fill kernels), in numpy.
 
 TEST INFRASTRUCTURE: it checks the ALGORITHM (chunks of 16 tiles of 4096
 positions, an 8192-slot ring, the max-span halo, long-read end events as a
@@ -38,14 +38,32 @@ def model(lengths, tid, pos, span):
         c0=a//CW+1; c1=(b-1)//CW+1
         if c1>c0: cdiff[c0]+=1; cdiff[c1]-=1
     carry_c=np.cumsum(cdiff)[:nch]
+    # chunk index as ingest_kernel builds it in its one pass over the reads:
+    # F[m] = first read starting at or after m*BW (a store at the read where
+    # m*BW falls between two starts), X[m] = first short read crossing m*BW
+    BTPC=4 if TPC>4 and TPC%4==0 else TPC; BW=W*BTPC; S=TPC//BTPC; NB=nch*S
+    F=np.full(NB+1,len(gs),np.int64); F[0]=0; Xidx=np.full(NB+1,np.iinfo(np.int64).max,np.int64)
+    prev=-1
+    for i in range(len(gs)):
+        for m in range((prev//BW+1) if prev>=0 else 1, min(gs[i]//BW, NB)+1): F[m]=i
+        mb=gs[i]//BW+1
+        if 0<span[i]<=SM and mb<NB and ge[i]>mb*BW: Xidx[mb]=min(Xidx[mb],i)
+        prev=gs[i]
+    def ref_first(C0):
+        # the definition it replaces: the first read of the max-span halo that
+        # crosses C0 (short reads), else the first read starting at or after C0
+        f=np.searchsorted(gs, C0-halo, 'left')
+        while f<len(gs) and not (gs[f]>=C0 or (span[f]<=SM and ge[f]>C0)):
+            f+=1
+        return f
     depth=np.zeros(alloc,np.int64)
     for c in range(nch):
         C0=c*CW
-        first=np.searchsorted(gs, C0-halo, 'left')
-        # chunk_halo_kernel: the first halo read that crosses C0 (short reads),
-        # else the first read starting at or after C0
-        while first<len(gs) and not (gs[first]>=C0 or (span[first]<=SM and ge[first]>C0)):
-            first+=1
+        # ingest_kernel's index (base chunks of BW, a full chunk is S of them):
+        # the first short read crossing C0, else the first read starting at or after C0
+        b0=c*S
+        first=0 if b0==0 else min(Xidx[b0], F[b0])
+        assert first==ref_first(C0)
         first&=~3
         ring=np.zeros(RING,np.int64)
         i=first; carry=carry_c[c] if long_.any() else 0
