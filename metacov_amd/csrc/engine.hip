@@ -160,11 +160,12 @@ struct mc_ctx {
     // long-read path (spans > short_max)
     bool has_long = false;
     int short_max = 0;
-    int64_t n_long_events = 0;
     DevBuf<unsigned> d_tile_cnt;
     DevBuf<int64_t> d_tile_off;
     DevBuf<int32_t> d_tile_ev;
     DevBuf<int> d_chunk_carry;
+    DevBuf<long long> d_scan_part;        // long_scan partial sums
+    int long_grid = 0;                    // resident long_count / long_fill workgroups
     DevBuf<int32_t> d_depth;
     bool depth_valid = false;
     int32_t max_depth = -1;
@@ -265,6 +266,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
     ctx->d_chunk_carry.release();
+    ctx->d_scan_part.release();
     ctx->d_depth.release();
     ctx->d_scratch.release();
     ctx->d_maxend.release();
@@ -618,47 +620,43 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
     (void)off;
     ctx->has_long = ctx->max_span > ctx->short_max;
-    ctx->n_long_events = 0;
     if (ctx->has_long) {
+        // end-event buckets and chunk carries, all on the device (count ->
+        // offsets -> fill), no host round trip; the bucket array is sized for
+        // every read being long
         HIP_TRY(ctx->d_tile_cnt.reserve(n_tiles + 1));
         HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
         HIP_TRY(ctx->d_tile_off.reserve(n_tiles + 1));
+        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(n + kBatch)));   // K2 loads whole int4 batches
         HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
         HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
-        const int64_t nb = std::min<int64_t>((n + kBlock - 1) / kBlock, 8192);
-        hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len,
-                           ctx->chunk_w, ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
-        HIP_TRY(hipGetLastError());
-        std::vector<unsigned> cnt(n_tiles + 1);
-        std::vector<int> cdiff(ctx->n_chunks + 1);
-        HIP_TRY(hipMemcpyAsync(cnt.data(), ctx->d_tile_cnt.p, (n_tiles + 1) * 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(cdiff.data(), ctx->d_chunk_carry.p, (ctx->n_chunks + 1) * 4,
-                               hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        std::vector<int64_t> toff(n_tiles + 1);
-        int64_t acc = 0;
-        for (int64_t t = 0; t < n_tiles; ++t) {
-            toff[t] = acc;
-            acc += cnt[t];
+        if (ctx->long_grid <= 0) {
+            int dev = 0, ncu = 0, per = 0;
+            HIP_TRY(hipGetDevice(&dev));
+            HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)long_fill_kernel, kBlock, 0));
+            ctx->long_grid = ncu * std::max(1, per);
         }
-        toff[n_tiles] = acc;
-        int run = 0;
-        for (int64_t c = 0; c < ctx->n_chunks; ++c) {
-            run += cdiff[c];
-            cdiff[c] = run;
-        }
-        ctx->n_long_events = acc;
-        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(acc + kBatch)));   // K2 loads whole int4 batches
-        HIP_TRY(hipMemcpyAsync(ctx->d_tile_off.p, toff.data(), (n_tiles + 1) * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(ctx->d_chunk_carry.p, cdiff.data(), ctx->n_chunks * 4,
-                               hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
-        hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                           ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len,
-                           ctx->chunk_w, ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        LongGeo G{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len, 0, 0};
+        while (((int64_t)1 << G.lcw) < ctx->chunk_w) ++G.lcw;
+        const int64_t subs = (n + kLongSub - 1) / kLongSub;
+        const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(subs, ctx->long_grid));
+        G.per = (subs + nb - 1) / nb * kLongSub;
+        hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
+                           ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipStreamSynchronize(s));   // host vectors go out of scope
+        const int bt = (int)((n_tiles + kScanSeg - 1) / kScanSeg);
+        const int bc = (int)((ctx->n_chunks + kScanSeg - 1) / kScanSeg);
+        HIP_TRY(ctx->d_scan_part.reserve(bt + bc));
+        ScanArgs A{ctx->d_tile_cnt.p, n_tiles, ctx->d_tile_off.p, ctx->d_chunk_carry.p, ctx->n_chunks,
+                   ctx->d_scan_part.p, bt};
+        hipLaunchKernelGGL(long_scan_partial_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(long_scan_final_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
+                           ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(ctx->ev[3], s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -467,110 +467,282 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 // event in the LDS ring.  For them:
 //   * +1 is applied by K2 in-stream at the read start (its own chunk only);
 //   * -1 goes to an end-event bucket of the tile holding the end (CSR over
-//     tiles, filled here, applied by K2 at the start of that tile);
+//     tiles: long_count_kernel counts, long_scan_kernel turns the counts into
+//     offsets, long_fill_kernel fills; K2 streams a chunk's events in tile
+//     order);
 //   * chunk_diff builds the count of long reads covering each chunk's first
 //     position that started in an earlier chunk (K2's initial carry).
+//
+// Each workgroup walks a contiguous range of reads in sub-ranges of
+// kLongSub reads (16 per thread, int4 loads).  Reads are sorted by start, so
+// a sub-range's end events fall in a short run of tiles from the tile of its
+// first start: they are counted in an LDS window of kLongTileWin tiles (and
+// kLongChunkWin chunks for the carries), then flushed with one global atomic
+// per non-empty bin; an event past the window goes straight to global memory.
+// The fill pass reserves each bin's slots with one atomic per bin and ranks
+// the sub-range's events inside it with LDS atomics.  (Per-wave ballot
+// grouping with a returning global atomic per 64 reads was latency-bound:
+// 0.35 + 0.39 ms for C5's 47 M long reads, plus a host round trip for the
+// offsets.)
+constexpr int kLongPer = 16;                      // reads per thread and sub-range
+constexpr int kLongSub = kBlock * kLongPer;
+constexpr int kLongTileWin = 2048;                // 8 Mi positions
+constexpr int kLongChunkWin = 512;
 
-// Wave-aggregated counter increments: lanes with equal keys (key < 0: none)
-// share one atomic (reads are position-sorted, so a wave's 64 reads touch a
-// handful of tiles / chunks).  Returns each lane's slot: the counter value
-// before the group's add plus the lane's rank within its group.
-// (keys are tile / chunk indices < 2^31; readlane with the uniform leader,
-// no LDS round trips)
-__device__ __forceinline__ unsigned wave_key_add(unsigned* arr, int key, int lane) {
-    // group the lanes by key (ballots only), then every group's leader adds
-    // its count in one atomic instruction: one round trip per wave
-    unsigned rank = 0, count = 0;
-    int leader_of = lane;
-    unsigned long long pending = __ballot(key >= 0);
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int k = __builtin_amdgcn_readlane(key, leader);
-        const unsigned long long m = __ballot(key == k) & pending;
-        if (lane == leader) count = (unsigned)__popcll(m);
-        if ((m >> lane) & 1ull) {
-            leader_of = leader;
-            rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-        }
-        pending &= ~m;
-    }
-    unsigned base = 0;
-    if (count) base = atomicAdd(&arr[key], count);
-    base = (unsigned)__shfl((int)base, leader_of, 64);
-    return base + rank;
-}
-
-__device__ __forceinline__ void wave_key_add_signed(int* arr, int key, int sign, int lane) {
-    unsigned long long pending = __ballot(key >= 0);
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int k = __builtin_amdgcn_readlane(key, leader);
-        const unsigned long long m = __ballot(key == k) & pending;
-        if (lane == leader) atomicAdd(&arr[k], sign * (int)__popcll(m));
-        pending &= ~m;
-    }
-}
-
-// Long-read events of read i (short_max < span): the tile of its end event
-// (or -1: past the allocation, or exactly on a chunk start, where the next
-// chunk's carry already excludes it) and its chunk-carry range [c0, c1).
-struct LongEv {
-    int tile, c0, c1;
+struct LongGeo {
+    const int32_t* tid;
+    const int32_t* pos;
+    const int32_t* span;
+    int64_t n;
+    const int64_t* coff;
+    int short_max;
+    int64_t alloc_len;
+    int lcw;                                      // chunk width 2^lcw
+    int64_t per;                                  // reads per workgroup (multiple of kLongSub)
 };
 
-__device__ __forceinline__ LongEv long_events(const int32_t* tid, const int32_t* pos,
-                                              const int32_t* span, int64_t i, int64_t n,
-                                              const int64_t* coff, int short_max,
-                                              int64_t alloc_len, int64_t chunk_w, int64_t* ge_out) {
-    LongEv e{-1, -1, -1};
-    if (i >= n) return e;
-    const int sp = span[i];
-    if (sp <= short_max) return e;
-    const int64_t gs = coff[tid[i]] + pos[i];
-    const int64_t ge = gs + sp;
-    *ge_out = ge;
-    if (ge < alloc_len && ge % chunk_w) e.tile = (int)(ge / kTileW);
-    const int64_t c0 = gs / chunk_w + 1, c1 = (ge - 1) / chunk_w + 1;
-    if (c1 > c0) {
-        e.c0 = (int)c0;
-        e.c1 = (int)c1;
+// Global starts and spans of this thread's kLongPer reads of the sub-range at
+// `sub` (read sub + (v * kBlock + threadIdx.x) * 4 + k); live = bit mask of
+// reads below `r1`.  Contig offsets by scalar loads per distinct contig of
+// the wave (one or two per sub-range).
+__device__ __forceinline__ void long_load(const LongGeo& G, int64_t sub, int64_t r1, int64_t (&g)[kLongPer],
+                                          int (&sp)[kLongPer], unsigned& live) {
+    int tt[kLongPer], pp[kLongPer];
+    live = 0;
+#pragma unroll
+    for (int v = 0; v < kLongPer / 4; ++v) {
+        const int64_t i0 = sub + ((int64_t)v * kBlock + threadIdx.x) * 4;
+        i32x4 t4 = {0, 0, 0, 0}, p4 = {0, 0, 0, 0}, s4 = {0, 0, 0, 0};
+        if (i0 < r1) {   // the read arrays are padded by a batch past n
+            t4 = *reinterpret_cast<const i32x4*>(G.tid + i0);
+            p4 = *reinterpret_cast<const i32x4*>(G.pos + i0);
+            s4 = *reinterpret_cast<const i32x4*>(G.span + i0);
+        }
+        tt[4 * v] = t4.x; tt[4 * v + 1] = t4.y; tt[4 * v + 2] = t4.z; tt[4 * v + 3] = t4.w;
+        pp[4 * v] = p4.x; pp[4 * v + 1] = p4.y; pp[4 * v + 2] = p4.z; pp[4 * v + 3] = p4.w;
+        sp[4 * v] = s4.x; sp[4 * v + 1] = s4.y; sp[4 * v + 2] = s4.z; sp[4 * v + 3] = s4.w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k < r1 && s4[k] > G.short_max) live |= 1u << (4 * v + k);
     }
-    return e;
+    unsigned todo = live;
+    for (;;) {
+        int cand = -1;
+#pragma unroll
+        for (int j = kLongPer - 1; j >= 0; --j)
+            if ((todo >> j) & 1u) cand = tt[j];
+        const unsigned long long act = __ballot(cand >= 0);
+        if (!act) break;
+        const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
+        const int64_t c = uload(G.coff, t0);
+#pragma unroll
+        for (int j = 0; j < kLongPer; ++j)
+            if (((todo >> j) & 1u) && tt[j] == t0) {
+                g[j] = c + pp[j];
+                todo &= ~(1u << j);
+            }
+    }
+}
+
+// global start of read i (wave-uniform i): the sub-range's window base
+__device__ __forceinline__ int64_t long_first_start(const LongGeo& G, int64_t i) {
+    return uload(G.coff, uload(G.tid, i)) + uload(G.pos, i);
+}
+
+// the tile of read j's end event, or -1 (past the allocation, or exactly on
+// a chunk start, where the next chunk's carry already excludes it)
+__device__ __forceinline__ int64_t long_end_tile(const LongGeo& G, int64_t ge) {
+    return (ge < G.alloc_len && (ge & (((int64_t)1 << G.lcw) - 1))) ? ge / kTileW : -1;
 }
 
 __global__ void __launch_bounds__(kBlock)
-long_count_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                  const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
-                  int short_max, int64_t alloc_len, int64_t chunk_w,
-                  unsigned* __restrict__ tile_cnt, int* __restrict__ chunk_diff) {
-    const int lane = threadIdx.x & 63;
-    // whole waves stride together (the aggregation loops are wave-wide)
-    for (int64_t w0 = blockIdx.x * (int64_t)kBlock + (threadIdx.x & ~63); w0 < n;
-         w0 += (int64_t)gridDim.x * kBlock) {
-        int64_t ge = 0;
-        const LongEv e = long_events(tid, pos, span, w0 + lane, n, coff, short_max, alloc_len,
-                                     chunk_w, &ge);
-        (void)wave_key_add(tile_cnt, e.tile, lane);
-        wave_key_add_signed(chunk_diff, e.c0, 1, lane);
-        wave_key_add_signed(chunk_diff, e.c1, -1, lane);
+long_count_kernel(LongGeo G, unsigned* __restrict__ tile_cnt, int* __restrict__ chunk_diff) {
+    __shared__ int wt[kLongTileWin];
+    __shared__ int wc[kLongChunkWin];
+    const int64_t r0 = blockIdx.x * G.per, r1 = min(G.n, r0 + G.per);
+    for (int64_t sub = r0; sub < r1; sub += kLongSub) {
+        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
+        for (int k = threadIdx.x; k < kLongChunkWin; k += kBlock) wc[k] = 0;
+        int64_t g[kLongPer];
+        int sp[kLongPer];
+        unsigned live;
+        long_load(G, sub, r1, g, sp, live);
+        const int64_t gf = long_first_start(G, sub);
+        const int64_t TB = gf / kTileW, CB = gf >> G.lcw;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kLongPer; ++j) {
+            if (!((live >> j) & 1u)) continue;
+            const int64_t ge = g[j] + sp[j];
+            const int64_t te = long_end_tile(G, ge);
+            if (te >= 0) {
+                if (te - TB < kLongTileWin) atomicAdd(&wt[te - TB], 1);
+                else atomicAdd(&tile_cnt[te], 1u);
+            }
+            const int64_t c0 = (g[j] >> G.lcw) + 1, c1 = ((ge - 1) >> G.lcw) + 1;
+            if (c1 > c0) {
+                if (c0 - CB < kLongChunkWin) atomicAdd(&wc[c0 - CB], 1);
+                else atomicAdd(&chunk_diff[c0], 1);
+                if (c1 - CB < kLongChunkWin) atomicAdd(&wc[c1 - CB], -1);
+                else atomicAdd(&chunk_diff[c1], -1);
+            }
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) {
+            const int v = wt[k];
+            if (v) atomicAdd(&tile_cnt[TB + k], (unsigned)v);
+        }
+        for (int k = threadIdx.x; k < kLongChunkWin; k += kBlock) {
+            const int v = wc[k];
+            if (v) atomicAdd(&chunk_diff[CB + k], v);
+        }
+        __syncthreads();
     }
 }
 
+// tile_off = exclusive prefix of tile_cnt (n_tiles + 1 entries), tile_cnt
+// zeroed (the fill pass's cursors), chunk_diff turned into the per-chunk
+// carry (inclusive prefix, in place): a reduce-then-scan over segments of
+// kScanSeg entries, the first bt blocks on the tiles, the next on the chunks.
+constexpr int kScanPer = 16;
+constexpr int kScanSeg = kBlock * kScanPer;
+
+struct ScanArgs {
+    unsigned* tile_cnt;
+    int64_t n_tiles;
+    int64_t* tile_off;
+    int* chunk;
+    int64_t n_chunks;
+    long long* partial;                            // [bt + bc]
+    int bt;
+};
+
+__device__ __forceinline__ long long block_sum_ll(long long v, long long* red) {
+    v = wave_sum64(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) t += red[w];
+    __syncthreads();
+    return t;
+}
+
 __global__ void __launch_bounds__(kBlock)
-long_fill_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                 const int32_t* __restrict__ span, int64_t n, const int64_t* __restrict__ coff,
-                 int short_max, int64_t alloc_len, int64_t chunk_w,
-                 const int64_t* __restrict__ tile_off,
-                 unsigned* __restrict__ tile_cursor, int32_t* __restrict__ ev) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t w0 = blockIdx.x * (int64_t)kBlock + (threadIdx.x & ~63); w0 < n;
-         w0 += (int64_t)gridDim.x * kBlock) {
-        int64_t ge = 0;
-        const LongEv e = long_events(tid, pos, span, w0 + lane, n, coff, short_max, alloc_len,
-                                     chunk_w, &ge);
-        const unsigned slot = wave_key_add(tile_cursor, e.tile, lane);
-        // chunk-relative end (grouped by tile, so a chunk's events stream in tile order)
-        if (e.tile >= 0) ev[tile_off[e.tile] + slot] = (int32_t)(ge - ge / chunk_w * chunk_w);
+long_scan_partial_kernel(ScanArgs A) {
+    __shared__ long long red[kWaves];
+    const bool tiles = (int)blockIdx.x < A.bt;
+    const int64_t b = tiles ? blockIdx.x : blockIdx.x - A.bt;
+    const int64_t N = tiles ? A.n_tiles : A.n_chunks;
+    long long v = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = b * kScanSeg + (int64_t)k * kBlock + threadIdx.x;
+        if (i < N) v += tiles ? (long long)A.tile_cnt[i] : (long long)A.chunk[i];
+    }
+    v = block_sum_ll(v, red);
+    if (threadIdx.x == 0) A.partial[blockIdx.x] = v;
+}
+
+__global__ void __launch_bounds__(kBlock)
+long_scan_final_kernel(ScanArgs A) {
+    __shared__ long long red[kWaves];
+    const bool tiles = (int)blockIdx.x < A.bt;
+    const int64_t b = tiles ? blockIdx.x : blockIdx.x - A.bt;
+    const int64_t N = tiles ? A.n_tiles : A.n_chunks;
+    const int p0 = tiles ? 0 : A.bt;
+    long long pre = 0;                             // the segments before this one
+    for (int q = p0 + threadIdx.x; q < (int)blockIdx.x; q += kBlock) pre += A.partial[q];
+    pre = block_sum_ll(pre, red);
+    // this thread's kScanPer consecutive entries
+    const int64_t i0 = b * kScanSeg + (int64_t)threadIdx.x * kScanPer;
+    long long x[kScanPer], tot = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = i0 + k;
+        x[k] = i < N ? (tiles ? (long long)A.tile_cnt[i] : (long long)A.chunk[i]) : 0;
+        tot += x[k];
+    }
+    // exclusive block scan of the thread totals (64-bit wave scans + wave carries)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    long long incl = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) red[wave] = incl;
+    __syncthreads();
+    long long run = pre + incl - tot;
+    for (int w = 0; w < wave; ++w) run += red[w];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = i0 + k;
+        if (i >= N) break;
+        if (tiles) {
+            A.tile_off[i] = run;
+            A.tile_cnt[i] = 0;
+            run += x[k];
+        } else {
+            run += x[k];
+            A.chunk[i] = (int)run;                // inclusive
+        }
+    }
+    if (tiles && i0 < N && i0 + kScanPer >= N) A.tile_off[N] = run;   // the thread holding the last tile
+}
+
+__global__ void __launch_bounds__(kBlock)
+long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __restrict__ cursor,
+                 int32_t* __restrict__ ev) {
+    __shared__ int wt[kLongTileWin];      // counts, then ranks
+    __shared__ int wb[kLongTileWin];      // first slot of the sub-range's events per tile
+    const int64_t r0 = blockIdx.x * G.per, r1 = min(G.n, r0 + G.per);
+    const int64_t cmask = ((int64_t)1 << G.lcw) - 1;
+    for (int64_t sub = r0; sub < r1; sub += kLongSub) {
+        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
+        int64_t g[kLongPer];
+        int sp[kLongPer];
+        unsigned live;
+        long_load(G, sub, r1, g, sp, live);
+        const int64_t TB = long_first_start(G, sub) / kTileW;
+        __syncthreads();
+        int te[kLongPer];                  // window bin, or -1
+#pragma unroll
+        for (int j = 0; j < kLongPer; ++j) {
+            te[j] = -1;
+            if (!((live >> j) & 1u)) continue;
+            const int64_t ge = g[j] + sp[j];
+            const int64_t t = long_end_tile(G, ge);
+            if (t < 0) {
+                live &= ~(1u << j);
+            } else if (t - TB < kLongTileWin) {
+                te[j] = (int)(t - TB);
+                atomicAdd(&wt[te[j]], 1);
+            }
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) {
+            const int v = wt[k];
+            if (v) {
+                wb[k] = (int)(tile_off[TB + k] + atomicAdd(&cursor[TB + k], (unsigned)v));
+                wt[k] = 0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kLongPer; ++j) {
+            if (!((live >> j) & 1u)) continue;
+            const int64_t ge = g[j] + sp[j];
+            int64_t slot;
+            if (te[j] >= 0) {
+                slot = wb[te[j]] + atomicAdd(&wt[te[j]], 1);
+            } else {
+                const int64_t t = ge / kTileW;
+                slot = tile_off[t] + atomicAdd(&cursor[t], 1u);
+            }
+            ev[slot] = (int32_t)(ge & cmask);   // chunk-relative end
+        }
+        __syncthreads();
     }
 }
 
