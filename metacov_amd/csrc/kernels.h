@@ -484,10 +484,13 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 // grouping with a returning global atomic per 64 reads was latency-bound:
 // 0.35 + 0.39 ms for C5's 47 M long reads, plus a host round trip for the
 // offsets.)
-constexpr int kLongPer = 16;                      // reads per thread and sub-range
+#ifndef MC_LONG_PER
+#define MC_LONG_PER 8
+#endif
+constexpr int kLongPer = MC_LONG_PER;             // reads per thread and sub-range
 constexpr int kLongSub = kBlock * kLongPer;
-constexpr int kLongTileWin = 2048;                // 8 Mi positions
-constexpr int kLongChunkWin = 512;
+constexpr int kLongTileWin = 256;                 // 1 Mi positions past the sub-range's first start
+constexpr int kLongChunkWin = 64;
 
 struct LongGeo {
     const int32_t* tid;
@@ -501,29 +504,40 @@ struct LongGeo {
     int64_t per;                                  // reads per workgroup (multiple of kLongSub)
 };
 
-// Global starts and spans of this thread's kLongPer reads of the sub-range at
-// `sub` (read sub + (v * kBlock + threadIdx.x) * 4 + k); live = bit mask of
-// reads below `r1`.  Contig offsets by scalar loads per distinct contig of
-// the wave (one or two per sub-range).
-__device__ __forceinline__ void long_load(const LongGeo& G, int64_t sub, int64_t r1, int64_t (&g)[kLongPer],
-                                          int (&sp)[kLongPer], unsigned& live) {
+struct LongRaw {                                  // a thread's reads of one sub-range, as loaded
+    i32x4 t[kLongPer / 4], p[kLongPer / 4], s[kLongPer / 4];
+};
+
+// this thread's reads of the sub-range at `sub`: read sub + (v * kBlock +
+// threadIdx.x) * 4 + k (the read arrays are padded by a batch past n)
+__device__ __forceinline__ void long_issue(const LongGeo& G, int64_t sub, int64_t r1, LongRaw& r) {
+#pragma unroll
+    for (int v = 0; v < kLongPer / 4; ++v) {
+        const int64_t i0 = sub + ((int64_t)v * kBlock + threadIdx.x) * 4;
+        const int64_t o = i0 < r1 ? i0 : 0;
+        r.t[v] = *reinterpret_cast<const i32x4*>(G.tid + o);
+        r.p[v] = *reinterpret_cast<const i32x4*>(G.pos + o);
+        r.s[v] = *reinterpret_cast<const i32x4*>(G.span + o);
+    }
+}
+
+// Global starts and spans of the loaded reads; live = bit mask of the long
+// reads below r1.  Contig offsets by scalar loads per distinct contig of the
+// wave (one or two per sub-range).
+__device__ __forceinline__ void long_finish(const LongGeo& G, int64_t sub, int64_t r1, const LongRaw& r,
+                                            int64_t (&g)[kLongPer], int (&sp)[kLongPer], unsigned& live) {
     int tt[kLongPer], pp[kLongPer];
     live = 0;
 #pragma unroll
     for (int v = 0; v < kLongPer / 4; ++v) {
         const int64_t i0 = sub + ((int64_t)v * kBlock + threadIdx.x) * 4;
-        i32x4 t4 = {0, 0, 0, 0}, p4 = {0, 0, 0, 0}, s4 = {0, 0, 0, 0};
-        if (i0 < r1) {   // the read arrays are padded by a batch past n
-            t4 = *reinterpret_cast<const i32x4*>(G.tid + i0);
-            p4 = *reinterpret_cast<const i32x4*>(G.pos + i0);
-            s4 = *reinterpret_cast<const i32x4*>(G.span + i0);
-        }
-        tt[4 * v] = t4.x; tt[4 * v + 1] = t4.y; tt[4 * v + 2] = t4.z; tt[4 * v + 3] = t4.w;
-        pp[4 * v] = p4.x; pp[4 * v + 1] = p4.y; pp[4 * v + 2] = p4.z; pp[4 * v + 3] = p4.w;
-        sp[4 * v] = s4.x; sp[4 * v + 1] = s4.y; sp[4 * v + 2] = s4.z; sp[4 * v + 3] = s4.w;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (i0 + k < r1 && s4[k] > G.short_max) live |= 1u << (4 * v + k);
+        for (int k = 0; k < 4; ++k) {
+            tt[4 * v + k] = r.t[v][k];
+            pp[4 * v + k] = r.p[v][k];
+            sp[4 * v + k] = r.s[v][k];
+            if (i0 + k < r1 && r.s[v][k] > G.short_max) live |= 1u << (4 * v + k);
+        }
     }
     unsigned todo = live;
     for (;;) {
@@ -555,21 +569,34 @@ __device__ __forceinline__ int64_t long_end_tile(const LongGeo& G, int64_t ge) {
     return (ge < G.alloc_len && (ge & (((int64_t)1 << G.lcw) - 1))) ? ge / kTileW : -1;
 }
 
+// Sub-range loop shared by the count and fill passes: the next sub-range's
+// loads are in flight while the current one is counted / filled.
+template <class F>
+__device__ __forceinline__ void long_walk(const LongGeo& G, F&& body) {
+    const int64_t r0 = blockIdx.x * G.per, r1 = min(G.n, r0 + G.per);
+    LongRaw cur, nxt;
+    if (r0 < r1) long_issue(G, r0, r1, cur);
+    for (int64_t sub = r0; sub < r1; sub += kLongSub) {
+        if (sub + kLongSub < r1) long_issue(G, sub + kLongSub, r1, nxt);
+        int64_t g[kLongPer];
+        int sp[kLongPer];
+        unsigned live;
+        long_finish(G, sub, r1, cur, g, sp, live);
+        body(sub, g, sp, live);
+        cur = nxt;
+    }
+}
+
 __global__ void __launch_bounds__(kBlock)
 long_count_kernel(LongGeo G, unsigned* __restrict__ tile_cnt, int* __restrict__ chunk_diff) {
     __shared__ int wt[kLongTileWin];
     __shared__ int wc[kLongChunkWin];
-    const int64_t r0 = blockIdx.x * G.per, r1 = min(G.n, r0 + G.per);
-    for (int64_t sub = r0; sub < r1; sub += kLongSub) {
-        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
-        for (int k = threadIdx.x; k < kLongChunkWin; k += kBlock) wc[k] = 0;
-        int64_t g[kLongPer];
-        int sp[kLongPer];
-        unsigned live;
-        long_load(G, sub, r1, g, sp, live);
+    for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
+    for (int k = threadIdx.x; k < kLongChunkWin; k += kBlock) wc[k] = 0;
+    __syncthreads();
+    long_walk(G, [&](int64_t sub, const int64_t (&g)[kLongPer], const int (&sp)[kLongPer], unsigned live) {
         const int64_t gf = long_first_start(G, sub);
         const int64_t TB = gf / kTileW, CB = gf >> G.lcw;
-        __syncthreads();
 #pragma unroll
         for (int j = 0; j < kLongPer; ++j) {
             if (!((live >> j) & 1u)) continue;
@@ -590,14 +617,20 @@ long_count_kernel(LongGeo G, unsigned* __restrict__ tile_cnt, int* __restrict__ 
         __syncthreads();
         for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) {
             const int v = wt[k];
-            if (v) atomicAdd(&tile_cnt[TB + k], (unsigned)v);
+            if (v) {
+                atomicAdd(&tile_cnt[TB + k], (unsigned)v);
+                wt[k] = 0;
+            }
         }
         for (int k = threadIdx.x; k < kLongChunkWin; k += kBlock) {
             const int v = wc[k];
-            if (v) atomicAdd(&chunk_diff[CB + k], v);
+            if (v) {
+                atomicAdd(&chunk_diff[CB + k], v);
+                wc[k] = 0;
+            }
         }
         __syncthreads();
-    }
+    });
 }
 
 // tile_off = exclusive prefix of tile_cnt (n_tiles + 1 entries), tile_cnt
@@ -696,23 +729,17 @@ long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __re
                  int32_t* __restrict__ ev) {
     __shared__ int wt[kLongTileWin];      // counts, then ranks
     __shared__ int wb[kLongTileWin];      // first slot of the sub-range's events per tile
-    const int64_t r0 = blockIdx.x * G.per, r1 = min(G.n, r0 + G.per);
     const int64_t cmask = ((int64_t)1 << G.lcw) - 1;
-    for (int64_t sub = r0; sub < r1; sub += kLongSub) {
-        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
-        int64_t g[kLongPer];
-        int sp[kLongPer];
-        unsigned live;
-        long_load(G, sub, r1, g, sp, live);
+    for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
+    __syncthreads();
+    long_walk(G, [&](int64_t sub, const int64_t (&g)[kLongPer], const int (&sp)[kLongPer], unsigned live) {
         const int64_t TB = long_first_start(G, sub) / kTileW;
-        __syncthreads();
         int te[kLongPer];                  // window bin, or -1
 #pragma unroll
         for (int j = 0; j < kLongPer; ++j) {
             te[j] = -1;
             if (!((live >> j) & 1u)) continue;
-            const int64_t ge = g[j] + sp[j];
-            const int64_t t = long_end_tile(G, ge);
+            const int64_t t = long_end_tile(G, g[j] + sp[j]);
             if (t < 0) {
                 live &= ~(1u << j);
             } else if (t - TB < kLongTileWin) {
@@ -743,7 +770,9 @@ long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __re
             ev[slot] = (int32_t)(ge & cmask);   // chunk-relative end
         }
         __syncthreads();
-    }
+        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
+        __syncthreads();
+    });
 }
 
 // ----------------------------------------------------------------- K1
