@@ -25,7 +25,8 @@
 // the 13 result fields with the reference's expression types.  The per-
 // position arrays of the reference are never materialised:
 //   cov   sum over reads of |[max(0,rstart), min(L,rend))|         (exact)
-//   covc  the same lengths times 1/rcor                  (order differs: fp)
+//   covc  per-position 1/rcor sums in read order, np.mean's pairwise sum
+//         (the array is built only when some 1/rcor != 1)          (exact)
 //   starts / cor   the distinct rstart in [0, L) and the 1/rcor of the last
 //         read starting there; np.mean(cor) is re-summed exactly the way
 //         numpy 2.x's add.reduce does (8192-element chunks, pairwise within)
@@ -272,6 +273,40 @@ double pairwise_block(const int64_t* off, const double* v, size_t m, int64_t bas
            pairwise_block(off + split, v + split, m - split, base + n2, n - n2);
 }
 
+// numpy 2.x pairwise sum of a dense block of n float64 (n <= 8192)
+double pairwise_dense(const double* a, int64_t n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int64_t i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int64_t i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return pairwise_dense(a, n2) + pairwise_dense(a + n2, n - n2);
+}
+
+// np.add.reduce over a dense float64 array: 8192-element chunks, pairwise within
+double numpy_sum_dense(const std::vector<double>& v) {
+    constexpr int64_t kChunk = 8192;
+    const int64_t L = (int64_t)v.size();
+    double total = 0;
+    for (int64_t c = 0; c < L; c += kChunk) {
+        const double s = pairwise_dense(v.data() + c, std::min(kChunk, L - c));
+        total = c == 0 ? s : total + s;
+    }
+    return total;
+}
+
 // np.add.reduce over a float64 array of length L with the given sparse
 // entries: 8192-element chunks, pairwise within, chunk sums added in order.
 double numpy_sum_sparse(const std::vector<int64_t>& off, const std::vector<double>& v, int64_t L) {
@@ -299,7 +334,16 @@ void one_region(const mc_reads& r, const Tables& tab, int32_t tid, int64_t start
                 RegionOut out, std::vector<uint64_t>& events) {
     const int64_t L = end - start;
     int64_t secondary = 0, improper = 0, nreads = 0, cov_sum = 0, cov2_sum = 0;
-    double covc_sum = 0, wnf = 0;
+    double wnf = 0;
+    // cov_cor (pileup.py:141): per position, the reads' 1/rcor added in read
+    // order, then np.mean's pairwise sum; materialised only once a read
+    // with rcor != 1 covers the region (with every 1/rcor == 1 the float sums
+    // are exact integers and equal cov's)
+    std::vector<double> cov_cor;
+    struct Cover {
+        int64_t a, b;
+    };
+    std::vector<Cover> unit;   // reads with 1/rcor == 1 seen before cov_cor existed
     int64_t status = kOk;
     struct Start {
         int64_t at;
@@ -364,10 +408,21 @@ void one_region(const mc_reads& r, const Tables& tab, int32_t tid, int64_t start
             rs = r.pos[i] - start;
             re = rs + rl;
         }
-        const int64_t clip = std::min(L, re) - std::max<int64_t>(0, rs);
-        if (clip > 0) {
-            cov_sum += clip;
-            covc_sum += (double)clip * inv;
+        const int64_t a0 = std::max<int64_t>(0, rs), b0 = std::min(L, re);
+        if (b0 > a0) {
+            cov_sum += b0 - a0;
+            if (cov_cor.empty() && inv != 1.0) {   // replay the unit reads so far, in order
+                cov_cor.assign((size_t)L, 0.0);
+                for (const Cover& c : unit)
+                    for (int64_t p = c.a; p < c.b; ++p) cov_cor[p] += 1.0;
+                unit.clear();
+                unit.shrink_to_fit();
+            }
+            if (!cov_cor.empty()) {
+                for (int64_t p = a0; p < b0; ++p) cov_cor[p] += inv;
+            } else {
+                unit.push_back({a0, b0});
+            }
         }
         if (rs >= 0 && rs < L) {
             starts.push_back({rs, i, inv});
@@ -397,7 +452,7 @@ void one_region(const mc_reads& r, const Tables& tab, int32_t tid, int64_t start
     out.counts[5] = (int64_t)off.size();
     out.counts[6] = cov2_sum;
     out.counts[7] = (int64_t)events.size();
-    out.sums[0] = covc_sum;
+    out.sums[0] = cov_cor.empty() ? (double)cov_sum : numpy_sum_dense(cov_cor);
     out.sums[1] = seq_sum;
     out.sums[2] = numpy_sum_sparse(off, val, L);
     out.sums[3] = wnf;

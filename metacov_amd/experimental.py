@@ -12,8 +12,8 @@ where the data does:
 * reads (host C++, `mc_experimental_reads`): one pass over the records each
   region fetches -- mate pairing by name, the k-mer correction of each read,
   pair spans -- reduced to exact aggregates instead of the reference's
-  per-position arrays (exact for every field but `covc`, whose float sum is
-  re-associated);
+  per-position arrays, exact for every field (`covc` keeps its per-position
+  float sums, in read order, once a read with 1/rcor != 1 covers the region);
 * sequence (GPU, `mc_ecor_run`): the k-mer weights of every window and the
   900-tap normal-pdf correlation, O(length x 900) fp64 per region -- the
   part that dominates the reference's run time (a Python loop with one
