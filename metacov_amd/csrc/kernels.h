@@ -1077,6 +1077,60 @@ __device__ __attribute__((noinline, cold)) void ov_add_lane(OvLds* ov, int v0, i
     }
 }
 
+// MC_OV_REGS: out-of-window runs accumulate in each lane's registers (an
+// OvReg, 8 VGPRs) while the region stays open in the chunk, and go to the
+// lane's LDS record only before the region's histogram is flushed.  On C5,
+// where the end ramps of deep contigs fall below the window, adding every
+// int4's runs to the LDS records (6 atomics) cost 0.075 ms of a 1.13 ms fused K2.
+#ifndef MC_OV_REGS
+#define MC_OV_REGS 1
+#endif
+struct OvReg {
+    unsigned cnt, low;
+    unsigned long long sum, sq;
+    int vmin, vmax;
+};
+
+__device__ __forceinline__ void ov_reg_reset(OvReg& r) {
+    r.cnt = r.low = 0;
+    r.sum = r.sq = 0;
+    r.vmin = 0x7fffffff;
+    r.vmax = 0;
+}
+
+__device__ __forceinline__ void ov_reg_take(OvReg& r, bool o, int v, int n, int base) {
+    if (o) {
+        r.cnt += n;
+        r.low += v < base ? n : 0;
+        r.sum += (unsigned long long)v * (unsigned long long)n;
+        r.sq += (unsigned long long)((long long)v * v) * (unsigned long long)n;
+        r.vmin = min(r.vmin, v);
+        r.vmax = max(r.vmax, v);
+    }
+}
+
+// a lane's accumulated out-of-window statistics into its LDS record
+__device__ __attribute__((noinline)) void ov_spill(OvLds* ov, unsigned cnt, unsigned low, unsigned long long sum,
+                                                   unsigned long long sq, int mn, int mx) {
+    if (cnt) {
+        atomicAdd(&ov->cnt, cnt);
+        if (low) atomicAdd(&ov->low, low);
+        atomicAdd(&ov->sum, sum);
+        atomicAdd(&ov->sq, sq);
+        atomicMin(&ov->vmin, mn);
+        atomicMax(&ov->vmax, mx);
+    }
+}
+
+// every lane of the wave calls it: the register record goes to LDS (before a
+// flush's barrier) and starts over
+__device__ __forceinline__ void ov_reg_spill(OvReg& r, OvLds* ovf) {
+    if (__any(r.cnt != 0)) {
+        ov_spill(ovf + (threadIdx.x & (kOvRecs - 1)), r.cnt, r.low, r.sum, r.sq, r.vmin, r.vmax);
+        ov_reg_reset(r);
+    }
+}
+
 // Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
 // one predicated LDS atomic per run of equal values, no branches except the
 // rare out-of-window path (same run arithmetic as region_seg_kernel).
@@ -1087,8 +1141,8 @@ __device__ __attribute__((noinline, cold)) void ov_add_lane(OvLds* ov, int v0, i
 // issues its atomic, lanes with nothing to add put 0 into their own pad slot;
 // the predicated form cost ~6 SALU exec-mask instructions per atomic, and the
 // fused K2 is bound by instruction issue, not by LDS (SQ counters, r02a).
-__device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, int y0, int y1, int y2,
-                                          int y3, int base) {
+__device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, OvReg& ovr, int y0, int y1,
+                                          int y2, int y3, int base) {
     const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
     const int l2 = s3 ? 1 : 2;
     const int l1 = s2 ? 1 : l2 + 1;
@@ -1114,12 +1168,22 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, int
 #endif
     const bool o0 = e0 && !w0, o1 = e1 && !w1, o2 = e2 && !w2, o3 = e3 && !w3;
 #ifndef MC_EXP_NO_OV
-    if (__builtin_expect(__any(o0 || o1 || o2 || o3), 0))
+    if (__builtin_expect(__any(o0 || o1 || o2 || o3), 0)) {
 #else
-    if (false)
+    if (false) {
 #endif
+#if MC_OV_REGS
+        (void)ov;
+        ov_reg_take(ovr, o0, y0, l0, base);
+        ov_reg_take(ovr, o1, y1, l1, base);
+        ov_reg_take(ovr, o2, y2, l2, base);
+        ov_reg_take(ovr, o3, y3, 1, base);
+#else
+        (void)ovr;
         ov_add_lane(ov + (threadIdx.x & (kOvRecs - 1)), o0 ? y0 : -1, l0, o1 ? y1 : -1, l1,
                     o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
+#endif
+    }
 }
 
 // Block-wide AND of two predicates with one barrier: each wave's votes are
@@ -1269,6 +1333,8 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     constexpr bool kDefer = MC_DEFER_STORE && !(kStats && kLong);
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
+    OvReg ovr;                 // kStats: this lane's out-of-window runs of the open region
+    ov_reg_reset(ovr);
     if (kStats) {
         for (int k = threadIdx.x; k < kHistLds; k += kBlock) hist[k] = 0;
         if (threadIdx.x < kOvRecs) ov_reset(ovf + threadIdx.x);   // ordered by the first barrier
@@ -1466,9 +1532,10 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
                             y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        hist_int4(hist_lane, hist_dummy, ovf, y0, y1, y2, y3, r_base);
+                        hist_int4(hist_lane, hist_dummy, ovf, ovr, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
+                        if (MC_OV_REGS) ov_reg_spill(ovr, ovf);
                         flush_region(R, rcur, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
@@ -1483,6 +1550,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             }
         }
         if (kDefer && pend_T0 >= 0) store_tile(pend_T0);   // the chunk's last tile
+        if (kStats && MC_OV_REGS) ov_reg_spill(ovr, ovf);   // ordered by the barrier below
         __syncthreads();   // everyone is past hdr / ring of this chunk (and its atomics)
         if (kStats) {
             // a region still open at the chunk end has partials here; the
