@@ -1716,13 +1716,21 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     unsigned long long s2 = 0;
     int lmin = 0x7fffffff, lmax = -1;
     int buf = 0;
-    for (int t0 = 0; t0 < nb; t0 += kBlock * 4, buf ^= 1) {
-        const int b = t0 + (int)threadIdx.x * 4;
-        long long c[4];
+    // tiles of kBlock x kFinRun bins: thread t owns kFinRun consecutive bins,
+    // sums them, one 64-bit block scan gives its first rank, then it walks its
+    // bins again from registers (one barrier per tile; a C5 fallback region's
+    // ~8,000 bins are one tile)
+    constexpr int kFinRun = 32;
+    for (int t0 = 0; t0 < nb; t0 += kBlock * kFinRun, buf ^= 1) {
+        const int b = t0 + (int)threadIdx.x * kFinRun;
+        unsigned c[kFinRun];
+        long long mine = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            c[k] = b + k < nb ? (long long)hr[b + k] + (b + k == 0 ? zx_bin : 0) : 0;
-        const long long mine = c[0] + c[1] + c[2] + c[3];
+        for (int k = 0; k < kFinRun; ++k) {
+            c[k] = b + k < nb ? hr[b + k] : 0u;
+            mine += c[k];
+        }
+        if (b == 0) mine += zx_bin;
         long long incl = mine;               // 64-bit wave scan
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -1739,22 +1747,24 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
             tile += tw;
         }
         running += tile;
+        if (mine) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const long long cnt = c[k];
-            if (cnt == 0) continue;
-            const long long v = base + b + k;
-            const long long e = cum + cnt;
-            if (r_lo >= cum && r_lo < e) s_med[0] = v;
-            if (r_hi >= cum && r_hi < e) s_med[1] = v;
-            const long long lo = cum > q_lo ? cum : q_lo;
-            const long long hi = e < q_hi ? e : q_hi;
-            if (hi > lo) qsum += (hi - lo) * v;
-            s1 += cnt * v;
-            s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
-            lmin = min(lmin, b + k);
-            lmax = max(lmax, b + k);
-            cum = e;
+            for (int k = 0; k < kFinRun; ++k) {
+                const long long cnt = (long long)c[k] + (b + k == 0 ? zx_bin : 0);
+                if (cnt == 0) continue;
+                const long long v = base + b + k;
+                const long long e = cum + cnt;
+                if (r_lo >= cum && r_lo < e) s_med[0] = v;
+                if (r_hi >= cum && r_hi < e) s_med[1] = v;
+                const long long lo = cum > q_lo ? cum : q_lo;
+                const long long hi = e < q_hi ? e : q_hi;
+                if (hi > lo) qsum += (hi - lo) * v;
+                s1 += cnt * v;
+                s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
+                lmin = min(lmin, b + k);
+                lmax = max(lmax, b + k);
+                cum = e;
+            }
         }
     }
     const long long in_hist = running - low;
