@@ -198,6 +198,8 @@ struct mc_ctx {
     DevBuf<unsigned> d_flow;
     DevBuf<unsigned> d_fhist;
     HostMapped<int> h_fflag;              // fallback flags, written by region_final_kernel
+    bool fused_clean = false;             // K3b left hist / low / acc / queue initialised
+    int64_t fused_clean_R = 0;
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
@@ -705,7 +707,8 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     int grid = 0;
     if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))
         return rc;
-    if (!stats) {   // the fused path's fused_init_kernel zeroes them
+    if (!stats) {   // the fused path's fused_init_kernel (or the last K3b) zeroes them
+        ctx->fused_clean = false;   // this K2 consumes the queue
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 32, s));
         HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
     }
@@ -813,6 +816,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
                    (long long)end[r]);
     }
     if (R == 0) return MC_OK;
+    ctx->fused_clean = false;   // d_acc is shared with the fused path
     if (int rc = fetch_max_depth(ctx)) return rc;
     const int nbins = ctx->max_depth + 1;
     hipStream_t s = ctx->stream;
@@ -954,7 +958,11 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     HIP_TRY(ctx->d_acc.reserve(R));
     unsigned char* d = ctx->fstage.d.p;
     const int64_t* d_fge = reinterpret_cast<const int64_t*>(d + o_ge);
-    {
+    // the previous call's K3b left the fused buffers initialised for this
+    // region set (no fallback, nothing else used them since): no init launch
+    const bool clean = ctx->fused_clean && ctx->fused_clean_R == R && ctx->fcache.chunk_first;
+    ctx->fused_clean = false;
+    if (!clean) {
         // the chunk -> first region index depends only on the staged region
         // set: built once per set (the binary searches are most of this
         // launch), reused by repeated calls
@@ -987,7 +995,7 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                        reinterpret_cast<const int64_t*>(d + o_ntot),
                        reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,
                        reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,
-                       ctx->d_maxdepth.p, ctx->h_fflag.d + R);
+                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
@@ -1006,6 +1014,10 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
             fr_idx.push_back(r);
         }
     ctx->fused_fallbacks = (int64_t)ft.size();
+    if (ft.empty()) {    // K3b reset the buffers behind it
+        ctx->fused_clean = true;
+        ctx->fused_clean_R = R;
+    }
     if (!ft.empty()) {   // exact recompute, rows written in place
         if (int rc = region_stats_impl(ctx, (int64_t)ft.size(), ft.data(), fs.data(), fe.data(),
                                        d_out, fr_idx.data()))

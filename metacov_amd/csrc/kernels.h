@@ -1843,17 +1843,26 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
 constexpr int kFinPer = (kHistBins + 63) / 64;
 
 __global__ void __launch_bounds__(kBlock)
-region_final_wave_kernel(const unsigned* __restrict__ hist, int64_t R,
-                         const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
+region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
+                         RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
                          const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
                          int* __restrict__ fallback, const int32_t* __restrict__ base_of,
-                         const unsigned* __restrict__ low_of, const int* __restrict__ max_depth,
-                         int* __restrict__ max_out) {
+                         unsigned* __restrict__ low_of, int* __restrict__ max_depth,
+                         int* __restrict__ max_out, unsigned* __restrict__ queue) {
     const int lane = threadIdx.x & 63;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && max_out) *max_out = *max_depth;
+    // queue != null: leave the fused buffers as fused_init_kernel does (zero
+    // histograms and below-window counts, initial accumulators, K2's queue
+    // and max depth), so a repeated call on the same regions skips that launch
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (max_out) *max_out = *max_depth;
+        if (queue) {
+            for (int k = 0; k < 4; ++k) max_depth[k] = 0;
+            for (int k = 0; k < 8; ++k) queue[k] = 0;
+        }
+    }
     const int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
     if (r >= R) return;
-    const unsigned* hr = hist + r * kHistBins;
+    unsigned* hr = hist + r * kHistBins;
     const long long n = n_total[r];
     const long long zx = n_zero_extra[r];
     const long long base = base_of[r];
@@ -1869,6 +1878,11 @@ region_final_wave_kernel(const unsigned* __restrict__ hist, int64_t R,
         const int b = b0 + k;
         c[k] = b < kHistBins ? (long long)hr[b] + (b == 0 ? zx_bin : 0) : 0;
         mine += c[k];
+    }
+    if (queue) {
+#pragma unroll
+        for (int k = 0; k < kFinPer; ++k)
+            if (b0 + k < kHistBins && c[k]) hr[b0 + k] = 0;
     }
     long long incl = mine;                   // 64-bit wave scan
 #pragma unroll
@@ -1913,6 +1927,13 @@ region_final_wave_kernel(const unsigned* __restrict__ hist, int64_t R,
     fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi))
                       ? 1 : 0;
     const RegionAcc a = acc[r];
+    if (queue) {
+        acc[r].sum = 0;
+        acc[r].sumsq = 0;
+        acc[r].min = 0x7fffffff;
+        acc[r].max = 0;
+        low_of[r] = 0;
+    }
     RegionOut o;
     o.n = n;
     const long long high = n - win_hi;       // values above the window

@@ -606,3 +606,69 @@ def test_fused_timing_totals(eng):
     dk3 = t1["fused_stats_ms_total"] - t0["fused_stats_ms_total"]
     assert dk2 > 0 and dk3 > 0
     assert dk2 >= t1["depth_ms"] * 0.99   # three launches, the last one among them
+
+
+def test_fused_clean_buffers_across_mixed_calls(eng):
+    """K3b leaves the fused buffers initialised for the next call on the same
+    regions (no init launch); a plain K2, a K3 pass, a fallback or a
+    re-prepare in between must not leave stale queue / histogram state."""
+    lengths, tid, pos, span = make_case([60_000, 90_000, 30_000], 30_000, (1, 300), 31)
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    whole = (np.arange(3, dtype=np.int32), np.zeros(3, np.int64), np.asarray(lengths, np.int64))
+    want = coracle.region_stats(d, ext, coff, *whole)
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+
+    def fused():
+        got = eng.compute_depth_stats(*whole)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+
+    def plain():
+        eng.compute_depth()
+        got = eng.region_stats(*whole)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+        assert np.array_equal(eng.depth(1), d[coff[1]:coff[1] + lengths[1]])
+
+    for step in (fused, fused, fused, plain, fused, fused, plain, plain, fused):
+        step()
+    eng.invalidate()      # re-prepare the same reads: restaged regions, init again
+    fused()
+    fused()
+    # a region set with a fallback (a contig whose depth ramps from 4000 to 0:
+    # its quartile ranks span far more values than the histogram window)
+    lt = np.zeros(4000, np.int32)
+    lp = np.zeros(4000, np.int32)
+    ls = np.random.default_rng(3).integers(1, 5001, 4000).astype(np.int32)
+    t2 = np.concatenate([tid, lt + 3])
+    o = np.lexsort((np.concatenate([pos, lp]), t2))
+    lengths2 = np.array(list(lengths) + [5_000], np.int64)
+    t2, p2, s2 = t2[o], np.concatenate([pos, lp])[o], np.concatenate([span, ls])[o]
+    eng.set_contigs(lengths2)
+    eng.add_reads(t2, p2, s2)
+    d2, ext2, coff2 = coracle.depth(lengths2, t2, p2, s2)
+    regs2 = (np.arange(4, dtype=np.int32), np.zeros(4, np.int64), lengths2)
+    want2 = coracle.region_stats(d2, ext2, coff2, *regs2)
+    for _ in range(3):
+        got = eng.compute_depth_stats(*regs2)
+        for f in want2.dtype.names:
+            assert np.array_equal(got[f], want2[f]), f
+        assert eng.fused_fallbacks() >= 1
+
+
+def test_invalidate_reprepares_same_reads(eng):
+    """mc_invalidate drops the prepared index; the next compute call
+    re-prepares the same device reads and gives the same results."""
+    lengths, tid, pos, span = make_case([70_000, 40_000], 20_000, (1, 400), 37)
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    regs = (np.arange(2, dtype=np.int32), np.zeros(2, np.int64), np.asarray(lengths, np.int64))
+    want = coracle.region_stats(d, ext, coff, *regs)
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+    for _ in range(3):
+        eng.invalidate()
+        got = eng.compute_depth_stats(*regs)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), f
+    assert eng.aligned_bases() == int(span.astype(np.int64).sum())
