@@ -1154,6 +1154,15 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, OvR
                w2 = e2 && b2 < (unsigned)kHistBins, w3 = e3 && b3 < (unsigned)kHistBins;
 #ifdef MC_EXP_NO_HIST
     asm volatile("" :: "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(l0), "v"(l1), "v"(l2));
+#elif defined(MC_EXP_NO_CONFLICT)   // diagnostic (wrong results): every lane its own bin
+    {
+        const int lb = (int)(threadIdx.x & 63) * 8 % (kHistBins - 8);
+        atomicAdd(&h[lb], w0 ? (unsigned)l0 : 0u);
+        atomicAdd(&h[lb + 1], w1 ? (unsigned)l1 : 0u);
+        atomicAdd(&h[lb + 2], w2 ? (unsigned)l2 : 0u);
+        atomicAdd(&h[lb + 3], w3 ? 1u : 0u);
+        (void)b0; (void)b1; (void)b2; (void)b3; (void)dummy;
+    }
 #elif MC_HIST_BRANCHLESS
     atomicAdd(&h[w0 ? (int)b0 : dummy], w0 ? (unsigned)l0 : 0u);
     atomicAdd(&h[w1 ? (int)b1 : dummy], w1 ? (unsigned)l1 : 0u);
