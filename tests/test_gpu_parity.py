@@ -672,3 +672,53 @@ def test_invalidate_reprepares_same_reads(eng):
         for f in want.dtype.names:
             assert np.array_equal(got[f], want[f]), f
     assert eng.aligned_bases() == int(span.astype(np.int64).sum())
+
+
+def _edge_index_cases():
+    """Read layouts aimed at ingest_kernel's chunk index (base chunks of
+    16 Ki positions on genomes of >= 2048 chunks, 8 Ki below that)."""
+    cases = {}
+    # starts exactly on base-chunk boundaries, reads crossing them, reads ending on
+    # them: 8 Ki base chunks (a small genome) and 16 Ki ones (>= 2048 full chunks)
+    for name, W, length in (("on_boundaries_8k", 8192, 40 * 8192),
+                            ("on_boundaries_16k", 16384, 72 * 10**6)):
+        lengths = np.array([length], np.int64)
+        k = np.arange(1, 40) * (length // 40 // W) * W
+        p = np.sort(np.concatenate([k, k - 100, k - 1, k + 1, k - W // 2]))
+        s = np.tile(np.array([100, 150, 1, 4096, 5000, W // 2], np.int32), len(p) // 6 + 1)[:len(p)]
+        cases[name] = (lengths, np.zeros(len(p), np.int32), p.astype(np.int32), s)
+    # sparse reads over long empty stretches, many empty contigs, a read at the very end
+    lengths = np.array([3 * 10**6, 5, 0, 2 * 10**6, 7, 1 * 10**6], np.int64)
+    t = np.array([0, 0, 0, 3, 3, 5], np.int32)
+    p = np.array([17, 1_500_000, 2_999_990, 0, 1_999_999, 999_999], np.int32)
+    s = np.array([300, 20_000, 50, 1, 40, 1], np.int32)
+    cases["sparse_tail"] = (lengths, t, p, s)
+    # 1..3 reads (partial int4 groups)
+    for k in (1, 2, 3):
+        lengths = np.array([100_000], np.int64)
+        cases["n%d" % k] = (lengths, np.zeros(k, np.int32),
+                            np.array([5, 16_380, 16_383][:k], np.int32), np.array([10, 9, 4000][:k], np.int32))
+    # overhangs (the second ingest pass) together with long reads (the long path)
+    rng = np.random.default_rng(11)
+    lengths = np.array([50_000, 80_000, 30_000], np.int64)
+    t = rng.integers(0, 3, 6000).astype(np.int32)
+    p = (rng.random(6000) * lengths[t]).astype(np.int32)
+    s = np.where(rng.random(6000) < 0.3, rng.integers(4097, 30_000, 6000),
+                 rng.integers(1, 300, 6000)).astype(np.int32)
+    o = np.lexsort((p, t))
+    cases["overhang_long"] = (lengths, t[o], p[o], s[o])
+    return cases
+
+
+@pytest.mark.parametrize("name", sorted(_edge_index_cases()))
+def test_index_edge_layouts(eng, name):
+    lengths, tid, pos, span = _edge_index_cases()[name]
+    run_engine(eng, lengths, tid, pos, span)
+    d, ext, coff = check_depth_vs_oracle(eng, lengths, tid, pos, span)
+    assert eng.aligned_bases() == int(span.astype(np.int64).sum())
+    whole = (np.arange(len(lengths), dtype=np.int32), np.zeros(len(lengths), np.int64),
+             np.maximum(lengths, 1))
+    want = coracle.region_stats(d, ext, coff, *whole)
+    got = eng.compute_depth_stats(*whole)
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
