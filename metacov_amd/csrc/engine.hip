@@ -527,7 +527,10 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ingest_kernel, kBlock, 0));
-        ctx->ingest_grid = ncu * std::max(1, per);
+#ifndef MC_INGEST_GRID_PCT
+#define MC_INGEST_GRID_PCT 100   // experiment knob: ingest grid as a percentage of the resident WGs
+#endif
+        ctx->ingest_grid = std::max(1, ncu * std::max(1, per) * MC_INGEST_GRID_PCT / 100);
     }
     // ---- layout for given extents: contig offsets and chunk geometry.  One
     // chunk index serves both K2 variants: its base chunks are the plain K2's,
