@@ -956,7 +956,8 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                  o_nzx = L.nzx, o_brow = L.brow;
     HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
-    HIP_TRY(ctx->d_fhist.reserve((size_t)(R * kHistBins)));
+    const int vals = fused_hist_vals(ctx->has_long);   // values per region row
+    HIP_TRY(ctx->d_fhist.reserve((size_t)(R * vals)));
     HIP_TRY(ctx->h_fflag.reserve(R + 1));
     HIP_TRY(ctx->d_acc.reserve(R));
     unsigned char* d = ctx->fstage.d.p;
@@ -970,10 +971,10 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         // set: built once per set (the binary searches are most of this
         // launch), reused by repeated calls
         const int64_t idx_chunks = ctx->fcache.chunk_first ? 0 : ctx->n_chunks;
-        const int64_t work = std::max<int64_t>({R * kHistBins / 4, R, idx_chunks});
+        const int64_t work = std::max<int64_t>({R * vals / 4, R, idx_chunks});
         const unsigned g = (unsigned)std::min<int64_t>(4096, (work + kBlock - 1) / kBlock);
         hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
-                           ctx->d_fhist.p, R * kHistBins, ctx->d_flow.p, ctx->d_acc.p, R, d_fge, nf,
+                           ctx->d_fhist.p, R * vals, ctx->d_flow.p, ctx->d_acc.p, R, d_fge, nf,
                            ctx->chunk_w, idx_chunks, ctx->d_fchunk.p, ctx->d_queue.p,
                            ctx->d_maxdepth.p);
         HIP_TRY(hipGetLastError());
@@ -993,12 +994,16 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     // K3b: its span is timed from K2's end event (one event fewer per call)
     ctx->stats_after_depth = true;
     // one wave per region; flags [0, R) and K2's max depth [R] land in mapped host memory
-    hipLaunchKernelGGL(region_final_wave_kernel, dim3((unsigned)((R + kWaves - 1) / kWaves)),
-                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,
-                       reinterpret_cast<const int64_t*>(d + o_ntot),
-                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,
-                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,
-                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p);
+#define MC_LAUNCH_K3B(V)                                                                         \
+    hipLaunchKernelGGL(region_final_wave_kernel<V>, dim3((unsigned)((R + kWaves - 1) / kWaves)),  \
+                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,                        \
+                       reinterpret_cast<const int64_t*>(d + o_ntot),                              \
+                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,         \
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,               \
+                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p)
+    if (vals == kHistBins) MC_LAUNCH_K3B(kHistBins);
+    else MC_LAUNCH_K3B(2 * kHistBins);
+#undef MC_LAUNCH_K3B
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
@@ -1052,6 +1057,9 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     // histogram window of each region: kHistBins values, kWinBelow of them
     // below its contig's estimated body depth
     std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
+    // the long-read K2 packs two values per bin: a window twice as wide
+    const int vals = fused_hist_vals(ctx->has_long);
+    const int64_t win_below = (int64_t)kWinBelow * vals / kHistBins;
     const double span_mean = ctx->n_reads ? (double)ctx->aligned_bases / (double)ctx->n_reads : 0.0;
     std::vector<Reg> regs;
     regs.reserve(R);
@@ -1073,14 +1081,14 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         // below, 123 at 3 / 4)
         const double body = ext > 2 * span_mean ? (double)ext - span_mean : (double)ext;
         const double depth_est = ext > 0 ? (double)ctx->cbases[tid[r]] / body : 0.0;
-        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(depth_est) - kWinBelow);
+        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(depth_est) - win_below);
         if (b > a)
             regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
     }
     std::sort(regs.begin(), regs.end(), [](const Reg& x, const Reg& y) { return x.gs < y.gs; });
     bool overlap = false;
     for (size_t k = 1; k < regs.size(); ++k) overlap |= regs[k].gs < regs[k - 1].ge;
-    const bool fusable = R > 0 && !overlap && R * (int64_t)kHistBins <= (int64_t(1) << 28);
+    const bool fusable = R > 0 && !overlap && R * (int64_t)vals <= (int64_t(1) << 28);
     if (!fusable) {
         FusedRegions none{};
         if (int rc = launch_depth(ctx, none)) return rc;

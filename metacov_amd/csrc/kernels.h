@@ -1137,10 +1137,29 @@ __device__ __forceinline__ void ov_reg_spill(OvReg& r, OvLds* ovf) {
 #ifndef MC_HIST_BRANCHLESS
 #define MC_HIST_BRANCHLESS 1
 #endif
+#ifndef MC_HIST_PACK_LONG
+// 1: the long-read fused K2 packs two values per bin (hist_int4).  C5 A/B (bench
+// --config c5): fallback regions 123 -> 25, but K2 +0.025 ms for the packing
+// arithmetic and K3b no faster (its fixed cost is the fallback round trip,
+// not the number of regions in it): step 1.305 -> 1.335 ms.  Off.
+#define MC_HIST_PACK_LONG 0
+#endif
+// values per region row of the global fused histogram
+__host__ __device__ constexpr int fused_hist_vals(bool long_reads) {
+    return (long_reads && MC_HIST_PACK_LONG) ? 2 * kHistBins : kHistBins;
+}
 // dummy: this lane's pad slot (index into h).  MC_HIST_BRANCHLESS: every slot
 // issues its atomic, lanes with nothing to add put 0 into their own pad slot;
 // the predicated form cost ~6 SALU exec-mask instructions per atomic, and the
 // fused K2 is bound by instruction issue, not by LDS (SQ counters, r02a).
+// kPack (the long-read variant): a bin holds two values as 16-bit counters
+// (value base + 2b in the low half, base + 2b + 1 in the high half), so the
+// same LDS and the same one atomic per run cover a window of 2 kHistBins
+// values.  A half cannot carry: a chunk has 32 Ki positions and the bins are
+// flushed at every chunk end, and the copies split those positions.  The
+// wider window is what the ramps of deep contigs need (their quartile ranks
+// span more than kHistBins values: a fallback to K3 otherwise).
+template <bool kPack>
 __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, OvReg& ovr, int y0, int y1,
                                           int y2, int y3, int base) {
     const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
@@ -1148,32 +1167,39 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, OvR
     const int l1 = s2 ? 1 : l2 + 1;
     const int l0 = s1 ? 1 : l1 + 1;
     const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
-    const unsigned b0 = (unsigned)(y0 - base), b1 = (unsigned)(y1 - base),
-                   b2 = (unsigned)(y2 - base), b3 = (unsigned)(y3 - base);
-    const bool w0 = e0 && b0 < (unsigned)kHistBins, w1 = e1 && b1 < (unsigned)kHistBins,
-               w2 = e2 && b2 < (unsigned)kHistBins, w3 = e3 && b3 < (unsigned)kHistBins;
+    constexpr unsigned kWin = kPack ? 2u * kHistBins : (unsigned)kHistBins;
+    const unsigned d0 = (unsigned)(y0 - base), d1 = (unsigned)(y1 - base),
+                   d2 = (unsigned)(y2 - base), d3 = (unsigned)(y3 - base);
+    const bool w0 = e0 && d0 < kWin, w1 = e1 && d1 < kWin, w2 = e2 && d2 < kWin, w3 = e3 && d3 < kWin;
+    const unsigned b0 = kPack ? d0 >> 1 : d0, b1 = kPack ? d1 >> 1 : d1, b2 = kPack ? d2 >> 1 : d2,
+                   b3 = kPack ? d3 >> 1 : d3;
+    // the run lengths, shifted into their value's half
+    const unsigned i0 = kPack ? (unsigned)l0 << ((d0 & 1u) << 4) : (unsigned)l0;
+    const unsigned i1 = kPack ? (unsigned)l1 << ((d1 & 1u) << 4) : (unsigned)l1;
+    const unsigned i2 = kPack ? (unsigned)l2 << ((d2 & 1u) << 4) : (unsigned)l2;
+    const unsigned i3 = kPack ? 1u << ((d3 & 1u) << 4) : 1u;
 #ifdef MC_EXP_NO_HIST
     asm volatile("" :: "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(l0), "v"(l1), "v"(l2));
 #elif defined(MC_EXP_NO_CONFLICT)   // diagnostic (wrong results): every lane its own bin
     {
         const int lb = (int)(threadIdx.x & 63) * 8 % (kHistBins - 8);
-        atomicAdd(&h[lb], w0 ? (unsigned)l0 : 0u);
-        atomicAdd(&h[lb + 1], w1 ? (unsigned)l1 : 0u);
-        atomicAdd(&h[lb + 2], w2 ? (unsigned)l2 : 0u);
-        atomicAdd(&h[lb + 3], w3 ? 1u : 0u);
+        atomicAdd(&h[lb], w0 ? i0 : 0u);
+        atomicAdd(&h[lb + 1], w1 ? i1 : 0u);
+        atomicAdd(&h[lb + 2], w2 ? i2 : 0u);
+        atomicAdd(&h[lb + 3], w3 ? i3 : 0u);
         (void)b0; (void)b1; (void)b2; (void)b3; (void)dummy;
     }
 #elif MC_HIST_BRANCHLESS
-    atomicAdd(&h[w0 ? (int)b0 : dummy], w0 ? (unsigned)l0 : 0u);
-    atomicAdd(&h[w1 ? (int)b1 : dummy], w1 ? (unsigned)l1 : 0u);
-    atomicAdd(&h[w2 ? (int)b2 : dummy], w2 ? (unsigned)l2 : 0u);
-    atomicAdd(&h[w3 ? (int)b3 : dummy], w3 ? 1u : 0u);
+    atomicAdd(&h[w0 ? (int)b0 : dummy], w0 ? i0 : 0u);
+    atomicAdd(&h[w1 ? (int)b1 : dummy], w1 ? i1 : 0u);
+    atomicAdd(&h[w2 ? (int)b2 : dummy], w2 ? i2 : 0u);
+    atomicAdd(&h[w3 ? (int)b3 : dummy], w3 ? i3 : 0u);
 #else
     (void)dummy;
-    if (w0) atomicAdd(&h[b0], (unsigned)l0);
-    if (w1) atomicAdd(&h[b1], (unsigned)l1);
-    if (w2) atomicAdd(&h[b2], (unsigned)l2);
-    if (w3) atomicAdd(&h[b3], 1u);
+    if (w0) atomicAdd(&h[b0], i0);
+    if (w1) atomicAdd(&h[b1], i1);
+    if (w2) atomicAdd(&h[b2], i2);
+    if (w3) atomicAdd(&h[b3], i3);
 #endif
     const bool o0 = e0 && !w0, o1 = e1 && !w1, o2 = e2 && !w2, o3 = e3 && !w3;
 #ifndef MC_EXP_NO_OV
@@ -1239,7 +1265,7 @@ __device__ __forceinline__ void load_events(EvBatch& e, const int32_t* __restric
 // into the region's global accumulator and flushes the LDS histogram.
 // kBarriers = false: the caller has just passed a barrier after the last
 // atomics, and a barrier follows before the histogram is used again.
-template <bool kBarriers = true>
+template <bool kBarriers = true, bool kPack = false>
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
                                              OvLds* ov) {
 #ifdef MC_EXP_NO_FLUSH
@@ -1258,14 +1284,20 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, u
             ov_reset(o);
         }
     }
-    unsigned* g = R.hist + (int64_t)id * kHistBins;
+    // the region's row holds one counter per value: kHistBins, or 2 kHistBins packed
+    unsigned* g = R.hist + (int64_t)id * (kPack ? 2 * kHistBins : kHistBins);
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
         unsigned cnt = 0;
 #pragma unroll
         for (int c = 0; c < kHistCopies; ++c) cnt += h[c * kHistStride + k];
         if (cnt) {
 #ifndef MC_EXP_NO_GATOMIC
-            atomicAdd(&g[k], cnt);
+            if (kPack) {
+                if (cnt & 0xffffu) atomicAdd(&g[2 * k], cnt & 0xffffu);
+                if (cnt >> 16) atomicAdd(&g[2 * k + 1], cnt >> 16);
+            } else {
+                atomicAdd(&g[k], cnt);
+            }
 #endif
 #pragma unroll
             for (int c = 0; c < kHistCopies; ++c) h[c * kHistStride + k] = 0;
@@ -1340,6 +1372,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     // deferred tile stores: not in the fused long-read variant, which is at its
     // register budget (C5 fused +0.9 %; plain C3 -2.4 %, C5 -4.9 %, fused C3 -1.2 %)
     constexpr bool kDefer = MC_DEFER_STORE && !(kStats && kLong);
+    constexpr bool kPack = kStats && kLong && MC_HIST_PACK_LONG;   // see hist_int4
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
     OvReg ovr;                 // kStats: this lane's out-of-window runs of the open region
@@ -1541,11 +1574,11 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                             y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
                             y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        hist_int4(hist_lane, hist_dummy, ovf, ovr, y0, y1, y2, y3, r_base);
+                        hist_int4<kPack>(hist_lane, hist_dummy, ovf, ovr, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
                         if (MC_OV_REGS) ov_reg_spill(ovr, ovf);
-                        flush_region(R, rcur, hist, ovf);
+                        flush_region<true, kPack>(R, rcur, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = uload(R.gs, rcur);
@@ -1564,7 +1597,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (kStats) {
             // a region still open at the chunk end has partials here; the
             // barrier above and the one after the ring zeroing bracket it
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false>(R, rcur, hist, ovf);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, kPack>(R, rcur, hist, ovf);
         }
         if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks, qk);
     }
@@ -1849,8 +1882,7 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
 // 40 us).  Lane L owns bins [L * kFinPer, L * kFinPer + kFinPer).  Block 0
 // also copies K2's max depth to max_out (mapped host memory: the fallback
 // path needs it without a device-to-host copy).
-constexpr int kFinPer = (kHistBins + 63) / 64;
-
+template <int kVals>
 __global__ void __launch_bounds__(kBlock)
 region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
                          RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
@@ -1858,6 +1890,7 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
                          int* __restrict__ fallback, const int32_t* __restrict__ base_of,
                          unsigned* __restrict__ low_of, int* __restrict__ max_depth,
                          int* __restrict__ max_out, unsigned* __restrict__ queue) {
+    constexpr int kFinPer = (kVals + 63) / 64;
     const int lane = threadIdx.x & 63;
     // queue != null: leave the fused buffers as fused_init_kernel does (zero
     // histograms and below-window counts, initial accumulators, K2's queue
@@ -1871,7 +1904,7 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     }
     const int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
     if (r >= R) return;
-    unsigned* hr = hist + r * kHistBins;
+    unsigned* hr = hist + r * kVals;
     const long long n = n_total[r];
     const long long zx = n_zero_extra[r];
     const long long base = base_of[r];
@@ -1885,13 +1918,13 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
 #pragma unroll
     for (int k = 0; k < kFinPer; ++k) {
         const int b = b0 + k;
-        c[k] = b < kHistBins ? (long long)hr[b] + (b == 0 ? zx_bin : 0) : 0;
+        c[k] = b < kVals ? (long long)hr[b] + (b == 0 ? zx_bin : 0) : 0;
         mine += c[k];
     }
     if (queue) {
 #pragma unroll
         for (int k = 0; k < kFinPer; ++k)
-            if (b0 + k < kHistBins && c[k]) hr[b0 + k] = 0;
+            if (b0 + k < kVals && c[k]) hr[b0 + k] = 0;
     }
     long long incl = mine;                   // 64-bit wave scan
 #pragma unroll
