@@ -122,6 +122,31 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
     return v;
 }
 
+// 64-bit lane moves on DPP (two 32-bit halves, same control), for the
+// 64-bit scans and sums of the statistics kernels
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ long long dpp64(long long v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffff), kCtrl, kRowMask, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), kCtrl, kRowMask, 0xf, false);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ long long wave_incl_scan64(long long v) {
+    v += dpp64<0x111, 0xf>(v);   // row_shr:1
+    v += dpp64<0x112, 0xf>(v);   // row_shr:2
+    v += dpp64<0x114, 0xf>(v);   // row_shr:4
+    v += dpp64<0x118, 0xf>(v);   // row_shr:8
+    v += dpp64<0x142, 0xa>(v);   // row_bcast:15
+    v += dpp64<0x143, 0xc>(v);   // row_bcast:31
+    return v;
+}
+
+__device__ __forceinline__ long long readlane64(long long v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
@@ -1926,13 +1951,10 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
         for (int k = 0; k < kFinPer; ++k)
             if (b0 + k < kVals && c[k]) hr[b0 + k] = 0;
     }
-    long long incl = mine;                   // 64-bit wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const long long y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    const long long in_hist = __shfl(incl, 63, 64);
+    // 64-bit wave scan on DPP (the __shfl_up / __shfl_xor version went through
+    // ds_bpermute: C5's 10,000 regions took 33 us of LDS permutes)
+    const long long incl = wave_incl_scan64(mine);
+    const long long in_hist = readlane64(incl, 63);
     long long cum = low + incl - mine;
     long long qsum = 0, s1 = 0, med_lo = -1, med_hi = -1;
     unsigned long long s2 = 0;
@@ -1954,16 +1976,18 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
         lmax = max(lmax, b0 + k);
         cum = e;
     }
-    qsum = wave_sum64(qsum);
-    s1 = wave_sum64(s1);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        s2 += __shfl_xor(s2, d, 64);
-        med_lo = max(med_lo, (long long)__shfl_xor(med_lo, d, 64));
-        med_hi = max(med_hi, (long long)__shfl_xor(med_hi, d, 64));
+    qsum = readlane64(wave_incl_scan64(qsum), 63);
+    s1 = readlane64(wave_incl_scan64(s1), 63);
+    s2 = (unsigned long long)readlane64(wave_incl_scan64((long long)s2), 63);
+    // the one lane holding each rank, the first / last lane holding a bin
+    const unsigned long long hm_lo = __ballot(med_lo >= 0), hm_hi = __ballot(med_hi >= 0);
+    med_lo = hm_lo ? readlane64(med_lo, __ffsll((long long)hm_lo) - 1) : -1;
+    med_hi = hm_hi ? readlane64(med_hi, __ffsll((long long)hm_hi) - 1) : -1;
+    const unsigned long long hb = __ballot(lmax >= 0);
+    if (hb) {
+        lmin = __builtin_amdgcn_readlane(lmin, __ffsll((long long)hb) - 1);
+        lmax = __builtin_amdgcn_readlane(lmax, 63 - __builtin_clzll(hb));
     }
-    lmin = wave_min(lmin);
-    lmax = wave_max(lmax);
     if (lane != 0) return;
     const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
     fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi))
