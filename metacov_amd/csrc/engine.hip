@@ -126,6 +126,26 @@ struct Stage {
 
 inline size_t stage_align(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Page-locked host memory (hipHostMalloc): copies from / to it are plain
+// DMAs, not staged through a bounce buffer as pageable copies are.
+struct Pinned {
+    void* h = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        release();
+        hipError_t e = hipHostMalloc(&h, n, hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        else h = nullptr;
+        return e;
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = nullptr;
+        cap = 0;
+    }
+};
+
 }  // namespace
 
 struct mc_ctx {
@@ -170,9 +190,10 @@ struct mc_ctx {
     bool depth_valid = false;
     int32_t max_depth = -1;
 
-    DevBuf<unsigned long long> d_scratch;   // ingest counters
-    DevBuf<long long> d_maxend;
-    DevBuf<unsigned long long> d_cbases;
+    // ingest results: [0, 8) counters, [8, 8 + nc) furthest ends, [8 + nc,
+    // 8 + 2 nc) aligned bases per contig; one memset, one copy back
+    DevBuf<unsigned long long> d_scratch;
+    Pinned pin_io;                        // contig offsets up, ingest results down
     std::vector<unsigned long long> cbases;   // aligned bases per contig
     DevBuf<unsigned> d_queue;
     DevBuf<int> d_maxdepth;
@@ -271,8 +292,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_scan_part.release();
     ctx->d_depth.release();
     ctx->d_scratch.release();
-    ctx->d_maxend.release();
-    ctx->d_cbases.release();
+    ctx->pin_io.release();
     ctx->d_queue.release();
     ctx->d_maxdepth.release();
     ctx->k3_stage.release();
@@ -517,8 +537,11 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     // events in LDS; longer ones take the bucketed long-read path.
     ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
-    HIP_TRY(ctx->d_maxend.reserve(std::max<int32_t>(nc, 1)));
-    HIP_TRY(ctx->d_cbases.reserve(std::max<int32_t>(nc, 1)));
+    const size_t n_res = 8 + 2 * (size_t)nc;   // ingest results (see d_scratch)
+    HIP_TRY(ctx->d_scratch.reserve(n_res));
+    HIP_TRY(ctx->pin_io.reserve((n_res + nc + 1) * 8));
+    unsigned long long* res = static_cast<unsigned long long*>(ctx->pin_io.h);
+    int64_t* coff_up = reinterpret_cast<int64_t*>(res + n_res);
     HIP_TRY(ctx->d_coff.reserve(nc + 1));
     if (n && ctx->ingest_grid <= 0) {
         // one resident wave per range: a second round of waves would start
@@ -574,16 +597,14 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     // the pass runs again on the final layout
     std::vector<int64_t> ext(ctx->len);
     layout(ext);
-    unsigned long long h[4];
-    std::vector<long long> maxend(std::max<int32_t>(nc, 1));
-    ctx->cbases.assign(std::max<int32_t>(nc, 1), 0);
+    const unsigned long long* h = res;                         // counters
+    const long long* maxend = reinterpret_cast<const long long*>(res + 8);
     for (int pass = 0;; ++pass) {
         const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every full chunk's base chunks
         HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
-        HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, ctx->coff.data(), (nc + 1) * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(ctx->d_cbases.p, 0, std::max<int32_t>(nc, 1) * 8, s));
-        HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, 8 * sizeof(unsigned long long), s));
-        HIP_TRY(hipMemsetAsync(ctx->d_maxend.p, 0, std::max<int32_t>(nc, 1) * sizeof(long long), s));
+        std::memcpy(coff_up, ctx->coff.data(), (nc + 1) * 8);   // (pass 1's copy has drained)
+        HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, coff_up, (nc + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, n_res * 8, s));
         if (n) {
             HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0xff, 2 * n_base * 8, s));   // no crossing read
             IngestIndex ix{ctx->d_coff.p, 0, ctx->short_max, n_base, ctx->d_chunk_first.p};
@@ -592,15 +613,13 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
                                                                       ctx->ingest_grid));
             hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
                                ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
-                               ctx->d_maxend.p, ctx->d_cbases.p, ix);
+                               reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
+                               ctx->d_scratch.p + 8 + nc, ix);
             HIP_TRY(hipGetLastError());
         } else {
             HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * n_base * 8, s));
         }
-        HIP_TRY(hipMemcpyAsync(h, ctx->d_scratch.p, sizeof h, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(maxend.data(), ctx->d_maxend.p, maxend.size() * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(ctx->cbases.data(), ctx->d_cbases.p, ctx->cbases.size() * 8,
-                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(res, ctx->d_scratch.p, n_res * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         MC_REQUIRE(h[0] == 0, MC_E_INVALID,
                    "%llu reads have tid outside [0, %d), negative pos or negative span", h[0], nc);
@@ -619,6 +638,8 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     }
     ctx->aligned_bases = (int64_t)h[2];
     ctx->max_span = (int32_t)h[3];
+    ctx->cbases.assign(res + 8 + nc, res + 8 + 2 * nc);
+    if (ctx->cbases.empty()) ctx->cbases.assign(1, 0);
     const int64_t off = ctx->total_len;
     const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
     const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
