@@ -1783,21 +1783,13 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     unsigned long long s2 = 0;
     int lmin = 0x7fffffff, lmax = -1;
     int buf = 0;
-    // tiles of kBlock x kFinRun bins: thread t owns kFinRun consecutive bins,
-    // sums them, one 64-bit block scan gives its first rank, then it walks its
-    // bins again from registers (one barrier per tile; a C5 fallback region's
-    // ~8,000 bins are one tile)
-    constexpr int kFinRun = 32;
-    for (int t0 = 0; t0 < nb; t0 += kBlock * kFinRun, buf ^= 1) {
-        const int b = t0 + (int)threadIdx.x * kFinRun;
-        unsigned c[kFinRun];
-        long long mine = 0;
+    for (int t0 = 0; t0 < nb; t0 += kBlock * 4, buf ^= 1) {
+        const int b = t0 + (int)threadIdx.x * 4;
+        long long c[4];
 #pragma unroll
-        for (int k = 0; k < kFinRun; ++k) {
-            c[k] = b + k < nb ? hr[b + k] : 0u;
-            mine += c[k];
-        }
-        if (b == 0) mine += zx_bin;
+        for (int k = 0; k < 4; ++k)
+            c[k] = b + k < nb ? (long long)hr[b + k] + (b + k == 0 ? zx_bin : 0) : 0;
+        const long long mine = c[0] + c[1] + c[2] + c[3];
         long long incl = mine;               // 64-bit wave scan
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -1814,24 +1806,22 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
             tile += tw;
         }
         running += tile;
-        if (mine) {
 #pragma unroll
-            for (int k = 0; k < kFinRun; ++k) {
-                const long long cnt = (long long)c[k] + (b + k == 0 ? zx_bin : 0);
-                if (cnt == 0) continue;
-                const long long v = base + b + k;
-                const long long e = cum + cnt;
-                if (r_lo >= cum && r_lo < e) s_med[0] = v;
-                if (r_hi >= cum && r_hi < e) s_med[1] = v;
-                const long long lo = cum > q_lo ? cum : q_lo;
-                const long long hi = e < q_hi ? e : q_hi;
-                if (hi > lo) qsum += (hi - lo) * v;
-                s1 += cnt * v;
-                s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
-                lmin = min(lmin, b + k);
-                lmax = max(lmax, b + k);
-                cum = e;
-            }
+        for (int k = 0; k < 4; ++k) {
+            const long long cnt = c[k];
+            if (cnt == 0) continue;
+            const long long v = base + b + k;
+            const long long e = cum + cnt;
+            if (r_lo >= cum && r_lo < e) s_med[0] = v;
+            if (r_hi >= cum && r_hi < e) s_med[1] = v;
+            const long long lo = cum > q_lo ? cum : q_lo;
+            const long long hi = e < q_hi ? e : q_hi;
+            if (hi > lo) qsum += (hi - lo) * v;
+            s1 += cnt * v;
+            s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
+            lmin = min(lmin, b + k);
+            lmax = max(lmax, b + k);
+            cum = e;
         }
     }
     const long long in_hist = running - low;
@@ -1937,33 +1927,30 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     const long long low = (long long)low_of[r] + (base == 0 ? 0 : zx);
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;
     const long long q_lo = n / 4, q_hi = n - n / 4;
-    const int b0 = lane * kFinPer;
+    // bins k * 64 + lane (row k of the region's bins: one coalesced load per
+    // row), a 64-bit DPP scan per row carried across rows
     long long c[kFinPer];
-    long long mine = 0;
 #pragma unroll
     for (int k = 0; k < kFinPer; ++k) {
-        const int b = b0 + k;
+        const int b = k * 64 + lane;
         c[k] = b < kVals ? (long long)hr[b] + (b == 0 ? zx_bin : 0) : 0;
-        mine += c[k];
     }
     if (queue) {
 #pragma unroll
         for (int k = 0; k < kFinPer; ++k)
-            if (b0 + k < kVals && c[k]) hr[b0 + k] = 0;
+            if (k * 64 + lane < kVals && c[k]) hr[k * 64 + lane] = 0;
     }
-    // 64-bit wave scan on DPP (the __shfl_up / __shfl_xor version went through
-    // ds_bpermute: C5's 10,000 regions took 33 us of LDS permutes)
-    const long long incl = wave_incl_scan64(mine);
-    const long long in_hist = readlane64(incl, 63);
-    long long cum = low + incl - mine;
     long long qsum = 0, s1 = 0, med_lo = -1, med_hi = -1;
     unsigned long long s2 = 0;
-    int lmin = 0x7fffffff, lmax = -1;
+    long long run = low;                      // ranks before row k
 #pragma unroll
     for (int k = 0; k < kFinPer; ++k) {
         const long long cnt = c[k];
+        const long long incl = wave_incl_scan64(cnt);
+        const long long cum = run + incl - cnt;
+        run += readlane64(incl, 63);
         if (cnt == 0) continue;
-        const long long v = base + b0 + k;
+        const long long v = base + k * 64 + lane;
         const long long e = cum + cnt;
         if (r_lo >= cum && r_lo < e) med_lo = v;
         if (r_hi >= cum && r_hi < e) med_hi = v;
@@ -1972,9 +1959,25 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
         if (hi > lo) qsum += (hi - lo) * v;
         s1 += cnt * v;
         s2 += (unsigned long long)cnt * (unsigned long long)(v * v);
-        lmin = min(lmin, b0 + k);
-        lmax = max(lmax, b0 + k);
-        cum = e;
+    }
+    const long long in_hist = run - low;
+    // the lowest and highest occupied bins
+    int lmin = 0x7fffffff, lmax = -1;
+#pragma unroll
+    for (int k = 0; k < kFinPer; ++k) {
+        const unsigned long long m = __ballot(c[k] != 0);
+        if (m) {
+            lmin = k * 64 + __ffsll((long long)m) - 1;
+            break;
+        }
+    }
+#pragma unroll
+    for (int k = kFinPer - 1; k >= 0; --k) {
+        const unsigned long long m = __ballot(c[k] != 0);
+        if (m) {
+            lmax = k * 64 + 63 - __builtin_clzll(m);
+            break;
+        }
     }
     qsum = readlane64(wave_incl_scan64(qsum), 63);
     s1 = readlane64(wave_incl_scan64(s1), 63);
@@ -1983,11 +1986,6 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     const unsigned long long hm_lo = __ballot(med_lo >= 0), hm_hi = __ballot(med_hi >= 0);
     med_lo = hm_lo ? readlane64(med_lo, __ffsll((long long)hm_lo) - 1) : -1;
     med_hi = hm_hi ? readlane64(med_hi, __ffsll((long long)hm_hi) - 1) : -1;
-    const unsigned long long hb = __ballot(lmax >= 0);
-    if (hb) {
-        lmin = __builtin_amdgcn_readlane(lmin, __ffsll((long long)hb) - 1);
-        lmax = __builtin_amdgcn_readlane(lmax, 63 - __builtin_clzll(hb));
-    }
     if (lane != 0) return;
     const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
     fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi))
