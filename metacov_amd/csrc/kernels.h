@@ -266,18 +266,19 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     constexpr int64_t kStep = 64 * U;
     const int64_t per = ((n4 + n_waves - 1) / n_waves + kStep - 1) / kStep * kStep;
     const int64_t g0 = gw * per, g1 = min(n4, g0 + per);
-    long long bad = 0, unsorted = 0, bases = 0;
+    long long bases = 0;
+    unsigned nbad = 0, nuns = 0;
     int mspan = 0;
     IngestAcc acc;
     // the read before the wave's range (every wave checks its first read too);
-    // carry_g = -1: none (the first read of all: boundaries from 1 on)
-    int carry_t = -1, carry_p = 0;
-    int64_t carry_g = -1;
+    // carry_c = -1: none (the first read of all: boundaries from 1 on)
+    int carry_t = -1, carry_p = 0, carry_c = -1;   // carry_c: its base chunk
     if (g0 < g1 && g0 > 0) {
         carry_t = uload(tid, g0 * 4 - 1);
         carry_p = uload(pos, g0 * 4 - 1);
-        if (carry_t >= 0 && carry_t < n_contigs && carry_p >= 0)
-            carry_g = uload(X.coff, carry_t) + carry_p;
+        const int carry_s = uload(span, g0 * 4 - 1);
+        if (carry_t >= 0 && carry_t < n_contigs && (carry_p | carry_s) >= 0)
+            carry_c = (int)((uload(X.coff, carry_t) + carry_p) >> X.lw);
     }
     i32x4 ct[U], cp[U], cs[U], nt[U], np[U], ns[U];
 #define MC_INGEST_LOAD(T, P, S, GB)                                                  \
@@ -308,6 +309,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         }
         carry_t = __builtin_amdgcn_readlane(ct[U - 1].w, 63);
         carry_p = __builtin_amdgcn_readlane(cp[U - 1].w, 63);
+        // validity and order, branch-free (32-bit per-lane counters)
         unsigned todo = 0;   // bit 4u+k: valid live read
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -316,25 +318,27 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int j = 4 * u + k;
-                const bool live = q < g1 && q * 4 + k < n;
-                if (!live) continue;
+                // past the end: every later slot of the lane is past it too
+                const bool live = (q < g1) & (q * 4 + k < n);
                 const int t = tt[j], p = ps[j], sp = ss[j];
-                if (t < 0 || t >= n_contigs || p < 0 || sp < 0) {
-                    ++bad;
-                } else {
-                    if (tp > t || (tp == t && pp > p)) ++unsorted;
-                    todo |= 1u << j;
-                }
+                const bool ok = ((unsigned)t < (unsigned)n_contigs) & ((p | sp) >= 0);
+                const bool uns = (tp > t) | ((tp == t) & (pp > p));
+                nbad += (live & !ok) ? 1u : 0u;
+                nuns += (live & ok & uns) ? 1u : 0u;
+                todo |= (live & ok) ? 1u << j : 0u;
                 tp = t;
                 pp = p;
             }
         }
         const unsigned valid = todo;
         // per contig of this step (one, unless the wave crosses a boundary):
-        // global starts, bases / max end / max span into the running record
-        int64_t g[4 * U];
+        // base chunk ids and offsets in 32 bits (contig offset c0 = hi * w +
+        // lo, lo < w: the chunk of c0 + p is hi + ((lo + p) >> lw)), bases /
+        // max end / max span into the running record
+        int cid[4 * U], off[4 * U];
 #pragma unroll
-        for (int j = 0; j < 4 * U; ++j) g[j] = -1;
+        for (int j = 0; j < 4 * U; ++j) cid[j] = off[j] = -1;
+        const unsigned wmask = (1u << X.lw) - 1u;
         for (;;) {
             int cand = -1;
 #pragma unroll
@@ -344,17 +348,22 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             if (!act) break;
             const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
             const int64_t c0 = uload(X.coff, t0);
-            long long b = 0, e = 0;
+            const int c0hi = (int)(c0 >> X.lw);
+            const unsigned c0lo = (unsigned)c0 & wmask;
+            unsigned long long b = 0;
+            unsigned e = 0;
             int m = 0;
 #pragma unroll
-            for (int j = 0; j < 4 * U; ++j)
-                if (((todo >> j) & 1u) && tt[j] == t0) {
-                    b += ss[j];
-                    e = max(e, (long long)ps[j] + ss[j]);
-                    m = max(m, ss[j]);
-                    g[j] = c0 + ps[j];
-                    todo &= ~(1u << j);
-                }
+            for (int j = 0; j < 4 * U; ++j) {
+                const bool in = ((todo >> j) & 1u) & (tt[j] == t0);
+                const unsigned rel = c0lo + (unsigned)ps[j];
+                b += in ? (unsigned)ss[j] : 0u;
+                e = max(e, in ? (unsigned)ps[j] + (unsigned)ss[j] : 0u);
+                m = max(m, in ? ss[j] : 0);
+                cid[j] = in ? c0hi + (int)(rel >> X.lw) : cid[j];
+                off[j] = in ? (int)(rel & wmask) : off[j];
+                todo &= in ? ~(1u << j) : ~0u;
+            }
             mspan = max(mspan, m);
             bases += b;
             if (t0 != acc.cur) {
@@ -362,39 +371,36 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 acc.cur = t0;
             }
             acc.bases += b;
-            acc.end = max(acc.end, e);
+            acc.end = max(acc.end, (long long)e);
         }
         // chunk index: boundaries m*w with prev < m*w <= g get "first read at
         // or after" = i (usually none between two neighbouring starts); the
         // last read of all also closes every boundary after it with n
-        int64_t gprev[U];
+        int cprev[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t up = shfl_up_i64(g[4 * u + 3]);
-            const int64_t l0 = u ? readlane_i64(g[4 * u - 1], 63) : carry_g;
-            gprev[u] = lane ? up : l0;
+            const int up = __shfl_up(cid[4 * u + 3], 1, 64);
+            const int l0 = u ? __builtin_amdgcn_readlane(cid[4 * u - 1], 63) : carry_c;
+            cprev[u] = lane ? up : l0;
         }
-        carry_g = readlane_i64(g[4 * U - 1], 63);
+        carry_c = __builtin_amdgcn_readlane(cid[4 * U - 1], 63);
         // bit j of bnd: a base chunk boundary lies in (prev start, start]
         // (rare: one read in ~1,600 at C3); bit j of cross: a short read
         // crossing the boundary after its start
         unsigned bnd = 0, cross = 0;
-        int mc[4 * U];
+        const int w = 1 << X.lw;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            int cp_id = gprev[u] < 0 ? -1 : (int)(gprev[u] >> X.lw);
+            int cp_id = cprev[u];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int j = 4 * u + k;
-                const int cid = (int)(g[j] >> X.lw);
                 const int sp = ss[j];
-                const bool ok = (valid >> j) & 1u;
-                if (ok && cid > cp_id) bnd |= 1u << j;
-                mc[j] = cid + 1;
-                if (ok && sp > 0 && sp <= X.short_max && cid + 1 < X.n_base &&
-                    (int)((g[j] + sp - 1) >> X.lw) > cid)
-                    cross |= 1u << j;
-                cp_id = ok ? cid : -1;
+                const bool ok = (valid >> j) & 1u;   // cid[j] = -1 otherwise
+                bnd |= (ok & (cid[j] > cp_id)) ? 1u << j : 0u;
+                cross |= (ok & (sp > 0) & (sp <= X.short_max) & (cid[j] + 1 < X.n_base) &
+                          (off[j] + sp > w)) ? 1u << j : 0u;
+                cp_id = cid[j];
             }
         }
         if (__builtin_expect(__any(bnd != 0), 0)) {
@@ -404,16 +410,15 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 bnd &= bnd - 1;
                 const int u = j >> 2, k = j & 3;
                 const int64_t i = (gb + 64 * u + lane) * 4 + k;
-                int64_t gp = -1;
+                int cp = -1, ch = 0;
 #pragma unroll
                 for (int jj = 0; jj < 4 * U; ++jj)
-                    if (jj == j) gp = (k == 0) ? gprev[u] : (((valid >> (jj - 1)) & 1u) ? g[jj - 1] : -1);
-                const int64_t m_lo = (gp < 0 ? 0 : (gp >> X.lw)) + 1;
-                int64_t m_hi = 0;
-#pragma unroll
-                for (int jj = 0; jj < 4 * U; ++jj)
-                    if (jj == j) m_hi = g[jj] >> X.lw;
-                if (m_hi > X.n_base) m_hi = X.n_base;
+                    if (jj == j) {
+                        cp = (k == 0) ? cprev[u] : cid[jj - 1];
+                        ch = cid[jj];
+                    }
+                const int64_t m_lo = (cp < 0 ? 0 : cp) + 1;
+                const int64_t m_hi = ch < X.n_base ? ch : X.n_base;
                 for (int64_t mm = m_lo; mm <= m_hi; ++mm) X.index[2 * mm - 1] = i;
             }
         }
@@ -423,7 +428,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             for (int j = 0; j < 4 * U; ++j) {
                 const int64_t i = (gb + 64 * (j >> 2) + lane) * 4 + (j & 3);
                 if (i == n - 1 && ((valid >> j) & 1u))
-                    for (int64_t mm = (g[j] >> X.lw) + 1; mm <= X.n_base; ++mm) X.index[2 * mm - 1] = n;
+                    for (int64_t mm = (int64_t)cid[j] + 1; mm <= X.n_base; ++mm) X.index[2 * mm - 1] = n;
             }
         }
         // first crossing read per boundary: per slot, the wave's earliest
@@ -437,7 +442,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 #pragma unroll
                 for (int k = 3; k >= 0; --k)
                     if ((pend >> k) & 1u) {
-                        cm = mc[4 * u + k];
+                        cm = cid[4 * u + k] + 1;
                         ck = k;
                     }
                 const unsigned long long act = __ballot(cm >= 0);
@@ -449,7 +454,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                               (unsigned long long)((gb + 64 * u + lane) * 4 + ck));
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (((pend >> k) & 1u) && mc[4 * u + k] == m0) pend &= ~(1u << k);
+                    if (((pend >> k) & 1u) && cid[4 * u + k] + 1 == m0) pend &= ~(1u << k);
             }
         }
 #pragma unroll
@@ -465,8 +470,8 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     // wave of the grid serialise at the end of the launch
     __shared__ long long red[4][kWaves];
     const int wave = threadIdx.x >> 6;
-    bad = wave_sum64(bad);
-    unsorted = wave_sum64(unsorted);
+    const long long bad = wave_sum64(nbad);
+    const long long unsorted = wave_sum64(nuns);
     bases = wave_sum64(bases);
     mspan = wave_max(mspan);
     if (lane == 0) {
