@@ -722,3 +722,118 @@ def test_index_edge_layouts(eng, name):
     got = eng.compute_depth_stats(*whole)
     for f in want.dtype.names:
         assert np.array_equal(got[f], want[f]), f
+
+
+# ------------------------------------------------------------- large coordinates
+
+def _sparse_row(starts, ends, L):
+    """Exact stat row of region [0, L) from read intervals (clipped to it),
+    without a dense vector: the depth is piecewise constant between events,
+    so its value histogram (value -> positions) gives every classic() field
+    (test infrastructure: the dense oracle would need L int64s)."""
+    s = np.clip(starts, 0, L)
+    e = np.clip(ends, 0, L)
+    keep = e > s
+    ev = np.concatenate([s[keep], e[keep]])
+    dv = np.concatenate([np.ones(keep.sum(), np.int64), -np.ones(keep.sum(), np.int64)])
+    o = np.argsort(ev, kind="stable")
+    ev, dv = ev[o], dv[o]
+    pts = np.concatenate([[0], ev, [L]])
+    val = np.concatenate([[0], np.cumsum(dv)])          # depth on [pts[k], pts[k+1])
+    run = np.diff(pts)
+    hist = {}
+    for v, r in zip(val.tolist(), run.tolist()):
+        if r:
+            hist[v] = hist.get(v, 0) + r
+    vals = sorted(hist)
+    n = L
+
+    def at(rank):
+        c = 0
+        for v in vals:
+            c += hist[v]
+            if rank < c:
+                return v
+        raise AssertionError
+    q_lo, q_hi = n // 4, n - n // 4
+    q23, c = 0, 0
+    for v in vals:
+        lo, hi = max(c, q_lo), min(c + hist[v], q_hi)
+        if hi > lo:
+            q23 += (hi - lo) * v
+        c += hist[v]
+    return {"n": n, "sum": sum(v * k for v, k in hist.items()),
+            "sumsq": sum(v * v * k for v, k in hist.items()), "min": vals[0], "max": vals[-1],
+            "med_lo": at((n - 1) // 2), "med_hi": at(n // 2), "q23_sum": q23, "q23_cnt": q_hi - q_lo}
+
+
+def test_large_coordinates(eng):
+    """A 5.2 Gbp genome (20.8 GB depth vector): global offsets past 2^31 and
+    2^32, a contig of 2.1 Gbp (positions near the int32 limit), read clusters
+    with long reads at those boundaries and at contig ends, and an
+    overhanging read (second ingest pass on the grown layout).  Windows
+    around every cluster are checked against the oracle on the clipped reads;
+    whole contigs against the exact sparse value histogram."""
+    rng = np.random.default_rng(2024)
+    lengths = np.array([1_900_000_000, 2_100_000_000, 1_200_000_000], np.int64)
+    g0 = np.concatenate([[0], np.cumsum(lengths)])
+    centers = [(0, 0), (0, 1_000_000_000), (0, int(lengths[0]) - 1),
+               (1, 2 ** 31 - int(g0[1])), (1, 2 ** 31 - 1 - 2 ** 15 - int(g0[1]) + 5),
+               (1, int(lengths[1]) - 10), (2, 2 ** 32 - int(g0[2])), (2, int(lengths[2]) - 1)]
+    T, P, S = [], [], []
+    for t, c in centers:
+        L = int(lengths[t])
+        sp = rng.integers(100, 301, size=3000)
+        p = np.clip(c + rng.integers(-2000, 2001, size=3000), 0, L - sp)
+        T.append(np.full(3000, t)); P.append(p); S.append(sp)
+        lsp = rng.integers(5000, 50_001, size=20)
+        lp = np.clip(c - rng.integers(0, 60_001, size=20), 0, L - lsp)
+        T.append(np.full(20, t)); P.append(lp); S.append(lsp)
+    for t in range(3):   # sparse background
+        sp = np.full(50_000, 150)
+        T.append(np.full(50_000, t)); P.append(rng.integers(0, int(lengths[t]) - 150, size=50_000)); S.append(sp)
+    T.append(np.array([2])); P.append(np.array([int(lengths[2]) - 100])); S.append(np.array([400]))  # overhang
+    tid = np.concatenate(T).astype(np.int64)
+    pos = np.concatenate(P).astype(np.int64)
+    span = np.concatenate(S).astype(np.int64)
+    o = np.lexsort((pos, tid))
+    tid, pos, span = tid[o].astype(np.int32), pos[o].astype(np.int32), span[o].astype(np.int32)
+    ends = pos.astype(np.int64) + span
+
+    # windows around the clusters (non-overlapping: the fused path)
+    wt, ws, we = [], [], []
+    for t, c in centers:
+        L = int(lengths[t])
+        wt.append(t); ws.append(max(0, c - 70_000)); we.append(min(L, c + 6000))
+    wt, ws, we = np.array(wt, np.int32), np.array(ws, np.int64), np.array(we, np.int64)
+    want = []
+    for t, a, b in zip(wt, ws, we):
+        m = (tid == t) & (pos < b) & (ends > a)
+        lp = np.maximum(pos[m], a) - a
+        ls = np.minimum(ends[m], b) - np.maximum(pos[m], a)
+        o = np.argsort(lp, kind="stable")
+        dl, ext_l, coff_l = coracle.depth([b - a], np.zeros(m.sum(), np.int32),
+                                          lp[o].astype(np.int32), ls[o].astype(np.int32))
+        want.append((dl[:b - a], coracle.region_stats(dl, ext_l, coff_l, np.zeros(1, np.int32),
+                                                      np.zeros(1, np.int64), np.array([b - a], np.int64))))
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+    got = eng.compute_depth_stats(wt, ws, we)
+    assert eng.contig_offset(2)[1] == lengths[2] + 300          # grown by the overhang
+    assert eng.contig_offset(1)[0] < 2 ** 31 < eng.contig_offset(2)[0] < 2 ** 32 < eng.contig_offset(2)[0] + lengths[2]
+    for k, (t, a, b) in enumerate(zip(wt, ws, we)):
+        dl, row = want[k]
+        for f in row.dtype.names:
+            assert got[f][k] == row[f][0], (k, f)
+        assert np.array_equal(eng.depth(int(t), int(a), int(b)), dl), k
+    # the unfused path (K2 + K3) on the same windows
+    got2 = eng.region_stats(wt, ws, we)
+    for f in got.dtype.names:
+        assert np.array_equal(got2[f], got[f]), f
+    # whole contigs, fused
+    rows = eng.compute_depth_stats(np.arange(3, dtype=np.int32), np.zeros(3, np.int64), lengths)
+    for t in range(3):
+        m = tid == t
+        exp = _sparse_row(pos[m].astype(np.int64), ends[m], int(lengths[t]))
+        for f, v in exp.items():
+            assert int(rows[f][t]) == v, (t, f)
