@@ -41,6 +41,7 @@ template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;   // elements
+    uint64_t gen = 0; // allocations so far (a cache key: a new block may reuse the old address)
     hipError_t reserve(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) {
@@ -55,12 +56,14 @@ struct DevBuf {
             return e;
         }
         cap = n;
+        ++gen;
         return hipSuccess;
     }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
+        ++gen;
     }
 };
 
@@ -155,6 +158,8 @@ struct mc_ctx {
 
     std::vector<int64_t> len, extent, coff;   // coff: n_contigs + 1
     DevBuf<int64_t> d_len, d_coff;
+    std::vector<int64_t> coff_dev;            // what d_coff holds (allocation coff_dev_gen)
+    uint64_t coff_dev_gen = ~0ull;
 
     int64_t n_reads = 0;
     DevBuf<int32_t> d_tid, d_pos, d_span;
@@ -215,6 +220,11 @@ struct mc_ctx {
         std::vector<int64_t> start, end;
         int64_t nf = 0;
         bool chunk_first = false;   // d_fchunk holds this region set's chunk -> region index
+        // the layout the staged arrays were built on (a re-prepare that keeps
+        // it keeps them, the window bases aside)
+        int vals = 0;
+        int64_t chunk_w = 0, n_chunks = 0;
+        std::vector<int64_t> extent, coff;
     } fcache;
     DevBuf<unsigned> d_flow;
     DevBuf<unsigned> d_fhist;
@@ -531,8 +541,8 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     }
     HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // K2 loads whole int4 batches past n: the tid padding must index coff
-    if (ctx->d_tid.cap > (size_t)n)
-        HIP_TRY(hipMemsetAsync(ctx->d_tid.p + n, 0, (ctx->d_tid.cap - n) * 4, s));
+    // (zeroed by prep_clear_kernel with the first ingest pass)
+    const int64_t n_pad = ctx->d_tid.cap > (size_t)n ? (int64_t)(ctx->d_tid.cap - n) : 0;
     // LDS ring of 2 tiles: reads up to short_max = ring - kTileW keep both
     // events in LDS; longer ones take the bucketed long-read path.
     ctx->ring = kRing;
@@ -602,11 +612,25 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     for (int pass = 0;; ++pass) {
         const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every full chunk's base chunks
         HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
-        std::memcpy(coff_up, ctx->coff.data(), (nc + 1) * 8);   // (pass 1's copy has drained)
-        HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, coff_up, (nc + 1) * 8, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(ctx->d_scratch.p, 0, n_res * 8, s));
+        // the device layout is uploaded only when it changed (a new batch over
+        // the same contigs keeps it)
+        if (ctx->coff_dev != ctx->coff || ctx->coff_dev_gen != ctx->d_coff.gen) {
+            std::memcpy(coff_up, ctx->coff.data(), (nc + 1) * 8);   // (pass 1's copy has drained)
+            HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, coff_up, (nc + 1) * 8, hipMemcpyHostToDevice, s));
+            ctx->coff_dev = ctx->coff;
+            ctx->coff_dev_gen = ctx->d_coff.gen;
+        }
+        {
+            const int64_t np_ = pass == 0 ? n_pad : 0, ni = 2 * n_base;
+            const unsigned g = (unsigned)std::max<int64_t>(
+                1, std::min<int64_t>(1024, (np_ + (int64_t)n_res + ni + kBlock - 1) / kBlock));
+            hipLaunchKernelGGL(prep_clear_kernel, dim3(g), dim3(kBlock), 0, s, ctx->d_tid.p + n, np_,
+                               ctx->d_scratch.p, (int64_t)n_res,
+                               reinterpret_cast<unsigned long long*>(ctx->d_chunk_first.p), ni,
+                               n ? ~0ull : 0ull);   // all ones: no crossing read
+            HIP_TRY(hipGetLastError());
+        }
         if (n) {
-            HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0xff, 2 * n_base * 8, s));   // no crossing read
             IngestIndex ix{ctx->d_coff.p, 0, ctx->short_max, n_base, ctx->d_chunk_first.p};
             while (((int64_t)1 << ix.lw) < (int64_t)ctx->tpc_base * kTileW) ++ix.lw;
             const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
@@ -616,8 +640,6 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
                                reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
                                ctx->d_scratch.p + 8 + nc, ix);
             HIP_TRY(hipGetLastError());
-        } else {
-            HIP_TRY(hipMemsetAsync(ctx->d_chunk_first.p, 0, 2 * n_base * 8, s));
         }
         HIP_TRY(hipMemcpyAsync(res, ctx->d_scratch.p, n_res * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -1066,22 +1088,50 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     if (int rc = mc_prepare(ctx)) return rc;
     MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
     auto& fc = ctx->fcache;
-    const bool hit = R > 0 && fc.valid && fc.gen == ctx->prep_gen && (int64_t)fc.tid.size() == R &&
-                     std::memcmp(fc.tid.data(), tid, R * 4) == 0 &&
-                     std::memcmp(fc.start.data(), start, R * 8) == 0 &&
-                     std::memcmp(fc.end.data(), end, R * 8) == 0;
-    if (hit) return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
-    fc.valid = false;
-    fc.chunk_first = false;
-    const int32_t nc = (int32_t)ctx->len.size();
-    struct Reg { int64_t gs, ge; int32_t id, base; };
     // histogram window of each region: kHistBins values, kWinBelow of them
     // below its contig's estimated body depth
-    std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
     // the long-read K2 packs two values per bin: a window twice as wide
     const int vals = fused_hist_vals(ctx->has_long);
     const int64_t win_below = (int64_t)kWinBelow * vals / kHistBins;
     const double span_mean = ctx->n_reads ? (double)ctx->aligned_bases / (double)ctx->n_reads : 0.0;
+    // the contig's body depth: its aligned bases over its length less one
+    // mean read span (the two end ramps hold about half a span of depth
+    // each); the window sits mostly below it, where the quartile ranks of a
+    // contig with long-read ramps fall (C5 fallbacks: 259 at kHistBins / 2
+    // below, 123 at 3 / 4)
+    auto window_base = [&](int32_t t) {
+        const int64_t ext = ctx->extent[t];
+        const double body = ext > 2 * span_mean ? (double)ext - span_mean : (double)ext;
+        const double depth_est = ext > 0 ? (double)ctx->cbases[t] / body : 0.0;
+        return (int32_t)std::max<int64_t>(0, std::llround(depth_est) - win_below);
+    };
+    const bool same = R > 0 && fc.valid && (int64_t)fc.tid.size() == R &&
+                      std::memcmp(fc.tid.data(), tid, R * 4) == 0 &&
+                      std::memcmp(fc.start.data(), start, R * 8) == 0 &&
+                      std::memcmp(fc.end.data(), end, R * 8) == 0;
+    if (same && fc.gen == ctx->prep_gen) return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
+    if (same && fc.vals == vals && fc.chunk_w == ctx->chunk_w && fc.n_chunks == ctx->n_chunks &&
+        fc.extent == ctx->extent && fc.coff == ctx->coff) {
+        // a new batch (or a re-prepare) over the same layout: the staged
+        // regions, their order and the chunk -> region index stand; only the
+        // window bases follow the new per-contig bases (one small upload)
+        const FusedLayout L = fused_layout(fc.nf, R);
+        unsigned char* h = ctx->fstage.host();
+        int32_t* brow = reinterpret_cast<int32_t*>(h + L.brow);
+        int32_t* fbase = reinterpret_cast<int32_t*>(h + L.base);
+        const int32_t* fid = reinterpret_cast<const int32_t*>(h + L.id);
+        for (int64_t r = 0; r < R; ++r) brow[r] = window_base(tid[r]);
+        for (int64_t k = 0; k < fc.nf; ++k) fbase[k] = brow[fid[k]];
+        HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p + L.base, h + L.base, L.up - L.base, hipMemcpyHostToDevice,
+                               ctx->stream));
+        fc.gen = ctx->prep_gen;
+        return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
+    }
+    fc.valid = false;
+    fc.chunk_first = false;
+    const int32_t nc = (int32_t)ctx->len.size();
+    struct Reg { int64_t gs, ge; int32_t id, base; };
+    std::vector<int32_t> base_row(std::max<int64_t>(R, 1), 0);
     std::vector<Reg> regs;
     regs.reserve(R);
     std::vector<int64_t> ntot(std::max<int64_t>(R, 1)), nzx(std::max<int64_t>(R, 1));
@@ -1095,14 +1145,7 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
         ntot[r] = end[r] - start[r];
         nzx[r] = ntot[r] - (b - a);
-        // the contig's body depth: its aligned bases over its length less one
-        // mean read span (the two end ramps hold about half a span of depth
-        // each); the window sits mostly below it, where the quartile ranks
-        // of a contig with long-read ramps fall (C5 fallbacks: 259 at kHistBins / 2
-        // below, 123 at 3 / 4)
-        const double body = ext > 2 * span_mean ? (double)ext - span_mean : (double)ext;
-        const double depth_est = ext > 0 ? (double)ctx->cbases[tid[r]] / body : 0.0;
-        base_row[r] = (int32_t)std::max<int64_t>(0, std::llround(depth_est) - win_below);
+        base_row[r] = window_base(tid[r]);
         if (b > a)
             regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
     }
@@ -1134,6 +1177,11 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     fc.end.assign(end, end + R);
     fc.nf = nf;
     fc.gen = ctx->prep_gen;
+    fc.vals = vals;
+    fc.chunk_w = ctx->chunk_w;
+    fc.n_chunks = ctx->n_chunks;
+    fc.extent = ctx->extent;
+    fc.coff = ctx->coff;
     fc.valid = true;
     return depth_stats_launch(ctx, R, tid, start, end, d_out, nf);
 }

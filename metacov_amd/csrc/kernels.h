@@ -491,6 +491,23 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     }
 }
 
+// Prepare's buffer setup in one launch (three fills were three commands in
+// the stream ahead of ingest_kernel): the tid padding K2's whole-batch loads
+// read past n (zeros: a valid contig), the ingest counters / ends / bases
+// (zeros) and the chunk index (all ones: no crossing read yet; zeros when
+// there are no reads).
+__global__ void __launch_bounds__(kBlock)
+prep_clear_kernel(int32_t* __restrict__ tid_pad, int64_t n_pad, unsigned long long* __restrict__ scratch,
+                  int64_t n_scratch, unsigned long long* __restrict__ index, int64_t n_index,
+                  unsigned long long index_fill) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad + n_scratch + n_index; i += stride) {
+        if (i < n_pad) tid_pad[i] = 0;
+        else if (i < n_pad + n_scratch) scratch[i - n_pad] = 0;
+        else index[i - n_pad - n_scratch] = index_fill;
+    }
+}
+
 // ------------------------------------------------------ long reads (prepare)
 //
 // Reads longer than `short_max` (= ring - kTileW) cannot keep their -1 end

@@ -674,6 +674,34 @@ def test_invalidate_reprepares_same_reads(eng):
     assert eng.aligned_bases() == int(span.astype(np.int64).sum())
 
 
+def test_new_batch_same_layout_moves_windows(eng):
+    """A second batch over the same contigs and regions keeps the staged
+    region table (same layout) but must move the histogram windows to the
+    new depth: a shallow batch, then one ~3000 deep, then shallow again, each
+    exact and without fallbacks (a window left at the first batch's depth
+    would send every deep region to the K3 fallback)."""
+    lengths = [60_000, 45_000]
+    regs = (np.array([0, 1, 0], np.int32), np.array([0, 0, 30_000], np.int64),
+            np.array([30_000, 45_000, 60_000], np.int64))
+    eng.set_contigs(lengths)
+    for k, n in enumerate([4_000, 1_000_000, 6_000]):
+        rng = np.random.default_rng(70 + k)
+        t = np.sort(rng.integers(0, 2, size=n)).astype(np.int32)
+        span = rng.integers(100, 200, size=n).astype(np.int32)
+        L = np.asarray(lengths)[t]
+        pos = rng.integers(0, L - span + 1).astype(np.int32)
+        o = np.lexsort((pos, t))
+        t, pos, span = t[o], pos[o], span[o]
+        d, ext, coff = coracle.depth(lengths, t, pos, span)
+        want = coracle.region_stats(d, ext, coff, *regs)
+        eng.clear_reads()
+        eng.add_reads(t, pos, span)
+        got = eng.compute_depth_stats(*regs)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), (k, f)
+        assert eng.fused_fallbacks() == 0, k
+
+
 def _edge_index_cases():
     """Read layouts aimed at ingest_kernel's chunk index (base chunks of
     16 Ki positions on genomes of >= 2048 chunks, 8 Ki below that)."""
