@@ -732,6 +732,23 @@ static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t l
     return MC_OK;
 }
 
+// Chunk geometry of a K2 launch.  The plain K2 runs on the index's base
+// chunks unless long reads need full ones (their end buckets and carries are
+// per full chunk).  MC_FUSED_BASE_CHUNKS: the fused K2 too.
+#ifndef MC_FUSED_BASE_CHUNKS
+#define MC_FUSED_BASE_CHUNKS 0
+#endif
+struct K2Geom {
+    int tpc;
+    int64_t n_chunks, chunk_w;
+    int cstride;
+};
+static K2Geom k2_geom(const mc_ctx* ctx, bool stats) {
+    const bool full = ctx->has_long || (stats && !MC_FUSED_BASE_CHUNKS);
+    if (full) return {ctx->tiles_per_chunk, ctx->n_chunks, ctx->chunk_w, ctx->cstride};
+    return {ctx->tpc_base, ctx->n_chunks_base, (int64_t)ctx->tpc_base * kTileW, 1};
+}
+
 // K2 launch (plain or with fused region statistics)
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
@@ -743,12 +760,10 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const bool lng = ctx->has_long;
     const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
                             : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);
-    // the plain kernel's own chunk geometry when prepare built one (short reads)
-    // the plain K2 runs on the base chunks unless long reads need full ones
-    const bool full = stats || ctx->has_long;
-    const int tpc = full ? ctx->tiles_per_chunk : ctx->tpc_base;
-    const int64_t nch = full ? ctx->n_chunks : ctx->n_chunks_base;
-    const int cstride = full ? ctx->cstride : 1;
+    const K2Geom geo = k2_geom(ctx, stats);
+    const int tpc = geo.tpc;
+    const int64_t nch = geo.n_chunks;
+    const int cstride = geo.cstride;
     const int64_t* cfirst = ctx->d_chunk_first.p;
     int grid = 0;
     if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))
@@ -997,7 +1012,8 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     const FusedLayout L = fused_layout(nf, R);
     const size_t o_gs = L.gs, o_ge = L.ge, o_id = L.id, o_base = L.base, o_ntot = L.ntot,
                  o_nzx = L.nzx, o_brow = L.brow;
-    HIP_TRY(ctx->d_fchunk.reserve(ctx->n_chunks));
+    const K2Geom geo = k2_geom(ctx, true);
+    HIP_TRY(ctx->d_fchunk.reserve(geo.n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
     const int vals = fused_hist_vals(ctx->has_long);   // values per region row
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * vals)));
@@ -1013,12 +1029,12 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         // the chunk -> first region index depends only on the staged region
         // set: built once per set (the binary searches are most of this
         // launch), reused by repeated calls
-        const int64_t idx_chunks = ctx->fcache.chunk_first ? 0 : ctx->n_chunks;
+        const int64_t idx_chunks = ctx->fcache.chunk_first ? 0 : geo.n_chunks;
         const int64_t work = std::max<int64_t>({R * vals / 4, R, idx_chunks});
         const unsigned g = (unsigned)std::min<int64_t>(4096, (work + kBlock - 1) / kBlock);
         hipLaunchKernelGGL(fused_init_kernel, dim3(std::max(g, 1u)), dim3(kBlock), 0, s,
                            ctx->d_fhist.p, R * vals, ctx->d_flow.p, ctx->d_acc.p, R, d_fge, nf,
-                           ctx->chunk_w, idx_chunks, ctx->d_fchunk.p, ctx->d_queue.p,
+                           geo.chunk_w, idx_chunks, ctx->d_fchunk.p, ctx->d_queue.p,
                            ctx->d_maxdepth.p);
         HIP_TRY(hipGetLastError());
         ctx->fcache.chunk_first = true;
@@ -1110,7 +1126,8 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
                       std::memcmp(fc.start.data(), start, R * 8) == 0 &&
                       std::memcmp(fc.end.data(), end, R * 8) == 0;
     if (same && fc.gen == ctx->prep_gen) return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
-    if (same && fc.vals == vals && fc.chunk_w == ctx->chunk_w && fc.n_chunks == ctx->n_chunks &&
+    const K2Geom geo = k2_geom(ctx, true);
+    if (same && fc.vals == vals && fc.chunk_w == geo.chunk_w && fc.n_chunks == geo.n_chunks &&
         fc.extent == ctx->extent && fc.coff == ctx->coff) {
         // a new batch (or a re-prepare) over the same layout: the staged
         // regions, their order and the chunk -> region index stand; only the
@@ -1178,8 +1195,8 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     fc.nf = nf;
     fc.gen = ctx->prep_gen;
     fc.vals = vals;
-    fc.chunk_w = ctx->chunk_w;
-    fc.n_chunks = ctx->n_chunks;
+    fc.chunk_w = geo.chunk_w;
+    fc.n_chunks = geo.n_chunks;
     fc.extent = ctx->extent;
     fc.coff = ctx->coff;
     fc.valid = true;

@@ -1313,12 +1313,12 @@ __device__ __forceinline__ void load_events(EvBatch& e, const int32_t* __restric
 // kBarriers = false: the caller has just passed a barrier after the last
 // atomics, and a barrier follows before the histogram is used again.
 template <bool kBarriers = true, bool kPack = false>
-__device__ __forceinline__ void flush_region(const FusedRegions& R, int64_t r, unsigned* h,
-                                             OvLds* ov) {
+__device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsigned* h, OvLds* ov) {
 #ifdef MC_EXP_NO_FLUSH
     return;
 #endif
-    const int id = uload(R.id, r);
+    // id: the region's row, loaded with its other fields (no scalar load on
+    // the chunk end's path)
     if (kBarriers) __syncthreads();   // every wave's histogram and overflow atomics are in
     if (threadIdx.x < kOvRecs) {
         OvLds* o = ov + threadIdx.x;
@@ -1455,13 +1455,14 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         const int64_t cend = uload(chunk_first, 2 * (c + 1) * cstride - 1);   // reads of this chunk end
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
-        int r_base = 0;
+        int r_base = 0, r_id = 0;
         if (kStats) {
             rcur = uload(R.chunk_first, c);
             if (rcur < R.n) {
                 r_gs = uload(R.gs, rcur);
                 r_ge = uload(R.ge, rcur);
                 r_base = uload(R.base, rcur);
+                r_id = uload(R.id, rcur);
             }
         }
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
@@ -1625,12 +1626,13 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     }
                     if (rge <= Tend) {
                         if (MC_OV_REGS) ov_reg_spill(ovr, ovf);
-                        flush_region<true, kPack>(R, rcur, hist, ovf);
+                        flush_region<true, kPack>(R, r_id, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = uload(R.gs, rcur);
                             r_ge = uload(R.ge, rcur);
                             r_base = uload(R.base, rcur);
+                            r_id = uload(R.id, rcur);
                         }
                     } else {
                         break;
@@ -1644,7 +1646,7 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (kStats) {
             // a region still open at the chunk end has partials here; the
             // barrier above and the one after the ring zeroing bracket it
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, kPack>(R, rcur, hist, ovf);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, kPack>(R, r_id, hist, ovf);
         }
         if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks, qk);
     }
