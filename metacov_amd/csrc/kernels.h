@@ -1181,6 +1181,10 @@ __device__ __forceinline__ void ov_reg_spill(OvReg& r, OvLds* ovf) {
 // Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
 // one predicated LDS atomic per run of equal values, no branches except the
 // rare out-of-window path (same run arithmetic as region_seg_kernel).
+#ifndef MC_HALF_RING_ZERO
+#define MC_HALF_RING_ZERO 1            // K2 zeroes one tile of ring slots per chunk, not the whole ring
+#endif
+static_assert(!MC_HALF_RING_ZERO || kRing == 2 * kTileW, "the ring tail is one tile (short_max = kTileW)");
 #ifndef MC_FLUSH_VEC
 #define MC_FLUSH_VEC 1                 // histogram flush in 16-byte bin groups
 #endif
@@ -1467,10 +1471,15 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
     constexpr bool kAhead = MC_QUEUE_AHEAD || (MC_QUEUE_AHEAD_FUSED_LONG && kStats && kLong);
     int ticket = 0, qk = 0;
     if (threadIdx.x == 0) hdr[0] = take_chunk(queue, n_chunks, qk);
+    // the whole ring before the first chunk; after a chunk only the tile of
+    // slots after its last tile, where the ends of reads running past the
+    // chunk (at most short_max = one tile) landed: every tile's own slots are
+    // zeroed by its scan
+    const int ring_tail = MC_HALF_RING_ZERO ? (int)(((int64_t)tiles_per_chunk * kTileW) % kRing) : 0;
+    for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
+        *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
     for (;;) {
-        // zero the ring (also orders the hdr write before the reads)
-        for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
-            *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
+        // (the barrier also orders the hdr write before the reads)
         __syncthreads();
         const int64_t c = (unsigned)__builtin_amdgcn_readfirstlane(hdr[0]);
         if (c >= n_chunks) break;
@@ -1678,6 +1687,8 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, kPack>(R, r_id, hist, ovf);
         }
         if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks, qk);
+        for (int k = threadIdx.x * 4; k < (MC_HALF_RING_ZERO ? kTileW : kRing); k += kBlock * 4)
+            *reinterpret_cast<i32x4*>(ring + ring_tail + k) = i32x4{0, 0, 0, 0};
     }
     // one atomic per workgroup (same-address atomics of every wave at the end of
     // the launch serialise); hdr[8..11] are free once the queue is drained
