@@ -212,6 +212,16 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
 #define MC_INGEST_U 1                  // C3 prepare: 1 0.406, 2 0.426, 4 0.82 ms (VGPR-bound occupancy)
 #endif
 constexpr int kIngestU = MC_INGEST_U;
+#ifndef MC_INGEST_NT_LOAD
+// ingest's read loads non-temporal (streamed once): C3 prepare -4.5 %.  The
+// same for K2's read batches (plain +3 %), the long-read kernels (+2 %) and
+// K1's CIGAR words (+13 %) measured worse.
+#define MC_INGEST_NT_LOAD 1
+#endif
+__device__ __forceinline__ i32x4 ingest_load(const int32_t* p) {
+    if (MC_INGEST_NT_LOAD) return __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));
+    return *reinterpret_cast<const i32x4*>(p);
+}
 
 struct IngestAcc {                     // running record of contig cur (wave-uniform)
     int cur = -1;
@@ -286,9 +296,9 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         const int64_t q_ = (GB) + 64 * u + lane;                                     \
         const bool in_ = q_ < g1;                                                    \
         const int64_t o_ = in_ ? q_ * 4 : 0;                                         \
-        T[u] = *reinterpret_cast<const i32x4*>(tid + o_);                            \
-        P[u] = *reinterpret_cast<const i32x4*>(pos + o_);                            \
-        S[u] = *reinterpret_cast<const i32x4*>(span + o_);                           \
+        T[u] = ingest_load(tid + o_);                                                \
+        P[u] = ingest_load(pos + o_);                                                \
+        S[u] = ingest_load(span + o_);                                               \
     }
     if (g0 < g1) { MC_INGEST_LOAD(ct, cp, cs, g0) }
     for (int64_t gb = g0; gb < g1; gb += kStep) {
