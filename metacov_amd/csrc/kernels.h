@@ -542,7 +542,7 @@ prep_clear_kernel(int32_t* __restrict__ tid_pad, int64_t n_pad, unsigned long lo
 // 0.35 + 0.39 ms for C5's 47 M long reads, plus a host round trip for the
 // offsets.)
 #ifndef MC_LONG_PER
-#define MC_LONG_PER 8
+#define MC_LONG_PER 4                  // C5 prepare: 4 0.606, 8 0.612, 16 0.674 ms (profiles/r02za_long_per.txt)
 #endif
 constexpr int kLongPer = MC_LONG_PER;             // reads per thread and sub-range
 constexpr int kLongSub = kBlock * kLongPer;

@@ -865,3 +865,35 @@ def test_large_coordinates(eng):
         exp = _sparse_row(pos[m].astype(np.int64), ends[m], int(lengths[t]))
         for f, v in exp.items():
             assert int(rows[f][t]) == v, (t, f)
+
+
+def test_assembly_scale_contig_count(eng):
+    """A metagenome assembly's contig count: 300,000 contigs of 1-1,000 bp
+    (whole-contig regions fused: 300,000 histogram rows) with reads that
+    overhang contig ends (the second ingest pass over a grown layout), then
+    the same regions plus overlapping ones through the K2 + K3 path."""
+    rng = np.random.default_rng(300)
+    lengths = rng.integers(1, 1001, size=300_000).astype(np.int64)
+    lengths, tid, pos, span = make_case(lengths, 1_000_000, (1, 150), 301)
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    R = len(lengths)
+    rt = np.arange(R, dtype=np.int32)
+    rs = np.zeros(R, np.int64)
+    re_ = lengths.copy()
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+    got = eng.compute_depth_stats(rt, rs, re_)
+    want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
+    # overlapping regions (K2 + K3): every contig, plus a second region per 8th contig
+    k = np.arange(0, R, 8)
+    rt2 = np.concatenate([rt, rt[k]])
+    rs2 = np.concatenate([rs, lengths[k] // 3])
+    re2 = np.concatenate([re_, lengths[k] + 20])
+    got2 = eng.compute_depth_stats(rt2, rs2, re2)
+    want2 = coracle.region_stats(d, ext, coff, rt2, rs2, re2)
+    for f in want2.dtype.names:
+        assert np.array_equal(got2[f], want2[f]), f
+    for t in (0, 1, R // 2, R - 1):
+        assert np.array_equal(eng.depth(t, 0, int(ext[t])), d[coff[t]:coff[t] + ext[t]])
