@@ -949,7 +949,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
         if (nseg) {
             if (lds_hist)
                 hipLaunchKernelGGL(region_seg_kernel<true>, dim3((unsigned)nseg), dim3(kBlock),
-                                   (size_t)nbins * 4, s, ctx->d_depth.p, d_seg_gs, d_seg_ge,
+                                   (size_t)round_up(nbins, 4) * 4, s, ctx->d_depth.p, d_seg_gs, d_seg_ge,
                                    d_seg_reg, nbins, ctx->d_hist.p, ctx->d_acc.p);
             else
                 hipLaunchKernelGGL(region_seg_kernel<false>, dim3((unsigned)nseg), dim3(kBlock), 0,

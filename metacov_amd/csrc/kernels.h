@@ -1765,12 +1765,14 @@ region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__
     const int r = seg_reg[sgi];
     unsigned* ghist = hist + (int64_t)r * nbins;
     unsigned* hh = kLdsHist ? h : ghist;
-    if (kLdsHist) {
-        for (int k = threadIdx.x; k < nbins; k += kBlock) h[k] = 0;
+    if (kLdsHist) {   // 16-byte stores (the LDS block is rounded up to whole int4s)
+        for (int k = threadIdx.x * 4; k < nbins; k += kBlock * 4)
+            *reinterpret_cast<i32x4*>(h + k) = i32x4{0, 0, 0, 0};
         __syncthreads();
     }
     constexpr int kU = 4;                                // int4 loads in flight per thread
     int vmax = 0;
+    unsigned vmin = 0xffffffffu;                         // (unsigned: the -1 pads never win)
     const int64_t a4 = gs & ~(int64_t)3;
     for (int64_t p0 = a4 + (int64_t)threadIdx.x * 4; p0 < ge; p0 += (int64_t)kBlock * 4 * kU) {
         i32x4 x[kU];
@@ -1797,13 +1799,30 @@ region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__
             if (s2 && y2 >= 0) atomicAdd(&hh[y2], (unsigned)l2);
             if (s3 && y3 >= 0) atomicAdd(&hh[y3], 1u);
             vmax = max(vmax, max(max(y0, y1), max(y2, y3)));
+            if (kLdsHist)
+                vmin = min(vmin, min(min((unsigned)y0, (unsigned)y1), min((unsigned)y2, (unsigned)y3)));
         }
     }
     vmax = wave_max(vmax);                   // bounds K3b's scan of this region's bins
     if ((threadIdx.x & 63) == 0 && vmax > 0) atomicMax(&acc[r].max, vmax);
     if (kLdsHist) {
+        // flush only the segment's value range [lo, hi] (its bins are all
+        // that can be non-zero; the fallback regions of the fused path have
+        // ~16 Ki bins of which a segment touches a few hundred)
+        __shared__ int ext[2 * kWaves];
+        const int wmin = wave_min((int)min(vmin, 0x7fffffffu));
+        if ((threadIdx.x & 63) == 0) {
+            ext[threadIdx.x >> 6] = wmin;
+            ext[kWaves + (threadIdx.x >> 6)] = vmax;
+        }
         __syncthreads();
-        for (int k = threadIdx.x; k < nbins; k += kBlock) {
+        int lo = ext[0], hi = ext[kWaves];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) {
+            lo = min(lo, ext[w]);
+            hi = max(hi, ext[kWaves + w]);
+        }
+        for (int k = lo + threadIdx.x; k <= hi && k < nbins; k += kBlock) {
             const unsigned c = h[k];
             if (c) atomicAdd(&ghist[k], c);
         }
