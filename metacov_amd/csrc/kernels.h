@@ -1195,9 +1195,6 @@ __device__ __forceinline__ void ov_reg_spill(OvReg& r, OvLds* ovf) {
 #define MC_HALF_RING_ZERO 1            // K2 zeroes one tile of ring slots per chunk, not the whole ring
 #endif
 static_assert(!MC_HALF_RING_ZERO || kRing == 2 * kTileW, "the ring tail is one tile (short_max = kTileW)");
-#ifndef MC_FLUSH_VEC
-#define MC_FLUSH_VEC 1                 // histogram flush in 16-byte bin groups
-#endif
 #ifndef MC_HIST_BRANCHLESS
 #define MC_HIST_BRANCHLESS 1
 #endif
@@ -1350,32 +1347,6 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsi
     }
     // the region's row holds one counter per value: kHistBins, or 2 kHistBins packed
     unsigned* g = R.hist + (int64_t)id * (kPack ? 2 * kHistBins : kHistBins);
-#if MC_FLUSH_VEC
-    if (!kPack) {
-        // 4 bins per thread: one 16-byte LDS read per copy, one pass (the
-        // per-bin loop was 4 dependent LDS round trips per thread)
-        static_assert(kHistBins % 4 == 0 && kHistStride % 4 == 0, "16-byte bin groups");
-        for (int q = threadIdx.x; q < kHistBins / 4; q += kBlock) {
-            i32x4 sum = *reinterpret_cast<const i32x4*>(h + 4 * q);
-#pragma unroll
-            for (int c = 1; c < kHistCopies; ++c)
-                sum += *reinterpret_cast<const i32x4*>(h + c * kHistStride + 4 * q);
-            if ((sum.x | sum.y | sum.z | sum.w) != 0) {
-#ifndef MC_EXP_NO_GATOMIC
-                if (sum.x) atomicAdd(&g[4 * q], (unsigned)sum.x);
-                if (sum.y) atomicAdd(&g[4 * q + 1], (unsigned)sum.y);
-                if (sum.z) atomicAdd(&g[4 * q + 2], (unsigned)sum.z);
-                if (sum.w) atomicAdd(&g[4 * q + 3], (unsigned)sum.w);
-#endif
-#pragma unroll
-                for (int c = 0; c < kHistCopies; ++c)
-                    *reinterpret_cast<i32x4*>(h + c * kHistStride + 4 * q) = i32x4{0, 0, 0, 0};
-            }
-        }
-        if (kBarriers) __syncthreads();
-        return;
-    }
-#endif
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
         unsigned cnt = 0;
 #pragma unroll
