@@ -897,3 +897,36 @@ def test_assembly_scale_contig_count(eng):
         assert np.array_equal(got2[f], want2[f]), f
     for t in (0, 1, R // 2, R - 1):
         assert np.array_equal(eng.depth(t, 0, int(ext[t])), d[coff[t]:coff[t] + ext[t]])
+
+
+def test_bench_json_contract(tmp_path):
+    """bench.py's one JSON line carries the fields the driver and the judge
+    read (metric / value / unit / roofline / cpu_baseline ...), on a short C2
+    run with a small CPU baseline sample."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", "c2", "--steps", "3",
+                          "--warmup", "1", "--prepare-steps", "2", "--cpu-sample-bases", "2e7",
+                          "--cpu-threads", "2"],
+                         capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert "workload" in d["config"]
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    c = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in c, k
+    assert c["value"] > 0 and c["kind"] in ("port", "reference")
