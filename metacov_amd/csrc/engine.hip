@@ -163,6 +163,7 @@ struct mc_ctx {
 
     int64_t n_reads = 0;
     DevBuf<int32_t> d_tid, d_pos, d_span;
+    DevBuf<uint32_t> d_gpos;              // K2's read starts (MC_GPOS; ingest_kernel)
     // raw-CIGAR mode
     bool spans_pending = false;
     DevBuf<int64_t> d_cig_off;
@@ -292,6 +293,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_tid.release();
     ctx->d_pos.release();
     ctx->d_span.release();
+    ctx->d_gpos.release();
     ctx->d_cig_off.release();
     ctx->d_cigar.release();
     ctx->d_chunk_first.release();
@@ -631,6 +633,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             HIP_TRY(hipGetLastError());
         }
         if (n) {
+            if (MC_GPOS) HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kBatch)));   // whole-batch loads
             IngestIndex ix{ctx->d_coff.p, 0, ctx->short_max, n_base, ctx->d_chunk_first.p};
             while (((int64_t)1 << ix.lw) < (int64_t)ctx->tpc_base * kTileW) ++ix.lw;
             const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
@@ -638,7 +641,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
                                ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
                                reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
-                               ctx->d_scratch.p + 8 + nc, ix);
+                               ctx->d_scratch.p + 8 + nc, ix, MC_GPOS ? ctx->d_gpos.p : nullptr);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipMemcpyAsync(res, ctx->d_scratch.p, n_res * 8, hipMemcpyDeviceToHost, s));
@@ -777,9 +780,10 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
+    const ReadArrays ra{ctx->d_gpos.p, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p};
 #define MC_LAUNCH_K2(S, L)                                                                     \
-    hipLaunchKernelGGL((depth_kernel<S, L>), dim3(grid), dim3(kBlock), lds, s, ctx->d_tid.p,     \
-                       ctx->d_pos.p, ctx->d_span.p, ctx->n_reads, ctx->d_coff.p,                  \
+    hipLaunchKernelGGL((depth_kernel<S, L>), dim3(grid), dim3(kBlock), lds, s, ra,               \
+                       ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr)
     if (stats) {

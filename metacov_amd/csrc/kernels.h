@@ -69,6 +69,14 @@ namespace mc {
 #ifndef MC_SCALAR_COFF
 #define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
 #endif
+#ifndef MC_GPOS
+// K2 reads each read as (low 32 bits of its global start, span), 8 B/read,
+// instead of (tid, pos, span), 12 B/read, and needs no contig offsets:
+// ingest_kernel writes the starts (4 B/read more in prepare).  Chunk-relative
+// starts are exact in 32-bit wrap-around arithmetic, since every read K2
+// applies starts within one tile before its chunk or inside it.
+#define MC_GPOS 1
+#endif
 
 constexpr int kBlock = 256;            // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
@@ -267,7 +275,7 @@ __global__ void __launch_bounds__(kBlock)
 ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
               const int32_t* __restrict__ span, int64_t n, int32_t n_contigs,
               unsigned long long* __restrict__ out, long long* __restrict__ maxend,
-              unsigned long long* __restrict__ cbases, IngestIndex X) {
+              unsigned long long* __restrict__ cbases, IngestIndex X, uint32_t* __restrict__ gpos) {
     constexpr int U = kIngestU;
     const int lane = threadIdx.x & 63;
     const int64_t n4 = (n + 3) / 4;
@@ -382,6 +390,19 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             }
             acc.bases += b;
             acc.end = max(acc.end, (long long)e);
+        }
+        if (MC_GPOS && gpos) {   // K2's starts: coff[tid] + pos mod 2^32 (= chunk * w + offset)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t q = gb + 64 * u + lane;
+                unsigned g[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    g[k] = ((unsigned)cid[4 * u + k] << X.lw) + (unsigned)off[4 * u + k];
+                if (q < g1)
+                    *reinterpret_cast<i32x4*>(gpos + q * 4) =
+                        i32x4{(int)g[0], (int)g[1], (int)g[2], (int)g[3]};
+            }
         }
         // chunk index: boundaries m*w with prev < m*w <= g get "first read at
         // or after" = i (usually none between two neighbouring starts); the
@@ -946,7 +967,19 @@ struct ReadBatch {                     // 4 reads in chunk-relative coordinates
 };
 
 struct RawBatch {                      // one batch of reads as loaded (int4 per array)
+#if MC_GPOS
+    i32x4 g, s;                        // low 32 bits of the global start, span
+#else
     i32x4 t, p, s;
+#endif
+};
+
+// The read arrays K2 loads: gpos (MC_GPOS) or tid + pos, and span
+struct ReadArrays {
+    const uint32_t* __restrict__ gpos;
+    const int32_t* __restrict__ tid;
+    const int32_t* __restrict__ pos;
+    const int32_t* __restrict__ span;
 };
 
 // Issue the three 16-byte loads of this thread's 4 reads.  The arrays are
@@ -955,29 +988,45 @@ struct RawBatch {                      // one batch of reads as loaded (int4 per
 // past the chunk) load nothing: those are the next chunk's reads, which
 // another workgroup, usually on another XCD, fetches again (PMC: the
 // overshoot was most of K2's 21-39 % fetch excess over 12 B/read).
-__device__ __forceinline__ void issue_raw(RawBatch& r, int64_t base,
-                                          const int32_t* __restrict__ tid,
-                                          const int32_t* __restrict__ pos,
-                                          const int32_t* __restrict__ span, int64_t cend) {
+__device__ __forceinline__ void issue_raw(RawBatch& r, int64_t base, const ReadArrays& A, int64_t cend) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
+#if MC_GPOS
     if (i0 < cend) {
-        r.t = *reinterpret_cast<const i32x4*>(tid + i0);
-        r.p = *reinterpret_cast<const i32x4*>(pos + i0);
-        r.s = *reinterpret_cast<const i32x4*>(span + i0);
+        r.g = *reinterpret_cast<const i32x4*>(A.gpos + i0);
+        r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
+    } else {
+        r.g = r.s = i32x4{0, 0, 0, 0};
+    }
+#else
+    if (i0 < cend) {
+        r.t = *reinterpret_cast<const i32x4*>(A.tid + i0);
+        r.p = *reinterpret_cast<const i32x4*>(A.pos + i0);
+        r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
     } else {
         r.t = r.p = r.s = i32x4{0, 0, 0, 0};
     }
+#endif
 }
 
 // Chunk-relative start of the 4 reads: 4 independent coff lookups (small
 // table, cache-resident); reads at or past n (the chunk's read end) are masked.  Starts far outside the
 // chunk are clamped (they are never applied: a read is applied only while
 // its start lies before the current tile end).
+// lo: the chunk's first read (reads before it in the first batch's aligned
+// group are masked: with MC_GPOS their start may lie any distance before the
+// chunk, outside the 32-bit wrap-around range).
 __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, int64_t base,
                                              int64_t n, int64_t C0,
-                                             const int64_t* __restrict__ coff) {
+                                             const int64_t* __restrict__ coff, int64_t lo) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-#if MC_SCALAR_COFF
+#if MC_GPOS
+    (void)coff;
+    const unsigned c0 = (unsigned)C0;
+    b.rs[0] = (int)((unsigned)r.g.x - c0);
+    b.rs[1] = (int)((unsigned)r.g.y - c0);
+    b.rs[2] = (int)((unsigned)r.g.z - c0);
+    b.rs[3] = (int)((unsigned)r.g.w - c0);
+#elif MC_SCALAR_COFF
     // The wave's distinct contigs (one or two per batch unless contigs are
     // tiny) one at a time: a uniform index, so coff comes in on the scalar
     // path (lgkmcnt).  Per-lane vector loads here would need a vmcnt(0),
@@ -1004,12 +1053,14 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
     const int64_t g[4] = {coff[r.t.x] + r.p.x, coff[r.t.y] + r.p.y, coff[r.t.z] + r.p.z,
                           coff[r.t.w] + r.p.w};
 #endif
+#if !MC_GPOS
     constexpr int64_t kClamp = int64_t(1) << 30;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t rel = g[k] - C0;
         b.rs[k] = (int)(rel < -kClamp ? -kClamp : rel > kClamp ? kClamp : rel);
     }
+#endif
     // The spans are copied into registers of their own here: used straight from
     // the load's destination, their first use inside the apply loop carried a
     // vmcnt(0) that ran every tile and drained the previous tile's depth stores
@@ -1027,6 +1078,8 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
 #endif
     const int64_t left = n - i0;
     b.pending = left >= 4 ? 0xfu : left <= 0 ? 0u : ((1u << left) - 1u);
+    const int64_t skip = lo - i0;   // > 0 only in thread 0 of the chunk's first batch
+    if (skip > 0) b.pending &= skip >= 4 ? 0u : ~((1u << skip) - 1u);
 }
 
 // Fused region statistics of K2 (optional): non-overlapping regions sorted by
@@ -1407,8 +1460,7 @@ template <bool kStats, bool kLong>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
 __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
                                                  : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
-depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-             const int32_t* __restrict__ span, int64_t n,
+depth_kernel(ReadArrays A, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
              int cstride, int64_t n_chunks, int tiles_per_chunk, int short_max,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
@@ -1491,9 +1543,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         b.pending = 0;
         if (more) {
             RawBatch r0;
-            issue_raw(r0, base, tid, pos, span, cend);
-            if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span, cend);
-            finish_batch(b, r0, base, cend, C0, coff);
+            issue_raw(r0, base, A, cend);
+            if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, A, cend);
+            finish_batch(b, r0, base, cend, C0, coff, cfirst);
         }
         constexpr bool has_long = kLong;
         int carry = has_long ? uload(chunk_carry, c) : 0;
@@ -1569,9 +1621,9 @@ depth_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     base += kBatch;
                     more = base < cend;
                     if (more) {
-                        if (!kPf) issue_raw(nxt, base, tid, pos, span, cend);
-                        finish_batch(b, nxt, base, cend, C0, coff);   // loaded one batch ago
-                        if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, tid, pos, span, cend);
+                        if (!kPf) issue_raw(nxt, base, A, cend);
+                        finish_batch(b, nxt, base, cend, C0, coff, cfirst);   // loaded one batch ago
+                        if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, A, cend);
                     }
                 }
             }
