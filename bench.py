@@ -364,9 +364,9 @@ def main():
 
     # roofline of the dominant kernel (K2)
     ext_sum = int(sum(eng.contig_offset(t)[1] for t in range(len(lengths))))
-    # K2 reads 8 B per read (the 32-bit global start ingest writes, and the
-    # span: MC_GPOS) and writes 4 B per position
-    k2_bytes = 8 * len(tid) + 4 * ext_sum
+    # K2 reads 4 B per read (start bits and capped span in one word, written
+    # by ingest: MC_GPOS) and writes 4 B per position
+    k2_bytes = 4 * len(tid) + 4 * ext_sum
     k2_ms = float(np.mean(k2))
     achieved = k2_bytes / (k2_ms * 1e-3) / 1e9
     k1_ms = float(np.mean(k1)) if args.cigar else 0.0

@@ -75,8 +75,18 @@ namespace mc {
 // ingest_kernel writes the starts (4 B/read more in prepare).  Chunk-relative
 // starts are exact in 32-bit wrap-around arithmetic, since every read K2
 // applies starts within one tile before its chunk or inside it.
-#define MC_GPOS 1
+// 2: one word per read, 4 B/read: the start's low kGposBits bits (the same
+// wrap-around, over a range that holds a chunk and the tile before it) and
+// the span capped at kGspanCap (> short_max, so the cap still marks a long
+// read; K2 needs a long read's span only to tell that it is one).
+// In-process A/B against 1 (profiles/r02zz_pack_ab_c*.txt): plain K2 C3
+// 0.811 -> 0.762 ms, C5 0.848 -> 0.806; fused C3 0.949 -> 0.950, C5 1.102 ->
+// 1.115 (the fused kernel is issue-bound: the decode costs what the bytes save).
+#define MC_GPOS 2
 #endif
+constexpr int kGposBits = 18;
+constexpr unsigned kGposMask = (1u << kGposBits) - 1u;
+constexpr int kGspanCap = (1 << (32 - kGposBits)) - 1;   // 16383
 
 constexpr int kBlock = 256;            // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
@@ -397,8 +407,11 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                 const int64_t q = gb + 64 * u + lane;
                 unsigned g[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4; ++k) {
                     g[k] = ((unsigned)cid[4 * u + k] << X.lw) + (unsigned)off[4 * u + k];
+                    if (MC_GPOS == 2)
+                        g[k] = (g[k] & kGposMask) | ((unsigned)min(ss[4 * u + k], kGspanCap) << kGposBits);
+                }
                 if (q < g1)
                     *reinterpret_cast<i32x4*>(gpos + q * 4) =
                         i32x4{(int)g[0], (int)g[1], (int)g[2], (int)g[3]};
@@ -967,7 +980,9 @@ struct ReadBatch {                     // 4 reads in chunk-relative coordinates
 };
 
 struct RawBatch {                      // one batch of reads as loaded (int4 per array)
-#if MC_GPOS
+#if MC_GPOS == 2
+    i32x4 g;                           // packed start bits and capped span
+#elif MC_GPOS
     i32x4 g, s;                        // low 32 bits of the global start, span
 #else
     i32x4 t, p, s;
@@ -990,7 +1005,9 @@ struct ReadArrays {
 // overshoot was most of K2's 21-39 % fetch excess over 12 B/read).
 __device__ __forceinline__ void issue_raw(RawBatch& r, int64_t base, const ReadArrays& A, int64_t cend) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-#if MC_GPOS
+#if MC_GPOS == 2
+    r.g = i0 < cend ? *reinterpret_cast<const i32x4*>(A.gpos + i0) : i32x4{0, 0, 0, 0};
+#elif MC_GPOS
     if (i0 < cend) {
         r.g = *reinterpret_cast<const i32x4*>(A.gpos + i0);
         r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
@@ -1019,7 +1036,23 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
                                              int64_t n, int64_t C0,
                                              const int64_t* __restrict__ coff, int64_t lo) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-#if MC_GPOS
+#if MC_GPOS == 2
+    (void)coff;
+    static_assert((int64_t)MC_TILES_PER_CHUNK * kTileW + kRing < (1 << (kGposBits - 1)),
+                  "packed starts: a chunk and its halo must fit the signed wrap-around range");
+    static_assert(kGspanCap > kRing - kTileW, "the span cap must exceed short_max");
+    {
+        const unsigned c0 = (unsigned)C0 & kGposMask;
+        const unsigned gg[4] = {(unsigned)r.g.x, (unsigned)r.g.y, (unsigned)r.g.z, (unsigned)r.g.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // sign-extend the kGposBits-bit difference
+            const int d = (int)(((gg[k] - c0) & kGposMask) << (32 - kGposBits)) >> (32 - kGposBits);
+            b.rs[k] = d;
+            b.sp[k] = (int)(gg[k] >> kGposBits);
+        }
+    }
+#elif MC_GPOS
     (void)coff;
     const unsigned c0 = (unsigned)C0;
     b.rs[0] = (int)((unsigned)r.g.x - c0);
@@ -1065,7 +1098,8 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, in
     // the load's destination, their first use inside the apply loop carried a
     // vmcnt(0) that ran every tile and drained the previous tile's depth stores
     // (in-order vmcnt); here the wait runs once per batch.
-#if MC_SP_COPY
+#if MC_GPOS == 2
+#elif MC_SP_COPY
     asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[0]) : "v"(r.s.x));
     asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[1]) : "v"(r.s.y));
     asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[2]) : "v"(r.s.z));
