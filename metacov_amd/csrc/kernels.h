@@ -84,6 +84,11 @@ namespace mc {
 // 1.115 (the fused kernel is issue-bound: the decode costs what the bytes save).
 #define MC_GPOS 2
 #endif
+#ifndef MC_GPOS_NT
+// non-temporal stores of the read words in ingest: C3 prepare 0.353 -> 0.368 ms,
+// C5 0.632 -> 0.636 (profiles/r02zz_nt_prep.txt).  Off.
+#define MC_GPOS_NT 0
+#endif
 constexpr int kGposBits = 18;
 constexpr unsigned kGposMask = (1u << kGposBits) - 1u;
 constexpr int kGspanCap = (1 << (32 - kGposBits)) - 1;   // 16383
@@ -412,9 +417,11 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
                     if (MC_GPOS == 2)
                         g[k] = (g[k] & kGposMask) | ((unsigned)min(ss[4 * u + k], kGspanCap) << kGposBits);
                 }
-                if (q < g1)
-                    *reinterpret_cast<i32x4*>(gpos + q * 4) =
-                        i32x4{(int)g[0], (int)g[1], (int)g[2], (int)g[3]};
+                if (q < g1) {
+                    const i32x4 w = i32x4{(int)g[0], (int)g[1], (int)g[2], (int)g[3]};
+                    if (MC_GPOS_NT) __builtin_nontemporal_store(w, reinterpret_cast<i32x4*>(gpos + q * 4));
+                    else *reinterpret_cast<i32x4*>(gpos + q * 4) = w;
+                }
             }
         }
         // chunk index: boundaries m*w with prev < m*w <= g get "first read at
