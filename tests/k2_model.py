@@ -11,6 +11,20 @@ bugs show up without a GPU.  Constants must match kernels.h.
 import numpy as np
 from oracle import coracle
 W=4096; TPC_MAX=8; RING=8192; SM=RING-W
+GB=18; GMASK=(1<<GB)-1; SCAP=(1<<(32-GB))-1   # K2's read words (kernels.h MC_GPOS 2)
+
+
+def read_words(gs, span):
+    """ingest_kernel's read words: low GB bits of the global start, span
+    capped at SCAP above them."""
+    return (gs & GMASK) | (np.minimum(span, SCAP).astype(np.int64) << GB)
+
+
+def decode(word, C0):
+    """finish_batch: chunk-relative start (sign-extended GB-bit difference)
+    and capped span."""
+    d = (int(word) - (C0 & GMASK)) & GMASK
+    return (d - (1 << GB) if d >= 1 << (GB - 1) else d), int(word) >> GB
 
 
 def tiles_per_chunk(G):
@@ -21,7 +35,9 @@ def tiles_per_chunk(G):
         tpc //= 2
     return tpc
 
-def model(lengths, tid, pos, span):
+def model(lengths, tid, pos, span, origin=0):
+    """origin: a multiple of the chunk width added to every global position
+    the read words see (as a genome past 2^32 would), the depth unchanged."""
     ext, coff64 = coracle.layout(lengths, tid, pos, span)
     coff=np.zeros(len(ext)+1,np.int64); 
     for i in range(len(ext)): coff[i+1]=coff[i]+ (ext[i]+63)//64*64
@@ -64,9 +80,12 @@ def model(lengths, tid, pos, span):
         b0=c*S
         first=0 if b0==0 else min(Xidx[b0], F[b0])
         assert first==ref_first(C0)
+        exact=first
         first&=~3
         ring=np.zeros(RING,np.int64)
         i=first; carry=carry_c[c] if long_.any() else 0
+        assert origin % CW == 0
+        words=read_words(gs+origin, span)
         stream=[r for _, r in sorted(ev.get(c, []), key=lambda e: e[0])]   # tile order
         k=0
         for t in range(TPC):
@@ -74,10 +93,13 @@ def model(lengths, tid, pos, span):
             while k<len(stream) and stream[k]<(t+1)*W:   # applied while before the tile end
                 ring[(C0+stream[k])&(RING-1)]-=1; k+=1
             while i<len(gs) and gs[i]<Tend:
-                if ge[i]-gs[i]<=SM:
-                    s=max(gs[i],C0); e=ge[i]
-                    if e>s: ring[s&(RING-1)]+=1; ring[e&(RING-1)]-=1
-                elif gs[i]>=C0: ring[gs[i]&(RING-1)]+=1
+                rs, sp = decode(words[i], C0+origin)
+                if i<exact: i+=1; continue          # masked: before the chunk's first read
+                assert rs==gs[i]-C0 and sp==min(span[i],SCAP)
+                if sp<=SM:
+                    s=max(rs,0); e=rs+sp
+                    if e>s: ring[(C0+s)&(RING-1)]+=1; ring[(C0+e)&(RING-1)]-=1
+                elif rs>=0: ring[(C0+rs)&(RING-1)]+=1
                 i+=1
             sl=np.arange(T0,Tend)&(RING-1)
             vals=carry+np.cumsum(ring[sl]); ring[sl]=0
