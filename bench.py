@@ -449,7 +449,7 @@ def main():
                 "input": ("raw BAM CIGAR words in HBM (%d words, %.1f GB, ~%g ops/read); per step "
                           "K1 CIGAR->span + prepare + K2 + K3b" % (cigar.numel(), cigar.numel() * 4e-9,
                                                                     args.cigar_ops))
-                         if args.cigar else "(tid, pos, span) tuples in HBM; prepared index reused",
+                         if args.cigar else "(tid, pos, span) tuples in HBM; prepared index and read words reused",
                 "parallelism": ("contig-shard x%d, %s all-gather of region table"
                                 % (world, "RCCL" if args.backend == "nccl" else "gloo"))
                                if world > 1 else "single GPU",
