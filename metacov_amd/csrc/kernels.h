@@ -1523,9 +1523,14 @@ depth_kernel(ReadArrays A, int64_t n,
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
-    // deferred tile stores: not in the fused long-read variant, which is at its
-    // register budget (C5 fused +0.9 %; plain C3 -2.4 %, C5 -4.9 %, fused C3 -1.2 %)
-    constexpr bool kDefer = MC_DEFER_STORE && !(kStats && kLong);
+    // deferred tile stores: plain K2 only.  With 12 B/read they gained plain C3
+    // -2.4 %, C5 -4.9 %, fused C3 -1.2 % (fused long +0.9 %); with the packed read
+    // words the fused C3 K2 runs 1.6 % faster without them and the plain one
+    // the same (profiles/r02zz_knobs_ab.txt)
+#ifndef MC_DEFER_FUSED
+#define MC_DEFER_FUSED 0
+#endif
+    constexpr bool kDefer = MC_DEFER_STORE && (!kStats || (MC_DEFER_FUSED && !kLong));
     constexpr bool kPack = kStats && kLong && MC_HIST_PACK_LONG;   // see hist_int4
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     int my_max = 0;
