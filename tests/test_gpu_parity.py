@@ -316,6 +316,34 @@ def test_long_read_ends_on_chunk_and_tile_starts(eng):
     check_depth_vs_oracle(eng, lengths, tid, pos[o], span[o])
 
 
+def test_read_words_alias_masked(eng):
+    # K2's read words keep 18 start bits: a read 262,044 positions before a
+    # chunk start decodes to chunk position 100.  Each group of 4 reads puts
+    # such a read A in the same aligned batch slot as the chunk's first read B
+    # (A at an index = 0 mod 4, B right after it), so A is loaded for B's chunk
+    # and for every empty chunk between them, and only the mask before the
+    # chunk's first read keeps it out.  B sits 50 past a multiple of 32768, so
+    # this holds for 2-, 4- and 8-tile chunks.
+    pos = []
+    for k in range(6):
+        b = (k * 12 + 10) * 32768 + 50
+        pos += [b - 50 - 262_044, b, b + 10, b + 20]
+    pos = np.array(pos, np.int32)
+    span = np.full(len(pos), 150, np.int32)
+    lengths = [int(pos[-1]) + 10_000]
+    tid = np.zeros(len(pos), np.int32)
+    run_engine(eng, lengths, tid, pos, span)
+    d, ext, coff = check_depth_vs_oracle(eng, lengths, tid, pos, span)
+    eng.set_contigs(lengths)
+    eng.add_reads(tid, pos, span)
+    got = eng.compute_depth_stats(np.zeros(1, np.int32), np.zeros(1, np.int64),
+                                  np.asarray(lengths, np.int64))
+    want = coracle.region_stats(d, ext, coff, np.zeros(1, np.int32), np.zeros(1, np.int64),
+                                np.asarray(lengths, np.int64))
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
+
+
 # ------------------------------------------------------------- fused K2 + stats
 
 def _tiling(rng, lengths, pieces):
