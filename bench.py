@@ -1,19 +1,21 @@
 """Benchmark: aligned bases/s into the per-position depth vector (+ per-region
-statistics), BASELINE.json metric, on the C3 workload per GPU.
+statistics), BASELINE.json metric, on the C3 workload.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-One step = K2 (depth of every contig from device-resident (tid, pos, span)
-tuples) + K3 (whole-contig region statistics into device memory) [+ for
-N > 1 the RCCL all-gather of the region table].  Inputs are generated on the
-GPU before timing (synthetic, SURVEY.md §8 d edge mix).
+One step = one pass of the hot path over one batch of reads resident in HBM
+(int32 tid, pos, span; SURVEY.md §8 d): the batch is new to the engine every
+step, so the step prepares it (the direct path: probe_kernel, then K2 reads
+and validates the raw tuples), computes the depth of every contig (K2) with
+the whole-contig region statistics folded in, and finalizes the region table
+(K3b) [+ for N > 1 the RCCL all-gather of the table].  Inputs are generated on
+the GPU before timing (synthetic).
 
-Default (weak scaling, as BASELINE configs[2] per GPU): every rank owns a
-full C3 workload — 1000 contigs (~1 Gbp, rng(42) lengths, lognormal(0,1)
-abundance) and 100M x ~150 bp reads; value = all ranks' aligned bases per
-second.  --strong: one C3 workload LPT-sharded by contig over the ranks
-(BASELINE configs[3]).
+`--gpus N` without torchrun around it starts `torch.distributed.run` with N
+ranks as a child process.  Default scaling is strong (BASELINE configs[3]):
+ONE C3 workload, contigs LPT-sharded over the ranks; --scaling weak gives
+every rank a full C3.  value = all ranks' aligned bases per second.
 """
 import argparse
 import json
@@ -23,9 +25,11 @@ import time
 import numpy as np
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks).  Without WORLD_SIZE in the environment, N > 1 starts "
+                         "`torch.distributed.run --nproc-per-node N` on this script as a child process")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"],
@@ -33,7 +37,10 @@ def parse():
                          "c5: 10k contigs, 50M lognormal ~10 kbp reads")
     ap.add_argument("--reads", type=int, default=None, help="reads per workload (config default)")
     ap.add_argument("--contigs", type=int, default=None)
-    ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong (default, BASELINE configs[3]): ONE workload LPT-sharded by contig over "
+                         "the ranks; weak: every rank owns a full workload")
+    ap.add_argument("--strong", action="store_true", help="(kept for old command lines: the default)")
     ap.add_argument("--unfused", action="store_true",
                     help="K2 then a separate K3 pass instead of the fused K2 statistics")
     ap.add_argument("--cigar", action="store_true",
@@ -47,13 +54,42 @@ def parse():
                     help="threads of the contig-parallel CPU baseline (the box's CPU share)")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer ingest (H2D)")
     ap.add_argument("--prepare-steps", type=int, default=None,
-                    help="steps of the second timed loop that re-prepares the batch every step "
+                    help="steps of the second timed loop, which reuses one explicit prepare's index "
                          "(default: --steps; 0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` outside torchrun: run N ranks of this script under
+    `python -m torch.distributed.run` as a CHILD process (this process never
+    imports torch or touches a GPU, so nothing is exec'd over a GPU context)
+    and relay rank 0's JSON line.  Returns the exit code."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    line = None
+    for raw in p.stdout:                  # stderr passes straight through
+        i = raw.find("{\"metric\"")
+        if i >= 0:
+            line = raw[i:].strip()
+        else:
+            sys.stderr.write(raw)
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    return rc if rc else (0 if line is not None else 1)
 
 
 CONFIGS = {   # name: (reads, contigs, description)
@@ -147,7 +183,12 @@ def cpu_baseline_parallel(lengths, tid, pos, span, sample_bases, threads):
                                     lengths[:k].astype(np.int64), threads)
     dt = time.perf_counter() - t0
     bases = int(s.astype(np.int64).sum())
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"value": bases / dt, "unit": "aligned bases/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cpus_in_affinity": affinity,
             "sample": "same %d contigs as cpu_baseline, contig-parallel on %d threads, %.2f s"
                       % (k, threads, dt)}
 
@@ -197,7 +238,12 @@ def load_pmc_traffic(root):
 
 
 def main():
-    args = parse()
+    import sys
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+    strong = args.scaling == "strong"
     import torch
     import torch.distributed as dist
     from metacov_amd import synth, dist as mdist
@@ -223,8 +269,8 @@ def main():
     args.contigs = args.contigs or d_contigs
     long_reads = args.config == "c5"
     lengths_all, weights_all = config_contigs(args.config, args.reads, args.contigs)
-    if args.strong:
-        # one C3 workload, contigs LPT-sharded over the ranks
+    if strong:
+        # one workload, contigs LPT-sharded over the ranks (at N = 1: all of it)
         tid, pos, span, counts = device_workload(torch, lengths_all, weights_all, args.reads,
                                                  args.seed, dev, long_reads)
         owned = mdist.lpt_shard(mdist.contig_costs(lengths_all, counts), world)[rank]
@@ -241,7 +287,7 @@ def main():
                                             args.seed + 1000 * rank, dev, long_reads)
         lengths = lengths_all
         region_index = np.arange(len(lengths)) + rank * len(lengths)
-    n_regions_total = int(len(lengths_all) if args.strong else len(lengths_all) * world)
+    n_regions_total = int(len(lengths_all) if strong else len(lengths_all) * world)
 
     eng = CoverageEngine(local)
     eng.set_contigs(lengths)
@@ -252,16 +298,11 @@ def main():
         eng.add_reads_cigar_device(tid, pos, cig_off, cigar)
     else:
         eng.add_reads(tid, pos, span)
-    eng.prepare()
-    prep = eng.timings()
-    bases = eng.aligned_bases()
-    if args.cigar:   # K1 re-derived exactly the generator's spans
-        assert bases == int(span.to(torch.int64).sum()), "K1 spans differ from the generator"
     R = len(lengths)
     rt = np.arange(R, dtype=np.int32)
     rs = np.zeros(R, np.int64)
     re_ = lengths.astype(np.int64)
-    r_max = int(n_regions_total if args.strong else R)
+    r_max = int(n_regions_total if strong else R)
     table = torch.empty((R, 9), dtype=torch.int64, device=dev)
     gathered = None
 
@@ -272,11 +313,17 @@ def main():
         coll_buf = gbuf if coll_dev == dev else gbuf.to(coll_dev)
         gout = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=coll_dev)
 
-    def step():
+    def step(fresh):
+        """One pass of the hot path over the resident batch.  fresh: the
+        batch is new to the engine (mc_invalidate first), so the step
+        prepares it — the direct path: probe + validating K2 — before K2 and
+        K3b; otherwise K2 reuses the index an explicit prepare() built."""
         nonlocal gathered
         if args.cigar:   # a fresh raw-CIGAR batch: K1 + prepare run inside this step
             eng.clear_reads()
             eng.add_reads_cigar_device(tid, pos, cig_off, cigar)
+        elif fresh:
+            eng.invalidate()
         if args.unfused:
             eng.compute_depth()
             eng.region_stats_device(rt, rs, re_, table.data_ptr())
@@ -289,69 +336,75 @@ def main():
             dist.all_gather_into_tensor(gout, coll_buf)
             gathered = gout
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    k2, k3, k1, kp = [], [], [], []
-    # fused steps: the library sums each call's K2 / K3b event times itself
-    # (the call drains its stream), so the timed loop carries no per-step
-    # timing query; other modes read the events after every step
-    per_step_query = args.unfused or args.cigar
-    before = eng.timings()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        if per_step_query:
-            tm = eng.timings()        # syncs the ctx stream; HIP events around K1 / K2 / K3
-            k2.append(tm["depth_ms"])
-            k3.append(tm["stats_ms"])
-            k1.append(tm["cigar_ms"])
-            kp.append(tm["prepare_ms"])
-    torch.cuda.synchronize()
-    if not per_step_query:
+    def sync_all():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed(n_steps, fresh):
+        """n_steps steps between barrier + synchronize pairs; kernel times
+        from the library's per-call event totals (fused) or per-step queries."""
+        sync_all()
+        per_step_query = args.unfused or args.cigar
+        k2, k3, k1, kp = [], [], [], []
+        before = eng.timings()
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            step(fresh)
+            if per_step_query:
+                tm = eng.timings()        # syncs the ctx stream; HIP events around K1 / K2 / K3
+                k2.append(tm["depth_ms"])
+                k3.append(tm["stats_ms"])
+                k1.append(tm["cigar_ms"])
+                kp.append(tm["prepare_ms"] if fresh else 0.0)
+        sync_all()
+        el = time.perf_counter() - t0
         after = eng.timings()
-        calls = max(1, after["fused_calls"] - before["fused_calls"])
-        k2 = [(after["fused_depth_ms_total"] - before["fused_depth_ms_total"]) / calls]
-        k3 = [(after["fused_stats_ms_total"] - before["fused_stats_ms_total"]) / calls]
-        k1, kp = [0.0], [0.0]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    # The same steps on a fresh batch each time: every step first drops the
-    # prepared index (mc_invalidate), so it re-runs mc_prepare (ingest:
-    # validation, aligned bases, extents; the chunk index; long-read
-    # buckets) on the resident reads before K2 + K3b.  (--cigar steps
-    # already re-add and re-prepare their batch.)
-    elapsed_prep, prep_ms = None, []
+        if not per_step_query:
+            calls = max(1, after["fused_calls"] - before["fused_calls"])
+            k2 = [(after["fused_depth_ms_total"] - before["fused_depth_ms_total"]) / calls]
+            k3 = [(after["fused_stats_ms_total"] - before["fused_stats_ms_total"]) / calls]
+            kp = [(after["prepare_ms_total"] - before["prepare_ms_total"]) / max(1, n_steps)]
+            k1 = [0.0]
+        paths = {"direct": after["direct_batches"] - before["direct_batches"],
+                 "full": after["full_prepares"] - before["full_prepares"]}
+        return el, [float(np.mean(x)) for x in (k2, k3, k1, kp)], paths
+
+    # ---- the headline: every step is a fresh batch (prepare inside the step)
+    for _ in range(args.warmup):
+        step(True)
+    elapsed, (k2_ms, k3_ms, k1_ms, kp_ms), paths = timed(args.steps, True)
+    bases = eng.aligned_bases()
+    if args.cigar:   # K1 re-derived exactly the generator's spans
+        assert bases == int(span.to(torch.int64).sum()), "K1 spans differ from the generator"
+    head_direct = paths["direct"] == args.steps
+    # ---- the same batch with the index of one explicit prepare() reused by
+    # every step (the reference's BAI analog), reported beside the headline
+    elapsed_re, re_k = None, None
     if not args.cigar and args.prepare_steps > 0:
         eng.invalidate()
-        step()                       # warm: the first re-prepare after the timed loop
+        eng.prepare()
+        step(False)
+        elapsed_re, re_k, _ = timed(args.prepare_steps, False)
+    # the region-table exchange alone (RCCL all-gather over xGMI), timed apart
+    allgather_ms = None
+    if world > 1:
+        n_ag = max(5, args.steps)
+        sync_all()
+        ta = time.perf_counter()
+        for _ in range(n_ag):
+            dist.all_gather_into_tensor(gout, coll_buf)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.prepare_steps):
-            eng.invalidate()
-            step()
-            prep_ms.append(eng.timings()["prepare_ms"])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        elapsed_prep = time.perf_counter() - t1
-    t_max = elapsed
-    t_max_prep = elapsed_prep
+        allgather_ms = (time.perf_counter() - ta) / n_ag * 1e3
+    t_max, t_max_re = elapsed, elapsed_re
     total_bases = bases
     if world > 1:
-        t = torch.tensor([elapsed, elapsed_prep or 0.0], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([elapsed, elapsed_re or 0.0, allgather_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t[0].item())
-        t_max_prep = float(t[1].item()) if elapsed_prep is not None else None
+        t_max_re = float(t[1].item()) if elapsed_re is not None else None
+        allgather_ms = float(t[2].item())
         b = torch.tensor([bases], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(b)
         total_bases = int(b.item())
@@ -362,41 +415,37 @@ def main():
         if not os.environ.get("MC_BENCH_NOCHECK"):   # set only for deliberately-wrong A/B builds
             assert int(rows["sum"].sum()) == total_bases
 
-    # roofline of the dominant kernel (K2)
+    # roofline of the dominant kernel of the headline step (K2): it reads the
+    # raw (tid, pos, span) tuples on the direct path (12 B/read) or the packed
+    # read words of a full prepare (4 B/read), and writes 4 B per position
     ext_sum = int(sum(eng.contig_offset(t)[1] for t in range(len(lengths))))
-    # K2 reads 4 B per read (start bits and capped span in one word, written
-    # by ingest: MC_GPOS) and writes 4 B per position
-    k2_bytes = 4 * len(tid) + 4 * ext_sum
-    k2_ms = float(np.mean(k2))
+    read_bytes = 12 if head_direct else 4
+    k2_bytes = read_bytes * len(tid) + 4 * ext_sum
     achieved = k2_bytes / (k2_ms * 1e-3) / 1e9
-    k1_ms = float(np.mean(k1)) if args.cigar else 0.0
+    long_path = args.config == "c5"
+    variant = "depth_kernel<%s, %s, %s>" % ("false" if args.unfused else "true",
+                                             "true" if long_path else "false",
+                                             "true" if head_direct else "false")
+    pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
+
+    def pmc_for(kernel_name):
+        for v in ([] if world > 1 else (pmc or {}).get("variants", [])):   # PMC of the one-GPU workload
+            if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
+                    and kernel_name in v.get("kernel", ""):
+                return v.get("hbm_bytes_per_launch")
+        return None
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                "frac": achieved / 8000.0, "traffic": pmc_for(variant),
+                "kernel": "%s (K2)" % variant, "algorithmic_bytes_per_launch": int(k2_bytes),
+                "bytes_per_unit": "%d B/read + 4 B/position" % read_bytes}
     if args.cigar and k1_ms > k2_ms:   # K1 streams the CIGAR words: the dominant kernel
         n_words = int(cigar.numel())
         k1_bytes = 4 * n_words + 8 * (len(tid) + 1) + 4 * len(tid)
         achieved_k1 = k1_bytes / (k1_ms * 1e-3) / 1e9
-    pmc = load_pmc_traffic(os.path.dirname(os.path.abspath(__file__)))
-    traffic = None
-    # depth_kernel<kStats, kLong>: the long-read variant runs when a span exceeds the LDS ring
-    long_path = args.config == "c5"
-    variant = "depth_kernel<%s, %s>" % ("false" if args.unfused else "true",
-                                         "true" if long_path else "false")
-    for v in ([] if args.strong else (pmc or {}).get("variants", [])):   # PMC of the per-GPU workload
-        if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
-                and variant in v.get("kernel", ""):
-            traffic = v.get("hbm_bytes_per_launch")
-    roofline = {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                "frac": achieved / 8000.0, "traffic": traffic,
-                "kernel": "%s (K2)" % variant,
-                "algorithmic_bytes_per_launch": int(k2_bytes)}
-    if args.cigar and k1_ms > k2_ms:
-        k1_traffic = None
-        for v in ([] if args.strong else (pmc or {}).get("variants", [])):
-            if v.get("reads") == args.reads and v.get("contigs") == args.contigs \
-                    and "cigar_span_kernel" in v.get("kernel", ""):
-                k1_traffic = v.get("hbm_bytes_per_launch")
         roofline = {"bound": "hbm", "achieved": achieved_k1, "peak": 8000.0, "unit": "GB/s",
-                    "frac": achieved_k1 / 8000.0, "traffic": k1_traffic,
-                    "kernel": "cigar_span_kernel (K1)", "algorithmic_bytes_per_launch": int(k1_bytes)}
+                    "frac": achieved_k1 / 8000.0, "traffic": pmc_for("cigar_span_kernel"),
+                    "kernel": "cigar_span_kernel (K1)", "algorithmic_bytes_per_launch": int(k1_bytes),
+                    "bytes_per_unit": "4 B/CIGAR word + 12 B/read"}
 
     if rank == 0:
         cpu = cpu_par = cpu_int = None
@@ -414,9 +463,7 @@ def main():
             e2.set_contigs(lengths)
             t1 = time.perf_counter()
             e2.add_reads(*h)
-            e2.prepare()
-            e2.compute_depth()
-            e2.region_stats(rt, rs, re_)
+            e2.compute_depth_stats(rt, rs, re_)
             pcie = time.perf_counter() - t1
             e2.close()
         value = total_bases * args.steps / t_max
@@ -429,7 +476,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int32",
             "data": ("synthetic (GPU-generated %s intervals, %s%s)"
@@ -437,8 +484,11 @@ def main():
                         "lognormal ~10 kbp spans" if args.config == "c5" else "SURVEY §8d span mix",
                         ", BAM CIGAR words generated on the GPU" if args.cigar else "")),
             "config": {
-                "workload": ("%s LPT-sharded by contig over %d GPUs" % (args.config.upper(), world))
-                            if args.strong else
+                "workload": ("%s LPT-sharded by contig over %d GPUs (%s)"
+                             % (args.config.upper(), world,
+                                desc % args.reads if args.config == "c2" else
+                                desc % (args.contigs, lengths_all.sum() / 1e9, args.reads)))
+                            if strong and world > 1 else
                             (desc % args.reads if args.config == "c2" else
                              desc % (args.contigs, lengths_all.sum() / 1e9, args.reads)),
                 "config": args.config,
@@ -449,32 +499,39 @@ def main():
                 "input": ("raw BAM CIGAR words in HBM (%d words, %.1f GB, ~%g ops/read); per step "
                           "K1 CIGAR->span + prepare + K2 + K3b" % (cigar.numel(), cigar.numel() * 4e-9,
                                                                     args.cigar_ops))
-                         if args.cigar else "(tid, pos, span) tuples in HBM; prepared index and read words reused",
+                         if args.cigar else
+                         "(tid, pos, span) int32 tuples resident in HBM; every step treats them as a "
+                         "fresh batch: prepare (%s) + K2 + K3b" % ("direct: probe + validating K2"
+                                                                   if head_direct else "full: ingest"),
                 "parallelism": ("contig-shard x%d, %s all-gather of region table"
                                 % (world, "RCCL" if args.backend == "nccl" else "gloo"))
                                if world > 1 else "single GPU",
             },
+            "prepare_path": {"direct_batches": paths["direct"], "full_prepares": paths["full"]},
             "kernels_ms": {**({"k1_cigar_span": k1_ms} if args.cigar else {}),
+                           "prepare" + ("_probe" if head_direct else "_ingest_index"): kp_ms,
                            "k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
-                           ("k3_region_stats" if args.unfused else "k3b_finalize"): float(np.mean(k3)),
-                           # steady state (the re-prepare loop) when measured; the first
-                           # prepare of a ctx also allocates the depth vector
-                           "prepare_ingest_index": float(np.mean(kp)) if args.cigar
-                           else float(np.median(prep_ms)) if prep_ms else prep["prepare_ms"]},
+                           ("k3_region_stats" if args.unfused else "k3b_finalize"): k3_ms},
             "fused_fallback_regions": None if args.unfused else eng.fused_fallbacks(),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
             "cpu_interval_count": cpu_int,
+            "world_size": world,
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "backend": (args.backend if world > 1 else None),
+            "allgather_ms": allgather_ms,
         }
-        if t_max_prep is not None:
-            line["with_prepare"] = {
-                "value": total_bases * args.prepare_steps / t_max_prep,
-                "ms_per_step": t_max_prep / args.prepare_steps * 1e3,
+        if t_max_re is not None:
+            line["reused_index"] = {
+                "value": total_bases * args.prepare_steps / t_max_re,
+                "ms_per_step": t_max_re / args.prepare_steps * 1e3,
                 "steps": args.prepare_steps,
-                "prepare_ms": float(np.median(prep_ms)),
-                "step": "mc_invalidate + the same step: mc_prepare (ingest, validation, extents, "
-                        "chunk index) re-runs on the resident batch before K2 + K3b",
+                "k2_ms": re_k[0],
+                "k3b_ms": re_k[1],
+                "step": "one explicit mc_prepare (ingest: chunk index + packed 4 B read words), then "
+                        "every step reuses it: K2 (depth_kernel<%s, %s, false>) + K3b"
+                        % ("false" if args.unfused else "true", "true" if long_path else "false"),
             }
         if pcie is not None:
             line["host_buffer_end_to_end_s"] = pcie

@@ -75,6 +75,11 @@ typedef struct mc_timings {
     double fused_depth_ms_total;   /* K2 */
     double fused_stats_ms_total;   /* K3b (+ fallback K3) */
     int64_t fused_calls;
+    /* Batches prepared by the direct path and accepted by K2's checks, and
+     * full mc_prepare passes (explicit, or a direct batch handed over). */
+    int64_t direct_batches;
+    int64_t full_prepares;
+    double prepare_ms_total;       /* every prepare's prepare_ms (direct: the probe) */
 } mc_timings;
 
 typedef struct mc_ctx mc_ctx;
@@ -139,14 +144,29 @@ int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,
 /* Drops the ctx's reads (the contigs stay): the next batch starts empty. */
 int mc_clear_reads(mc_ctx* ctx);
 
-/* Validates order, computes contig extents (max of length and furthest
- * read end) and the tile index.  Called by mc_compute_depth if needed. */
+/* The full prepare: validates order, computes contig extents (max of length
+ * and furthest read end), the chunk index, K2's packed read words and the
+ * long-read buckets.  Compute calls run it when the direct path (see
+ * mc_set_direct_prepare) cannot take the batch; an explicit call builds an
+ * index that later compute calls reuse. */
 int mc_prepare(mc_ctx* ctx);
 
 /* Drops the prepared index and depth (the reads stay): the next compute call
- * re-runs mc_prepare over the same device reads, as for a fresh batch (what
- * the benchmark's per-batch step times). */
+ * prepares the same device reads again, as for a fresh batch (what the
+ * benchmark's per-batch step times). */
 int mc_invalidate(mc_ctx* ctx);
+
+/* Per-batch prepare of the compute calls (default on).  A compute call on a
+ * batch that mc_prepare has not seen takes the DIRECT path: a sparse sample
+ * of the reads (every 256th) locates each chunk's reads, K2 loads the raw
+ * (tid, pos, span) and checks every read itself (range, order, end within
+ * its contig, span <= 4096), so no separate pass over the batch runs before
+ * K2.  A batch the direct path cannot take (unsorted / invalid reads: the
+ * full prepare raises its exact error; long reads or reads past their
+ * contig's end: handled by the full prepare, and later batches of the same
+ * contig set go there directly) is re-run through mc_prepare inside the same
+ * call, so results never depend on the path.  enable = 0: always mc_prepare. */
+int mc_set_direct_prepare(mc_ctx* ctx, int enable);
 
 /* ---- compute ------------------------------------------------------------ */
 /* Per-position depth of every contig (K1 if needed, then K2). */
@@ -192,6 +212,19 @@ int mc_aligned_bases(mc_ctx* ctx, int64_t* out);
 int mc_max_depth(mc_ctx* ctx, int32_t* out);
 int mc_get_timings(mc_ctx* ctx, mc_timings* out);
 int mc_synchronize(mc_ctx* ctx);
+
+/* ---- htslib's pileup read cap (opt-in) -----------------------------------
+ * pysam's AlignmentFile.pileup(ref, start, end) (pileup.py:13) runs htslib's
+ * pileup with max_depth = 8000: bam_plp_push drops a read that starts where
+ * its predecessor started while the pileup's read pool holds more than
+ * max_depth nodes.  keep[i] = 0 for the reads it would drop, given the
+ * coordinate-sorted reads one pileup call sees (for classic(): the region's
+ * overlapping records).  Host C++ (contigs on n_threads threads); the depth
+ * of the kept reads is then computed as usual.  Version-dependent htslib
+ * behaviour: parity unpinned (no htslib in this image); the closed form is
+ * pinned by a literal restatement of the push/next loop (oracle/htslib_plp.py). */
+int mc_depth_cap_mask(int64_t n, const int32_t* tid, const int32_t* pos, const int32_t* span,
+                      int32_t max_depth, int n_threads, uint8_t* keep, int64_t* n_dropped);
 
 /* ---- host BAM decoder (C++, multi-threaded BGZF inflate) ----------------
  * Replaces the pysam/htslib read path the reference uses: AlignmentFile

@@ -53,7 +53,8 @@ class Timings(ctypes.Structure):
                 ("stats_ms", ctypes.c_float), ("prepare_ms", ctypes.c_float),
                 ("depth_launches", ctypes.c_int64), ("stats_launches", ctypes.c_int64),
                 ("fused_depth_ms_total", ctypes.c_double), ("fused_stats_ms_total", ctypes.c_double),
-                ("fused_calls", ctypes.c_int64)]
+                ("fused_calls", ctypes.c_int64), ("direct_batches", ctypes.c_int64),
+                ("full_prepares", ctypes.c_int64), ("prepare_ms_total", ctypes.c_double)]
 
 
 _P = ctypes.c_void_p
@@ -83,6 +84,7 @@ SIGNATURES = {
     "mc_add_reads_cigar_device": [_P, _I64, _P, _P, _P, _P],
     "mc_clear_reads": [_P],
     "mc_invalidate": [_P],
+    "mc_set_direct_prepare": [_P, ctypes.c_int],
     "mc_prepare": [_P],
     "mc_compute_depth": [_P],
     "mc_get_depth": [_P, _I32, _I64, _I64, _P],
@@ -97,6 +99,7 @@ SIGNATURES = {
     "mc_max_depth": [_P, _PI32],
     "mc_get_timings": [_P, ctypes.POINTER(Timings)],
     "mc_synchronize": [_P],
+    "mc_depth_cap_mask": [_I64, _P, _P, _P, _I32, ctypes.c_int, _P, _PI64],
     "mc_bam_open": [ctypes.c_char_p, ctypes.c_int, _U32, ctypes.c_int, _PP],
     "mc_bam_close": [_P],
     "mc_bam_n_targets": [_P, _PI32],

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmetacov_amd.so")
 SOURCES = ["engine.hip", "ecor.hip", "scan.hip", "bam_decode.cpp", "bam_index.cpp",
-           "bam_write.cpp", "exp_reads.cpp", "scan_src.cpp", "common.cpp"]
+           "bam_write.cpp", "exp_reads.cpp", "scan_src.cpp", "depth_cap.cpp", "common.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

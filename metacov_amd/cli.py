@@ -28,6 +28,7 @@ import sys
 import click
 import numpy as np
 
+from . import depthcap as _depthcap
 from . import experimental as _experimental
 from . import regions as _regions
 from . import scan as _scan
@@ -66,8 +67,11 @@ def main():
 @click.option('--stream/--no-stream', default=True,
               help="Decode in bounded-memory windows, feeding the GPU through pinned double "
                    "buffers (default; --no-stream decodes the whole file into host memory first)")
+@click.option('--max-depth', type=click.IntRange(1), default=None, metavar="N",
+              help="Reproduce htslib's pileup read cap (pysam's default is 8000) per region "
+                   "query; default: exact depths, no cap")
 def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
-           kmer_histogram, kmer_length, outfile, device, stream):
+           kmer_histogram, kmer_length, outfile, device, stream, max_depth):
     """
     Compute fold coverage values
     """
@@ -76,11 +80,14 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     k_cor = _experimental.load_kmerhist(kmer_histogram) if kmer_histogram else None
     exp = (k_cor, kmer_length, fasta) if k_cor is not None else None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp)
-    bam = StreamedBam(bamfile.name, device=device) if stream else BamFile(bamfile.name)
+        return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp,
+                                  max_depth=max_depth)
+    # the cap needs each region's records (a decoded file, not a stream)
+    bam = StreamedBam(bamfile.name, device=device) if stream and max_depth is None \
+        else BamFile(bamfile.name)
     regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam))
     log_counts(bam)
-    write_rows(bam, regions, outfile, device=device, exp=exp)
+    write_rows(bam, regions, outfile, device=device, exp=exp, max_depth=max_depth)
 
 
 def log_counts(bam):
@@ -110,12 +117,18 @@ def resolve_regions(bam, regions):
     return (np.array(tids, np.int32), np.array(starts, np.int64), np.array(ends, np.int64))
 
 
-def compute_rows(bam, tids, starts, ends, device=0):
+def compute_rows(bam, tids, starts, ends, device=0, max_depth=None):
     """Exact stat rows of the regions (header contig ids) on `bam`'s engine:
     depth and statistics in one pass (fused K2) when the regions do not
-    overlap; the library falls back to K2 + K3 otherwise."""
+    overlap; the library falls back to K2 + K3 otherwise.  max_depth: htslib's
+    read cap per region query (metacov_amd.depthcap), one engine call per
+    region."""
     if len(tids) == 0:
         return np.zeros(0, dtype=REGION_STAT_DTYPE)
+    if max_depth is not None:
+        rows, dropped = _depthcap.capped_rows(bam, tids, starts, ends, max_depth, device)
+        log.info("max_depth %d: %d reads dropped by the pileup cap", max_depth, dropped)
+        return rows
     eng = bam.engine(device, compute=False)
     rows = eng.compute_depth_stats(np.asarray(bam.local_tid(tids), np.int32), starts, ends)
     eng._depth_ready = True
@@ -123,17 +136,19 @@ def compute_rows(bam, tids, starts, ends, device=0):
     return rows
 
 
-HTSLIB_MAX_DEPTH = 8000   # pysam pileup's default max_depth (the htslib read-pool cap)
+HTSLIB_MAX_DEPTH = _depthcap.HTSLIB_MAX_DEPTH
 
 
 def warn_depth_cap(max_depth):
-    """The reference's pysam pileup stops adding reads to a column's pool past
-    max_depth=8000 (version-dependent); this engine never caps.
-    Above the cap the two disagree, so say so."""
-    if max_depth > HTSLIB_MAX_DEPTH:
-        log.warning("maximum depth %d exceeds pysam's pileup cap of %d: the reference would "
-                    "report capped depths there; these values are exact", max_depth,
-                    HTSLIB_MAX_DEPTH)
+    """The reference's pysam pileup drops reads from a column's pool past
+    max_depth=8000 (version-dependent); by default this engine
+    never caps (--max-depth 8000 reproduces the cap).  Above half the cap the
+    two may disagree (a read is dropped once its start's buffered reads,
+    depth plus the reads ending there, exceed it), so say so."""
+    if 2 * max_depth > HTSLIB_MAX_DEPTH:
+        log.warning("maximum depth %d: pysam's pileup cap of %d may drop reads here (use "
+                    "--max-depth %d to reproduce it); these values are exact", max_depth,
+                    HTSLIB_MAX_DEPTH, HTSLIB_MAX_DEPTH)
 
 
 def experimental_results(path, exp, references, tids, starts, ends, device=0):
@@ -161,16 +176,16 @@ def write_csv(regions, rows, outfile, extra=None):
         writer.writerow(result)
 
 
-def write_rows(bam, regions, outfile, device=0, exp=None):
+def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=None):
     """Resolves names like cli.py:80-91, reduces all regions in one GPU call,
     then writes rows in input order exactly as cli.py:97-108 does."""
     tids, starts, ends = resolve_regions(bam, regions)
-    rows = compute_rows(bam, tids, starts, ends, device)
+    rows = compute_rows(bam, tids, starts, ends, device, max_depth)
     extra = experimental_results(bam.filename, exp, bam.references, tids, starts, ends, device)
     write_csv(regions, rows, outfile, extra)
 
 
-def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None):
+def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None, max_depth=None):
     """One rank of a multi-GPU `pileup` (launched by torch.distributed.run).
     With -k, rank 0 adds the experimental columns for all regions after the
     gather (their read side is host work over the whole file)."""
@@ -189,7 +204,8 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
     try:
         err = None
         try:
-            table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device)
+            table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
+                                       max_depth)
         except Exception as e:   # every rank learns of it before the table gather
             err = e
         mdist.agree_on_error(err, device=coll_dev)
@@ -204,7 +220,7 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         dist.destroy_process_group()
 
 
-def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device):
+def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device, max_depth=None):
     """This rank's part of a distributed pileup: header and regions (every
     rank), LPT contig shards, and the rows of the regions on its contigs."""
     from . import dist as mdist
@@ -228,7 +244,7 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device):
     rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
     if len(mine):
         bam = BamFile(path, contigs=shards[rank]) if have_index else head.restrict(shards[rank])
-        rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device)
+        rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
     return head, regions, tids, starts, ends, rows, mine, r_max
 
 

@@ -163,7 +163,7 @@ struct mc_ctx {
 
     int64_t n_reads = 0;
     DevBuf<int32_t> d_tid, d_pos, d_span;
-    DevBuf<uint32_t> d_gpos;              // K2's read starts (MC_GPOS; ingest_kernel)
+    DevBuf<uint32_t> d_gpos;              // K2's packed read words (ingest_kernel)
     // raw-CIGAR mode
     bool spans_pending = false;
     DevBuf<int64_t> d_cig_off;
@@ -172,6 +172,17 @@ struct mc_ctx {
     const uint32_t* cigar_ext = nullptr;
 
     bool prepared = false;
+    // direct per-batch prepare (probe_kernel; K2 validates): prepared this way,
+    // K2's results not checked yet, allowed for this contig set, enabled
+    bool direct = false;
+    bool direct_checked = false;
+    bool direct_ok = true;
+    bool direct_enabled = true;
+    bool direct_retry_full = false;       // the batch K2 just refused goes to mc_prepare
+    unsigned long long direct_gen = 0;
+    DevBuf<int32_t> d_jidx;               // [2 * (n_base + 1)]: J(k w), J(k w - short_max)
+    DevBuf<int32_t> d_fsamp;              // [nc + 1] first sample of each contig
+    DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
     int32_t max_span = 0;
     int64_t aligned_bases = 0;
     int ring = 0;                 // LDS ring ints
@@ -236,8 +247,8 @@ struct mc_ctx {
 
     hipEvent_t ev[8] = {};
     int ingest_grid = 0;                  // resident ingest workgroups
-    int k2_resident[4] = {0, 0, 0, 0};    // resident K2 workgroups (plain, fused) x (short, long)
-    size_t k2_resident_lds[4] = {0, 0, 0, 0};
+    int k2_resident[6] = {};              // resident K2 workgroups (plain, fused) x (short, long, direct)
+    size_t k2_resident_lds[6] = {};
     mc_timings t{};
     bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
     bool stats_after_depth = false;       // the statistics span starts at ev[5] (fused call)
@@ -251,6 +262,8 @@ static int ctx_use(mc_ctx* ctx) {
 
 static void invalidate(mc_ctx* ctx) {
     ctx->prepared = false;
+    ctx->direct = false;
+    ctx->direct_checked = false;
     ctx->depth_valid = false;
     ctx->max_depth = -1;
 }
@@ -297,6 +310,9 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_cig_off.release();
     ctx->d_cigar.release();
     ctx->d_chunk_first.release();
+    ctx->d_jidx.release();
+    ctx->d_fsamp.release();
+    ctx->d_dres.release();
     ctx->d_tile_cnt.release();
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
@@ -352,6 +368,7 @@ extern "C" int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths) {
         MC_REQUIRE(lengths[i] >= 0 && lengths[i] < (int64_t(1) << 40), MC_E_INVALID,
                    "contig %d: bad length %lld", i, (long long)lengths[i]);
     ctx->len.assign(lengths, lengths + n);
+    ctx->direct_ok = true;
     ctx->n_reads = 0;
     ctx->spans_pending = false;
     ctx->cig_off_ext = nullptr;
@@ -519,28 +536,100 @@ static float elapsed(mc_ctx* ctx, int a, int b) {
     return ms;
 }
 
+// ---- layout for given extents: contig offsets and chunk geometry.  One
+// chunk index serves both K2 variants: its base chunks are the plain K2's,
+// half-size (kPlainTilesPerChunk tiles), where the plain kernel balances
+// better (C3: 0.995 -> 0.936 ms); the fused one is faster on full chunks
+// (its chunk-end flushes double) and reads its chunk c as base chunks
+// [c*s, c*s + s).  Long reads' end buckets and carries are per full
+// chunk, so with long reads the plain K2 runs on full chunks too.
+static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
+    const int32_t nc = (int32_t)ctx->len.size();
+    ctx->extent = ext;
+    ctx->coff.resize(nc + 1);
+    int64_t off = 0;
+    for (int32_t i = 0; i < nc; ++i) {
+        ctx->coff[i] = off;
+        off += round_up(ext[i], 64);
+    }
+    ctx->coff[nc] = off;
+    ctx->total_len = off;
+    // chunks of kTilesPerChunk tiles; fewer (>= the tiles of one ring, so
+    // the ring divides the chunk) when the genome is too small to fill the GPU
+    const int64_t tiles = std::max<int64_t>(1, (off + kTileW - 1) / kTileW);
+    const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : kTilesPerChunk;
+    int tpc = kTilesPerChunk;
+    while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < 2048 &&
+           ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
+        tpc /= 2;
+    ctx->tiles_per_chunk = tpc;
+    ctx->chunk_w = (int64_t)tpc * kTileW;
+    ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
+    int tpc_base = tpc;
+    if (tpc > kPlainTilesPerChunk && tpc % kPlainTilesPerChunk == 0 &&
+        ((int64_t)kPlainTilesPerChunk * kTileW) % kRing == 0)
+        tpc_base = kPlainTilesPerChunk;
+    ctx->tpc_base = tpc_base;
+    ctx->cstride = tpc / tpc_base;
+    const int64_t wb = (int64_t)tpc_base * kTileW;
+    ctx->n_chunks_base = std::max<int64_t>(1, (off + wb - 1) / wb);
+}
+
+// log2 of the base chunk width (a power of two: kTileW and the tiles per
+// chunk are)
+static int base_lw(const mc_ctx* ctx) {
+    int lw = 0;
+    while (((int64_t)1 << lw) < (int64_t)ctx->tpc_base * kTileW) ++lw;
+    return lw;
+}
+static_assert((kTileW & (kTileW - 1)) == 0 && (kTilesPerChunk & (kTilesPerChunk - 1)) == 0 &&
+                  (kPlainTilesPerChunk & (kPlainTilesPerChunk - 1)) == 0,
+              "chunk widths must be powers of two (ingest and the probe shift by log2 of them)");
+
+// The contig offsets on the device, uploaded only when they changed (a new
+// batch over the same contigs keeps them).  coff_up: pinned staging.
+static int upload_coff(mc_ctx* ctx, int64_t* coff_up) {
+    const int32_t nc = (int32_t)ctx->len.size();
+    HIP_TRY(ctx->d_coff.reserve(nc + 1));
+    if (ctx->coff_dev != ctx->coff || ctx->coff_dev_gen != ctx->d_coff.gen) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));   // the staging buffer's last copy has drained
+        std::memcpy(coff_up, ctx->coff.data(), (nc + 1) * 8);
+        HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, coff_up, (nc + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        ctx->coff_dev = ctx->coff;
+        ctx->coff_dev_gen = ctx->d_coff.gen;
+    }
+    return MC_OK;
+}
+
+// K1 on a raw-CIGAR batch whose spans are still pending (CIGAR words -> span)
+static int run_k1(mc_ctx* ctx) {
+    ctx->t_cigar = false;
+    if (!ctx->spans_pending) return MC_OK;
+    hipStream_t s = ctx->stream;
+    const int64_t n = ctx->n_reads;
+    HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    const int64_t nb = (n + kBlock - 1) / kBlock;
+    const size_t lds = (kBlock + 1) * 8 + 8 + kBlock * 4 + kOwnerBuckets;
+    const int64_t* co = ctx->cig_off_ext ? ctx->cig_off_ext : ctx->d_cig_off.p;
+    const uint32_t* cw = ctx->cigar_ext ? ctx->cigar_ext : ctx->d_cigar.p;
+    hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s, co, cw, n, ctx->d_span.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    ctx->t_cigar = true;
+    ctx->spans_pending = false;
+    ctx->cig_off_ext = nullptr;   // borrowed until this prepare's stream sync
+    ctx->cigar_ext = nullptr;
+    return MC_OK;
+}
+
 extern "C" int mc_prepare(mc_ctx* ctx) {
     if (int rc = ctx_use(ctx)) return rc;
     if (ctx->prepared) return MC_OK;
+    ctx->direct_retry_full = false;
     const int32_t nc = (int32_t)ctx->len.size();
     const int64_t n = ctx->n_reads;
     hipStream_t s = ctx->stream;
-    ctx->t_cigar = false;
-    if (ctx->spans_pending) {
-        HIP_TRY(hipEventRecord(ctx->ev[0], s));
-        const int64_t nb = (n + kBlock - 1) / kBlock;
-        const size_t lds = (kBlock + 1) * 8 + 8 + kBlock * 4 + kOwnerBuckets;
-        const int64_t* co = ctx->cig_off_ext ? ctx->cig_off_ext : ctx->d_cig_off.p;
-        const uint32_t* cw = ctx->cigar_ext ? ctx->cigar_ext : ctx->d_cigar.p;
-        hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s, co, cw, n,
-                           ctx->d_span.p);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ctx->ev[1], s));
-        ctx->t_cigar = true;
-        ctx->spans_pending = false;
-        ctx->cig_off_ext = nullptr;   // borrowed until this prepare's stream sync
-        ctx->cigar_ext = nullptr;
-    }
+    if (int rc = run_k1(ctx)) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // K2 loads whole int4 batches past n: the tid padding must index coff
     // (zeroed by prep_clear_kernel with the first ingest pass)
@@ -574,54 +663,17 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     // (its chunk-end flushes double) and reads its chunk c as base chunks
     // [c*s, c*s + s).  Long reads' end buckets and carries are per full
     // chunk, so with long reads the plain K2 runs on full chunks too.
-    auto layout = [&](const std::vector<int64_t>& ext) {
-        ctx->extent = ext;
-        ctx->coff.resize(nc + 1);
-        int64_t off = 0;
-        for (int32_t i = 0; i < nc; ++i) {
-            ctx->coff[i] = off;
-            off += round_up(ext[i], 64);
-        }
-        ctx->coff[nc] = off;
-        ctx->total_len = off;
-        // chunks of kTilesPerChunk tiles; fewer (>= the tiles of one ring, so
-        // the ring divides the chunk) when the genome is too small to fill the GPU
-        const int64_t tiles = std::max<int64_t>(1, (off + kTileW - 1) / kTileW);
-        const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : kTilesPerChunk;
-        int tpc = kTilesPerChunk;
-        while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < 2048 &&
-               ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
-            tpc /= 2;
-        ctx->tiles_per_chunk = tpc;
-        ctx->chunk_w = (int64_t)tpc * kTileW;
-        ctx->n_chunks = std::max<int64_t>(1, (off + ctx->chunk_w - 1) / ctx->chunk_w);
-        int tpc_base = tpc;
-        if (tpc > kPlainTilesPerChunk && tpc % kPlainTilesPerChunk == 0 &&
-            ((int64_t)kPlainTilesPerChunk * kTileW) % ctx->ring == 0)
-            tpc_base = kPlainTilesPerChunk;
-        ctx->tpc_base = tpc_base;
-        ctx->cstride = tpc / tpc_base;
-        const int64_t wb = (int64_t)tpc_base * kTileW;
-        ctx->n_chunks_base = std::max<int64_t>(1, (off + wb - 1) / wb);
-    };
     // ---- ingest + chunk index in one pass over the reads, on the layout the
     // contig lengths give; a read past its contig's end grows the extent, and
     // the pass runs again on the final layout
     std::vector<int64_t> ext(ctx->len);
-    layout(ext);
+    set_layout(ctx, ext);
     const unsigned long long* h = res;                         // counters
     const long long* maxend = reinterpret_cast<const long long*>(res + 8);
     for (int pass = 0;; ++pass) {
         const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every full chunk's base chunks
         HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
-        // the device layout is uploaded only when it changed (a new batch over
-        // the same contigs keeps it)
-        if (ctx->coff_dev != ctx->coff || ctx->coff_dev_gen != ctx->d_coff.gen) {
-            std::memcpy(coff_up, ctx->coff.data(), (nc + 1) * 8);   // (pass 1's copy has drained)
-            HIP_TRY(hipMemcpyAsync(ctx->d_coff.p, coff_up, (nc + 1) * 8, hipMemcpyHostToDevice, s));
-            ctx->coff_dev = ctx->coff;
-            ctx->coff_dev_gen = ctx->d_coff.gen;
-        }
+        if (int rc = upload_coff(ctx, coff_up)) return rc;
         {
             const int64_t np_ = pass == 0 ? n_pad : 0, ni = 2 * n_base;
             const unsigned g = (unsigned)std::max<int64_t>(
@@ -633,15 +685,14 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             HIP_TRY(hipGetLastError());
         }
         if (n) {
-            if (MC_GPOS) HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kBatch)));   // whole-batch loads
-            IngestIndex ix{ctx->d_coff.p, 0, ctx->short_max, n_base, ctx->d_chunk_first.p};
-            while (((int64_t)1 << ix.lw) < (int64_t)ctx->tpc_base * kTileW) ++ix.lw;
+            HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kBatch)));   // whole-batch loads
+            IngestIndex ix{ctx->d_coff.p, base_lw(ctx), ctx->short_max, n_base, ctx->d_chunk_first.p};
             const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
                                                                       ctx->ingest_grid));
             hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
                                ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
                                reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
-                               ctx->d_scratch.p + 8 + nc, ix, MC_GPOS ? ctx->d_gpos.p : nullptr);
+                               ctx->d_scratch.p + 8 + nc, ix, ctx->d_gpos.p);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipMemcpyAsync(res, ctx->d_scratch.p, n_res * 8, hipMemcpyDeviceToHost, s));
@@ -659,7 +710,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             }
         if (!grew) break;
         MC_REQUIRE(pass == 0, MC_E_STATE, "contig extents changed on the second ingest pass");
-        layout(ext);
+        set_layout(ctx, ext);
     }
     ctx->aligned_bases = (int64_t)h[2];
     ctx->max_span = (int32_t)h[3];
@@ -712,10 +763,103 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     HIP_TRY(hipEventRecord(ctx->ev[3], s));
     HIP_TRY(hipStreamSynchronize(s));
     ctx->t.prepare_ms = elapsed(ctx, 2, 3);
+    ctx->t.prepare_ms_total += ctx->t.prepare_ms;
     ctx->t.cigar_ms = ctx->t_cigar ? elapsed(ctx, 0, 1) : 0.f;
     ctx->prepared = true;
     ctx->depth_valid = false;
     ++ctx->prep_gen;
+    ctx->t.full_prepares += 1;
+    return MC_OK;
+}
+
+// ---- the direct per-batch prepare (see probe_kernel): the layout the contig
+// lengths give, the sample probe, nothing synchronous.  K2 then validates
+// every read; check_direct() reads its verdict after the call's sync and
+// direct_fallback() hands a batch it cannot take to mc_prepare.
+static bool direct_eligible(const mc_ctx* ctx) {
+    return ctx->direct_enabled && ctx->direct_ok && ctx->n_reads > 0 && !ctx->len.empty();
+}
+
+static int prepare_direct(mc_ctx* ctx) {
+    const int32_t nc = (int32_t)ctx->len.size();
+    const int64_t n = ctx->n_reads;
+    hipStream_t s = ctx->stream;
+    if (int rc = run_k1(ctx)) return rc;
+    HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    ctx->ring = kRing;
+    ctx->short_max = ctx->ring - kTileW;
+    const size_t n_res = 8 + 2 * (size_t)nc;   // (pin_io's layout, shared with mc_prepare)
+    HIP_TRY(ctx->pin_io.reserve((n_res + nc + 1) * 8));
+    int64_t* coff_up = reinterpret_cast<int64_t*>(static_cast<unsigned long long*>(ctx->pin_io.h) + n_res);
+    set_layout(ctx, ctx->len);
+    if (int rc = upload_coff(ctx, coff_up)) return rc;
+    const int64_t n_base = ctx->n_chunks * ctx->cstride;
+    HIP_TRY(ctx->d_jidx.reserve(2 * (n_base + 1)));
+    HIP_TRY(ctx->d_fsamp.reserve(nc + 1));
+    if (!ctx->d_dres.p) {
+        HIP_TRY(ctx->d_dres.reserve(kDresWords));
+        HIP_TRY(hipMemsetAsync(ctx->d_dres.p, 0, kDresWords * 8, s));   // generation stamps start below 1
+    }
+    // (K2's whole-batch loads read up to 3 reads of padding past n; the
+    // direct K2 neither applies nor checks reads at or past n)
+    ProbeArgs P{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_coff.p, base_lw(ctx),
+                ctx->short_max, n_base, ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_fsamp.p,
+                ctx->d_dres.p, ++ctx->direct_gen};
+    const int64_t M = (n + kProbeStride - 1) >> kProbeShift;
+    hipLaunchKernelGGL(probe_kernel, dim3((unsigned)std::max<int64_t>(1, (M + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, s, P);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->ev[3], s));
+    HIP_TRY(ctx->d_depth.reserve((size_t)(ctx->n_chunks * ctx->chunk_w)));
+    ctx->has_long = false;
+    ctx->max_span = 0;
+    ctx->aligned_bases = -1;   // K2 counts them
+    ctx->prepared = true;
+    ctx->direct = true;
+    ctx->direct_checked = false;
+    ctx->depth_valid = false;
+    ++ctx->prep_gen;
+    return MC_OK;
+}
+
+// K2's verdict on a direct batch (res: a host copy of d_dres).  True: the
+// batch is exactly what the direct path computed (the counts become the
+// prepare's results); false: direct_fallback + mc_prepare must redo it.
+static bool check_direct(mc_ctx* ctx, const unsigned long long* res) {
+    const unsigned long long g = ctx->direct_gen;
+    if (res[kDresBadSample] == g || res[kDresLongSample] == g || res[kDresFlags]) return false;
+    ctx->aligned_bases = (int64_t)res[kDresBases];
+    ctx->direct_checked = true;
+    ctx->t.direct_batches += 1;
+    ctx->t.prepare_ms = elapsed(ctx, 2, 3);
+    ctx->t.prepare_ms_total += ctx->t.prepare_ms;
+    ctx->t.cigar_ms = ctx->t_cigar ? elapsed(ctx, 0, 1) : 0.f;
+    return true;
+}
+
+// A batch the direct path cannot represent: long reads or reads past their
+// contig's end keep this contig set on the full prepare from now on; invalid
+// or unsorted reads only get mc_prepare's exact error.
+static void direct_fallback(mc_ctx* ctx, const unsigned long long* res) {
+    const unsigned long long g = ctx->direct_gen;
+    if (res[kDresLongSample] == g || (res[kDresFlags] & kDirectUnfit)) ctx->direct_ok = false;
+    ctx->direct_retry_full = true;
+    ctx->fused_clean = false;
+    invalidate(ctx);
+}
+
+// Prepare for a compute call: the direct path when it may apply, else the
+// full one.
+static int prepare_for_compute(mc_ctx* ctx) {
+    if (ctx->prepared) return MC_OK;
+    if (direct_eligible(ctx) && !ctx->direct_retry_full) return prepare_direct(ctx);
+    return mc_prepare(ctx);
+}
+
+extern "C" int mc_set_direct_prepare(mc_ctx* ctx, int enable) {
+    if (int rc = ctx_use(ctx)) return rc;
+    ctx->direct_enabled = enable != 0;
+    if (!ctx->direct_enabled && ctx->direct) invalidate(ctx);
     return MC_OK;
 }
 
@@ -761,15 +905,20 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
 #endif
     const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistLds + kOvInts : 0)) * 4 + MC_EXTRA_LDS;
     const bool lng = ctx->has_long;
-    const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true> : (const void*)depth_kernel<true, false>)
-                            : (lng ? (const void*)depth_kernel<false, true> : (const void*)depth_kernel<false, false>);
+    const bool dir = ctx->direct;
+    const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true, false>
+                                   : dir ? (const void*)depth_kernel<true, false, true>
+                                         : (const void*)depth_kernel<true, false, false>)
+                            : (lng ? (const void*)depth_kernel<false, true, false>
+                                   : dir ? (const void*)depth_kernel<false, false, true>
+                                         : (const void*)depth_kernel<false, false, false>);
     const K2Geom geo = k2_geom(ctx, stats);
     const int tpc = geo.tpc;
     const int64_t nch = geo.n_chunks;
     const int cstride = geo.cstride;
     const int64_t* cfirst = ctx->d_chunk_first.p;
     int grid = 0;
-    if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : 0), kfn, lds, nch, &grid))
+    if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : dir ? 4 : 0), kfn, lds, nch, &grid))
         return rc;
     if (!stats) {   // the fused path's fused_init_kernel (or the last K3b) zeroes them
         ctx->fused_clean = false;   // this K2 consumes the queue
@@ -781,17 +930,22 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
     const ReadArrays ra{ctx->d_gpos.p, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p};
-#define MC_LAUNCH_K2(S, L)                                                                     \
-    hipLaunchKernelGGL((depth_kernel<S, L>), dim3(grid), dim3(kBlock), lds, s, ra,               \
+    const int64_t n_base = ctx->n_chunks * ctx->cstride;
+    const DirectArgs da{ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_len.p, (int32_t)ctx->len.size(),
+                        ctx->d_dres.p, ctx->direct_gen};
+#define MC_LAUNCH_K2(S, L, D)                                                                  \
+    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, ra,            \
                        ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
-                       toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr)
+                       toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr, da)
     if (stats) {
-        if (lng) MC_LAUNCH_K2(true, true);
-        else MC_LAUNCH_K2(true, false);
+        if (lng) MC_LAUNCH_K2(true, true, false);
+        else if (dir) MC_LAUNCH_K2(true, false, true);
+        else MC_LAUNCH_K2(true, false, false);
     } else {
-        if (lng) MC_LAUNCH_K2(false, true);
-        else MC_LAUNCH_K2(false, false);
+        if (lng) MC_LAUNCH_K2(false, true, false);
+        else if (dir) MC_LAUNCH_K2(false, false, true);
+        else MC_LAUNCH_K2(false, false, false);
     }
 #undef MC_LAUNCH_K2
     HIP_TRY(hipGetLastError());
@@ -805,9 +959,20 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
 
 extern "C" int mc_compute_depth(mc_ctx* ctx) {
     if (int rc = ctx_use(ctx)) return rc;
-    if (int rc = mc_prepare(ctx)) return rc;
+    if (int rc = prepare_for_compute(ctx)) return rc;
     FusedRegions none{};
-    return launch_depth(ctx, none);
+    if (int rc = launch_depth(ctx, none)) return rc;
+    if (ctx->direct && !ctx->direct_checked) {   // K2's verdict on the batch
+        unsigned long long* res = static_cast<unsigned long long*>(ctx->pin_io.h);
+        HIP_TRY(hipMemcpyAsync(res, ctx->d_dres.p, kDresWords * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (!check_direct(ctx, res)) {
+            direct_fallback(ctx, res);
+            if (int rc = mc_prepare(ctx)) return rc;
+            return launch_depth(ctx, none);
+        }
+    }
+    return MC_OK;
 }
 
 static int fetch_max_depth(mc_ctx* ctx) {
@@ -991,7 +1156,7 @@ constexpr int kWinBelow = MC_WIN_BELOW;   // window bins below the estimated bod
 // Staging layout of a fused call: sorted region arrays (nf), then per-region
 // arrays (R).  The fallback flags come back through ctx->h_fflag.
 struct FusedLayout {
-    size_t gs, ge, id, base, ntot, nzx, brow, up, total;
+    size_t gs, ge, id, base, ntot, nzx, brow, rtid, rfused, up, total;
 };
 static FusedLayout fused_layout(int64_t nf, int64_t R) {
     auto al = stage_align;
@@ -1003,9 +1168,46 @@ static FusedLayout fused_layout(int64_t nf, int64_t R) {
     L.ntot = L.base + al(nf * 4);
     L.nzx = L.ntot + al(R * 8);
     L.brow = L.nzx + al(R * 8);
-    L.up = L.brow + al(R * 4);
+    L.rtid = L.brow + al(R * 4);        // each row's contig (window_kernel)
+    L.rfused = L.rtid + al(R * 4);      // each row's fused entry, or -1
+    L.up = L.rfused + al(R * 4);
     L.total = L.up;
     return L;
+}
+
+// Internal return code: the direct batch went back to the full prepare
+// (direct_fallback); the call starts over.
+constexpr int kRedo = 1;
+
+// mapped host words after the fused call's flags: [R] fallback flags, [R]
+// K2's max depth, then (8-byte aligned) a copy of d_dres
+static size_t fflag_ints(int64_t R) { return (size_t)round_up(R + 1, 2) + 2 * kDresWords; }
+static unsigned long long* fflag_dres(int* base, int64_t R) {
+    return reinterpret_cast<unsigned long long*>(base + round_up(R + 1, 2));
+}
+
+// Histogram windows of a direct batch: window_kernel from the probe's samples.
+static int launch_window(mc_ctx* ctx, int64_t R, const FusedLayout& L) {
+    if (R == 0) return MC_OK;
+    unsigned char* d = ctx->fstage.d.p;
+    hipLaunchKernelGGL(window_kernel, dim3((unsigned)((R + kWaves - 1) / kWaves)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_fsamp.p, ctx->d_span.p, ctx->n_reads, ctx->d_len.p,
+                       reinterpret_cast<const int32_t*>(d + L.rtid), reinterpret_cast<const int32_t*>(d + L.rfused),
+                       R, kWinBelow, reinterpret_cast<int32_t*>(d + L.brow), reinterpret_cast<int32_t*>(d + L.base));
+    HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+// K2's verdict on a direct batch outside the fused call (a D2H copy + sync):
+// MC_OK, or kRedo after direct_fallback.
+static int direct_verdict_sync(mc_ctx* ctx) {
+    if (!ctx->direct || ctx->direct_checked) return MC_OK;
+    unsigned long long* res = static_cast<unsigned long long*>(ctx->pin_io.h);
+    HIP_TRY(hipMemcpyAsync(res, ctx->d_dres.p, kDresWords * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (check_direct(ctx, res)) return MC_OK;
+    direct_fallback(ctx, res);
+    return kRedo;
 }
 
 // The launches of a fused call whose region arrays are staged in
@@ -1019,9 +1221,10 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     const K2Geom geo = k2_geom(ctx, true);
     HIP_TRY(ctx->d_fchunk.reserve(geo.n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
-    const int vals = fused_hist_vals(ctx->has_long);   // values per region row
+    const int vals = kHistBins;   // values per region row
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * vals)));
-    HIP_TRY(ctx->h_fflag.reserve(R + 1));
+    HIP_TRY(ctx->h_fflag.reserve(fflag_ints(R)));
+    const bool verdict = ctx->direct && !ctx->direct_checked;   // K3b hands K2's counters back
     HIP_TRY(ctx->d_acc.reserve(R));
     unsigned char* d = ctx->fstage.d.p;
     const int64_t* d_fge = reinterpret_cast<const int64_t*>(d + o_ge);
@@ -1057,16 +1260,13 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     // K3b: its span is timed from K2's end event (one event fewer per call)
     ctx->stats_after_depth = true;
     // one wave per region; flags [0, R) and K2's max depth [R] land in mapped host memory
-#define MC_LAUNCH_K3B(V)                                                                         \
-    hipLaunchKernelGGL(region_final_wave_kernel<V>, dim3((unsigned)((R + kWaves - 1) / kWaves)),  \
-                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,                        \
-                       reinterpret_cast<const int64_t*>(d + o_ntot),                              \
-                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,         \
-                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,               \
-                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p)
-    if (vals == kHistBins) MC_LAUNCH_K3B(kHistBins);
-    else MC_LAUNCH_K3B(2 * kHistBins);
-#undef MC_LAUNCH_K3B
+    hipLaunchKernelGGL(region_final_wave_kernel<kHistBins>, dim3((unsigned)((R + kWaves - 1) / kWaves)),
+                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,
+                       reinterpret_cast<const int64_t*>(d + o_ntot),
+                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,
+                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p,
+                       verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
@@ -1074,6 +1274,10 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     // the flags are in host memory once the stream has drained (no copy command)
     HIP_TRY(hipStreamSynchronize(s));
     const int* flags = ctx->h_fflag.h;
+    if (verdict && !check_direct(ctx, fflag_dres(ctx->h_fflag.h, R))) {
+        direct_fallback(ctx, fflag_dres(ctx->h_fflag.h, R));
+        return kRedo;
+    }
     ctx->max_depth = flags[R];   // a fallback's K3 sizes its histogram by it
     std::vector<int32_t> ft;
     std::vector<int64_t> fs, fe, fr_idx;
@@ -1103,16 +1307,17 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     return MC_OK;
 }
 
-static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
                             const int64_t* end, RegionOut* d_out) {
-    if (int rc = mc_prepare(ctx)) return rc;
+    if (int rc = prepare_for_compute(ctx)) return rc;
     MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
     auto& fc = ctx->fcache;
+    // direct batch: the windows come from the probe's samples (window_kernel)
+    const bool direct = ctx->direct;
     // histogram window of each region: kHistBins values, kWinBelow of them
     // below its contig's estimated body depth
-    // the long-read K2 packs two values per bin: a window twice as wide
-    const int vals = fused_hist_vals(ctx->has_long);
-    const int64_t win_below = (int64_t)kWinBelow * vals / kHistBins;
+    const int vals = kHistBins;
+    const int64_t win_below = kWinBelow;
     const double span_mean = ctx->n_reads ? (double)ctx->aligned_bases / (double)ctx->n_reads : 0.0;
     // the contig's body depth: its aligned bases over its length less one
     // mean read span (the two end ramps hold about half a span of depth
@@ -1137,14 +1342,19 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         // regions, their order and the chunk -> region index stand; only the
         // window bases follow the new per-contig bases (one small upload)
         const FusedLayout L = fused_layout(fc.nf, R);
-        unsigned char* h = ctx->fstage.host();
-        int32_t* brow = reinterpret_cast<int32_t*>(h + L.brow);
-        int32_t* fbase = reinterpret_cast<int32_t*>(h + L.base);
-        const int32_t* fid = reinterpret_cast<const int32_t*>(h + L.id);
-        for (int64_t r = 0; r < R; ++r) brow[r] = window_base(tid[r]);
-        for (int64_t k = 0; k < fc.nf; ++k) fbase[k] = brow[fid[k]];
-        HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p + L.base, h + L.base, L.up - L.base, hipMemcpyHostToDevice,
-                               ctx->stream));
+        if (direct) {
+            if (int rc = launch_window(ctx, R, L)) return rc;
+        } else {
+            unsigned char* h = ctx->fstage.host();
+            int32_t* brow = reinterpret_cast<int32_t*>(h + L.brow);
+            int32_t* fbase = reinterpret_cast<int32_t*>(h + L.base);
+            const int32_t* fid = reinterpret_cast<const int32_t*>(h + L.id);
+            HIP_TRY(hipStreamSynchronize(ctx->stream));   // the staging buffer's last upload has drained
+            for (int64_t r = 0; r < R; ++r) brow[r] = window_base(tid[r]);
+            for (int64_t k = 0; k < fc.nf; ++k) fbase[k] = brow[fid[k]];
+            HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p + L.base, h + L.base, L.rtid - L.base, hipMemcpyHostToDevice,
+                                   ctx->stream));
+        }
         fc.gen = ctx->prep_gen;
         return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
     }
@@ -1166,7 +1376,7 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         const int64_t a = std::min(start[r], ext), b = std::min(end[r], ext);
         ntot[r] = end[r] - start[r];
         nzx[r] = ntot[r] - (b - a);
-        base_row[r] = window_base(tid[r]);
+        base_row[r] = direct ? 0 : window_base(tid[r]);
         if (b > a)
             regs.push_back({ctx->coff[tid[r]] + a, ctx->coff[tid[r]] + b, (int32_t)r, base_row[r]});
     }
@@ -1177,6 +1387,7 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     if (!fusable) {
         FusedRegions none{};
         if (int rc = launch_depth(ctx, none)) return rc;
+        if (int rc = direct_verdict_sync(ctx)) return rc;
         return region_stats_impl(ctx, R, tid, start, end, d_out);
     }
     const int64_t nf = (int64_t)regs.size();
@@ -1192,7 +1403,15 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     std::memcpy(h + L.ntot, ntot.data(), R * 8);
     std::memcpy(h + L.nzx, nzx.data(), R * 8);
     std::memcpy(h + L.brow, base_row.data(), R * 4);
+    std::memcpy(h + L.rtid, tid, R * 4);
+    {
+        int32_t* rf = reinterpret_cast<int32_t*>(h + L.rfused);
+        for (int64_t r = 0; r < R; ++r) rf[r] = -1;
+        for (int64_t k = 0; k < nf; ++k) rf[regs[k].id] = (int32_t)k;
+    }
     HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p, h, L.up, hipMemcpyHostToDevice, ctx->stream));
+    if (direct)
+        if (int rc = launch_window(ctx, R, L)) return rc;
     fc.tid.assign(tid, tid + R);
     fc.start.assign(start, start + R);
     fc.end.assign(end, end + R);
@@ -1207,6 +1426,14 @@ static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     return depth_stats_launch(ctx, R, tid, start, end, d_out, nf);
 }
 
+
+static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                            const int64_t* end, RegionOut* d_out) {
+    int rc = depth_stats_once(ctx, R, tid, start, end, d_out);
+    if (rc == kRedo) rc = depth_stats_once(ctx, R, tid, start, end, d_out);   // now on the full prepare
+    MC_REQUIRE(rc != kRedo, MC_E_STATE, "direct prepare fell back twice");
+    return rc;
+}
 
 extern "C" int mc_compute_depth_stats(mc_ctx* ctx, int64_t R, const int32_t* tid,
                                       const int64_t* start, const int64_t* end,
@@ -1261,6 +1488,7 @@ extern "C" int mc_region_stats(mc_ctx* ctx, int64_t R, const int32_t* tid, const
 extern "C" int mc_aligned_bases(mc_ctx* ctx, int64_t* out) {
     if (int rc = ctx_use(ctx)) return rc;
     MC_REQUIRE(out, MC_E_INVALID, "null out");
+    if (ctx->direct && !ctx->direct_checked) invalidate(ctx);   // (only after a failed call)
     if (int rc = mc_prepare(ctx)) return rc;
     *out = ctx->aligned_bases;
     return MC_OK;

@@ -44,51 +44,15 @@ namespace mc {
 #ifndef MC_WAVES_STATS
 #define MC_WAVES_STATS 4               // __launch_bounds__ waves/SIMD, fused K2 (<= 128 VGPRs)
 #endif
-#ifndef MC_SP_COPY
-#define MC_SP_COPY 1                   // spans waited for at the batch advance, not in the apply loop
-#endif
-#ifndef MC_DEFER_STORE
-#define MC_DEFER_STORE 1               // a tile's depth stores wait until the next tile's reads are applied
-#endif
-#ifndef MC_QUEUE_AHEAD
-// K2: reserve the next chunk at the start of the current one (in-process A/B:
-// C3 plain +6.7 %, fused +3.0 %, C5 plain +3.5 %, C5 fused -3.6 %): only the
-// fused long-read variant does
-#define MC_QUEUE_AHEAD 0
-#endif
-#ifndef MC_QUEUE_AHEAD_FUSED_LONG
-#define MC_QUEUE_AHEAD_FUSED_LONG 1
-#endif
-#ifndef MC_XCD_QUEUES
-// K2: 8 chunk queues over contiguous chunk ranges, one per blockIdx % 8 group
-// (an XCD), stealing when empty.  In-process A/B: C3 plain +0.8 %, fused
-// +2.0 %, C5 fused +1.0 % (K2's HBM traffic is within 5 % of its algorithmic
-// bytes, so there is little L2 reuse to win, and one queue is not the limit)
-#define MC_XCD_QUEUES 0
-#endif
-#ifndef MC_SCALAR_COFF
-#define MC_SCALAR_COFF 1               // contig offsets of a read batch by scalar loads
-#endif
-#ifndef MC_GPOS
-// K2 reads each read as (low 32 bits of its global start, span), 8 B/read,
-// instead of (tid, pos, span), 12 B/read, and needs no contig offsets:
-// ingest_kernel writes the starts (4 B/read more in prepare).  Chunk-relative
-// starts are exact in 32-bit wrap-around arithmetic, since every read K2
-// applies starts within one tile before its chunk or inside it.
-// 2: one word per read, 4 B/read: the start's low kGposBits bits (the same
-// wrap-around, over a range that holds a chunk and the tile before it) and
-// the span capped at kGspanCap (> short_max, so the cap still marks a long
-// read; K2 needs a long read's span only to tell that it is one).
-// In-process A/B against 1 (profiles/r02zz_pack_ab_c*.txt): plain K2 C3
-// 0.811 -> 0.762 ms, C5 0.848 -> 0.806; fused C3 0.949 -> 0.950, C5 1.102 ->
-// 1.115 (the fused kernel is issue-bound: the decode costs what the bytes save).
-#define MC_GPOS 2
-#endif
-#ifndef MC_GPOS_NT
-// non-temporal stores of the read words in ingest: C3 prepare 0.353 -> 0.368 ms,
-// C5 0.632 -> 0.636 (profiles/r02zz_nt_prep.txt).  Off.
-#define MC_GPOS_NT 0
-#endif
+// K2 reads each read of a prepared batch as ONE 4-byte word, written by
+// ingest_kernel: the low kGposBits bits of its global start (chunk-relative
+// starts are exact as the sign-extended difference, since every read K2
+// applies starts at most one tile before its chunk or inside it) and its span
+// capped at kGspanCap (> short_max, so the cap still marks a long read; K2
+// needs a long read's span only to tell that it is one).  In-process A/B
+// against (start, span) words (profiles/r02zz_pack_ab_c*.txt): plain K2 C3
+// 0.811 -> 0.762 ms, C5 0.848 -> 0.806; against (tid, pos, span) 0.904 ->
+// 0.762.  The direct path (probe_kernel) reads the raw tuples instead.
 constexpr int kGposBits = 18;
 constexpr unsigned kGposMask = (1u << kGposBits) - 1u;
 constexpr int kGspanCap = (1 << (32 - kGposBits)) - 1;   // 16383
@@ -406,7 +370,7 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             acc.bases += b;
             acc.end = max(acc.end, (long long)e);
         }
-        if (MC_GPOS && gpos) {   // K2's starts: coff[tid] + pos mod 2^32 (= chunk * w + offset)
+        if (gpos) {   // K2's read words: start bits (coff[tid] + pos = chunk * w + offset) and span
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t q = gb + 64 * u + lane;
@@ -414,13 +378,12 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     g[k] = ((unsigned)cid[4 * u + k] << X.lw) + (unsigned)off[4 * u + k];
-                    if (MC_GPOS == 2)
-                        g[k] = (g[k] & kGposMask) | ((unsigned)min(ss[4 * u + k], kGspanCap) << kGposBits);
+                    g[k] = (g[k] & kGposMask) | ((unsigned)min(ss[4 * u + k], kGspanCap) << kGposBits);
                 }
                 if (q < g1) {
                     const i32x4 w = i32x4{(int)g[0], (int)g[1], (int)g[2], (int)g[3]};
-                    if (MC_GPOS_NT) __builtin_nontemporal_store(w, reinterpret_cast<i32x4*>(gpos + q * 4));
-                    else *reinterpret_cast<i32x4*>(gpos + q * 4) = w;
+                    // (non-temporal stores: C3 prepare 0.353 -> 0.368 ms, r02zz_nt_prep.txt)
+                    *reinterpret_cast<i32x4*>(gpos + q * 4) = w;
                 }
             }
         }
@@ -540,6 +503,176 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
         if (threadIdx.x == 3) atomicMax(&out[3], (unsigned long long)v);
         else if (v) atomicAdd(&out[threadIdx.x], (unsigned long long)v);
     }
+}
+
+// ------------------------------------------------------ direct prepare
+//
+// The per-batch path without the ingest pass.  ingest_kernel streams all
+// 12 B/read once before K2 (0.35 ms at C3) only to find each chunk's reads,
+// the extents and the per-contig bases.  The direct path gets the chunk
+// ranges from a sparse sample instead and lets K2, which reads every read
+// anyway, do the validation:
+//
+//   probe_kernel   one thread per sample (every kProbeStride-th read): its
+//                  global start key_j = coff[tid] + pos in the layout the
+//                  contig lengths give.  For each chunk-grid target P, J(P) =
+//                  the number of samples with key < P is j + 1 exactly when
+//                  key_j < P <= key_{j+1}, so thread j writes J for the
+//                  targets in that interval (usually none or one): no search.
+//                  lb(P), the first read with key >= P, then lies in
+//                  ((J-1)*S, J*S].  The same sweep gives each contig's first
+//                  sample (fsamp, for the histogram windows) and flags
+//                  unsorted or invalid samples and long spans.
+//   window_kernel  each fused region's histogram window from its contig's
+//                  samples (count x mean span over the contig length).
+//   depth_kernel<.., kDirect = true>  chunk c loads the reads in
+//                  [lower(J(C0 - short_max)), upper(J(C0 + W))) as raw
+//                  (tid, pos, span), applies those that overlap it, and
+//                  validates the reads in [lower(J(C0)), lower(J(C0 + W))):
+//                  these ranges partition [0, n) whenever the samples are
+//                  sorted (J is monotone), so every read is checked exactly
+//                  once (range, order against its predecessor, overhang past
+//                  its contig, span <= short_max) and its span summed.
+// Anything the direct path cannot represent (unsorted or invalid reads, a
+// read past its contig's end, a long read) is reported in DirectRes; the host
+// then re-runs the batch through the full prepare, which raises the exact
+// errors or builds the extents and long-read buckets.
+constexpr int kProbeShift = 8;                 // sample stride S = 256 reads
+constexpr int kProbeStride = 1 << kProbeShift;
+
+// dres[]: probe flags (the call's generation stamp, so they need no reset)
+// and K2's verdict (zeroed by the probe, or-ed / added by K2's workgroups)
+enum : int {
+    kDresBadSample = 0,      // gen: an unsorted or invalid sample
+    kDresLongSample = 1,     // gen: a sampled span > short_max
+    kDresFlags = 2,          // K2: kDirectInvalid | kDirectUnfit
+    kDresBases = 3,          // K2: aligned bases
+    kDresWords = 4
+};
+constexpr unsigned kDirectInvalid = 1;   // an invalid or unsorted read: mc_prepare's error
+constexpr unsigned kDirectUnfit = 2;     // a long read or one past its contig's end
+
+struct ProbeArgs {
+    const int32_t* tid;
+    const int32_t* pos;
+    const int32_t* span;
+    int64_t n;
+    int32_t nc;
+    const int64_t* coff;               // [nc + 1] layout from the contig lengths
+    int lw;                            // grid step w = 2^lw (the plain K2's chunks)
+    int short_max;
+    int64_t n_base;                    // grid targets k = 0 .. n_base
+    int32_t* j0;                       // [n_base + 1] J(k * w)
+    int32_t* jh;                       // [n_base + 1] J(k * w - short_max)
+    int32_t* fsamp;                    // [nc + 1] first sample of contig t
+    unsigned long long* dres;
+    unsigned long long gen;
+};
+
+__device__ __forceinline__ int64_t probe_key(const ProbeArgs& A, int t, int p) {
+    const int ct = t < 0 ? 0 : t >= A.nc ? A.nc - 1 : t;
+    const int64_t k = A.coff[ct] + (int64_t)(p < 0 ? 0 : p);
+    return k;
+}
+
+// J(P) = j + 1 for the targets k of one grid with key_j < P(k) <= key_next,
+// P(k) = k * w - off: k in [(key_j + off) >> lw + 1, (key_next + off) >> lw]
+__device__ __forceinline__ void probe_fill(int32_t* J, int64_t n_base, int lw, int64_t off, int64_t key,
+                                           int64_t key_next, bool first, bool last, int32_t val) {
+    int64_t k0 = first ? 0 : ((key + off) >> lw) + 1;
+    int64_t k1 = last ? n_base : ((key_next + off) >> lw);
+    if (k1 > n_base) k1 = n_base;
+    if (first) {   // targets at or below the first sample: J = 0
+        int64_t kz = (key + off) >> lw;
+        if (kz > n_base) kz = n_base;
+        for (int64_t k = 0; k <= kz; ++k) J[k] = 0;
+        k0 = kz + 1;
+    }
+    for (int64_t k = k0; k <= k1; ++k) J[k] = val;
+}
+
+__global__ void __launch_bounds__(kBlock)
+probe_kernel(ProbeArgs A) {
+    const int64_t M = (A.n + kProbeStride - 1) >> kProbeShift;
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x >= kDresFlags && threadIdx.x < kDresWords)
+        A.dres[threadIdx.x] = 0;   // K2's counters (K2 runs after this launch)
+    int t = 0, p = 0, s = 0;
+    int64_t key = 0;
+    if (j < M) {
+        const int64_t i = j << kProbeShift;
+        t = A.tid[i];
+        p = A.pos[i];
+        s = A.span[i];
+        key = probe_key(A, t, p);
+    }
+    // the next sample: from the neighbouring lane, lane 63 loads its own
+    int64_t key_next = (int64_t)(((uint64_t)(uint32_t)__shfl_down((int)(key >> 32), 1, 64) << 32) |
+                                 (uint32_t)__shfl_down((int)(key & 0xffffffff), 1, 64));
+    int t_next = __shfl_down(t, 1, 64);
+    int p_next = __shfl_down(p, 1, 64);
+    if (j >= M) return;
+    const bool last = j == M - 1;
+    if (lane == 63 && !last) {
+        const int64_t i = (j + 1) << kProbeShift;
+        t_next = A.tid[i];
+        p_next = A.pos[i];
+        key_next = probe_key(A, t_next, p_next);
+    }
+    const bool bad = ((unsigned)t >= (unsigned)A.nc) | (p < 0) | (s < 0);
+    const bool uns = !last && ((t > t_next) | ((t == t_next) & (p > p_next)) | (key > key_next));
+    if (bad | uns) atomicMax(&A.dres[kDresBadSample], A.gen);
+    if (s > A.short_max) atomicMax(&A.dres[kDresLongSample], A.gen);
+    const bool first = j == 0;
+    probe_fill(A.j0, A.n_base, A.lw, 0, key, key_next, first, last, (int32_t)(j + 1));
+    probe_fill(A.jh, A.n_base, A.lw, A.short_max, key, key_next, first, last, (int32_t)(j + 1));
+    // contigs (tid_j, tid_next] start after sample j
+    const int ct = t < 0 ? 0 : t >= A.nc ? A.nc - 1 : t;
+    const int cn = last ? A.nc : (t_next < 0 ? 0 : t_next >= A.nc ? A.nc - 1 : t_next);
+    if (first)
+        for (int k = 0; k <= ct; ++k) A.fsamp[k] = 0;
+    for (int k = ct + 1; k <= cn; ++k) A.fsamp[k] = (int32_t)(j + 1);
+}
+
+// One wave per region row: the window base of its histogram from its
+// contig's samples (the same estimate the full prepare makes from exact
+// per-contig bases: depth over the contig less one mean read span, kWinBelow
+// bins of the window below it).  Writes the row's base and its fused entry's.
+__global__ void __launch_bounds__(kBlock)
+window_kernel(const int32_t* __restrict__ fsamp, const int32_t* __restrict__ span, int64_t n,
+              const int64_t* __restrict__ len, const int32_t* __restrict__ rtid,
+              const int32_t* __restrict__ rfused, int64_t R, int win_below,
+              int32_t* __restrict__ brow, int32_t* __restrict__ fbase) {
+    const int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= R) return;
+    const int t = rtid[r];
+    const int64_t a = fsamp[t], b = fsamp[t + 1];
+    const int64_t ns = b - a;
+    // up to 1024 of the contig's samples, evenly strided
+    const int64_t take = ns < 1024 ? ns : 1024;
+    long long sum = 0;
+    for (int64_t k = lane; k < take; k += 64) {
+        const int64_t smp = a + k * ns / take;
+        const int64_t i = smp << kProbeShift;
+        if (i < n) sum += span[i];
+    }
+    sum = wave_sum64(sum);
+    if (lane != 0) return;
+    int32_t base = 0;
+    if (ns > 0 && take > 0) {
+        const double mean = (double)sum / (double)take;
+        const double bases = (double)ns * (double)kProbeStride * mean;
+        const double ext = (double)len[t];
+        const double body = ext > 2.0 * mean ? ext - mean : ext;
+        const double est = ext > 0 ? bases / body : 0.0;
+        const long long b0 = llrint(est) - win_below;
+        base = (int32_t)(b0 > 0 ? b0 : 0);
+    }
+    brow[r] = base;
+    const int32_t k = rfused[r];
+    if (k >= 0) fbase[k] = base;
 }
 
 // Prepare's buffer setup in one launch (three fills were three commands in
@@ -986,17 +1119,17 @@ struct ReadBatch {                     // 4 reads in chunk-relative coordinates
     unsigned pending;                  // bit k: read k still to apply
 };
 
-struct RawBatch {                      // one batch of reads as loaded (int4 per array)
-#if MC_GPOS == 2
+// One batch of reads as loaded (int4 per array): the packed read words of a
+// prepared batch (ingest_kernel), or the raw tuples (direct path).
+template <bool kDirect> struct RawBatch;
+template <> struct RawBatch<false> {
     i32x4 g;                           // packed start bits and capped span
-#elif MC_GPOS
-    i32x4 g, s;                        // low 32 bits of the global start, span
-#else
+};
+template <> struct RawBatch<true> {
     i32x4 t, p, s;
-#endif
 };
 
-// The read arrays K2 loads: gpos (MC_GPOS) or tid + pos, and span
+// The read arrays K2 loads: the packed words, or tid / pos / span
 struct ReadArrays {
     const uint32_t* __restrict__ gpos;
     const int32_t* __restrict__ tid;
@@ -1004,123 +1137,167 @@ struct ReadArrays {
     const int32_t* __restrict__ span;
 };
 
-// Issue the three 16-byte loads of this thread's 4 reads.  The arrays are
-// padded by one batch past n (tid padding zero-filled), so no bounds check.
-// Lanes whose 4 reads all lie at or past `cend` (the chunk's last batch runs
-// past the chunk) load nothing: those are the next chunk's reads, which
-// another workgroup, usually on another XCD, fetches again (PMC: the
-// overshoot was most of K2's 21-39 % fetch excess over 12 B/read).
-__device__ __forceinline__ void issue_raw(RawBatch& r, int64_t base, const ReadArrays& A, int64_t cend) {
+// Issue the 16-byte loads of this thread's 4 reads.  The arrays are padded
+// by one batch past n, so no bounds check.  Lanes whose 4 reads all lie at or
+// past `cend` (the chunk's last batch runs past the chunk) load nothing:
+// those are the next chunk's reads, which another workgroup, usually on
+// another XCD, fetches again (PMC: the overshoot was most of K2's 21-39 %
+// fetch excess over its algorithmic bytes).
+template <bool kDirect>
+__device__ __forceinline__ void issue_raw(RawBatch<kDirect>& r, int64_t base, const ReadArrays& A,
+                                          int64_t cend) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-#if MC_GPOS == 2
-    r.g = i0 < cend ? *reinterpret_cast<const i32x4*>(A.gpos + i0) : i32x4{0, 0, 0, 0};
-#elif MC_GPOS
-    if (i0 < cend) {
-        r.g = *reinterpret_cast<const i32x4*>(A.gpos + i0);
-        r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
+    if constexpr (kDirect) {
+        if (i0 < cend) {
+            r.t = *reinterpret_cast<const i32x4*>(A.tid + i0);
+            r.p = *reinterpret_cast<const i32x4*>(A.pos + i0);
+            r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
+        } else {
+            r.t = r.p = r.s = i32x4{0, 0, 0, 0};
+        }
     } else {
-        r.g = r.s = i32x4{0, 0, 0, 0};
+        r.g = i0 < cend ? *reinterpret_cast<const i32x4*>(A.gpos + i0) : i32x4{0, 0, 0, 0};
     }
-#else
-    if (i0 < cend) {
-        r.t = *reinterpret_cast<const i32x4*>(A.tid + i0);
-        r.p = *reinterpret_cast<const i32x4*>(A.pos + i0);
-        r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
-    } else {
-        r.t = r.p = r.s = i32x4{0, 0, 0, 0};
-    }
-#endif
 }
 
-// Chunk-relative start of the 4 reads: 4 independent coff lookups (small
-// table, cache-resident); reads at or past n (the chunk's read end) are masked.  Starts far outside the
-// chunk are clamped (they are never applied: a read is applied only while
-// its start lies before the current tile end).
-// lo: the chunk's first read (reads before it in the first batch's aligned
-// group are masked: with MC_GPOS their start may lie any distance before the
-// chunk, outside the 32-bit wrap-around range).
-__device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch& r, int64_t base,
-                                             int64_t n, int64_t C0,
-                                             const int64_t* __restrict__ coff, int64_t lo) {
+// Packed read words: chunk-relative start and span of the 4 reads; reads at
+// or past n (the chunk's read end) are masked.  lo: the chunk's first read
+// (reads before it in the first batch's aligned group are masked: their start
+// may lie any distance before the chunk, outside the wrap-around range).
+__device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch<false>& r, int64_t base,
+                                             int64_t n, int64_t C0, int64_t lo) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-#if MC_GPOS == 2
-    (void)coff;
     static_assert((int64_t)MC_TILES_PER_CHUNK * kTileW + kRing < (1 << (kGposBits - 1)),
                   "packed starts: a chunk and its halo must fit the signed wrap-around range");
     static_assert(kGspanCap > kRing - kTileW, "the span cap must exceed short_max");
-    {
-        const unsigned c0 = (unsigned)C0 & kGposMask;
-        const unsigned gg[4] = {(unsigned)r.g.x, (unsigned)r.g.y, (unsigned)r.g.z, (unsigned)r.g.w};
+    const unsigned c0 = (unsigned)C0 & kGposMask;
+    const unsigned gg[4] = {(unsigned)r.g.x, (unsigned)r.g.y, (unsigned)r.g.z, (unsigned)r.g.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            // sign-extend the kGposBits-bit difference
-            const int d = (int)(((gg[k] - c0) & kGposMask) << (32 - kGposBits)) >> (32 - kGposBits);
-            b.rs[k] = d;
-            b.sp[k] = (int)(gg[k] >> kGposBits);
-        }
+    for (int k = 0; k < 4; ++k) {
+        // sign-extend the kGposBits-bit difference
+        const int d = (int)(((gg[k] - c0) & kGposMask) << (32 - kGposBits)) >> (32 - kGposBits);
+        b.rs[k] = d;
+        b.sp[k] = (int)(gg[k] >> kGposBits);
     }
-#elif MC_GPOS
-    (void)coff;
-    const unsigned c0 = (unsigned)C0;
-    b.rs[0] = (int)((unsigned)r.g.x - c0);
-    b.rs[1] = (int)((unsigned)r.g.y - c0);
-    b.rs[2] = (int)((unsigned)r.g.z - c0);
-    b.rs[3] = (int)((unsigned)r.g.w - c0);
-#elif MC_SCALAR_COFF
-    // The wave's distinct contigs (one or two per batch unless contigs are
-    // tiny) one at a time: a uniform index, so coff comes in on the scalar
-    // path (lgkmcnt).  Per-lane vector loads here would need a vmcnt(0),
-    // which on gfx9 also waits for every depth store still in flight.
+    const int64_t left = n - i0;
+    b.pending = left >= 4 ? 0xfu : left <= 0 ? 0u : ((1u << left) - 1u);
+    const int64_t skip = lo - i0;   // > 0 only in thread 0 of the chunk's first batch
+    if (skip > 0) b.pending &= skip >= 4 ? 0u : ~((1u << skip) - 1u);
+}
+
+// Direct path (see probe_kernel): K2's own view of the batch and what it checks.
+struct DirectArgs {
+    const int32_t* j0;                 // [n_base + 1] J(k * w)       (probe_kernel)
+    const int32_t* jh;                 // [n_base + 1] J(k * w - short_max)
+    const int64_t* len;                // [nc] contig lengths (= extents on this path)
+    int32_t nc;
+    unsigned long long* dres;
+    unsigned long long gen;
+};
+
+struct DirectChunk {                   // wave-uniform per chunk
+    int64_t lo, hi;                    // reads loaded (and applied where they overlap)
+    int64_t vlo, vhi;                  // reads this chunk validates
+};
+
+struct DirectAcc {                     // per-lane verdict
+    unsigned flags = 0;                // kDirectInvalid | kDirectUnfit
+    unsigned long long bases = 0;
+};
+
+// Raw tuples: chunk-relative starts (contig offsets and lengths by scalar
+// loads per distinct contig of the wave: a per-lane vector load would need a
+// vmcnt(0), which on gfx9 also waits for every depth store in flight), the
+// apply mask (valid reads of [lo, hi) starting before the chunk end), and the
+// checks of the reads in [vlo, vhi): range, order against the predecessor
+// (the neighbouring lane's last read; lane 0 loads its own by scalar loads),
+// overhang, span.
+__device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch<true>& r, int64_t base,
+                                                    int64_t C0, int64_t chunk_w, const DirectChunk& dc,
+                                                    const ReadArrays& A, const int64_t* __restrict__ coff,
+                                                    const DirectArgs& D, int short_max, DirectAcc& acc) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
     const int tt[4] = {r.t.x, r.t.y, r.t.z, r.t.w};
     const int pp[4] = {r.p.x, r.p.y, r.p.z, r.p.w};
-    int64_t g[4] = {0, 0, 0, 0};
-    unsigned todo = 0xfu;   // tids are >= 0 (validated by ingest; padding is 0)
+    int sp[4];
+    asm volatile("v_mov_b32 %0, %1" : "=v"(sp[0]) : "v"(r.s.x));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(sp[1]) : "v"(r.s.y));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(sp[2]) : "v"(r.s.z));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(sp[3]) : "v"(r.s.w));
+    unsigned valid = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        valid |= (((unsigned)tt[k] < (unsigned)D.nc) & (pp[k] >= 0) & (sp[k] >= 0)) ? 1u << k : 0u;
+    constexpr int64_t kClamp = int64_t(1) << 30;
+    int rs[4] = {0, 0, 0, 0};
+    unsigned L[4] = {0, 0, 0, 0};          // contig length (positions fit 32 bits)
+    unsigned todo = valid;
     for (;;) {
         const int cand = (todo & 1u) ? tt[0] : (todo & 2u) ? tt[1] : (todo & 4u) ? tt[2]
                        : (todo & 8u) ? tt[3] : -1;
         const unsigned long long act = __ballot(cand >= 0);
         if (!act) break;
         const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
-        const int64_t c = coff[t0];
+        const int64_t c = uload(coff, t0) - C0, ln = uload(D.len, t0);
+        const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (((todo >> k) & 1u) && tt[k] == t0) {
-                g[k] = c + pp[k];
+                const int64_t rel = c + pp[k];
+                rs[k] = (int)(rel < -kClamp ? -kClamp : rel > kClamp ? kClamp : rel);
+                L[k] = l32;
                 todo &= ~(1u << k);
             }
     }
-#else
-    const int64_t g[4] = {coff[r.t.x] + r.p.x, coff[r.t.y] + r.p.y, coff[r.t.z] + r.p.z,
-                          coff[r.t.w] + r.p.w};
-#endif
-#if !MC_GPOS
-    constexpr int64_t kClamp = int64_t(1) << 30;
+    // predecessor of read 0: lane - 1's read 3; lane 0 of each wave by scalar loads
+    const int64_t wfirst = base + (int64_t)(threadIdx.x & ~63) * kReadsPerThread;
+    int pt = __shfl_up(tt[3], 1, 64), ppv = __shfl_up(pp[3], 1, 64);
+    if (lane == 0) {
+        pt = wfirst > 0 ? uload(A.tid, wfirst - 1) : -1;
+        ppv = wfirst > 0 ? uload(A.pos, wfirst - 1) : 0;
+    }
+    unsigned pend = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int64_t rel = g[k] - C0;
-        b.rs[k] = (int)(rel < -kClamp ? -kClamp : rel > kClamp ? kClamp : rel);
+        const int64_t i = i0 + k;
+        b.rs[k] = rs[k];
+        b.sp[k] = sp[k];
+        const bool ok = (valid >> k) & 1u;
+        pend |= (ok & (i >= dc.lo) & (i < dc.hi) & (rs[k] < chunk_w) & (sp[k] <= short_max)) ? 1u << k : 0u;
+        const bool own = (i >= dc.vlo) & (i < dc.vhi);
+        const int qt = k ? tt[k - 1] : pt, qp = k ? pp[k - 1] : ppv;
+        const bool uns = (i > 0) & ((qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k])));
+        const bool unfit = (sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k]);
+        acc.flags |= own ? (!ok | uns ? kDirectInvalid : unfit ? kDirectUnfit : 0u) : 0u;
+        acc.bases += (own & ok) ? (unsigned)sp[k] : 0u;
     }
-#endif
-    // The spans are copied into registers of their own here: used straight from
-    // the load's destination, their first use inside the apply loop carried a
-    // vmcnt(0) that ran every tile and drained the previous tile's depth stores
-    // (in-order vmcnt); here the wait runs once per batch.
-#if MC_GPOS == 2
-#elif MC_SP_COPY
-    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[0]) : "v"(r.s.x));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[1]) : "v"(r.s.y));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[2]) : "v"(r.s.z));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(b.sp[3]) : "v"(r.s.w));
-#else
-    b.sp[0] = r.s.x;
-    b.sp[1] = r.s.y;
-    b.sp[2] = r.s.z;
-    b.sp[3] = r.s.w;
-#endif
-    const int64_t left = n - i0;
-    b.pending = left >= 4 ? 0xfu : left <= 0 ? 0u : ((1u << left) - 1u);
-    const int64_t skip = lo - i0;   // > 0 only in thread 0 of the chunk's first batch
-    if (skip > 0) b.pending &= skip >= 4 ? 0u : ~((1u << skip) - 1u);
+    b.pending = pend;
+}
+
+// K2 direct: the per-workgroup verdict into dres (one atomic each)
+__device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArgs& D, long long* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned f = a.flags;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) f |= __shfl_xor(f, d, 64);
+    const long long bases = wave_sum64((long long)a.bases);
+    __syncthreads();
+    if (lane == 0) {
+        red[wave] = bases;
+        red[kWaves + wave] = f;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0, ff = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            t += red[w];
+            ff |= red[kWaves + w];
+        }
+        if (ff) atomicOr(&D.dres[kDresFlags], (unsigned long long)ff);
+        if (t) atomicAdd(&D.dres[kDresBases], (unsigned long long)t);
+    }
 }
 
 // Fused region statistics of K2 (optional): non-overlapping regions sorted by
@@ -1196,46 +1373,11 @@ __device__ __forceinline__ void ov_reset(OvLds* ov) {
     ov->cnt = ov->low = 0;
 }
 
-// A lane's runs outside the histogram window (contig ends, depth far from
-// the mean), summed in the lane, then added to its record (ov = the record).
-// Out of line: its temporaries stay off the hot loop's register budget.
-// v < 0: no run in that slot.
-__device__ __attribute__((noinline, cold)) void ov_add_lane(OvLds* ov, int v0, int n0, int v1, int n1,
-                                                       int v2, int n2, int v3, int base) {
-    unsigned long long s = 0, q = 0;
-    unsigned c = 0, lo = 0;
-    int mn = 0x7fffffff, mx = 0;
-    auto take = [&](int v, int n) {
-        if (v < 0) return;
-        s += (unsigned long long)v * (unsigned long long)n;
-        q += (unsigned long long)((long long)v * v) * (unsigned long long)n;
-        c += n;
-        if (v < base) lo += n;
-        mn = min(mn, v);
-        mx = max(mx, v);
-    };
-    take(v0, n0);
-    take(v1, n1);
-    take(v2, n2);
-    take(v3, 1);
-    if (c) {
-        atomicAdd(&ov->cnt, c);
-        if (lo) atomicAdd(&ov->low, lo);
-        atomicAdd(&ov->sum, s);
-        atomicAdd(&ov->sq, q);
-        atomicMin(&ov->vmin, mn);
-        atomicMax(&ov->vmax, mx);
-    }
-}
-
-// MC_OV_REGS: out-of-window runs accumulate in each lane's registers (an
-// OvReg, 8 VGPRs) while the region stays open in the chunk, and go to the
-// lane's LDS record only before the region's histogram is flushed.  On C5,
-// where the end ramps of deep contigs fall below the window, adding every
-// int4's runs to the LDS records (6 atomics) cost 0.075 ms of a 1.13 ms fused K2.
-#ifndef MC_OV_REGS
-#define MC_OV_REGS 1
-#endif
+// Out-of-window runs accumulate in each lane's registers (an OvReg, 8 VGPRs)
+// while the region stays open in the chunk, and go to the lane's LDS record
+// only before the region's histogram is flushed.  On C5, where the end ramps
+// of deep contigs fall below the window, adding every int4's runs to the LDS
+// records (6 atomics) cost 0.075 ms of a 1.13 ms fused K2.
 struct OvReg {
     unsigned cnt, low;
     unsigned long long sum, sq;
@@ -1282,97 +1424,37 @@ __device__ __forceinline__ void ov_reg_spill(OvReg& r, OvLds* ovf) {
     }
 }
 
+// K2 zeroes one tile of ring slots per chunk (where the ends of reads running
+// past the chunk landed), not the whole ring
+static_assert(kRing == 2 * kTileW, "the ring tail is one tile (short_max = kTileW)");
+
 // Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
-// one predicated LDS atomic per run of equal values, no branches except the
-// rare out-of-window path (same run arithmetic as region_seg_kernel).
-#ifndef MC_HALF_RING_ZERO
-#define MC_HALF_RING_ZERO 1            // K2 zeroes one tile of ring slots per chunk, not the whole ring
-#endif
-static_assert(!MC_HALF_RING_ZERO || kRing == 2 * kTileW, "the ring tail is one tile (short_max = kTileW)");
-#ifndef MC_HIST_BRANCHLESS
-#define MC_HIST_BRANCHLESS 1
-#endif
-#ifndef MC_HIST_PACK_LONG
-// 1: the long-read fused K2 packs two values per bin (hist_int4).  C5 A/B (bench
-// --config c5): fallback regions 123 -> 25, but K2 +0.025 ms for the packing
-// arithmetic and K3b no faster (its fixed cost is the fallback round trip,
-// not the number of regions in it): step 1.305 -> 1.335 ms.  Off.
-#define MC_HIST_PACK_LONG 0
-#endif
-// values per region row of the global fused histogram
-__host__ __device__ constexpr int fused_hist_vals(bool long_reads) {
-    return (long_reads && MC_HIST_PACK_LONG) ? 2 * kHistBins : kHistBins;
-}
-// dummy: this lane's pad slot (index into h).  MC_HIST_BRANCHLESS: every slot
-// issues its atomic, lanes with nothing to add put 0 into their own pad slot;
+// one LDS atomic per run of equal values, branch-free (every slot issues its
+// atomic; lanes with nothing to add put 0 into their own pad slot `dummy`:
 // the predicated form cost ~6 SALU exec-mask instructions per atomic, and the
-// fused K2 is bound by instruction issue, not by LDS (SQ counters, r02a).
-// kPack (the long-read variant): a bin holds two values as 16-bit counters
-// (value base + 2b in the low half, base + 2b + 1 in the high half), so the
-// same LDS and the same one atomic per run cover a window of 2 kHistBins
-// values.  A half cannot carry: a chunk has 32 Ki positions and the bins are
-// flushed at every chunk end, and the copies split those positions.  The
-// wider window is what the ramps of deep contigs need (their quartile ranks
-// span more than kHistBins values: a fallback to K3 otherwise).
-template <bool kPack>
-__device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvLds* ov, OvReg& ovr, int y0, int y1,
-                                          int y2, int y3, int base) {
+// fused K2 is bound by instruction issue, not by LDS), and the rare
+// out-of-window path (same run arithmetic as region_seg_kernel).
+__device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, int y0, int y1, int y2, int y3,
+                                          int base) {
     const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
     const int l2 = s3 ? 1 : 2;
     const int l1 = s2 ? 1 : l2 + 1;
     const int l0 = s1 ? 1 : l1 + 1;
     const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
-    constexpr unsigned kWin = kPack ? 2u * kHistBins : (unsigned)kHistBins;
+    constexpr unsigned kWin = (unsigned)kHistBins;
     const unsigned d0 = (unsigned)(y0 - base), d1 = (unsigned)(y1 - base),
                    d2 = (unsigned)(y2 - base), d3 = (unsigned)(y3 - base);
     const bool w0 = e0 && d0 < kWin, w1 = e1 && d1 < kWin, w2 = e2 && d2 < kWin, w3 = e3 && d3 < kWin;
-    const unsigned b0 = kPack ? d0 >> 1 : d0, b1 = kPack ? d1 >> 1 : d1, b2 = kPack ? d2 >> 1 : d2,
-                   b3 = kPack ? d3 >> 1 : d3;
-    // the run lengths, shifted into their value's half
-    const unsigned i0 = kPack ? (unsigned)l0 << ((d0 & 1u) << 4) : (unsigned)l0;
-    const unsigned i1 = kPack ? (unsigned)l1 << ((d1 & 1u) << 4) : (unsigned)l1;
-    const unsigned i2 = kPack ? (unsigned)l2 << ((d2 & 1u) << 4) : (unsigned)l2;
-    const unsigned i3 = kPack ? 1u << ((d3 & 1u) << 4) : 1u;
-#ifdef MC_EXP_NO_HIST
-    asm volatile("" :: "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(l0), "v"(l1), "v"(l2));
-#elif defined(MC_EXP_NO_CONFLICT)   // diagnostic (wrong results): every lane its own bin
-    {
-        const int lb = (int)(threadIdx.x & 63) * 8 % (kHistBins - 8);
-        atomicAdd(&h[lb], w0 ? i0 : 0u);
-        atomicAdd(&h[lb + 1], w1 ? i1 : 0u);
-        atomicAdd(&h[lb + 2], w2 ? i2 : 0u);
-        atomicAdd(&h[lb + 3], w3 ? i3 : 0u);
-        (void)b0; (void)b1; (void)b2; (void)b3; (void)dummy;
-    }
-#elif MC_HIST_BRANCHLESS
-    atomicAdd(&h[w0 ? (int)b0 : dummy], w0 ? i0 : 0u);
-    atomicAdd(&h[w1 ? (int)b1 : dummy], w1 ? i1 : 0u);
-    atomicAdd(&h[w2 ? (int)b2 : dummy], w2 ? i2 : 0u);
-    atomicAdd(&h[w3 ? (int)b3 : dummy], w3 ? i3 : 0u);
-#else
-    (void)dummy;
-    if (w0) atomicAdd(&h[b0], i0);
-    if (w1) atomicAdd(&h[b1], i1);
-    if (w2) atomicAdd(&h[b2], i2);
-    if (w3) atomicAdd(&h[b3], i3);
-#endif
+    atomicAdd(&h[w0 ? (int)d0 : dummy], w0 ? (unsigned)l0 : 0u);
+    atomicAdd(&h[w1 ? (int)d1 : dummy], w1 ? (unsigned)l1 : 0u);
+    atomicAdd(&h[w2 ? (int)d2 : dummy], w2 ? (unsigned)l2 : 0u);
+    atomicAdd(&h[w3 ? (int)d3 : dummy], w3 ? 1u : 0u);
     const bool o0 = e0 && !w0, o1 = e1 && !w1, o2 = e2 && !w2, o3 = e3 && !w3;
-#ifndef MC_EXP_NO_OV
     if (__builtin_expect(__any(o0 || o1 || o2 || o3), 0)) {
-#else
-    if (false) {
-#endif
-#if MC_OV_REGS
-        (void)ov;
         ov_reg_take(ovr, o0, y0, l0, base);
         ov_reg_take(ovr, o1, y1, l1, base);
         ov_reg_take(ovr, o2, y2, l2, base);
         ov_reg_take(ovr, o3, y3, 1, base);
-#else
-        (void)ovr;
-        ov_add_lane(ov + (threadIdx.x & (kOvRecs - 1)), o0 ? y0 : -1, l0, o1 ? y1 : -1, l1,
-                    o2 ? y2 : -1, l2, o3 ? y3 : -1, base);
-#endif
     }
 }
 
@@ -1420,11 +1502,8 @@ __device__ __forceinline__ void load_events(EvBatch& e, const int32_t* __restric
 // into the region's global accumulator and flushes the LDS histogram.
 // kBarriers = false: the caller has just passed a barrier after the last
 // atomics, and a barrier follows before the histogram is used again.
-template <bool kBarriers = true, bool kPack = false>
+template <bool kBarriers = true>
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsigned* h, OvLds* ov) {
-#ifdef MC_EXP_NO_FLUSH
-    return;
-#endif
     // id: the region's row, loaded with its other fields (no scalar load on
     // the chunk end's path)
     if (kBarriers) __syncthreads();   // every wave's histogram and overflow atomics are in
@@ -1439,21 +1518,13 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsi
             ov_reset(o);
         }
     }
-    // the region's row holds one counter per value: kHistBins, or 2 kHistBins packed
-    unsigned* g = R.hist + (int64_t)id * (kPack ? 2 * kHistBins : kHistBins);
+    unsigned* g = R.hist + (int64_t)id * kHistBins;
     for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
         unsigned cnt = 0;
 #pragma unroll
         for (int c = 0; c < kHistCopies; ++c) cnt += h[c * kHistStride + k];
         if (cnt) {
-#ifndef MC_EXP_NO_GATOMIC
-            if (kPack) {
-                if (cnt & 0xffffu) atomicAdd(&g[2 * k], cnt & 0xffffu);
-                if (cnt >> 16) atomicAdd(&g[2 * k + 1], cnt >> 16);
-            } else {
-                atomicAdd(&g[k], cnt);
-            }
-#endif
+            atomicAdd(&g[k], cnt);
 #pragma unroll
             for (int c = 0; c < kHistCopies; ++c) h[c * kHistStride + k] = 0;
         }
@@ -1461,43 +1532,31 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsi
     if (kBarriers) __syncthreads();
 }
 
-// K2's chunk queue (thread 0).  MC_XCD_QUEUES: queue q hands out the chunks
-// [n * q / 8, n * (q + 1) / 8); workgroup b starts on queue b % 8 (the blocks
-// the dispatcher places on one XCD, so neighbouring chunks, which share read
-// cache lines, meet in one L2; 8 counters instead of one contended address)
-// and moves on to the next queue when its own is empty.  Placement only
-// changes speed: every chunk is taken exactly once either way.
-__device__ __forceinline__ int take_chunk(unsigned* queue, int64_t n_chunks, int& qk) {
-#if MC_XCD_QUEUES
-    const int xq = blockIdx.x & 7;
-    while (qk < 8) {
-        const int q = (xq + qk) & 7;
-        const int64_t lo = n_chunks * q / 8, hi = n_chunks * (q + 1) / 8;
-        const unsigned t = atomicAdd(&queue[q], 1u);
-        if (lo + (int64_t)t < hi) return (int)(lo + t);
-        ++qk;
-    }
-    return (int)n_chunks;
-#else
-    (void)qk;
+// K2's chunk queue (thread 0): one counter.  (Eight queues over contiguous
+// chunk ranges, one per blockIdx % 8 group = one XCD, with stealing, ran
+// C3 plain +0.8 %, fused +2.0 %: K2's traffic is at its algorithmic bytes, so
+// there is no L2 reuse to win.)
+__device__ __forceinline__ int take_chunk(unsigned* queue, int64_t n_chunks) {
     const unsigned t = atomicAdd(queue, 1u);
     return t < (unsigned)n_chunks ? (int)t : (int)n_chunks;
-#endif
 }
 
 // One workgroup walks chunks of `tiles_per_chunk` tiles of kTileW positions
-// (dynamic queue).  Per chunk: the reads from chunk_first[c] (which already
-// includes the max-span halo) are applied as +1 at max(start, chunk start)
-// and -1 at end into an LDS ring of `ring` ints; each finished tile is
-// prefix-scanned (int4 per lane, wave scan, block carry) and stored to HBM
-// with 1 KiB-per-wave-instruction stores, and its ring slots are zeroed.
-// Reads longer than short_max = ring - kTileW take the long-read path (see
-// long_count_kernel); the halo of chunk_first is min(max_span, short_max).
+// (dynamic queue).  Per chunk: the chunk's reads are applied as +1 at
+// max(start, chunk start) and -1 at end into an LDS ring of kRing ints; each
+// finished tile is prefix-scanned (int4 per lane, wave scan, block carry) and
+// stored to HBM with 1 KiB-per-wave-instruction stores, and its ring slots
+// are zeroed.  Reads longer than short_max = kRing - kTileW take the long-read
+// path (see long_count_kernel).
 // kStats: fold the tile into FusedRegions before it leaves the registers.
 // kLong: the long-read path is compiled in (spans > short_max exist); without
 // it the event stream's registers are not held (the fused variant is at its
 // 128-VGPR budget).
-template <bool kStats, bool kLong>
+// kDirect: the batch was not prepared: the chunk's read range comes from the
+// probe's J arrays, the reads are loaded as raw (tid, pos, span), and K2
+// validates them (probe_kernel); otherwise the chunk index and the packed
+// read words of ingest_kernel.
+template <bool kStats, bool kLong, bool kDirect>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
 __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
                                                  : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
@@ -1507,9 +1566,10 @@ depth_kernel(ReadArrays A, int64_t n,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
              const int* __restrict__ chunk_carry,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
-             int* __restrict__ max_depth, FusedRegions R) {
+             int* __restrict__ max_depth, FusedRegions R, DirectArgs D) {
+    static_assert(!(kDirect && kLong), "the direct path has no long reads");
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    // [0] chunk id, [4..7] wave totals, [12..13] block_all votes
+    // [0] chunk id, [4..7] wave totals, [8..11] wave max, [12..13] block_all votes
     int* hdr = lds;
     int and_flip = 0;
     int* ring = lds + kLdsHeader;
@@ -1523,17 +1583,20 @@ depth_kernel(ReadArrays A, int64_t n,
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
-    // deferred tile stores: plain K2 only.  With 12 B/read they gained plain C3
-    // -2.4 %, C5 -4.9 %, fused C3 -1.2 % (fused long +0.9 %); with the packed read
-    // words the fused C3 K2 runs 1.6 % faster without them and the plain one
-    // the same (profiles/r02zz_knobs_ab.txt)
-#ifndef MC_DEFER_FUSED
-#define MC_DEFER_FUSED 0
-#endif
-    constexpr bool kDefer = MC_DEFER_STORE && (!kStats || (MC_DEFER_FUSED && !kLong));
-    constexpr bool kPack = kStats && kLong && MC_HIST_PACK_LONG;   // see hist_int4
+    // Deferred tile stores (a tile's stores issued after the next tile's
+    // apply loop), plain K2 only: with 12 B/read they gained plain C3 -2.4 %,
+    // C5 -4.9 %; with the packed read words the fused C3 K2 runs 1.6 % faster
+    // without them (profiles/r02zz_knobs_ab.txt).
+    constexpr bool kDefer = !kStats;
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
+    // The probe saw an unsorted / invalid sample or a long span: the host
+    // re-runs this batch through the full prepare; nothing to do here.
+    if (kDirect) {
+        const unsigned long long f0 = uload(D.dres, kDresBadSample), f1 = uload(D.dres, kDresLongSample);
+        if (f0 == D.gen || f1 == D.gen) return;
+    }
     int my_max = 0;
+    DirectAcc dacc;            // kDirect: this lane's validation counters
     OvReg ovr;                 // kStats: this lane's out-of-window runs of the open region
     ov_reg_reset(ovr);
     if (kStats) {
@@ -1542,19 +1605,19 @@ depth_kernel(ReadArrays A, int64_t n,
     }
 
     // chunk ids come from an atomic queue (thread 0); everything indexed by
-    // the chunk id is then loaded by every wave at a uniform index (uload)
-    // kAhead: the next chunk is reserved at the start of the current one,
-    // together with its first read batch, so the queue atomic's round trip
-    // overlaps that load instead of following the chunk's end (the WG then
-    // holds a chunk others cannot take: the tail balances worse).
-    constexpr bool kAhead = MC_QUEUE_AHEAD || (MC_QUEUE_AHEAD_FUSED_LONG && kStats && kLong);
-    int ticket = 0, qk = 0;
-    if (threadIdx.x == 0) hdr[0] = take_chunk(queue, n_chunks, qk);
+    // the chunk id is then loaded by every wave at a uniform index (uload).
+    // kAhead (the fused long-read variant): the next chunk is reserved at the
+    // start of the current one, so the queue atomic's round trip overlaps the
+    // chunk instead of following its end (C5 fused -3.6 %; elsewhere the held
+    // chunk worsens the tail balance: C3 plain +6.7 %, fused +3.0 %).
+    constexpr bool kAhead = kStats && kLong;
+    int ticket = 0;
+    if (threadIdx.x == 0) hdr[0] = take_chunk(queue, n_chunks);
     // the whole ring before the first chunk; after a chunk only the tile of
     // slots after its last tile, where the ends of reads running past the
     // chunk (at most short_max = one tile) landed: every tile's own slots are
     // zeroed by its scan
-    const int ring_tail = MC_HALF_RING_ZERO ? (int)(((int64_t)tiles_per_chunk * kTileW) % kRing) : 0;
+    const int ring_tail = (int)(((int64_t)tiles_per_chunk * kTileW) % kRing);
     for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
         *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
     for (;;) {
@@ -1562,14 +1625,33 @@ depth_kernel(ReadArrays A, int64_t n,
         __syncthreads();
         const int64_t c = (unsigned)__builtin_amdgcn_readfirstlane(hdr[0]);
         if (c >= n_chunks) break;
-        if (kAhead && threadIdx.x == 0) ticket = take_chunk(queue, n_chunks, qk);
-        // chunk c = base chunks [c * cstride, (c + 1) * cstride) of the index
-        // (ingest_kernel): its reads start at the first short read crossing
-        // its start, else at the first read starting in it
+        if (kAhead && threadIdx.x == 0) ticket = take_chunk(queue, n_chunks);
+        // chunk c = base chunks [c * cstride, (c + 1) * cstride)
         const int64_t b0 = c * cstride;
-        const int64_t cfirst = b0 ? (int64_t)min((uint64_t)uload(chunk_first, 2 * b0),
-                                                 (uint64_t)uload(chunk_first, 2 * b0 - 1)) : 0;
-        const int64_t cend = uload(chunk_first, 2 * (c + 1) * cstride - 1);   // reads of this chunk end
+        int64_t cfirst, cend;
+        DirectChunk dc{0, 0, 0, 0};
+        if (kDirect) {
+            // read ranges from the probe's sample counts J: lb(P) lies in
+            // ((J - 1) * S, J * S]; the first chunk starts at 0, the last ends at n
+            const int64_t b1 = b0 + cstride;
+            auto lower = [&](int64_t J) { return J <= 0 ? (int64_t)0 : min(n, ((J - 1) << kProbeShift) + 1); };
+            auto upper = [&](int64_t J) { return J <= 0 ? (int64_t)0 : min(n, J << kProbeShift); };
+            const bool last = c + 1 == n_chunks;
+            dc.lo = c ? lower(uload(D.jh, b0)) : 0;
+            dc.vlo = c ? lower(uload(D.j0, b0)) : 0;
+            dc.hi = last ? n : upper(uload(D.j0, b1));
+            dc.vhi = last ? n : lower(uload(D.j0, b1));
+            dc.lo = min(dc.lo, dc.vlo);   // (apart only on unsorted input, which is reported)
+            dc.hi = max(dc.hi, dc.vhi);
+            cfirst = dc.lo;
+            cend = dc.hi;
+        } else {
+            // index of ingest_kernel: the chunk's reads start at the first short
+            // read crossing its start, else at the first read starting in it
+            cfirst = b0 ? (int64_t)min((uint64_t)uload(chunk_first, 2 * b0),
+                                       (uint64_t)uload(chunk_first, 2 * b0 - 1)) : 0;
+            cend = uload(chunk_first, 2 * (c + 1) * cstride - 1);
+        }
         const int64_t C0 = c * chunk_w;
         int64_t rcur = 0, r_gs = 0, r_ge = 0;
         int r_base = 0, r_id = 0;
@@ -1585,16 +1667,21 @@ depth_kernel(ReadArrays A, int64_t n,
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
         bool more = base < cend;
         ReadBatch b;
-        RawBatch nxt;
+        RawBatch<kDirect> nxt;
         b.pending = 0;
+        auto finish = [&](const RawBatch<kDirect>& r, int64_t at) {
+            if constexpr (kDirect)
+                finish_batch_direct(b, r, at, C0, chunk_w, dc, A, coff, D, short_max, dacc);
+            else
+                finish_batch(b, r, at, cend, C0, cfirst);
+        };
         if (more) {
-            RawBatch r0;
-            issue_raw(r0, base, A, cend);
-            if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, A, cend);
-            finish_batch(b, r0, base, cend, C0, coff, cfirst);
+            RawBatch<kDirect> r0;
+            issue_raw<kDirect>(r0, base, A, cend);
+            if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
+            finish(r0, base);
         }
-        constexpr bool has_long = kLong;
-        int carry = has_long ? uload(chunk_carry, c) : 0;
+        int carry = kLong ? uload(chunk_carry, c) : 0;
         // -1 end events of long reads (chunk-relative, in tile order): a
         // second stream of 1024-event batches, applied like the reads while
         // they lie before the current tile end (a dependent load chain per
@@ -1603,7 +1690,7 @@ depth_kernel(ReadArrays A, int64_t n,
         eb.pending = 0;
         int64_t ev_lo = 0, ev_hi = 0, ev_base = 0;
         bool ev_more = false;
-        if (has_long) {   // the chunk's range of long-read end events
+        if (kLong) {   // the chunk's range of long-read end events
             ev_lo = uload(tile_ev_off, c * tiles_per_chunk);
             ev_hi = uload(tile_ev_off, (c + 1) * tiles_per_chunk);
             ev_base = ev_lo & ~(int64_t)3;
@@ -1611,7 +1698,7 @@ depth_kernel(ReadArrays A, int64_t n,
             if (ev_more) load_events(eb, tile_ev, ev_base, ev_lo, ev_hi);
         }
         i32x4 v[kChunks];          // the scanned tile (this wave's span)
-        int64_t pend_T0 = -1;      // MC_DEFER_STORE: tile whose depth in v is not stored yet
+        int64_t pend_T0 = -1;      // kDefer: tile whose depth in v is not stored yet
         auto store_tile = [&](int64_t tile0) {
             int32_t* dst = depth + tile0 + wave * kWaveSpan + lane * 4;
 #pragma unroll
@@ -1627,7 +1714,7 @@ depth_kernel(ReadArrays A, int64_t n,
             const int64_t Tend = T0 + kTileW;
             const int tend_rel = (t + 1) * kTileW;   // C0 is a multiple of the ring size
             for (;;) {
-                if (has_long) {
+                if (kLong) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
                         if (((eb.pending >> k) & 1u) && eb.rel[k] < tend_rel) {
@@ -1667,9 +1754,9 @@ depth_kernel(ReadArrays A, int64_t n,
                     base += kBatch;
                     more = base < cend;
                     if (more) {
-                        if (!kPf) issue_raw(nxt, base, A, cend);
-                        finish_batch(b, nxt, base, cend, C0, coff, cfirst);   // loaded one batch ago
-                        if (kPf && base + kBatch < cend) issue_raw(nxt, base + kBatch, A, cend);
+                        if (!kPf) issue_raw<kDirect>(nxt, base, A, cend);
+                        finish(nxt, base);   // loaded one batch ago
+                        if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
                     }
                 }
             }
@@ -1723,7 +1810,7 @@ depth_kernel(ReadArrays A, int64_t n,
                 // Only the value histogram is built here (runs of equal values
                 // within a lane share one LDS atomic); min/max/sum/sumsq follow
                 // from it in region_final_kernel.  Values outside the window
-                // go to the wave-reduced LDS overflow record (hist_int4).
+                // go to the lane's out-of-window record (hist_int4).
                 while (rcur < R.n && r_gs < Tend) {
                     const int64_t rgs = r_gs, rge = r_ge;
                     const int lo = (int)((rgs > T0 ? rgs : T0) - T0);
@@ -1739,11 +1826,11 @@ depth_kernel(ReadArrays A, int64_t n,
                             y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
                             y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        hist_int4<kPack>(hist_lane, hist_dummy, ovf, ovr, y0, y1, y2, y3, r_base);
+                        hist_int4(hist_lane, hist_dummy, ovr, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
-                        if (MC_OV_REGS) ov_reg_spill(ovr, ovf);
-                        flush_region<true, kPack>(R, r_id, hist, ovf);
+                        ov_reg_spill(ovr, ovf);
+                        flush_region<true>(R, r_id, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = uload(R.gs, rcur);
@@ -1758,15 +1845,15 @@ depth_kernel(ReadArrays A, int64_t n,
             }
         }
         if (kDefer && pend_T0 >= 0) store_tile(pend_T0);   // the chunk's last tile
-        if (kStats && MC_OV_REGS) ov_reg_spill(ovr, ovf);   // ordered by the barrier below
+        if (kStats) ov_reg_spill(ovr, ovf);   // ordered by the barrier below
         __syncthreads();   // everyone is past hdr / ring of this chunk (and its atomics)
         if (kStats) {
             // a region still open at the chunk end has partials here; the
             // barrier above and the one after the ring zeroing bracket it
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, kPack>(R, r_id, hist, ovf);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false>(R, r_id, hist, ovf);
         }
-        if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks, qk);
-        for (int k = threadIdx.x * 4; k < (MC_HALF_RING_ZERO ? kTileW : kRing); k += kBlock * 4)
+        if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks);
+        for (int k = threadIdx.x * 4; k < kTileW; k += kBlock * 4)
             *reinterpret_cast<i32x4*>(ring + ring_tail + k) = i32x4{0, 0, 0, 0};
     }
     // one atomic per workgroup (same-address atomics of every wave at the end of
@@ -1778,6 +1865,7 @@ depth_kernel(ReadArrays A, int64_t n,
         const int m = max(max(hdr[8], hdr[9]), max(hdr[10], hdr[11]));
         if (m > 0) atomicMax(max_depth, m);
     }
+    if (kDirect) direct_flush(dacc, D, reinterpret_cast<long long*>(ring));   // (ring: free now)
 }
 
 // ----------------------------------------------------------------- K3
@@ -2066,9 +2154,13 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
                          const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
                          int* __restrict__ fallback, const int32_t* __restrict__ base_of,
                          unsigned* __restrict__ low_of, int* __restrict__ max_depth,
-                         int* __restrict__ max_out, unsigned* __restrict__ queue) {
+                         int* __restrict__ max_out, unsigned* __restrict__ queue,
+                         const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out) {
     constexpr int kFinPer = (kVals + 63) / 64;
     const int lane = threadIdx.x & 63;
+    // dres_out (mapped host memory): the direct K2's validation counters, so
+    // the host reads its verdict with the flags, without a copy command
+    if (blockIdx.x == 0 && dres_out && threadIdx.x < kDresWords) dres_out[threadIdx.x] = dres_in[threadIdx.x];
     // queue != null: leave the fused buffers as fused_init_kernel does (zero
     // histograms and below-window counts, initial accumulators, K2's queue
     // and max depth), so a repeated call on the same regions skips that launch

@@ -176,6 +176,11 @@ class CoverageEngine:
     def prepare(self):
         self._check(self._lib.mc_prepare(self._h))
 
+    def set_direct_prepare(self, enable=True):
+        """Direct per-batch prepare on (default) or off (always mc_prepare):
+        see include/metacov_amd.h."""
+        self._check(self._lib.mc_set_direct_prepare(self._h, 1 if enable else 0))
+
     def invalidate(self):
         """Drop the prepared index: the next compute call re-prepares the
         same device reads, as for a fresh batch."""

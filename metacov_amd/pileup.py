@@ -16,6 +16,7 @@ region raises ValueError (pileup.py:19 on a zero-size vector); an unknown
 """
 import numpy as np
 
+from . import depthcap
 from .bam import BamFile
 from .engine import classic_stats
 from .experimental import experimental, load_kmerhist  # noqa: F401  (pileup.py:29-173)
@@ -43,13 +44,15 @@ def _resolve(bf, ref):
         raise KeyError(ref)
 
 
-def classic(bam, ref, start, end, device=0):
-    return classic_batch(bam, [(ref, start, end)], device=device)[0]
+def classic(bam, ref, start, end, device=0, max_depth=None):
+    return classic_batch(bam, [(ref, start, end)], device=device, max_depth=max_depth)[0]
 
 
-def classic_batch(bam, regions, device=0):
+def classic_batch(bam, regions, device=0, max_depth=None):
     """[(ref, start, end), ...] -> [dict, ...] in input order.  Each dict is
-    classic()'s; an empty region raises ValueError like classic()."""
+    classic()'s; an empty region raises ValueError like classic().
+    max_depth (opt-in, e.g. 8000 = pysam's default): reproduce htslib's
+    pileup read cap per region query (metacov_amd.depthcap); None: exact."""
     bf = _as_bamfile(bam)
     regions = list(regions)
     if not regions:
@@ -65,7 +68,10 @@ def classic_batch(bam, regions, device=0):
         if s < 0:
             raise ValueError("region start %d < 0" % s)
         starts[i], ends[i] = s, e
-    rows = bf.engine(device).region_stats(tids, starts, ends)
+    if max_depth is not None:
+        rows, _ = depthcap.capped_rows(bf, tids, starts, ends, int(max_depth), device)
+    else:
+        rows = bf.engine(device).region_stats(tids, starts, ends)
     return [classic_stats(r) for r in rows]
 
 

@@ -1,0 +1,87 @@
+"""htslib's pileup read cap (opt-in max_depth): the library's closed form
+(mc_depth_cap_mask, host C++) against a literal restatement of htslib's
+bam_plp_push / bam_plp_next loop (oracle/htslib_plp.py), per region query
+the way pysam's AlignmentFile.pileup(ref, start, end) runs it
+(metacov/pileup.py:13).  Parity with htslib itself is unpinned (htslib is
+absent here and the cap is version-dependent)."""
+import numpy as np
+import pytest
+
+from metacov_amd import depthcap
+from oracle import htslib_plp
+
+
+def kept_depth(pos, span, keep, start, end):
+    """classic()'s column vector from the kept reads (difference array)."""
+    d = np.zeros(end - start + 1, np.int64)
+    for p, s in zip(pos[keep], span[keep]):
+        a, b = max(p, start), min(p + max(s, 1), end)
+        if b > a:
+            d[a - start] += 1
+            d[b - start] -= 1
+    return np.cumsum(d)[:-1]
+
+
+def piles(rng, n_piles, pile_size, bg, L, span_rng):
+    starts = [int(x) for x in rng.integers(0, L - 400, size=n_piles)]
+    pos = [np.full(pile_size, s) for s in starts]
+    pos.append(rng.integers(0, L - 200, size=bg))
+    pos = np.concatenate(pos)
+    span = rng.integers(span_rng[0], span_rng[1] + 1, size=len(pos))
+    span = np.minimum(span, L - pos)
+    o = np.argsort(pos, kind="stable")
+    return pos[o].astype(np.int32), span[o].astype(np.int32)
+
+
+@pytest.mark.parametrize("cap,n_piles,pile,bg,seed", [
+    (5, 20, 12, 300, 1), (20, 10, 40, 500, 2), (64, 6, 150, 2000, 3), (3, 50, 6, 100, 4),
+    (1, 10, 5, 50, 5)])
+def test_cap_mask_matches_literal_htslib(cap, n_piles, pile, bg, seed):
+    rng = np.random.default_rng(seed)
+    L = 5000
+    pos, span = piles(rng, n_piles, pile, bg, L, (1, 300))
+    tid = np.zeros(len(pos), np.int32)
+    for (s, e) in [(0, L), (0, 1), (100, 2600), (2500, 4999), (1234, 1300)]:
+        want, dropped = htslib_plp.region_depth(tid, pos, span, 0, s, e, max_depth=cap)
+        idx = depthcap.region_reads(tid, pos, span, 0, s, e)
+        keep, d2 = depthcap.cap_mask(tid[idx], pos[idx], span[idx], cap)
+        assert d2 == dropped, (s, e)
+        got = kept_depth(pos[idx], span[idx], keep, s, e)
+        assert np.array_equal(got, want), (s, e)
+
+
+def test_cap_8000_amplicon_piles():
+    """Amplicon-like piles deeper than pysam's default cap: 3 starts with
+    9000-12000 reads each over background coverage (> 8000x columns)."""
+    rng = np.random.default_rng(11)
+    L = 3000
+    pos = np.concatenate([np.full(12_000, 500), np.full(9_000, 520), np.full(10_500, 1400),
+                          rng.integers(0, 2800, size=4000)])
+    span = np.concatenate([np.full(12_000, 150), rng.integers(100, 200, size=9_000),
+                           np.full(10_500, 120), rng.integers(1, 200, size=4000)])
+    o = np.argsort(pos, kind="stable")
+    pos, span = pos[o].astype(np.int32), span[o].astype(np.int32)
+    tid = np.zeros(len(pos), np.int32)
+    want, dropped = htslib_plp.region_depth(tid, pos, span, 0, 0, L, max_depth=8000)
+    keep, d2 = depthcap.cap_mask(tid, pos, span, 8000)
+    assert dropped > 0 and d2 == dropped
+    assert np.array_equal(kept_depth(pos, span, keep, 0, L), want)
+    full = kept_depth(pos, span, np.ones(len(pos), bool), 0, L)
+    assert full.max() > 8000 and want.max() < full.max()
+
+
+def test_cap_mask_contigs_independent_and_errors():
+    rng = np.random.default_rng(5)
+    tid = np.repeat(np.arange(4, dtype=np.int32), 300)
+    pos = np.concatenate([np.sort(rng.integers(0, 40, size=300)) for _ in range(4)]).astype(np.int32)
+    span = rng.integers(1, 50, size=len(pos)).astype(np.int32)
+    keep, _ = depthcap.cap_mask(tid, pos, span, 7, n_threads=3)
+    for t in range(4):
+        m = tid == t
+        k1, _ = depthcap.cap_mask(tid[m], pos[m], span[m], 7, n_threads=1)
+        assert np.array_equal(keep[m], k1)
+    from metacov_amd._lib import MetacovError
+    with pytest.raises(MetacovError):
+        depthcap.cap_mask(np.zeros(2, np.int32), np.array([5, 3], np.int32), np.ones(2, np.int32), 7)
+    with pytest.raises(MetacovError):
+        depthcap.cap_mask(tid, pos, span, 0)

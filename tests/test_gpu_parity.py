@@ -958,3 +958,233 @@ def test_bench_json_contract(tmp_path):
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c, k
     assert c["value"] > 0 and c["kind"] in ("port", "reference")
+
+
+def test_bench_gpus_two_launches_ranks(tmp_path):
+    """`bench.py --gpus 2` (no torchrun around it) starts two ranks through a
+    child torch.distributed.run and prints rank 0's line: n_gpus == 2, the
+    contig-sharded (strong) layout, the all-gather timed apart.  gloo lets
+    both ranks share the box's one GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                          "--config", "c3", "--reads", "2000000", "--contigs", "64", "--steps", "2",
+                          "--warmup", "1", "--prepare-steps", "1"],
+                         capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["ranks_seen"] == 2
+    assert d["scaling"] == "strong" and d["backend"] == "gloo"
+    assert d["allgather_ms"] is not None and d["allgather_ms"] > 0
+    assert d["config"]["regions"] == 64
+    assert d["value"] > 0
+
+
+# ------------------------------------------------------------- direct prepare
+
+def _paths(eng):
+    t = eng.timings()
+    return t["direct_batches"], t["full_prepares"]
+
+
+def _fresh(lib_built):
+    return CoverageEngine(0)
+
+
+def test_direct_path_taken_and_equal_to_full(lib_built):
+    """Sorted in-bounds short reads go the direct way (probe + validating
+    K2), and give the same depth, rows and aligned bases as the full
+    prepare, for the plain and the fused K2."""
+    lengths, weights = synth.c3_workload(2_000_000, 300)
+    tid, pos, span = synth.interval_workload(lengths, 2_000_000, seed=31, weights=weights)
+    rt = np.arange(len(lengths), dtype=np.int32)
+    rs = np.zeros(len(lengths), np.int64)
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    want = coracle.region_stats(d, ext, coff, rt, rs, lengths)
+    e = _fresh(lib_built)
+    try:
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span)
+        e.compute_depth()
+        assert _paths(e) == (1, 0)
+        assert e.aligned_bases() == int(span.astype(np.int64).sum())
+        got = np.concatenate([e.depth(t, 0, int(ext[t])) for t in range(len(lengths))])
+        assert np.array_equal(got, np.concatenate([d[coff[t]:coff[t] + ext[t]] for t in range(len(lengths))]))
+        for direct in (True, False):
+            e.set_direct_prepare(direct)
+            e.invalidate()
+            rows = e.compute_depth_stats(rt, rs, lengths)
+            for f in want.dtype.names:
+                assert np.array_equal(rows[f], want[f]), (direct, f)
+            assert e.fused_fallbacks() == 0
+        assert _paths(e) == (2, 1)
+    finally:
+        e.close()
+
+
+def _direct_case(lib_built, lengths, tid, pos, span, expect_direct, regions=True):
+    e = _fresh(lib_built)
+    try:
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span)
+        e.compute_depth()
+        assert (_paths(e)[0] == 1) == expect_direct, _paths(e)
+        check_depth_vs_oracle(e, lengths, tid, pos, span)
+        if regions:
+            d, ext, coff = coracle.depth(lengths, tid, pos, span)
+            rt = np.arange(len(lengths), dtype=np.int32)
+            e.invalidate()
+            got = e.compute_depth_stats(rt, np.zeros(len(lengths), np.int64), np.asarray(lengths, np.int64))
+            want = coracle.region_stats(d, ext, coff, rt, np.zeros(len(lengths), np.int64),
+                                        np.asarray(lengths, np.int64))
+            for f in want.dtype.names:
+                assert np.array_equal(got[f], want[f]), f
+        return _paths(e)
+    finally:
+        e.close()
+
+
+def test_direct_hands_over_unsampled_long_read(lib_built):
+    """A read longer than 4096 at an index the probe does not sample: K2's
+    check sends the batch to the full prepare (long-read path), exactly."""
+    lengths, tid, pos, span = make_case([400_000, 100_000], 20_000, (1, 150), 41, overhang=False)
+    i = 1001                      # not a multiple of 256
+    assert i % 256
+    span = span.copy()
+    span[i] = min(9000, int(lengths[tid[i]] - pos[i]))
+    assert span[i] > 4096
+    paths = _direct_case(lib_built, lengths, tid, pos, span, expect_direct=False)
+    assert paths[1] >= 1
+
+
+def test_direct_hands_over_unsampled_overhang(lib_built):
+    lengths, tid, pos, span = make_case([300_000, 50_000], 20_000, (1, 150), 42, overhang=False)
+    last = np.nonzero(tid == 0)[0][-1]
+    assert last % 256
+    pos = pos.copy()
+    pos[last] = lengths[0] - 10
+    span = span.copy()
+    span[last] = 40               # runs 30 past contig 0's end
+    o = np.lexsort((pos, tid))
+    tid, pos, span = tid[o], pos[o], span[o]
+    _direct_case(lib_built, lengths, tid, pos, span, expect_direct=False)
+
+
+def test_direct_rejects_unsampled_disorder_and_invalid(lib_built):
+    """Unsorted or invalid reads between the samples: the same errors as the
+    full prepare (K2's check, then mc_prepare's exact message)."""
+    lengths, tid, pos, span = make_case([200_000], 5_000, (1, 150), 43, overhang=False)
+    bad_order = pos.copy()
+    bad_order[[700, 701]] = bad_order[[701, 700]]
+    assert bad_order[700] != bad_order[701]
+    e = _fresh(lib_built)
+    try:
+        e.set_contigs(lengths)
+        e.add_reads(tid, bad_order, span)
+        with pytest.raises(MetacovError) as ei:
+            e.compute_depth()
+        assert ei.value.code == MC_E_INVALID and "sorted" in str(ei.value)
+        e.set_contigs(lengths)
+        bad_tid = tid.copy()
+        bad_tid[3001] = 5
+        e.add_reads(bad_tid, pos, span)
+        with pytest.raises(MetacovError) as ei:
+            e.compute_depth_stats([0], [0], [200_000])
+        assert ei.value.code == MC_E_INVALID
+        # a good batch afterwards on the same ctx goes direct again
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span)
+        e.compute_depth()
+        assert _paths(e)[0] == 1
+        check_depth_vs_oracle(e, lengths, tid, pos, span)
+    finally:
+        e.close()
+
+
+def test_direct_sparse_and_empty_contigs(lib_built):
+    """Sample blocks spanning empty contigs, huge gaps and contig boundaries
+    (chunk ranges from the J counts only), and fewer reads than one sample
+    block."""
+    rng = np.random.default_rng(44)
+    lengths = np.array([5, 0, 1_000_000, 3, 2_000_000, 64, 65, 4096 * 9 + 1, 0, 7_000_000], np.int64)
+    for n in (1, 3, 255, 257, 2000):
+        live = np.array([0, 2, 4, 6, 7, 9])
+        t = rng.choice(live, size=n).astype(np.int32)
+        sp = rng.integers(1, 150, size=n).astype(np.int32)
+        sp = np.minimum(sp, lengths[t]).astype(np.int32)
+        p = (rng.random(n) * (lengths[t] - sp + 1)).astype(np.int32)
+        o = np.lexsort((p, t))
+        _direct_case(lib_built, lengths, t[o], p[o], sp[o], expect_direct=True)
+
+
+def test_direct_ctx_sticks_to_full_after_long_reads(lib_built):
+    lengths, tid, pos, span = make_case([300_000], 8_000, (1, 150), 45, overhang=False)
+    span_long = span.copy()
+    span_long[500] = min(6000, int(lengths[0] - pos[500]))
+    e = _fresh(lib_built)
+    try:
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span_long)
+        e.compute_depth()
+        assert _paths(e) == (0, 1)
+        e.clear_reads()
+        e.add_reads(tid, pos, span)
+        e.compute_depth()            # same contig set: straight to the full prepare
+        assert _paths(e) == (0, 2)
+        check_depth_vs_oracle(e, lengths, tid, pos, span)
+        e.set_contigs(lengths)       # a new contig set tries the direct path again
+        e.add_reads(tid, pos, span)
+        e.compute_depth()
+        assert _paths(e) == (1, 2)
+    finally:
+        e.close()
+
+
+# ------------------------------------------------------------- htslib cap (opt-in)
+
+def test_max_depth_cap_gpu_rows(lib_built):
+    """classic(..., max_depth=8000) on a >8000x synthetic contig (amplicon
+    piles): the per-region capped rows equal classic() over the literal
+    htslib restatement's columns (oracle/htslib_plp.py).  Parity with htslib
+    itself unpinned."""
+    import types
+    from metacov_amd import depthcap
+    from oracle import htslib_plp
+    from oracle.classic_np import classic_from_vector
+    rng = np.random.default_rng(12)
+    L = 4000
+    pos = np.concatenate([np.full(12_000, 700), np.full(9_500, 710), np.full(11_000, 2100),
+                          rng.integers(0, 3800, size=6000)])
+    span = np.concatenate([np.full(12_000, 150), rng.integers(100, 200, size=9_500),
+                           np.full(11_000, 300), rng.integers(1, 200, size=6000)])
+    o = np.argsort(pos, kind="stable")
+    bf = types.SimpleNamespace(tid=np.zeros(len(pos), np.int32), pos=pos[o].astype(np.int32),
+                               span=span[o].astype(np.int32), lengths=(L,))
+    regions = [(0, L), (650, 900), (705, 2500), (2200, 2300), (0, 1)]
+    rows, dropped = depthcap.capped_rows(bf, np.zeros(len(regions), np.int32),
+                                         np.array([r[0] for r in regions], np.int64),
+                                         np.array([r[1] for r in regions], np.int64), 8000)
+    assert dropped > 0
+    for row, (s, e) in zip(rows, regions):
+        want, _ = htslib_plp.region_depth(bf.tid, bf.pos, bf.span, 0, s, e, max_depth=8000)
+        assert classic_stats(row) == classic_from_vector(want.astype(np.float64)), (s, e)
+
+
+def test_cli_max_depth_option(lib_built, fixture_golden, golden_dir, tmp_path):
+    """--max-depth on the reference's fixture (depth < 8000: nothing dropped,
+    the same CSV bytes as the exact path)."""
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    out = tmp_path / "o.csv"
+    r = CliRunner().invoke(cli_pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
+                                        "-rb", os.path.join(golden_dir, "regions.blast7"),
+                                        "-o", str(out), "--max-depth", "8000"])
+    assert r.exit_code == 0, r.output
+    with open(out, newline="") as fh:
+        assert fh.read() == fixture_golden["csv_blast7"]
