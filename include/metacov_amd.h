@@ -86,6 +86,9 @@ typedef struct mc_ctx mc_ctx;
 
 const char* mc_last_error(void);
 const char* mc_version(void);
+/* "mc-source-sha256:<hex>": the sources and flags this library was built from
+ * (metacov_amd/build.py rebuilds when the tree's hash differs). */
+const char* mc_build_id(void);
 
 /* ---- context ------------------------------------------------------------ */
 int mc_ctx_create(int device, mc_ctx** out);

@@ -70,6 +70,7 @@ _PP = ctypes.POINTER(ctypes.c_void_p)
 SIGNATURES = {
     "mc_last_error": [],
     "mc_version": [],
+    "mc_build_id": [],
     "mc_ctx_create": [ctypes.c_int, _PP],
     "mc_ctx_destroy": [_P],
     "mc_ctx_set_stream": [_P, _P],
@@ -151,7 +152,8 @@ SIGNATURES = {
     "mc_scan_results": [_P, _P, _P, _P, _P, _P],
     "mc_scan_timing": [_P, ctypes.POINTER(ctypes.c_float), _PI64],
 }
-_RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p}
+_RESTYPE = {"mc_last_error": ctypes.c_char_p, "mc_version": ctypes.c_char_p,
+            "mc_build_id": ctypes.c_char_p}
 
 _lib = None
 _variants = {}

@@ -18,4 +18,10 @@ const char* last_error() { return g_err.c_str(); }
 }  // namespace mc
 
 extern "C" const char* mc_last_error(void) { return mc::last_error(); }
-extern "C" const char* mc_version(void) { return "metacov_amd 0.1.0 (gfx950)"; }
+extern "C" const char* mc_version(void) { return "metacov_amd 0.3.0 (gfx950)"; }
+
+#ifndef MC_SOURCE_HASH
+#define MC_SOURCE_HASH "unstamped"
+#endif
+// metacov_amd/build.py stamps the SHA-256 of the sources it built from
+extern "C" const char* mc_build_id(void) { return "mc-source-sha256:" MC_SOURCE_HASH; }

@@ -296,6 +296,38 @@ double pairwise_dense(const double* a, int64_t n) {
 }
 
 // np.add.reduce over a dense float64 array: 8192-element chunks, pairwise within
+// np.add.reduce of the per-position sums of covers [a, b) += inv (added per
+// position in cover order) over [0, L), chunk by chunk: the covers touching
+// each 8192-position chunk are listed in cover order (CSR), their sums built
+// in one chunk buffer, which is summed as numpy_sum_dense sums that chunk.
+template <class Cover>
+double numpy_sum_covers(const Cover* cv, size_t m, int64_t L) {
+    constexpr int64_t kChunk = 8192;
+    const int64_t nb = (L + kChunk - 1) / kChunk;
+    std::vector<int64_t> first((size_t)nb + 1, 0);
+    for (size_t j = 0; j < m; ++j)
+        for (int64_t k = cv[j].a / kChunk; k <= (cv[j].b - 1) / kChunk; ++k) ++first[(size_t)k + 1];
+    for (int64_t k = 0; k < nb; ++k) first[(size_t)k + 1] += first[(size_t)k];
+    std::vector<uint32_t> list((size_t)first[(size_t)nb]);
+    std::vector<int64_t> fill(first.begin(), first.end() - 1);
+    for (size_t j = 0; j < m; ++j)
+        for (int64_t k = cv[j].a / kChunk; k <= (cv[j].b - 1) / kChunk; ++k) list[(size_t)fill[(size_t)k]++] = (uint32_t)j;
+    std::vector<double> buf((size_t)kChunk);
+    double total = 0;
+    for (int64_t k = 0; k < nb; ++k) {
+        const int64_t c0 = k * kChunk, n = std::min(kChunk, L - c0);
+        std::fill(buf.begin(), buf.begin() + n, 0.0);
+        for (int64_t q = first[(size_t)k]; q < first[(size_t)k + 1]; ++q) {
+            const Cover& c = cv[list[(size_t)q]];
+            const int64_t a = std::max(c.a, c0), b = std::min(c.b, c0 + n);
+            for (int64_t p = a; p < b; ++p) buf[(size_t)(p - c0)] += c.inv;
+        }
+        const double s = pairwise_dense(buf.data(), n);
+        total = k == 0 ? s : total + s;
+    }
+    return total;
+}
+
 double numpy_sum_dense(const std::vector<double>& v) {
     constexpr int64_t kChunk = 8192;
     const int64_t L = (int64_t)v.size();
@@ -336,14 +368,17 @@ void one_region(const mc_reads& r, const Tables& tab, int32_t tid, int64_t start
     int64_t secondary = 0, improper = 0, nreads = 0, cov_sum = 0, cov2_sum = 0;
     double wnf = 0;
     // cov_cor (pileup.py:141): per position, the reads' 1/rcor added in read
-    // order, then np.mean's pairwise sum; materialised only once a read
-    // with rcor != 1 covers the region (with every 1/rcor == 1 the float sums
-    // are exact integers and equal cov's)
-    std::vector<double> cov_cor;
+    // order, then np.mean's sum: numpy's add.reduce over 8192-element chunks,
+    // pairwise within each.  The reads' covers are kept in read order and the
+    // per-position sums are built one 8192-position chunk at a time at the
+    // end (memory O(reads + one chunk), not O(region length)); with every
+    // 1/rcor == 1 the float sums are exact integers and equal cov's.
     struct Cover {
         int64_t a, b;
+        double inv;
     };
-    std::vector<Cover> unit;   // reads with 1/rcor == 1 seen before cov_cor existed
+    std::vector<Cover> covers;
+    bool any_inv = false;
     int64_t status = kOk;
     struct Start {
         int64_t at;
@@ -411,18 +446,8 @@ void one_region(const mc_reads& r, const Tables& tab, int32_t tid, int64_t start
         const int64_t a0 = std::max<int64_t>(0, rs), b0 = std::min(L, re);
         if (b0 > a0) {
             cov_sum += b0 - a0;
-            if (cov_cor.empty() && inv != 1.0) {   // replay the unit reads so far, in order
-                cov_cor.assign((size_t)L, 0.0);
-                for (const Cover& c : unit)
-                    for (int64_t p = c.a; p < c.b; ++p) cov_cor[p] += 1.0;
-                unit.clear();
-                unit.shrink_to_fit();
-            }
-            if (!cov_cor.empty()) {
-                for (int64_t p = a0; p < b0; ++p) cov_cor[p] += inv;
-            } else {
-                unit.push_back({a0, b0});
-            }
+            covers.push_back({a0, b0, inv});
+            any_inv |= inv != 1.0;
         }
         if (rs >= 0 && rs < L) {
             starts.push_back({rs, i, inv});
@@ -452,7 +477,7 @@ void one_region(const mc_reads& r, const Tables& tab, int32_t tid, int64_t start
     out.counts[5] = (int64_t)off.size();
     out.counts[6] = cov2_sum;
     out.counts[7] = (int64_t)events.size();
-    out.sums[0] = cov_cor.empty() ? (double)cov_sum : numpy_sum_dense(cov_cor);
+    out.sums[0] = any_inv ? numpy_sum_covers(covers.data(), covers.size(), L) : (double)cov_sum;
     out.sums[1] = seq_sum;
     out.sums[2] = numpy_sum_sparse(off, val, L);
     out.sums[3] = wnf;
@@ -509,18 +534,26 @@ extern "C" int mc_experimental_reads(mc_reads* r, int k_len, const double* val1,
     r->events.assign((size_t)R, {});
     const int nt = std::max(1, std::min<int>(n_threads_or_all(n_threads), (int)std::max<int64_t>(R, 1)));
     std::atomic<int64_t> next{0};
+    std::atomic<int64_t> failed{-1};      // a region whose pass threw (e.g. std::bad_alloc)
     auto worker = [&]() {
         for (;;) {
             const int64_t q = next.fetch_add(1);
             if (q >= R) break;
-            one_region(*r, tab, tid[q], start[q], end[q], {counts + 8 * q, sums + 4 * q},
-                       r->events[q]);
+            try {
+                one_region(*r, tab, tid[q], start[q], end[q], {counts + 8 * q, sums + 4 * q},
+                           r->events[q]);
+            } catch (const std::exception&) {
+                int64_t none = -1;
+                failed.compare_exchange_strong(none, q);
+            }
         }
     };
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; ++t) pool.emplace_back(worker);
     worker();
     for (auto& th : pool) th.join();
+    MC_REQUIRE(failed.load() < 0, MC_E_RANGE, "region %lld: the reads pass ran out of host memory",
+               (long long)failed.load());
     return MC_OK;
 }
 

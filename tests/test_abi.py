@@ -62,3 +62,13 @@ def test_missing_library_is_loud(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.LibraryNotBuilt):
         _lib.load()
+
+
+def test_library_built_from_this_tree(lib_built):
+    """The library's stamped source hash is the tree's (a stale .so would be
+    rebuilt by build.build, never silently reused)."""
+    from metacov_amd import build
+    lib = ctypes.CDLL(lib_built)
+    lib.mc_build_id.restype = ctypes.c_char_p
+    assert lib.mc_build_id().decode() == "mc-source-sha256:" + build.source_hash()
+    assert build.built_hash() == build.source_hash()
