@@ -187,8 +187,9 @@ def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=None):
 
 def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None, max_depth=None):
     """One rank of a multi-GPU `pileup` (launched by torch.distributed.run).
-    With -k, rank 0 adds the experimental columns for all regions after the
-    gather (their read side is host work over the whole file)."""
+    With -k, each rank also computes the experimental columns of the regions
+    on its contigs (cli.py:93-95 per region), and rank 0 gathers them with
+    the table."""
     import torch
     import torch.distributed as dist
     from . import dist as mdist
@@ -206,14 +207,24 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         try:
             table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
                                        max_depth)
-        except Exception as e:   # every rank learns of it before the table gather
+            head, regions, tids, starts, ends, rows, mine, r_max = table_args
+            mine_extra = experimental_results(path, exp, head.references, tids[mine], starts[mine],
+                                              ends[mine], device)
+        except BaseException as e:   # every rank learns of it before the table gather
             err = e
         mdist.agree_on_error(err, device=coll_dev)
-        head, regions, tids, starts, ends, rows, mine, r_max = table_args
         table = mdist.all_gather_table(mdist.pack_rows(rows, mine), r_max, device=coll_dev)
+        extra = None
+        if exp is not None:          # each rank's experimental results (our own objects) to rank 0
+            parts = [None] * world if rank == 0 else None
+            dist.gather_object((mine.tolist(), mine_extra), parts, dst=0)
+            if rank == 0:
+                extra = [None] * len(regions)
+                for idx, res in parts:
+                    for i, r in zip(idx, res):
+                        extra[i] = r
         if rank == 0:
             log_counts(head)
-            extra = experimental_results(path, exp, head.references, tids, starts, ends, device)
             write_csv(regions, mdist.unpack_rows(table, len(regions), REGION_STAT_DTYPE), outfile,
                       extra)
     finally:

@@ -422,6 +422,7 @@ static int add_reads_impl(mc_ctx* ctx, int64_t n, const int32_t* tid, const int3
         if (wait) HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     ctx->n_reads += n;
+    ctx->t_cigar = false;
     invalidate(ctx);
     return MC_OK;
 }
@@ -484,6 +485,7 @@ extern "C" int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid, co
     ctx->spans_pending = n > 0;
     ctx->cig_off_ext = nullptr;
     ctx->cigar_ext = nullptr;
+    ctx->t_cigar = false;
     invalidate(ctx);
     return MC_OK;
 }
@@ -509,6 +511,7 @@ extern "C" int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* 
     ctx->cigar_ext = cigar;
     ctx->n_reads = n;
     ctx->spans_pending = n > 0;
+    ctx->t_cigar = false;
     invalidate(ctx);
     return MC_OK;
 }
@@ -521,6 +524,7 @@ extern "C" int mc_invalidate(mc_ctx* ctx) {
 
 extern "C" int mc_clear_reads(mc_ctx* ctx) {
     if (int rc = ctx_use(ctx)) return rc;
+    ctx->t_cigar = false;
     ctx->n_reads = 0;
     ctx->spans_pending = false;
     ctx->cig_off_ext = nullptr;
@@ -603,7 +607,8 @@ static int upload_coff(mc_ctx* ctx, int64_t* coff_up) {
 
 // K1 on a raw-CIGAR batch whose spans are still pending (CIGAR words -> span)
 static int run_k1(mc_ctx* ctx) {
-    ctx->t_cigar = false;
+    // (t_cigar stays set for the batch K1 ran on: a direct batch handed over
+    // to mc_prepare keeps its K1 time)
     if (!ctx->spans_pending) return MC_OK;
     hipStream_t s = ctx->stream;
     const int64_t n = ctx->n_reads;

@@ -337,3 +337,45 @@ def test_cli_kmer_histogram_gpu(golden_dir, fixture_golden, lib_built, tmp_path)
                 assert abs(float(g[key]) - float(v)) <= 1.0001e-3 * max(1.0, abs(float(v))), key
             else:
                 assert g[key] == str(v), (key, g[key], v)
+
+
+@pytest.mark.gpu
+def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path):
+    """`metacov pileup -k` under torch.distributed.run with 2 ranks: each rank
+    computes the experimental columns of the regions on its own contigs and
+    rank 0 gathers them with the region table; the CSV equals one process's
+    byte for byte (gloo: both ranks share the box's one GPU)."""
+    import socket
+    import subprocess
+    import sys
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    rng = np.random.default_rng(12)
+    keys = ["".join(p) for p in __import__("itertools").product("ACGT", repeat=7)]
+    rows = ["kmer,n0,n1,n2,R,Mapped"]
+    for r in ("R1", "R2"):
+        for x in keys:
+            if rng.random() < 0.7:
+                rows.append("%s,%d,%d,%d,%s,Mapped" % (x, rng.integers(1, 50), rng.integers(1, 50),
+                                                       rng.integers(1, 50), r))
+    hist = tmp_path / "k.csv"
+    hist.write_text("\n".join(rows) + "\n")
+    fasta = os.path.join(golden_dir, "reference_1K.fa.gz")
+    bam = os.path.join(golden_dir, "bbmap.sorted.bam")
+    args = ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"), "-k", str(hist), "-f", fasta]
+    one = tmp_path / "one.csv"
+    res = CliRunner().invoke(cli_pileup, args + ["-o", str(one)])
+    assert res.exit_code == 0, res.output
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    two = tmp_path / "two.csv"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MC_DIST_BACKEND="gloo",
+               PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, "-m", "metacov_amd.cli", "pileup",
+           *args, "-o", str(two)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert open(two, newline="").read() == open(one, newline="").read()
