@@ -905,10 +905,9 @@ static K2Geom k2_geom(const mc_ctx* ctx, bool stats) {
 static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
-#ifndef MC_EXTRA_LDS
-#define MC_EXTRA_LDS 0   // experiment knob: bytes of unused LDS per workgroup (occupancy sweeps)
-#endif
-    const size_t lds = (size_t)(kLdsHeader + ctx->ring + (stats ? kHistLds + kOvInts : 0)) * 4 + MC_EXTRA_LDS;
+    const size_t lds = (size_t)(kLdsHeader + ctx->ring +
+                                (stats ? (ctx->has_long ? HistCfg<true>::kLds : HistCfg<false>::kLds) + kOvInts
+                                       : 0)) * 4;
     const bool lng = ctx->has_long;
     const bool dir = ctx->direct;
     const void* kfn = stats ? (lng ? (const void*)depth_kernel<true, true, false>
@@ -1226,7 +1225,7 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     const K2Geom geo = k2_geom(ctx, true);
     HIP_TRY(ctx->d_fchunk.reserve(geo.n_chunks));
     HIP_TRY(ctx->d_flow.reserve(R));
-    const int vals = kHistBins;   // values per region row
+    const int vals = fused_hist_vals(ctx->has_long);   // values per region row
     HIP_TRY(ctx->d_fhist.reserve((size_t)(R * vals)));
     HIP_TRY(ctx->h_fflag.reserve(fflag_ints(R)));
     const bool verdict = ctx->direct && !ctx->direct_checked;   // K3b hands K2's counters back
@@ -1265,13 +1264,17 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     // K3b: its span is timed from K2's end event (one event fewer per call)
     ctx->stats_after_depth = true;
     // one wave per region; flags [0, R) and K2's max depth [R] land in mapped host memory
-    hipLaunchKernelGGL(region_final_wave_kernel<kHistBins>, dim3((unsigned)((R + kWaves - 1) / kWaves)),
-                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,
-                       reinterpret_cast<const int64_t*>(d + o_ntot),
-                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,
-                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,
-                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p,
-                       verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr);
+#define MC_LAUNCH_K3B(V)                                                                           \
+    hipLaunchKernelGGL(region_final_wave_kernel<V>, dim3((unsigned)((R + kWaves - 1) / kWaves)),        \
+                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,                          \
+                       reinterpret_cast<const int64_t*>(d + o_ntot),                                \
+                       reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,           \
+                       reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,                 \
+                       ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p,                       \
+                       verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr)
+    if (vals == HistCfg<false>::kBins) MC_LAUNCH_K3B(HistCfg<false>::kBins);
+    else MC_LAUNCH_K3B(HistCfg<true>::kBins);
+#undef MC_LAUNCH_K3B
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
@@ -1321,8 +1324,8 @@ static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     const bool direct = ctx->direct;
     // histogram window of each region: kHistBins values, kWinBelow of them
     // below its contig's estimated body depth
-    const int vals = kHistBins;
-    const int64_t win_below = kWinBelow;
+    const int vals = fused_hist_vals(ctx->has_long);
+    const int64_t win_below = (int64_t)kWinBelow * vals / kHistBins;
     const double span_mean = ctx->n_reads ? (double)ctx->aligned_bases / (double)ctx->n_reads : 0.0;
     // the contig's body depth: its aligned bases over its length less one
     // mean read span (the two end ramps hold about half a span of depth

@@ -537,6 +537,9 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 // read past its contig's end, a long read) is reported in DirectRes; the host
 // then re-runs the batch through the full prepare, which raises the exact
 // errors or builds the extents and long-read buckets.
+#ifndef MC_DIRECT_VALIDATE_END
+#define MC_DIRECT_VALIDATE_END 0       // K2 checks a chunk's own reads at the chunk end, not per batch
+#endif
 constexpr int kProbeShift = 8;                 // sample stride S = 256 reads
 constexpr int kProbeStride = 1 << kProbeShift;
 
@@ -591,35 +594,27 @@ __device__ __forceinline__ void probe_fill(int32_t* J, int64_t n_base, int lw, i
     for (int64_t k = k0; k <= k1; ++k) J[k] = val;
 }
 
+// probe_kernel samples every read's (tid, pos) at stride S, its span at
+// stride 4 S (only the long-read flag reads it: a long read the sparser
+// sample misses is still caught by K2's check)
+constexpr int kProbeSpanEvery = 4;
+
 __global__ void __launch_bounds__(kBlock)
 probe_kernel(ProbeArgs A) {
     const int64_t M = (A.n + kProbeStride - 1) >> kProbeShift;
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && threadIdx.x >= kDresFlags && threadIdx.x < kDresWords)
         A.dres[threadIdx.x] = 0;   // K2's counters (K2 runs after this launch)
-    int t = 0, p = 0, s = 0;
-    int64_t key = 0;
-    if (j < M) {
-        const int64_t i = j << kProbeShift;
-        t = A.tid[i];
-        p = A.pos[i];
-        s = A.span[i];
-        key = probe_key(A, t, p);
-    }
-    // the next sample: from the neighbouring lane, lane 63 loads its own
-    int64_t key_next = (int64_t)(((uint64_t)(uint32_t)__shfl_down((int)(key >> 32), 1, 64) << 32) |
-                                 (uint32_t)__shfl_down((int)(key & 0xffffffff), 1, 64));
-    int t_next = __shfl_down(t, 1, 64);
-    int p_next = __shfl_down(p, 1, 64);
     if (j >= M) return;
     const bool last = j == M - 1;
-    if (lane == 63 && !last) {
-        const int64_t i = (j + 1) << kProbeShift;
-        t_next = A.tid[i];
-        p_next = A.pos[i];
-        key_next = probe_key(A, t_next, p_next);
-    }
+    // this sample and the next one, all loads issued together (the next
+    // sample's from the neighbouring lane would leave lane 63 a second round trip)
+    const int64_t i = j << kProbeShift, i1 = last ? i : i + kProbeStride;
+    const int t = A.tid[i], p = A.pos[i];
+    const int t_next = A.tid[i1], p_next = A.pos[i1];
+    const int s = (j % kProbeSpanEvery) == 0 ? A.span[i] : 0;
+    const int64_t key = probe_key(A, t, p);
+    const int64_t key_next = probe_key(A, t_next, p_next);
     const bool bad = ((unsigned)t >= (unsigned)A.nc) | (p < 0) | (s < 0);
     const bool uns = !last && ((t > t_next) | ((t == t_next) & (p > p_next)) | (key > key_next));
     if (bad | uns) atomicMax(&A.dres[kDresBadSample], A.gen);
@@ -650,13 +645,15 @@ window_kernel(const int32_t* __restrict__ fsamp, const int32_t* __restrict__ spa
     const int t = rtid[r];
     const int64_t a = fsamp[t], b = fsamp[t + 1];
     const int64_t ns = b - a;
-    // up to 1024 of the contig's samples, evenly strided
-    const int64_t take = ns < 1024 ? ns : 1024;
+    // up to 256 of the contig's samples, evenly strided: four independent
+    // loads per lane (the mean span to ~2 % at C3, ~3 % at C5's lognormal spans)
+    const int64_t take = ns < 256 ? ns : 256;
     long long sum = 0;
-    for (int64_t k = lane; k < take; k += 64) {
-        const int64_t smp = a + k * ns / take;
-        const int64_t i = smp << kProbeShift;
-        if (i < n) sum += span[i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t k = lane + 64 * u;
+        const int64_t i = k < take ? (a + k * ns / take) << kProbeShift : n;
+        sum += i < n ? span[i] : 0;
     }
     sum = wave_sum64(sum);
     if (lane != 0) return;
@@ -1127,6 +1124,7 @@ template <> struct RawBatch<false> {
 };
 template <> struct RawBatch<true> {
     i32x4 t, p, s;
+    int pt, pp;                        // lane 0: the read before the lane's first (order check)
 };
 
 // The read arrays K2 loads: the packed words, or tid / pos / span
@@ -1154,6 +1152,15 @@ __device__ __forceinline__ void issue_raw(RawBatch<kDirect>& r, int64_t base, co
             r.s = *reinterpret_cast<const i32x4*>(A.span + i0);
         } else {
             r.t = r.p = r.s = i32x4{0, 0, 0, 0};
+        }
+        // lane 0's predecessor (the previous wave's last read) comes with the
+        // batch: a scalar load of it at the batch advance stalled every batch
+        // on an L2 round trip (0.12 ms of a C3 launch)
+        r.pt = -1;
+        r.pp = 0;
+        if ((threadIdx.x & 63) == 0 && i0 > 0 && i0 < cend) {
+            r.pt = A.tid[i0 - 1];
+            r.pp = A.pos[i0 - 1];
         }
     } else {
         r.g = i0 < cend ? *reinterpret_cast<const i32x4*>(A.gpos + i0) : i32x4{0, 0, 0, 0};
@@ -1239,7 +1246,11 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         const unsigned long long act = __ballot(cand >= 0);
         if (!act) break;
         const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
+#if defined(MC_EXP_NO_LEN) || MC_DIRECT_VALIDATE_END
+        const int64_t c = uload(coff, t0) - C0, ln = 0;
+#else
         const int64_t c = uload(coff, t0) - C0, ln = uload(D.len, t0);
+#endif
         const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -1250,12 +1261,11 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
                 todo &= ~(1u << k);
             }
     }
-    // predecessor of read 0: lane - 1's read 3; lane 0 of each wave by scalar loads
-    const int64_t wfirst = base + (int64_t)(threadIdx.x & ~63) * kReadsPerThread;
+    // predecessor of read 0: lane - 1's read 3; lane 0's came with the batch
     int pt = __shfl_up(tt[3], 1, 64), ppv = __shfl_up(pp[3], 1, 64);
     if (lane == 0) {
-        pt = wfirst > 0 ? uload(A.tid, wfirst - 1) : -1;
-        ppv = wfirst > 0 ? uload(A.pos, wfirst - 1) : 0;
+        pt = r.pt;
+        ppv = r.pp;
     }
     unsigned pend = 0;
 #pragma unroll
@@ -1265,10 +1275,23 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         b.sp[k] = sp[k];
         const bool ok = (valid >> k) & 1u;
         pend |= (ok & (i >= dc.lo) & (i < dc.hi) & (rs[k] < chunk_w) & (sp[k] <= short_max)) ? 1u << k : 0u;
+#if defined(MC_DIRECT_NOCHECK) || MC_DIRECT_VALIDATE_END   // (no validation here)
+        const bool own = false;
+#else
         const bool own = (i >= dc.vlo) & (i < dc.vhi);
+#endif
         const int qt = k ? tt[k - 1] : pt, qp = k ? pp[k - 1] : ppv;
+#ifdef MC_EXP_NO_ORDER
+        const bool uns = false;
+        (void)qt; (void)qp;
+#else
         const bool uns = (i > 0) & ((qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k])));
+#endif
+#ifdef MC_EXP_NO_LEN
+        const bool unfit = (sp[k] > short_max);
+#else
         const bool unfit = (sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k]);
+#endif
         acc.flags |= own ? (!ok | uns ? kDirectInvalid : unfit ? kDirectUnfit : 0u) : 0u;
         acc.bases += (own & ok) ? (unsigned)sp[k] : 0u;
     }
@@ -1300,6 +1323,65 @@ __device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArg
     }
 }
 
+// The checks of finish_batch_direct over a chunk's own reads [vlo, vhi), as
+// a loop of its own at the chunk end (the tile registers are dead there).
+__device__ __forceinline__ void validate_own(int64_t vlo, int64_t vhi, const ReadArrays& A,
+                                             const DirectArgs& D, int short_max, DirectAcc& acc) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t b = vlo & ~(int64_t)3; b < vhi; b += kBatch) {
+        const int64_t i0 = b + (int64_t)threadIdx.x * kReadsPerThread;
+        i32x4 t = i32x4{-1, -1, -1, -1}, p = i32x4{0, 0, 0, 0}, sv = i32x4{0, 0, 0, 0};
+        const bool any = i0 < vhi && i0 + 4 >= vlo;   // (the read before vlo: vlo's predecessor)
+        if (any) {
+            t = *reinterpret_cast<const i32x4*>(A.tid + i0);
+            p = *reinterpret_cast<const i32x4*>(A.pos + i0);
+            sv = *reinterpret_cast<const i32x4*>(A.span + i0);
+        }
+        int pt = __shfl_up(t.w, 1, 64), ppv = __shfl_up(p.w, 1, 64);
+        if (lane == 0) {
+            pt = -1;
+            ppv = 0;
+            if (any && i0 > 0) {
+                pt = A.tid[i0 - 1];
+                ppv = A.pos[i0 - 1];
+            }
+        }
+        const int tt[4] = {t.x, t.y, t.z, t.w}, pp[4] = {p.x, p.y, p.z, p.w}, sp[4] = {sv.x, sv.y, sv.z, sv.w};
+        unsigned valid = 0, own = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            valid |= (((unsigned)tt[k] < (unsigned)D.nc) & (pp[k] >= 0) & (sp[k] >= 0)) ? 1u << k : 0u;
+            own |= (i0 + k >= vlo && i0 + k < vhi) ? 1u << k : 0u;
+        }
+        unsigned L[4] = {0, 0, 0, 0};
+        unsigned todo = valid & own;
+        for (;;) {
+            const int cand = (todo & 1u) ? tt[0] : (todo & 2u) ? tt[1] : (todo & 4u) ? tt[2]
+                           : (todo & 8u) ? tt[3] : -1;
+            const unsigned long long act = __ballot(cand >= 0);
+            if (!act) break;
+            const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
+            const int64_t ln = uload(D.len, t0);
+            const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (((todo >> k) & 1u) && tt[k] == t0) {
+                    L[k] = l32;
+                    todo &= ~(1u << k);
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool ok = (valid >> k) & 1u, mine = (own >> k) & 1u;
+            const int qt = k ? tt[k - 1] : pt, qp = k ? pp[k - 1] : ppv;
+            const bool uns = (i0 + k > 0) & ((qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k])));
+            const bool unfit = (sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k]);
+            acc.flags |= mine ? (!ok | uns ? kDirectInvalid : unfit ? kDirectUnfit : 0u) : 0u;
+            acc.bases += (mine & ok) ? (unsigned)sp[k] : 0u;
+        }
+    }
+}
+
 // Fused region statistics of K2 (optional): non-overlapping regions sorted by
 // global start.  Each tile folds the positions it owns into the region(s)
 // covering them: min/max/sum/sum of squares per thread, value histogram of
@@ -1326,16 +1408,32 @@ __device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArg
 #define MC_HIST_BINS (MC_HIST_COPIES == 1 ? 1024 : MC_HIST_COPIES == 2 ? 864 \
                       : MC_HIST_COPIES == 4 ? 480 : MC_HIST_COPIES == 8 ? 224 : 96)
 #endif
-constexpr int kHistBins = MC_HIST_BINS;
-constexpr int kHistCopies = MC_HIST_COPIES;
-static_assert(kHistBins % 32 == 0 && (kHistCopies & (kHistCopies - 1)) == 0 && kHistCopies <= 32,
-              "histogram bins: multiple of 32; copies: power of two");
-// Each copy is followed by a pad of kHistPad ints: it offsets the next copy by
-// 32 / kHistCopies banks, and holds the per-lane dummy slots the branch-free
+// The long-read variant (C5-like deep contigs with long end ramps, whose
+// quartile ranks span more values): its own copies / bins in the same LDS
+#ifndef MC_HIST_COPIES_LONG
+#define MC_HIST_COPIES_LONG MC_HIST_COPIES
+#endif
+#ifndef MC_HIST_BINS_LONG
+#define MC_HIST_BINS_LONG (MC_HIST_COPIES_LONG == 1 ? 1728 : MC_HIST_BINS)
+#endif
+// Each copy is followed by a pad of kPad ints: it offsets the next copy by
+// 32 / kCopies banks, and holds the per-lane dummy slots the branch-free
 // histogram adds 0 into (hist_int4).
-constexpr int kHistPad = kHistCopies > 1 ? 32 / kHistCopies : 32;
-constexpr int kHistStride = kHistBins + kHistPad;
-constexpr int kHistLds = kHistCopies * kHistStride;   // ints of LDS
+template <bool kLong>
+struct HistCfg {
+    static constexpr int kCopies = kLong ? MC_HIST_COPIES_LONG : MC_HIST_COPIES;
+    static constexpr int kBins = kLong ? MC_HIST_BINS_LONG : MC_HIST_BINS;
+    static constexpr int kPad = kCopies > 1 ? 32 / kCopies : 32;
+    static constexpr int kStride = kBins + kPad;
+    static constexpr int kLds = kCopies * kStride;   // ints of LDS
+    static_assert(kBins % 32 == 0 && (kCopies & (kCopies - 1)) == 0 && kCopies <= 32,
+                  "histogram bins: multiple of 32; copies: power of two");
+};
+constexpr int kHistBins = HistCfg<false>::kBins;          // the short-read variant's window
+// values per region row of the global fused histogram
+__host__ __device__ constexpr int fused_hist_vals(bool long_reads) {
+    return long_reads ? HistCfg<true>::kBins : HistCfg<false>::kBins;
+}
 
 struct FusedRegions {
     int64_t n;                         // 0 = no fused statistics
@@ -1345,7 +1443,7 @@ struct FusedRegions {
     const int32_t* id;                 // [n] caller's row index
     const int32_t* base;               // [n] value of histogram bin 0 (window base)
     RegionAcc* acc;                    // [rows] statistics of the values outside the window
-    unsigned* hist;                    // [rows][kHistBins]
+    unsigned* hist;                    // [rows][HistCfg<kLong>::kBins]
     unsigned* low;                     // [rows] count of values below the window
 };
 
@@ -1434,6 +1532,7 @@ static_assert(kRing == 2 * kTileW, "the ring tail is one tile (short_max = kTile
 // the predicated form cost ~6 SALU exec-mask instructions per atomic, and the
 // fused K2 is bound by instruction issue, not by LDS), and the rare
 // out-of-window path (same run arithmetic as region_seg_kernel).
+template <int kWinBins>
 __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, int y0, int y1, int y2, int y3,
                                           int base) {
     const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
@@ -1441,7 +1540,7 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, in
     const int l1 = s2 ? 1 : l2 + 1;
     const int l0 = s1 ? 1 : l1 + 1;
     const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
-    constexpr unsigned kWin = (unsigned)kHistBins;
+    constexpr unsigned kWin = (unsigned)kWinBins;
     const unsigned d0 = (unsigned)(y0 - base), d1 = (unsigned)(y1 - base),
                    d2 = (unsigned)(y2 - base), d3 = (unsigned)(y3 - base);
     const bool w0 = e0 && d0 < kWin, w1 = e1 && d1 < kWin, w2 = e2 && d2 < kWin, w3 = e3 && d3 < kWin;
@@ -1502,7 +1601,7 @@ __device__ __forceinline__ void load_events(EvBatch& e, const int32_t* __restric
 // into the region's global accumulator and flushes the LDS histogram.
 // kBarriers = false: the caller has just passed a barrier after the last
 // atomics, and a barrier follows before the histogram is used again.
-template <bool kBarriers = true>
+template <bool kBarriers, class HC>
 __device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsigned* h, OvLds* ov) {
     // id: the region's row, loaded with its other fields (no scalar load on
     // the chunk end's path)
@@ -1518,15 +1617,15 @@ __device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsi
             ov_reset(o);
         }
     }
-    unsigned* g = R.hist + (int64_t)id * kHistBins;
-    for (int k = threadIdx.x; k < kHistBins; k += kBlock) {
+    unsigned* g = R.hist + (int64_t)id * HC::kBins;
+    for (int k = threadIdx.x; k < HC::kBins; k += kBlock) {
         unsigned cnt = 0;
 #pragma unroll
-        for (int c = 0; c < kHistCopies; ++c) cnt += h[c * kHistStride + k];
+        for (int c = 0; c < HC::kCopies; ++c) cnt += h[c * HC::kStride + k];
         if (cnt) {
             atomicAdd(&g[k], cnt);
 #pragma unroll
-            for (int c = 0; c < kHistCopies; ++c) h[c * kHistStride + k] = 0;
+            for (int c = 0; c < HC::kCopies; ++c) h[c * HC::kStride + k] = 0;
         }
     }
     if (kBarriers) __syncthreads();
@@ -1574,11 +1673,12 @@ depth_kernel(ReadArrays A, int64_t n,
     int and_flip = 0;
     int* ring = lds + kLdsHeader;
     unsigned* hist = reinterpret_cast<unsigned*>(ring + kRing);   // kStats only
-    OvLds* ovf = reinterpret_cast<OvLds*>(hist + kHistLds);            // kStats only
+    using HC = HistCfg<kLong>;
+    OvLds* ovf = reinterpret_cast<OvLds*>(hist + HC::kLds);            // kStats only
     const int lane = threadIdx.x & 63;
-    unsigned* hist_lane = hist + (lane & (kHistCopies - 1)) * kHistStride;   // this lane's copy
+    unsigned* hist_lane = hist + (lane & (HC::kCopies - 1)) * HC::kStride;   // this lane's copy
     // this lane's pad slot: distinct among the lanes of its copy in a half-wave
-    const int hist_dummy = kHistBins + (lane / kHistCopies) % kHistPad;
+    const int hist_dummy = HC::kBins + (lane / HC::kCopies) % HC::kPad;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform per wave
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
     constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
@@ -1600,7 +1700,7 @@ depth_kernel(ReadArrays A, int64_t n,
     OvReg ovr;                 // kStats: this lane's out-of-window runs of the open region
     ov_reg_reset(ovr);
     if (kStats) {
-        for (int k = threadIdx.x; k < kHistLds; k += kBlock) hist[k] = 0;
+        for (int k = threadIdx.x; k < HC::kLds; k += kBlock) hist[k] = 0;
         if (threadIdx.x < kOvRecs) ov_reset(ovf + threadIdx.x);   // ordered by the first barrier
     }
 
@@ -1826,11 +1926,11 @@ depth_kernel(ReadArrays A, int64_t n,
                             y2 = (q0 + 2 >= lo && q0 + 2 < hi) ? y2 : -1;
                             y3 = (q0 + 3 >= lo && q0 + 3 < hi) ? y3 : -1;
                         }
-                        hist_int4(hist_lane, hist_dummy, ovr, y0, y1, y2, y3, r_base);
+                        hist_int4<HC::kBins>(hist_lane, hist_dummy, ovr, y0, y1, y2, y3, r_base);
                     }
                     if (rge <= Tend) {
                         ov_reg_spill(ovr, ovf);
-                        flush_region<true>(R, r_id, hist, ovf);
+                        flush_region<true, HC>(R, r_id, hist, ovf);
                         ++rcur;
                         if (rcur < R.n) {
                             r_gs = uload(R.gs, rcur);
@@ -1850,11 +1950,12 @@ depth_kernel(ReadArrays A, int64_t n,
         if (kStats) {
             // a region still open at the chunk end has partials here; the
             // barrier above and the one after the ring zeroing bracket it
-            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false>(R, r_id, hist, ovf);
+            if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, HC>(R, r_id, hist, ovf);
         }
         if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks);
         for (int k = threadIdx.x * 4; k < kTileW; k += kBlock * 4)
             *reinterpret_cast<i32x4*>(ring + ring_tail + k) = i32x4{0, 0, 0, 0};
+        if (kDirect && MC_DIRECT_VALIDATE_END) validate_own(dc.vlo, dc.vhi, A, D, short_max, dacc);
     }
     // one atomic per workgroup (same-address atomics of every wave at the end of
     // the launch serialise); hdr[8..11] are free once the queue is drained

@@ -21,7 +21,9 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", nargs="+", required=True)
-    ap.add_argument("--mode", default="plain", choices=["plain", "fused", "both"])
+    ap.add_argument("--mode", default="plain", choices=["plain", "fused", "both", "direct", "all"],
+                    help="plain / fused: K2 on one explicit prepare's index; direct: every call a "
+                         "fresh batch (mc_invalidate first: the direct prepare + validating fused K2)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reads", type=int, default=100_000_000)
@@ -44,19 +46,27 @@ def main():
         e = CoverageEngine(0, lib_path=os.path.abspath(lib))
         e.set_contigs(lengths)
         e.add_reads(tid, pos, span)
-        e.prepare()
         engines.append(e)
-    modes = ["plain", "fused"] if a.mode == "both" else [a.mode]
+    modes = {"both": ["plain", "fused"], "all": ["plain", "fused", "direct"]}.get(a.mode, [a.mode])
     for mode in modes:
         times = {lib: [] for lib in a.libs}
+        walls = {lib: [] for lib in a.libs}
         ref_rows = None
+        import time
         for _ in range(a.rounds):
             for lib, e in zip(a.libs, engines):
+                if mode != "direct":
+                    e.prepare()
                 for _ in range(a.steps):
+                    t0 = time.perf_counter()
                     if mode == "plain":
                         e.compute_depth()
                     else:
+                        if mode == "direct":
+                            e.invalidate()
                         rows = e.compute_depth_stats(rt, rs, re_)
+                    e.synchronize()
+                    walls[lib].append((time.perf_counter() - t0) * 1e3)
                     times[lib].append(e.timings()["depth_ms"])
                 if mode == "plain":
                     rows = e.region_stats(rt, rs, re_)
@@ -67,8 +77,10 @@ def main():
                         assert np.array_equal(rows[f], ref_rows[f]), (lib, f)
         for lib in a.libs:
             t = np.array(times[lib])
-            print("%-6s %-48s K2 median %.4f ms  min %.4f ms  (n=%d)"
-                  % (mode, os.path.basename(lib), np.median(t), t.min(), len(t)), flush=True)
+            w = np.array(walls[lib])
+            fb = engines[a.libs.index(lib)].fused_fallbacks() if mode != "plain" else 0
+            print("%-6s %-48s K2 median %.4f ms  min %.4f ms  call median %.4f ms  fallbacks %d  (n=%d)"
+                  % (mode, os.path.basename(lib), np.median(t), t.min(), np.median(w), fb, len(t)), flush=True)
 
 
 if __name__ == "__main__":
