@@ -513,6 +513,7 @@ def main():
                            "k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
                            ("k3_region_stats" if args.unfused else "k3b_finalize"): k3_ms},
             "fused_fallback_regions": None if args.unfused else eng.fused_fallbacks(),
+            "fused_device_recomputes": None if args.unfused else eng.fused_recomputes(),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,

@@ -200,8 +200,10 @@ int mc_region_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
  * depth vector is written once and never re-read.  Regions must not overlap
  * each other for the fused path (whole contigs, a tiling of a contig, most
  * BLAST hit lists); otherwise this runs K2 then K3.  Same rows as
- * mc_region_stats.  Regions whose median / q23 ranks reach depths >= 1024
- * are recomputed exactly by K3 (mc_fused_fallbacks counts them). */
+ * mc_region_stats.  Each region's histogram window holds 864 values (1728 for
+ * long reads) around its contig's estimated depth; a region whose median /
+ * q23 ranks fall outside it is recomputed exactly from the depth vector
+ * (mc_fused_recomputes / mc_fused_fallbacks). */
 int mc_compute_depth_stats(mc_ctx* ctx, int64_t R, const int32_t* tid,
                            const int64_t* start, const int64_t* end,
                            mc_region_stat* out);
@@ -209,6 +211,12 @@ int mc_compute_depth_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
                                   const int64_t* start, const int64_t* end,
                                   mc_region_stat* d_out);
 int mc_fused_fallbacks(mc_ctx* ctx, int64_t* out);
+/* Regions of the last fused call whose median / q23 ranks left their LDS
+ * window and were recomputed exactly ON THE DEVICE within the call (long-read
+ * batches, or after a call that had such regions: the depth vector is
+ * re-read for those regions only, no host round trip); mc_fused_fallbacks
+ * counts the ones the host's K3 recomputed instead. */
+int mc_fused_recomputes(mc_ctx* ctx, int64_t* out);
 
 /* Aligned bases (sum of spans) of the reads added so far. */
 int mc_aligned_bases(mc_ctx* ctx, int64_t* out);

@@ -96,6 +96,7 @@ SIGNATURES = {
     "mc_compute_depth_stats": [_P, _I64, _P, _P, _P, _P],
     "mc_compute_depth_stats_device": [_P, _I64, _P, _P, _P, _P],
     "mc_fused_fallbacks": [_P, _PI64],
+    "mc_fused_recomputes": [_P, _PI64],
     "mc_aligned_bases": [_P, _PI64],
     "mc_max_depth": [_P, _PI32],
     "mc_get_timings": [_P, ctypes.POINTER(Timings)],

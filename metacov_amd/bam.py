@@ -154,7 +154,8 @@ class BamFile:
                 tid = np.searchsorted(self.contigs, self.tid).astype(np.int32)
             eng.set_contigs(lengths)
             eng.add_reads(tid, self.pos, self.span)
-            eng.prepare()
+            # (no explicit prepare: the first compute call prepares the batch,
+            # by the direct path when it can take it)
             eng._depth_ready = False
             self._engines[device] = eng
         if compute and not eng._depth_ready:
@@ -289,7 +290,6 @@ class StreamedBam:
                 i ^= 1
             eng.synchronize()
             self.n_records, self.mapped, self.unmapped = st.counts()
-        eng.prepare()
         eng._depth_ready = False
         self._eng, self._device = eng, device
 

@@ -241,6 +241,14 @@ struct mc_ctx {
     DevBuf<unsigned> d_flow;
     DevBuf<unsigned> d_fhist;
     HostMapped<int> h_fflag;              // fallback flags, written by region_final_kernel
+    // device-side recompute of the fused call's out-of-window regions (fb_seg_kernel)
+    DevBuf<unsigned> d_fb_hist;           // [kFbSlots][kLdsBins]
+    DevBuf<RegionAcc> d_fb_acc;           // [kFbSlots]
+    DevBuf<int32_t> d_fb_list;            // [kFbSlots]
+    DevBuf<unsigned> d_fb_cnt;            // [2] (by call parity)
+    int64_t fb_calls = 0;
+    bool fb_recent = false;               // the last fused call had out-of-window regions
+    int64_t device_recomputes = 0;
     bool fused_clean = false;             // K3b left hist / low / acc / queue initialised
     int64_t fused_clean_R = 0;
     int64_t fused_fallbacks = 0;
@@ -334,6 +342,10 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->fcache.chunk_first = false;
     ctx->d_flow.release();
     ctx->d_fhist.release();
+    ctx->d_fb_hist.release();
+    ctx->d_fb_acc.release();
+    ctx->d_fb_list.release();
+    ctx->d_fb_cnt.release();
     for (auto ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1263,6 +1275,39 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     if (int rc = launch_depth(ctx, fr)) return rc;
     // K3b: its span is timed from K2's end event (one event fewer per call)
     ctx->stats_after_depth = true;
+    // the device-side recompute of out-of-window regions: on for long reads
+    // (deep contigs with long end ramps) and after a call that had them
+    const bool devfb = ctx->has_long || ctx->fb_recent;
+    FbArgs F{};
+    if (devfb) {
+        if (!ctx->d_fb_cnt.p) {
+            HIP_TRY(ctx->d_fb_hist.reserve((size_t)kFbSlots * kLdsBins));
+            HIP_TRY(ctx->d_fb_acc.reserve(kFbSlots));
+            HIP_TRY(ctx->d_fb_list.reserve(kFbSlots));
+            HIP_TRY(ctx->d_fb_cnt.reserve(2));
+            HIP_TRY(hipMemsetAsync(ctx->d_fb_cnt.p, 0, 8, s));
+            hipLaunchKernelGGL(fused_init_kernel, dim3(1024), dim3(kBlock), 0, s, ctx->d_fb_hist.p,
+                               (int64_t)kFbSlots * kLdsBins, (unsigned*)nullptr, ctx->d_fb_acc.p,
+                               (int64_t)kFbSlots, (const int64_t*)nullptr, (int64_t)0, (int64_t)1, (int64_t)0,
+                               (int64_t*)nullptr, (unsigned*)nullptr, (int*)nullptr);
+            HIP_TRY(hipGetLastError());
+        }
+        F = FbArgs{ctx->d_depth.p,
+                   reinterpret_cast<const int32_t*>(d + L.rfused),
+                   reinterpret_cast<const int64_t*>(d + o_gs),
+                   reinterpret_cast<const int64_t*>(d + o_ge),
+                   reinterpret_cast<const int64_t*>(d + o_ntot),
+                   reinterpret_cast<const int64_t*>(d + o_nzx),
+                   // K2's max depth as K3b copied it out (K3b resets d_maxdepth for the next call)
+                   ctx->h_fflag.d + R,
+                   ctx->d_fb_list.p,
+                   ctx->d_fb_cnt.p,
+                   (int)(ctx->fb_calls & 1),
+                   ctx->d_fb_hist.p,
+                   ctx->d_fb_acc.p,
+                   d_out};
+        ctx->fb_calls += 1;
+    }
     // one wave per region; flags [0, R) and K2's max depth [R] land in mapped host memory
 #define MC_LAUNCH_K3B(V)                                                                           \
     hipLaunchKernelGGL(region_final_wave_kernel<V>, dim3((unsigned)((R + kWaves - 1) / kWaves)),        \
@@ -1271,11 +1316,18 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                        reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,           \
                        reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,                 \
                        ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p,                       \
-                       verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr)
+                       verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr, \
+                       devfb ? F.cnt + F.parity : nullptr, devfb ? F.list : nullptr)
     if (vals == HistCfg<false>::kBins) MC_LAUNCH_K3B(HistCfg<false>::kBins);
     else MC_LAUNCH_K3B(HistCfg<true>::kBins);
 #undef MC_LAUNCH_K3B
     HIP_TRY(hipGetLastError());
+    if (devfb) {
+        hipLaunchKernelGGL(fb_seg_kernel, dim3(1024), dim3(kBlock), (size_t)kLdsBins * 4, s, F);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(fb_final_kernel, dim3(kFbSlots), dim3(kBlock), 0, s, F);
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(ctx->ev[7], s));
     ctx->t_stats = true;
     ctx->t.stats_launches += 1;
@@ -1287,16 +1339,24 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         return kRedo;
     }
     ctx->max_depth = flags[R];   // a fallback's K3 sizes its histogram by it
+    int64_t n_flag = 0;
+    for (int64_t r = 0; r < R; ++r) n_flag += flags[r] ? 1 : 0;
+    // the device recomputed them in this call unless there were too many or
+    // the depth exceeds its histogram
+    const bool on_device = devfb && n_flag <= kFbSlots && ctx->max_depth < kLdsBins;
     std::vector<int32_t> ft;
     std::vector<int64_t> fs, fe, fr_idx;
-    for (int64_t r = 0; r < R; ++r)
-        if (flags[r]) {
-            ft.push_back(tid[r]);
-            fs.push_back(start[r]);
-            fe.push_back(end[r]);
-            fr_idx.push_back(r);
-        }
+    if (!on_device)
+        for (int64_t r = 0; r < R; ++r)
+            if (flags[r]) {
+                ft.push_back(tid[r]);
+                fs.push_back(start[r]);
+                fe.push_back(end[r]);
+                fr_idx.push_back(r);
+            }
     ctx->fused_fallbacks = (int64_t)ft.size();
+    ctx->device_recomputes = on_device ? n_flag : 0;
+    ctx->fb_recent = n_flag > 0;
     if (ft.empty()) {    // K3b reset the buffers behind it
         ctx->fused_clean = true;
         ctx->fused_clean_R = R;
@@ -1468,6 +1528,12 @@ extern "C" int mc_compute_depth_stats_device(mc_ctx* ctx, int64_t R, const int32
 extern "C" int mc_fused_fallbacks(mc_ctx* ctx, int64_t* out) {
     MC_REQUIRE(ctx && out, MC_E_INVALID, "null argument");
     *out = ctx->fused_fallbacks;
+    return MC_OK;
+}
+
+extern "C" int mc_fused_recomputes(mc_ctx* ctx, int64_t* out) {
+    MC_REQUIRE(ctx && out, MC_E_INVALID, "null argument");
+    *out = ctx->device_recomputes;
     return MC_OK;
 }
 

@@ -1267,35 +1267,47 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         pt = r.pt;
         ppv = r.pp;
     }
-    unsigned pend = 0;
+    // 4-bit masks of this lane's reads: in [lo, hi) (applied) and in [vlo,
+    // vhi) (checked here), from two 64-bit differences per range
+    auto range4 = [&](int64_t lo, int64_t hi) -> unsigned {
+        const int64_t a = lo - i0, z = hi - i0;
+        const int ka = a < 0 ? 0 : a > 4 ? 4 : (int)a, kz = z < 0 ? 0 : z > 4 ? 4 : (int)z;
+        return ((1u << kz) - 1u) & ~((1u << ka) - 1u);
+    };
+    unsigned pend = 0, bad = 0, unfit = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int64_t i = i0 + k;
         b.rs[k] = rs[k];
         b.sp[k] = sp[k];
         const bool ok = (valid >> k) & 1u;
-        pend |= (ok & (i >= dc.lo) & (i < dc.hi) & (rs[k] < chunk_w) & (sp[k] <= short_max)) ? 1u << k : 0u;
-#if defined(MC_DIRECT_NOCHECK) || MC_DIRECT_VALIDATE_END   // (no validation here)
-        const bool own = false;
-#else
-        const bool own = (i >= dc.vlo) & (i < dc.vhi);
-#endif
+        pend |= (ok & (rs[k] < chunk_w) & (sp[k] <= short_max)) ? 1u << k : 0u;
         const int qt = k ? tt[k - 1] : pt, qp = k ? pp[k - 1] : ppv;
 #ifdef MC_EXP_NO_ORDER
         const bool uns = false;
         (void)qt; (void)qp;
 #else
-        const bool uns = (i > 0) & ((qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k])));
+        const bool uns = (qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k]));   // (read 0 of all: pt = -1)
 #endif
+        bad |= (!ok | uns) ? 1u << k : 0u;
 #ifdef MC_EXP_NO_LEN
-        const bool unfit = (sp[k] > short_max);
+        unfit |= (sp[k] > short_max) ? 1u << k : 0u;
 #else
-        const bool unfit = (sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k]);
+        unfit |= ((sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k])) ? 1u << k : 0u;
 #endif
-        acc.flags |= own ? (!ok | uns ? kDirectInvalid : unfit ? kDirectUnfit : 0u) : 0u;
-        acc.bases += (own & ok) ? (unsigned)sp[k] : 0u;
     }
-    b.pending = pend;
+    b.pending = pend & range4(dc.lo, dc.hi);
+#if !(defined(MC_DIRECT_NOCHECK) || MC_DIRECT_VALIDATE_END)
+    const unsigned own = range4(dc.vlo, dc.vhi);
+    acc.flags |= (bad & own) ? kDirectInvalid : (unfit & own) ? kDirectUnfit : 0u;
+#ifndef MC_EXP_NO_BASES
+    const unsigned keep = own & valid;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc.bases += ((keep >> k) & 1u) ? (unsigned)sp[k] : 0u;
+#endif
+#else
+    (void)bad;
+    (void)unfit;
+#endif
 }
 
 // K2 direct: the per-workgroup verdict into dres (one atomic each)
@@ -2080,7 +2092,8 @@ region_seg_kernel(const int32_t* __restrict__ depth, const int64_t* __restrict__
             lo = min(lo, ext[w]);
             hi = max(hi, ext[kWaves + w]);
         }
-        for (int k = lo + threadIdx.x; k <= hi && k < nbins; k += kBlock) {
+        if (lo <= hi)   // (lo = INT_MAX when the segment has no position: lo + tid would overflow)
+        for (int k = lo + (int)threadIdx.x; k <= hi && k < nbins; k += kBlock) {
             const unsigned c = h[k];
             if (c) atomicAdd(&ghist[k], c);
         }
@@ -2105,27 +2118,22 @@ struct RegionOut {                     // mirrors mc_region_stat
 // is written to out[out_row[r]] (scattered fallback rows).  fallback[r] = 1
 // when a needed rank lies outside the window: the host recomputes that region
 // with the full-range K3.  Positions past the contig extent (zx) are zeros.
-__global__ void __launch_bounds__(kBlock)
-region_final_kernel(const unsigned* __restrict__ hist, int nbins,
-                    const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
-                    const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
-                    int* __restrict__ fallback, int hist_stats,
-                    const int32_t* __restrict__ base_of, const unsigned* __restrict__ low_of,
-                    int bound_by_max, const int64_t* __restrict__ out_row) {
+// One region's row from its value histogram (the body of region_final_kernel;
+// every thread of the block calls it).  hr: the region's bins; a: its
+// accumulator; out_p: where the row goes; fb: its fallback flag (may be null).
+__device__ __forceinline__ void region_final_row(const unsigned* __restrict__ hr, int nbins, const RegionAcc& a,
+                                                 long long n, long long zx, RegionOut* out_p, int* fb,
+                                                 int hist_stats, long long base, long long low_in,
+                                                 int bound_by_max) {
     __shared__ long long s_tot[2][kWaves];
     __shared__ long long s_red[4][kWaves];
     __shared__ long long s_med[2];
-    const int r = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned* hr = hist + (int64_t)r * nbins;
-    const long long n = n_total[r];
-    const long long zx = n_zero_extra[r];
-    const long long base = base_of ? base_of[r] : 0;
     // zeros past the extent land in bin 0 when the window starts at 0,
     // otherwise below the window
     const long long zx_bin = base == 0 ? zx : 0;
-    const long long low = (low_of ? (long long)low_of[r] : 0) + (base == 0 ? 0 : zx);
-    const int nb = bound_by_max ? min(nbins, max(acc[r].max, 0) + 1) : nbins;
+    const long long low = low_in + (base == 0 ? 0 : zx);
+    const int nb = bound_by_max ? min(nbins, max(a.max, 0) + 1) : nbins;
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;
     const long long q_lo = n / 4, q_hi = n - n / 4;
     if (threadIdx.x < 2) s_med[threadIdx.x] = 0;
@@ -2191,9 +2199,8 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
     __syncthreads();
     if (threadIdx.x == 0) {
         const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
-        if (fallback)
-            fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo ||
-                                     q_hi - 1 >= win_hi)) ? 1 : 0;
+        if (fb)
+            *fb = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi)) ? 1 : 0;
         long long q = 0, t1 = 0;
         unsigned long long t2 = 0;
         int hmin = 0x7fffffff, hmax = -1;
@@ -2204,7 +2211,6 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
             hmin = min(hmin, (int)(s_red[3][w] >> 32));
             hmax = max(hmax, (int)(s_red[3][w] & 0xffffffff) - 1);
         }
-        const RegionAcc a = acc[r];
         RegionOut o;
         o.n = n;
         if (hist_stats) {
@@ -2237,7 +2243,149 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
             o.sum = 0;
             o.sumsq = 0;
         }
-        out[out_row ? out_row[r] : r] = o;
+        *out_p = o;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+region_final_kernel(const unsigned* __restrict__ hist, int nbins,
+                    const RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
+                    const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
+                    int* __restrict__ fallback, int hist_stats,
+                    const int32_t* __restrict__ base_of, const unsigned* __restrict__ low_of,
+                    int bound_by_max, const int64_t* __restrict__ out_row) {
+    const int r = blockIdx.x;
+    region_final_row(hist + (int64_t)r * nbins, nbins, acc[r], n_total[r], n_zero_extra[r],
+                     out + (out_row ? out_row[r] : r), fallback ? fallback + r : nullptr, hist_stats,
+                     base_of ? base_of[r] : 0, low_of ? (long long)low_of[r] : 0, bound_by_max);
+}
+
+// ---- the fused call's exact recompute on the device ----------------------
+// Regions whose ranks leave their LDS window (region_final_wave_kernel flags
+// them and lists them in fb_list) are recomputed in the same call from the
+// depth vector K2 just wrote, without the host round trip the K3 fallback
+// takes: fb_seg_kernel builds each listed region's full value histogram
+// (kLdsBins values, enough while the maximum depth is below it), workgroups
+// splitting the region's positions, and fb_final_kernel derives its row
+// and scatters it into place.  Both leave their buffers zeroed for the next
+// call.  Listed regions beyond kFbSlots, or a maximum depth >= kLdsBins, are
+// left to the host's K3 fallback.
+constexpr int kFbSlots = 512;
+
+// The histogram of depth[gs, ge) into h (LDS, nb bins), runs of equal values
+// within an int4 sharing one atomic; returns this thread's max and min.
+__device__ __forceinline__ void seg_hist(const int32_t* __restrict__ depth, int64_t gs, int64_t ge, unsigned* h,
+                                         int nb, int& vmax, unsigned& vmin) {
+    constexpr int kU = 4;
+    const int64_t a4 = gs & ~(int64_t)3;
+    for (int64_t p0 = a4 + (int64_t)threadIdx.x * 4; p0 < ge; p0 += (int64_t)kBlock * 4 * kU) {
+        i32x4 x[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t q = p0 + (int64_t)u * kBlock * 4;
+            x[u] = q < ge ? *reinterpret_cast<const i32x4*>(depth + q) : i32x4{-1, -1, -1, -1};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t q = p0 + (int64_t)u * kBlock * 4;
+            // (values outside [0, nb) are never there after a K2 that ran; the
+            // bound keeps a stale vector from writing past the LDS histogram)
+            const int y0 = (q >= gs && q < ge && x[u].x < nb) ? x[u].x : -1;
+            const int y1 = (q + 1 >= gs && q + 1 < ge && x[u].y < nb) ? x[u].y : -1;
+            const int y2 = (q + 2 >= gs && q + 2 < ge && x[u].z < nb) ? x[u].z : -1;
+            const int y3 = (q + 3 >= gs && q + 3 < ge && x[u].w < nb) ? x[u].w : -1;
+            const bool s1 = y1 != y0, s2 = y2 != y1, s3 = y3 != y2;
+            const int l2 = s3 ? 1 : 2;
+            const int l1 = s2 ? 1 : l2 + 1;
+            const int l0 = s1 ? 1 : l1 + 1;
+            if (y0 >= 0) atomicAdd(&h[y0], (unsigned)l0);
+            if (s1 && y1 >= 0) atomicAdd(&h[y1], (unsigned)l1);
+            if (s2 && y2 >= 0) atomicAdd(&h[y2], (unsigned)l2);
+            if (s3 && y3 >= 0) atomicAdd(&h[y3], 1u);
+            vmax = max(vmax, max(max(y0, y1), max(y2, y3)));
+            vmin = min(vmin, min(min((unsigned)y0, (unsigned)y1), min((unsigned)y2, (unsigned)y3)));
+        }
+    }
+}
+
+struct FbArgs {
+    const int32_t* depth;
+    const int32_t* rfused;             // [R] row -> fused entry, or -1 (staged)
+    const int64_t* fgs;                // [nf] entry global start / end (staged)
+    const int64_t* fge;
+    const int64_t* ntot;               // [R] positions / positions past the extent (staged)
+    const int64_t* nzx;
+    const int* max_depth;              // K2's, as region_final_wave_kernel copied it (max_out)
+    int32_t* list;                     // [kFbSlots] listed rows
+    unsigned* cnt;                     // [2] per call parity
+    int parity;
+    unsigned* hist;                    // [kFbSlots][kLdsBins]
+    RegionAcc* acc;                    // [kFbSlots]
+    RegionOut* out;                    // the call's rows
+};
+
+__global__ void __launch_bounds__(kBlock)
+fb_seg_kernel(FbArgs F) {
+    extern __shared__ __attribute__((aligned(16))) unsigned hb[];
+    const int n = (int)min(F.cnt[F.parity], (unsigned)kFbSlots);
+    const int maxd = *F.max_depth;
+    if (n == 0 || maxd >= kLdsBins) return;
+    const int nb = maxd + 1;
+    const int per = max(1, (int)gridDim.x / n);        // workgroups per region
+    __shared__ int ext[2 * kWaves];
+    for (int w = blockIdx.x; w < n * per; w += gridDim.x) {
+        const int i = w / per, part = w % per;
+        const int k = F.rfused[F.list[i]];
+        if (k < 0) continue;                           // no covered position: zeros only
+        const int64_t gs0 = F.fgs[k], len = F.fge[k] - gs0;
+        const int64_t gs = gs0 + len * part / per, ge = gs0 + len * (part + 1) / per;
+        for (int q = threadIdx.x * 4; q < nb; q += kBlock * 4)
+            *reinterpret_cast<i32x4*>(hb + q) = i32x4{0, 0, 0, 0};
+        __syncthreads();
+        int vmax = 0;
+        unsigned vmin = 0xffffffffu;
+        seg_hist(F.depth, gs, ge, hb, nb, vmax, vmin);
+        vmax = wave_max(vmax);
+        const int wmin = wave_min((int)min(vmin, 0x7fffffffu));
+        if ((threadIdx.x & 63) == 0) {
+            ext[threadIdx.x >> 6] = wmin;
+            ext[kWaves + (threadIdx.x >> 6)] = vmax;
+        }
+        __syncthreads();
+        int lo = ext[0], hi = ext[kWaves];
+#pragma unroll
+        for (int q = 1; q < kWaves; ++q) {
+            lo = min(lo, ext[q]);
+            hi = max(hi, ext[kWaves + q]);
+        }
+        unsigned* g = F.hist + (int64_t)i * kLdsBins;
+        // (an empty part leaves lo = INT_MAX > hi: nothing to flush; lo + tid would overflow)
+        if (lo <= hi)
+        for (int q = lo + (int)threadIdx.x; q <= hi && q < nb; q += kBlock) {
+            const unsigned c = hb[q];
+            if (c) atomicAdd(&g[q], c);
+        }
+        if (threadIdx.x == 0 && hi > 0) atomicMax(&F.acc[i].max, hi);
+        __syncthreads();                               // before the next item zeroes hb
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+fb_final_kernel(FbArgs F) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) F.cnt[F.parity ^ 1] = 0;   // the next call's counter
+    const int n = (int)min(F.cnt[F.parity], (unsigned)kFbSlots);
+    const int maxd = *F.max_depth;
+    const int b = blockIdx.x;
+    if (b >= n || maxd >= kLdsBins) return;
+    const int r = F.list[b];
+    unsigned* hr = F.hist + (int64_t)b * kLdsBins;
+    region_final_row(hr, maxd + 1, F.acc[b], F.ntot[r], F.nzx[r], F.out + r, nullptr, 1, 0, 0, 1);
+    __syncthreads();
+    for (int q = threadIdx.x; q <= maxd; q += kBlock) hr[q] = 0;
+    if (threadIdx.x == 0) {
+        F.acc[b].sum = F.acc[b].sumsq = 0;
+        F.acc[b].min = 0x7fffffff;
+        F.acc[b].max = 0;
     }
 }
 
@@ -2256,7 +2404,8 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
                          int* __restrict__ fallback, const int32_t* __restrict__ base_of,
                          unsigned* __restrict__ low_of, int* __restrict__ max_depth,
                          int* __restrict__ max_out, unsigned* __restrict__ queue,
-                         const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out) {
+                         const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out,
+                         unsigned* __restrict__ fb_cnt, int32_t* __restrict__ fb_list) {
     constexpr int kFinPer = (kVals + 63) / 64;
     const int lane = threadIdx.x & 63;
     // dres_out (mapped host memory): the direct K2's validation counters, so
@@ -2343,8 +2492,12 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     med_hi = hm_hi ? readlane64(med_hi, __ffsll((long long)hm_hi) - 1) : -1;
     if (lane != 0) return;
     const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
-    fallback[r] = (n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi))
-                      ? 1 : 0;
+    const bool fb = n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi);
+    fallback[r] = fb ? 1 : 0;
+    if (fb && fb_cnt) {   // listed for the device-side recompute (fb_seg_kernel)
+        const unsigned slot = atomicAdd(fb_cnt, 1u);
+        if (slot < (unsigned)kFbSlots) fb_list[slot] = (int32_t)r;
+    }
     const RegionAcc a = acc[r];
     if (queue) {
         acc[r].sum = 0;

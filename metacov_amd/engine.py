@@ -243,8 +243,15 @@ class CoverageEngine:
                                                       ptr(ends), ctypes.c_void_p(d_out_ptr)))
 
     def fused_fallbacks(self):
+        """Regions of the last fused call the host's K3 recomputed."""
         v = ctypes.c_int64()
         self._check(self._lib.mc_fused_fallbacks(self._h, ctypes.byref(v)))
+        return v.value
+
+    def fused_recomputes(self):
+        """Regions of the last fused call recomputed on the device in the call."""
+        v = ctypes.c_int64()
+        self._check(self._lib.mc_fused_recomputes(self._h, ctypes.byref(v)))
         return v.value
 
     def aligned_bases(self):

@@ -14,20 +14,21 @@ stop_if_fatal() {
     *) echo "fatal status $1: stopping"; exit "$1" ;;
   esac
 }
+faulted() { if grep -qiE "illegal memory access|memory access fault|hipErrorLaunchFailure|gpu hang" "$@" 2>/dev/null; then echo "GPU fault in $*: stopping"; exit 90; fi; }
 if [ -z "${SKIP_TESTS:-}" ]; then
 timeout -k 10 240 python __graft_entry__.py smoke > $O/${TAG}_smoke.log 2>&1
-s=$?; cat $O/${TAG}_smoke.log; stop_if_fatal $s
+s=$?; cat $O/${TAG}_smoke.log; faulted $O/${TAG}_smoke.log; stop_if_fatal $s
 timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu ${PYTEST_ARGS:--x} -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/${TAG}_pytest_gpu.log 2>&1
-s=$?; grep -E "passed|failed|error" $O/${TAG}_pytest_gpu.log | tail -15; stop_if_fatal $s
+s=$?; grep -E "passed|failed|error" $O/${TAG}_pytest_gpu.log | tail -15; faulted $O/${TAG}_pytest_gpu.log; stop_if_fatal $s
 fi
 if [ -z "${SKIP_BENCH:-}" ]; then
 timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $O/${TAG}_bench.log 2>&1
-s=$?; tail -2 $O/${TAG}_bench.log; stop_if_fatal $s
+s=$?; tail -2 $O/${TAG}_bench.log; faulted $O/${TAG}_bench.log; stop_if_fatal $s
 fi
 if [ -n "${PROF:-}" ]; then
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $O/${TAG}_prof.log 2>&1
-s=$?; tail -2 $O/${TAG}_prof.log; stop_if_fatal $s
+s=$?; tail -2 $O/${TAG}_prof.log; faulted $O/${TAG}_prof.log; stop_if_fatal $s
 cd $R
 fi
 exit 0

@@ -72,7 +72,7 @@ def test_c3_full_size():
         rows = eng.compute_depth_stats(np.arange(len(lengths), dtype=np.int32),
                                        np.zeros(len(lengths), np.int64), lengths)
         assert _paths(eng) == (1, 0)
-        assert eng.fused_fallbacks() == 0
+        assert eng.fused_fallbacks() == 0 and eng.fused_recomputes() == 0
         _compare(eng, lengths, h, rows)
         # the reused-index path (explicit full prepare, packed read words) on the same batch
         eng.invalidate()
@@ -101,8 +101,9 @@ def test_c5_full_size_and_cigar_path():
         rt = np.arange(len(lengths), dtype=np.int32)
         rows = eng.compute_depth_stats(rt, np.zeros(len(lengths), np.int64), lengths)
         assert _paths(eng)[1] >= 1            # long reads: the full prepare
-        fallbacks = eng.fused_fallbacks()
-        print("C5 fused fallback regions:", fallbacks)
+        print("C5 out-of-window regions: %d recomputed on the device, %d by the host"
+              % (eng.fused_recomputes(), eng.fused_fallbacks()))
+        assert eng.fused_fallbacks() == 0
         d = _compare(eng, lengths, h, rows)
         # K1: CIGAR words -> the same spans
         tid, pos, span = dev_reads

@@ -398,10 +398,10 @@ def test_fused_overlapping_and_high_depth(eng):
         want = coracle.region_stats(d, ext, coff, rt, rs, re_)
         for f in want.dtype.names:
             assert np.array_equal(got[f], want[f]), f
-        if k == 1:
-            assert eng.fused_fallbacks() == 1      # median of [0,120) is > 1024
+        if k == 1:      # median of [0,120) is > 1024: recomputed (device or host K3)
+            assert eng.fused_fallbacks() + eng.fused_recomputes() == 1
         if k == 2:
-            assert eng.fused_fallbacks() == 0
+            assert eng.fused_fallbacks() + eng.fused_recomputes() == 0
 
 
 def test_fused_fixture_goldens(eng, fixture_golden):
@@ -678,11 +678,13 @@ def test_fused_clean_buffers_across_mixed_calls(eng):
     d2, ext2, coff2 = coracle.depth(lengths2, t2, p2, s2)
     regs2 = (np.arange(4, dtype=np.int32), np.zeros(4, np.int64), lengths2)
     want2 = coracle.region_stats(d2, ext2, coff2, *regs2)
-    for _ in range(3):
+    for k in range(3):
         got = eng.compute_depth_stats(*regs2)
         for f in want2.dtype.names:
             assert np.array_equal(got[f], want2[f]), f
-        assert eng.fused_fallbacks() >= 1
+        assert eng.fused_fallbacks() + eng.fused_recomputes() >= 1
+        if k:           # after a call with out-of-window regions: recomputed on the device
+            assert eng.fused_recomputes() >= 1 and eng.fused_fallbacks() == 0
 
 
 def test_invalidate_reprepares_same_reads(eng):
@@ -1188,3 +1190,49 @@ def test_cli_max_depth_option(lib_built, fixture_golden, golden_dir, tmp_path):
     assert r.exit_code == 0, r.output
     with open(out, newline="") as fh:
         assert fh.read() == fixture_golden["csv_blast7"]
+
+
+
+def test_fused_device_recompute(lib_built):
+    """Out-of-window regions recomputed on the device within the fused call
+    (long reads, or after a call that had them): many deep ramped contigs
+    (C5 in miniature), rows exact against the oracle, no host fallback; a
+    depth beyond the device histogram (16384) hands them to the host K3."""
+    rng = np.random.default_rng(77)
+    lengths = rng.integers(20_000, 40_000, size=60).astype(np.int64)
+    w = rng.lognormal(0, 1.2, size=60)
+    n = 400_000
+    tid = np.sort(rng.choice(60, size=n, p=w / w.sum())).astype(np.int32)
+    span = np.minimum(rng.lognormal(np.log(8000), 0.4, size=n).astype(np.int64), lengths[tid]).astype(np.int32)
+    pos = (rng.random(n) * (lengths[tid] - span + 1)).astype(np.int32)
+    o = np.lexsort((pos, tid))
+    tid, pos, span = tid[o], pos[o], span[o]
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    regs = (np.arange(60, dtype=np.int32), np.zeros(60, np.int64), lengths)
+    want = coracle.region_stats(d, ext, coff, *regs)
+    e = CoverageEngine(0)
+    try:
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span)
+        for k in range(3):
+            got = e.compute_depth_stats(*regs)
+            for f in want.dtype.names:
+                assert np.array_equal(got[f], want[f]), (k, f)
+            assert e.fused_fallbacks() == 0          # long reads: the device recomputes
+        assert e.fused_recomputes() > 0, "the case should have out-of-window regions"
+        # depth above 16384 at one spot: the device histogram cannot hold it
+        t2 = np.concatenate([tid, np.zeros(17_000, np.int32)])
+        p2 = np.concatenate([pos, np.full(17_000, 100, np.int32)])
+        s2 = np.concatenate([span, np.full(17_000, 50, np.int32)])
+        o = np.lexsort((p2, t2))
+        t2, p2, s2 = t2[o], p2[o], s2[o]
+        d2, ext2, coff2 = coracle.depth(lengths, t2, p2, s2)
+        want2 = coracle.region_stats(d2, ext2, coff2, *regs)
+        e.clear_reads()
+        e.add_reads(t2, p2, s2)
+        got = e.compute_depth_stats(*regs)
+        for f in want2.dtype.names:
+            assert np.array_equal(got[f], want2[f]), f
+        assert e.max_depth() > 16384 and e.fused_recomputes() == 0 and e.fused_fallbacks() > 0
+    finally:
+        e.close()
