@@ -173,12 +173,33 @@ def load(path=None):
     return _lib
 
 
+def _share_torch_hip_runtime():
+    """Loads PyTorch's bundled HIP runtime (soname libamdhip64.so.7, as the
+    library's own dependency) before the library, so both use one runtime in
+    any import order.  Loaded the other way round, /opt/rocm's runtime came
+    first and a later `import torch` found no device (hipErrorNoDevice) in
+    the same process.  No-op without torch."""
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        hip = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(hip):
+            ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def _open(path, partial=False):
     """partial: an A/B build of an older revision may lack newer entry points."""
     if not os.path.exists(path):
         raise LibraryNotBuilt(
             "%s not found: build it with `python -m metacov_amd.build` "
             "(hipcc --offload-arch=gfx950). metacov_amd has no CPU fallback." % path)
+    _share_torch_hip_runtime()
     lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
         if partial and not hasattr(lib, name):

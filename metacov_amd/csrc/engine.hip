@@ -845,7 +845,7 @@ static int prepare_direct(mc_ctx* ctx) {
 static bool check_direct(mc_ctx* ctx, const unsigned long long* res) {
     const unsigned long long g = ctx->direct_gen;
     if (res[kDresBadSample] == g || res[kDresLongSample] == g || res[kDresFlags]) return false;
-    ctx->aligned_bases = (int64_t)res[kDresBases];
+    ctx->aligned_bases = -1;   // summed on request (direct_bases)
     ctx->direct_checked = true;
     ctx->t.direct_batches += 1;
     ctx->t.prepare_ms = elapsed(ctx, 2, 3);
@@ -1559,11 +1559,30 @@ extern "C" int mc_region_stats(mc_ctx* ctx, int64_t R, const int32_t* tid, const
     return MC_OK;
 }
 
+// The aligned bases of a direct batch K2 accepted: the sum of its spans
+// (span_sum_kernel), once per batch.
+static int direct_bases(mc_ctx* ctx) {
+    hipStream_t s = ctx->stream;
+    const int64_t n = ctx->n_reads;
+    HIP_TRY(hipMemsetAsync(ctx->d_dres.p + kDresBases, 0, 8, s));
+    const int64_t g = std::max<int64_t>(1, std::min<int64_t>(2048, (n / 4 + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(span_sum_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, ctx->d_span.p, n,
+                       ctx->d_dres.p + kDresBases);
+    HIP_TRY(hipGetLastError());
+    unsigned long long v = 0;
+    HIP_TRY(hipMemcpyAsync(&v, ctx->d_dres.p + kDresBases, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ctx->aligned_bases = (int64_t)v;
+    return MC_OK;
+}
+
 extern "C" int mc_aligned_bases(mc_ctx* ctx, int64_t* out) {
     if (int rc = ctx_use(ctx)) return rc;
     MC_REQUIRE(out, MC_E_INVALID, "null out");
     if (ctx->direct && !ctx->direct_checked) invalidate(ctx);   // (only after a failed call)
     if (int rc = mc_prepare(ctx)) return rc;
+    if (ctx->direct && ctx->aligned_bases < 0)
+        if (int rc = direct_bases(ctx)) return rc;
     *out = ctx->aligned_bases;
     return MC_OK;
 }

@@ -532,14 +532,11 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 //                  these ranges partition [0, n) whenever the samples are
 //                  sorted (J is monotone), so every read is checked exactly
 //                  once (range, order against its predecessor, overhang past
-//                  its contig, span <= short_max) and its span summed.
+//                  its contig, span <= short_max).
 // Anything the direct path cannot represent (unsorted or invalid reads, a
 // read past its contig's end, a long read) is reported in DirectRes; the host
 // then re-runs the batch through the full prepare, which raises the exact
 // errors or builds the extents and long-read buckets.
-#ifndef MC_DIRECT_VALIDATE_END
-#define MC_DIRECT_VALIDATE_END 0       // K2 checks a chunk's own reads at the chunk end, not per batch
-#endif
 constexpr int kProbeShift = 8;                 // sample stride S = 256 reads
 constexpr int kProbeStride = 1 << kProbeShift;
 
@@ -549,7 +546,7 @@ enum : int {
     kDresBadSample = 0,      // gen: an unsorted or invalid sample
     kDresLongSample = 1,     // gen: a sampled span > short_max
     kDresFlags = 2,          // K2: kDirectInvalid | kDirectUnfit
-    kDresBases = 3,          // K2: aligned bases
+    kDresBases = 3,          // span_sum_kernel: aligned bases (on request)
     kDresWords = 4
 };
 constexpr unsigned kDirectInvalid = 1;   // an invalid or unsorted read: mc_prepare's error
@@ -1156,7 +1153,7 @@ __device__ __forceinline__ void issue_raw(RawBatch<kDirect>& r, int64_t base, co
         // lane 0's predecessor (the previous wave's last read) comes with the
         // batch: a scalar load of it at the batch advance stalled every batch
         // on an L2 round trip (0.12 ms of a C3 launch)
-        r.pt = -1;
+        r.pt = 0;
         r.pp = 0;
         if ((threadIdx.x & 63) == 0 && i0 > 0 && i0 < cend) {
             r.pt = A.tid[i0 - 1];
@@ -1209,7 +1206,6 @@ struct DirectChunk {                   // wave-uniform per chunk
 
 struct DirectAcc {                     // per-lane verdict
     unsigned flags = 0;                // kDirectInvalid | kDirectUnfit
-    unsigned long long bases = 0;
 };
 
 // Raw tuples: chunk-relative starts (contig offsets and lengths by scalar
@@ -1223,7 +1219,6 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
                                                     int64_t C0, int64_t chunk_w, const DirectChunk& dc,
                                                     const ReadArrays& A, const int64_t* __restrict__ coff,
                                                     const DirectArgs& D, int short_max, DirectAcc& acc) {
-    const int lane = threadIdx.x & 63;
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
     const int tt[4] = {r.t.x, r.t.y, r.t.z, r.t.w};
     const int pp[4] = {r.p.x, r.p.y, r.p.z, r.p.w};
@@ -1246,11 +1241,7 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         const unsigned long long act = __ballot(cand >= 0);
         if (!act) break;
         const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
-#if defined(MC_EXP_NO_LEN) || MC_DIRECT_VALIDATE_END
-        const int64_t c = uload(coff, t0) - C0, ln = 0;
-#else
         const int64_t c = uload(coff, t0) - C0, ln = uload(D.len, t0);
-#endif
         const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -1261,12 +1252,10 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
                 todo &= ~(1u << k);
             }
     }
-    // predecessor of read 0: lane - 1's read 3; lane 0's came with the batch
-    int pt = __shfl_up(tt[3], 1, 64), ppv = __shfl_up(pp[3], 1, 64);
-    if (lane == 0) {
-        pt = r.pt;
-        ppv = r.pp;
-    }
+    // predecessor of read 0: lane - 1's read 3 (DPP wave_shr:1, no LDS
+    // permute); lane 0 keeps its own, which came with the batch
+    const int pt = __builtin_amdgcn_update_dpp(r.pt, tt[3], 0x138, 0xf, 0xf, false);
+    const int ppv = __builtin_amdgcn_update_dpp(r.pp, pp[3], 0x138, 0xf, 0xf, false);
     // 4-bit masks of this lane's reads: in [lo, hi) (applied) and in [vlo,
     // vhi) (checked here), from two 64-bit differences per range
     auto range4 = [&](int64_t lo, int64_t hi) -> unsigned {
@@ -1282,116 +1271,53 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         const bool ok = (valid >> k) & 1u;
         pend |= (ok & (rs[k] < chunk_w) & (sp[k] <= short_max)) ? 1u << k : 0u;
         const int qt = k ? tt[k - 1] : pt, qp = k ? pp[k - 1] : ppv;
-#ifdef MC_EXP_NO_ORDER
-        const bool uns = false;
-        (void)qt; (void)qp;
-#else
-        const bool uns = (qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k]));   // (read 0 of all: pt = -1)
-#endif
+        // (tid, pos) as one unsigned 64-bit key: one compare (3 compares and 2
+        // mask operations as a lexicographic pair: C3 K2 -0.02 ms).  Reads
+        // with a negative field are invalid whatever the order says; the first
+        // read of all has the predecessor (0, 0).
+        const bool uns = (((uint64_t)(unsigned)tt[k] << 32) | (unsigned)pp[k]) <
+                         (((uint64_t)(unsigned)qt << 32) | (unsigned)qp);
         bad |= (!ok | uns) ? 1u << k : 0u;
-#ifdef MC_EXP_NO_LEN
-        unfit |= (sp[k] > short_max) ? 1u << k : 0u;
-#else
         unfit |= ((sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k])) ? 1u << k : 0u;
-#endif
     }
     b.pending = pend & range4(dc.lo, dc.hi);
-#if !(defined(MC_DIRECT_NOCHECK) || MC_DIRECT_VALIDATE_END)
     const unsigned own = range4(dc.vlo, dc.vhi);
     acc.flags |= (bad & own) ? kDirectInvalid : (unfit & own) ? kDirectUnfit : 0u;
-#ifndef MC_EXP_NO_BASES
-    const unsigned keep = own & valid;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc.bases += ((keep >> k) & 1u) ? (unsigned)sp[k] : 0u;
-#endif
-#else
-    (void)bad;
-    (void)unfit;
-#endif
 }
 
-// K2 direct: the per-workgroup verdict into dres (one atomic each)
-__device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArgs& D, long long* red) {
+// K2 direct: the per-workgroup verdict into dres (one atomic, only when a
+// read failed a check).  The aligned bases are not counted here: summing
+// the spans cost 0.03 ms of a C3 launch for a figure few callers ask for
+// (span_sum_kernel computes it on request).
+__device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArgs& D, int* red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned f = a.flags;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) f |= __shfl_xor(f, d, 64);
-    const long long bases = wave_sum64((long long)a.bases);
     __syncthreads();
-    if (lane == 0) {
-        red[wave] = bases;
-        red[kWaves + wave] = f;
-    }
+    if (lane == 0) red[wave] = (int)f;
     __syncthreads();
     if (threadIdx.x == 0) {
-        long long t = 0, ff = 0;
+        unsigned ff = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
-            t += red[w];
-            ff |= red[kWaves + w];
-        }
+        for (int w = 0; w < kWaves; ++w) ff |= (unsigned)red[w];
         if (ff) atomicOr(&D.dres[kDresFlags], (unsigned long long)ff);
-        if (t) atomicAdd(&D.dres[kDresBases], (unsigned long long)t);
     }
 }
 
-// The checks of finish_batch_direct over a chunk's own reads [vlo, vhi), as
-// a loop of its own at the chunk end (the tile registers are dead there).
-__device__ __forceinline__ void validate_own(int64_t vlo, int64_t vhi, const ReadArrays& A,
-                                             const DirectArgs& D, int short_max, DirectAcc& acc) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t b = vlo & ~(int64_t)3; b < vhi; b += kBatch) {
-        const int64_t i0 = b + (int64_t)threadIdx.x * kReadsPerThread;
-        i32x4 t = i32x4{-1, -1, -1, -1}, p = i32x4{0, 0, 0, 0}, sv = i32x4{0, 0, 0, 0};
-        const bool any = i0 < vhi && i0 + 4 >= vlo;   // (the read before vlo: vlo's predecessor)
-        if (any) {
-            t = *reinterpret_cast<const i32x4*>(A.tid + i0);
-            p = *reinterpret_cast<const i32x4*>(A.pos + i0);
-            sv = *reinterpret_cast<const i32x4*>(A.span + i0);
-        }
-        int pt = __shfl_up(t.w, 1, 64), ppv = __shfl_up(p.w, 1, 64);
-        if (lane == 0) {
-            pt = -1;
-            ppv = 0;
-            if (any && i0 > 0) {
-                pt = A.tid[i0 - 1];
-                ppv = A.pos[i0 - 1];
-            }
-        }
-        const int tt[4] = {t.x, t.y, t.z, t.w}, pp[4] = {p.x, p.y, p.z, p.w}, sp[4] = {sv.x, sv.y, sv.z, sv.w};
-        unsigned valid = 0, own = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            valid |= (((unsigned)tt[k] < (unsigned)D.nc) & (pp[k] >= 0) & (sp[k] >= 0)) ? 1u << k : 0u;
-            own |= (i0 + k >= vlo && i0 + k < vhi) ? 1u << k : 0u;
-        }
-        unsigned L[4] = {0, 0, 0, 0};
-        unsigned todo = valid & own;
-        for (;;) {
-            const int cand = (todo & 1u) ? tt[0] : (todo & 2u) ? tt[1] : (todo & 4u) ? tt[2]
-                           : (todo & 8u) ? tt[3] : -1;
-            const unsigned long long act = __ballot(cand >= 0);
-            if (!act) break;
-            const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
-            const int64_t ln = uload(D.len, t0);
-            const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (((todo >> k) & 1u) && tt[k] == t0) {
-                    L[k] = l32;
-                    todo &= ~(1u << k);
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool ok = (valid >> k) & 1u, mine = (own >> k) & 1u;
-            const int qt = k ? tt[k - 1] : pt, qp = k ? pp[k - 1] : ppv;
-            const bool uns = (i0 + k > 0) & ((qt > tt[k]) | ((qt == tt[k]) & (qp > pp[k])));
-            const bool unfit = (sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k]);
-            acc.flags |= mine ? (!ok | uns ? kDirectInvalid : unfit ? kDirectUnfit : 0u) : 0u;
-            acc.bases += (mine & ok) ? (unsigned)sp[k] : 0u;
-        }
+// The aligned bases of a direct batch K2 accepted (every span >= 0): the sum
+// of span[0, n), on request (mc_aligned_bases).
+__global__ void __launch_bounds__(kBlock)
+span_sum_kernel(const int32_t* __restrict__ span, int64_t n, unsigned long long* out) {
+    long long s = 0;
+    const int64_t n4 = n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
+        const i32x4 v = reinterpret_cast<const i32x4*>(span)[i];
+        s += (long long)v.x + v.y + v.z + v.w;
     }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) s += span[(n4 << 2) + threadIdx.x];
+    s = wave_sum64(s);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, (unsigned long long)s);
 }
 
 // Fused region statistics of K2 (optional): non-overlapping regions sorted by
@@ -1967,7 +1893,6 @@ depth_kernel(ReadArrays A, int64_t n,
         if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks);
         for (int k = threadIdx.x * 4; k < kTileW; k += kBlock * 4)
             *reinterpret_cast<i32x4*>(ring + ring_tail + k) = i32x4{0, 0, 0, 0};
-        if (kDirect && MC_DIRECT_VALIDATE_END) validate_own(dc.vlo, dc.vhi, A, D, short_max, dacc);
     }
     // one atomic per workgroup (same-address atomics of every wave at the end of
     // the launch serialise); hdr[8..11] are free once the queue is drained
@@ -1978,7 +1903,7 @@ depth_kernel(ReadArrays A, int64_t n,
         const int m = max(max(hdr[8], hdr[9]), max(hdr[10], hdr[11]));
         if (m > 0) atomicMax(max_depth, m);
     }
-    if (kDirect) direct_flush(dacc, D, reinterpret_cast<long long*>(ring));   // (ring: free now)
+    if (kDirect) direct_flush(dacc, D, ring);   // (ring: free now)
 }
 
 // ----------------------------------------------------------------- K3
