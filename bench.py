@@ -368,7 +368,9 @@ def main():
             kp = [(after["prepare_ms_total"] - before["prepare_ms_total"]) / max(1, n_steps)]
             k1 = [0.0]
         paths = {"direct": after["direct_batches"] - before["direct_batches"],
-                 "full": after["full_prepares"] - before["full_prepares"]}
+                 "full": after["full_prepares"] - before["full_prepares"],
+                 "halo_redos": after["halo_redos"] - before["halo_redos"],
+                 "halo": after["direct_halo"]}
         return el, [float(np.mean(x)) for x in (k2, k3, k1, kp)], paths
 
     # ---- the headline: every step is a fresh batch (prepare inside the step)
@@ -507,7 +509,8 @@ def main():
                                 % (world, "RCCL" if args.backend == "nccl" else "gloo"))
                                if world > 1 else "single GPU",
             },
-            "prepare_path": {"direct_batches": paths["direct"], "full_prepares": paths["full"]},
+            "prepare_path": {"direct_batches": paths["direct"], "full_prepares": paths["full"],
+                             "halo_redos": paths["halo_redos"], "chunk_halo_positions": paths["halo"]},
             "kernels_ms": {**({"k1_cigar_span": k1_ms} if args.cigar else {}),
                            "prepare" + ("_probe" if head_direct else "_ingest_index"): kp_ms,
                            "k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,

@@ -80,6 +80,10 @@ typedef struct mc_timings {
     int64_t direct_batches;
     int64_t full_prepares;
     double prepare_ms_total;       /* every prepare's prepare_ms (direct: the probe) */
+    /* Direct batches redone with a wider halo (their spans outgrew the one
+     * the previous batch set), and the halo (positions) of the last one. */
+    int64_t halo_redos;
+    int64_t direct_halo;
 } mc_timings;
 
 typedef struct mc_ctx mc_ctx;

@@ -54,7 +54,8 @@ class Timings(ctypes.Structure):
                 ("depth_launches", ctypes.c_int64), ("stats_launches", ctypes.c_int64),
                 ("fused_depth_ms_total", ctypes.c_double), ("fused_stats_ms_total", ctypes.c_double),
                 ("fused_calls", ctypes.c_int64), ("direct_batches", ctypes.c_int64),
-                ("full_prepares", ctypes.c_int64), ("prepare_ms_total", ctypes.c_double)]
+                ("full_prepares", ctypes.c_int64), ("prepare_ms_total", ctypes.c_double),
+                ("halo_redos", ctypes.c_int64), ("direct_halo", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p

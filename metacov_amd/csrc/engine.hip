@@ -180,7 +180,12 @@ struct mc_ctx {
     bool direct_enabled = true;
     bool direct_retry_full = false;       // the batch K2 just refused goes to mc_prepare
     unsigned long long direct_gen = 0;
-    DevBuf<int32_t> d_jidx;               // [2 * (n_base + 1)]: J(k w), J(k w - short_max)
+    // halo of the next direct batch (0: short_max): the previous batch's
+    // maximum span and 1/8 more, so a chunk loads the reads starting up to
+    // that far before it instead of short_max (C3: 4096 -> ~2400 positions)
+    int direct_halo = 0;
+    int direct_halo_used = 0;
+    DevBuf<int32_t> d_jidx;               // [2 * (n_base + 1)]: J(k w), J(k w - halo)
     DevBuf<int32_t> d_fsamp;              // [nc + 1] first sample of each contig
     DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
     int32_t max_span = 0;
@@ -819,8 +824,9 @@ static int prepare_direct(mc_ctx* ctx) {
     }
     // (K2's whole-batch loads read up to 3 reads of padding past n; the
     // direct K2 neither applies nor checks reads at or past n)
+    ctx->direct_halo_used = ctx->direct_halo > 0 ? std::min(ctx->direct_halo, ctx->short_max) : ctx->short_max;
     ProbeArgs P{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_coff.p, base_lw(ctx),
-                ctx->short_max, n_base, ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_fsamp.p,
+                ctx->short_max, ctx->direct_halo_used, n_base, ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_fsamp.p,
                 ctx->d_dres.p, ++ctx->direct_gen};
     const int64_t M = (n + kProbeStride - 1) >> kProbeShift;
     hipLaunchKernelGGL(probe_kernel, dim3((unsigned)std::max<int64_t>(1, (M + kBlock - 1) / kBlock)),
@@ -842,9 +848,18 @@ static int prepare_direct(mc_ctx* ctx) {
 // K2's verdict on a direct batch (res: a host copy of d_dres).  True: the
 // batch is exactly what the direct path computed (the counts become the
 // prepare's results); false: direct_fallback + mc_prepare must redo it.
+static int next_halo(unsigned long long max_span, int short_max) {
+    const long long h = round_up((long long)max_span + (long long)max_span / 8, 64);
+    return (int)std::max<long long>(64, std::min<long long>(h, short_max));
+}
+
 static bool check_direct(mc_ctx* ctx, const unsigned long long* res) {
     const unsigned long long g = ctx->direct_gen;
-    if (res[kDresBadSample] == g || res[kDresLongSample] == g || res[kDresFlags]) return false;
+    if (res[kDresBadSample] == g || res[kDresLongSample] == g || res[kDresFlags] ||
+        res[kDresMaxSpan] > (unsigned long long)ctx->direct_halo_used)
+        return false;
+    ctx->max_span = (int32_t)res[kDresMaxSpan];
+    ctx->direct_halo = next_halo(res[kDresMaxSpan], ctx->short_max);
     ctx->aligned_bases = -1;   // summed on request (direct_bases)
     ctx->direct_checked = true;
     ctx->t.direct_batches += 1;
@@ -856,11 +871,19 @@ static bool check_direct(mc_ctx* ctx, const unsigned long long* res) {
 
 // A batch the direct path cannot represent: long reads or reads past their
 // contig's end keep this contig set on the full prepare from now on; invalid
-// or unsorted reads only get mc_prepare's exact error.
+// or unsorted reads only get mc_prepare's exact error.  A batch whose spans
+// only outgrew the halo is redone on the direct path with a halo that covers
+// its (now known) maximum span.
 static void direct_fallback(mc_ctx* ctx, const unsigned long long* res) {
     const unsigned long long g = ctx->direct_gen;
-    if (res[kDresLongSample] == g || (res[kDresFlags] & kDirectUnfit)) ctx->direct_ok = false;
-    ctx->direct_retry_full = true;
+    const bool long_reads = res[kDresLongSample] == g || res[kDresMaxSpan] > (unsigned long long)ctx->short_max;
+    if (long_reads || (res[kDresFlags] & kDirectUnfit)) ctx->direct_ok = false;
+    if (long_reads || res[kDresBadSample] == g || res[kDresFlags]) {
+        ctx->direct_retry_full = true;
+    } else {
+        ctx->direct_halo = next_halo(res[kDresMaxSpan], ctx->short_max);
+        ctx->t.halo_redos += 1;
+    }
     ctx->fused_clean = false;
     invalidate(ctx);
 }
@@ -975,20 +998,21 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
 
 extern "C" int mc_compute_depth(mc_ctx* ctx) {
     if (int rc = ctx_use(ctx)) return rc;
-    if (int rc = prepare_for_compute(ctx)) return rc;
-    FusedRegions none{};
-    if (int rc = launch_depth(ctx, none)) return rc;
-    if (ctx->direct && !ctx->direct_checked) {   // K2's verdict on the batch
-        unsigned long long* res = static_cast<unsigned long long*>(ctx->pin_io.h);
+    // a direct batch K2 refuses is redone: on the direct path with a wider
+    // halo, else on the full prepare (which K2 does not refuse)
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        if (int rc = prepare_for_compute(ctx)) return rc;
+        FusedRegions none{};
+        if (int rc = launch_depth(ctx, none)) return rc;
+        if (!ctx->direct || ctx->direct_checked) return MC_OK;
+        unsigned long long* res = static_cast<unsigned long long*>(ctx->pin_io.h);   // K2's verdict
         HIP_TRY(hipMemcpyAsync(res, ctx->d_dres.p, kDresWords * 8, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
-        if (!check_direct(ctx, res)) {
-            direct_fallback(ctx, res);
-            if (int rc = mc_prepare(ctx)) return rc;
-            return launch_depth(ctx, none);
-        }
+        if (check_direct(ctx, res)) return MC_OK;
+        direct_fallback(ctx, res);
     }
-    return MC_OK;
+    MC_REQUIRE(false, MC_E_STATE, "direct prepare refused three times");
+    return MC_E_STATE;
 }
 
 static int fetch_max_depth(mc_ctx* ctx) {
@@ -1498,8 +1522,9 @@ static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
 static int depth_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
                             const int64_t* end, RegionOut* d_out) {
     int rc = depth_stats_once(ctx, R, tid, start, end, d_out);
-    if (rc == kRedo) rc = depth_stats_once(ctx, R, tid, start, end, d_out);   // now on the full prepare
-    MC_REQUIRE(rc != kRedo, MC_E_STATE, "direct prepare fell back twice");
+    // redone on the direct path with a wider halo, or on the full prepare
+    for (int k = 0; k < 2 && rc == kRedo; ++k) rc = depth_stats_once(ctx, R, tid, start, end, d_out);
+    MC_REQUIRE(rc != kRedo, MC_E_STATE, "direct prepare refused three times");
     return rc;
 }
 
@@ -1599,6 +1624,7 @@ extern "C" int mc_get_timings(mc_ctx* ctx, mc_timings* out) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (ctx->t_depth) ctx->t.depth_ms = elapsed(ctx, 4, 5);
     if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, ctx->stats_after_depth ? 5 : 6, 7);
+    ctx->t.direct_halo = ctx->direct_halo_used;
     *out = ctx->t;
     return MC_OK;
 }

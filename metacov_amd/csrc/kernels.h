@@ -547,10 +547,11 @@ enum : int {
     kDresLongSample = 1,     // gen: a sampled span > short_max
     kDresFlags = 2,          // K2: kDirectInvalid | kDirectUnfit
     kDresBases = 3,          // span_sum_kernel: aligned bases (on request)
-    kDresWords = 4
+    kDresMaxSpan = 4,        // K2: the batch's maximum span (atomicMax per workgroup)
+    kDresWords = 5
 };
 constexpr unsigned kDirectInvalid = 1;   // an invalid or unsorted read: mc_prepare's error
-constexpr unsigned kDirectUnfit = 2;     // a long read or one past its contig's end
+constexpr unsigned kDirectUnfit = 2;     // a read past its contig's end (long reads: kDresMaxSpan)
 
 struct ProbeArgs {
     const int32_t* tid;
@@ -561,9 +562,10 @@ struct ProbeArgs {
     const int64_t* coff;               // [nc + 1] layout from the contig lengths
     int lw;                            // grid step w = 2^lw (the plain K2's chunks)
     int short_max;
+    int halo;                          // <= short_max: the batch's spans are taken to be <= halo
     int64_t n_base;                    // grid targets k = 0 .. n_base
     int32_t* j0;                       // [n_base + 1] J(k * w)
-    int32_t* jh;                       // [n_base + 1] J(k * w - short_max)
+    int32_t* jh;                       // [n_base + 1] J(k * w - halo)
     int32_t* fsamp;                    // [nc + 1] first sample of contig t
     unsigned long long* dres;
     unsigned long long gen;
@@ -618,7 +620,7 @@ probe_kernel(ProbeArgs A) {
     if (s > A.short_max) atomicMax(&A.dres[kDresLongSample], A.gen);
     const bool first = j == 0;
     probe_fill(A.j0, A.n_base, A.lw, 0, key, key_next, first, last, (int32_t)(j + 1));
-    probe_fill(A.jh, A.n_base, A.lw, A.short_max, key, key_next, first, last, (int32_t)(j + 1));
+    probe_fill(A.jh, A.n_base, A.lw, A.halo, key, key_next, first, last, (int32_t)(j + 1));
     // contigs (tid_j, tid_next] start after sample j
     const int ct = t < 0 ? 0 : t >= A.nc ? A.nc - 1 : t;
     const int cn = last ? A.nc : (t_next < 0 ? 0 : t_next >= A.nc ? A.nc - 1 : t_next);
@@ -1192,7 +1194,7 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch<false>
 // Direct path (see probe_kernel): K2's own view of the batch and what it checks.
 struct DirectArgs {
     const int32_t* j0;                 // [n_base + 1] J(k * w)       (probe_kernel)
-    const int32_t* jh;                 // [n_base + 1] J(k * w - short_max)
+    const int32_t* jh;                 // [n_base + 1] J(k * w - halo)
     const int64_t* len;                // [nc] contig lengths (= extents on this path)
     int32_t nc;
     unsigned long long* dres;
@@ -1206,6 +1208,7 @@ struct DirectChunk {                   // wave-uniform per chunk
 
 struct DirectAcc {                     // per-lane verdict
     unsigned flags = 0;                // kDirectInvalid | kDirectUnfit
+    int max_span = 0;                  // over the valid reads loaded for [lo, hi)
 };
 
 // Raw tuples: chunk-relative starts (contig offsets and lengths by scalar
@@ -1278,9 +1281,16 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         const bool uns = (((uint64_t)(unsigned)tt[k] << 32) | (unsigned)pp[k]) <
                          (((uint64_t)(unsigned)qt << 32) | (unsigned)qp);
         bad |= (!ok | uns) ? 1u << k : 0u;
-        unfit |= ((sp[k] > short_max) | ((unsigned)pp[k] + (unsigned)sp[k] > L[k])) ? 1u << k : 0u;
+        unfit |= ((unsigned)pp[k] + (unsigned)sp[k] > L[k]) ? 1u << k : 0u;
     }
-    b.pending = pend & range4(dc.lo, dc.hi);
+    const unsigned inr = range4(dc.lo, dc.hi);
+    b.pending = pend & inr;
+    // the batch's maximum span (every read is loaded by the chunk it belongs
+    // to, so the maximum over the workgroups is exact): the host takes long
+    // reads (> short_max) to the full prepare and sizes the next batch's halo
+    const unsigned mm = valid & inr;
+    acc.max_span = max(acc.max_span, max(max((mm & 1u) ? sp[0] : 0, (mm & 2u) ? sp[1] : 0),
+                                         max((mm & 4u) ? sp[2] : 0, (mm & 8u) ? sp[3] : 0)));
     const unsigned own = range4(dc.vlo, dc.vhi);
     acc.flags |= (bad & own) ? kDirectInvalid : (unfit & own) ? kDirectUnfit : 0u;
 }
@@ -1292,16 +1302,28 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
 __device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArgs& D, int* red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned f = a.flags;
+    int m = a.max_span;
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) f |= __shfl_xor(f, d, 64);
+    for (int d = 32; d > 0; d >>= 1) {
+        f |= __shfl_xor(f, d, 64);
+        m = max(m, __shfl_xor(m, d, 64));
+    }
     __syncthreads();
-    if (lane == 0) red[wave] = (int)f;
+    if (lane == 0) {
+        red[wave] = (int)f;
+        red[kWaves + wave] = m;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned ff = 0;
+        int mm = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) ff |= (unsigned)red[w];
+        for (int w = 0; w < kWaves; ++w) {
+            ff |= (unsigned)red[w];
+            mm = max(mm, red[kWaves + w]);
+        }
         if (ff) atomicOr(&D.dres[kDresFlags], (unsigned long long)ff);
+        if (mm > 0) atomicMax(&D.dres[kDresMaxSpan], (unsigned long long)mm);
     }
 }
 

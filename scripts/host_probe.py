@@ -42,8 +42,9 @@ def main():
         table = torch.empty((R, 9), dtype=torch.int64, device=dev)
         for _ in range(3):
             e.compute_depth_stats_device(rt, rs, re_, table.data_ptr())
-        rows = {"call (cached regions)": [], "invalidate+prepare": [], "call after prepare": []}
-        kern = {"call (cached regions)": [], "invalidate+prepare": [], "call after prepare": []}
+        keys = ["call (cached regions)", "invalidate+prepare", "call after prepare", "direct fresh call"]
+        rows = {k: [] for k in keys}
+        kern = {k: [] for k in keys}
         for _ in range(a.reps):
             t0 = e.timings()
             w0 = time.perf_counter()
@@ -67,6 +68,17 @@ def main():
             rows["call after prepare"].append((w1 - w0) * 1e3)
             kern["call after prepare"].append((t1["fused_depth_ms_total"] - t0["fused_depth_ms_total"]) +
                                               (t1["fused_stats_ms_total"] - t0["fused_stats_ms_total"]))
+            # a fresh batch on the direct path: probe + window + validating K2 + K3b
+            t0 = e.timings()
+            w0 = time.perf_counter()
+            e.invalidate()
+            e.compute_depth_stats_device(rt, rs, re_, table.data_ptr())
+            w1 = time.perf_counter()
+            t1 = e.timings()
+            assert t1["direct_batches"] == t0["direct_batches"] + 1
+            rows["direct fresh call"].append((w1 - w0) * 1e3)
+            kern["direct fresh call"].append(sum(t1[k] - t0[k] for k in (
+                "fused_depth_ms_total", "fused_stats_ms_total", "prepare_ms_total")))
         for k in rows:
             w, g = np.median(rows[k]), np.median(kern[k])
             name = os.path.basename(lib or "libmetacov_amd.so")

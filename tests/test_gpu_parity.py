@@ -1002,6 +1002,7 @@ def test_library_then_torch_same_process():
         "e = CoverageEngine(0)\n"
         "e.set_contigs(np.array([1000], np.int64))\n"
         "e.add_reads(np.zeros(3, np.int32), np.array([1, 5, 9], np.int32), np.array([10, 10, 10], np.int32))\n"
+        "e.compute_depth()\n"
         "d = e.depth(0, 0, 20)\n"
         "import torch\n"
         "assert torch.cuda.is_available()\n"
@@ -1148,6 +1149,44 @@ def test_direct_sparse_and_empty_contigs(lib_built):
         p = (rng.random(n) * (lengths[t] - sp + 1)).astype(np.int32)
         o = np.lexsort((p, t))
         _direct_case(lib_built, lengths, t[o], p[o], sp[o], expect_direct=True)
+
+
+def test_direct_halo_follows_the_spans(lib_built):
+    """The chunk halo of a direct batch is the previous batch's maximum span
+    (+1/8): a batch with a longer read than that (3000 bp crossing a chunk
+    boundary from 1000 before it) is redone on the direct path with a halo
+    that covers it, exactly, for the plain and the fused K2; no full prepare."""
+    lengths, tid, pos, span = make_case([400_000], 20_000, (1, 150), 46, overhang=False)
+    t2 = np.append(tid, np.int32(0))
+    p2 = np.append(pos, np.int32(131_072 - 1000))
+    s2 = np.append(span, np.int32(3000))
+    o = np.lexsort((p2, t2))
+    t2, p2, s2 = t2[o], p2[o], s2[o]
+    rt, rs, re_ = np.zeros(1, np.int32), np.zeros(1, np.int64), np.asarray(lengths, np.int64)
+    e = _fresh(lib_built)
+    try:
+        e.set_contigs(lengths)
+        for k, fused in enumerate((False, True)):
+            e.clear_reads()
+            e.add_reads(tid, pos, span)          # max span 150: the next halo is 192
+            e.compute_depth()
+            assert e.timings()["halo_redos"] == k
+            e.clear_reads()
+            e.add_reads(t2, p2, s2)
+            if fused:
+                d, ext, coff = coracle.depth(lengths, t2, p2, s2)
+                want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+                got = e.compute_depth_stats(rt, rs, re_)
+                for f in want.dtype.names:
+                    assert np.array_equal(got[f], want[f]), f
+            else:
+                e.compute_depth()
+            check_depth_vs_oracle(e, lengths, t2, p2, s2)
+            t = e.timings()
+            assert t["halo_redos"] == k + 1 and t["direct_halo"] >= 3000, t
+            assert t["full_prepares"] == 0 and t["direct_batches"] == 2 * (k + 1), t
+    finally:
+        e.close()
 
 
 def test_direct_ctx_sticks_to_full_after_long_reads(lib_built):
