@@ -259,12 +259,29 @@ struct mc_ctx {
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
+    // The fused call's events, one set per call in a ring (prep start, K2
+    // start, K2 end, K3b end): a call's elapsed times are read once the next
+    // call has issued its launches, while the GPU runs them, not between the
+    // two (3 x ~2.5 us there).  At most the previous call's set is pending.
+    struct TimingSet {
+        hipEvent_t e[4] = {};
+        bool prep = false;      // e[0] was recorded (a direct prepare)
+        bool pending = false;   // not yet added to t
+    };
+    static constexpr int kTimingSets = 4;
+    TimingSet ts[kTimingSets];
+    int ts_cur = 0;
+    // completion stamp: the stream writes done_seq into mapped host memory
+    // after a fused call's last kernel, and the host spins on it (a stream
+    // synchronize woke ~10 us after the last kernel's end)
+    HostMapped<unsigned long long> h_done;
+    unsigned long long done_seq = 0;
+    bool stamp_ok = true;
     int ingest_grid = 0;                  // resident ingest workgroups
     int k2_resident[6] = {};              // resident K2 workgroups (plain, fused) x (short, long, direct)
     size_t k2_resident_lds[6] = {};
     mc_timings t{};
     bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
-    bool stats_after_depth = false;       // the statistics span starts at ev[5] (fused call)
 };
 
 static int ctx_use(mc_ctx* ctx) {
@@ -300,6 +317,8 @@ extern "C" int mc_ctx_create(int device, mc_ctx** out) {
     }
     c->own_stream = true;
     for (auto& ev : c->ev) (void)hipEventCreate(&ev);
+    for (auto& T : c->ts)
+        for (auto& ev : T.e) (void)hipEventCreate(&ev);
     if (c->d_scratch.reserve(8) != hipSuccess || c->d_queue.reserve(8) != hipSuccess ||
         c->d_maxdepth.reserve(4) != hipSuccess) {
         mc_ctx_destroy(c);
@@ -353,6 +372,10 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_fb_cnt.release();
     for (auto ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& T : ctx->ts)
+        for (auto ev : T.e)
+            if (ev) (void)hipEventDestroy(ev);
+    ctx->h_done.release();
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MC_OK;
@@ -551,10 +574,32 @@ extern "C" int mc_clear_reads(mc_ctx* ctx) {
     return MC_OK;
 }
 
-static float elapsed(mc_ctx* ctx, int a, int b) {
+static float elapsed(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]) != hipSuccess) return 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
     return ms;
+}
+
+static float elapsed(mc_ctx* ctx, int a, int b) { return elapsed(ctx->ev[a], ctx->ev[b]); }
+
+// Adds the pending fused calls' event times to t (oldest first; the current
+// set only with `all`, after the stream has drained).
+static void resolve_timings(mc_ctx* ctx, bool all) {
+    for (int i = 1; i <= mc_ctx::kTimingSets; ++i) {
+        const int k = (ctx->ts_cur + i) % mc_ctx::kTimingSets;
+        auto& T = ctx->ts[k];
+        if (!T.pending || (k == ctx->ts_cur && !all)) continue;
+        const float a = elapsed(T.e[1], T.e[2]), b = elapsed(T.e[2], T.e[3]);
+        ctx->t.fused_depth_ms_total += a;
+        ctx->t.fused_stats_ms_total += b;
+        ctx->t.depth_ms = a;
+        ctx->t.stats_ms = b;
+        if (T.prep) {
+            ctx->t.prepare_ms = elapsed(T.e[0], T.e[1]);
+            ctx->t.prepare_ms_total += ctx->t.prepare_ms;
+        }
+        T.prep = T.pending = false;
+    }
 }
 
 // ---- layout for given extents: contig offsets and chunk geometry.  One
@@ -807,7 +852,10 @@ static int prepare_direct(mc_ctx* ctx) {
     const int64_t n = ctx->n_reads;
     hipStream_t s = ctx->stream;
     if (int rc = run_k1(ctx)) return rc;
-    HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    // the prepare's span: this event to K2's start event (probe + window)
+    auto& T = ctx->ts[ctx->ts_cur];
+    HIP_TRY(hipEventRecord(T.e[0], s));
+    T.prep = true;
     ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
     const size_t n_res = 8 + 2 * (size_t)nc;   // (pin_io's layout, shared with mc_prepare)
@@ -832,7 +880,6 @@ static int prepare_direct(mc_ctx* ctx) {
     hipLaunchKernelGGL(probe_kernel, dim3((unsigned)std::max<int64_t>(1, (M + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, s, P);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev[3], s));
     HIP_TRY(ctx->d_depth.reserve((size_t)(ctx->n_chunks * ctx->chunk_w)));
     ctx->has_long = false;
     ctx->max_span = 0;
@@ -853,7 +900,9 @@ static int next_halo(unsigned long long max_span, int short_max) {
     return (int)std::max<long long>(64, std::min<long long>(h, short_max));
 }
 
-static bool check_direct(mc_ctx* ctx, const unsigned long long* res) {
+// deferred: the fused call adds the prepare's time with its other event
+// times (resolve_timings); otherwise it is read here (K2 start = ev[4]).
+static bool check_direct(mc_ctx* ctx, const unsigned long long* res, bool deferred = false) {
     const unsigned long long g = ctx->direct_gen;
     if (res[kDresBadSample] == g || res[kDresLongSample] == g || res[kDresFlags] ||
         res[kDresMaxSpan] > (unsigned long long)ctx->direct_halo_used)
@@ -863,8 +912,12 @@ static bool check_direct(mc_ctx* ctx, const unsigned long long* res) {
     ctx->aligned_bases = -1;   // summed on request (direct_bases)
     ctx->direct_checked = true;
     ctx->t.direct_batches += 1;
-    ctx->t.prepare_ms = elapsed(ctx, 2, 3);
-    ctx->t.prepare_ms_total += ctx->t.prepare_ms;
+    auto& T = ctx->ts[ctx->ts_cur];
+    if (!deferred && T.prep) {
+        ctx->t.prepare_ms = elapsed(T.e[0], ctx->ev[4]);
+        ctx->t.prepare_ms_total += ctx->t.prepare_ms;
+        T.prep = false;
+    }
     ctx->t.cigar_ms = ctx->t_cigar ? elapsed(ctx, 0, 1) : 0.f;
     return true;
 }
@@ -937,7 +990,9 @@ static K2Geom k2_geom(const mc_ctx* ctx, bool stats) {
 }
 
 // K2 launch (plain or with fused region statistics)
-static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
+// ea / eb: K2's start / end events (default ev[4] / ev[5], read lazily by
+// mc_get_timings)
+static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     hipStream_t s = ctx->stream;
     const bool stats = fr.n > 0;
     const size_t lds = (size_t)(kLdsHeader + ctx->ring +
@@ -964,7 +1019,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 32, s));
         HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
     }
-    HIP_TRY(hipEventRecord(ctx->ev[4], s));
+    HIP_TRY(hipEventRecord(ea ? ea : ctx->ev[4], s));
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
@@ -988,8 +1043,8 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr) {
     }
 #undef MC_LAUNCH_K2
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev[5], s));
-    ctx->t_depth = true;
+    HIP_TRY(hipEventRecord(eb ? eb : ctx->ev[5], s));
+    ctx->t_depth = ea == nullptr;   // else the caller's set carries the time
     ctx->t.depth_launches += 1;
     ctx->depth_valid = true;
     ctx->max_depth = -1;   // read lazily
@@ -1094,10 +1149,7 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
     const int64_t max_hist = int64_t(1) << 28;
     const int64_t rb = std::max<int64_t>(1, std::min<int64_t>(R, max_hist / nbins));
     const bool lds_hist = nbins <= kLdsBins;
-    if (!out_rows) {   // (a fallback extends the fused K3b span)
-        HIP_TRY(hipEventRecord(ctx->ev[6], s));
-        ctx->stats_after_depth = false;
-    }
+    HIP_TRY(hipEventRecord(ctx->ev[6], s));   // (a fallback's time is added to the fused K3b's)
     int64_t launches = 0;
     for (int64_t r0 = 0; r0 < R; r0 += rb) {
         const int64_t nr = std::min(rb, R - r0);
@@ -1252,6 +1304,25 @@ static int direct_verdict_sync(mc_ctx* ctx) {
 
 // The launches of a fused call whose region arrays are staged in
 // ctx->fstage (just now, or by an identical earlier call).
+// Waits until the stream has written stamp `seq` (spinning on mapped host
+// memory; a stream query every ~1k spins reports a failed stream), or, where
+// the stream cannot write stamps, for the stream to drain.
+static int wait_stamp(mc_ctx* ctx, unsigned long long seq) {
+    if (!ctx->stamp_ok) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        return MC_OK;
+    }
+    for (unsigned k = 1;; ++k) {
+        if (__atomic_load_n(ctx->h_done.h, __ATOMIC_ACQUIRE) >= seq) return MC_OK;
+        __builtin_ia32_pause();
+        if ((k & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(ctx->stream);
+            if (e == hipSuccess) return MC_OK;
+            if (e != hipErrorNotReady) HIP_TRY(e);
+        }
+    }
+}
+
 static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
                               const int64_t* end, RegionOut* d_out, int64_t nf) {
     hipStream_t s = ctx->stream;
@@ -1296,9 +1367,9 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                     ctx->d_fhist.p,
                     ctx->d_flow.p};
     if (nf == 0) fr.n = 0;
-    if (int rc = launch_depth(ctx, fr)) return rc;
+    auto& T = ctx->ts[ctx->ts_cur];
+    if (int rc = launch_depth(ctx, fr, T.e[1], T.e[2])) return rc;
     // K3b: its span is timed from K2's end event (one event fewer per call)
-    ctx->stats_after_depth = true;
     // the device-side recompute of out-of-window regions: on for long reads
     // (deep contigs with long end ramps) and after a call that had them
     const bool devfb = ctx->has_long || ctx->fb_recent;
@@ -1352,16 +1423,33 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         hipLaunchKernelGGL(fb_final_kernel, dim3(kFbSlots), dim3(kBlock), 0, s, F);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(ctx->ev[7], s));
-    ctx->t_stats = true;
+    HIP_TRY(hipEventRecord(T.e[3], s));
+    ctx->t_stats = false;
     ctx->t.stats_launches += 1;
-    // the flags are in host memory once the stream has drained (no copy command)
-    HIP_TRY(hipStreamSynchronize(s));
+    // the flags are in host memory once the stream has passed K3b (no copy
+    // command): the completion stamp after it, while the previous call's
+    // event times are read
+    const unsigned long long seq = ++ctx->done_seq;
+    if (ctx->stamp_ok) {
+        if (!ctx->h_done.h) {
+            HIP_TRY(ctx->h_done.reserve(1));
+            __atomic_store_n(ctx->h_done.h, 0ull, __ATOMIC_RELEASE);
+        }
+        if (hipStreamWriteValue64(s, ctx->h_done.d, seq, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->stamp_ok = false;
+        }
+    }
+    resolve_timings(ctx, false);
+    if (int rc = wait_stamp(ctx, seq)) return rc;
     const int* flags = ctx->h_fflag.h;
-    if (verdict && !check_direct(ctx, fflag_dres(ctx->h_fflag.h, R))) {
+    if (verdict && !check_direct(ctx, fflag_dres(ctx->h_fflag.h, R), true)) {
         direct_fallback(ctx, fflag_dres(ctx->h_fflag.h, R));
+        T.prep = T.pending = false;   // the redo records this set again
         return kRedo;
     }
+    T.pending = true;
+    ctx->ts_cur = (ctx->ts_cur + 1) % mc_ctx::kTimingSets;
     ctx->max_depth = flags[R];   // a fallback's K3 sizes its histogram by it
     int64_t n_flag = 0;
     for (int64_t r = 0; r < R; ++r) n_flag += flags[r] ? 1 : 0;
@@ -1389,12 +1477,10 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         if (int rc = region_stats_impl(ctx, (int64_t)ft.size(), ft.data(), fs.data(), fe.data(),
                                        d_out, fr_idx.data()))
             return rc;
+        // the fallback recorded ev[6] / ev[7] around its launches and synced
+        HIP_TRY(hipEventSynchronize(ctx->ev[7]));
+        ctx->t.fused_stats_ms_total += elapsed(ctx, 6, 7);
     }
-    // the stream has drained up to the flags; a fallback recorded ev[7] after
-    // its own last sync
-    if (!ft.empty()) HIP_TRY(hipEventSynchronize(ctx->ev[7]));
-    ctx->t.fused_depth_ms_total += elapsed(ctx, 4, 5);
-    ctx->t.fused_stats_ms_total += elapsed(ctx, 5, 7);
     ctx->t.fused_calls += 1;
     return MC_OK;
 }
@@ -1622,8 +1708,9 @@ extern "C" int mc_get_timings(mc_ctx* ctx, mc_timings* out) {
     if (int rc = ctx_use(ctx)) return rc;
     MC_REQUIRE(out, MC_E_INVALID, "null out");
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    resolve_timings(ctx, true);
     if (ctx->t_depth) ctx->t.depth_ms = elapsed(ctx, 4, 5);
-    if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, ctx->stats_after_depth ? 5 : 6, 7);
+    if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, 6, 7);
     ctx->t.direct_halo = ctx->direct_halo_used;
     *out = ctx->t;
     return MC_OK;

@@ -1487,11 +1487,16 @@ __device__ __forceinline__ void ov_reg_spill(OvReg& r, OvLds* ovf) {
 static_assert(kRing == 2 * kTileW, "the ring tail is one tile (short_max = kTileW)");
 
 // Histogram of 4 consecutive positions (y < 0: outside the region, skipped):
-// one LDS atomic per run of equal values, branch-free (every slot issues its
-// atomic; lanes with nothing to add put 0 into their own pad slot `dummy`:
-// the predicated form cost ~6 SALU exec-mask instructions per atomic, and the
-// fused K2 is bound by instruction issue, not by LDS), and the rare
-// out-of-window path (same run arithmetic as region_seg_kernel).
+// one LDS atomic per run of equal values, branch-free: every slot issues its
+// atomic, and a slot that is no run start, or whose value is outside the
+// window, adds into the lane's own pad slot `dummy` (>= kWinBins), so its
+// address is one unsigned min (y < 0 and values below the window wrap to
+// large unsigned bins).  The predicated form cost ~6 SALU exec-mask
+// instructions per atomic; testing in-window and in-region per slot before
+// the atomic cost twice the VALU of this form.  The rare out-of-window path
+// (any bin >= kWinBins in the wave: window misses, or positions outside the
+// region) classifies the runs exactly (same run arithmetic as
+// region_seg_kernel).
 template <int kWinBins>
 __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, int y0, int y1, int y2, int y3,
                                           int base) {
@@ -1499,21 +1504,20 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, in
     const int l2 = s3 ? 1 : 2;
     const int l1 = s2 ? 1 : l2 + 1;
     const int l0 = s1 ? 1 : l1 + 1;
-    const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
     constexpr unsigned kWin = (unsigned)kWinBins;
+    const unsigned du = (unsigned)dummy;
     const unsigned d0 = (unsigned)(y0 - base), d1 = (unsigned)(y1 - base),
                    d2 = (unsigned)(y2 - base), d3 = (unsigned)(y3 - base);
-    const bool w0 = e0 && d0 < kWin, w1 = e1 && d1 < kWin, w2 = e2 && d2 < kWin, w3 = e3 && d3 < kWin;
-    atomicAdd(&h[w0 ? (int)d0 : dummy], w0 ? (unsigned)l0 : 0u);
-    atomicAdd(&h[w1 ? (int)d1 : dummy], w1 ? (unsigned)l1 : 0u);
-    atomicAdd(&h[w2 ? (int)d2 : dummy], w2 ? (unsigned)l2 : 0u);
-    atomicAdd(&h[w3 ? (int)d3 : dummy], w3 ? 1u : 0u);
-    const bool o0 = e0 && !w0, o1 = e1 && !w1, o2 = e2 && !w2, o3 = e3 && !w3;
-    if (__builtin_expect(__any(o0 || o1 || o2 || o3), 0)) {
-        ov_reg_take(ovr, o0, y0, l0, base);
-        ov_reg_take(ovr, o1, y1, l1, base);
-        ov_reg_take(ovr, o2, y2, l2, base);
-        ov_reg_take(ovr, o3, y3, 1, base);
+    atomicAdd(&h[min(d0, du)], (unsigned)l0);
+    atomicAdd(&h[s1 ? min(d1, du) : du], (unsigned)l1);
+    atomicAdd(&h[s2 ? min(d2, du) : du], (unsigned)l2);
+    atomicAdd(&h[s3 ? min(d3, du) : du], 1u);
+    if (__builtin_expect(__any(max(max(d0, d1), max(d2, d3)) >= kWin), 0)) {
+        const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
+        ov_reg_take(ovr, e0 && d0 >= kWin, y0, l0, base);
+        ov_reg_take(ovr, e1 && d1 >= kWin, y1, l1, base);
+        ov_reg_take(ovr, e2 && d2 >= kWin, y2, l2, base);
+        ov_reg_take(ovr, e3 && d3 >= kWin, y3, 1, base);
     }
 }
 
