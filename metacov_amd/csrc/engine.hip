@@ -189,6 +189,7 @@ struct mc_ctx {
     DevBuf<int32_t> d_fsamp;              // [nc + 1] first sample of each contig
     DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
     int32_t max_span = 0;
+    bool long_hint = false;               // the last full prepare of this contig set had long reads
     int64_t aligned_bases = 0;
     int ring = 0;                 // LDS ring ints
     int tiles_per_chunk = 16;
@@ -277,7 +278,7 @@ struct mc_ctx {
     HostMapped<unsigned long long> h_done;
     unsigned long long done_seq = 0;
     bool stamp_ok = true;
-    int ingest_grid = 0;                  // resident ingest workgroups
+    int ingest_grid[2] = {0, 0};          // resident ingest workgroups (without / with long counting)
     int k2_resident[6] = {};              // resident K2 workgroups (plain, fused) x (short, long, direct)
     size_t k2_resident_lds[6] = {};
     mc_timings t{};
@@ -409,6 +410,7 @@ extern "C" int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths) {
                    "contig %d: bad length %lld", i, (long long)lengths[i]);
     ctx->len.assign(lengths, lengths + n);
     ctx->direct_ok = true;
+    ctx->long_hint = false;
     ctx->n_reads = 0;
     ctx->spans_pending = false;
     ctx->cig_off_ext = nullptr;
@@ -711,18 +713,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     unsigned long long* res = static_cast<unsigned long long*>(ctx->pin_io.h);
     int64_t* coff_up = reinterpret_cast<int64_t*>(res + n_res);
     HIP_TRY(ctx->d_coff.reserve(nc + 1));
-    if (n && ctx->ingest_grid <= 0) {
-        // one resident wave per range: a second round of waves would start
-        // its ranges only when the first finished
-        int dev = 0, ncu = 0, per = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ingest_kernel, kBlock, 0));
-#ifndef MC_INGEST_GRID_PCT
-#define MC_INGEST_GRID_PCT 100   // experiment knob: ingest grid as a percentage of the resident WGs
-#endif
-        ctx->ingest_grid = std::max(1, ncu * std::max(1, per) * MC_INGEST_GRID_PCT / 100);
-    }
+    // (the long-read counting is known before the pass loop; see count_long)
     // ---- layout for given extents: contig offsets and chunk geometry.  One
     // chunk index serves both K2 variants: its base chunks are the plain K2's,
     // half-size (kPlainTilesPerChunk tiles), where the plain kernel balances
@@ -737,29 +728,63 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     set_layout(ctx, ext);
     const unsigned long long* h = res;                         // counters
     const long long* maxend = reinterpret_cast<const long long*>(res + 8);
+    // the previous batch of this contig set had long reads: ingest counts
+    // their end events and chunk carries itself (long_count_kernel's pass,
+    // 0.2 ms of a C5 prepare, and its two fills)
+    const bool count_long = ctx->long_hint && n > 0;
+    int& igrid = ctx->ingest_grid[count_long ? 1 : 0];
+    if (n && igrid <= 0) {
+        // one resident wave per range: a second round of waves would start
+        // its ranges only when the first finished
+        int dev = 0, ncu = 0, per = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, count_long ? (const void*)ingest_kernel<true> : (const void*)ingest_kernel<false>, kBlock, 0));
+        igrid = std::max(1, ncu * std::max(1, per));
+    }
+    int lcw = 0;
     for (int pass = 0;; ++pass) {
         const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every full chunk's base chunks
+        const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
+        lcw = 0;
+        while (((int64_t)1 << lcw) < ctx->chunk_w) ++lcw;
         HIP_TRY(ctx->d_chunk_first.reserve(2 * n_base));
+        if (count_long) {
+            HIP_TRY(ctx->d_tile_cnt.reserve(n_tiles + 1));
+            HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
+        }
         if (int rc = upload_coff(ctx, coff_up)) return rc;
         {
             const int64_t np_ = pass == 0 ? n_pad : 0, ni = 2 * n_base;
+            const int64_t nt = count_long ? n_tiles + 1 : 0, ncc = count_long ? ctx->n_chunks + 1 : 0;
             const unsigned g = (unsigned)std::max<int64_t>(
-                1, std::min<int64_t>(1024, (np_ + (int64_t)n_res + ni + kBlock - 1) / kBlock));
+                1, std::min<int64_t>(1024, (np_ + (int64_t)n_res + ni + nt + ncc + kBlock - 1) / kBlock));
             hipLaunchKernelGGL(prep_clear_kernel, dim3(g), dim3(kBlock), 0, s, ctx->d_tid.p + n, np_,
                                ctx->d_scratch.p, (int64_t)n_res,
                                reinterpret_cast<unsigned long long*>(ctx->d_chunk_first.p), ni,
-                               n ? ~0ull : 0ull);   // all ones: no crossing read
+                               n ? ~0ull : 0ull,   // all ones: no crossing read
+                               reinterpret_cast<int32_t*>(count_long ? ctx->d_tile_cnt.p : nullptr), nt,
+                               count_long ? ctx->d_chunk_carry.p : nullptr, ncc);
             HIP_TRY(hipGetLastError());
         }
         if (n) {
             HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kBatch)));   // whole-batch loads
-            IngestIndex ix{ctx->d_coff.p, base_lw(ctx), ctx->short_max, n_base, ctx->d_chunk_first.p};
+            IngestIndex ix{ctx->d_coff.p, base_lw(ctx), ctx->short_max, n_base, ctx->d_chunk_first.p,
+                           count_long ? ctx->d_tile_cnt.p : nullptr, count_long ? ctx->d_chunk_carry.p : nullptr,
+                           ctx->n_chunks * ctx->chunk_w, lcw};
             const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
-                                                                      ctx->ingest_grid));
-            hipLaunchKernelGGL(ingest_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
-                               ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
-                               reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
-                               ctx->d_scratch.p + 8 + nc, ix, ctx->d_gpos.p);
+                                                                      igrid));
+            if (count_long)
+                hipLaunchKernelGGL(ingest_kernel<true>, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                                   ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
+                                   reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
+                                   ctx->d_scratch.p + 8 + nc, ix, ctx->d_gpos.p);
+            else
+                hipLaunchKernelGGL(ingest_kernel<false>, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_tid.p,
+                                   ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_scratch.p,
+                                   reinterpret_cast<long long*>(ctx->d_scratch.p + 8),
+                                   ctx->d_scratch.p + 8 + nc, ix, ctx->d_gpos.p);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipMemcpyAsync(res, ctx->d_scratch.p, n_res * 8, hipMemcpyDeviceToHost, s));
@@ -789,6 +814,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
     (void)off;
     ctx->has_long = ctx->max_span > ctx->short_max;
+    ctx->long_hint = ctx->has_long;
     if (ctx->has_long) {
         // end-event buckets and chunk carries, all on the device (count ->
         // offsets -> fill), no host round trip; the bucket array is sized for
@@ -797,8 +823,10 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
         HIP_TRY(ctx->d_tile_off.reserve(n_tiles + 1));
         HIP_TRY(ctx->d_tile_ev.reserve((size_t)(n + kBatch)));   // K2 loads whole int4 batches
-        HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
-        HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
+        if (!count_long) {
+            HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
+            HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
+        }
         if (ctx->long_grid <= 0) {
             int dev = 0, ncu = 0, per = 0;
             HIP_TRY(hipGetDevice(&dev));
@@ -811,9 +839,11 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         const int64_t subs = (n + kLongSub - 1) / kLongSub;
         const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(subs, ctx->long_grid));
         G.per = (subs + nb - 1) / nb * kLongSub;
-        hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
-                           ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
-        HIP_TRY(hipGetLastError());
+        if (!count_long) {   // (else ingest counted)
+            hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
+                               ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
+            HIP_TRY(hipGetLastError());
+        }
         const int bt = (int)((n_tiles + kScanSeg - 1) / kScanSeg);
         const int bc = (int)((ctx->n_chunks + kScanSeg - 1) / kScanSeg);
         HIP_TRY(ctx->d_scan_part.reserve(bt + bc));

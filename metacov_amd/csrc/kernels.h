@@ -237,7 +237,19 @@ struct IngestIndex {
     int short_max;
     int64_t n_base;                    // base chunks
     int64_t* index;                    // [2 * n_base]
+    // long_count_kernel's counts, folded into this pass when the batch is
+    // expected to hold long reads (the previous one did); null: not counted
+    unsigned* tile_cnt;                // [n_tiles + 1] end events per tile
+    int* chunk_diff;                   // [n_chunks + 1] long reads covering a chunk start (difference form)
+    int64_t alloc_len;                 // the depth vector's length
+    int lcw;                           // (full) chunk width 2^lcw
 };
+
+// Per-wave LDS windows of the folded long-read counts: end tiles within 64
+// tiles (256 Ki positions) and chunk boundaries within 16 chunks of the
+// step's first long read start; farther ones take a global atomic.
+constexpr int kIngestTileWin = 64;
+constexpr int kIngestChunkWin = 16;
 
 __device__ __forceinline__ int64_t shfl_up_i64(int64_t v) {
     const int lo = __shfl_up((int)(v & 0xffffffff), 1, 64), hi = __shfl_up((int)(v >> 32), 1, 64);
@@ -250,13 +262,25 @@ __device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// kCount: the long-read counting compiled in (its registers cost the plain
+// pass an occupancy step: 90 -> 111 VGPRs)
+template <bool kCount>
 __global__ void __launch_bounds__(kBlock)
 ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
               const int32_t* __restrict__ span, int64_t n, int32_t n_contigs,
               unsigned long long* __restrict__ out, long long* __restrict__ maxend,
               unsigned long long* __restrict__ cbases, IngestIndex X, uint32_t* __restrict__ gpos) {
     constexpr int U = kIngestU;
+    static_assert(kIngestTileWin == 64 && kIngestChunkWin <= 64, "one window entry per lane");
     const int lane = threadIdx.x & 63;
+    __shared__ int lw_tiles[kWaves][kIngestTileWin];
+    __shared__ int lw_chunks[kWaves][kIngestChunkWin];
+    int* wtile = lw_tiles[threadIdx.x >> 6];
+    int* wchunk = lw_chunks[threadIdx.x >> 6];
+    if (kCount) {   // (this wave's windows only: no barrier)
+        wtile[lane] = 0;
+        if (lane < kIngestChunkWin) wchunk[lane] = 0;
+    }
     const int64_t n4 = (n + 3) / 4;
     const int64_t n_waves = (int64_t)gridDim.x * kWaves;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -369,6 +393,59 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
             }
             acc.bases += b;
             acc.end = max(acc.end, (long long)e);
+        }
+        if (kCount) {
+            // long reads (span > short_max): end event per tile and chunk carry
+            // differences, as long_count_kernel counts them (the same rules),
+            // into the wave's LDS windows, flushed after the step
+            unsigned lng = 0;
+#pragma unroll
+            for (int j = 0; j < 4 * U; ++j)
+                lng |= (((valid >> j) & 1u) && ss[j] > X.short_max) ? 1u << j : 0u;
+            const unsigned long long la = __ballot(lng != 0);
+            if (la) {
+                // window base: the wave's first long read (its smallest start when sorted;
+                // on unsorted input, which prepare rejects, windows just miss)
+                const int jf = lng ? __ffs(lng) - 1 : 0;
+                int64_t gl = 0;
+#pragma unroll
+                for (int j = 0; j < 4 * U; ++j)
+                    if (j == jf) gl = ((int64_t)cid[j] << X.lw) + off[j];
+                const int64_t gf = readlane_i64(gl, __ffsll((long long)la) - 1);
+                const int64_t TB = gf / kTileW, CB = gf >> X.lcw;
+                const int64_t cmask = ((int64_t)1 << X.lcw) - 1;
+#pragma unroll
+                for (int j = 0; j < 4 * U; ++j) {
+                    if (!((lng >> j) & 1u)) continue;
+                    const int64_t g = ((int64_t)cid[j] << X.lw) + off[j];
+                    const int64_t ge = g + ss[j];
+                    if (ge < X.alloc_len && (ge & cmask)) {   // (an end on a chunk start: no event)
+                        const int64_t te = ge / kTileW;
+                        if ((uint64_t)(te - TB) < (uint64_t)kIngestTileWin) atomicAdd(&wtile[te - TB], 1);
+                        else atomicAdd(&X.tile_cnt[te], 1u);
+                    }
+                    const int64_t c0 = (g >> X.lcw) + 1, c1 = ((ge - 1) >> X.lcw) + 1;
+                    if (c1 > c0) {
+                        if ((uint64_t)(c0 - CB) < (uint64_t)kIngestChunkWin) atomicAdd(&wchunk[c0 - CB], 1);
+                        else atomicAdd(&X.chunk_diff[c0], 1);
+                        if ((uint64_t)(c1 - CB) < (uint64_t)kIngestChunkWin) atomicAdd(&wchunk[c1 - CB], -1);
+                        else atomicAdd(&X.chunk_diff[c1], -1);
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the wave's LDS atomics are done
+                const int v = wtile[lane];
+                if (v) {
+                    atomicAdd(&X.tile_cnt[TB + lane], (unsigned)v);
+                    wtile[lane] = 0;
+                }
+                if (lane < kIngestChunkWin) {
+                    const int c = wchunk[lane];
+                    if (c) {
+                        atomicAdd(&X.chunk_diff[CB + lane], c);
+                        wchunk[lane] = 0;
+                    }
+                }
+            }
         }
         if (gpos) {   // K2's read words: start bits (coff[tid] + pos = chunk * w + offset) and span
 #pragma unroll
@@ -679,12 +756,16 @@ window_kernel(const int32_t* __restrict__ fsamp, const int32_t* __restrict__ spa
 __global__ void __launch_bounds__(kBlock)
 prep_clear_kernel(int32_t* __restrict__ tid_pad, int64_t n_pad, unsigned long long* __restrict__ scratch,
                   int64_t n_scratch, unsigned long long* __restrict__ index, int64_t n_index,
-                  unsigned long long index_fill) {
+                  unsigned long long index_fill, int32_t* __restrict__ zero32, int64_t n_zero32,
+                  int32_t* __restrict__ zero32b, int64_t n_zero32b) {
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_pad + n_scratch + n_index; i += stride) {
+    const int64_t e1 = n_pad + n_scratch, e2 = e1 + n_index, e3 = e2 + n_zero32, e4 = e3 + n_zero32b;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < e4; i += stride) {
         if (i < n_pad) tid_pad[i] = 0;
-        else if (i < n_pad + n_scratch) scratch[i - n_pad] = 0;
-        else index[i - n_pad - n_scratch] = index_fill;
+        else if (i < e1) scratch[i - n_pad] = 0;
+        else if (i < e2) index[i - e1] = index_fill;
+        else if (i < e3) zero32[i - e2] = 0;          // (the folded long-read counts)
+        else zero32b[i - e3] = 0;
     }
 }
 

@@ -152,6 +152,50 @@ def test_ont_like_long_reads(eng):
     check_regions_vs_oracle(eng, d, ext, coff, rtid, rs, re_)
 
 
+def _long_batch(lengths, n, seed, extra_far=False):
+    rng = np.random.default_rng(seed)
+    tid = np.sort(rng.integers(0, len(lengths), size=n)).astype(np.int32)
+    span = np.minimum(rng.lognormal(np.log(10_000), 0.6, size=n).astype(np.int64), lengths[tid]).astype(np.int32)
+    if extra_far:   # ends far past their start tile (outside ingest's 64-tile window) and one overhang
+        span[:50] = np.minimum(300_000, lengths[tid[:50]]).astype(np.int32)
+    pos = (rng.random(n) * (lengths[tid] - span + 1)).astype(np.int32)
+    if extra_far:
+        k = n // 2
+        pos[k] = lengths[tid[k]] - 100
+        span[k] = 5000                     # runs 4900 past its contig: the extents grow (second pass)
+    o = np.lexsort((pos, tid))
+    return tid[o], pos[o], span[o]
+
+
+def test_long_counts_folded_into_ingest(lib_built):
+    """Batches after one with long reads count the end events and chunk
+    carries inside ingest (long_count_kernel's pass folded in): exact depth
+    and rows for a following long batch (ends outside the LDS window, an
+    overhang that re-runs the pass), a short-only batch, and long again."""
+    rng = np.random.default_rng(91)
+    lengths = rng.integers(60_000, 400_000, size=30).astype(np.int64)
+    rt = np.arange(len(lengths), dtype=np.int32)
+    rs = np.zeros(len(lengths), np.int64)
+    e = CoverageEngine(0)
+    try:
+        e.set_contigs(lengths)
+        batches = [_long_batch(lengths, 40_000, 1), _long_batch(lengths, 30_000, 2, extra_far=True),
+                   make_case(lengths, 50_000, (1, 150), 3, overhang=False)[1:],
+                   _long_batch(lengths, 20_000, 4)]
+        for k, (tid, pos, span) in enumerate(batches):
+            e.clear_reads()
+            e.add_reads(tid, pos, span)
+            d, ext, coff = coracle.depth(lengths, tid, pos, span)
+            re_ = np.asarray(ext, np.int64)
+            want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+            got = e.compute_depth_stats(rt, rs, re_)
+            for f in want.dtype.names:
+                assert np.array_equal(got[f], want[f]), (k, f)
+            check_depth_vs_oracle(e, lengths, tid, pos, span)
+    finally:
+        e.close()
+
+
 def make_case(lengths, n, span_rng, seed, overhang=True):
     rng = np.random.default_rng(seed)
     lengths = np.asarray(lengths, np.int64)
