@@ -190,6 +190,7 @@ struct mc_ctx {
     DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
     int32_t max_span = 0;
     bool long_hint = false;               // the last full prepare of this contig set had long reads
+    bool prep_pending = false;            // the last full prepare's time is not read yet
     int64_t aligned_bases = 0;
     int ring = 0;                 // LDS ring ints
     int tiles_per_chunk = 16;
@@ -584,6 +585,15 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
 
 static float elapsed(mc_ctx* ctx, int a, int b) { return elapsed(ctx->ev[a], ctx->ev[b]); }
 
+// The last full prepare's time (ev[2] -> ev[3]), once its events are complete
+// (mc_prepare does not wait for its own kernels).
+static void resolve_prepare_timing(mc_ctx* ctx) {
+    if (!ctx->prep_pending || hipEventQuery(ctx->ev[3]) != hipSuccess) return;
+    ctx->t.prepare_ms = elapsed(ctx, 2, 3);
+    ctx->t.prepare_ms_total += ctx->t.prepare_ms;
+    ctx->prep_pending = false;
+}
+
 // Adds the pending fused calls' event times to t (oldest first; the current
 // set only with `all`, after the stream has drained).
 static void resolve_timings(mc_ctx* ctx, bool all) {
@@ -698,6 +708,8 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     const int32_t nc = (int32_t)ctx->len.size();
     const int64_t n = ctx->n_reads;
     hipStream_t s = ctx->stream;
+    resolve_prepare_timing(ctx);   // the previous prepare's events, before ev[2] / ev[3] are reused
+    const bool k1_now = ctx->spans_pending;
     if (int rc = run_k1(ctx)) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // K2 loads whole int4 batches past n: the tid padding must index coff
@@ -743,6 +755,54 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             &per, count_long ? (const void*)ingest_kernel<true> : (const void*)ingest_kernel<false>, kBlock, 0));
         igrid = std::max(1, ncu * std::max(1, per));
     }
+    // The long-read end-event buckets and chunk carries on the current layout
+    // (count unless ingest counted -> offsets -> fill), all on the device; the
+    // bucket array is sized for every read being long.  With ingest's counts
+    // they are queued behind ingest before its results are read (speculative:
+    // unused if the batch has no long reads, redone if the extents grow), so
+    // the host's round trip overlaps them.
+    auto launch_long = [&](bool counted) -> int {
+        const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
+        const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
+        HIP_TRY(ctx->d_tile_cnt.reserve(n_tiles + 1));
+        HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
+        HIP_TRY(ctx->d_tile_off.reserve(n_tiles + 1));
+        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(n + kBatch)));   // K2 loads whole int4 batches
+        if (!counted) {
+            HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
+            HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
+        }
+        if (ctx->long_grid <= 0) {
+            int dev = 0, ncu = 0, per = 0;
+            HIP_TRY(hipGetDevice(&dev));
+            HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)long_fill_kernel, kBlock, 0));
+            ctx->long_grid = ncu * std::max(1, per);
+        }
+        LongGeo G{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len, 0, 0};
+        while (((int64_t)1 << G.lcw) < ctx->chunk_w) ++G.lcw;
+        const int64_t subs = (n + kLongSub - 1) / kLongSub;
+        const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(subs, ctx->long_grid));
+        G.per = (subs + nb - 1) / nb * kLongSub;
+        if (!counted) {
+            hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
+                               ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
+            HIP_TRY(hipGetLastError());
+        }
+        const int bt = (int)((n_tiles + kScanSeg - 1) / kScanSeg);
+        const int bc = (int)((ctx->n_chunks + kScanSeg - 1) / kScanSeg);
+        HIP_TRY(ctx->d_scan_part.reserve(bt + bc));
+        ScanArgs A{ctx->d_tile_cnt.p, n_tiles, ctx->d_tile_off.p, ctx->d_chunk_carry.p, ctx->n_chunks,
+                   ctx->d_scan_part.p, bt};
+        hipLaunchKernelGGL(long_scan_partial_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(long_scan_final_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
+                           ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        HIP_TRY(hipGetLastError());
+        return MC_OK;
+    };
     int lcw = 0;
     for (int pass = 0;; ++pass) {
         const int64_t n_base = ctx->n_chunks * ctx->cstride;   // every full chunk's base chunks
@@ -787,6 +847,8 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
                                    ctx->d_scratch.p + 8 + nc, ix, ctx->d_gpos.p);
             HIP_TRY(hipGetLastError());
         }
+        if (count_long)
+            if (int rc = launch_long(true)) return rc;
         HIP_TRY(hipMemcpyAsync(res, ctx->d_scratch.p, n_res * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         MC_REQUIRE(h[0] == 0, MC_E_INVALID,
@@ -808,60 +870,21 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     ctx->max_span = (int32_t)h[3];
     ctx->cbases.assign(res + 8 + nc, res + 8 + 2 * nc);
     if (ctx->cbases.empty()) ctx->cbases.assign(1, 0);
-    const int64_t off = ctx->total_len;
-    const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
-    const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
-    HIP_TRY(ctx->d_depth.reserve((size_t)alloc_len));
-    (void)off;
+    HIP_TRY(ctx->d_depth.reserve((size_t)(ctx->n_chunks * ctx->chunk_w)));
     ctx->has_long = ctx->max_span > ctx->short_max;
     ctx->long_hint = ctx->has_long;
-    if (ctx->has_long) {
-        // end-event buckets and chunk carries, all on the device (count ->
-        // offsets -> fill), no host round trip; the bucket array is sized for
-        // every read being long
-        HIP_TRY(ctx->d_tile_cnt.reserve(n_tiles + 1));
-        HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
-        HIP_TRY(ctx->d_tile_off.reserve(n_tiles + 1));
-        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(n + kBatch)));   // K2 loads whole int4 batches
-        if (!count_long) {
-            HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
-            HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
-        }
-        if (ctx->long_grid <= 0) {
-            int dev = 0, ncu = 0, per = 0;
-            HIP_TRY(hipGetDevice(&dev));
-            HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)long_fill_kernel, kBlock, 0));
-            ctx->long_grid = ncu * std::max(1, per);
-        }
-        LongGeo G{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len, 0, 0};
-        while (((int64_t)1 << G.lcw) < ctx->chunk_w) ++G.lcw;
-        const int64_t subs = (n + kLongSub - 1) / kLongSub;
-        const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(subs, ctx->long_grid));
-        G.per = (subs + nb - 1) / nb * kLongSub;
-        if (!count_long) {   // (else ingest counted)
-            hipLaunchKernelGGL(long_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
-                               ctx->d_tile_cnt.p, ctx->d_chunk_carry.p);
-            HIP_TRY(hipGetLastError());
-        }
-        const int bt = (int)((n_tiles + kScanSeg - 1) / kScanSeg);
-        const int bc = (int)((ctx->n_chunks + kScanSeg - 1) / kScanSeg);
-        HIP_TRY(ctx->d_scan_part.reserve(bt + bc));
-        ScanArgs A{ctx->d_tile_cnt.p, n_tiles, ctx->d_tile_off.p, ctx->d_chunk_carry.p, ctx->n_chunks,
-                   ctx->d_scan_part.p, bt};
-        hipLaunchKernelGGL(long_scan_partial_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(long_scan_final_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
-                           ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
-        HIP_TRY(hipGetLastError());
-    }
+    if (ctx->has_long && !count_long)
+        if (int rc = launch_long(false)) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[3], s));
-    HIP_TRY(hipStreamSynchronize(s));
-    ctx->t.prepare_ms = elapsed(ctx, 2, 3);
-    ctx->t.prepare_ms_total += ctx->t.prepare_ms;
-    ctx->t.cigar_ms = ctx->t_cigar ? elapsed(ctx, 0, 1) : 0.f;
+    if (k1_now) {
+        // K1 read borrowed CIGAR arrays (mc_add_reads_cigar_device): they are
+        // the caller's again once this prepare has drained
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->t.cigar_ms = elapsed(ctx, 0, 1);
+    } else if (ctx->t_cigar) {   // K1 ran for the direct attempt this batch was handed over from
+        ctx->t.cigar_ms = elapsed(ctx, 0, 1);
+    }
+    ctx->prep_pending = true;   // prepare_ms: read once the events are complete
     ctx->prepared = true;
     ctx->depth_valid = false;
     ++ctx->prep_gen;
@@ -1552,16 +1575,18 @@ static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         const FusedLayout L = fused_layout(fc.nf, R);
         if (direct) {
             if (int rc = launch_window(ctx, R, L)) return rc;
-        } else {
-            unsigned char* h = ctx->fstage.host();
-            int32_t* brow = reinterpret_cast<int32_t*>(h + L.brow);
-            int32_t* fbase = reinterpret_cast<int32_t*>(h + L.base);
-            const int32_t* fid = reinterpret_cast<const int32_t*>(h + L.id);
-            HIP_TRY(hipStreamSynchronize(ctx->stream));   // the staging buffer's last upload has drained
-            for (int64_t r = 0; r < R; ++r) brow[r] = window_base(tid[r]);
-            for (int64_t k = 0; k < fc.nf; ++k) fbase[k] = brow[fid[k]];
-            HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p + L.base, h + L.base, L.rtid - L.base, hipMemcpyHostToDevice,
-                                   ctx->stream));
+        } else if (R > 0) {
+            // from ingest's per-contig bases, still in d_scratch, on the
+            // device (the host loop over the rows and its upload were 0.05 ms
+            // between C5's prepare and K2)
+            const int32_t nc = (int32_t)ctx->len.size();
+            unsigned char* d = ctx->fstage.d.p;
+            hipLaunchKernelGGL(window_bases_kernel, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                               ctx->stream, ctx->d_scratch.p, ctx->d_scratch.p + 8 + nc, ctx->n_reads, ctx->d_len.p,
+                               reinterpret_cast<const int32_t*>(d + L.rtid), reinterpret_cast<const int32_t*>(d + L.rfused),
+                               R, (int)win_below, reinterpret_cast<int32_t*>(d + L.brow),
+                               reinterpret_cast<int32_t*>(d + L.base));
+            HIP_TRY(hipGetLastError());
         }
         fc.gen = ctx->prep_gen;
         return depth_stats_launch(ctx, R, tid, start, end, d_out, fc.nf);
@@ -1739,6 +1764,7 @@ extern "C" int mc_get_timings(mc_ctx* ctx, mc_timings* out) {
     MC_REQUIRE(out, MC_E_INVALID, "null out");
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     resolve_timings(ctx, true);
+    resolve_prepare_timing(ctx);
     if (ctx->t_depth) ctx->t.depth_ms = elapsed(ctx, 4, 5);
     if (ctx->t_stats) ctx->t.stats_ms = elapsed(ctx, 6, 7);
     ctx->t.direct_halo = ctx->direct_halo_used;

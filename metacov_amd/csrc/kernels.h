@@ -748,6 +748,30 @@ window_kernel(const int32_t* __restrict__ fsamp, const int32_t* __restrict__ spa
     if (k >= 0) fbase[k] = base;
 }
 
+// The full prepare's window bases on the device (a repeated call over the
+// same layout with a new batch): the estimate the host makes at staging time
+// (depth over the contig less one mean read span, kWinBelow bins of the
+// window below it) from ingest's per-contig bases, with the contig length
+// for the extent.  One thread per region row.
+__global__ void __launch_bounds__(kBlock)
+window_bases_kernel(const unsigned long long* __restrict__ ingest_out, const unsigned long long* __restrict__ cbases,
+                    int64_t n, const int64_t* __restrict__ len, const int32_t* __restrict__ rtid,
+                    const int32_t* __restrict__ rfused, int64_t R, int win_below, int32_t* __restrict__ brow,
+                    int32_t* __restrict__ fbase) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    const int t = rtid[r];
+    const double mean = n > 0 ? (double)ingest_out[2] / (double)n : 0.0;
+    const double ext = (double)len[t];
+    const double body = ext > 2.0 * mean ? ext - mean : ext;
+    const double est = ext > 0 ? (double)cbases[t] / body : 0.0;
+    const long long b0 = llrint(est) - win_below;
+    const int32_t base = (int32_t)(b0 > 0 ? b0 : 0);
+    brow[r] = base;
+    const int32_t k = rfused[r];
+    if (k >= 0) fbase[k] = base;
+}
+
 // Prepare's buffer setup in one launch (three fills were three commands in
 // the stream ahead of ingest_kernel): the tid padding K2's whole-batch loads
 // read past n (zeros: a valid contig), the ingest counters / ends / bases
