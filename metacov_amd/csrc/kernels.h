@@ -1327,7 +1327,7 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
                                                     int64_t C0, int64_t chunk_w, const DirectChunk& dc,
                                                     const ReadArrays& A, const int64_t* __restrict__ coff,
                                                     const DirectArgs& D, int short_max, DirectAcc& acc) {
-    const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
+    const int lane4 = (int)threadIdx.x * kReadsPerThread;   // this lane's first read, relative to base
     const int tt[4] = {r.t.x, r.t.y, r.t.z, r.t.w};
     const int pp[4] = {r.p.x, r.p.y, r.p.z, r.p.w};
     int sp[4];
@@ -1338,7 +1338,7 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
     unsigned valid = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        valid |= (((unsigned)tt[k] < (unsigned)D.nc) & (pp[k] >= 0) & (sp[k] >= 0)) ? 1u << k : 0u;
+        valid |= (((unsigned)tt[k] < (unsigned)D.nc) & ((pp[k] | sp[k]) >= 0)) ? 1u << k : 0u;
     constexpr int64_t kClamp = int64_t(1) << 30;
     int rs[4] = {0, 0, 0, 0};
     unsigned L[4] = {0, 0, 0, 0};          // contig length (positions fit 32 bits)
@@ -1351,24 +1351,40 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
         const int64_t c = uload(coff, t0) - C0, ln = uload(D.len, t0);
         const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
+        // rs = clamp(c + pos, -2^30, 2^30) in 32 bits: pos (>= 0 when valid)
+        // clamped to [p_lo, p_hi] per contig (scalar), then c + pos wraps
+        // into an int32 that is exact (one med3 and one add per read instead
+        // of a 64-bit add, two 64-bit compares and selects)
+        int c32, p_lo, p_hi;
+        if (c > kClamp) {
+            c32 = (int)kClamp;
+            p_lo = p_hi = 0;
+        } else if (c < -kClamp - (int64_t)INT32_MAX) {
+            c32 = -(int)kClamp;
+            p_lo = p_hi = 0;
+        } else {
+            c32 = (int)(uint32_t)(uint64_t)c;
+            p_lo = (int)(c < -kClamp ? -kClamp - c : 0);
+            p_hi = (int)(kClamp - c > (int64_t)INT32_MAX ? (int64_t)INT32_MAX : kClamp - c);
+        }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (((todo >> k) & 1u) && tt[k] == t0) {
-                const int64_t rel = c + pp[k];
-                rs[k] = (int)(rel < -kClamp ? -kClamp : rel > kClamp ? kClamp : rel);
-                L[k] = l32;
-                todo &= ~(1u << k);
-            }
+        for (int k = 0; k < 4; ++k) {
+            const bool m = ((todo >> k) & 1u) && tt[k] == t0;
+            rs[k] = m ? (int)((unsigned)c32 + (unsigned)min(max(pp[k], p_lo), p_hi)) : rs[k];
+            L[k] = m ? l32 : L[k];
+            todo &= m ? ~(1u << k) : ~0u;
+        }
     }
     // predecessor of read 0: lane - 1's read 3 (DPP wave_shr:1, no LDS
     // permute); lane 0 keeps its own, which came with the batch
     const int pt = __builtin_amdgcn_update_dpp(r.pt, tt[3], 0x138, 0xf, 0xf, false);
     const int ppv = __builtin_amdgcn_update_dpp(r.pp, pp[3], 0x138, 0xf, 0xf, false);
     // 4-bit masks of this lane's reads: in [lo, hi) (applied) and in [vlo,
-    // vhi) (checked here), from two 64-bit differences per range
+    // vhi) (checked here); the bounds relative to the batch are scalar
     auto range4 = [&](int64_t lo, int64_t hi) -> unsigned {
-        const int64_t a = lo - i0, z = hi - i0;
-        const int ka = a < 0 ? 0 : a > 4 ? 4 : (int)a, kz = z < 0 ? 0 : z > 4 ? 4 : (int)z;
+        const int la = (int)(lo - base < -8 ? -8 : lo - base > kBatch + 8 ? kBatch + 8 : lo - base);
+        const int ha = (int)(hi - base < -8 ? -8 : hi - base > kBatch + 8 ? kBatch + 8 : hi - base);
+        const int ka = min(max(la - lane4, 0), 4), kz = min(max(ha - lane4, 0), 4);
         return ((1u << kz) - 1u) & ~((1u << ka) - 1u);
     };
     unsigned pend = 0, bad = 0, unfit = 0;
