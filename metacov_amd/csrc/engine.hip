@@ -635,8 +635,9 @@ static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     // chunks of kTilesPerChunk tiles; fewer (>= the tiles of one ring, so
     // the ring divides the chunk) when the genome is too small to fill the GPU
     const int64_t tiles = std::max<int64_t>(1, (off + kTileW - 1) / kTileW);
-    const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : kTilesPerChunk;
-    int tpc = kTilesPerChunk;
+    const int top = ctx->long_hint ? kTilesPerChunkLong : kTilesPerChunk;
+    const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : top;
+    int tpc = top;
     while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < 2048 &&
            ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
         tpc /= 2;
@@ -661,6 +662,7 @@ static int base_lw(const mc_ctx* ctx) {
     return lw;
 }
 static_assert((kTileW & (kTileW - 1)) == 0 && (kTilesPerChunk & (kTilesPerChunk - 1)) == 0 &&
+                  (kTilesPerChunkLong & (kTilesPerChunkLong - 1)) == 0 &&
                   (kPlainTilesPerChunk & (kPlainTilesPerChunk - 1)) == 0,
               "chunk widths must be powers of two (ingest and the probe shift by log2 of them)");
 

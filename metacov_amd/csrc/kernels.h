@@ -66,6 +66,14 @@ static_assert(kRing % 256 == 0 && kRing > kTileW, "ring must hold a tile plus a 
 // ring slot of a chunk-relative position (the ring is re-zeroed per chunk)
 __device__ __forceinline__ int ring_slot(int rel) { return rel % kRing; }
 constexpr int kTilesPerChunk = MC_TILES_PER_CHUNK;
+// Chunks of a contig set with long reads (C5): twice as long.  Their
+// per-chunk costs (the first event and read batches, the histogram flush, the
+// carry) weigh more there: C5 K2 1.081 -> 1.057 ms, while C3 loses 2-4 % on
+// them (profiles/r03u_chunk16_ab.txt).
+#ifndef MC_TILES_PER_CHUNK_LONG
+#define MC_TILES_PER_CHUNK_LONG 16
+#endif
+constexpr int kTilesPerChunkLong = MC_TILES_PER_CHUNK_LONG;
 constexpr int kReadsPerThread = 4;     // int4 loads of tid/pos/span
 constexpr int kBatch = kBlock * kReadsPerThread;
 constexpr int kLdsHeader = 20;         // ints reserved in front of the ring (K2: see depth_kernel)
@@ -1278,7 +1286,8 @@ __device__ __forceinline__ void issue_raw(RawBatch<kDirect>& r, int64_t base, co
 __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch<false>& r, int64_t base,
                                              int64_t n, int64_t C0, int64_t lo) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
-    static_assert((int64_t)MC_TILES_PER_CHUNK * kTileW + kRing < (1 << (kGposBits - 1)),
+    static_assert((int64_t)(kTilesPerChunkLong > kTilesPerChunk ? kTilesPerChunkLong : kTilesPerChunk) * kTileW +
+                          kRing < (1 << (kGposBits - 1)),
                   "packed starts: a chunk and its halo must fit the signed wrap-around range");
     static_assert(kGspanCap > kRing - kTileW, "the span cap must exceed short_max");
     const unsigned c0 = (unsigned)C0 & kGposMask;
