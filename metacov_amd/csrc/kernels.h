@@ -1579,17 +1579,6 @@ __device__ __forceinline__ void ov_reg_reset(OvReg& r) {
     r.vmax = 0;
 }
 
-__device__ __forceinline__ void ov_reg_take(OvReg& r, bool o, int v, int n, int base) {
-    if (o) {
-        r.cnt += n;
-        r.low += v < base ? n : 0;
-        r.sum += (unsigned long long)v * (unsigned long long)n;
-        r.sq += (unsigned long long)((long long)v * v) * (unsigned long long)n;
-        r.vmin = min(r.vmin, v);
-        r.vmax = max(r.vmax, v);
-    }
-}
-
 // a lane's accumulated out-of-window statistics into its LDS record
 __device__ __attribute__((noinline)) void ov_spill(OvLds* ov, unsigned cnt, unsigned low, unsigned long long sum,
                                                    unsigned long long sq, int mn, int mx) {
@@ -1643,11 +1632,22 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, in
     atomicAdd(&h[s2 ? min(d2, du) : du], (unsigned)l2);
     atomicAdd(&h[s3 ? min(d3, du) : du], 1u);
     if (__builtin_expect(__any(max(max(d0, d1), max(d2, d3)) >= kWin), 0)) {
-        const bool e0 = y0 >= 0, e1 = s1 && y1 >= 0, e2 = s2 && y2 >= 0, e3 = s3 && y3 >= 0;
-        ov_reg_take(ovr, e0 && d0 >= kWin, y0, l0, base);
-        ov_reg_take(ovr, e1 && d1 >= kWin, y1, l1, base);
-        ov_reg_take(ovr, e2 && d2 >= kWin, y2, l2, base);
-        ov_reg_take(ovr, e3 && d3 >= kWin, y3, 1, base);
+        // per position, branch-free (the per-run form took an exec-mask
+        // branch per slot: 4 % of a C5 K2, where the ramps of deep contigs
+        // fall below the window)
+        const int y[4] = {y0, y1, y2, y3};
+        const unsigned d[4] = {d0, d1, d2, d3};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool o = (y[k] >= 0) & (d[k] >= kWin);
+            const unsigned v = o ? (unsigned)y[k] : 0u;
+            ovr.cnt += o ? 1u : 0u;
+            ovr.low += (o & (y[k] < base)) ? 1u : 0u;
+            ovr.sum += v;
+            ovr.sq += (unsigned long long)v * v;
+            ovr.vmin = min(ovr.vmin, o ? y[k] : 0x7fffffff);
+            ovr.vmax = max(ovr.vmax, (int)v);
+        }
     }
 }
 
