@@ -252,7 +252,7 @@ struct mc_ctx {
     DevBuf<unsigned> d_fb_hist;           // [kFbSlots][kLdsBins]
     DevBuf<RegionAcc> d_fb_acc;           // [kFbSlots]
     DevBuf<int32_t> d_fb_list;            // [kFbSlots]
-    DevBuf<unsigned> d_fb_cnt;            // [2] (by call parity), then [kFbSlots] per-region done counters
+    DevBuf<unsigned> d_fb_cnt;            // [2] (by call parity)
     int64_t fb_calls = 0;
     bool fb_recent = false;               // the last fused call had out-of-window regions
     int64_t device_recomputes = 0;
@@ -1434,8 +1434,8 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
             HIP_TRY(ctx->d_fb_hist.reserve((size_t)kFbSlots * kLdsBins));
             HIP_TRY(ctx->d_fb_acc.reserve(kFbSlots));
             HIP_TRY(ctx->d_fb_list.reserve(kFbSlots));
-            HIP_TRY(ctx->d_fb_cnt.reserve(2 + kFbSlots));   // [2] per-parity counts, [kFbSlots] done counters
-            HIP_TRY(hipMemsetAsync(ctx->d_fb_cnt.p, 0, (2 + kFbSlots) * 4, s));
+            HIP_TRY(ctx->d_fb_cnt.reserve(2));
+            HIP_TRY(hipMemsetAsync(ctx->d_fb_cnt.p, 0, 8, s));
             hipLaunchKernelGGL(fused_init_kernel, dim3(1024), dim3(kBlock), 0, s, ctx->d_fb_hist.p,
                                (int64_t)kFbSlots * kLdsBins, (unsigned*)nullptr, ctx->d_fb_acc.p,
                                (int64_t)kFbSlots, (const int64_t*)nullptr, (int64_t)0, (int64_t)1, (int64_t)0,
@@ -1454,7 +1454,6 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                    ctx->d_fb_cnt.p,
                    (int)(ctx->fb_calls & 1),
                    ctx->d_fb_hist.p,
-                   ctx->d_fb_cnt.p + 2,
                    ctx->d_fb_acc.p,
                    d_out};
         ctx->fb_calls += 1;
@@ -1475,6 +1474,8 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     HIP_TRY(hipGetLastError());
     if (devfb) {
         hipLaunchKernelGGL(fb_seg_kernel, dim3(1024), dim3(kBlock), (size_t)kLdsBins * 4, s, F);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(fb_final_kernel, dim3(kFbSlots), dim3(kBlock), 0, s, F);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(T.e[3], s));

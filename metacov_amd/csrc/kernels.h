@@ -2363,9 +2363,9 @@ region_final_kernel(const unsigned* __restrict__ hist, int nbins,
 // depth vector K2 just wrote, without the host round trip the K3 fallback
 // takes: fb_seg_kernel builds each listed region's full value histogram
 // (kLdsBins values, enough while the maximum depth is below it), workgroups
-// splitting the region's positions; the last of a region's workgroups
-// derives its row and scatters it into place.  Buffers are left zeroed for
-// the next call.  Listed regions beyond kFbSlots, or a maximum depth >= kLdsBins, are
+// splitting the region's positions, and fb_final_kernel derives its row
+// and scatters it into place.  Both leave their buffers zeroed for the next
+// call.  Listed regions beyond kFbSlots, or a maximum depth >= kLdsBins, are
 // left to the host's K3 fallback.
 constexpr int kFbSlots = 512;
 
@@ -2417,7 +2417,6 @@ struct FbArgs {
     unsigned* cnt;                     // [2] per call parity
     int parity;
     unsigned* hist;                    // [kFbSlots][kLdsBins]
-    unsigned* done;                    // [kFbSlots] workgroups finished per listed region
     RegionAcc* acc;                    // [kFbSlots]
     RegionOut* out;                    // the call's rows
 };
@@ -2425,68 +2424,65 @@ struct FbArgs {
 __global__ void __launch_bounds__(kBlock)
 fb_seg_kernel(FbArgs F) {
     extern __shared__ __attribute__((aligned(16))) unsigned hb[];
-    if (blockIdx.x == 0 && threadIdx.x == 0) F.cnt[F.parity ^ 1] = 0;   // the next call's counter
     const int n = (int)min(F.cnt[F.parity], (unsigned)kFbSlots);
     const int maxd = *F.max_depth;
     if (n == 0 || maxd >= kLdsBins) return;
     const int nb = maxd + 1;
     const int per = max(1, (int)gridDim.x / n);        // workgroups per region
     __shared__ int ext[2 * kWaves];
-    __shared__ int s_last;
     for (int w = blockIdx.x; w < n * per; w += gridDim.x) {
         const int i = w / per, part = w % per;
-        const int r = F.list[i];
-        const int k = F.rfused[r];
-        unsigned* g = F.hist + (int64_t)i * kLdsBins;
-        if (k >= 0) {   // (k < 0: no covered position, zeros only)
-            const int64_t gs0 = F.fgs[k], len = F.fge[k] - gs0;
-            const int64_t gs = gs0 + len * part / per, ge = gs0 + len * (part + 1) / per;
-            for (int q = threadIdx.x * 4; q < nb; q += kBlock * 4)
-                *reinterpret_cast<i32x4*>(hb + q) = i32x4{0, 0, 0, 0};
-            __syncthreads();
-            int vmax = 0;
-            unsigned vmin = 0xffffffffu;
-            seg_hist(F.depth, gs, ge, hb, nb, vmax, vmin);
-            vmax = wave_max(vmax);
-            const int wmin = wave_min((int)min(vmin, 0x7fffffffu));
-            if ((threadIdx.x & 63) == 0) {
-                ext[threadIdx.x >> 6] = wmin;
-                ext[kWaves + (threadIdx.x >> 6)] = vmax;
-            }
-            __syncthreads();
-            int lo = ext[0], hi = ext[kWaves];
+        const int k = F.rfused[F.list[i]];
+        if (k < 0) continue;                           // no covered position: zeros only
+        const int64_t gs0 = F.fgs[k], len = F.fge[k] - gs0;
+        const int64_t gs = gs0 + len * part / per, ge = gs0 + len * (part + 1) / per;
+        for (int q = threadIdx.x * 4; q < nb; q += kBlock * 4)
+            *reinterpret_cast<i32x4*>(hb + q) = i32x4{0, 0, 0, 0};
+        __syncthreads();
+        int vmax = 0;
+        unsigned vmin = 0xffffffffu;
+        seg_hist(F.depth, gs, ge, hb, nb, vmax, vmin);
+        vmax = wave_max(vmax);
+        const int wmin = wave_min((int)min(vmin, 0x7fffffffu));
+        if ((threadIdx.x & 63) == 0) {
+            ext[threadIdx.x >> 6] = wmin;
+            ext[kWaves + (threadIdx.x >> 6)] = vmax;
+        }
+        __syncthreads();
+        int lo = ext[0], hi = ext[kWaves];
 #pragma unroll
-            for (int q = 1; q < kWaves; ++q) {
-                lo = min(lo, ext[q]);
-                hi = max(hi, ext[kWaves + q]);
-            }
-            // (an empty part leaves lo = INT_MAX > hi: nothing to flush; lo + tid would overflow)
-            if (lo <= hi)
-                for (int q = lo + (int)threadIdx.x; q <= hi && q < nb; q += kBlock) {
-                    const unsigned c = hb[q];
-                    if (c) atomicAdd(&g[q], c);
-                }
-            if (threadIdx.x == 0 && hi > 0) atomicMax(&F.acc[i].max, hi);
+        for (int q = 1; q < kWaves; ++q) {
+            lo = min(lo, ext[q]);
+            hi = max(hi, ext[kWaves + q]);
         }
-        // the last of the region's workgroups derives its row and leaves the
-        // slot zeroed (a second kernel of 512 workgroups did this: 0.03 ms)
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) s_last = atomicAdd(&F.done[i], 1u) == (unsigned)(per - 1);
-        __syncthreads();
-        if (s_last) {
-            __threadfence();
-            region_final_row(g, nb, F.acc[i], F.ntot[r], F.nzx[r], F.out + r, nullptr, 1, 0, 0, 1);
-            __syncthreads();
-            for (int q = threadIdx.x; q < nb; q += kBlock) g[q] = 0;
-            if (threadIdx.x == 0) {
-                F.acc[i].sum = F.acc[i].sumsq = 0;
-                F.acc[i].min = 0x7fffffff;
-                F.acc[i].max = 0;
-                F.done[i] = 0;
-            }
+        unsigned* g = F.hist + (int64_t)i * kLdsBins;
+        // (an empty part leaves lo = INT_MAX > hi: nothing to flush; lo + tid would overflow)
+        if (lo <= hi)
+        for (int q = lo + (int)threadIdx.x; q <= hi && q < nb; q += kBlock) {
+            const unsigned c = hb[q];
+            if (c) atomicAdd(&g[q], c);
         }
+        if (threadIdx.x == 0 && hi > 0) atomicMax(&F.acc[i].max, hi);
         __syncthreads();                               // before the next item zeroes hb
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+fb_final_kernel(FbArgs F) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) F.cnt[F.parity ^ 1] = 0;   // the next call's counter
+    const int n = (int)min(F.cnt[F.parity], (unsigned)kFbSlots);
+    const int maxd = *F.max_depth;
+    const int b = blockIdx.x;
+    if (b >= n || maxd >= kLdsBins) return;
+    const int r = F.list[b];
+    unsigned* hr = F.hist + (int64_t)b * kLdsBins;
+    region_final_row(hr, maxd + 1, F.acc[b], F.ntot[r], F.nzx[r], F.out + r, nullptr, 1, 0, 0, 1);
+    __syncthreads();
+    for (int q = threadIdx.x; q <= maxd; q += kBlock) hr[q] = 0;
+    if (threadIdx.x == 0) {
+        F.acc[b].sum = F.acc[b].sumsq = 0;
+        F.acc[b].min = 0x7fffffff;
+        F.acc[b].max = 0;
     }
 }
 
