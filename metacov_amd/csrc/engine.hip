@@ -1044,6 +1044,18 @@ static K2Geom k2_geom(const mc_ctx* ctx, bool stats) {
     return {ctx->tpc_base, ctx->n_chunks_base, (int64_t)ctx->tpc_base * kTileW, 1};
 }
 
+#ifndef MC_WIN_BELOW
+#define MC_WIN_BELOW (3 * kHistBins / 4)
+#endif
+constexpr int kWinBelow = MC_WIN_BELOW;   // window bins below the estimated body depth
+
+// The direct path's window parameters (direct_window_base): this
+// generation's span sums, the window placement of the short-read variant.
+static DirectWindow direct_window(const mc_ctx* ctx) {
+    return DirectWindow{ctx->d_fsamp.p, ctx->d_len.p, ctx->d_dres.p, (int)(ctx->direct_gen & 1),
+                        (int)((int64_t)kWinBelow * fused_hist_vals(ctx->has_long) / kHistBins)};
+}
+
 // K2 launch (plain or with fused region statistics)
 // ea / eb: K2's start / end events (default ev[4] / ev[5], read lazily by
 // mc_get_timings)
@@ -1081,7 +1093,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     const ReadArrays ra{ctx->d_gpos.p, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p};
     const int64_t n_base = ctx->n_chunks * ctx->cstride;
     const DirectArgs da{ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_len.p, (int32_t)ctx->len.size(),
-                        ctx->d_dres.p, ctx->direct_gen};
+                        ctx->d_dres.p, ctx->direct_gen, direct_window(ctx)};
 #define MC_LAUNCH_K2(S, L, D)                                                                  \
     hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, ra,            \
                        ctx->n_reads, ctx->d_coff.p,                                               \
@@ -1295,10 +1307,6 @@ static int region_stats_impl(mc_ctx* ctx, int64_t R, const int32_t* tid, const i
 // while they are in registers), then the histogram finalize.  Needs regions
 // that do not overlap each other; otherwise K2 then K3.  Regions whose order
 // statistics reach depths >= kHistBins are recomputed by K3.
-#ifndef MC_WIN_BELOW
-#define MC_WIN_BELOW (3 * kHistBins / 4)
-#endif
-constexpr int kWinBelow = MC_WIN_BELOW;   // window bins below the estimated body depth
 
 // Staging layout of a fused call: sorted region arrays (nf), then per-region
 // arrays (R).  The fallback flags come back through ctx->h_fflag.
@@ -1315,7 +1323,7 @@ static FusedLayout fused_layout(int64_t nf, int64_t R) {
     L.ntot = L.base + al(nf * 4);
     L.nzx = L.ntot + al(R * 8);
     L.brow = L.nzx + al(R * 8);
-    L.rtid = L.brow + al(R * 4);        // each row's contig (window_kernel)
+    L.rtid = L.brow + al(R * 4);        // each row's contig (the direct path's windows)
     L.rfused = L.rtid + al(R * 4);      // each row's fused entry, or -1
     L.up = L.rfused + al(R * 4);
     L.total = L.up;
@@ -1331,18 +1339,6 @@ constexpr int kRedo = 1;
 static size_t fflag_ints(int64_t R) { return (size_t)round_up(R + 1, 2) + 2 * kDresWords; }
 static unsigned long long* fflag_dres(int* base, int64_t R) {
     return reinterpret_cast<unsigned long long*>(base + round_up(R + 1, 2));
-}
-
-// Histogram windows of a direct batch: window_kernel from the probe's samples.
-static int launch_window(mc_ctx* ctx, int64_t R, const FusedLayout& L) {
-    if (R == 0) return MC_OK;
-    unsigned char* d = ctx->fstage.d.p;
-    hipLaunchKernelGGL(window_kernel, dim3((unsigned)((R + kWaves - 1) / kWaves)), dim3(kBlock), 0, ctx->stream,
-                       ctx->d_fsamp.p, ctx->d_span.p, ctx->n_reads, ctx->d_len.p,
-                       reinterpret_cast<const int32_t*>(d + L.rtid), reinterpret_cast<const int32_t*>(d + L.rfused),
-                       R, kWinBelow, reinterpret_cast<int32_t*>(d + L.brow), reinterpret_cast<int32_t*>(d + L.base));
-    HIP_TRY(hipGetLastError());
-    return MC_OK;
 }
 
 // K2's verdict on a direct batch outside the fused call (a D2H copy + sync):
@@ -1418,6 +1414,7 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                     d_fge,
                     reinterpret_cast<const int32_t*>(d + o_id),
                     reinterpret_cast<const int32_t*>(d + o_base),
+                    reinterpret_cast<const int32_t*>(d + L.rtid),
                     ctx->d_acc.p,
                     ctx->d_fhist.p,
                     ctx->d_flow.p};
@@ -1467,7 +1464,9 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                        reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,                 \
                        ctx->d_maxdepth.p, ctx->h_fflag.d + R, ctx->d_queue.p,                       \
                        verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr, \
-                       devfb ? F.cnt + F.parity : nullptr, devfb ? F.list : nullptr)
+                       devfb ? F.cnt + F.parity : nullptr, devfb ? F.list : nullptr,                \
+                       ctx->direct ? direct_window(ctx) : DirectWindow{},                          \
+                       ctx->direct ? reinterpret_cast<const int32_t*>(d + L.rtid) : nullptr)
     if (vals == HistCfg<false>::kBins) MC_LAUNCH_K3B(HistCfg<false>::kBins);
     else MC_LAUNCH_K3B(HistCfg<true>::kBins);
 #undef MC_LAUNCH_K3B
@@ -1545,7 +1544,7 @@ static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
     if (int rc = prepare_for_compute(ctx)) return rc;
     MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end)), MC_E_INVALID, "bad region arrays");
     auto& fc = ctx->fcache;
-    // direct batch: the windows come from the probe's samples (window_kernel)
+    // direct batch: K2 and K3b derive the windows from the probe's samples
     const bool direct = ctx->direct;
     // histogram window of each region: kHistBins values, kWinBelow of them
     // below its contig's estimated body depth
@@ -1575,9 +1574,7 @@ static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         // regions, their order and the chunk -> region index stand; only the
         // window bases follow the new per-contig bases (one small upload)
         const FusedLayout L = fused_layout(fc.nf, R);
-        if (direct) {
-            if (int rc = launch_window(ctx, R, L)) return rc;
-        } else if (R > 0) {
+        if (!direct && R > 0) {   // (direct: K2 and K3b derive the windows from the probe's samples)
             // from ingest's per-contig bases, still in d_scratch, on the
             // device (the host loop over the rows and its upload were 0.05 ms
             // between C5's prepare and K2)
@@ -1645,8 +1642,6 @@ static int depth_stats_once(mc_ctx* ctx, int64_t R, const int32_t* tid, const in
         for (int64_t k = 0; k < nf; ++k) rf[regs[k].id] = (int32_t)k;
     }
     HIP_TRY(hipMemcpyAsync(ctx->fstage.d.p, h, L.up, hipMemcpyHostToDevice, ctx->stream));
-    if (direct)
-        if (int rc = launch_window(ctx, R, L)) return rc;
     fc.tid.assign(tid, tid + R);
     fc.start.assign(start, start + R);
     fc.end.assign(end, end + R);

@@ -622,12 +622,11 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 //                  targets in that interval (usually none or one): no search.
 //                  lb(P), the first read with key >= P, then lies in
 //                  ((J-1)*S, J*S].  The same sweep gives each contig's first
-//                  sample (fsamp, for the histogram windows) and flags
-//                  unsorted or invalid samples and long spans.
-//   window_kernel  each fused region's histogram window from its contig's
-//                  samples (count x mean span over the contig length).
+//                  sample and the sampled spans' sum (for the histogram
+//                  windows: direct_window_base) and flags unsorted or
+//                  invalid samples and long spans.
 //   depth_kernel<.., kDirect = true>  chunk c loads the reads in
-//                  [lower(J(C0 - short_max)), upper(J(C0 + W))) as raw
+//                  [lower(J(C0 - halo)), upper(J(C0 + W))) as raw
 //                  (tid, pos, span), applies those that overlap it, and
 //                  validates the reads in [lower(J(C0)), lower(J(C0 + W))):
 //                  these ranges partition [0, n) whenever the samples are
@@ -649,7 +648,9 @@ enum : int {
     kDresFlags = 2,          // K2: kDirectInvalid | kDirectUnfit
     kDresBases = 3,          // span_sum_kernel: aligned bases (on request)
     kDresMaxSpan = 4,        // K2: the batch's maximum span (atomicMax per workgroup)
-    kDresWords = 5
+    kDresSpanSum = 5,        // probe: sampled spans' sum / count, [5, 6] for even generations, [7, 8] for
+    kDresSpanCnt = 6,        //   odd ones (each probe zeroes the other pair for the next batch)
+    kDresWords = 9
 };
 constexpr unsigned kDirectInvalid = 1;   // an invalid or unsorted read: mc_prepare's error
 constexpr unsigned kDirectUnfit = 2;     // a read past its contig's end (long reads: kDresMaxSpan)
@@ -671,6 +672,35 @@ struct ProbeArgs {
     unsigned long long* dres;
     unsigned long long gen;
 };
+
+// The histogram window of a region on the direct path, from the probe's
+// samples: its contig's reads ~ (samples of the contig) x S, the mean span of
+// the sampled spans, its depth over the contig less one mean span (the same
+// estimate the full prepare makes from exact per-contig bases), kWinBelow
+// bins of the window below it.  K2 and K3b both evaluate it, bit for bit
+// alike (a window_kernel launch between the probe and K2 was 0.012 ms of a
+// C3 step with its gap).
+struct DirectWindow {
+    const int32_t* fsamp;              // [nc + 1] first sample of each contig (probe)
+    const int64_t* len;                // [nc]
+    const unsigned long long* dres;    // the span sums of this generation at [kDresSpanSum + 2 * parity]
+    int parity;
+    int win_below;
+};
+
+__device__ __forceinline__ int direct_window_base(const DirectWindow& W, int t) {
+    const long long ns = (long long)uload(W.fsamp, t + 1) - uload(W.fsamp, t);
+    const unsigned long long ssum = uload(W.dres, kDresSpanSum + 2 * W.parity);
+    const unsigned long long scnt = uload(W.dres, kDresSpanCnt + 2 * W.parity);
+    if (ns <= 0 || scnt == 0) return 0;
+    const double mean = (double)ssum / (double)scnt;
+    const double bases = (double)ns * (double)kProbeStride * mean;
+    const double ext = (double)uload(W.len, t);
+    const double body = ext > 2.0 * mean ? ext - mean : ext;
+    const double est = ext > 0 ? bases / body : 0.0;
+    const long long b0 = llrint(est) - W.win_below;
+    return b0 > 0 ? (int)b0 : 0;
+}
 
 __device__ __forceinline__ int64_t probe_key(const ProbeArgs& A, int t, int p) {
     const int ct = t < 0 ? 0 : t >= A.nc ? A.nc - 1 : t;
@@ -698,13 +728,45 @@ __device__ __forceinline__ void probe_fill(int32_t* J, int64_t n_base, int lw, i
 // stride 4 S (only the long-read flag reads it: a long read the sparser
 // sample misses is still caught by K2's check)
 constexpr int kProbeSpanEvery = 4;
+constexpr unsigned kProbeMeanBlocks = 64;
 
 __global__ void __launch_bounds__(kBlock)
 probe_kernel(ProbeArgs A) {
     const int64_t M = (A.n + kProbeStride - 1) >> kProbeShift;
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x >= kDresFlags && threadIdx.x < kDresWords)
-        A.dres[threadIdx.x] = 0;   // K2's counters (K2 runs after this launch)
+    const int par = (int)(A.gen & 1);
+    // K2's counters (K2 runs after this launch) and the next generation's span sums
+    if (blockIdx.x == 0 && threadIdx.x >= kDresFlags && threadIdx.x <= kDresMaxSpan) A.dres[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 2) A.dres[kDresSpanSum + 2 * (par ^ 1) + threadIdx.x] = 0;
+    const bool sampled = j < M && (j % kProbeSpanEvery) == 0;
+    const int s0 = sampled ? A.span[j << kProbeShift] : 0;
+    // the mean span for the windows: the sampled spans of kProbeMeanBlocks
+    // workgroups spread over the batch, one atomic pair per workgroup (one
+    // pair per wave of all workgroups, on one address, serialised: +0.1 ms)
+    const unsigned every = max(1u, gridDim.x / kProbeMeanBlocks);
+    if (blockIdx.x % every == 0) {
+        __shared__ long long red[2 * kWaves];
+        const bool s_ok = sampled && s0 >= 0;
+        const long long wsum = wave_sum64(s_ok ? (long long)s0 : 0);
+        const long long wcnt = wave_sum64(s_ok ? 1 : 0);
+        if ((threadIdx.x & 63) == 0) {
+            red[threadIdx.x >> 6] = wsum;
+            red[kWaves + (threadIdx.x >> 6)] = wcnt;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long ts = 0, tc = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                ts += red[w];
+                tc += red[kWaves + w];
+            }
+            if (tc) {
+                atomicAdd(&A.dres[kDresSpanSum + 2 * par], (unsigned long long)ts);
+                atomicAdd(&A.dres[kDresSpanCnt + 2 * par], (unsigned long long)tc);
+            }
+        }
+    }
     if (j >= M) return;
     const bool last = j == M - 1;
     // this sample and the next one, all loads issued together (the next
@@ -712,7 +774,7 @@ probe_kernel(ProbeArgs A) {
     const int64_t i = j << kProbeShift, i1 = last ? i : i + kProbeStride;
     const int t = A.tid[i], p = A.pos[i];
     const int t_next = A.tid[i1], p_next = A.pos[i1];
-    const int s = (j % kProbeSpanEvery) == 0 ? A.span[i] : 0;
+    const int s = s0;
     const int64_t key = probe_key(A, t, p);
     const int64_t key_next = probe_key(A, t_next, p_next);
     const bool bad = ((unsigned)t >= (unsigned)A.nc) | (p < 0) | (s < 0);
@@ -728,48 +790,6 @@ probe_kernel(ProbeArgs A) {
     if (first)
         for (int k = 0; k <= ct; ++k) A.fsamp[k] = 0;
     for (int k = ct + 1; k <= cn; ++k) A.fsamp[k] = (int32_t)(j + 1);
-}
-
-// One wave per region row: the window base of its histogram from its
-// contig's samples (the same estimate the full prepare makes from exact
-// per-contig bases: depth over the contig less one mean read span, kWinBelow
-// bins of the window below it).  Writes the row's base and its fused entry's.
-__global__ void __launch_bounds__(kBlock)
-window_kernel(const int32_t* __restrict__ fsamp, const int32_t* __restrict__ span, int64_t n,
-              const int64_t* __restrict__ len, const int32_t* __restrict__ rtid,
-              const int32_t* __restrict__ rfused, int64_t R, int win_below,
-              int32_t* __restrict__ brow, int32_t* __restrict__ fbase) {
-    const int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= R) return;
-    const int t = rtid[r];
-    const int64_t a = fsamp[t], b = fsamp[t + 1];
-    const int64_t ns = b - a;
-    // up to 256 of the contig's samples, evenly strided: four independent
-    // loads per lane (the mean span to ~2 % at C3, ~3 % at C5's lognormal spans)
-    const int64_t take = ns < 256 ? ns : 256;
-    long long sum = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int64_t k = lane + 64 * u;
-        const int64_t i = k < take ? (a + k * ns / take) << kProbeShift : n;
-        sum += i < n ? span[i] : 0;
-    }
-    sum = wave_sum64(sum);
-    if (lane != 0) return;
-    int32_t base = 0;
-    if (ns > 0 && take > 0) {
-        const double mean = (double)sum / (double)take;
-        const double bases = (double)ns * (double)kProbeStride * mean;
-        const double ext = (double)len[t];
-        const double body = ext > 2.0 * mean ? ext - mean : ext;
-        const double est = ext > 0 ? bases / body : 0.0;
-        const long long b0 = llrint(est) - win_below;
-        base = (int32_t)(b0 > 0 ? b0 : 0);
-    }
-    brow[r] = base;
-    const int32_t k = rfused[r];
-    if (k >= 0) fbase[k] = base;
 }
 
 // The full prepare's window bases on the device (a repeated call over the
@@ -1329,6 +1349,7 @@ struct DirectArgs {
     int32_t nc;
     unsigned long long* dres;
     unsigned long long gen;
+    DirectWindow win;                  // the fused regions' window bases (direct_window_base)
 };
 
 struct DirectChunk {                   // wave-uniform per chunk
@@ -1547,7 +1568,8 @@ struct FusedRegions {
     const int64_t* gs;                 // [n] global start (sorted)
     const int64_t* ge;                 // [n] global end (clipped to the contig extent)
     const int32_t* id;                 // [n] caller's row index
-    const int32_t* base;               // [n] value of histogram bin 0 (window base)
+    const int32_t* base;               // [n] value of histogram bin 0 (window base; direct: computed)
+    const int32_t* rtid;               // [rows] each row's contig (direct path's window)
     RegionAcc* acc;                    // [rows] statistics of the values outside the window
     unsigned* hist;                    // [rows][HistCfg<kLong>::kBins]
     unsigned* low;                     // [rows] count of values below the window
@@ -1870,8 +1892,8 @@ depth_kernel(ReadArrays A, int64_t n,
             if (rcur < R.n) {
                 r_gs = uload(R.gs, rcur);
                 r_ge = uload(R.ge, rcur);
-                r_base = uload(R.base, rcur);
                 r_id = uload(R.id, rcur);
+                r_base = kDirect ? direct_window_base(D.win, uload(R.rtid, r_id)) : uload(R.base, rcur);
             }
         }
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
@@ -2045,8 +2067,9 @@ depth_kernel(ReadArrays A, int64_t n,
                         if (rcur < R.n) {
                             r_gs = uload(R.gs, rcur);
                             r_ge = uload(R.ge, rcur);
-                            r_base = uload(R.base, rcur);
                             r_id = uload(R.id, rcur);
+                            r_base = kDirect ? direct_window_base(D.win, uload(R.rtid, r_id))
+                                             : uload(R.base, rcur);
                         }
                     } else {
                         break;
@@ -2502,7 +2525,8 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
                          unsigned* __restrict__ low_of, int* __restrict__ max_depth,
                          int* __restrict__ max_out, unsigned* __restrict__ queue,
                          const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out,
-                         unsigned* __restrict__ fb_cnt, int32_t* __restrict__ fb_list) {
+                         unsigned* __restrict__ fb_cnt, int32_t* __restrict__ fb_list,
+                         DirectWindow dwin, const int32_t* __restrict__ rtid) {
     constexpr int kFinPer = (kVals + 63) / 64;
     const int lane = threadIdx.x & 63;
     // dres_out (mapped host memory): the direct K2's validation counters, so
@@ -2523,7 +2547,8 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     unsigned* hr = hist + r * kVals;
     const long long n = n_total[r];
     const long long zx = n_zero_extra[r];
-    const long long base = base_of[r];
+    // (direct path: the window K2 used, from the probe's samples)
+    const long long base = rtid ? direct_window_base(dwin, __builtin_amdgcn_readfirstlane(rtid[r])) : base_of[r];
     const long long zx_bin = base == 0 ? zx : 0;
     const long long low = (long long)low_of[r] + (base == 0 ? 0 : zx);
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;
