@@ -621,6 +621,13 @@ static void resolve_timings(mc_ctx* ctx, bool all) {
 // (its chunk-end flushes double) and reads its chunk c as base chunks
 // [c*s, c*s + s).  Long reads' end buckets and carries are per full
 // chunk, so with long reads the plain K2 runs on full chunks too.
+// chunks are halved while a layout would have fewer than this many: a
+// strong-scaling shard (C3 / 8: 3.8 k chunks of 8 tiles for 1024 resident
+// workgroups) runs K2 2.5 % faster on 4-tile chunks; 8192 was 33 % slower
+// (profiles/r03ii_min_chunks_ab.txt)
+#ifndef MC_MIN_CHUNKS
+#define MC_MIN_CHUNKS 4096
+#endif
 static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     const int32_t nc = (int32_t)ctx->len.size();
     ctx->extent = ext;
@@ -638,7 +645,7 @@ static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     const int top = ctx->long_hint ? kTilesPerChunkLong : kTilesPerChunk;
     const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : top;
     int tpc = top;
-    while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < 2048 &&
+    while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < MC_MIN_CHUNKS &&
            ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
         tpc /= 2;
     ctx->tiles_per_chunk = tpc;

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reads", type=int, default=100_000_000)
+    ap.add_argument("--contigs", type=int, default=None, help="(c3) contigs, e.g. a strong-scaling shard")
     ap.add_argument("--nocheck", action="store_true", help="deliberately-wrong experiment builds")
     ap.add_argument("--config", default="c3", choices=["c3", "c5"])
     a = ap.parse_args()
@@ -36,7 +37,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     reads = a.reads if a.config == "c3" else CONFIGS[a.config][0]
-    lengths, weights = config_contigs(a.config, reads, CONFIGS[a.config][1])
+    lengths, weights = config_contigs(a.config, reads, a.contigs or CONFIGS[a.config][1])
     tid, pos, span, _ = device_workload(torch, lengths, weights, reads, 1, dev,
                                         long_reads=a.config == "c5")
     R = len(lengths)
