@@ -306,12 +306,19 @@ def main():
     table = torch.empty((R, 9), dtype=torch.int64, device=dev)
     gathered = None
 
-    gbuf = coll_buf = gout = None
-    if world > 1:   # exchange buffers, allocated once: [r_max, 9 stats + region index]
-        gbuf = torch.full((r_max, mdist.ROW_WIDTH), -1, dtype=torch.int64, device=dev)
-        gbuf[:R, 9] = torch.from_numpy(np.asarray(region_index, np.int64)).to(dev)
-        coll_buf = gbuf if coll_dev == dev else gbuf.to(coll_dev)
-        gout = torch.empty((world * r_max, mdist.ROW_WIDTH), dtype=torch.int64, device=coll_dev)
+    xbuf = coll_buf = gout = gidx = None
+    if world > 1:
+        # exchange buffers, allocated once: [r_max, 9 stats]; the engine writes
+        # its rows straight into the first R (no copy per step), and the rows'
+        # original region indices are gathered once here, not every step
+        xbuf = torch.full((r_max, 9), -1, dtype=torch.int64, device=dev)
+        table = xbuf[:R]
+        ibuf = torch.full((r_max, 1), -1, dtype=torch.int64, device=coll_dev)
+        ibuf[:R, 0] = torch.from_numpy(np.asarray(region_index, np.int64)).to(coll_dev)
+        gidx = torch.empty((world * r_max, 1), dtype=torch.int64, device=coll_dev)
+        dist.all_gather_into_tensor(gidx, ibuf)
+        coll_buf = xbuf if coll_dev == dev else torch.empty((r_max, 9), dtype=torch.int64, device=coll_dev)
+        gout = torch.empty((world * r_max, 9), dtype=torch.int64, device=coll_dev)
 
     def step(fresh):
         """One pass of the hot path over the resident batch.  fresh: the
@@ -329,10 +336,9 @@ def main():
             eng.region_stats_device(rt, rs, re_, table.data_ptr())
         else:
             eng.compute_depth_stats_device(rt, rs, re_, table.data_ptr())
-        if world > 1:   # rows into the padded exchange table (index column preset), one all-gather
-            gbuf[:R, :9].copy_(table)
-            if coll_buf is not gbuf:
-                coll_buf.copy_(gbuf)
+        if world > 1:   # the rows are in the exchange buffer already: one all-gather
+            if coll_buf is not xbuf:   # (gloo: through host memory)
+                coll_buf.copy_(xbuf)
             dist.all_gather_into_tensor(gout, coll_buf)
             gathered = gout
 
@@ -410,7 +416,8 @@ def main():
         b = torch.tensor([bases], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(b)
         total_bases = int(b.item())
-        rows = mdist.unpack_rows(gathered.cpu().numpy(), n_regions_total, REGION_STAT_DTYPE)
+        full = torch.cat([gathered, gidx], dim=1)   # [world * r_max, 9 stats + region index]
+        rows = mdist.unpack_rows(full.cpu().numpy(), n_regions_total, REGION_STAT_DTYPE)
         assert int(rows["sum"].sum()) == total_bases, "gathered region table lost bases"
     else:
         rows = table.cpu().numpy().view(REGION_STAT_DTYPE).reshape(-1)
