@@ -493,10 +493,11 @@ def main():
                         "lognormal ~10 kbp spans" if args.config == "c5" else "SURVEY §8d span mix",
                         ", BAM CIGAR words generated on the GPU" if args.cigar else "")),
             "config": {
-                "workload": ("%s LPT-sharded by contig over %d GPUs (%s)"
+                "workload": ("one %s workload LPT-sharded by contig over %d GPUs (the whole workload: %s)"
                              % (args.config.upper(), world,
-                                desc % args.reads if args.config == "c2" else
-                                desc % (args.contigs, lengths_all.sum() / 1e9, args.reads)))
+                                (desc % args.reads if args.config == "c2" else
+                                 desc % (args.contigs, lengths_all.sum() / 1e9, args.reads))
+                                .replace("%s per GPU: " % args.config.upper(), "")))
                             if strong and world > 1 else
                             (desc % args.reads if args.config == "c2" else
                              desc % (args.contigs, lengths_all.sum() / 1e9, args.reads)),
