@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of two K2 builds: direct (C3), fused on the packed words (C3), fused C5;
+# A/B of K2 builds (LIBS="a.so b.so ..."): direct (C3), fused on the packed words (C3), fused C5;
 # then the GPU tests of the histogram path.  Stops on a fault.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
