@@ -111,15 +111,21 @@ def test_synth_bams(eng, synth_golden, golden_dir, tag):
 
 
 @pytest.mark.parametrize("tag", ["synth_edge", "synth_longcigar"])
-def test_cigar_mode(eng, golden_dir, tag):
+def test_cigar_mode(eng, synth_golden, golden_dir, tag):
+    """K1 (raw CIGAR words -> span on the GPU, CG-tag CIGARs included) against
+    the oracle: the depth of the golden intervals, which the pure-Python BAM
+    reader decoded with its own bam_cigar2rlen rule (oracle/bamread.py)."""
+    g = synth_golden[tag]
     bf = BamFile(os.path.join(golden_dir, tag + ".bam"), keep_cigar=True)
-    eng.set_contigs(np.asarray(bf.lengths, np.int64))
+    lengths = np.asarray(bf.lengths, np.int64)
+    eng.set_contigs(lengths)
     eng.add_reads_cigar(bf.tid, bf.pos, bf.cig_off, bf.cigar)
     eng.compute_depth()
-    got = [eng.depth(t) for t in range(len(bf.lengths))]
-    run_engine(eng, bf.lengths, bf.tid, bf.pos, bf.span)
-    for t in range(len(bf.lengths)):
-        assert np.array_equal(got[t], eng.depth(t))
+    tid, pos, span = [np.array(g["intervals"][k], np.int32) for k in ("tid", "pos", "span")]
+    d, ext, coff = coracle.depth(lengths, tid, pos, span)
+    for t in range(len(lengths)):
+        assert np.array_equal(eng.depth(t, 0, int(ext[t])), d[coff[t]:coff[t] + ext[t]]), t
+    assert eng.aligned_bases() == int(span.astype(np.int64).sum())
 
 
 # ------------------------------------------------------------- oracle parity
