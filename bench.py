@@ -520,7 +520,7 @@ def main():
             "prepare_path": {"direct_batches": paths["direct"], "full_prepares": paths["full"],
                              "halo_redos": paths["halo_redos"], "chunk_halo_positions": paths["halo"]},
             "kernels_ms": {**({"k1_cigar_span": k1_ms} if args.cigar else {}),
-                           "prepare" + ("_probe_window" if head_direct else "_ingest_index"): kp_ms,
+                           "prepare" + ("_probe" if head_direct else "_ingest_index"): kp_ms,
                            "k2_depth" + ("" if args.unfused else "_fused_stats"): k2_ms,
                            ("k3_region_stats" if args.unfused else "k3b_finalize"): k3_ms},
             "fused_fallback_regions": None if args.unfused else eng.fused_fallbacks(),
