@@ -1239,6 +1239,70 @@ def test_direct_halo_follows_the_spans(lib_built):
         e.close()
 
 
+def _fuzz_batch(rng):
+    """A random batch: contig count / lengths from tiny to 300 kbp (some
+    empty), a span mix of zero, short, N-skip-like and (sometimes) long
+    spans, deep piles at one start, optional overhangs; sorted."""
+    nc = int(rng.integers(1, 40))
+    lengths = rng.integers(0, 300_000, size=nc).astype(np.int64)
+    lengths[rng.random(nc) < 0.1] = 0
+    lengths[rng.random(nc) < 0.1] = rng.integers(1, 100)
+    live = np.nonzero(lengths > 0)[0]
+    if len(live) == 0:
+        lengths[0] = 5000
+        live = np.array([0])
+    n = int(rng.integers(1, 60_000))
+    tid = rng.choice(live, size=n).astype(np.int32)
+    span = rng.integers(0, 300, size=n)
+    u = rng.random(n)
+    span[u < 0.01] = rng.integers(300, 4000, size=int((u < 0.01).sum()))
+    if rng.random() < 0.3:
+        span[u > 0.9995] = rng.integers(4097, 20_000, size=int((u > 0.9995).sum()))
+    pos = (rng.random(n) * lengths[tid]).astype(np.int64)
+    if rng.random() < 0.5:   # no overhang
+        span = np.minimum(span, lengths[tid] - pos)
+    if rng.random() < 0.3:   # a deep pile at one start
+        k = int(rng.integers(0, n))
+        pos[max(0, k - 500):k] = pos[k]
+        tid[max(0, k - 500):k] = tid[k]
+    o = np.lexsort((pos, tid))
+    return lengths, tid[o], pos[o].astype(np.int32), span[o].astype(np.int32)
+
+
+def test_direct_and_full_fuzz(lib_built):
+    """Random batches through one ctx (the direct path with its halo carried
+    from batch to batch, the full prepare for long reads and overhangs):
+    depth, whole-contig fused rows and random-region rows equal the oracle."""
+    rng = np.random.default_rng(2024)
+    e = _fresh(lib_built)
+    try:
+        for k in range(24):
+            lengths, tid, pos, span = _fuzz_batch(rng)
+            e.set_contigs(lengths)
+            e.add_reads(tid, pos, span)
+            d, ext, coff = coracle.depth(lengths, tid, pos, span)
+            rt = np.arange(len(lengths), dtype=np.int32)
+            rs = np.zeros(len(lengths), np.int64)
+            re_ = np.asarray(ext, np.int64)
+            want = coracle.region_stats(d, ext, coff, rt, rs, re_)
+            got = e.compute_depth_stats(rt, rs, re_)
+            for f in want.dtype.names:
+                assert np.array_equal(got[f], want[f]), (k, f)
+            check_depth_vs_oracle(e, lengths, tid, pos, span)
+            check_regions_vs_oracle(e, d, ext, coff, *random_regions(rng, lengths, 50))
+            # the same contigs, a second batch: the direct path with the halo the first one set
+            e.clear_reads()
+            lengths2, tid2, pos2, span2 = lengths, tid, pos, np.maximum(span - 1, 0).astype(np.int32)
+            e.add_reads(tid2, pos2, span2)
+            d2, ext2, coff2 = coracle.depth(lengths2, tid2, pos2, span2)
+            got2 = e.compute_depth_stats(rt, rs, np.asarray(ext2, np.int64))
+            want2 = coracle.region_stats(d2, ext2, coff2, rt, rs, np.asarray(ext2, np.int64))
+            for f in want2.dtype.names:
+                assert np.array_equal(got2[f], want2[f]), (k, "second", f)
+    finally:
+        e.close()
+
+
 def test_direct_ctx_sticks_to_full_after_long_reads(lib_built):
     lengths, tid, pos, span = make_case([300_000], 8_000, (1, 150), 45, overhang=False)
     span_long = span.copy()
