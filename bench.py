@@ -306,26 +306,39 @@ def main():
     table = torch.empty((R, 9), dtype=torch.int64, device=dev)
     gathered = None
 
-    xbuf = coll_buf = gout = gidx = None
+    xbufs = coll_bufs = gouts = gidx = None
+    works = [None, None]   # in-flight all-gathers, one per exchange buffer
+    n_calls = [0]
     if world > 1:
-        # exchange buffers, allocated once: [r_max, 9 stats]; the engine writes
-        # its rows straight into the first R (no copy per step), and the rows'
-        # original region indices are gathered once here, not every step
-        xbuf = torch.full((r_max, 9), -1, dtype=torch.int64, device=dev)
-        table = xbuf[:R]
+        # two exchange buffers, allocated once: [r_max, 9 stats]; the engine
+        # writes a batch's rows straight into the first R of one (no copy per
+        # step) while the previous batch's all-gather may still read the other,
+        # and the rows' original region indices are gathered once here
+        xbufs = [torch.full((r_max, 9), -1, dtype=torch.int64, device=dev) for _ in range(2)]
         ibuf = torch.full((r_max, 1), -1, dtype=torch.int64, device=coll_dev)
         ibuf[:R, 0] = torch.from_numpy(np.asarray(region_index, np.int64)).to(coll_dev)
         gidx = torch.empty((world * r_max, 1), dtype=torch.int64, device=coll_dev)
         dist.all_gather_into_tensor(gidx, ibuf)
-        coll_buf = xbuf if coll_dev == dev else torch.empty((r_max, 9), dtype=torch.int64, device=coll_dev)
-        gout = torch.empty((world * r_max, 9), dtype=torch.int64, device=coll_dev)
+        coll_bufs = [x if coll_dev == dev else torch.empty((r_max, 9), dtype=torch.int64, device=coll_dev)
+                     for x in xbufs]
+        gouts = [torch.empty((world * r_max, 9), dtype=torch.int64, device=coll_dev) for _ in range(2)]
 
     def step(fresh):
         """One pass of the hot path over the resident batch.  fresh: the
         batch is new to the engine (mc_invalidate first), so the step
         prepares it — the direct path: probe + validating K2 — before K2 and
-        K3b; otherwise K2 reuses the index an explicit prepare() built."""
+        K3b; otherwise K2 reuses the index an explicit prepare() built.
+        For N > 1 the batch's rows leave in an asynchronous all-gather that
+        runs under the next batch's kernels; drain() waits for the last."""
         nonlocal gathered
+        i = n_calls[0] & 1
+        n_calls[0] += 1
+        tbl = table
+        if world > 1:
+            if works[i] is not None:   # this buffer's previous gather must be done
+                works[i].wait()
+                works[i] = None
+            tbl = xbufs[i][:R]
         if args.cigar:   # a fresh raw-CIGAR batch: K1 + prepare run inside this step
             eng.clear_reads()
             eng.add_reads_cigar_device(tid, pos, cig_off, cigar)
@@ -333,16 +346,23 @@ def main():
             eng.invalidate()
         if args.unfused:
             eng.compute_depth()
-            eng.region_stats_device(rt, rs, re_, table.data_ptr())
+            eng.region_stats_device(rt, rs, re_, tbl.data_ptr())
         else:
-            eng.compute_depth_stats_device(rt, rs, re_, table.data_ptr())
+            eng.compute_depth_stats_device(rt, rs, re_, tbl.data_ptr())
         if world > 1:   # the rows are in the exchange buffer already: one all-gather
-            if coll_buf is not xbuf:   # (gloo: through host memory)
-                coll_buf.copy_(xbuf)
-            dist.all_gather_into_tensor(gout, coll_buf)
-            gathered = gout
+            if coll_bufs[i] is not xbufs[i]:   # (gloo: through host memory)
+                coll_bufs[i].copy_(xbufs[i])
+            works[i] = dist.all_gather_into_tensor(gouts[i], coll_bufs[i], async_op=True)
+            gathered = gouts[i]
+
+    def drain():
+        for j, w in enumerate(works):
+            if w is not None:
+                w.wait()
+                works[j] = None
 
     def sync_all():
+        drain()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -402,7 +422,7 @@ def main():
         sync_all()
         ta = time.perf_counter()
         for _ in range(n_ag):
-            dist.all_gather_into_tensor(gout, coll_buf)
+            dist.all_gather_into_tensor(gouts[0], coll_bufs[0])
         torch.cuda.synchronize()
         allgather_ms = (time.perf_counter() - ta) / n_ag * 1e3
     t_max, t_max_re = elapsed, elapsed_re
