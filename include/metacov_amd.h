@@ -295,6 +295,48 @@ int mc_bam_open_contigs(const char* path, const char* bai_path, int n_threads,
                         uint32_t flag_filter, int keep_cigar, int32_t n_sel,
                         const int32_t* sel, mc_bam** out);
 
+/* ---- GPU BAM decode ------------------------------------------------------
+ * The records mc_bam_open keeps (same intervals in file order, same record /
+ * mapped / unmapped counts, same error classes), decoded on `device`: the
+ * host reads the file (n_threads pread threads into pinned staging, 0 = 16)
+ * and scans the BGZF block headers; one GPU lane inflates each BGZF block,
+ * and the BAM records are found and parsed per 64 KiB segment of the
+ * inflated stream (csrc/bam_gpu.hip).  window_bytes: inflated bytes per
+ * window (0 = 4 GiB); a record cut by a window is carried to the next.
+ * The kept intervals stay in device memory owned by the handle
+ * (mc_bam_gpu_intervals_device: valid until mc_bam_gpu_close; hand them to
+ * mc_add_reads_device).  Replaces, like mc_bam_open, the record walk under
+ * pysam's pileup (IteratorRowAll, scan.pyx:204-216). */
+typedef struct mc_bam_gpu mc_bam_gpu;
+typedef struct mc_bam_gpu_timings {
+    double read_ms;      /* host: file read + upload of the compressed windows */
+    double inflate_ms;   /* gz_inflate_kernel (HIP events) */
+    double parse_ms;     /* record sync / walk / fill, with their host checks */
+    double total_ms;     /* the whole mc_bam_gpu_open */
+    int64_t windows;
+    int64_t blocks;
+    int64_t resyncs;     /* segment starts corrected after a walk (sync false positives) */
+    int64_t compressed_bytes;
+    int64_t inflated_bytes;
+} mc_bam_gpu_timings;
+int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
+                    int64_t window_bytes, mc_bam_gpu** out);
+int mc_bam_gpu_header(const mc_bam_gpu* g, const mc_bam** header);
+int mc_bam_gpu_intervals_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_tid,
+                                const int32_t** d_pos, const int32_t** d_span);
+int mc_bam_gpu_intervals(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int32_t* span);
+int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t);
+int mc_bam_gpu_close(mc_bam_gpu* g);
+/* Test hooks (no GPU): the lane decoder of the inflate kernel and the record
+ * parse of the walk kernels, run on the host.  mc_gz_inflate_host: one raw
+ * deflate stream into exactly isize bytes (MC_E_IO otherwise).
+ * mc_bam_rec_parse_host: record body r[0, len) after block_size -> 0
+ * dropped, 1 kept (out3 = tid, pos, span), 2 tid beyond n_ref, 3 CIGAR
+ * overruns, 4 span exceeds int32. */
+int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize);
+int mc_bam_rec_parse_host(const uint8_t* r, int64_t len, int32_t n_ref, uint32_t flag_filter,
+                          int32_t* out3);
+
 /* ---- synthetic BAM writer ------------------------------------------------
  * Writes coordinate-sorted records from SoA arrays as BGZF-compressed BAM
  * (blocks deflated on n_threads threads; level = zlib level).  The role of

@@ -58,6 +58,14 @@ class Timings(ctypes.Structure):
                 ("halo_redos", ctypes.c_int64), ("direct_halo", ctypes.c_int64)]
 
 
+class GpuDecodeTimings(ctypes.Structure):
+    """mc_bam_gpu_timings."""
+    _fields_ = [("read_ms", ctypes.c_double), ("inflate_ms", ctypes.c_double),
+                ("parse_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("windows", ctypes.c_int64), ("blocks", ctypes.c_int64), ("resyncs", ctypes.c_int64),
+                ("compressed_bytes", ctypes.c_int64), ("inflated_bytes", ctypes.c_int64)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -121,6 +129,14 @@ SIGNATURES = {
                             _P, _PP],
     "mc_bam_write": [ctypes.c_char_p, _I32, _P, _P, _I64, _P, _P, _P, _P, _P, _I32, ctypes.c_int,
                      ctypes.c_int],
+    "mc_bam_gpu_open": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _U32, _I64, _PP],
+    "mc_bam_gpu_header": [_P, _PP],
+    "mc_bam_gpu_intervals_device": [_P, _PI64, _PP, _PP, _PP],
+    "mc_bam_gpu_intervals": [_P, _P, _P, _P],
+    "mc_bam_gpu_stats": [_P, _P],
+    "mc_bam_gpu_close": [_P],
+    "mc_gz_inflate_host": [_P, _I64, _P, _I64],
+    "mc_bam_rec_parse_host": [_P, _I64, _I32, _U32, _P],
     # pileup.experimental: read side (host) and sequence side (GPU)
     "mc_reads_open": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _PP],
     "mc_reads_close": [_P],

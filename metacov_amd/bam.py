@@ -233,6 +233,109 @@ class BamStream:
         self.close()
 
 
+def _header_of(lib, hdr):
+    n = ctypes.c_int32()
+    check(lib.mc_bam_n_targets(hdr, ctypes.byref(n)))
+    names, lengths = [], []
+    for i in range(n.value):
+        nm = ctypes.c_char_p()
+        ln = ctypes.c_int64()
+        check(lib.mc_bam_target(hdr, i, ctypes.byref(nm), ctypes.byref(ln)))
+        names.append(nm.value.decode())
+        lengths.append(ln.value)
+    c = [ctypes.c_int64() for _ in range(4)]
+    check(lib.mc_bam_counts(hdr, *[ctypes.byref(x) for x in c]))
+    return tuple(names), tuple(lengths), (c[0].value, c[2].value, c[3].value)
+
+
+class GpuBamFile:
+    """The whole file decoded on the GPU (mc_bam_gpu_*: BGZF inflate and
+    record parse in HBM).  Same header, counts and kept intervals as
+    BamFile(path); the intervals stay on `device` and go into the engine by
+    a device copy (mc_add_reads_device).  Offers what the CLI uses of
+    BamFile: references, lengths, mapped, unmapped, engine(), local_tid()."""
+
+    def __init__(self, path, device=0, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0):
+        self.filename = os.fspath(getattr(path, "filename", path))
+        self.contigs = None
+        self.device = device
+        self._lib = _lib.load()
+        self._h = ctypes.c_void_p()
+        check(self._lib.mc_bam_gpu_open(self.filename.encode(), int(device), int(n_threads),
+                                        int(flag_filter), int(window_bytes), ctypes.byref(self._h)))
+        hdr = ctypes.c_void_p()
+        check(self._lib.mc_bam_gpu_header(self._h, ctypes.byref(hdr)))
+        self.references, self.lengths, (self.n_records, self.mapped, self.unmapped) = \
+            _header_of(self._lib, hdr)
+        n = ctypes.c_int64()
+        self._dptr = [ctypes.c_void_p() for _ in range(3)]
+        check(self._lib.mc_bam_gpu_intervals_device(self._h, ctypes.byref(n),
+                                                    *[ctypes.byref(p) for p in self._dptr]))
+        self.n_kept = n.value
+        self._eng = None
+
+    @property
+    def nreferences(self):
+        return len(self.references)
+
+    def get_tid(self, name):
+        try:
+            return self.references.index(name)
+        except ValueError:
+            raise KeyError(name)
+
+    def local_tid(self, tid):
+        return tid
+
+    def intervals(self):
+        """(tid, pos, span) copied to host numpy arrays (tests)."""
+        out = tuple(np.empty(self.n_kept, np.int32) for _ in range(3))
+        if self.n_kept:
+            check(self._lib.mc_bam_gpu_intervals(self._h, *[_lib.ptr(a) for a in out]))
+        return out
+
+    def timings(self):
+        t = _lib.GpuDecodeTimings()
+        check(self._lib.mc_bam_gpu_stats(self._h, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+    def engine(self, device=None, compute=True):
+        if device is not None and device != self.device:
+            raise ValueError("a GpuBamFile's reads live on device %d" % self.device)
+        if self._eng is None:
+            from .engine import CoverageEngine
+            eng = CoverageEngine(self.device)
+            eng.set_contigs(np.asarray(self.lengths, dtype=np.int64))
+            if self.n_kept:
+                eng._check(self._lib.mc_add_reads_device(eng._h, self.n_kept, *self._dptr))
+            eng._depth_ready = False
+            self._eng = eng
+        if compute and not self._eng._depth_ready:
+            self._eng.compute_depth()
+            self._eng._depth_ready = True
+        return self._eng
+
+    def close(self):
+        if self._eng is not None:
+            self._eng.close()
+            self._eng = None
+        if self._h:
+            self._lib.mc_bam_gpu_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class PinnedInt32:
     """int32 numpy array over page-locked host memory (mc_pinned_alloc), so
     mc_add_reads_async's DMA overlaps the host's next decode."""

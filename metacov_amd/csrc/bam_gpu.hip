@@ -1,0 +1,703 @@
+// GPU BAM decode: BGZF inflate and BAM record parse on the device, so the
+// whole pileup path after the file read runs in HBM.
+//
+// The host decoder (bam_decode.cpp) follows the reference's record walk
+// (IteratorRowAll, metacov/scan.pyx:204-216) with libdeflate on host threads;
+// at C3 scale it is the end-to-end bound (1.56 s of 1.78 s for a 5.2 GB BAM,
+// profiles/r03pp_e2e.json).  This path keeps its semantics record for record
+// (same kept set, intervals, counts and error classes) and moves the work:
+//
+//   host    read the file in windows of BGZF blocks (pread on threads into
+//           pinned staging, copied up while the next slice is read); block
+//           headers scanned on the host (BSIZE hops, bgzf::scan_blocks)
+//   K-gz    gz_inflate_kernel: one lane per BGZF block (inflate.h)
+//   K-sync  rec_sync_kernel: one wave per 64 KiB segment of the inflated
+//           stream finds the first offset that starts a chain of 8
+//           structurally valid records (the host decoder's sync_at rule)
+//   K-walk  rec_count_kernel: one lane per segment walks its records from its
+//           start to the next segment's start, counting kept records and
+//           checking each; the host then checks that every walk lands on the
+//           next segment's start (segment 0 starts at the first record, so
+//           consistent segments are exact) and re-walks from the landing
+//           point where a sync was a false positive
+//   K-fill  rec_fill_kernel: the same walk writes the kept (tid, pos, span)
+//           at each segment's offset (file order, as mc_bam_open)
+//
+// A window's incomplete last record is carried to the front of the next
+// window's inflated buffer.  The kept intervals stay in HBM
+// (mc_bam_gpu_intervals_device) for mc_add_reads_device.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <memory>
+
+#include "bgzf.h"
+#include "inflate.h"
+
+using namespace mc::bgzf;
+
+#define HIP_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            mc::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                          __FILE__, __LINE__);                                 \
+            return MC_E_HIP;                                                   \
+        }                                                                      \
+    } while (0)
+
+namespace {
+
+constexpr int kGzBlock = 256;
+constexpr int64_t kSeg = 64 << 10;        // inflated bytes per parse segment
+constexpr int kSyncChain = 8;             // records a sync candidate must chain
+constexpr int kPad = 64;                  // readable bytes past a compressed window
+
+struct GzBlock {
+    int64_t cdata;    // deflate payload, relative to the window's first block
+    int64_t out;      // inflated offset in the window buffer
+    int32_t clen;
+    int32_t isize;
+};
+
+struct SegRes {
+    int64_t landing;  // first record boundary at or past the next segment's start (or where the walk stopped)
+    int64_t records, mapped, kept;
+    int64_t err_at;
+    int32_t err;      // 0, kSegIncomplete, or an error class
+    int32_t pad;
+};
+
+enum : int32_t {
+    kSegIncomplete = 1,   // an incomplete record at `landing` (the window's tail, or truncation)
+    kSegBadSize = 2,      // block_size < 32
+    kSegTid = 3,          // rec_parse 2
+    kSegCigar = 4,        // rec_parse 3
+    kSegSpan = 5,         // rec_parse 4
+};
+
+__global__ void __launch_bounds__(kGzBlock)
+gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ blk, int64_t nblk,
+                  uint8_t* __restrict__ out, uint16_t* __restrict__ scratch, int* __restrict__ status,
+                  int* __restrict__ any_err) {
+    const int64_t lane = (int64_t)blockIdx.x * kGzBlock + threadIdx.x;
+    const int64_t lanes = (int64_t)gridDim.x * kGzBlock;
+    uint16_t* S = scratch + lane * mc::gz::kScratchWords;
+    for (int64_t b = lane; b < nblk; b += lanes) {
+        const GzBlock g = blk[b];
+        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S);
+        status[b] = rc;
+        if (rc) atomicOr(any_err, 1);
+    }
+}
+
+// One wave per segment i in [1, nseg): found[i] = the first offset q in
+// [cut_i, min(cut_i + kSeg, n)) that starts kSyncChain plausible records
+// (or a shorter chain ending exactly at n), else n.
+__global__ void __launch_bounds__(256)
+rec_sync_kernel(const uint8_t* __restrict__ d, int64_t o, int64_t n, int64_t nseg, int32_t n_ref,
+                int64_t* __restrict__ found) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    for (int64_t i = 1 + wave; i < nseg; i += waves) {
+        const int64_t cut = o + i * kSeg;
+        const int64_t lim = cut + kSeg < n ? cut + kSeg : n;
+        int64_t res = n;
+        for (int64_t base = cut; base < lim; base += 64) {
+            const int64_t q = base + lane;
+            bool ok = false;
+            if (q < lim && mc::gz::rec_plausible(d, q, n, n_ref)) {
+                int64_t z = q;
+                int k = 0;
+                for (; k < kSyncChain && z < n && mc::gz::rec_plausible(d, z, n, n_ref); ++k)
+                    z += 4 + (int64_t)mc::gz::ld_i32(d + z);
+                ok = k == kSyncChain || z == n;
+            }
+            const unsigned long long m = __ballot(ok);
+            if (m) {
+                res = base + __ffsll((long long)m) - 1;
+                break;
+            }
+        }
+        if (lane == 0) found[i] = res;
+    }
+}
+
+// One lane per segment: walk [seg_off[i], seg_off[i+1]) (kFill: write the
+// kept intervals at out_off[i]).  The walk of a segment ends at the first
+// record boundary >= seg_off[i+1], at an incomplete record, or at an error.
+template <bool kFill>
+__global__ void __launch_bounds__(256)
+rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restrict__ seg_off, int64_t first,
+                int64_t nseg, int32_t n_ref, uint32_t flag_filter, SegRes* __restrict__ res,
+                const int64_t* __restrict__ out_off, int32_t* __restrict__ tid, int32_t* __restrict__ pos,
+                int32_t* __restrict__ span) {
+    const int64_t i = first + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nseg) return;
+    int64_t q = seg_off[i];
+    const int64_t end = seg_off[i + 1];
+    int64_t records = 0, mapped = 0, kept = 0, err_at = 0;
+    int32_t err = 0;
+    int64_t w = 0, w_end = 0;
+    if (kFill) {
+        w = out_off[i];
+        w_end = w + res[i].kept;
+    }
+    while (q < end) {
+        if (q + 4 > n) {
+            err = kSegIncomplete;
+            break;
+        }
+        const int32_t bs = mc::gz::ld_i32(d + q);
+        if (bs < 32) {
+            err = kSegBadSize;
+            err_at = q;
+            break;
+        }
+        if (q + 4 + (int64_t)bs > n) {
+            err = kSegIncomplete;
+            break;
+        }
+        const uint8_t* r = d + q + 4;
+        mc::gz::RecOut ro;
+        const int rc = mc::gz::rec_parse(r, r + bs, n_ref, flag_filter, ro);
+        q += 4 + (int64_t)bs;
+        ++records;
+        mapped += ro.mapped ? 1 : 0;
+        if (rc >= 2) {
+            err = rc == 2 ? kSegTid : rc == 3 ? kSegCigar : kSegSpan;
+            err_at = q;
+            break;
+        }
+        if (rc == 1) {
+            if (kFill && w < w_end) {
+                tid[w] = ro.tid;
+                pos[w] = ro.pos;
+                span[w] = ro.span;
+                ++w;
+            }
+            ++kept;
+        }
+    }
+    if (!kFill) {
+        SegRes s;
+        s.landing = q;
+        s.records = records;
+        s.mapped = mapped;
+        s.kept = kept;
+        s.err_at = err_at;
+        s.err = err;
+        s.pad = 0;
+        res[i] = s;
+    }
+}
+
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+    // keep_elems: the first elements survive a reallocation
+    hipError_t reserve(size_t n, hipStream_t st = nullptr, size_t keep_elems = 0) {
+        if (n <= cap) return hipSuccess;
+        const size_t ncap = std::max(n, cap + cap / 2);
+        T* np = nullptr;
+        hipError_t e = hipMalloc(&np, ncap * sizeof(T));
+        if (e != hipSuccess) return e;
+        if (p && keep_elems) {
+            e = hipMemcpyAsync(np, p, keep_elems * sizeof(T), hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                (void)hipFree(np);
+                return e;
+            }
+        }
+        if (p) (void)hipFree(p);
+        p = np;
+        cap = ncap;
+        return hipSuccess;
+    }
+};
+
+template <typename T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), n * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+};
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct mc_bam_gpu {
+    mc_bam hdr;                       // names, lengths, record counts
+    std::string path;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int nt = 16;
+    uint32_t flag_filter = 0;
+    DBuf<int32_t> tid, pos, span;     // kept intervals, file order
+    int64_t n_kept = 0;
+    DBuf<uint8_t> comp, inflated, tail;
+    DBuf<GzBlock> blk;
+    DBuf<int> status;
+    DBuf<uint16_t> scratch;
+    DBuf<int64_t> seg_off, found, out_off;
+    DBuf<SegRes> res;
+    PinnedBuf<uint8_t> stage[2];
+    PinnedBuf<int64_t> h64;
+    PinnedBuf<SegRes> hres;
+    PinnedBuf<GzBlock> hblk;
+    // timings (ms)
+    double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0;
+    int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
+    ~mc_bam_gpu() {
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+    }
+};
+
+namespace {
+
+const char* seg_err_msg(int32_t e) {
+    switch (e) {
+        case kSegIncomplete: return "truncated record";
+        case kSegBadSize: return "bad record size";
+        case kSegTid: return "record tid beyond the reference list";
+        case kSegCigar: return "CIGAR overruns record";
+        default: return "reference span exceeds int32";
+    }
+}
+
+const char* gz_err_msg(int e) {
+    switch (e) {
+        case mc::gz::kErrBlockType: return "invalid block type";
+        case mc::gz::kErrStored: return "stored block length mismatch";
+        case mc::gz::kErrCodes: return "invalid code lengths";
+        case mc::gz::kErrSymbol: return "invalid code";
+        case mc::gz::kErrDistance: return "distance too far back";
+        case mc::gz::kErrOutput: return "more data than ISIZE";
+        case mc::gz::kErrInput: return "payload overrun";
+        default: return "fewer bytes than ISIZE";
+    }
+}
+
+// File bytes [off, off + len) into device memory at dst: pread on threads
+// into a pinned staging slice, copied up while the next slice is read.
+int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst) {
+    constexpr size_t kSlice = 64ull << 20;
+    for (auto& s : g->stage) HIP_TRY(s.reserve(kSlice));
+    hipEvent_t done[2] = {nullptr, nullptr};
+    for (auto& e : done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    struct Guard {
+        hipEvent_t* e;
+        ~Guard() {
+            for (int i = 0; i < 2; ++i)
+                if (e[i]) (void)hipEventDestroy(e[i]);
+        }
+    } guard{done};
+    bool used[2] = {false, false};
+    int k = 0;
+    for (size_t at = 0; at < len; at += kSlice, k ^= 1) {
+        const size_t n = std::min(kSlice, len - at);
+        if (used[k]) HIP_TRY(hipEventSynchronize(done[k]));   // the slice's previous copy is out
+        uint8_t* buf = g->stage[k].p;
+        const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)g->nt, n >> 20));
+        std::atomic<bool> bad{false};
+        auto work = [&](int t) {
+            const size_t a = n * t / nt, b = n * (t + 1) / nt;
+            size_t got = a;
+            while (got < b) {
+                const ssize_t r = pread(fd, buf + got, b - got, (off_t)(off + at + got));
+                if (r <= 0) {
+                    bad = true;
+                    return;
+                }
+                got += (size_t)r;
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
+        work(0);
+        for (auto& th : pool) th.join();
+        MC_REQUIRE(!bad, MC_E_IO, "%s: read failed at offset %zu", g->path.c_str(), off + at);
+        HIP_TRY(hipMemcpyAsync(dst + at, buf, n, hipMemcpyHostToDevice, g->stream));
+        HIP_TRY(hipEventRecord(done[k], g->stream));
+        used[k] = true;
+    }
+    HIP_TRY(hipStreamSynchronize(g->stream));
+    return MC_OK;
+}
+
+// Parses the records in inflated[o, n); partial: the window is not the
+// file's last, so an incomplete last record is carried (*consumed = its
+// offset).  Appends kept intervals to g->tid/pos/span.
+int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* consumed) {
+    hipStream_t st = g->stream;
+    const int32_t n_ref = (int32_t)g->hdr.names.size();
+    const uint8_t* d = g->inflated.p;
+    const int64_t nseg = std::max<int64_t>(1, (n - o + kSeg - 1) / kSeg);
+    HIP_TRY(g->seg_off.reserve(nseg + 1));
+    HIP_TRY(g->found.reserve(nseg + 1));
+    HIP_TRY(g->out_off.reserve(nseg + 1));
+    HIP_TRY(g->res.reserve(nseg));
+    HIP_TRY(g->h64.reserve(nseg + 1));
+    HIP_TRY(g->hres.reserve(nseg));
+    int64_t* h = g->h64.p;
+    if (nseg > 1) {
+        const int grid = (int)std::min<int64_t>((nseg - 1 + 3) / 4, 65536);
+        rec_sync_kernel<<<grid, 256, 0, st>>>(d, o, n, nseg, n_ref, g->found.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h, g->found.p, (nseg + 1) * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    std::vector<int64_t> seg(nseg + 1);
+    seg[0] = o;
+    seg[nseg] = n;
+    for (int64_t i = nseg - 1; i >= 1; --i) seg[i] = std::min(std::min(h[i], n), seg[i + 1]);
+    // walk / check rounds: segments before `first` are exact and consistent
+    int64_t first = 0;
+    SegRes* R = g->hres.p;
+    for (int round = 0;; ++round) {
+        if (round == 16) {   // bounded: the rest becomes one segment walked by one lane
+            for (int64_t j = first + 1; j < nseg; ++j) seg[j] = n;
+        }
+        std::memcpy(h, seg.data() + first, (nseg + 1 - first) * 8);
+        HIP_TRY(hipMemcpyAsync(g->seg_off.p + first, h, (nseg + 1 - first) * 8, hipMemcpyHostToDevice, st));
+        const int grid = (int)((nseg - first + 255) / 256);
+        rec_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->flag_filter,
+                                                     g->res.p, nullptr, nullptr, nullptr, nullptr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(R + first, g->res.p + first, (nseg - first) * sizeof(SegRes),
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        int64_t redo = -1;
+        for (int64_t i = first; i < nseg; ++i) {
+            const SegRes& r = R[i];
+            const int64_t end = seg[i + 1];
+            if (r.err == kSegIncomplete) {
+                if (partial) {
+                    // the window's records end here: later segments are empty
+                    if (end != n) {
+                        for (int64_t j = i + 1; j < nseg; ++j) seg[j] = n;
+                        redo = i + 1;   // (their walks are empty: nothing to redo but the copy)
+                    }
+                    break;
+                }
+                mc::set_error("%s: %s at byte %lld of the inflated stream", g->path.c_str(),
+                              seg_err_msg(r.err), (long long)r.landing);
+                return MC_E_IO;
+            }
+            if (r.err) {
+                mc::set_error("%s: %s at byte %lld of the inflated stream", g->path.c_str(),
+                              seg_err_msg(r.err), (long long)r.err_at);
+                return MC_E_IO;
+            }
+            if (r.landing != end) {   // segment i+1's sync was a false positive
+                for (int64_t j = i + 1; j < nseg && seg[j] < r.landing; ++j) seg[j] = r.landing;
+                ++g->resyncs;
+                redo = i + 1;
+                break;
+            }
+        }
+        if (redo < 0) break;
+        first = redo;
+        if (first >= nseg) {
+            // only the bookkeeping changed: make the remaining results empty
+            break;
+        }
+    }
+    // segments after an incomplete stop are empty; their results may be stale
+    int64_t total = 0, records = 0, mapped = 0, tail = n;
+    std::vector<int64_t> koff(nseg + 1);
+    for (int64_t i = 0; i < nseg; ++i) {
+        SegRes& r = R[i];
+        if (seg[i] >= seg[i + 1] && seg[i] == n) {   // empty tail segment
+            r.kept = r.records = r.mapped = 0;
+        }
+        koff[i] = g->n_kept + total;
+        total += r.kept;
+        records += r.records;
+        mapped += r.mapped;
+        if (r.err == kSegIncomplete) {
+            tail = r.landing;
+            for (int64_t j = i + 1; j < nseg; ++j) {
+                koff[j] = g->n_kept + total;
+                R[j].kept = R[j].records = R[j].mapped = 0;
+            }
+            break;
+        }
+    }
+    *consumed = partial ? tail : n;
+    // device copies of the final results (kept counts bound the fill writes)
+    HIP_TRY(hipMemcpyAsync(g->res.p, R, nseg * sizeof(SegRes), hipMemcpyHostToDevice, st));
+    std::memcpy(h, koff.data(), nseg * 8);
+    HIP_TRY(hipMemcpyAsync(g->out_off.p, h, nseg * 8, hipMemcpyHostToDevice, st));
+    const size_t need = (size_t)(g->n_kept + total) + 4;
+    HIP_TRY(g->tid.reserve(need, st, g->n_kept));
+    HIP_TRY(g->pos.reserve(need, st, g->n_kept));
+    HIP_TRY(g->span.reserve(need, st, g->n_kept));
+    if (total) {
+        const int grid = (int)((nseg + 255) / 256);
+        rec_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->flag_filter, g->res.p,
+                                                    g->out_off.p, g->tid.p, g->pos.p, g->span.p);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    g->n_kept += total;
+    g->hdr.n_records += records;
+    g->hdr.n_mapped += mapped;
+    g->hdr.n_unmapped += records - mapped;
+    return MC_OK;
+}
+
+int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
+    const double t_start = now_s();
+    MappedFile mf;
+    if (int rc = mf.open(g->path.c_str())) return rc;
+    std::vector<Block> blocks;
+    size_t total = 0;
+    if (int rc = scan_blocks(mf.data, mf.size, 0, SIZE_MAX, blocks, total)) return rc;
+    g->blocks = (int64_t)blocks.size();
+    g->inflated_bytes = (int64_t)total;
+    g->compressed_bytes = (int64_t)mf.size;
+    const size_t win = (size_t)std::max<int64_t>(window_bytes > 0 ? window_bytes : (4ll << 30), 1 << 20);
+    hipStream_t st = g->stream;
+    hipEvent_t ev[4];
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() {
+            for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
+        }
+    } evg{ev};
+    // scratch for the inflate lanes
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
+    const int64_t max_lanes = (int64_t)dev_cus * 8 * 64;   // 8 waves per CU (a multiple of kGzBlock)
+    size_t carry = 0;
+    bool have_header = false;
+    int64_t o = 0;
+    size_t b0 = 0;
+    while (b0 < blocks.size() || !have_header) {
+        MC_REQUIRE(b0 < blocks.size(), MC_E_IO, "%s: no valid BAM header", g->path.c_str());
+        size_t b1 = b0, wsize = 0;
+        while (b1 < blocks.size() && (b1 == b0 || wsize + blocks[b1].isize <= win)) wsize += blocks[b1++].isize;
+        const bool last = b1 == blocks.size();
+        const size_t coff = blocks[b0].off;
+        const size_t cend = b1 < blocks.size() ? blocks[b1].off : mf.size;
+        const size_t clen = cend - coff;
+        // compressed window up, block table up
+        const double t0 = now_s();
+        HIP_TRY(g->comp.reserve(clen + kPad));
+        if (int rc = upload_file_range(g, mf.fd, coff, clen, g->comp.p)) return rc;
+        HIP_TRY(hipMemsetAsync(g->comp.p + clen, 0, kPad, st));
+        const int64_t nb = (int64_t)(b1 - b0);
+        HIP_TRY(g->hblk.reserve(nb));
+        for (int64_t i = 0; i < nb; ++i) {
+            const Block& b = blocks[b0 + i];
+            g->hblk.p[i] = GzBlock{(int64_t)(b.cdata - coff), (int64_t)(carry + (b.out - blocks[b0].out)),
+                                   (int32_t)b.clen, (int32_t)b.isize};
+        }
+        HIP_TRY(g->blk.reserve(nb));
+        HIP_TRY(hipMemcpyAsync(g->blk.p, g->hblk.p, nb * sizeof(GzBlock), hipMemcpyHostToDevice, st));
+        // inflated buffer: carry (already at the front) + this window
+        const size_t n = carry + wsize;
+        if (n + 8 > g->inflated.cap) {
+            HIP_TRY(g->tail.reserve(std::max<size_t>(carry, 1)));
+            if (carry) HIP_TRY(hipMemcpyAsync(g->tail.p, g->inflated.p, carry, hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(g->inflated.reserve(n + 8));
+            if (carry) HIP_TRY(hipMemcpyAsync(g->inflated.p, g->tail.p, carry, hipMemcpyDeviceToDevice, st));
+        }
+        HIP_TRY(g->status.reserve(nb + 1));
+        HIP_TRY(hipMemsetAsync(g->status.p + nb, 0, sizeof(int), st));
+        // a multiple of the workgroup: every launched lane owns a scratch slot
+        const int64_t lanes = std::min<int64_t>(max_lanes, (nb + kGzBlock - 1) / kGzBlock * kGzBlock);
+        HIP_TRY(g->scratch.reserve((size_t)lanes * mc::gz::kScratchWords));
+        g->t_read += (now_s() - t0) * 1e3;
+        HIP_TRY(hipEventRecord(ev[0], st));
+        gz_inflate_kernel<<<(int)((lanes + kGzBlock - 1) / kGzBlock), kGzBlock, 0, st>>>(
+            g->comp.p, g->blk.p, nb, g->inflated.p, g->scratch.p, g->status.p, g->status.p + nb);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ev[1], st));
+        int any = 0;
+        HIP_TRY(hipMemcpyAsync(&any, g->status.p + nb, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        g->t_inflate += ms;
+        if (any) {
+            std::vector<int> s(nb);
+            HIP_TRY(hipMemcpy(s.data(), g->status.p, nb * sizeof(int), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < nb; ++i)
+                if (s[i]) {
+                    mc::set_error("BGZF inflate failed in %s (block at file offset %zu: %s)", g->path.c_str(),
+                                  blocks[b0 + i].off, gz_err_msg(s[i]));
+                    return MC_E_IO;
+                }
+        }
+        if (!have_header) {
+            // header from a growing prefix of the inflated bytes
+            size_t p = std::min<size_t>(n, 1 << 20);
+            std::vector<uint8_t> hb;
+            for (;;) {
+                hb.resize(p);
+                HIP_TRY(hipMemcpy(hb.data(), g->inflated.p, p, hipMemcpyDeviceToHost));
+                std::vector<std::string> names;
+                std::vector<int64_t> lens;
+                size_t ho = 0;
+                if (parse_header(hb.data(), p, g->path.c_str(), names, lens, &ho) == MC_OK) {
+                    g->hdr.names = std::move(names);
+                    g->hdr.lens = std::move(lens);
+                    o = (int64_t)ho;
+                    have_header = true;
+                    break;
+                }
+                if (p >= n) break;
+                p = std::min(n, p * 4);
+            }
+            if (!have_header) {
+                // the header continues in the next window: keep everything
+                MC_REQUIRE(!last, MC_E_IO, "%s: no valid BAM header", g->path.c_str());
+                carry = n;
+                b0 = b1;
+                ++g->windows;
+                continue;
+            }
+        }
+        const double t1 = now_s();
+        int64_t consumed = 0;
+        if (int rc = parse_window(g, o, (int64_t)n, !last, &consumed)) return rc;
+        g->t_parse += (now_s() - t1) * 1e3;
+        carry = n - (size_t)consumed;
+        if (last) {
+            MC_REQUIRE(carry == 0, MC_E_IO, "%s: truncated record at byte %lld of the inflated stream",
+                       g->path.c_str(), (long long)consumed);
+        } else if (carry) {
+            HIP_TRY(g->tail.reserve(carry));
+            HIP_TRY(hipMemcpyAsync(g->tail.p, g->inflated.p + consumed, carry, hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(g->inflated.p, g->tail.p, carry, hipMemcpyDeviceToDevice, st));
+        }
+        o = 0;
+        b0 = b1;
+        ++g->windows;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    g->t_total = (now_s() - t_start) * 1e3;
+    return MC_OK;
+}
+
+}  // namespace
+
+extern "C" int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
+                               int64_t window_bytes, mc_bam_gpu** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    MC_REQUIRE(device >= 0 && device < ndev, MC_E_INVALID, "no HIP device %d", device);
+    HIP_TRY(hipSetDevice(device));
+    std::unique_ptr<mc_bam_gpu> g(new mc_bam_gpu());
+    g->path = path;
+    g->device = device;
+    g->nt = n_threads > 0 ? n_threads : std::min(16, n_threads_or_all(0));   // file reads only
+    g->flag_filter = flag_filter;
+    HIP_TRY(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
+    // the staging and parse buffers are not needed after the decode
+    g->comp = DBuf<uint8_t>();
+    g->inflated = DBuf<uint8_t>();
+    g->scratch = DBuf<uint16_t>();
+    *out = g.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_header(const mc_bam_gpu* g, const mc_bam** header) {
+    MC_REQUIRE(g && header, MC_E_INVALID, "null argument");
+    *header = &g->hdr;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_intervals_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_tid,
+                                           const int32_t** d_pos, const int32_t** d_span) {
+    MC_REQUIRE(g && n && d_tid && d_pos && d_span, MC_E_INVALID, "null argument");
+    *n = g->n_kept;
+    *d_tid = g->tid.p;
+    *d_pos = g->pos.p;
+    *d_span = g->span.p;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_intervals(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int32_t* span) {
+    MC_REQUIRE(g && tid && pos && span, MC_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(g->device));
+    if (g->n_kept) {
+        HIP_TRY(hipMemcpy(tid, g->tid.p, g->n_kept * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pos, g->pos.p, g->n_kept * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(span, g->span.p, g->n_kept * 4, hipMemcpyDeviceToHost));
+    }
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t) {
+    MC_REQUIRE(g && t, MC_E_INVALID, "null argument");
+    t->read_ms = g->t_read;
+    t->inflate_ms = g->t_inflate;
+    t->parse_ms = g->t_parse;
+    t->total_ms = g->t_total;
+    t->windows = g->windows;
+    t->blocks = g->blocks;
+    t->resyncs = g->resyncs;
+    t->compressed_bytes = g->compressed_bytes;
+    t->inflated_bytes = g->inflated_bytes;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_close(mc_bam_gpu* g) {
+    delete g;
+    return MC_OK;
+}
+
+// The lane decoder of gz_inflate_kernel run on the host (unit tests: the
+// same inflate.h code against zlib without a GPU).  Not a product path.
+extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize) {
+    MC_REQUIRE(src && dst && clen >= 0 && isize >= 0, MC_E_INVALID, "bad argument");
+    std::vector<uint8_t> padded((size_t)clen + kPad + 4, 0);
+    std::memcpy(padded.data(), src, (size_t)clen);
+    std::vector<uint16_t> scratch(mc::gz::kScratchWords);
+    const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data());
+    MC_REQUIRE(rc == 0, MC_E_IO, "inflate failed: %s", gz_err_msg(rc));
+    return MC_OK;
+}
+
+// rec_parse on the host for one record body (unit tests)
+extern "C" int mc_bam_rec_parse_host(const uint8_t* r, int64_t len, int32_t n_ref, uint32_t flag_filter,
+                                     int32_t* out3) {
+    MC_REQUIRE(r && out3 && len >= 32, MC_E_INVALID, "bad argument");
+    mc::gz::RecOut ro{};
+    const int rc = mc::gz::rec_parse(r, r + len, n_ref, flag_filter, ro);
+    out3[0] = ro.tid;
+    out3[1] = ro.pos;
+    out3[2] = ro.span;
+    return rc;
+}

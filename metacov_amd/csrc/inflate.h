@@ -1,0 +1,405 @@
+// DEFLATE (RFC 1951) decoding of one BGZF block by one GPU lane, and the BAM
+// record arithmetic of the GPU decode (bam_gpu.hip).
+//
+// The host decoder (bgzf.h) inflates BGZF blocks with libdeflate on host
+// threads; at 16 threads it is the end-to-end bound of `metacov pileup`
+// (profiles/r03pp_e2e.json: 1.56 s of 1.78 s for a 5.2 GB BAM).  Here every
+// BGZF block (<= 64 KiB out, an independent deflate stream) is one lane's
+// work: a 64-bit bit buffer refilled by aligned 32-bit loads, canonical
+// Huffman codes decoded by a primary lookup table (10 bits literal/length,
+// 8 bits distance; longer codes by the count/symbol walk of RFC 1951 §3.2.2),
+// LZ77 copies from the lane's own output.  The per-lane tables live in a
+// global scratch slab (a lane owns kScratchWords u16).
+//
+// Every function is __host__ __device__: mc_gz_inflate_host runs the same
+// code on the CPU for the unit tests (tests/test_gpu_decode.py compares it
+// with zlib), the kernels run it per lane.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mc {
+namespace gz {
+
+#define MC_HD __host__ __device__ __forceinline__
+
+constexpr int kLitBits = 10;    // primary table index bits, literal/length alphabet
+constexpr int kDistBits = 8;    // distance alphabet
+// per-lane scratch (u16 words)
+constexpr int kLitT = 0;                          // [1 << kLitBits] primary entries (sym << 4 | len)
+constexpr int kDistT = kLitT + (1 << kLitBits);   // [1 << kDistBits]
+constexpr int kLitCnt = kDistT + (1 << kDistBits);   // [16] codes per length
+constexpr int kDistCnt = kLitCnt + 16;            // [16]
+constexpr int kLitSym = kDistCnt + 16;            // [288] symbols in canonical order
+constexpr int kDistSym = kLitSym + 288;           // [32]
+constexpr int kLens = kDistSym + 32;              // [320] code lengths being read
+constexpr int kOffs = kLens + 320;                // [16] build temporary
+constexpr int kScratchWords = kOffs + 16;
+
+enum : int {
+    kOk = 0,
+    kErrBlockType = 1,     // BTYPE 3
+    kErrStored = 2,        // stored block LEN / NLEN mismatch
+    kErrCodes = 3,         // bad code lengths (over-subscribed, counts out of range, no end code)
+    kErrSymbol = 4,        // a bit pattern that is no code, or a length/distance symbol out of range
+    kErrDistance = 5,      // distance before the block's output start
+    kErrOutput = 6,        // more output than ISIZE
+    kErrInput = 7,         // read past the compressed payload
+    kErrSize = 8,          // the stream ended before ISIZE bytes
+};
+
+// Bit reader over src[0, clen): 32-bit aligned loads; the buffer src points
+// into must be readable up to 8 bytes past an aligned clen (callers pad it).
+struct Bits {
+    const uint32_t* w;      // next aligned word
+    const uint32_t* wend;   // words at or past it read as 0 (past the payload)
+    uint64_t buf;
+    int cnt;                // valid bits in buf
+    int64_t end_bits;       // bits from src[0] to the end of the loaded words
+};
+
+MC_HD void bits_init(Bits& b, const uint8_t* src, int64_t byte_off, int64_t clen) {
+    const uintptr_t a = (uintptr_t)(src + byte_off);
+    const int mis = (int)(a & 3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a - (uintptr_t)mis);
+    b.wend = reinterpret_cast<const uint32_t*>(((uintptr_t)(src + clen) + 3) & ~(uintptr_t)3) + 1;
+    b.buf = (w < b.wend ? (uint64_t)*w : 0ull) >> (8 * mis);
+    b.cnt = 32 - 8 * mis;
+    b.w = w + 1;
+    b.end_bits = (byte_off + 4 - mis) * 8;
+}
+
+MC_HD void bits_refill(Bits& b) {   // afterwards cnt > 32
+    if (b.cnt <= 32) {
+        const uint64_t x = b.w < b.wend ? (uint64_t)*b.w : 0ull;
+        b.buf |= x << b.cnt;
+        b.cnt += 32;
+        ++b.w;
+        b.end_bits += 32;
+    }
+}
+
+MC_HD uint32_t bits_take(Bits& b, int n) {   // n <= cnt, n < 32
+    const uint32_t v = (uint32_t)b.buf & ((1u << n) - 1u);
+    b.buf >>= n;
+    b.cnt -= n;
+    return v;
+}
+
+MC_HD int64_t bits_pos(const Bits& b) { return b.end_bits - b.cnt; }   // next unread bit
+
+MC_HD uint32_t bitrev(uint32_t code, int len) {
+    uint32_t r = 0;
+    for (int i = 0; i < len; ++i) {
+        r = (r << 1) | (code & 1u);
+        code >>= 1;
+    }
+    return r;
+}
+
+// Canonical Huffman code from lens[0, n): counts, symbols in code order and
+// the primary table of `tb` index bits.  Over-subscribed lengths are an
+// error; incomplete codes are accepted (their missing patterns fail in
+// decode_slow).
+MC_HD int build_code(uint16_t* S, int t_off, int tb, int cnt_off, int sym_off, const uint16_t* lens, int n) {
+    uint16_t* cnt = S + cnt_off;
+    uint16_t* sym = S + sym_off;
+    uint16_t* offs = S + kOffs;
+    for (int l = 0; l < 16; ++l) cnt[l] = 0;
+    for (int s = 0; s < n; ++s) cnt[lens[s] & 15]++;
+    int left = 1;
+    for (int l = 1; l < 16; ++l) {
+        left = (left << 1) - cnt[l];
+        if (left < 0) return kErrCodes;
+    }
+    offs[1] = 0;
+    for (int l = 1; l < 15; ++l) offs[l + 1] = (uint16_t)(offs[l] + cnt[l]);
+    for (int s = 0; s < n; ++s) {
+        const int l = lens[s] & 15;
+        if (l) sym[offs[l]++] = (uint16_t)s;
+    }
+    uint16_t* T = S + t_off;
+    const int size = 1 << tb;
+    for (int i = 0; i < size; ++i) T[i] = 0;
+    uint32_t code = 0;
+    int k = 0;
+    for (int l = 1; l <= tb; ++l) {
+        for (int c = 0; c < cnt[l]; ++c, ++k, ++code) {
+            const uint16_t e = (uint16_t)((sym[k] << 4) | l);
+            for (uint32_t r = bitrev(code, l); r < (uint32_t)size; r += 1u << l) T[r] = e;
+        }
+        code <<= 1;
+    }
+    return kOk;
+}
+
+// RFC 1951 §3.2.2 walk over the code lengths (codes longer than the table,
+// and patterns the table does not hold): -1 when the bits are no code.
+MC_HD int decode_slow(uint64_t bits, const uint16_t* cnt, const uint16_t* sym, int* used) {
+    int code = 0, first = 0, index = 0;
+    for (int l = 1; l < 16; ++l) {
+        code |= (int)((bits >> (l - 1)) & 1u);
+        const int count = cnt[l];
+        if (code - count < first) {
+            *used = l;
+            return sym[index + (code - first)];
+        }
+        index += count;
+        first = (first + count) << 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+MC_HD int decode_sym(Bits& b, const uint16_t* S, int t_off, int tb, int cnt_off, int sym_off) {
+    const uint16_t e = S[t_off + ((uint32_t)b.buf & ((1u << tb) - 1u))];
+    int used, s;
+    if (e) {
+        used = e & 15;
+        s = e >> 4;
+    } else {
+        s = decode_slow(b.buf, S + cnt_off, S + sym_off, &used);
+        if (s < 0) return -1;
+    }
+    b.buf >>= used;
+    b.cnt -= used;
+    return s;
+}
+
+// Dynamic block header: code length code, then the literal/length and
+// distance code lengths (RFC 1951 §3.2.7), then both tables.
+MC_HD int read_dynamic(Bits& b, uint16_t* S) {
+    bits_refill(b);
+    const int nlen = (int)bits_take(b, 5) + 257;
+    const int ndist = (int)bits_take(b, 5) + 1;
+    const int ncode = (int)bits_take(b, 4) + 4;
+    if (nlen > 286 || ndist > 30) return kErrCodes;
+    uint16_t* lens = S + kLens;
+    const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    for (int i = 0; i < 19; ++i) lens[i] = 0;
+    for (int i = 0; i < ncode; ++i) {
+        bits_refill(b);
+        lens[order[i]] = (uint16_t)bits_take(b, 3);
+    }
+    // the code length code (<= 7 bits) goes through the literal table's slots
+    int rc = build_code(S, kLitT, 7, kLitCnt, kLitSym, lens, 19);
+    if (rc) return rc;
+    int idx = 0;
+    while (idx < nlen + ndist) {
+        bits_refill(b);
+        const int sym = decode_sym(b, S, kLitT, 7, kLitCnt, kLitSym);
+        if (sym < 0) return kErrCodes;
+        if (sym < 16) {
+            lens[idx++] = (uint16_t)sym;
+            continue;
+        }
+        int len = 0, rep;
+        if (sym == 16) {
+            if (idx == 0) return kErrCodes;
+            len = lens[idx - 1];
+            rep = 3 + (int)bits_take(b, 2);
+        } else if (sym == 17) {
+            rep = 3 + (int)bits_take(b, 3);
+        } else {
+            rep = 11 + (int)bits_take(b, 7);
+        }
+        if (idx + rep > nlen + ndist) return kErrCodes;
+        while (rep--) lens[idx++] = (uint16_t)len;
+    }
+    if (lens[256] == 0) return kErrCodes;
+    // the distance lengths follow the literal ones in lens[]; the literal
+    // table is built last because its build overwrites nothing of them
+    rc = build_code(S, kDistT, kDistBits, kDistCnt, kDistSym, lens + nlen, ndist);
+    if (rc) return rc;
+    return build_code(S, kLitT, kLitBits, kLitCnt, kLitSym, lens, nlen);
+}
+
+MC_HD int read_fixed(uint16_t* S) {
+    uint16_t* lens = S + kLens;
+    for (int s = 0; s < 288; ++s) lens[s] = (uint16_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
+    int rc = build_code(S, kLitT, kLitBits, kLitCnt, kLitSym, lens, 288);
+    if (rc) return rc;
+    for (int s = 0; s < 30; ++s) lens[s] = 5;
+    return build_code(S, kDistT, kDistBits, kDistCnt, kDistSym, lens, 30);
+}
+
+// One raw deflate stream src[0, clen) into dst[0, isize): kOk iff it ends
+// (BFINAL) with exactly isize bytes and without reading past clen.
+MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S) {
+    if (isize == 0) return kOk;
+    Bits b;
+    bits_init(b, src, 0, clen);
+    const int64_t limit_bits = clen * 8;
+    int64_t o = 0;
+    for (;;) {
+        bits_refill(b);
+        const int final = (int)bits_take(b, 1);
+        const int type = (int)bits_take(b, 2);
+        if (type == 0) {
+            // stored: skip to the byte boundary, LEN, NLEN, then LEN raw bytes
+            const int64_t p = (bits_pos(b) + 7) >> 3;
+            if (p + 4 > clen) return kErrInput;
+            const uint32_t len = (uint32_t)src[p] | ((uint32_t)src[p + 1] << 8);
+            const uint32_t nlen = (uint32_t)src[p + 2] | ((uint32_t)src[p + 3] << 8);
+            if ((len ^ 0xffffu) != nlen) return kErrStored;
+            if (p + 4 + (int64_t)len > clen) return kErrInput;
+            if (o + (int64_t)len > isize) return kErrOutput;
+            for (uint32_t k = 0; k < len; ++k) dst[o + k] = src[p + 4 + k];
+            o += len;
+            bits_init(b, src, p + 4 + len, clen);
+        } else if (type == 3) {
+            return kErrBlockType;
+        } else {
+            const int rc = type == 1 ? read_fixed(S) : read_dynamic(b, S);
+            if (rc) return rc;
+            for (;;) {
+                if (bits_pos(b) > limit_bits) return kErrInput;
+                bits_refill(b);
+                int s = decode_sym(b, S, kLitT, kLitBits, kLitCnt, kLitSym);
+                if (s < 0) return kErrSymbol;
+                if (s < 256) {
+                    if (o >= isize) return kErrOutput;
+                    dst[o++] = (uint8_t)s;
+                    continue;
+                }
+                if (s == 256) break;
+                s -= 257;
+                if (s >= 29) return kErrSymbol;
+                int len;
+                if (s < 8) {
+                    len = s + 3;
+                } else if (s == 28) {
+                    len = 258;
+                } else {
+                    const int e = (s - 4) >> 2;
+                    len = ((4 + (s & 3)) << e) + 3 + (int)bits_take(b, e);
+                }
+                bits_refill(b);
+                const int d = decode_sym(b, S, kDistT, kDistBits, kDistCnt, kDistSym);
+                if (d < 0 || d >= 30) return kErrSymbol;
+                int dist;
+                if (d < 4) {
+                    dist = d + 1;
+                } else {
+                    const int e = (d - 2) >> 1;
+                    dist = ((2 + (d & 1)) << e) + 1 + (int)bits_take(b, e);
+                }
+                if ((int64_t)dist > o) return kErrDistance;
+                if (o + len > isize) return kErrOutput;
+                uint8_t* q = dst + o;
+                for (int k = 0; k < len; ++k) q[k] = q[k - dist];
+                o += len;
+            }
+        }
+        if (bits_pos(b) > limit_bits) return kErrInput;
+        if (final) break;
+    }
+    return o == isize ? kOk : kErrSize;
+}
+
+// ---------------------------------------------------------------- BAM records
+// (the host decoder's rules, bam_decode.cpp:32-205 / bgzf.h:222-289)
+
+MC_HD uint32_t ld_u16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+MC_HD uint32_t ld_u32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+MC_HD int32_t ld_i32(const uint8_t* p) { return (int32_t)ld_u32(p); }
+
+// a structurally valid record starts at q of d[0, n)
+MC_HD bool rec_plausible(const uint8_t* d, int64_t q, int64_t n, int32_t n_ref) {
+    if (q + 36 > n) return false;
+    const int32_t bs = ld_i32(d + q);
+    if (bs < 32 || q + 4 + (int64_t)bs > n) return false;
+    const int32_t tid = ld_i32(d + q + 4), pos = ld_i32(d + q + 8);
+    const uint32_t lrn = d[q + 12];
+    const uint32_t ncig = ld_u16(d + q + 16);
+    const int32_t lseq = ld_i32(d + q + 20), ntid = ld_i32(d + q + 24);
+    if (tid < -1 || tid >= n_ref || ntid < -1 || ntid >= n_ref || pos < -1 || lrn == 0 || lseq < 0)
+        return false;
+    const uint64_t need = 32 + (uint64_t)lrn + 4ull * ncig + ((uint64_t)lseq + 1) / 2 + (uint64_t)lseq;
+    if (need > (uint64_t)bs) return false;
+    return d[q + 36 + lrn - 1] == 0;
+}
+
+// CG:B,I in the aux data [p, end) (SAMv1 §4.2.2)
+MC_HD bool find_cg(const uint8_t* p, const uint8_t* end, const uint8_t** words, uint32_t* count) {
+    while (p + 3 <= end) {
+        const char t0 = (char)p[0], t1 = (char)p[1], ty = (char)p[2];
+        p += 3;
+        switch (ty) {
+            case 'A': case 'c': case 'C': p += 1; break;
+            case 's': case 'S': p += 2; break;
+            case 'i': case 'I': case 'f': p += 4; break;
+            case 'Z': case 'H':
+                while (p < end && *p) ++p;
+                ++p;
+                break;
+            case 'B': {
+                if (p + 5 > end) return false;
+                const char sub = (char)p[0];
+                const uint32_t cnt = ld_u32(p + 1);
+                p += 5;
+                const uint64_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                if (t0 == 'C' && t1 == 'G' && sub == 'I') {
+                    if (p + (uint64_t)cnt * 4 > end) return false;
+                    *words = p;
+                    *count = cnt;
+                    return true;
+                }
+                p += es * cnt;
+                break;
+            }
+            default:
+                return false;
+        }
+    }
+    return true;
+}
+
+// Record body r[0, rend - r) after block_size: 0 = dropped, 1 = kept with
+// (tid, pos, span), or an error: 2 tid beyond the reference list, 3 CIGAR
+// overruns record, 4 reference span exceeds int32.
+struct RecOut {
+    int32_t tid, pos, span;
+    bool mapped;
+};
+
+MC_HD int rec_parse(const uint8_t* r, const uint8_t* rend, int32_t n_ref, uint32_t flag_filter, RecOut& out) {
+    const int32_t tid = ld_i32(r);
+    const uint32_t flag = ld_u16(r + 14);
+    out.mapped = tid >= 0 && !(flag & 4u);
+    if (tid < 0 || (flag & flag_filter)) return 0;
+    if (tid >= n_ref) return 2;
+    const uint32_t l_read_name = r[8];
+    uint32_t n_cigar = ld_u16(r + 12);
+    const int32_t l_seq = ld_i32(r + 16);
+    const uint8_t* cig = r + 32 + l_read_name;
+    if (cig + (uint64_t)n_cigar * 4 > rend) return 3;
+    if (n_cigar == 2 && ld_u32(cig) == (((uint32_t)l_seq << 4) | 4u) && (ld_u32(cig + 4) & 0xFu) == 3u) {
+        const uint8_t* aux = cig + 8 + ((uint64_t)l_seq + 1) / 2 + (uint64_t)l_seq;
+        const uint8_t* words = nullptr;
+        uint32_t cnt = 0;
+        if (aux <= rend && find_cg(aux, rend, &words, &cnt) && words) {
+            cig = words;
+            n_cigar = cnt;
+        }
+    }
+    int64_t rlen = 0;
+    for (uint32_t k = 0; k < n_cigar; ++k) {
+        const uint32_t cw = ld_u32(cig + 4ull * k);
+        if ((0x18Du >> (cw & 0xFu)) & 1u) rlen += cw >> 4;
+    }
+    if (rlen <= 0) rlen = 1;
+    if (rlen > 0x7fffffffll) return 4;
+    out.tid = tid;
+    out.pos = ld_i32(r + 4);
+    out.span = (int32_t)rlen;
+    return 1;
+}
+
+#undef MC_HD
+
+}  // namespace gz
+}  // namespace mc

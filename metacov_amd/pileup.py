@@ -2,7 +2,7 @@
 
     classic(bam, ref, start, end) -> {min, max, med, std, avg, q23, sum}
 
-`bam` may be a path, a `metacov_amd.bam.BamFile`, or a `pysam.AlignmentFile`
+`bam` may be a path, a `metacov_amd.bam.BamFile` / `GpuBamFile`, or a `pysam.AlignmentFile`
 (its `.filename` is decoded by this library).  The depth of every contig is
 computed once per file on the GPU (K2) and each call reduces one region
 (K3); `classic_batch` reduces many regions in one launch.  Semantics match
@@ -25,7 +25,7 @@ _open_files = {}
 
 
 def _as_bamfile(bam):
-    if isinstance(bam, BamFile):
+    if isinstance(bam, BamFile) or hasattr(bam, "engine"):   # BamFile, GpuBamFile, StreamedBam
         return bam
     key = getattr(bam, "filename", bam)
     if isinstance(key, bytes):

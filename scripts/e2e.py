@@ -5,6 +5,8 @@
 Writes an edge-mix BAM with the library's writer, then times the phases of
 the CLI path: C++ decode (BGZF inflate + parse, all host threads), ingest
 (H2D + prepare), fused depth + statistics on the GPU, CSV formatting.
+Then the same file through the GPU decode (GpuBamFile: BGZF inflate and
+record parse on the device); every path's CSV must equal the first.
 Prints one JSON line.
 """
 import argparse
@@ -68,6 +70,21 @@ def main():
     t_cmp2 = time.perf_counter() - t0
     assert out2.getvalue() == csv_full, "streamed CSV differs"
     sb.close()
+    # the GPU decode path: compressed windows up, inflate + record parse in HBM
+    from metacov_amd.bam import GpuBamFile
+    t0 = time.perf_counter()
+    gb = GpuBamFile(path, device=0, n_threads=a.threads)
+    t_gdec = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    gb.engine(0, compute=False)
+    t_ging = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    out3 = io.StringIO()
+    write_rows(gb, regs, out3)
+    t_cmp3 = time.perf_counter() - t0
+    assert out3.getvalue() == csv_full, "GPU-decoded CSV differs"
+    gtm = gb.timings()
+    gb.close()
     print(json.dumps({
         "bam_bytes": os.path.getsize(path), "records": n_rec, "kept": n_kept,
         "aligned_bases": bases, "host_threads": a.threads,
@@ -77,7 +94,10 @@ def main():
         "timings": tm,
         "stream_decode_ingest_prepare_s": t_stream, "stream_gpu_stats_csv_s": t_cmp2,
         "stream_end_to_end_s": t_stream + t_cmp2,
-        "stream_end_to_end_aligned_bases_per_s": bases / (t_stream + t_cmp2)}))
+        "stream_end_to_end_aligned_bases_per_s": bases / (t_stream + t_cmp2),
+        "gpu_decode_s": t_gdec, "gpu_decode_timings": gtm, "gpu_ingest_s": t_ging,
+        "gpudec_stats_csv_s": t_cmp3, "gpu_end_to_end_s": t_gdec + t_ging + t_cmp3,
+        "gpu_end_to_end_aligned_bases_per_s": bases / (t_gdec + t_ging + t_cmp3)}))
     os.remove(path)
 
 

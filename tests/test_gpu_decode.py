@@ -1,0 +1,266 @@
+"""GPU BAM decode (csrc/bam_gpu.hip, csrc/inflate.h).
+
+CPU tests: the lane decoder of the inflate kernel (run on the host through
+mc_gz_inflate_host) against zlib on raw deflate streams of every block type
+and on the BGZF blocks of the fixture and synthetic BAMs; the record parse
+against the host decoder's rules.  GPU tests: mc_bam_gpu_open against the
+host decoder (mc_bam_open, itself pinned by the goldens in test_decoder.py)
+record for record, including windows far smaller than one record, records
+spanning many 64 KiB parse segments, and the error classes.
+"""
+import ctypes
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from metacov_amd import synth
+from metacov_amd._lib import MetacovError
+
+
+def _lib():
+    from metacov_amd import _lib as L
+    return L.load()
+
+
+def _raw_deflate(data, level, strategy=zlib.Z_DEFAULT_STRATEGY):
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, strategy)
+    return c.compress(data) + c.flush()
+
+
+def _inflate_host(comp, isize):
+    lib = _lib()
+    out = ctypes.create_string_buffer(max(isize, 1))
+    rc = lib.mc_gz_inflate_host(comp, len(comp), out, isize)
+    return rc, out.raw[:isize]
+
+
+def _bgzf_blocks(raw):
+    """(payload, isize) of every BGZF block of a file's bytes."""
+    o, out = 0, []
+    while o < len(raw):
+        assert raw[o:o + 4] == b"\x1f\x8b\x08\x04"
+        xlen, = struct.unpack_from("<H", raw, o + 10)
+        x, bsize = o + 12, None
+        while x < o + 12 + xlen:
+            si1, si2, slen = raw[x], raw[x + 1], struct.unpack_from("<H", raw, x + 2)[0]
+            if si1 == 66 and si2 == 67:
+                bsize = struct.unpack_from("<H", raw, x + 4)[0] + 1
+            x += 4 + slen
+        payload = raw[o + 12 + xlen:o + bsize - 8]
+        isize, = struct.unpack_from("<I", raw, o + bsize - 4)
+        out.append((payload, isize))
+        o += bsize
+    return out
+
+
+def test_inflate_host_matches_zlib(lib_built):
+    rng = np.random.default_rng(0)
+    cases = [b"", b"a", b"ab" * 3,
+             bytes(rng.integers(0, 256, 65280, dtype=np.uint8)),          # incompressible
+             bytes(rng.integers(0, 4, 65280, dtype=np.uint8) + 65),
+             b"ACGT" * 16000,                                             # long matches
+             bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), 60000, p=[.3, .2, .2, .29, .01])),
+             bytes(range(256)) * 200]
+    for data in cases:
+        for level in (0, 1, 6, 9):
+            for strat in (zlib.Z_DEFAULT_STRATEGY, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE):
+                comp = _raw_deflate(data, level, strat)
+                rc, got = _inflate_host(comp, len(data))
+                assert rc == 0 and got == data, (len(data), level, strat)
+    # wrong ISIZE either way is an error
+    comp = _raw_deflate(b"x" * 1000, 6)
+    assert _inflate_host(comp, 999)[0] != 0
+    assert _inflate_host(comp, 1001)[0] != 0
+
+
+def test_inflate_host_bgzf_blocks(lib_built, golden_dir, tmp_path):
+    """Every BGZF block of the reference's fixture (samtools-written) and of
+    synthetic BAMs (zlib levels 1 and 6) decodes to zlib's bytes."""
+    paths = [os.path.join(golden_dir, f) for f in ("bbmap.sorted.bam", "synth_longcigar.bam",
+                                                   "synth_edge.bam")]
+    lengths = [300_000, 900]
+    arrs = synth.edge_mix_arrays(lengths, 20_000, seed=9)
+    for level in (1, 6):
+        p = str(tmp_path / ("l%d.bam" % level))
+        synth.write_bam_fast(p, ["a", "b"], lengths, *arrs, level=level, n_threads=2)
+        paths.append(p)
+    n = 0
+    for p in paths:
+        for payload, isize in _bgzf_blocks(open(p, "rb").read()):
+            want = zlib.decompress(payload, -15)
+            assert len(want) == isize
+            rc, got = _inflate_host(payload, isize)
+            assert rc == 0 and got == want
+            n += 1
+    assert n > 20
+
+
+def test_inflate_host_corrupt_streams_fail_cleanly(lib_built, golden_dir):
+    """Flipped bytes in real blocks: the lane decoder returns (ok or an
+    error) without reading or writing out of bounds; where it reports ok,
+    zlib agrees on the bytes."""
+    blocks = _bgzf_blocks(open(os.path.join(golden_dir, "bbmap.sorted.bam"), "rb").read())
+    rng = np.random.default_rng(3)
+    for trial in range(300):
+        payload, isize = blocks[trial % (len(blocks) - 1)]
+        b = bytearray(payload)
+        for _ in range(1 + trial % 4):
+            b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+        if trial % 7 == 0:
+            b = b[: int(rng.integers(1, len(b)))]
+        rc, got = _inflate_host(bytes(b), isize)
+        if rc == 0:
+            try:
+                want = zlib.decompress(bytes(b), -15)
+            except zlib.error:
+                continue   # zlib is stricter about some incomplete codes
+            assert got == want[:isize]
+
+
+def _parse_host(body, n_ref=3, flag_filter=0x704):
+    out = (ctypes.c_int32 * 3)()
+    rc = _lib().mc_bam_rec_parse_host(body, len(body), n_ref, flag_filter, out)
+    return rc, tuple(out)
+
+
+def test_rec_parse_host(lib_built):
+    R = synth.SynthRecord
+    cases = [
+        (R("r", 0, 100, 0, [(0, 50), (2, 3), (1, 4), (0, 20)], 74), (1, (0, 100, 73))),   # M D I M
+        (R("r", 1, 5, 0, [(4, 10), (7, 30), (8, 2), (3, 1000)], 40), (1, (1, 5, 1032))),  # S = X N
+        (R("r", 2, 7, 0, [(4, 20)], 20), (1, (2, 7, 1))),        # no reference op: span 1
+        (R("r", 0, 7, 0x100, [(0, 20)], 20), (0, None)),          # secondary: dropped
+        (R("r", 0, 7, 0x800, [(0, 20)], 20), (1, (0, 7, 20))),   # supplementary: kept
+        (R("r", -1, -1, 4, [], 20), (0, None)),
+        (R("r", 5, 7, 0, [(0, 20)], 20), (2, None)),             # tid beyond n_ref
+    ]
+    for rec, (rc_want, iv) in cases:
+        body = synth.encode_record(rec)[4:]
+        rc, out = _parse_host(body)
+        assert rc == rc_want, rec.cigar
+        if iv:
+            assert out == iv
+    # CG:B,I placeholder resolved (> 65535 ops)
+    ops = [(0, 1), (2, 1)] * 40_000
+    body = synth.encode_record(R("r", 0, 9, 0, ops, 40_000), long_cigar_threshold=65535)[4:]
+    assert _parse_host(body) == (1, (0, 9, 80_000))
+
+
+# ---------------------------------------------------------------- GPU
+
+def _host_and_gpu(path, **kw):
+    from metacov_amd.bam import BamFile, GpuBamFile
+    h = BamFile(path)
+    g = GpuBamFile(path, **kw)
+    return h, g
+
+
+def _assert_same(h, g):
+    assert g.references == h.references and g.lengths == h.lengths
+    assert (g.n_records, g.mapped, g.unmapped) == (h.n_records, h.mapped, h.unmapped)
+    tid, pos, span = g.intervals()
+    assert np.array_equal(tid, h.tid) and np.array_equal(pos, h.pos) and np.array_equal(span, h.span)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["bbmap.sorted.bam", "synth_edge.bam", "synth_multi.bam",
+                                  "synth_longcigar.bam"])
+@pytest.mark.parametrize("window", [0, 1 << 20])
+def test_gpu_decode_goldens(lib_built, golden_dir, name, window):
+    h, g = _host_and_gpu(os.path.join(golden_dir, name), window_bytes=window)
+    _assert_same(h, g)
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level,window", [(1, 0), (6, 1 << 20), (1, 3 << 20)])
+def test_gpu_decode_large(lib_built, tmp_path, level, window):
+    """2M records over several windows (records cut by window ends carried),
+    ~600 parse segments per window."""
+    lengths = [3_000_000, 1_000, 900_000]
+    arrs = synth.edge_mix_arrays(lengths, 2_000_000, seed=11)
+    p = str(tmp_path / "big.bam")
+    synth.write_bam_fast(p, ["x", "y", "z"], lengths, *arrs, level=level, n_threads=8)
+    h, g = _host_and_gpu(p, window_bytes=window)
+    _assert_same(h, g)
+    t = g.timings()
+    assert t["blocks"] > 100 and t["inflated_bytes"] > 0
+    if window:
+        assert t["windows"] > 1
+    g.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_long_records(lib_built, tmp_path):
+    """Records of 30-200 KB (long reads with their sequence): most 64 KiB
+    parse segments hold no record start."""
+    rng = np.random.default_rng(2)
+    lengths = [5_000_000, 2_000_000]
+    recs = []
+    for t, L in enumerate(lengths):
+        for p in np.sort(rng.integers(0, L - 150_000, 60)):
+            rl = int(rng.integers(10_000, 120_000))
+            recs.append(synth.SynthRecord("long%d" % len(recs), t, int(p), 0, [(4, 50), (0, rl), (2, 7)], rl + 50))
+    path = str(tmp_path / "long.bam")
+    synth.write_bam(path, ["a", "b"], lengths, recs)
+    for window in (0, 1 << 20):
+        h, g = _host_and_gpu(path, window_bytes=window)
+        _assert_same(h, g)
+        g.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_header_only_and_tiny(lib_built, tmp_path):
+    p = str(tmp_path / "empty.bam")
+    synth.write_bam(p, ["a", "b"], [100, 200], [])
+    h, g = _host_and_gpu(p)
+    _assert_same(h, g)
+    assert g.n_kept == 0
+    g.close()
+    p = str(tmp_path / "one.bam")
+    synth.write_bam(p, ["a"], [1000], [synth.SynthRecord("r", 0, 10, 0, [(0, 30)], 30)])
+    h, g = _host_and_gpu(p)
+    _assert_same(h, g)
+    g.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_errors(lib_built, tmp_path, golden_dir):
+    from metacov_amd.bam import GpuBamFile
+    with pytest.raises(MetacovError):
+        GpuBamFile(str(tmp_path / "missing.bam"))
+    raw = open(os.path.join(golden_dir, "bbmap.sorted.bam"), "rb").read()
+    t = tmp_path / "trunc.bam"
+    t.write_bytes(raw[: len(raw) // 2])
+    with pytest.raises(MetacovError):
+        GpuBamFile(str(t))
+    # a corrupted deflate payload in a whole block
+    blocks = _bgzf_blocks(raw)
+    b = bytearray(raw)
+    off = len(raw) // 3
+    while raw[off:off + 4] != b"\x1f\x8b\x08\x04":
+        off += 1
+    for k in range(40, 200):
+        b[off + k] ^= 0x5a
+    c = tmp_path / "corrupt.bam"
+    c.write_bytes(bytes(b))
+    with pytest.raises(MetacovError, match="inflate|record|CIGAR|BGZF"):
+        GpuBamFile(str(c))
+    assert len(blocks) > 3
+
+
+@pytest.mark.gpu
+def test_gpu_decode_feeds_engine(lib_built, golden_dir, fixture_golden):
+    """The decoded intervals go into a ctx by a device copy: classic() rows
+    equal the host-decoded file's."""
+    from metacov_amd.bam import BamFile, GpuBamFile
+    from metacov_amd import pileup
+    path = os.path.join(golden_dir, "bbmap.sorted.bam")
+    h = BamFile(path)
+    g = GpuBamFile(path)
+    for ref, L in zip(h.references, h.lengths):
+        assert pileup.classic(g, ref, 0, L) == pileup.classic(h, ref, 0, L)
+    g.close()
