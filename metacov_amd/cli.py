@@ -32,7 +32,7 @@ from . import depthcap as _depthcap
 from . import experimental as _experimental
 from . import regions as _regions
 from . import scan as _scan
-from .bam import BamFile, StreamedBam, index_stats
+from .bam import BamFile, GpuBamFile, StreamedBam, index_stats
 from .engine import REGION_STAT_DTYPE, classic_stats
 
 logging.basicConfig(level=logging.INFO,
@@ -70,8 +70,11 @@ def main():
 @click.option('--max-depth', type=click.IntRange(1), default=None, metavar="N",
               help="Reproduce htslib's pileup read cap (pysam's default is 8000) per region "
                    "query; default: exact depths, no cap")
+@click.option('--decode', type=click.Choice(['gpu', 'host']), default='gpu',
+              help="gpu (default): BGZF inflate and record parse on the device (csrc/bam_gpu.hip); "
+                   "host: the C++ decoder on host threads (--stream / --no-stream)")
 def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
-           kmer_histogram, kmer_length, outfile, device, stream, max_depth):
+           kmer_histogram, kmer_length, outfile, device, stream, max_depth, decode):
     """
     Compute fold coverage values
     """
@@ -82,9 +85,13 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp,
                                   max_depth=max_depth)
-    # the cap needs each region's records (a decoded file, not a stream)
-    bam = StreamedBam(bamfile.name, device=device) if stream and max_depth is None \
-        else BamFile(bamfile.name)
+    # the cap needs each region's records on the host (a decoded file)
+    if max_depth is not None:
+        bam = BamFile(bamfile.name)
+    elif decode == 'gpu':
+        bam = GpuBamFile(bamfile.name, device=device)
+    else:
+        bam = StreamedBam(bamfile.name, device=device) if stream else BamFile(bamfile.name)
     regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam))
     log_counts(bam)
     write_rows(bam, regions, outfile, device=device, exp=exp, max_depth=max_depth)

@@ -76,16 +76,54 @@ enum : int32_t {
     kSegSpan = 5,         // rec_parse 4
 };
 
-__global__ void __launch_bounds__(kGzBlock)
+// primary Huffman tables per lane in LDS (MC_GZ_LDS) or in the lane's
+// global scratch slot
+#ifndef MC_GZ_LDS
+#define MC_GZ_LDS 1
+#endif
+#ifndef MC_GZ_WAVES_PER_CU
+#define MC_GZ_WAVES_PER_CU 8
+#endif
+#ifndef MC_GZ_LANES
+#define MC_GZ_LANES 32     // active lanes (blocks in flight) per wave: 64 100.9, 32 82.6, 16 135.6 ms
+#endif
+#if MC_GZ_PROFILE
+__device__ unsigned long long g_gz_prof[8];
+#endif
+// One wave per workgroup with LDS tables; a wave inflates kGzLanes blocks at
+// a time.  A lane's symbol loop is a chain of dependent short-latency steps,
+// and a window holds fewer blocks than the chip has lanes, so fewer blocks
+// per wave buys waves to hide that latency (and less divergence per step).
+constexpr int kGzLanes = MC_GZ_LDS ? MC_GZ_LANES : kGzBlock;
+constexpr int kGzThreads = MC_GZ_LDS ? 64 : kGzBlock;
+constexpr int64_t kGzSlotWords = mc::gz::kScratchWords + (MC_GZ_LDS ? 0 : mc::gz::kPrimaryWords);
+
+#ifndef MC_GZ_MIN_WAVES
+#define MC_GZ_MIN_WAVES 1      // __launch_bounds__ waves per SIMD (register budget)
+#endif
+__global__ void __launch_bounds__(kGzThreads, MC_GZ_MIN_WAVES)
 gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ blk, int64_t nblk,
                   uint8_t* __restrict__ out, uint16_t* __restrict__ scratch, int* __restrict__ status,
                   int* __restrict__ any_err) {
-    const int64_t lane = (int64_t)blockIdx.x * kGzBlock + threadIdx.x;
-    const int64_t lanes = (int64_t)gridDim.x * kGzBlock;
-    uint16_t* S = scratch + lane * mc::gz::kScratchWords;
+    if (threadIdx.x >= kGzLanes) return;
+    const int64_t lane = (int64_t)blockIdx.x * kGzLanes + threadIdx.x;
+    const int64_t lanes = (int64_t)gridDim.x * kGzLanes;
+    uint16_t* S = scratch + lane * kGzSlotWords;
+#if MC_GZ_LDS
+    using lds_u16 = __attribute__((address_space(3))) uint16_t;
+    __shared__ uint16_t tabs[kGzLanes * mc::gz::kPrimaryWords];
+    lds_u16* TL = (lds_u16*)(tabs + threadIdx.x * mc::gz::kPrimaryWords);
+#else
+    uint16_t* TL = S + mc::gz::kScratchWords;
+#endif
+    auto TD = TL + (1 << mc::gz::kLitBits);
     for (int64_t b = lane; b < nblk; b += lanes) {
         const GzBlock g = blk[b];
-        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S);
+#if MC_GZ_PROFILE
+        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, g_gz_prof);
+#else
+        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD);
+#endif
         status[b] = rc;
         if (rc) atomicOr(any_err, 1);
     }
@@ -493,7 +531,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     // scratch for the inflate lanes
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
-    const int64_t max_lanes = (int64_t)dev_cus * 8 * 64;   // 8 waves per CU (a multiple of kGzBlock)
+    const int64_t max_lanes = (int64_t)dev_cus * MC_GZ_WAVES_PER_CU * (MC_GZ_LDS ? kGzLanes : 64);
     size_t carry = 0;
     bool have_header = false;
     int64_t o = 0;
@@ -532,11 +570,12 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         HIP_TRY(g->status.reserve(nb + 1));
         HIP_TRY(hipMemsetAsync(g->status.p + nb, 0, sizeof(int), st));
         // a multiple of the workgroup: every launched lane owns a scratch slot
-        const int64_t lanes = std::min<int64_t>(max_lanes, (nb + kGzBlock - 1) / kGzBlock * kGzBlock);
-        HIP_TRY(g->scratch.reserve((size_t)lanes * mc::gz::kScratchWords));
+        // a multiple of the lanes per workgroup: every launched lane owns a scratch slot
+        const int64_t lanes = std::min<int64_t>(max_lanes, (nb + kGzLanes - 1) / kGzLanes * kGzLanes);
+        HIP_TRY(g->scratch.reserve((size_t)lanes * kGzSlotWords));
         g->t_read += (now_s() - t0) * 1e3;
         HIP_TRY(hipEventRecord(ev[0], st));
-        gz_inflate_kernel<<<(int)((lanes + kGzBlock - 1) / kGzBlock), kGzBlock, 0, st>>>(
+        gz_inflate_kernel<<<(int)(lanes / kGzLanes), kGzThreads, 0, st>>>(
             g->comp.p, g->blk.p, nb, g->inflated.p, g->scratch.p, g->status.p, g->status.p + nb);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ev[1], st));
@@ -604,6 +643,13 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     }
     HIP_TRY(hipStreamSynchronize(st));
     g->t_total = (now_s() - t_start) * 1e3;
+#if MC_GZ_PROFILE
+    unsigned long long pr[8];
+    HIP_TRY(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_gz_prof), sizeof pr));
+    std::fprintf(stderr, "[gz prof] build %.3g cyc  loop %.3g cyc  deflate blocks %llu  symbols %llu  matches %llu  "
+                 "copied %llu B  (per symbol %.1f cyc, build per block %.0f cyc)\n", (double)pr[0], (double)pr[1],
+                 pr[2], pr[3], pr[4], pr[5], pr[3] ? (double)pr[1] / pr[3] : 0.0, pr[2] ? (double)pr[0] / pr[2] : 0.0);
+#endif
     return MC_OK;
 }
 
@@ -682,10 +728,12 @@ extern "C" int mc_bam_gpu_close(mc_bam_gpu* g) {
 // same inflate.h code against zlib without a GPU).  Not a product path.
 extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize) {
     MC_REQUIRE(src && dst && clen >= 0 && isize >= 0, MC_E_INVALID, "bad argument");
-    std::vector<uint8_t> padded((size_t)clen + kPad + 4, 0);
+    std::vector<uint8_t> padded((size_t)clen + kPad + 32, 0);
     std::memcpy(padded.data(), src, (size_t)clen);
-    std::vector<uint16_t> scratch(mc::gz::kScratchWords);
-    const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data());
+    std::vector<uint16_t> scratch(mc::gz::kScratchWords + mc::gz::kPrimaryWords);
+    uint16_t* TL = scratch.data() + mc::gz::kScratchWords;
+    const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data(), TL,
+                                         TL + (1 << mc::gz::kLitBits));
     MC_REQUIRE(rc == 0, MC_E_IO, "inflate failed: %s", gz_err_msg(rc));
     return MC_OK;
 }

@@ -24,12 +24,30 @@ namespace gz {
 
 #define MC_HD __host__ __device__ __forceinline__
 
-constexpr int kLitBits = 10;    // primary table index bits, literal/length alphabet
-constexpr int kDistBits = 8;    // distance alphabet
-// per-lane scratch (u16 words)
-constexpr int kLitT = 0;                          // [1 << kLitBits] primary entries (sym << 4 | len)
-constexpr int kDistT = kLitT + (1 << kLitBits);   // [1 << kDistBits]
-constexpr int kLitCnt = kDistT + (1 << kDistBits);   // [16] codes per length
+#ifndef MC_GZ_PROFILE
+#define MC_GZ_PROFILE 0
+#endif
+#ifndef MC_GZ_QUEUE
+#define MC_GZ_QUEUE 16          // matches a lane defers (0: copy each at once)
+#endif
+#ifndef MC_GZ_COPY_BATCH
+#define MC_GZ_COPY_BATCH 1
+#endif
+
+// Tuning knobs (scripts/gz_ab.py): primary table bits, tables in LDS.
+#ifndef MC_GZ_LIT_BITS
+#define MC_GZ_LIT_BITS 8        // A/B (profiles/r03rc_gz_ab.txt): 8 with LDS tables; 9: half the lanes per CU
+#endif
+#ifndef MC_GZ_DIST_BITS
+#define MC_GZ_DIST_BITS 6
+#endif
+constexpr int kLitBits = MC_GZ_LIT_BITS;    // primary table index bits, literal/length alphabet
+constexpr int kDistBits = MC_GZ_DIST_BITS;  // distance alphabet
+static_assert(kLitBits >= 7, "the code length code (<= 7 bits) uses the literal table");
+constexpr int kPrimaryWords = (1 << kLitBits) + (1 << kDistBits);   // both primary tables (u16)
+// per-lane scratch (u16 words): counts, symbols, lengths (the primary tables
+// are separate: global scratch or LDS)
+constexpr int kLitCnt = 0;                        // [16] codes per length
 constexpr int kDistCnt = kLitCnt + 16;            // [16]
 constexpr int kLitSym = kDistCnt + 16;            // [288] symbols in canonical order
 constexpr int kDistSym = kLitSym + 288;           // [32]
@@ -49,34 +67,61 @@ enum : int {
     kErrSize = 8,          // the stream ended before ISIZE bytes
 };
 
-// Bit reader over src[0, clen): 32-bit aligned loads; the buffer src points
-// into must be readable up to 8 bytes past an aligned clen (callers pad it).
+// Bit reader over src[0, clen): 16-byte aligned loads, the next 16 bytes in
+// flight while the current ones are consumed (a lane's refill was a
+// dependent load every ~3 symbols).  The buffer src points into must be
+// readable up to 32 bytes past clen rounded up to 16 (callers pad it).
 struct Bits {
-    const uint32_t* w;      // next aligned word
-    const uint32_t* wend;   // words at or past it read as 0 (past the payload)
+    const uint4* p;         // next 16-byte group to load
+    const uint4* pend;      // groups at or past it read the last one again (past the payload)
+    uint4 cur, nxt;         // cur: words ci..3 not yet in buf
+    int ci;
     uint64_t buf;
     int cnt;                // valid bits in buf
-    int64_t end_bits;       // bits from src[0] to the end of the loaded words
+    int64_t end_bits;       // bits from src[0] to the end of the words moved into buf
 };
 
+// The address is clamped, not the value: a select on the loaded value made
+// the compiler wait for the load at once, defeating the prefetch.  Groups past
+// the payload are never consumed by a valid stream (bits_pos checks).
+MC_HD uint4 ld_group(const uint4* p, const uint4* pend) { return *(p < pend ? p : pend - 1); }
+
+MC_HD uint32_t word_of(const uint4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// (pointer arithmetic only, no integer round trip: the compiler keeps the
+// global address space and issues global loads, not flat ones, whose waits
+// also drain the lane's outstanding output stores)
 MC_HD void bits_init(Bits& b, const uint8_t* src, int64_t byte_off, int64_t clen) {
-    const uintptr_t a = (uintptr_t)(src + byte_off);
-    const int mis = (int)(a & 3);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a - (uintptr_t)mis);
-    b.wend = reinterpret_cast<const uint32_t*>(((uintptr_t)(src + clen) + 3) & ~(uintptr_t)3) + 1;
-    b.buf = (w < b.wend ? (uint64_t)*w : 0ull) >> (8 * mis);
-    b.cnt = 32 - 8 * mis;
-    b.w = w + 1;
-    b.end_bits = (byte_off + 4 - mis) * 8;
+    const uint8_t* a = src + byte_off;
+    const int mis = (int)((uintptr_t)a & 15);
+    const uint4* g = reinterpret_cast<const uint4*>(a - mis);
+    const uint8_t* e = src + clen;
+    b.pend = reinterpret_cast<const uint4*>(e + ((16 - (int)((uintptr_t)e & 15)) & 15)) + 1;
+    b.cur = ld_group(g, b.pend);
+    b.nxt = ld_group(g + 1, b.pend);
+    b.p = g + 2;
+    const int wi = mis >> 2, bi = mis & 3;
+    b.buf = (uint64_t)word_of(b.cur, wi) >> (8 * bi);
+    b.cnt = 32 - 8 * bi;
+    b.end_bits = (byte_off + 4 - bi) * 8;
+    b.ci = wi + 1;
+    if (b.ci == 4) {
+        b.cur = b.nxt;
+        b.nxt = ld_group(b.p++, b.pend);
+        b.ci = 0;
+    }
 }
 
 MC_HD void bits_refill(Bits& b) {   // afterwards cnt > 32
     if (b.cnt <= 32) {
-        const uint64_t x = b.w < b.wend ? (uint64_t)*b.w : 0ull;
-        b.buf |= x << b.cnt;
+        b.buf |= (uint64_t)word_of(b.cur, b.ci) << b.cnt;
         b.cnt += 32;
-        ++b.w;
         b.end_bits += 32;
+        if (++b.ci == 4) {
+            b.cur = b.nxt;
+            b.nxt = ld_group(b.p++, b.pend);
+            b.ci = 0;
+        }
     }
 }
 
@@ -102,7 +147,8 @@ MC_HD uint32_t bitrev(uint32_t code, int len) {
 // the primary table of `tb` index bits.  Over-subscribed lengths are an
 // error; incomplete codes are accepted (their missing patterns fail in
 // decode_slow).
-MC_HD int build_code(uint16_t* S, int t_off, int tb, int cnt_off, int sym_off, const uint16_t* lens, int n) {
+template <class TP>
+MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, int sym_off, const uint16_t* lens, int n) {
     uint16_t* cnt = S + cnt_off;
     uint16_t* sym = S + sym_off;
     uint16_t* offs = S + kOffs;
@@ -119,7 +165,6 @@ MC_HD int build_code(uint16_t* S, int t_off, int tb, int cnt_off, int sym_off, c
         const int l = lens[s] & 15;
         if (l) sym[offs[l]++] = (uint16_t)s;
     }
-    uint16_t* T = S + t_off;
     const int size = 1 << tb;
     for (int i = 0; i < size; ++i) T[i] = 0;
     uint32_t code = 0;
@@ -135,31 +180,43 @@ MC_HD int build_code(uint16_t* S, int t_off, int tb, int cnt_off, int sym_off, c
 }
 
 // RFC 1951 §3.2.2 walk over the code lengths (codes longer than the table,
-// and patterns the table does not hold): -1 when the bits are no code.
-MC_HD int decode_slow(uint64_t bits, const uint16_t* cnt, const uint16_t* sym, int* used) {
-    int code = 0, first = 0, index = 0;
+// and patterns the table does not hold): -1 when the bits are no code.  The
+// counts per length are registers (loaded once per table): walked from
+// memory, each length was a dependent global load, and with the walk
+// divergent some lane of the wave took it at most symbol steps.
+MC_HD int decode_slow(uint64_t bits, const int (&cnt)[16], const uint16_t* sym, int* used) {
+    int code = 0, first = 0, index = 0, found = -1, len = 0;
+#pragma unroll
     for (int l = 1; l < 16; ++l) {
         code |= (int)((bits >> (l - 1)) & 1u);
         const int count = cnt[l];
-        if (code - count < first) {
-            *used = l;
-            return sym[index + (code - first)];
+        if (found < 0 && code - count < first) {
+            found = index + (code - first);
+            len = l;
         }
         index += count;
         first = (first + count) << 1;
         code <<= 1;
     }
-    return -1;
+    if (found < 0) return -1;
+    *used = len;
+    return sym[found];
 }
 
-MC_HD int decode_sym(Bits& b, const uint16_t* S, int t_off, int tb, int cnt_off, int sym_off) {
-    const uint16_t e = S[t_off + ((uint32_t)b.buf & ((1u << tb) - 1u))];
+MC_HD void load_counts(const uint16_t* S, int cnt_off, int (&cnt)[16]) {
+#pragma unroll
+    for (int l = 0; l < 16; ++l) cnt[l] = S[cnt_off + l];
+}
+
+template <class TP>
+MC_HD int decode_sym(Bits& b, const uint16_t* S, TP T, int tb, const int (&cnt)[16], int sym_off) {
+    const uint16_t e = T[(uint32_t)b.buf & ((1u << tb) - 1u)];
     int used, s;
     if (e) {
         used = e & 15;
         s = e >> 4;
     } else {
-        s = decode_slow(b.buf, S + cnt_off, S + sym_off, &used);
+        s = decode_slow(b.buf, cnt, S + sym_off, &used);
         if (s < 0) return -1;
     }
     b.buf >>= used;
@@ -169,7 +226,8 @@ MC_HD int decode_sym(Bits& b, const uint16_t* S, int t_off, int tb, int cnt_off,
 
 // Dynamic block header: code length code, then the literal/length and
 // distance code lengths (RFC 1951 §3.2.7), then both tables.
-MC_HD int read_dynamic(Bits& b, uint16_t* S) {
+template <class TP>
+MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD) {
     bits_refill(b);
     const int nlen = (int)bits_take(b, 5) + 257;
     const int ndist = (int)bits_take(b, 5) + 1;
@@ -183,12 +241,14 @@ MC_HD int read_dynamic(Bits& b, uint16_t* S) {
         lens[order[i]] = (uint16_t)bits_take(b, 3);
     }
     // the code length code (<= 7 bits) goes through the literal table's slots
-    int rc = build_code(S, kLitT, 7, kLitCnt, kLitSym, lens, 19);
+    int rc = build_code(S, TL, 7, kLitCnt, kLitSym, lens, 19);
     if (rc) return rc;
+    int ccnt[16];
+    load_counts(S, kLitCnt, ccnt);
     int idx = 0;
     while (idx < nlen + ndist) {
         bits_refill(b);
-        const int sym = decode_sym(b, S, kLitT, 7, kLitCnt, kLitSym);
+        const int sym = decode_sym(b, S, TL, 7, ccnt, kLitSym);
         if (sym < 0) return kErrCodes;
         if (sym < 16) {
             lens[idx++] = (uint16_t)sym;
@@ -210,24 +270,119 @@ MC_HD int read_dynamic(Bits& b, uint16_t* S) {
     if (lens[256] == 0) return kErrCodes;
     // the distance lengths follow the literal ones in lens[]; the literal
     // table is built last because its build overwrites nothing of them
-    rc = build_code(S, kDistT, kDistBits, kDistCnt, kDistSym, lens + nlen, ndist);
+    rc = build_code(S, TD, kDistBits, kDistCnt, kDistSym, lens + nlen, ndist);
     if (rc) return rc;
-    return build_code(S, kLitT, kLitBits, kLitCnt, kLitSym, lens, nlen);
+    return build_code(S, TL, kLitBits, kLitCnt, kLitSym, lens, nlen);
 }
 
-MC_HD int read_fixed(uint16_t* S) {
+template <class TP>
+MC_HD int read_fixed(uint16_t* S, TP TL, TP TD) {
     uint16_t* lens = S + kLens;
     for (int s = 0; s < 288; ++s) lens[s] = (uint16_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
-    int rc = build_code(S, kLitT, kLitBits, kLitCnt, kLitSym, lens, 288);
+    int rc = build_code(S, TL, kLitBits, kLitCnt, kLitSym, lens, 288);
     if (rc) return rc;
     for (int s = 0; s < 30; ++s) lens[s] = 5;
-    return build_code(S, kDistT, kDistBits, kDistCnt, kDistSym, lens, 30);
+    return build_code(S, TD, kDistBits, kDistCnt, kDistSym, lens, 30);
+}
+
+// LZ77 copy of len bytes from dist back: every source byte precedes the
+// copy's first output byte, so a group's loads are all issued before its
+// stores (one memory round trip per 16 bytes, not per byte); the source
+// index runs modulo dist for overlapping copies.
+MC_HD void lz_copy(uint8_t* q, int len, int dist) {
+#if MC_GZ_COPY_BATCH
+    const uint8_t* s = q - dist;
+    int si = 0;
+    for (int k = 0; k < len; k += 16) {
+        uint8_t v[16];
+        int sj = si;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            v[j] = k + j < len ? s[sj] : 0;
+            sj = sj + 1 == dist ? 0 : sj + 1;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (k + j < len) q[k + j] = v[j];
+        si = sj;
+    }
+#else
+    for (int k = 0; k < len; ++k) q[k] = q[k - dist];
+#endif
 }
 
 // One raw deflate stream src[0, clen) into dst[0, isize): kOk iff it ends
-// (BFINAL) with exactly isize bytes and without reading past clen.
-MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S) {
+// (BFINAL) with exactly isize bytes and without reading past clen.  S: the
+// lane's scratch; TL / TD: its primary tables (1 << kLitBits, 1 << kDistBits).
+// prof (MC_GZ_PROFILE builds, else null): cycles in table builds and in the
+// symbol loops, deflate blocks, symbols, matches, copied bytes
+// TP: the tables' pointer type (uint16_t*, or an LDS-qualified pointer in the
+// kernel so lookups are ds_read, waited on by lgkmcnt alone).
+// A lane's deferred LZ77 copies.  With one lane per BGZF block, a copy
+// waits on its source bytes (global memory); done as decoded, some lane of
+// the wave has one at almost every symbol step (6 % of symbols are matches,
+// 1 - 0.94^64 = 98 %), so every step waited a memory round trip.  Queued, the
+// copies of all lanes run together when some lane's queue is full (a wave
+// vote), then at the block end.  The queue is registers (entries selected
+// by unrolled compares, no dynamic register indexing).
+struct MatchQueue {
+    uint64_t e[MC_GZ_QUEUE > 0 ? MC_GZ_QUEUE : 1];   // offset << 32 | dist << 9 | len
+    int n;
+};
+
+MC_HD void mq_flush(MatchQueue& q, uint8_t* dst) {
+#pragma unroll
+    for (int j = 0; j < (MC_GZ_QUEUE > 0 ? MC_GZ_QUEUE : 1); ++j) {
+        if (j < q.n) {
+            const uint64_t e = q.e[j];
+            lz_copy(dst + (uint32_t)(e >> 32), (int)(e & 511u), (int)((uint32_t)e >> 9));
+        }
+    }
+    q.n = 0;
+}
+
+MC_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __any(p);
+#else
+    return p;
+#endif
+}
+
+template <class TP>
+MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S, TP TL, TP TD,
+                        unsigned long long* prof = nullptr) {
     if (isize == 0) return kOk;
+#if MC_GZ_QUEUE
+    MatchQueue mq;
+    mq.n = 0;
+#endif
+#if MC_GZ_PROFILE
+    unsigned long long c_build = 0, c_loop = 0, n_blk = 0, n_sym = 0, n_match = 0, n_copy = 0;
+    auto tick = []() { return (unsigned long long)__builtin_readcyclecounter(); };
+    struct Flush {
+        unsigned long long* p;
+        unsigned long long *a, *b, *c, *d, *e, *f;
+        MC_HD ~Flush() {
+            if (p) {
+                __atomic_fetch_add(p + 0, *a, __ATOMIC_RELAXED);
+                __atomic_fetch_add(p + 1, *b, __ATOMIC_RELAXED);
+                __atomic_fetch_add(p + 2, *c, __ATOMIC_RELAXED);
+                __atomic_fetch_add(p + 3, *d, __ATOMIC_RELAXED);
+                __atomic_fetch_add(p + 4, *e, __ATOMIC_RELAXED);
+                __atomic_fetch_add(p + 5, *f, __ATOMIC_RELAXED);
+            }
+        }
+    } flush{prof, &c_build, &c_loop, &n_blk, &n_sym, &n_match, &n_copy};
+#define MC_GZ_TICK(v) unsigned long long v = tick()
+#define MC_GZ_ADD(dst, v) dst += tick() - v
+#define MC_GZ_CNT(dst, x) dst += (x)
+#else
+    (void)prof;
+#define MC_GZ_TICK(v)
+#define MC_GZ_ADD(dst, v)
+#define MC_GZ_CNT(dst, x)
+#endif
     Bits b;
     bits_init(b, src, 0, clen);
     const int64_t limit_bits = clen * 8;
@@ -251,12 +406,25 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
         } else if (type == 3) {
             return kErrBlockType;
         } else {
-            const int rc = type == 1 ? read_fixed(S) : read_dynamic(b, S);
+            MC_GZ_TICK(t0);
+            const int rc = type == 1 ? read_fixed(S, TL, TD) : read_dynamic(b, S, TL, TD);
+            MC_GZ_ADD(c_build, t0);
+            MC_GZ_CNT(n_blk, 1);
             if (rc) return rc;
+            int lcnt[16], dcnt[16];
+            load_counts(S, kLitCnt, lcnt);
+            load_counts(S, kDistCnt, dcnt);
+            MC_GZ_TICK(t1);
             for (;;) {
+                MC_GZ_CNT(n_sym, 1);
+#if MC_GZ_QUEUE
+                // all lanes still in a symbol loop vote: one full queue
+                // flushes every lane's (at most one push per iteration)
+                if (wave_any(mq.n == MC_GZ_QUEUE)) mq_flush(mq, dst);
+#endif
                 if (bits_pos(b) > limit_bits) return kErrInput;
                 bits_refill(b);
-                int s = decode_sym(b, S, kLitT, kLitBits, kLitCnt, kLitSym);
+                int s = decode_sym(b, S, TL, kLitBits, lcnt, kLitSym);
                 if (s < 0) return kErrSymbol;
                 if (s < 256) {
                     if (o >= isize) return kErrOutput;
@@ -276,7 +444,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                     len = ((4 + (s & 3)) << e) + 3 + (int)bits_take(b, e);
                 }
                 bits_refill(b);
-                const int d = decode_sym(b, S, kDistT, kDistBits, kDistCnt, kDistSym);
+                const int d = decode_sym(b, S, TD, kDistBits, dcnt, kDistSym);
                 if (d < 0 || d >= 30) return kErrSymbol;
                 int dist;
                 if (d < 4) {
@@ -287,15 +455,32 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                 }
                 if ((int64_t)dist > o) return kErrDistance;
                 if (o + len > isize) return kErrOutput;
-                uint8_t* q = dst + o;
-                for (int k = 0; k < len; ++k) q[k] = q[k - dist];
+#if MC_GZ_QUEUE
+                {
+                    const uint64_t e = ((uint64_t)o << 32) | ((uint32_t)dist << 9) | (uint32_t)len;
+#pragma unroll
+                    for (int j = 0; j < MC_GZ_QUEUE; ++j) mq.e[j] = j == mq.n ? e : mq.e[j];
+                    ++mq.n;
+                }
+#else
+                lz_copy(dst + o, len, dist);
+#endif
+                MC_GZ_CNT(n_match, 1);
+                MC_GZ_CNT(n_copy, len);
                 o += len;
             }
+            MC_GZ_ADD(c_loop, t1);
         }
         if (bits_pos(b) > limit_bits) return kErrInput;
         if (final) break;
     }
+#if MC_GZ_QUEUE
+    mq_flush(mq, dst);
+#endif
     return o == isize ? kOk : kErrSize;
+#undef MC_GZ_TICK
+#undef MC_GZ_ADD
+#undef MC_GZ_CNT
 }
 
 // ---------------------------------------------------------------- BAM records

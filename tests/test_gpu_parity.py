@@ -344,10 +344,12 @@ def test_classic_api(lib_built, fixture_golden, golden_dir):
 
 
 @pytest.mark.parametrize("mode", ["blast7", "whole"])
-def test_cli_csv_bytes(lib_built, fixture_golden, golden_dir, tmp_path, mode):
+@pytest.mark.parametrize("decode", ["gpu", "host"])
+def test_cli_csv_bytes(lib_built, fixture_golden, golden_dir, tmp_path, mode, decode):
     from click.testing import CliRunner
     from metacov_amd.cli import pileup as cli_pileup
-    args = ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"), "-o", str(tmp_path / "o.csv")]
+    args = ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"), "-o", str(tmp_path / "o.csv"),
+            "--decode", decode]
     if mode == "blast7":
         args += ["-rb", os.path.join(golden_dir, "regions.blast7")]
     res = CliRunner().invoke(cli_pileup, args)
