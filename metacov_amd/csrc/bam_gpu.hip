@@ -235,8 +235,14 @@ template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t cap = 0;
-    ~DBuf() {
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }
+    void release() {
         if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
     }
     // keep_elems: the first elements survive a reallocation
     hipError_t reserve(size_t n, hipStream_t st = nullptr, size_t keep_elems = 0) {
@@ -264,6 +270,9 @@ template <typename T>
 struct PinnedBuf {
     T* p = nullptr;
     size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
     ~PinnedBuf() {
         if (p) (void)hipHostFree(p);
     }
@@ -293,7 +302,8 @@ struct mc_bam_gpu {
     uint32_t flag_filter = 0;
     DBuf<int32_t> tid, pos, span;     // kept intervals, file order
     int64_t n_kept = 0;
-    DBuf<uint8_t> comp, inflated, tail;
+    DBuf<uint8_t> comp[2], inflated, tail;   // comp: window k's compressed bytes in comp[k & 1]
+    hipStream_t up_stream = nullptr;          // uploads of the next window (overlap the current one's kernels)
     DBuf<GzBlock> blk;
     DBuf<int> status;
     DBuf<uint16_t> scratch;
@@ -307,9 +317,11 @@ struct mc_bam_gpu {
     double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0;
     int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
     ~mc_bam_gpu() {
-        if (stream) {
-            (void)hipStreamSynchronize(stream);
-            (void)hipStreamDestroy(stream);
+        for (hipStream_t s : {stream, up_stream}) {
+            if (s) {
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamDestroy(s);
+            }
         }
     }
 };
@@ -341,7 +353,7 @@ const char* gz_err_msg(int e) {
 
 // File bytes [off, off + len) into device memory at dst: pread on threads
 // into a pinned staging slice, copied up while the next slice is read.
-int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst) {
+int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst, hipStream_t st) {
     constexpr size_t kSlice = 64ull << 20;
     for (auto& s : g->stage) HIP_TRY(s.reserve(kSlice));
     hipEvent_t done[2] = {nullptr, nullptr};
@@ -378,11 +390,11 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
         work(0);
         for (auto& th : pool) th.join();
         MC_REQUIRE(!bad, MC_E_IO, "%s: read failed at offset %zu", g->path.c_str(), off + at);
-        HIP_TRY(hipMemcpyAsync(dst + at, buf, n, hipMemcpyHostToDevice, g->stream));
-        HIP_TRY(hipEventRecord(done[k], g->stream));
+        HIP_TRY(hipMemcpyAsync(dst + at, buf, n, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(done[k], st));
         used[k] = true;
     }
-    HIP_TRY(hipStreamSynchronize(g->stream));
+    HIP_TRY(hipStreamSynchronize(st));
     return MC_OK;
 }
 
@@ -532,23 +544,80 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
     const int64_t max_lanes = (int64_t)dev_cus * MC_GZ_WAVES_PER_CU * (MC_GZ_LDS ? kGzLanes : 64);
+    // windows of blocks (<= win inflated bytes each, at least one block)
+    std::vector<std::pair<size_t, size_t>> wins;
+    for (size_t b0 = 0; b0 < blocks.size();) {
+        size_t b1 = b0, wsize = 0;
+        while (b1 < blocks.size() && (b1 == b0 || wsize + blocks[b1].isize <= win)) wsize += blocks[b1++].isize;
+        wins.emplace_back(b0, b1);
+        b0 = b1;
+    }
+    MC_REQUIRE(!wins.empty(), MC_E_IO, "%s: no valid BAM header", g->path.c_str());
+    auto crange = [&](size_t w, size_t* coff, size_t* clen) {
+        *coff = blocks[wins[w].first].off;
+        const size_t b1 = wins[w].second;
+        *clen = (b1 < blocks.size() ? blocks[b1].off : mf.size) - *coff;
+    };
+    // window w's compressed bytes into comp[w & 1] on the upload stream (an
+    // uploader thread runs it for window w + 1 while window w is inflated)
+    struct Upload {
+        int rc = MC_OK;
+        std::string msg;
+        double s = 0;
+    };
+    auto upload = [&](size_t w, Upload* u) {
+        const double t0 = now_s();
+        size_t coff, clen;
+        crange(w, &coff, &clen);
+        auto run = [&]() -> int {
+            HIP_TRY(hipSetDevice(g->device));
+            DBuf<uint8_t>& c = g->comp[w & 1];
+            HIP_TRY(c.reserve(clen + kPad));
+            if (int rc = upload_file_range(g, mf.fd, coff, clen, c.p, g->up_stream)) return rc;
+            HIP_TRY(hipMemsetAsync(c.p + clen, 0, kPad, g->up_stream));
+            HIP_TRY(hipStreamSynchronize(g->up_stream));
+            return MC_OK;
+        };
+        u->rc = run();
+        if (u->rc) u->msg = mc::last_error();
+        u->s = now_s() - t0;
+    };
+    struct Joiner {
+        std::thread t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } uploader;
+    Upload up_next;
     size_t carry = 0;
     bool have_header = false;
     int64_t o = 0;
-    size_t b0 = 0;
-    while (b0 < blocks.size() || !have_header) {
-        MC_REQUIRE(b0 < blocks.size(), MC_E_IO, "%s: no valid BAM header", g->path.c_str());
-        size_t b1 = b0, wsize = 0;
-        while (b1 < blocks.size() && (b1 == b0 || wsize + blocks[b1].isize <= win)) wsize += blocks[b1++].isize;
-        const bool last = b1 == blocks.size();
-        const size_t coff = blocks[b0].off;
-        const size_t cend = b1 < blocks.size() ? blocks[b1].off : mf.size;
-        const size_t clen = cend - coff;
-        // compressed window up, block table up
+    for (size_t w = 0; w < wins.size(); ++w) {
+        const size_t b0 = wins[w].first, b1 = wins[w].second;
+        size_t wsize = 0;
+        for (size_t b = b0; b < b1; ++b) wsize += blocks[b].isize;
+        const bool last = w + 1 == wins.size();
+        size_t coff, clen;
+        crange(w, &coff, &clen);
+        // this window's upload: done now (the first) or by the uploader
         const double t0 = now_s();
-        HIP_TRY(g->comp.reserve(clen + kPad));
-        if (int rc = upload_file_range(g, mf.fd, coff, clen, g->comp.p)) return rc;
-        HIP_TRY(hipMemsetAsync(g->comp.p + clen, 0, kPad, st));
+        Upload cur;
+        if (w == 0) {
+            upload(0, &cur);
+        } else {
+            uploader.t.join();
+            cur = up_next;
+        }
+        if (cur.rc) {
+            mc::set_error("%s", cur.msg.c_str());
+            return cur.rc;
+        }
+        g->t_read += (now_s() - t0) * 1e3;   // the part not hidden behind the previous window
+        if (!last) {
+            up_next = Upload();
+            uploader.t = std::thread(upload, w + 1, &up_next);
+        }
+        uint8_t* comp = g->comp[w & 1].p;
         const int64_t nb = (int64_t)(b1 - b0);
         HIP_TRY(g->hblk.reserve(nb));
         for (int64_t i = 0; i < nb; ++i) {
@@ -573,10 +642,9 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         // a multiple of the lanes per workgroup: every launched lane owns a scratch slot
         const int64_t lanes = std::min<int64_t>(max_lanes, (nb + kGzLanes - 1) / kGzLanes * kGzLanes);
         HIP_TRY(g->scratch.reserve((size_t)lanes * kGzSlotWords));
-        g->t_read += (now_s() - t0) * 1e3;
         HIP_TRY(hipEventRecord(ev[0], st));
         gz_inflate_kernel<<<(int)(lanes / kGzLanes), kGzThreads, 0, st>>>(
-            g->comp.p, g->blk.p, nb, g->inflated.p, g->scratch.p, g->status.p, g->status.p + nb);
+            comp, g->blk.p, nb, g->inflated.p, g->scratch.p, g->status.p, g->status.p + nb);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ev[1], st));
         int any = 0;
@@ -619,7 +687,6 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
                 // the header continues in the next window: keep everything
                 MC_REQUIRE(!last, MC_E_IO, "%s: no valid BAM header", g->path.c_str());
                 carry = n;
-                b0 = b1;
                 ++g->windows;
                 continue;
             }
@@ -638,7 +705,6 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
             HIP_TRY(hipMemcpyAsync(g->inflated.p, g->tail.p, carry, hipMemcpyDeviceToDevice, st));
         }
         o = 0;
-        b0 = b1;
         ++g->windows;
     }
     HIP_TRY(hipStreamSynchronize(st));
@@ -669,11 +735,14 @@ extern "C" int mc_bam_gpu_open(const char* path, int device, int n_threads, uint
     g->nt = n_threads > 0 ? n_threads : std::min(16, n_threads_or_all(0));   // file reads only
     g->flag_filter = flag_filter;
     HIP_TRY(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&g->up_stream, hipStreamNonBlocking));
     if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
     // the staging and parse buffers are not needed after the decode
-    g->comp = DBuf<uint8_t>();
-    g->inflated = DBuf<uint8_t>();
-    g->scratch = DBuf<uint16_t>();
+    g->comp[0].release();
+    g->comp[1].release();
+    g->inflated.release();
+    g->tail.release();
+    g->scratch.release();
     *out = g.release();
     return MC_OK;
 }
