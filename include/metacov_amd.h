@@ -305,7 +305,8 @@ int mc_bam_open_contigs(const char* path, const char* bai_path, int n_threads,
  * window (0 = 4 GiB); a record cut by a window is carried to the next.
  * The kept intervals stay in device memory owned by the handle
  * (mc_bam_gpu_intervals_device: valid until mc_bam_gpu_close; hand them to
- * mc_add_reads_device).  Replaces, like mc_bam_open, the record walk under
+ * mc_add_reads_device); so do the decode's window buffers (about 2.5 x the
+ * window size) until mc_bam_gpu_close.  Replaces, like mc_bam_open, the record walk under
  * pysam's pileup (IteratorRowAll, scan.pyx:204-216). */
 typedef struct mc_bam_gpu mc_bam_gpu;
 typedef struct mc_bam_gpu_timings {
@@ -318,6 +319,7 @@ typedef struct mc_bam_gpu_timings {
     int64_t resyncs;     /* segment starts corrected after a walk (sync false positives) */
     int64_t compressed_bytes;
     int64_t inflated_bytes;
+    double scan_ms;      /* host: BGZF block header scan */
 } mc_bam_gpu_timings;
 int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
                     int64_t window_bytes, mc_bam_gpu** out);
