@@ -337,6 +337,12 @@ def main():
         if world > 1:
             if works[i] is not None:   # this buffer's previous gather must be done
                 works[i].wait()
+                # RCCL: wait() only orders torch's current stream after the
+                # gather; the engine writes the buffer on its own stream, so
+                # the host waits for the gather itself (done two steps ago,
+                # normally: one event query)
+                while coll_dev.type == "cuda" and not works[i].is_completed():
+                    time.sleep(0)
                 works[i] = None
             tbl = xbufs[i][:R]
         if args.cigar:   # a fresh raw-CIGAR batch: K1 + prepare run inside this step

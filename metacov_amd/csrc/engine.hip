@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -258,6 +259,8 @@ struct mc_ctx {
     int64_t device_recomputes = 0;
     bool fused_clean = false;             // K3b left hist / low / acc / queue initialised
     int64_t fused_clean_R = 0;
+    bool check_clean = false;             // MC_CHECK_CLEAN=1: verify a skipped fused_init on the device
+    DevBuf<unsigned long long> d_check;   // [1] its mismatch count
     int64_t fused_fallbacks = 0;
 
     hipEvent_t ev[8] = {};
@@ -318,6 +321,7 @@ extern "C" int mc_ctx_create(int device, mc_ctx** out) {
         return MC_E_HIP;
     }
     c->own_stream = true;
+    if (const char* v = getenv("MC_CHECK_CLEAN")) c->check_clean = v[0] && v[0] != '0';
     for (auto& ev : c->ev) (void)hipEventCreate(&ev);
     for (auto& T : c->ts)
         for (auto& ev : T.e) (void)hipEventCreate(&ev);
@@ -1414,6 +1418,19 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                            ctx->d_maxdepth.p);
         HIP_TRY(hipGetLastError());
         ctx->fcache.chunk_first = true;
+    } else if (ctx->check_clean) {
+        // debug: the buffers the skipped init would have written must already
+        // hold its values (a path that used them without clearing the clean
+        // flag shows up here as MC_E_STATE, not as silently wrong statistics)
+        HIP_TRY(ctx->d_check.reserve(1));
+        HIP_TRY(hipMemsetAsync(ctx->d_check.p, 0, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(fused_clean_check_kernel, dim3(1024), dim3(kBlock), 0, s, ctx->d_fhist.p, R * vals,
+                           ctx->d_flow.p, ctx->d_acc.p, R, ctx->d_queue.p, ctx->d_maxdepth.p, ctx->d_check.p);
+        HIP_TRY(hipGetLastError());
+        unsigned long long bad = 0;
+        HIP_TRY(hipMemcpyAsync(&bad, ctx->d_check.p, sizeof bad, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        MC_REQUIRE(bad == 0, MC_E_STATE, "fused buffers not initialised on a clean call (%llu words differ)", bad);
     }
     FusedRegions fr{nf,
                     ctx->d_fchunk.p,

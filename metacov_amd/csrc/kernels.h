@@ -2139,6 +2139,29 @@ fused_init_kernel(unsigned* __restrict__ hist, int64_t hist_words, unsigned* __r
     }
 }
 
+// Debug check of the skipped fused_init (MC_CHECK_CLEAN=1 in the environment):
+// the buffers a clean call relies on hold exactly what fused_init_kernel
+// would write; every word that does not counts into *bad.
+__global__ void __launch_bounds__(kBlock)
+fused_clean_check_kernel(const unsigned* __restrict__ hist, int64_t hist_words, const unsigned* __restrict__ low,
+                         const RegionAcc* __restrict__ acc, int64_t R, const unsigned* __restrict__ queue,
+                         const int* __restrict__ max_depth, unsigned long long* __restrict__ bad) {
+    unsigned long long n = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 8) {
+        if (queue && queue[threadIdx.x] != 0) ++n;
+        if (max_depth && threadIdx.x < 4 && max_depth[threadIdx.x] != 0) ++n;
+    }
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    for (int64_t q = i0; q < hist_words; q += stride) n += hist[q] != 0;
+    for (int64_t r = i0; r < R; r += stride) {
+        n += (low && low[r] != 0) ? 1 : 0;
+        n += (acc[r].sum != 0) + (acc[r].sumsq != 0) + (acc[r].min != 0x7fffffff) + (acc[r].max != 0);
+    }
+    n = (unsigned long long)wave_sum64((long long)n);
+    if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
+}
+
 // One workgroup per segment (<= kSeg positions of one region, clipped to
 // the contig extent).  Builds the value histogram only (bins 0..nbins-1 cover
 // every depth: nbins = max depth + 1); region_final_kernel derives min, max,

@@ -688,10 +688,23 @@ def test_fused_timing_totals(eng):
     assert dk2 >= t1["depth_ms"] * 0.99   # three launches, the last one among them
 
 
-def test_fused_clean_buffers_across_mixed_calls(eng):
+@pytest.fixture
+def eng_checked(lib_built, monkeypatch):
+    """An engine that verifies every skipped fused_init on the device
+    (MC_CHECK_CLEAN=1, read at mc_ctx_create): a stale buffer is MC_E_STATE."""
+    monkeypatch.setenv("MC_CHECK_CLEAN", "1")
+    e = CoverageEngine(0)
+    yield e
+    e.close()
+
+
+def test_fused_clean_buffers_across_mixed_calls(eng_checked):
     """K3b leaves the fused buffers initialised for the next call on the same
     regions (no init launch); a plain K2, a K3 pass, a fallback or a
-    re-prepare in between must not leave stale queue / histogram state."""
+    re-prepare in between must not leave stale queue / histogram state.  The
+    engine also checks on the device, before each clean call, that every
+    buffer the skipped init would write holds its initial value."""
+    eng = eng_checked
     lengths, tid, pos, span = make_case([60_000, 90_000, 30_000], 30_000, (1, 300), 31)
     d, ext, coff = coracle.depth(lengths, tid, pos, span)
     whole = (np.arange(3, dtype=np.int32), np.zeros(3, np.int64), np.asarray(lengths, np.int64))
