@@ -251,11 +251,15 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # ex: the region-table exchange runs (N > 1; or one torchrun rank with
+    # MC_BENCH_FORCE_EXCHANGE=1, which exercises the RCCL all-gather path on a
+    # one-GPU box: tests/test_gpu_parity.py::test_bench_rccl_exchange_one_rank)
+    ex = world > 1 or ("WORLD_SIZE" in os.environ and os.environ.get("MC_BENCH_FORCE_EXCHANGE") == "1")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if ex:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -309,7 +313,7 @@ def main():
     xbufs = coll_bufs = gouts = gidx = None
     works = [None, None]   # in-flight all-gathers, one per exchange buffer
     n_calls = [0]
-    if world > 1:
+    if ex:
         # two exchange buffers, allocated once: [r_max, 9 stats]; the engine
         # writes a batch's rows straight into the first R of one (no copy per
         # step) while the previous batch's all-gather may still read the other,
@@ -334,7 +338,7 @@ def main():
         i = n_calls[0] & 1
         n_calls[0] += 1
         tbl = table
-        if world > 1:
+        if ex:
             if works[i] is not None:   # this buffer's previous gather must be done
                 works[i].wait()
                 # RCCL: wait() only orders torch's current stream after the
@@ -355,7 +359,7 @@ def main():
             eng.region_stats_device(rt, rs, re_, tbl.data_ptr())
         else:
             eng.compute_depth_stats_device(rt, rs, re_, tbl.data_ptr())
-        if world > 1:   # the rows are in the exchange buffer already: one all-gather
+        if ex:   # the rows are in the exchange buffer already: one all-gather
             if coll_bufs[i] is not xbufs[i]:   # (gloo: through host memory)
                 coll_bufs[i].copy_(xbufs[i])
             works[i] = dist.all_gather_into_tensor(gouts[i], coll_bufs[i], async_op=True)
@@ -370,7 +374,7 @@ def main():
     def sync_all():
         drain()
         torch.cuda.synchronize()
-        if world > 1:
+        if ex:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -423,7 +427,7 @@ def main():
         elapsed_re, re_k, _ = timed(args.prepare_steps, False)
     # the region-table exchange alone (RCCL all-gather over xGMI), timed apart
     allgather_ms = None
-    if world > 1:
+    if ex:
         n_ag = max(5, args.steps)
         sync_all()
         ta = time.perf_counter()
@@ -433,7 +437,7 @@ def main():
         allgather_ms = (time.perf_counter() - ta) / n_ag * 1e3
     t_max, t_max_re = elapsed, elapsed_re
     total_bases = bases
-    if world > 1:
+    if ex:
         t = torch.tensor([elapsed, elapsed_re or 0.0, allgather_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t[0].item())
@@ -556,8 +560,8 @@ def main():
             "cpu_baseline_parallel": cpu_par,
             "cpu_interval_count": cpu_int,
             "world_size": world,
-            "ranks_seen": dist.get_world_size() if world > 1 else 1,
-            "backend": (args.backend if world > 1 else None),
+            "ranks_seen": dist.get_world_size() if ex else 1,
+            "backend": (args.backend if ex else None),
             "allgather_ms": allgather_ms,
         }
         if t_max_re is not None:
@@ -575,7 +579,7 @@ def main():
             line["host_buffer_end_to_end_s"] = pcie
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if ex:
         dist.destroy_process_group()
 
 

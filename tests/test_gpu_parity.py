@@ -1053,6 +1053,38 @@ def test_bench_gpus_two_launches_ranks(tmp_path):
     assert d["value"] > 0
 
 
+def test_bench_rccl_exchange_one_rank(tmp_path):
+    """The bench's RCCL path on the one-GPU box: one torchrun rank with
+    MC_BENCH_FORCE_EXCHANGE=1 runs the nccl process group, the asynchronous
+    device-tensor all-gathers into alternating exchange buffers (with the
+    host-side completion wait before a buffer is rewritten) and the timed
+    all-gather, then checks the gathered table's bases (bench.py asserts it)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env["MC_BENCH_FORCE_EXCHANGE"] = "1"
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(root, "bench.py"), "--backend", "nccl", "--config", "c3",
+                          "--reads", "2000000", "--contigs", "64", "--steps", "6", "--warmup", "2",
+                          "--prepare-steps", "2", "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["ranks_seen"] == 1 and d["backend"] == "nccl"
+    assert d["allgather_ms"] is not None and d["allgather_ms"] > 0
+    assert d["config"]["regions"] == 64 and d["value"] > 0
+
+
 def test_library_then_torch_same_process():
     """The library first, torch after it, in one fresh process: one HIP
     runtime is shared (metacov_amd._lib preloads PyTorch's), so torch still
