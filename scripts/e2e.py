@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--length", type=int, default=5_000_000, help="bp per contig")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--gpu-windows", default="",
+                    help="comma-separated inflated window sizes in MiB: extra GPU decodes of the same file, "
+                         "timed (window_sweep in the JSON)")
     a = ap.parse_args()
     import numpy as np
     from metacov_amd import synth, regions as mreg
@@ -85,6 +88,17 @@ def main():
     assert out3.getvalue() == csv_full, "GPU-decoded CSV differs"
     gtm = gb.timings()
     gb.close()
+    sweep = []
+    for mib in [int(x) for x in a.gpu_windows.split(",") if x]:
+        t0 = time.perf_counter()
+        gw = GpuBamFile(path, device=0, n_threads=a.threads, window_bytes=mib << 20)
+        dt = time.perf_counter() - t0
+        wt = gw.timings()
+        assert gw.n_kept == n_kept
+        gw.close()
+        sweep.append({"window_mib": mib, "decode_s": dt, **{k: wt[k] for k in
+                      ("read_ms", "inflate_ms", "parse_ms", "scan_ms", "total_ms", "windows")}})
+        print(json.dumps(sweep[-1]), file=sys.stderr, flush=True)
     print(json.dumps({
         "bam_bytes": os.path.getsize(path), "records": n_rec, "kept": n_kept,
         "aligned_bases": bases, "host_threads": a.threads,
@@ -97,7 +111,8 @@ def main():
         "stream_end_to_end_aligned_bases_per_s": bases / (t_stream + t_cmp2),
         "gpu_decode_s": t_gdec, "gpu_decode_timings": gtm, "gpu_ingest_s": t_ging,
         "gpudec_stats_csv_s": t_cmp3, "gpu_end_to_end_s": t_gdec + t_ging + t_cmp3,
-        "gpu_end_to_end_aligned_bases_per_s": bases / (t_gdec + t_ging + t_cmp3)}))
+        "gpu_end_to_end_aligned_bases_per_s": bases / (t_gdec + t_ging + t_cmp3),
+        "window_sweep": sweep}))
     os.remove(path)
 
 
