@@ -304,6 +304,7 @@ struct mc_bam_gpu {
     int64_t n_kept = 0;
     DBuf<uint8_t> comp[2], inflated, tail;   // comp: window k's compressed bytes in comp[k & 1]
     hipStream_t up_stream = nullptr;          // uploads of the next window (overlap the current one's kernels)
+    hipStream_t kstream[3] = {};              // resident decode: inflate streams besides `stream`
     DBuf<GzBlock> blk;
     DBuf<int> status;
     DBuf<uint16_t> scratch;
@@ -317,7 +318,7 @@ struct mc_bam_gpu {
     double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0, t_scan = 0;
     int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
     ~mc_bam_gpu() {
-        for (hipStream_t s : {stream, up_stream}) {
+        for (hipStream_t s : {stream, up_stream, kstream[0], kstream[1], kstream[2]}) {
             if (s) {
                 (void)hipStreamSynchronize(s);
                 (void)hipStreamDestroy(s);
@@ -602,6 +603,142 @@ int scan_blocks_parallel(const uint8_t* d, size_t n, int nt, std::vector<Block>&
     return MC_OK;
 }
 
+// Header from a growing prefix of the inflated bytes [0, n): *ok = false if
+// no prefix holds a complete one.
+int header_from_prefix(mc_bam_gpu* g, size_t n, int64_t* o, bool* ok) {
+    *ok = false;
+    size_t p = std::min<size_t>(n, 1 << 20);
+    std::vector<uint8_t> hb;
+    for (;;) {
+        hb.resize(p);
+        HIP_TRY(hipMemcpy(hb.data(), g->inflated.p, p, hipMemcpyDeviceToHost));
+        std::vector<std::string> names;
+        std::vector<int64_t> lens;
+        size_t ho = 0;
+        if (parse_header(hb.data(), p, g->path.c_str(), names, lens, &ho) == MC_OK) {
+            g->hdr.names = std::move(names);
+            g->hdr.lens = std::move(lens);
+            *o = (int64_t)ho;
+            *ok = true;
+            return MC_OK;
+        }
+        if (p >= n) return MC_OK;
+        p = std::min(n, p * 4);
+    }
+}
+
+// Resident decode (the default when the compressed file and its inflated
+// stream fit in HBM): the file goes up in pieces of about a quarter of the
+// inflated stream, and each piece's inflate kernel is launched as soon as its
+// bytes are on the device, on alternating streams, into the piece's final
+// place in one inflated buffer.  A kernel's time has a floor (its slowest
+// lanes decode a whole block serially: ~72 ms for any window of 4 k to 32 k
+// blocks, profiles/r03sd_e2e_window_sweep.json), so successive pieces' kernels
+// overlap each other and the remaining uploads instead of running one window
+// after another; no carry between windows, one parse at the end.
+#ifndef MC_GZ_PIECE_STREAMS
+#define MC_GZ_PIECE_STREAMS 2
+#endif
+#ifndef MC_GZ_PIECES
+#define MC_GZ_PIECES 4                 // pieces per inflated stream (each >= 256 MiB, <= 4 GiB)
+#endif
+static_assert(MC_GZ_PIECE_STREAMS >= 1 && MC_GZ_PIECE_STREAMS <= 4, "inflate streams: stream + kstream[]");
+constexpr int kGzPieceStreams = MC_GZ_PIECE_STREAMS;
+
+int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<Block>& blocks, size_t total,
+                        int64_t max_lanes) {
+    const int64_t nb = (int64_t)blocks.size();
+    hipStream_t st = g->stream;
+    const size_t piece = std::min<size_t>(4ull << 30, std::max<size_t>(256ull << 20, total / MC_GZ_PIECES));
+    std::vector<std::pair<size_t, size_t>> pcs;
+    for (size_t b0 = 0; b0 < blocks.size();) {
+        size_t b1 = b0, sz = 0;
+        while (b1 < blocks.size() && (b1 == b0 || sz + blocks[b1].isize <= piece)) sz += blocks[b1++].isize;
+        pcs.emplace_back(b0, b1);
+        b0 = b1;
+    }
+    HIP_TRY(g->comp[0].reserve(mf.size + kPad));
+    HIP_TRY(g->inflated.reserve(total + 8));
+    HIP_TRY(g->hblk.reserve(nb));
+    for (int64_t i = 0; i < nb; ++i) {
+        const Block& b = blocks[i];
+        g->hblk.p[i] = GzBlock{(int64_t)b.cdata, (int64_t)b.out, (int32_t)b.clen, (int32_t)b.isize};
+    }
+    HIP_TRY(g->blk.reserve(nb));
+    HIP_TRY(g->status.reserve(nb + 1));
+    const int64_t slot = max_lanes * kGzSlotWords;   // scratch per inflate stream
+    HIP_TRY(g->scratch.reserve((size_t)(kGzPieceStreams * slot)));
+    HIP_TRY(hipMemcpyAsync(g->blk.p, g->hblk.p, nb * sizeof(GzBlock), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(g->status.p + nb, 0, sizeof(int), st));
+    HIP_TRY(hipMemsetAsync(g->comp[0].p + mf.size, 0, kPad, st));
+    hipStream_t ks[kGzPieceStreams];
+    ks[0] = st;
+    for (int k = 1; k < kGzPieceStreams; ++k) {
+        if (!g->kstream[k - 1]) HIP_TRY(hipStreamCreateWithFlags(&g->kstream[k - 1], hipStreamNonBlocking));
+        ks[k] = g->kstream[k - 1];
+    }
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() {
+            for (int i = 0; i < 2; ++i)
+                if (e[i]) (void)hipEventDestroy(e[i]);
+        }
+    } evg{ev};
+    HIP_TRY(hipEventRecord(ev[0], st));   // block table, status flag and pad are set
+    for (int k = 1; k < kGzPieceStreams; ++k) HIP_TRY(hipStreamWaitEvent(ks[k], ev[0], 0));
+    double t_first = now_s();
+    for (size_t p = 0; p < pcs.size(); ++p) {
+        const size_t b0 = pcs[p].first, b1 = pcs[p].second;
+        const size_t coff = blocks[b0].off, cend = b1 < blocks.size() ? blocks[b1].off : mf.size;
+        const double t0 = now_s();
+        // returns once the bytes are on the device (its stream synchronised)
+        if (int rc = upload_file_range(g, mf.fd, coff, cend - coff, g->comp[0].p + coff, g->up_stream)) return rc;
+        if (p == 0) {
+            g->t_read = (now_s() - t0) * 1e3;   // the exposed part: the first piece
+            t_first = now_s();
+        }
+        const int64_t n = (int64_t)(b1 - b0);
+        const int64_t lanes = std::min<int64_t>(max_lanes, (n + kGzLanes - 1) / kGzLanes * kGzLanes);
+        const int k = (int)(p % kGzPieceStreams);
+        gz_inflate_kernel<<<(int)(lanes / kGzLanes), kGzThreads, 0, ks[k]>>>(
+            g->comp[0].p, g->blk.p + b0, n, g->inflated.p, g->scratch.p + k * slot, g->status.p + b0,
+            g->status.p + nb);
+        HIP_TRY(hipGetLastError());
+    }
+    for (int k = 1; k < kGzPieceStreams; ++k) {
+        HIP_TRY(hipEventRecord(ev[1], ks[k]));
+        HIP_TRY(hipStreamWaitEvent(st, ev[1], 0));
+    }
+    int any = 0;
+    HIP_TRY(hipMemcpyAsync(&any, g->status.p + nb, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    g->t_inflate = (now_s() - t_first) * 1e3;
+    g->windows = (int64_t)pcs.size();
+    if (any) {
+        std::vector<int> sv(nb);
+        HIP_TRY(hipMemcpy(sv.data(), g->status.p, nb * sizeof(int), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < nb; ++i)
+            if (sv[i]) {
+                mc::set_error("BGZF inflate failed in %s (block at file offset %zu: %s)", g->path.c_str(),
+                              blocks[i].off, gz_err_msg(sv[i]));
+                return MC_E_IO;
+            }
+    }
+    int64_t o = 0;
+    bool ok = false;
+    if (int rc = header_from_prefix(g, total, &o, &ok)) return rc;
+    MC_REQUIRE(ok, MC_E_IO, "%s: no valid BAM header", g->path.c_str());
+    const double t1 = now_s();
+    int64_t consumed = 0;
+    if (int rc = parse_window(g, o, (int64_t)total, false, &consumed)) return rc;
+    g->t_parse += (now_s() - t1) * 1e3;
+    MC_REQUIRE(consumed == (int64_t)total, MC_E_IO, "%s: truncated record at byte %lld of the inflated stream",
+               g->path.c_str(), (long long)consumed);
+    return MC_OK;
+}
+
 int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     const double t_start = now_s();
     MappedFile mf;
@@ -627,6 +764,19 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
     const int64_t max_lanes = (int64_t)dev_cus * MC_GZ_WAVES_PER_CU * (MC_GZ_LDS ? kGzLanes : 64);
+    if (window_bytes <= 0 && !blocks.empty()) {
+        // resident when the compressed file, its inflated stream and the
+        // scratch take at most half of the free device memory
+        size_t free_b = 0, tot_b = 0;
+        HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
+        const size_t need = mf.size + total + blocks.size() * (sizeof(GzBlock) + sizeof(int)) +
+                            (size_t)kGzPieceStreams * (size_t)max_lanes * kGzSlotWords * sizeof(uint16_t);
+        if (need <= free_b / 2) {
+            const int rc = gpu_decode_resident(g, mf, blocks, total, max_lanes);
+            g->t_total = (now_s() - t_start) * 1e3;
+            return rc;
+        }
+    }
     // windows of blocks (<= win inflated bytes each, at least one block)
     std::vector<std::pair<size_t, size_t>> wins;
     for (size_t b0 = 0; b0 < blocks.size();) {
