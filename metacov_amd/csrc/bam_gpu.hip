@@ -636,6 +636,10 @@ int header_from_prefix(mc_bam_gpu* g, size_t n, int64_t* o, bool* ok) {
 // blocks, profiles/r03sd_e2e_window_sweep.json), so successive pieces' kernels
 // overlap each other and the remaining uploads instead of running one window
 // after another; no carry between windows, one parse at the end.
+// A/B on the 30 M-record BAM (profiles/r03sf_gz_pipeline_ab.txt, decode total
+// per build over 3 interleaved rounds): 2 / 3 / 4 streams with 4 pieces
+// 292-309 / 301-342 / 296-326 ms; 8 pieces 415-432 ms on 2 or 4 streams (the
+// per-launch floor is paid more often than the uploads hide it)
 #ifndef MC_GZ_PIECE_STREAMS
 #define MC_GZ_PIECE_STREAMS 2
 #endif
