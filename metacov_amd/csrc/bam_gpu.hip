@@ -354,8 +354,11 @@ const char* gz_err_msg(int e) {
 
 // File bytes [off, off + len) into device memory at dst: pread on threads
 // into a pinned staging slice, copied up while the next slice is read.
+#ifndef MC_UPLOAD_SLICE_MIB
+#define MC_UPLOAD_SLICE_MIB 64
+#endif
 int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst, hipStream_t st) {
-    constexpr size_t kSlice = 64ull << 20;
+    constexpr size_t kSlice = (size_t)MC_UPLOAD_SLICE_MIB << 20;
     for (auto& s : g->stage) HIP_TRY(s.reserve(kSlice));
     hipEvent_t done[2] = {nullptr, nullptr};
     for (auto& e : done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
