@@ -354,7 +354,8 @@ const char* gz_err_msg(int e) {
 
 // File bytes [off, off + len) into device memory at dst: pread on threads
 // into a pinned staging slice, copied up while the next slice is read.
-// 32 / 64 / 128 / 256 MiB slices: decode 271-329 / 273-298 / 304-350 / 323-334 ms
+// 32 / 64 / 128 / 256 MiB slices, decode in rounds 1-2 (round 0 includes a cold
+// first run): 271-288 / 273-298 / 304-307 / 323-334 ms
 // (profiles/r03si_upload_slice_ab.txt): larger slices expose a longer first read
 #ifndef MC_UPLOAD_SLICE_MIB
 #define MC_UPLOAD_SLICE_MIB 64
