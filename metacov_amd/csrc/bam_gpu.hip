@@ -643,9 +643,10 @@ int header_from_prefix(mc_bam_gpu* g, size_t n, int64_t* o, bool* ok) {
 // overlap each other and the remaining uploads instead of running one window
 // after another; no carry between windows, one parse at the end.
 // A/B on the 30 M-record BAM (profiles/r03sf_gz_pipeline_ab.txt, decode total
-// per build over 3 interleaved rounds): 2 / 3 / 4 streams with 4 pieces
-// 292-309 / 301-342 / 296-326 ms; 8 pieces 415-432 ms on 2 or 4 streams (the
-// per-launch floor is paid more often than the uploads hide it)
+// per build in interleaved rounds 1-2; round 0 includes a cold first run):
+// 2 / 3 / 4 streams with 4 pieces 292-309 / 310-342 / 296-298 ms; 8 pieces
+// 427-433 ms on 2 or 4 streams (the per-launch floor is paid more often than
+// the uploads hide it)
 #ifndef MC_GZ_PIECE_STREAMS
 #define MC_GZ_PIECE_STREAMS 2
 #endif
