@@ -109,7 +109,8 @@ int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths);
 /* Append coordinate-sorted pileup intervals (host pointers): read i covers
  * [pos[i], pos[i] + span[i]) on contig tid[i].  These are the records the
  * pileup "all" stepper keeps (flag & 0x704 == 0), span = reference length
- * of the CIGAR (ops M/D/N/=/X), 1 for a mapped read with none.
+ * of the CIGAR (ops M/D/N/=/X), 0 for a mapped read with none (1 under
+ * MC_LEGACY_ENDPOS); a span-0 read adds no depth.
  * Replaces: per-record AlignmentFileIterator.cnext()/get_tid()/get_pos()
  * (scan.pyx:213-283) feeding ReadProcessor.process_read (scan.pxd:35). */
 int mc_add_reads(mc_ctx* ctx, int64_t n, const int32_t* tid,
@@ -147,6 +148,11 @@ int mc_add_reads_cigar(mc_ctx* ctx, int64_t n, const int32_t* tid,
 int mc_add_reads_cigar_device(mc_ctx* ctx, int64_t n, const int32_t* d_tid,
                               const int32_t* d_pos, const int64_t* d_cig_off,
                               const uint32_t* d_cigar);
+
+/* K1's span of a read whose CIGAR has no reference-consuming op: 0 (current
+ * htslib bam_plp_push, the default) or 1 (legacy = 1: htslib <= 1.9
+ * bam_endpos; see MC_LEGACY_ENDPOS).  Applies to later mc_add_reads_cigar*. */
+int mc_set_legacy_endpos(mc_ctx* ctx, int legacy);
 
 /* Drops the ctx's reads (the contigs stay): the next batch starts empty. */
 int mc_clear_reads(mc_ctx* ctx);
@@ -244,9 +250,18 @@ int mc_depth_cap_mask(int64_t n, const int32_t* tid, const int32_t* pos, const i
 /* ---- host BAM decoder (C++, multi-threaded BGZF inflate) ----------------
  * Replaces the pysam/htslib read path the reference uses: AlignmentFile
  * header (bam.references / bam.lengths, cli.py:80, util.py:64-69),
- * IteratorRowAll over records (scan.pyx:204), and bam_cigar2rlen /
- * bam_endpos for the pileup interval. */
+ * IteratorRowAll over records (scan.pyx:204), and bam_plp_push's pileup
+ * interval [pos, pos + bam_cigar2rlen) (MC_LEGACY_ENDPOS: bam_endpos). */
 typedef struct mc_bam mc_bam;
+
+/* OR'd into any decoder's flag_filter (bits 0-15 are BAM flags): the pileup
+ * interval of a mapped read with no reference-consuming CIGAR op is
+ * [pos, pos + 1), as htslib <= 1.9 bam_plp_push set it (tail->end =
+ * bam_endpos(b)).  Default (bit clear): current htslib, whose bam_plp_push
+ * sets tail->end = pos + bam_cigar2rlen(...) ("raw rlen rather than
+ * bam_endpos() which adjusts rlen=0 to rlen=1"), so such a read has span 0
+ * and adds nothing to PileupColumn.n.  Version-dependent; parity unpinned. */
+#define MC_LEGACY_ENDPOS 0x10000u
 
 int mc_bam_open(const char* path, int n_threads, uint32_t flag_filter,
                 int keep_cigar, mc_bam** out);

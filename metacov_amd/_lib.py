@@ -96,6 +96,7 @@ SIGNATURES = {
     "mc_clear_reads": [_P],
     "mc_invalidate": [_P],
     "mc_set_direct_prepare": [_P, ctypes.c_int],
+    "mc_set_legacy_endpos": [_P, ctypes.c_int],
     "mc_prepare": [_P],
     "mc_compute_depth": [_P],
     "mc_get_depth": [_P, _I32, _I64, _I64, _P],

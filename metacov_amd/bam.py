@@ -20,6 +20,14 @@ from . import _lib
 from ._lib import check
 
 FLAG_FILTER = 0x704   # pysam pileup stepper "all": UNMAP|SECONDARY|QCFAIL|DUP
+# include/metacov_amd.h MC_LEGACY_ENDPOS: a mapped read without a
+# reference-consuming CIGAR op spans [pos, pos + 1) (htslib <= 1.9
+# bam_endpos) instead of current htslib's raw rlen 0 (bam_plp_push)
+LEGACY_ENDPOS = 0x10000
+
+
+def _filter(flag_filter, legacy_endpos):
+    return int(flag_filter) | (LEGACY_ENDPOS if legacy_endpos else 0)
 
 
 def build_index(path, index=None, n_threads=0):
@@ -45,13 +53,15 @@ def index_stats(index, n_ref):
 
 class BamFile:
     def __init__(self, path, n_threads=0, flag_filter=FLAG_FILTER, keep_cigar=False,
-                 contigs=None, index=None):
+                 contigs=None, index=None, legacy_endpos=False):
         if hasattr(path, "filename"):          # pysam.AlignmentFile
             path = path.filename
         if isinstance(path, bytes):
             path = path.decode()
         self.filename = os.fspath(path)
         self.index = os.fspath(index) if index else None
+        self.legacy_endpos = bool(legacy_endpos)
+        flag_filter = _filter(flag_filter, legacy_endpos)
         lib = _lib.load()
         h = ctypes.c_void_p()
         if contigs is None:
@@ -181,10 +191,12 @@ class BamStream:
     in file order.  references / lengths come from the header; record counts
     grow as the file is consumed."""
 
-    def __init__(self, path, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0):
+    def __init__(self, path, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0,
+                 legacy_endpos=False):
         self.filename = os.fspath(getattr(path, "filename", path))
         self._lib = _lib.load()
         self._h = ctypes.c_void_p()
+        flag_filter = _filter(flag_filter, legacy_endpos)
         check(self._lib.mc_bam_stream_open(self.filename.encode(), int(n_threads), int(flag_filter),
                                            int(window_bytes), ctypes.byref(self._h)))
         hdr = ctypes.c_void_p()
@@ -255,10 +267,13 @@ class GpuBamFile:
     a device copy (mc_add_reads_device).  Offers what the CLI uses of
     BamFile: references, lengths, mapped, unmapped, engine(), local_tid()."""
 
-    def __init__(self, path, device=0, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0):
+    def __init__(self, path, device=0, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0,
+                 legacy_endpos=False):
         self.filename = os.fspath(getattr(path, "filename", path))
         self.contigs = None
         self.device = device
+        self.legacy_endpos = bool(legacy_endpos)
+        flag_filter = _filter(flag_filter, legacy_endpos)
         self._lib = _lib.load()
         self._h = ctypes.c_void_p()
         check(self._lib.mc_bam_gpu_open(self.filename.encode(), int(device), int(n_threads),
@@ -371,11 +386,12 @@ class StreamedBam:
     engine(), local_tid()."""
 
     def __init__(self, path, device=0, n_threads=0, flag_filter=FLAG_FILTER,
-                 batch_reads=1 << 22, window_bytes=0, pinned=True):
+                 batch_reads=1 << 22, window_bytes=0, pinned=True, legacy_endpos=False):
         from .engine import CoverageEngine
         self.filename = os.fspath(getattr(path, "filename", path))
         self.contigs = None
-        with BamStream(self.filename, n_threads, flag_filter, window_bytes) as st:
+        self.legacy_endpos = bool(legacy_endpos)
+        with BamStream(self.filename, n_threads, flag_filter, window_bytes, legacy_endpos) as st:
             self.references, self.lengths = st.references, st.lengths
             eng = CoverageEngine(device)
             eng.set_contigs(np.asarray(self.lengths, dtype=np.int64))

@@ -4,8 +4,13 @@ reference command (metacov/cli.py:35-108).
     python -m metacov_amd.cli pileup -b X.bam [-rb R.blast7 | -rc R.csv] [-o out.csv]
 
 Differences from the reference, all outside the CSV: the BAM need not be
-indexed (it is decoded whole by the library's C++ decoder); all regions are
-reduced in one batched GPU call.  With `-k/--kmer-histogram` every row also
+indexed (it is decoded whole, on the GPU by default); all regions are
+reduced in one batched GPU call.  Defaults follow pysam: the pileup read cap
+of 8000 (`--max-depth`, 0 = exact depths; metacov_amd.depthcap) and current
+htslib's end of a read without reference-consuming ops (`--legacy-endpos`
+for htslib <= 1.9).  Rows are written in input order up to the first region
+the reference would fail on (unknown name, bad coordinate, empty region),
+and that error is raised after them, as cli.py:85-108 does.  With `-k/--kmer-histogram` every row also
 carries pileup.experimental's 13 columns (cli.py:81, :93-95; SURVEY.md §8 f):
 the read side runs on host threads, the k-mer correlation against `-f` on
 the GPU (metacov_amd/experimental.py).
@@ -67,14 +72,18 @@ def main():
 @click.option('--stream/--no-stream', default=True,
               help="Decode in bounded-memory windows, feeding the GPU through pinned double "
                    "buffers (default; --no-stream decodes the whole file into host memory first)")
-@click.option('--max-depth', type=click.IntRange(1), default=None, metavar="N",
-              help="Reproduce htslib's pileup read cap (pysam's default is 8000) per region "
-                   "query; default: exact depths, no cap")
+@click.option('--max-depth', type=click.IntRange(0), default=_depthcap.HTSLIB_MAX_DEPTH,
+              metavar="N", show_default=True,
+              help="htslib's pileup read cap per region query, as pysam's pileup applies it "
+                   "(its default is 8000); 0: exact depths, no cap")
+@click.option('--legacy-endpos', is_flag=True, default=False,
+              help="Count a mapped read without reference-consuming CIGAR ops on one column "
+                   "(htslib <= 1.9 bam_endpos); default: it adds nothing (current htslib)")
 @click.option('--decode', type=click.Choice(['gpu', 'host']), default='gpu',
               help="gpu (default): BGZF inflate and record parse on the device (csrc/bam_gpu.hip); "
                    "host: the C++ decoder on host threads (--stream / --no-stream)")
 def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
-           kmer_histogram, kmer_length, outfile, device, stream, max_depth, decode):
+           kmer_histogram, kmer_length, outfile, device, stream, max_depth, legacy_endpos, decode):
     """
     Compute fold coverage values
     """
@@ -84,15 +93,14 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     exp = (k_cor, kmer_length, fasta) if k_cor is not None else None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp,
-                                  max_depth=max_depth)
-    # the cap needs each region's records on the host (a decoded file)
-    if max_depth is not None:
-        bam = BamFile(bamfile.name)
-    elif decode == 'gpu':
-        bam = GpuBamFile(bamfile.name, device=device)
+                                  max_depth=max_depth, legacy_endpos=legacy_endpos)
+    if decode == 'gpu':
+        bam = GpuBamFile(bamfile.name, device=device, legacy_endpos=legacy_endpos)
+    elif stream:
+        bam = StreamedBam(bamfile.name, device=device, legacy_endpos=legacy_endpos)
     else:
-        bam = StreamedBam(bamfile.name, device=device) if stream else BamFile(bamfile.name)
-    regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam))
+        bam = BamFile(bamfile.name, legacy_endpos=legacy_endpos)
+    regions = _regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam)
     log_counts(bam)
     write_rows(bam, regions, outfile, device=device, exp=exp, max_depth=max_depth)
 
@@ -107,55 +115,66 @@ def log_counts(bam):
 
 def resolve_regions(bam, regions):
     """Header contig id and sorted 0-based half-open range per region, as
-    cli.py:80-91 (KeyError for an unknown name, as cli.py:86)."""
+    cli.py:80-91, for the regions before the first one the reference fails
+    on: returns (hits, tids, starts, ends, error).  The error is what the
+    reference raises at that region, in its order: the region file's own
+    parse error, KeyError for an unknown name (cli.py:86), ValueError from
+    int() (cli.py:89), then classic()'s ValueError for a negative start or an
+    empty region (pileup.py:19, a zero-size reduction).  None when every
+    region resolves."""
     name2ref = {w.split()[0]: w for w in bam.references}
     ref2tid = {}
     for t, w in enumerate(bam.references):
         ref2tid.setdefault(w, t)      # first header entry, as list.index
-    tids, starts, ends = [], [], []
-    for hit in regions:
-        ref = name2ref[hit.sacc]
-        start, end = sorted((int(hit.sstart), int(hit.send)))
-        if start < 0:
-            raise ValueError("region start %d < 0" % start)
+    hits, tids, starts, ends = [], [], [], []
+    err = None
+    it = iter(regions)
+    while True:
+        try:
+            hit = next(it)
+        except StopIteration:
+            break
+        except Exception as e:        # a malformed line of the region file
+            err = e
+            break
+        try:
+            ref = name2ref[hit.sacc]
+            start, end = sorted((int(hit.sstart), int(hit.send)))
+            if start < 0:
+                raise ValueError("start out of range (%d)" % start)
+            if start == end:
+                raise ValueError("zero-size array to reduction operation minimum which has "
+                                 "no identity")
+        except Exception as e:
+            err = e
+            break
+        hits.append(hit)
         tids.append(ref2tid[ref])
         starts.append(start)
         ends.append(end)
-    return (np.array(tids, np.int32), np.array(starts, np.int64), np.array(ends, np.int64))
+    return (hits, np.array(tids, np.int32), np.array(starts, np.int64),
+            np.array(ends, np.int64), err)
 
 
-def compute_rows(bam, tids, starts, ends, device=0, max_depth=None):
-    """Exact stat rows of the regions (header contig ids) on `bam`'s engine:
-    depth and statistics in one pass (fused K2) when the regions do not
-    overlap; the library falls back to K2 + K3 otherwise.  max_depth: htslib's
-    read cap per region query (metacov_amd.depthcap), one engine call per
-    region."""
+def compute_rows(bam, tids, starts, ends, device=0, max_depth=_depthcap.HTSLIB_MAX_DEPTH):
+    """Stat rows of the regions (header contig ids) on `bam`'s engine: depth
+    and statistics in one pass (fused K2) when the regions do not overlap;
+    the library falls back to K2 + K3 otherwise.  max_depth: htslib's read
+    cap per region query; only regions whose exact maximum could reach it
+    are recomputed, together in one more engine call (metacov_amd.depthcap);
+    0 / None: exact depths."""
     if len(tids) == 0:
         return np.zeros(0, dtype=REGION_STAT_DTYPE)
-    if max_depth is not None:
-        rows, dropped = _depthcap.capped_rows(bam, tids, starts, ends, max_depth, device)
-        log.info("max_depth %d: %d reads dropped by the pileup cap", max_depth, dropped)
-        return rows
     eng = bam.engine(device, compute=False)
     rows = eng.compute_depth_stats(np.asarray(bam.local_tid(tids), np.int32), starts, ends)
     eng._depth_ready = True
-    warn_depth_cap(eng.max_depth())
+    if max_depth:
+        rows, n_cap, dropped = _depthcap.apply_cap(bam, rows, tids, starts, ends, bam.lengths,
+                                                   max_depth, device)
+        if n_cap:
+            log.info("max_depth %d: %d regions deep enough for the pileup cap, %d reads dropped",
+                     max_depth, n_cap, dropped)
     return rows
-
-
-HTSLIB_MAX_DEPTH = _depthcap.HTSLIB_MAX_DEPTH
-
-
-def warn_depth_cap(max_depth):
-    """The reference's pysam pileup drops reads from a column's pool past
-    max_depth=8000 (version-dependent); by default this engine
-    never caps (--max-depth 8000 reproduces the cap).  Above half the cap the
-    two may disagree (a read is dropped once its start's buffered reads,
-    depth plus the reads ending there, exceed it), so say so."""
-    if 2 * max_depth > HTSLIB_MAX_DEPTH:
-        log.warning("maximum depth %d: pysam's pileup cap of %d may drop reads here (use "
-                    "--max-depth %d to reproduce it); these values are exact", max_depth,
-                    HTSLIB_MAX_DEPTH, HTSLIB_MAX_DEPTH)
 
 
 def experimental_results(path, exp, references, tids, starts, ends, device=0):
@@ -183,16 +202,20 @@ def write_csv(regions, rows, outfile, extra=None):
         writer.writerow(result)
 
 
-def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=None):
-    """Resolves names like cli.py:80-91, reduces all regions in one GPU call,
-    then writes rows in input order exactly as cli.py:97-108 does."""
-    tids, starts, ends = resolve_regions(bam, regions)
+def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=_depthcap.HTSLIB_MAX_DEPTH):
+    """Resolves names like cli.py:80-91, reduces the regions in one GPU call,
+    then writes rows in input order exactly as cli.py:97-108 does; the rows
+    before a failing region are written before its error is raised."""
+    hits, tids, starts, ends, err = resolve_regions(bam, regions)
     rows = compute_rows(bam, tids, starts, ends, device, max_depth)
     extra = experimental_results(bam.filename, exp, bam.references, tids, starts, ends, device)
-    write_csv(regions, rows, outfile, extra)
+    write_csv(hits, rows, outfile, extra)
+    if err is not None:
+        raise err
 
 
-def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None, max_depth=None):
+def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None,
+                       max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False):
     """One rank of a multi-GPU `pileup` (launched by torch.distributed.run).
     With -k, each rank also computes the experimental columns of the regions
     on its contigs (cli.py:93-95 per region), and rank 0 gathers them with
@@ -210,11 +233,11 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
     dist.init_process_group(backend)
     coll_dev = torch.device("cuda", device) if backend == "nccl" else None
     try:
-        err = None
+        err = region_err = None
         try:
             table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
-                                       max_depth)
-            head, regions, tids, starts, ends, rows, mine, r_max = table_args
+                                       max_depth, legacy_endpos)
+            head, regions, tids, starts, ends, rows, mine, r_max, region_err = table_args
             mine_extra = experimental_results(path, exp, head.references, tids[mine], starts[mine],
                                               ends[mine], device)
         except BaseException as e:   # every rank learns of it before the table gather
@@ -236,11 +259,15 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
                       extra)
     finally:
         dist.destroy_process_group()
+    if region_err is not None:       # every rank resolved the same regions
+        raise region_err
 
 
-def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device, max_depth=None):
+def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
+                  max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False):
     """This rank's part of a distributed pileup: header and regions (every
-    rank), LPT contig shards, and the rows of the regions on its contigs."""
+    rank; those before the first failing one, and its error), LPT contig
+    shards, and the rows of the regions on its contigs."""
     from . import dist as mdist
     index = path + ".bai"
     have_index = os.path.exists(index)
@@ -248,10 +275,10 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device, 
         head = BamFile(path, contigs=[])
         reads_per, _, _ = index_stats(index, len(head.lengths))
     else:
-        head = BamFile(path)
+        head = BamFile(path, legacy_endpos=legacy_endpos)
         reads_per = np.bincount(head.tid, minlength=len(head.lengths))
-    regions = list(_regions.make_region_iterator(regionfile_blast7, regionfile_csv, head))
-    tids, starts, ends = resolve_regions(head, regions)
+    regions, tids, starts, ends, region_err = resolve_regions(
+        head, _regions.make_region_iterator(regionfile_blast7, regionfile_csv, head))
     shards = mdist.lpt_shard(mdist.contig_costs(head.lengths, reads_per), world)
     owner = np.zeros(len(head.lengths), np.int64)
     for r, sh in enumerate(shards):
@@ -261,9 +288,10 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device, 
     r_max = max(1, int(np.bincount(region_rank, minlength=world).max()) if len(tids) else 1)
     rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
     if len(mine):
-        bam = BamFile(path, contigs=shards[rank]) if have_index else head.restrict(shards[rank])
+        bam = (BamFile(path, contigs=shards[rank], legacy_endpos=legacy_endpos) if have_index
+               else head.restrict(shards[rank]))
         rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
-    return head, regions, tids, starts, ends, rows, mine, r_max
+    return head, regions, tids, starts, ends, rows, mine, r_max, region_err
 
 
 @main.command()

@@ -8,8 +8,10 @@
 // interval htslib's pileup engine gives the read:
 //   kept   iff tid >= 0 and (flag & flag_filter) == 0     (pysam stepper "all":
 //          UNMAP|SECONDARY|QCFAIL|DUP = 0x704; supplementary reads kept)
-//   span = bam_cigar2rlen (ops M/D/N/=/X, op-type mask 0x18D), or 1 when the
-//          read has no reference-consuming op (bam_endpos: pos + 1)
+//   span = bam_cigar2rlen (ops M/D/N/=/X, op-type mask 0x18D): what current
+//          htslib's bam_plp_push takes as the read's end (tail->end = pos +
+//          raw rlen), so a read without a reference-consuming op has span 0;
+//          with MC_LEGACY_ENDPOS in flag_filter, 1 (htslib <= 1.9: bam_endpos)
 // Records with more than 65535 CIGAR ops carry the real CIGAR in a CG:B,I
 // tag behind a `<l_seq>S<rlen>N` placeholder (SAMv1 §4.2.2), as htslib's
 // bam_read1 resolves it.
@@ -187,7 +189,7 @@ int parse_records(const uint8_t* d, size_t o, size_t n, bool partial, int32_t n_
                         break;
                     }
                     int64_t rlen = cigar_rlen(cig, n_cigar);
-                    if (rlen <= 0) rlen = 1;
+                    if (rlen <= 0 && (flag_filter & MC_LEGACY_ENDPOS)) rlen = 1;
                     if (rlen > INT32_MAX) {
                         c.err = 3;
                         c.err_at = q;

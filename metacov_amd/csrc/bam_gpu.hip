@@ -447,10 +447,17 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
         HIP_TRY(hipMemcpyAsync(R + first, g->res.p + first, (nseg - first) * sizeof(SegRes),
                                hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        // Every inconsistent landing is applied in one round.  Only the chain
+        // up to the first one is verified (`exact`): later walks may have
+        // started at a false sync, so their errors are not reported, and
+        // their landings are hints the next round re-checks.  The verified
+        // prefix grows every round, so the rounds end.
         int64_t redo = -1;
+        bool exact = true;
         for (int64_t i = first; i < nseg; ++i) {
             const SegRes& r = R[i];
             const int64_t end = seg[i + 1];
+            if (r.err && !exact) break;
             if (r.err == kSegIncomplete) {
                 if (partial) {
                     // the window's records end here: later segments are empty
@@ -470,10 +477,14 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
                 return MC_E_IO;
             }
             if (r.landing != end) {   // segment i+1's sync was a false positive
-                for (int64_t j = i + 1; j < nseg && seg[j] < r.landing; ++j) seg[j] = r.landing;
+                if (r.landing > end) {
+                    for (int64_t j = i + 1; j < nseg && seg[j] < r.landing; ++j) seg[j] = r.landing;
+                } else {
+                    seg[i + 1] = r.landing;   // (only after an unverified walk: the next round checks)
+                }
                 ++g->resyncs;
-                redo = i + 1;
-                break;
+                if (redo < 0) redo = i + 1;
+                exact = false;
             }
         }
         if (redo < 0) break;
@@ -826,13 +837,15 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         if (u->rc) u->msg = mc::last_error();
         u->s = now_s() - t0;
     };
+    // up_next before the joiner: locals die in reverse order, so an early
+    // return joins the uploader thread before the Upload it writes is gone
+    Upload up_next;
     struct Joiner {
         std::thread t;
         ~Joiner() {
             if (t.joinable()) t.join();
         }
     } uploader;
-    Upload up_next;
     size_t carry = 0;
     bool have_header = false;
     int64_t o = 0;

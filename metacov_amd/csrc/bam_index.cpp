@@ -424,7 +424,7 @@ extern "C" int mc_bam_open_contigs(const char* path, const char* bai_path, int n
                 uint32_t n_cigar;
                 if (!cigar_of(r, rend, &cig, &n_cigar)) { p.err = 2; p.at = q; break; }
                 int64_t rlen = cigar_rlen(cig, n_cigar);
-                if (rlen <= 0) rlen = 1;
+                if (rlen <= 0 && (flag_filter & MC_LEGACY_ENDPOS)) rlen = 1;   // else raw (bam_plp_push)
                 if (rlen > INT32_MAX) { p.err = 3; p.at = q; break; }
                 p.tid.push_back(tid);
                 p.pos.push_back(rdi32(r + 4));

@@ -9,13 +9,17 @@
 // read is pushed, the pileup has produced every column before the previous
 // read's start, so iter->pos equals that start: only a read starting at the
 // SAME position as its predecessor can be dropped, and the buffered reads are
-// then the kept reads whose end (bam_endpos, exclusive) is >= that position
-// (bam_plp_next frees a read at the first column at or past its end; reads of
-// earlier contigs are all freed when the contig changes, and a contig's first
-// read is never dropped).  So for a group of m reads starting at s:
+// then the kept reads whose end (tail->end = pos + span, exclusive) is >= that
+// position (bam_plp_next frees a read at the first column at or past its end;
+// reads of earlier contigs are all freed when the contig changes, and a
+// contig's first read is never dropped).  A kept read joins the buffer only if
+// `tail->end > iter->pos`: a group's first read always does (iter->pos is
+// still the previous start), a later one only with span > 0 (current htslib
+// gives a read without reference-consuming ops span 0; under the legacy
+// bam_endpos rule every span is >= 1).  So for a group of reads starting at s:
 //   C = kept reads before the group with end >= s;
 //   the group's first read is kept; each further read is kept while
-//   1 + C + (group reads kept so far) <= maxcnt.
+//   1 + C + (group reads buffered so far) <= maxcnt.
 // One sweep per contig with a min-heap of the kept reads' ends.  The cap is
 // version-dependent (parity unpinned: htslib is absent here); the oracle's
 // literal restatement of the push / next loop (oracle/htslib_plp.py) pins
@@ -60,8 +64,10 @@ extern "C" int mc_depth_cap_mask(int64_t n, const int32_t* tid, const int32_t* p
                     const bool k = j == i || 1 + c + kept <= max_depth;
                     keep[j] = k ? 1 : 0;
                     if (k) {
-                        ++kept;
-                        ends.push((int64_t)pos[j] + span[j]);
+                        if (j == i || span[j] > 0) {
+                            ++kept;
+                            ends.push((int64_t)pos[j] + span[j]);
+                        }
                     } else {
                         ++lost;
                     }

@@ -179,6 +179,7 @@ struct mc_ctx {
     bool direct_checked = false;
     bool direct_ok = true;
     bool direct_enabled = true;
+    int min_span = 0;              // K1: span of a read with no reference-consuming op (mc_set_legacy_endpos)
     bool direct_retry_full = false;       // the batch K2 just refused goes to mc_prepare
     unsigned long long direct_gen = 0;
     // halo of the next direct batch (0: short_max): the previous batch's
@@ -704,7 +705,7 @@ static int run_k1(mc_ctx* ctx) {
     const size_t lds = (kBlock + 1) * 8 + 8 + kBlock * 4 + kOwnerBuckets;
     const int64_t* co = ctx->cig_off_ext ? ctx->cig_off_ext : ctx->d_cig_off.p;
     const uint32_t* cw = ctx->cigar_ext ? ctx->cigar_ext : ctx->d_cigar.p;
-    hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s, co, cw, n, ctx->d_span.p);
+    hipLaunchKernelGGL(cigar_span_kernel, dim3((unsigned)nb), dim3(kBlock), lds, s, co, cw, n, ctx->min_span, ctx->d_span.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->ev[1], s));
     ctx->t_cigar = true;
@@ -1013,6 +1014,12 @@ static int prepare_for_compute(mc_ctx* ctx) {
     if (ctx->prepared) return MC_OK;
     if (direct_eligible(ctx) && !ctx->direct_retry_full) return prepare_direct(ctx);
     return mc_prepare(ctx);
+}
+
+extern "C" int mc_set_legacy_endpos(mc_ctx* ctx, int legacy) {
+    if (int rc = ctx_use(ctx)) return rc;
+    ctx->min_span = legacy ? 1 : 0;
+    return MC_OK;
 }
 
 extern "C" int mc_set_direct_prepare(mc_ctx* ctx, int enable) {

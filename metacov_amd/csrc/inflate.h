@@ -576,7 +576,7 @@ MC_HD int rec_parse(const uint8_t* r, const uint8_t* rend, int32_t n_ref, uint32
         const uint32_t cw = ld_u32(cig + 4ull * k);
         if ((0x18Du >> (cw & 0xFu)) & 1u) rlen += cw >> 4;
     }
-    if (rlen <= 0) rlen = 1;
+    if (rlen <= 0 && (flag_filter & MC_LEGACY_ENDPOS)) rlen = 1;   // else raw rlen (bam_plp_push)
     if (rlen > 0x7fffffffll) return 4;
     out.tid = tid;
     out.pos = ld_i32(r + 4);

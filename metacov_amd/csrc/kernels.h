@@ -1156,8 +1156,9 @@ long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __re
 // One workgroup per 256 reads: the block streams the contiguous CIGAR words
 // of its reads as int4 (kU loads in flight per thread) and sums the
 // reference-consuming lengths per read (op-type mask 0x18D = M, D, N, =, X;
-// htslib bam_cigar2rlen).  A mapped read without such an op gets span 1
-// (htslib bam_endpos).  Each lane splits its 4 words into runs by read (one
+// htslib bam_cigar2rlen).  A mapped read without such an op gets span
+// min_span: 0 as current htslib's bam_plp_push (raw rlen), 1 for the legacy
+// bam_endpos rule (mc_set_legacy_endpos).  Each lane splits its 4 words into runs by read (one
 // LDS binary search per int4, then forward steps); a wave whose runs touch few
 // reads (long CIGARs) reduces them with shuffles before one LDS atomic per
 // read, otherwise (short CIGARs, low contention) each run adds directly.
@@ -1173,7 +1174,7 @@ __device__ __forceinline__ int cigar_ref_len(uint32_t c) {
 
 __global__ void __launch_bounds__(kBlock)
 cigar_span_kernel(const int64_t* __restrict__ cig_off, const uint32_t* __restrict__ cigar,
-                  int64_t n, int32_t* __restrict__ span) {
+                  int64_t n, int min_span, int32_t* __restrict__ span) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     long long* off = reinterpret_cast<long long*>(smem_raw);                 // kBlock + 1
     int* acc = reinterpret_cast<int*>(smem_raw + (kBlock + 1) * 8 + 8);      // kBlock
@@ -1252,7 +1253,7 @@ cigar_span_kernel(const int64_t* __restrict__ cig_off, const uint32_t* __restric
     __syncthreads();
     if (threadIdx.x < nr) {
         const int s = acc[threadIdx.x];
-        span[r0 + threadIdx.x] = s > 0 ? s : 1;
+        span[r0 + threadIdx.x] = s > min_span ? s : min_span;
     }
 }
 

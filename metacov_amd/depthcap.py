@@ -1,16 +1,24 @@
-"""htslib's pileup read cap, opt-in (`max_depth`).
+"""htslib's pileup read cap (pysam's `max_depth`, 8000 by default) — on by
+default, as in the reference.
 
 The reference's depth is pysam's `AlignmentFile.pileup(ref, start, end)`
 (metacov/pileup.py:13), i.e. htslib's pileup with pysam's default
 max_depth=8000: `bam_plp_push` drops a read that starts where its
 predecessor started once the pileup's read pool holds more than max_depth
-nodes (include/metacov_amd.h, mc_depth_cap_mask).  The engine never caps by
-default (exact depth); `classic(..., max_depth=8000)` / `metacov pileup
---max-depth 8000` reproduce the cap, per region query as pysam sees it: the
-records overlapping [start, end) of the region's contig.  Parity unpinned
-(version-dependent htslib behaviour, htslib absent here).
+nodes (include/metacov_amd.h, mc_depth_cap_mask).  Each region is its own
+query: the records overlapping [start, end) of the region's contig.
+
+The cap can only change a region whose exact maximum depth M is large: at a
+push the pool holds the tail node, the kept reads still covering the
+previous column (<= M) and the reads of the current start group buffered so
+far (<= M + 1, the group's first read may be a span-0 one), so no read is
+dropped while 2 + 2M <= max_depth (M <= 3999 for 8000).  `apply_cap` checks
+that on the exact rows and recomputes only the regions that fail it, all in
+one engine call (`capped_rows`).  Parity with htslib itself is unpinned
+(version-dependent, htslib absent here).
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -22,7 +30,7 @@ HTSLIB_MAX_DEPTH = 8000   # pysam pileup's default max_depth
 
 def cap_mask(tid, pos, span, max_depth=HTSLIB_MAX_DEPTH, n_threads=0):
     """bool keep mask of coordinate-sorted reads under the cap, and the number
-    of reads dropped."""
+    of reads dropped.  Each distinct tid is one pileup query."""
     tid = np.ascontiguousarray(tid, np.int32)
     pos = np.ascontiguousarray(pos, np.int32)
     span = np.ascontiguousarray(span, np.int32)
@@ -36,33 +44,80 @@ def cap_mask(tid, pos, span, max_depth=HTSLIB_MAX_DEPTH, n_threads=0):
 
 def region_reads(tid, pos, span, t, start, end):
     """Indices of the records of contig t overlapping [start, end) — what
-    htslib's region iterator hands the pileup (bam_endpos: at least pos + 1)."""
+    htslib's region iterator hands the pileup (hts_itr_next tests overlap
+    with bam_endpos, at least pos + 1, in every htslib version)."""
     lo, hi = np.searchsorted(tid, t, "left"), np.searchsorted(tid, t, "right")
     p = pos[lo:hi].astype(np.int64)
     e = p + np.maximum(span[lo:hi], 1)
     return lo + np.nonzero((p < end) & (e > start))[0]
 
 
-def capped_rows(bf, tids, starts, ends, max_depth=HTSLIB_MAX_DEPTH, device=0):
+def may_cap(rows, max_depth):
+    """Regions whose exact rows the cap could change (2 + 2 * max > cap)."""
+    return 2 + 2 * rows["max"].astype(np.int64) > int(max_depth)
+
+
+def host_intervals(src, contigs):
+    """(tid, pos, span) host arrays (header contig ids) holding at least the
+    records of `contigs`, from any of the library's BAM sources: a decoded
+    BamFile keeps them; a GpuBamFile copies them back from HBM; a StreamedBam
+    (intervals never kept on the host) decodes those contigs again, through
+    the BAI when there is one."""
+    if hasattr(src, "tid") and getattr(src, "tid", None) is not None:
+        return src.tid, src.pos, src.span
+    if hasattr(src, "intervals"):
+        return src.intervals()
+    from .bam import BamFile
+    path = src.filename
+    legacy = getattr(src, "legacy_endpos", False)
+    if os.path.exists(path + ".bai"):
+        bf = BamFile(path, contigs=np.unique(contigs), legacy_endpos=legacy)
+    else:
+        bf = BamFile(path, legacy_endpos=legacy)
+    return bf.tid, bf.pos, bf.span
+
+
+def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0):
     """Exact stat rows of regions (header contig ids) as pysam's capped
-    pileup would fill classic()'s column vector: per region, the overlapping
-    records, the cap, then the depth and statistics of the kept reads on the
-    GPU (one small engine call per region)."""
+    pileup would fill classic()'s column vector: per region the overlapping
+    records and the cap; then ONE engine call over all of them, each region
+    its own contig of the batch (the same contig's reads repeated when
+    regions share it).  Returns (rows, reads dropped)."""
     from .engine import CoverageEngine, REGION_STAT_DTYPE
-    rows = np.zeros(len(tids), dtype=REGION_STAT_DTYPE)
-    dropped = 0
+    tids = np.asarray(tids, np.int64)
+    starts = np.asarray(starts, np.int64)
+    ends = np.asarray(ends, np.int64)
+    if len(tids) == 0:
+        return np.zeros(0, dtype=REGION_STAT_DTYPE), 0
+    tid, pos, span = host_intervals(src, tids)
+    idx = [region_reads(tid, pos, span, int(t), int(s), int(e))
+           for t, s, e in zip(tids, starts, ends)]
+    counts = np.array([len(i) for i in idx], np.int64)
+    sel = np.concatenate(idx) if len(idx) else np.zeros(0, np.int64)
+    vt = np.repeat(np.arange(len(tids), dtype=np.int32), counts)
+    vpos, vspan = pos[sel], span[sel]
+    keep, dropped = cap_mask(vt, vpos, vspan, max_depth)
     eng = CoverageEngine(device)
     try:
-        for i, (t, s, e) in enumerate(zip(tids, starts, ends)):
-            t, s, e = int(t), int(s), int(e)
-            idx = region_reads(bf.tid, bf.pos, bf.span, t, s, e)
-            keep, d = cap_mask(np.zeros(len(idx), np.int32), bf.pos[idx], bf.span[idx], max_depth)
-            dropped += d
-            idx = idx[keep]
-            eng.set_contigs(np.array([bf.lengths[t]], np.int64))
-            eng.add_reads(np.zeros(len(idx), np.int32), bf.pos[idx], bf.span[idx])
-            rows[i] = eng.compute_depth_stats(np.zeros(1, np.int32), np.array([s], np.int64),
-                                              np.array([e], np.int64))[0]
+        eng.set_contigs(np.asarray(lengths, np.int64)[tids])
+        eng.add_reads(vt[keep], vpos[keep], vspan[keep])
+        rows = eng.compute_depth_stats(np.arange(len(tids), dtype=np.int32), starts, ends)
     finally:
         eng.close()
     return rows, dropped
+
+
+def apply_cap(src, rows, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0):
+    """Rows of the same regions under the cap: the exact `rows` where the cap
+    cannot act (may_cap), the capped recompute elsewhere.  Returns (rows,
+    regions recomputed, reads dropped)."""
+    if not max_depth or len(rows) == 0:
+        return rows, 0, 0
+    need = np.nonzero(may_cap(rows, max_depth))[0]
+    if len(need) == 0:
+        return rows, 0, 0
+    sub, dropped = capped_rows(src, np.asarray(tids)[need], np.asarray(starts)[need],
+                               np.asarray(ends)[need], lengths, max_depth, device)
+    out = rows.copy()
+    out[need] = sub
+    return out, len(need), dropped

@@ -182,6 +182,11 @@ class CoverageEngine:
         see include/metacov_amd.h."""
         self._check(self._lib.mc_set_direct_prepare(self._h, 1 if enable else 0))
 
+    def set_legacy_endpos(self, legacy=True):
+        """K1's span for a CIGAR without reference-consuming ops: 1 (htslib
+        <= 1.9 bam_endpos) instead of 0 (current bam_plp_push)."""
+        self._check(self._lib.mc_set_legacy_endpos(self._h, 1 if legacy else 0))
+
     def invalidate(self):
         """Drop the prepared index: the next compute call re-prepares the
         same device reads, as for a fresh batch."""

@@ -11,9 +11,18 @@ do not cover (or past the contig end) count as 0 (pileup.py:11-16); an empty
 region raises ValueError (pileup.py:19 on a zero-size vector); an unknown
 `ref` raises KeyError.
 
+Like pysam's pileup, the depth is capped: `max_depth` (default 8000, pysam's)
+reproduces htslib's read-pool cap per region query (metacov_amd.depthcap);
+`max_depth=None` gives exact depths.  A mapped read without a
+reference-consuming CIGAR op adds nothing (current htslib `bam_plp_push`);
+`legacy_endpos=True` counts it on one column (htslib <= 1.9).
+
 `experimental` and `load_kmerhist` (pileup.py:29-173) are re-exported from
 `metacov_amd.experimental`, so `pileup.<name>` resolves as in the reference.
 """
+import collections
+import os
+
 import numpy as np
 
 from . import depthcap
@@ -21,20 +30,34 @@ from .bam import BamFile
 from .engine import classic_stats
 from .experimental import experimental, load_kmerhist  # noqa: F401  (pileup.py:29-173)
 
-_open_files = {}
+HTSLIB_MAX_DEPTH = depthcap.HTSLIB_MAX_DEPTH
+_OPEN_MAX = 2                              # decoded files kept between calls
+_open_files = collections.OrderedDict()    # (path, size, mtime_ns, legacy) -> BamFile
 
 
-def _as_bamfile(bam):
+def _as_bamfile(bam, legacy_endpos=False):
     if isinstance(bam, BamFile) or hasattr(bam, "engine"):   # BamFile, GpuBamFile, StreamedBam
         return bam
-    key = getattr(bam, "filename", bam)
-    if isinstance(key, bytes):
-        key = key.decode()
-    f = _open_files.get(key)
+    path = getattr(bam, "filename", bam)
+    if isinstance(path, bytes):
+        path = path.decode()
+    path = os.fspath(path)
+    st = os.stat(path)
+    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns, bool(legacy_endpos))
+    f = _open_files.pop(key, None)
     if f is None:
-        f = BamFile(key)
-        _open_files[key] = f
+        f = BamFile(path, legacy_endpos=legacy_endpos)
+    _open_files[key] = f                   # most recently used last
+    while len(_open_files) > _OPEN_MAX:
+        _open_files.popitem(last=False)[1].close()
     return f
+
+
+def close_all():
+    """Releases the decoded files (and their GPU engines) kept for path
+    arguments."""
+    while _open_files:
+        _open_files.popitem()[1].close()
 
 
 def _resolve(bf, ref):
@@ -44,16 +67,19 @@ def _resolve(bf, ref):
         raise KeyError(ref)
 
 
-def classic(bam, ref, start, end, device=0, max_depth=None):
-    return classic_batch(bam, [(ref, start, end)], device=device, max_depth=max_depth)[0]
+def classic(bam, ref, start, end, device=0, max_depth=HTSLIB_MAX_DEPTH, legacy_endpos=False):
+    return classic_batch(bam, [(ref, start, end)], device=device, max_depth=max_depth,
+                         legacy_endpos=legacy_endpos)[0]
 
 
-def classic_batch(bam, regions, device=0, max_depth=None):
+def classic_batch(bam, regions, device=0, max_depth=HTSLIB_MAX_DEPTH, legacy_endpos=False):
     """[(ref, start, end), ...] -> [dict, ...] in input order.  Each dict is
     classic()'s; an empty region raises ValueError like classic().
-    max_depth (opt-in, e.g. 8000 = pysam's default): reproduce htslib's
-    pileup read cap per region query (metacov_amd.depthcap); None: exact."""
-    bf = _as_bamfile(bam)
+    max_depth (default 8000 = pysam's): htslib's pileup read cap per region
+    query, applied where it can act (metacov_amd.depthcap); None: exact.
+    legacy_endpos applies when `bam` is a path (an open file keeps the rule
+    it was decoded with)."""
+    bf = _as_bamfile(bam, legacy_endpos)
     regions = list(regions)
     if not regions:
         return []
@@ -68,15 +94,16 @@ def classic_batch(bam, regions, device=0, max_depth=None):
         if s < 0:
             raise ValueError("region start %d < 0" % s)
         starts[i], ends[i] = s, e
-    if max_depth is not None:
-        rows, _ = depthcap.capped_rows(bf, tids, starts, ends, int(max_depth), device)
-    else:
-        rows = bf.engine(device).region_stats(tids, starts, ends)
+    rows = bf.engine(device).region_stats(bf.local_tid(tids), starts, ends)
+    if max_depth:
+        rows, _, _ = depthcap.apply_cap(bf, rows, tids, starts, ends, bf.lengths, int(max_depth),
+                                        device)
     return [classic_stats(r) for r in rows]
 
 
 def depth(bam, ref, start=0, end=None, device=0):
-    """The per-position depth vector (int32) of [start, end) of `ref`."""
+    """The exact (uncapped) per-position depth vector (int32) of [start, end)
+    of `ref`."""
     bf = _as_bamfile(bam)
     t = _resolve(bf, ref)
     return bf.engine(device).depth(t, start, bf.lengths[t] if end is None else end)

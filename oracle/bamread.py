@@ -15,8 +15,11 @@ pysam/htslib on the pileup path:
 Third-party algorithm restated here: htslib (bundled in pysam, version
 unpinned by the reference: `requirements.txt:2`, `setup.py:45,53`) —
 `bam_cigar2rlen` (reference-consuming ops M, D, N, =, X; op-type mask 0x18D)
-and `bam_endpos` (a mapped read without reference-consuming CIGAR ops ends at
-pos + 1).  The pileup stepper "all" (pysam's default, the one
+and the end `bam_plp_push` gives a pileup read: current htslib sets
+`tail->end = pos + bam_cigar2rlen(...)` ("raw rlen rather than bam_endpos()
+which adjusts rlen=0 to rlen=1"), so a mapped read without reference-consuming
+ops has span 0 and adds nothing; htslib <= 1.9 used `bam_endpos` (pos + 1),
+kept here as `legacy_endpos=True`.  The pileup stepper "all" (pysam's default, the one
 `metacov/pileup.py:13` uses) drops records with any of
 UNMAP|SECONDARY|QCFAIL|DUP = 0x704.
 
@@ -44,14 +47,20 @@ class Record:
         """htslib bam_cigar2rlen: sum of lengths of reference-consuming ops."""
         return sum(ln for op, ln in self.cigar if (REF_CONSUMING_MASK >> op) & 1)
 
-    def pileup_span(self):
-        """Span of the read on the reference as the pileup engine sees it.
-
-        htslib bam_endpos(): pos + rlen for a mapped read with CIGAR, else
-        pos + 1; a zero-length alignment is treated as 1 bp.
+    def pileup_span(self, legacy_endpos=False):
+        """Span of the read on the reference as the pileup engine sees it:
+        bam_plp_push's tail->end - pos = bam_cigar2rlen (0 without a
+        reference-consuming op); legacy_endpos: bam_endpos() - pos, which
+        treats a zero-length alignment as 1 bp.
         """
         rl = self.ref_len() if self.cigar else 0
-        return rl if rl > 0 else 1
+        return 1 if (rl <= 0 and legacy_endpos) else rl
+
+    def endpos(self):
+        """htslib bam_endpos(): what the region iterator (hts_itr_next) tests
+        overlap with, in every htslib version."""
+        rl = self.ref_len() if (self.cigar and not self.flag & 4) else 0
+        return self.pos + (rl if rl > 0 else 1)
 
 
 def read_bam(path):
@@ -124,13 +133,13 @@ def _find_cg(data, p, end):
     return None
 
 
-def pileup_intervals(records, flag_filter=FLAG_FILTER):
+def pileup_intervals(records, flag_filter=FLAG_FILTER, legacy_endpos=False):
     """(tid, pos, span) of every record the "all" pileup stepper keeps."""
     out = []
     for r in records:
         if r.tid < 0 or (r.flag & flag_filter):
             continue
-        out.append((r.tid, r.pos, r.pileup_span()))
+        out.append((r.tid, r.pos, r.pileup_span(legacy_endpos)))
     return out
 
 

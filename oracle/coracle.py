@@ -89,9 +89,11 @@ def pileup_classic(tid, pos, span, rtid, rstart, rend):
 
 
 def pileup_classic_parallel(tid, pos, span, rtid, rstart, rend, threads):
-    """pileup_classic with the regions split over `threads` host threads
-    (contig-parallel: the C call releases the GIL; regions are dealt to the
-    threads longest-first).  Same rows as the one-core call."""
+    """pileup_classic with the regions spread over `threads` host threads
+    (contig-parallel: the C call releases the GIL; one task per region, the
+    costliest first — positions plus aligned bases — from a shared queue, so
+    deep contigs do not pile onto one thread).  Same rows as the one-core
+    call."""
     from concurrent.futures import ThreadPoolExecutor
     tid = np.ascontiguousarray(tid, np.int32)
     pos = np.ascontiguousarray(pos, np.int32)
@@ -101,8 +103,11 @@ def pileup_classic_parallel(tid, pos, span, rtid, rstart, rend, threads):
     rend = np.ascontiguousarray(rend, np.int64)
     out = np.zeros((len(rtid), 7), dtype=np.float64)
     ms = int(span.max()) if len(span) else 0
-    order = np.argsort(-(rend - rstart), kind="stable")
-    groups = [order[k::threads] for k in range(threads)]
+    per_tid = np.bincount(tid, weights=span.astype(np.float64),
+                          minlength=int(max(rtid.max(initial=-1), tid.max(initial=-1))) + 1)
+    cost = (rend - rstart).astype(np.float64) + per_tid[rtid]
+    order = np.argsort(-cost, kind="stable")
+    groups = [order[k:k + 1] for k in range(len(order))]
     lib = load()
 
     def run(g):

@@ -11,7 +11,10 @@ dependency the reference does not vendor and does not pin (`requirements.txt:2`,
       if (b->core.tid < 0 || b->core.flag & BAM_FUNMAP) return 0   (filtered before here)
       if (iter->tid == b->core.tid && iter->pos == b->core.pos
           && iter->mp->cnt > iter->maxcnt) return 0                  <- the cap: b dropped
-      copy b to the tail node; tail->beg = pos; tail->end = bam_endpos(b)
+      copy b to the tail node; tail->beg = pos;
+      tail->end = pos + bam_cigar2rlen(b)   (current htslib: "raw rlen rather
+                  than bam_endpos()"; htslib <= 1.9: bam_endpos(b), i.e. the
+                  spans passed in are then already >= 1)
       iter->max_tid = tid; iter->max_pos = beg
       if (tail->end > iter->pos || tid > iter->tid) tail->next = mp_alloc()   (cnt + 1)
 
@@ -28,8 +31,9 @@ dependency the reference does not vendor and does not pin (`requirements.txt:2`,
 
 mp->cnt starts at 1 (head == tail == one allocated node).  The reads fed in
 are the region query's: records of `tid` overlapping [start, end) (htslib's
-iterator returns only overlapping records), after the stepper "all" filter
-(flag & 0x704 == 0), in file order.  O(columns x buffered reads): small
+iterator, hts_itr_next, returns a record when beg < end and bam_endpos > start,
+bam_endpos = pos + max(rlen, 1) in every version), after the stepper "all"
+filter (flag & 0x704 == 0), in file order.  O(columns x buffered reads): small
 inputs only.
 """
 import numpy as np
@@ -92,12 +96,12 @@ def region_depth(tid, pos, span, t, start, end, max_depth=8000):
     tid = np.asarray(tid)
     pos = np.asarray(pos, np.int64)
     span = np.asarray(span, np.int64)
-    endp = pos + np.maximum(span, 1)                  # bam_endpos
+    endp = pos + np.maximum(span, 1)                  # bam_endpos: the iterator's overlap test
     sel = np.nonzero((tid == t) & (pos < end) & (endp > start))[0]
     it = PileupIter(max_depth)
     cols = []
     for i in sel:
-        it.push(t, int(pos[i]), int(endp[i]))
+        it.push(t, int(pos[i]), int(pos[i] + span[i]))   # bam_plp_push: tail->end
         cols += it.next_columns()
     it.is_eof = True
     cols += it.next_columns()

@@ -15,7 +15,11 @@ Outputs (JSON, plus synthetic BAMs written by `metacov_amd.synth`):
                 for whole contigs (util.py:64-69), and the expected CSV text
                 of `metacov pileup` for both (cli.py:97-108)
   stats.json    classic() on edge-case and random depth vectors
-  synth_*.bam + synth.json  edge-mix synthetic BAMs and their goldens
+  synth_*.bam + synth.json  edge-mix synthetic BAMs and their goldens; the
+                synth_edge / synth_multi entries follow current htslib's
+                bam_plp_push (a mapped read without reference-consuming ops
+                has span 0), their "legacy" sub-entries the htslib <= 1.9
+                bam_endpos rule (span 1)
 """
 import csv
 import io
@@ -178,9 +182,6 @@ def golden_synth():
         path = os.path.join(HERE, tag + ".bam")
         synth.write_bam(path, names, lengths, recs)
         _n, _l, recs2 = bamread.read_bam(path)
-        iv = bamread.pileup_intervals(recs2)
-        depth, ext = depth_with_extent(lengths, iv)
-        bam = DuckBam(names, depth)
         rng = np.random.default_rng(99)
         regions = [(n, 0, L) for n, L in zip(names, lengths)]
         for _ in range(20):
@@ -188,16 +189,26 @@ def golden_synth():
             a = int(rng.integers(0, lengths[t]))
             b = int(rng.integers(a + 1, lengths[t] + 200))
             regions.append((names[t], a, b))
-        out[tag] = {
-            "names": names, "lengths": [int(x) for x in lengths], "extents": ext,
-            "n_records": len(recs2),
-            "intervals": {"tid": [t for t, _, _ in iv], "pos": [p for _, p, _ in iv],
-                          "span": [s for _, _, s in iv]},
-            "depth_sha": [_sha(d) for d in depth],
-            "depth_sum": [int(d.sum()) for d in depth],
-            "regions": [{"sacc": s, "start": a, "end": b, "stats": run_classic(bam, s, a, b)}
-                        for s, a, b in regions],
-        }
+        entry = {}
+        for legacy in (False, True):
+            iv = bamread.pileup_intervals(recs2, legacy_endpos=legacy)
+            depth, ext = depth_with_extent(lengths, iv)
+            bam = DuckBam(names, depth)
+            e = {
+                "names": names, "lengths": [int(x) for x in lengths], "extents": ext,
+                "n_records": len(recs2),
+                "intervals": {"tid": [t for t, _, _ in iv], "pos": [p for _, p, _ in iv],
+                              "span": [s for _, _, s in iv]},
+                "depth_sha": [_sha(d) for d in depth],
+                "depth_sum": [int(d.sum()) for d in depth],
+                "regions": [{"sacc": s, "start": a, "end": b, "stats": run_classic(bam, s, a, b)}
+                            for s, a, b in regions],
+            }
+            if legacy:
+                entry["legacy"] = e
+            else:
+                entry.update(e)
+        out[tag] = entry
     # long-CIGAR record through the CG:B,I tag (> 65535 ops)
     names, lengths = ["long"], [400_000]
     cig = []

@@ -27,12 +27,19 @@ def test_fixture(lib_built, fixture_golden, golden_dir, threads):
 
 
 @pytest.mark.parametrize("tag", ["synth_edge", "synth_multi", "synth_longcigar"])
-def test_synth(lib_built, synth_golden, golden_dir, tag):
-    bf = BamFile(os.path.join(golden_dir, tag + ".bam"), n_threads=2)
+@pytest.mark.parametrize("legacy", [False, True])
+def test_synth(lib_built, synth_golden, golden_dir, tag, legacy):
+    """Both end rules: current htslib's raw rlen (span 0 for a mapped read
+    without reference-consuming ops) and the htslib <= 1.9 bam_endpos one."""
+    bf = BamFile(os.path.join(golden_dir, tag + ".bam"), n_threads=2, legacy_endpos=legacy)
     g = synth_golden[tag]
+    if legacy and "legacy" in g:
+        g = g["legacy"]
     assert list(bf.references) == g["names"]
     for got, want in zip((bf.tid, bf.pos, bf.span), _iv(g)):
         assert np.array_equal(got, want)
+    if tag != "synth_longcigar":
+        assert (bf.span == 0).any() != legacy      # the edge mix holds zero-length alignments
 
 
 def test_keep_cigar_spans(lib_built, golden_dir):
@@ -42,7 +49,7 @@ def test_keep_cigar_spans(lib_built, golden_dir):
     for i in range(len(bf.tid)):
         w = bf.cigar[bf.cig_off[i]:bf.cig_off[i + 1]]
         rl = sum(int(x >> 4) for x in w if (0x18D >> int(x & 0xF)) & 1)
-        assert max(rl, 1) == bf.span[i]
+        assert rl == bf.span[i]
 
 
 def test_flag_filter_override(lib_built, golden_dir):
@@ -62,7 +69,9 @@ def test_many_blocks_and_threads(lib_built, tmp_path):
         assert np.array_equal(x, y)
     kept = [r for r in recs if r.tid >= 0 and not (r.flag & 0x704)]
     assert len(a.tid) == len(kept)
-    assert a.span.tolist() == [max(synth.ref_len(r.cigar), 1) for r in kept]
+    assert a.span.tolist() == [synth.ref_len(r.cigar) for r in kept]
+    c = BamFile(p, n_threads=4, legacy_endpos=True)
+    assert c.span.tolist() == [max(synth.ref_len(r.cigar), 1) for r in kept]
 
 
 def test_errors(lib_built, tmp_path, golden_dir):

@@ -1,4 +1,4 @@
-"""htslib's pileup read cap (opt-in max_depth): the library's closed form
+"""htslib's pileup read cap (pysam's max_depth, on by default): the library's closed form
 (mc_depth_cap_mask, host C++) against a literal restatement of htslib's
 bam_plp_push / bam_plp_next loop (oracle/htslib_plp.py), per region query
 the way pysam's AlignmentFile.pileup(ref, start, end) runs it
@@ -12,10 +12,11 @@ from oracle import htslib_plp
 
 
 def kept_depth(pos, span, keep, start, end):
-    """classic()'s column vector from the kept reads (difference array)."""
+    """classic()'s column vector from the kept reads (difference array; a
+    span-0 read adds nothing, as current htslib's bam_plp_push)."""
     d = np.zeros(end - start + 1, np.int64)
     for p, s in zip(pos[keep], span[keep]):
-        a, b = max(p, start), min(p + max(s, 1), end)
+        a, b = max(p, start), min(p + s, end)
         if b > a:
             d[a - start] += 1
             d[b - start] -= 1
@@ -33,13 +34,18 @@ def piles(rng, n_piles, pile_size, bg, L, span_rng):
     return pos[o].astype(np.int32), span[o].astype(np.int32)
 
 
-@pytest.mark.parametrize("cap,n_piles,pile,bg,seed", [
-    (5, 20, 12, 300, 1), (20, 10, 40, 500, 2), (64, 6, 150, 2000, 3), (3, 50, 6, 100, 4),
-    (1, 10, 5, 50, 5)])
-def test_cap_mask_matches_literal_htslib(cap, n_piles, pile, bg, seed):
+@pytest.mark.parametrize("cap,n_piles,pile,bg,seed,smin", [
+    (5, 20, 12, 300, 1, 1), (20, 10, 40, 500, 2, 1), (64, 6, 150, 2000, 3, 1), (3, 50, 6, 100, 4, 1),
+    (1, 10, 5, 50, 5, 1), (5, 20, 12, 300, 6, 0), (20, 10, 40, 500, 7, 0), (3, 50, 6, 100, 8, 0),
+    (2, 30, 9, 200, 9, 0)])
+def test_cap_mask_matches_literal_htslib(cap, n_piles, pile, bg, seed, smin):
+    """smin = 0: span-0 reads (no reference-consuming op) in the piles and the
+    background, which enter the pool only as a start group's first read."""
     rng = np.random.default_rng(seed)
     L = 5000
-    pos, span = piles(rng, n_piles, pile, bg, L, (1, 300))
+    pos, span = piles(rng, n_piles, pile, bg, L, (smin, 300))
+    if smin == 0:
+        span[rng.random(len(span)) < 0.15] = 0
     tid = np.zeros(len(pos), np.int32)
     for (s, e) in [(0, L), (0, 1), (100, 2600), (2500, 4999), (1234, 1300)]:
         want, dropped = htslib_plp.region_depth(tid, pos, span, 0, s, e, max_depth=cap)
@@ -85,3 +91,49 @@ def test_cap_mask_contigs_independent_and_errors():
         depthcap.cap_mask(np.zeros(2, np.int32), np.array([5, 3], np.int32), np.ones(2, np.int32), 7)
     with pytest.raises(MetacovError):
         depthcap.cap_mask(tid, pos, span, 0)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_gate_never_misses_a_drop(seed):
+    """depthcap.may_cap's bound: while 2 + 2 * (exact max depth of the region)
+    <= max_depth, htslib's literal push/next loop drops nothing, so the
+    exact row is the capped one.  Random piles sized around the bound, with
+    span-0 reads and both end rules."""
+    rng = np.random.default_rng(100 + seed)
+    L = 600
+    cap = int(rng.integers(4, 24))
+    n = int(rng.integers(50, 400))
+    pos = np.sort(np.concatenate([rng.integers(0, L - 50, size=n),
+                                  np.full(int(rng.integers(0, cap)), int(rng.integers(0, L - 60)))]))
+    span = rng.integers(0, 60, size=len(pos))
+    span[rng.random(len(span)) < 0.2] = 0
+    if seed % 2:
+        span = np.maximum(span, 1)                      # legacy bam_endpos spans
+    pos, span = pos.astype(np.int32), span.astype(np.int32)
+    tid = np.zeros(len(pos), np.int32)
+    checked = 0
+    for _ in range(30):
+        s = int(rng.integers(0, L - 1))
+        e = int(rng.integers(s + 1, L + 20))
+        exact = kept_depth(pos, span, np.ones(len(pos), bool), s, e)
+        want, dropped = htslib_plp.region_depth(tid, pos, span, 0, s, e, max_depth=cap)
+        if 2 + 2 * int(exact.max()) <= cap:
+            checked += 1
+            assert dropped == 0 and np.array_equal(want, exact), (s, e, cap)
+        rows = np.zeros(1, dtype=[("max", np.int64)])
+        rows["max"] = exact.max()
+        assert depthcap.may_cap(rows, cap)[0] == (2 + 2 * int(exact.max()) > cap)
+
+
+def test_zero_span_reads_and_the_pool():
+    """A span-0 read that opens a start group occupies a pool node until its
+    column, so a later read of the same group can be dropped because of it;
+    one inside a group never joins the pool (bam_plp_push: tail->end > pos)."""
+    pos = np.array([10, 10, 10, 10, 20, 20, 20], np.int32)
+    span = np.array([0, 5, 5, 5, 5, 0, 5], np.int32)
+    tid = np.zeros(len(pos), np.int32)
+    for cap in (1, 2, 3, 4):
+        want, dropped = htslib_plp.region_depth(tid, pos, span, 0, 0, 40, max_depth=cap)
+        keep, d2 = depthcap.cap_mask(tid, pos, span, cap)
+        assert d2 == dropped, cap
+        assert np.array_equal(kept_depth(pos, span, keep, 0, 40), want), cap

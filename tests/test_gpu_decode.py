@@ -131,7 +131,7 @@ def test_rec_parse_host(lib_built):
     cases = [
         (R("r", 0, 100, 0, [(0, 50), (2, 3), (1, 4), (0, 20)], 74), (1, (0, 100, 73))),   # M D I M
         (R("r", 1, 5, 0, [(4, 10), (7, 30), (8, 2), (3, 1000)], 40), (1, (1, 5, 1032))),  # S = X N
-        (R("r", 2, 7, 0, [(4, 20)], 20), (1, (2, 7, 1))),        # no reference op: span 1
+        (R("r", 2, 7, 0, [(4, 20)], 20), (1, (2, 7, 0))),        # no reference op: span 0 (bam_plp_push)
         (R("r", 0, 7, 0x100, [(0, 20)], 20), (0, None)),          # secondary: dropped
         (R("r", 0, 7, 0x800, [(0, 20)], 20), (1, (0, 7, 20))),   # supplementary: kept
         (R("r", -1, -1, 4, [], 20), (0, None)),
@@ -143,6 +143,10 @@ def test_rec_parse_host(lib_built):
         assert rc == rc_want, rec.cigar
         if iv:
             assert out == iv
+    # htslib <= 1.9 bam_endpos rule (MC_LEGACY_ENDPOS): such a read spans 1
+    rc, out = _parse_host(synth.encode_record(R("r", 2, 7, 0, [(4, 20)], 20))[4:],
+                          flag_filter=0x704 | 0x10000)
+    assert (rc, out) == (1, (2, 7, 1))
     # CG:B,I placeholder resolved (> 65535 ops)
     ops = [(0, 1), (2, 1)] * 40_000
     body = synth.encode_record(R("r", 0, 9, 0, ops, 40_000), long_cigar_threshold=65535)[4:]
@@ -228,15 +232,19 @@ def test_gpu_decode_header_only_and_tiny(lib_built, tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_decode_errors(lib_built, tmp_path, golden_dir):
+@pytest.mark.parametrize("window", [0, 1 << 18])
+def test_gpu_decode_errors(lib_built, tmp_path, golden_dir, window):
+    """Truncated and corrupted files raise, resident (window 0) and windowed
+    (the next window's upload is in flight on the uploader thread when the
+    current window fails)."""
     from metacov_amd.bam import GpuBamFile
     with pytest.raises(MetacovError):
-        GpuBamFile(str(tmp_path / "missing.bam"))
+        GpuBamFile(str(tmp_path / "missing.bam"), window_bytes=window)
     raw = open(os.path.join(golden_dir, "bbmap.sorted.bam"), "rb").read()
     t = tmp_path / "trunc.bam"
     t.write_bytes(raw[: len(raw) // 2])
     with pytest.raises(MetacovError):
-        GpuBamFile(str(t))
+        GpuBamFile(str(t), window_bytes=window)
     # a corrupted deflate payload in a whole block
     blocks = _bgzf_blocks(raw)
     b = bytearray(raw)
@@ -248,7 +256,7 @@ def test_gpu_decode_errors(lib_built, tmp_path, golden_dir):
     c = tmp_path / "corrupt.bam"
     c.write_bytes(bytes(b))
     with pytest.raises(MetacovError, match="inflate|record|CIGAR|BGZF"):
-        GpuBamFile(str(c))
+        GpuBamFile(str(c), window_bytes=window)
     assert len(blocks) > 3
 
 

@@ -95,9 +95,13 @@ def test_stats_cases(eng, stats_golden):
 
 
 @pytest.mark.parametrize("tag", ["synth_edge", "synth_multi"])
-def test_synth_bams(eng, synth_golden, golden_dir, tag):
-    g = synth_golden[tag]
-    bf = BamFile(os.path.join(golden_dir, tag + ".bam"))
+@pytest.mark.parametrize("legacy", [False, True])
+def test_synth_bams(eng, synth_golden, golden_dir, tag, legacy):
+    """Depth and the real classic()'s rows under both end rules (current
+    htslib: a read without reference-consuming ops adds nothing; legacy
+    bam_endpos: one column)."""
+    g = synth_golden[tag]["legacy"] if legacy else synth_golden[tag]
+    bf = BamFile(os.path.join(golden_dir, tag + ".bam"), legacy_endpos=legacy)
     run_engine(eng, bf.lengths, bf.tid, bf.pos, bf.span)
     for t in range(len(bf.lengths)):
         v = np.ascontiguousarray(eng.depth(t, 0, g["extents"][t]), dtype="<i4")
@@ -110,14 +114,16 @@ def test_synth_bams(eng, synth_golden, golden_dir, tag):
         assert classic_stats(row) == r["stats"], r
 
 
-@pytest.mark.parametrize("tag", ["synth_edge", "synth_longcigar"])
-def test_cigar_mode(eng, synth_golden, golden_dir, tag):
+@pytest.mark.parametrize("tag,legacy", [("synth_edge", False), ("synth_edge", True),
+                                        ("synth_longcigar", False)])
+def test_cigar_mode(eng, synth_golden, golden_dir, tag, legacy):
     """K1 (raw CIGAR words -> span on the GPU, CG-tag CIGARs included) against
     the oracle: the depth of the golden intervals, which the pure-Python BAM
     reader decoded with its own bam_cigar2rlen rule (oracle/bamread.py)."""
-    g = synth_golden[tag]
+    g = synth_golden[tag]["legacy"] if legacy else synth_golden[tag]
     bf = BamFile(os.path.join(golden_dir, tag + ".bam"), keep_cigar=True)
     lengths = np.asarray(bf.lengths, np.int64)
+    eng.set_legacy_endpos(legacy)
     eng.set_contigs(lengths)
     eng.add_reads_cigar(bf.tid, bf.pos, bf.cig_off, bf.cigar)
     eng.compute_depth()
@@ -1373,13 +1379,13 @@ def test_direct_ctx_sticks_to_full_after_long_reads(lib_built):
         e.close()
 
 
-# ------------------------------------------------------------- htslib cap (opt-in)
+# ------------------------------------------------------------- pysam's defaults: the cap, span-0 reads
 
 def test_max_depth_cap_gpu_rows(lib_built):
-    """classic(..., max_depth=8000) on a >8000x synthetic contig (amplicon
-    piles): the per-region capped rows equal classic() over the literal
-    htslib restatement's columns (oracle/htslib_plp.py).  Parity with htslib
-    itself unpinned."""
+    """depthcap.capped_rows (one engine call for all regions) on a >8000x
+    synthetic contig (amplicon piles, span-0 reads among them): each row equals
+    classic() over the literal htslib restatement's columns
+    (oracle/htslib_plp.py).  Parity with htslib itself unpinned."""
     import types
     from metacov_amd import depthcap
     from oracle import htslib_plp
@@ -1389,33 +1395,160 @@ def test_max_depth_cap_gpu_rows(lib_built):
     pos = np.concatenate([np.full(12_000, 700), np.full(9_500, 710), np.full(11_000, 2100),
                           rng.integers(0, 3800, size=6000)])
     span = np.concatenate([np.full(12_000, 150), rng.integers(100, 200, size=9_500),
-                           np.full(11_000, 300), rng.integers(1, 200, size=6000)])
+                           np.full(11_000, 300), rng.integers(0, 200, size=6000)])
+    span[rng.random(len(span)) < 0.02] = 0
     o = np.argsort(pos, kind="stable")
     bf = types.SimpleNamespace(tid=np.zeros(len(pos), np.int32), pos=pos[o].astype(np.int32),
                                span=span[o].astype(np.int32), lengths=(L,))
     regions = [(0, L), (650, 900), (705, 2500), (2200, 2300), (0, 1)]
     rows, dropped = depthcap.capped_rows(bf, np.zeros(len(regions), np.int32),
                                          np.array([r[0] for r in regions], np.int64),
-                                         np.array([r[1] for r in regions], np.int64), 8000)
+                                         np.array([r[1] for r in regions], np.int64), bf.lengths, 8000)
     assert dropped > 0
     for row, (s, e) in zip(rows, regions):
         want, _ = htslib_plp.region_depth(bf.tid, bf.pos, bf.span, 0, s, e, max_depth=8000)
         assert classic_stats(row) == classic_from_vector(want.astype(np.float64)), (s, e)
 
 
-def test_cli_max_depth_option(lib_built, fixture_golden, golden_dir, tmp_path):
-    """--max-depth on the reference's fixture (depth < 8000: nothing dropped,
-    the same CSV bytes as the exact path)."""
+def _deep_bam(path):
+    """Two contigs: "amp" (1200 bp) with amplicon piles of 12,000 and 9,000
+    reads and span-0 records (30S: mapped, no reference-consuming op) opening
+    and inside the start groups; "bg" (5000 bp) shallow.  Plus filtered
+    records (secondary, duplicate, unmapped)."""
+    R = synth.SynthRecord
+    rng = np.random.default_rng(2024)
+    recs = []
+    k = [0]
+
+    def add(tid, pos, flag, cigar):
+        k[0] += 1
+        recs.append(R("r%d" % k[0], tid, pos, flag, cigar, 150))
+
+    for p in sorted(rng.integers(0, 290, size=600).tolist()):
+        add(0, p, 0, [(4, 30)] if rng.random() < 0.05 else [(0, 100)])
+    add(0, 300, 0, [(4, 30)])                                   # opens the group at 300
+    for i in range(12_000):
+        add(0, 300, 0x400 if i % 997 == 0 else 0, [(4, 30)] if i % 401 == 7 else [(0, 150)])
+    for i in range(9_000):
+        add(0, 310, 0x100 if i % 1009 == 0 else 0, [(0, 60), (2, 5), (0, 40)])
+    for p in sorted(rng.integers(311, 1150, size=900).tolist()):
+        add(0, p, 0, [(4, 30)] if rng.random() < 0.05 else [(0, 100)])
+    for p in sorted(rng.integers(0, 4900, size=3000).tolist()):
+        add(1, p, 0x4 if rng.random() < 0.01 else 0,
+            [(4, 30)] if rng.random() < 0.02 else [(0, 100)])
+    synth.write_bam(path, ["amp", "bg"], [1200, 5000], recs)
+
+
+def _oracle_csv(path, regions, max_depth, legacy=False):
+    """The CSV cli.py:85-108 writes, from the oracle: the pure-Python BAM
+    reader's intervals, htslib's literal push/next loop per region query
+    (max_depth None: a plain interval count), classic()'s numpy restatement."""
+    import csv
+    import io
+    from oracle import bamread, htslib_plp
+    from oracle.classic_np import classic_from_vector
+    names, lengths, recs = bamread.read_bam(path)
+    iv = bamread.pileup_intervals(recs, legacy_endpos=legacy)
+    tid = np.array([x[0] for x in iv], np.int32)
+    pos = np.array([x[1] for x in iv], np.int32)
+    span = np.array([x[2] for x in iv], np.int32)
+    out = io.StringIO()
+    writer = None
+    for sacc, a, b in regions:
+        s, e = sorted((int(a), int(b)))
+        t = names.index(sacc)
+        want, _ = htslib_plp.region_depth(tid, pos, span, t, s, e,
+                                          max_depth=max_depth or 10 ** 9)
+        res = classic_from_vector(want.astype(np.float64))
+        if writer is None:
+            writer = csv.DictWriter(out, fieldnames=["sacc", "start", "end"] + sorted(res))
+            writer.writeheader()
+        res.update({"sacc": sacc, "start": a, "end": b})
+        writer.writerow(res)
+    return out.getvalue()
+
+
+@pytest.mark.parametrize("decode", ["gpu", "host", "stream"])
+def test_cli_defaults_follow_pysam(lib_built, tmp_path, decode):
+    """`metacov pileup` with no options on a contig piled at 12,000x with
+    span-0 records: the CSV equals the oracle's (htslib's max_depth=8000 cap
+    per region query, current htslib's raw-rlen read end, classic()), for
+    whole contigs and for CSV regions; --max-depth 0 gives the exact counts;
+    --legacy-endpos the htslib <= 1.9 end."""
     from click.testing import CliRunner
     from metacov_amd.cli import pileup as cli_pileup
-    out = tmp_path / "o.csv"
-    r = CliRunner().invoke(cli_pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
-                                        "-rb", os.path.join(golden_dir, "regions.blast7"),
-                                        "-o", str(out), "--max-depth", "8000"])
-    assert r.exit_code == 0, r.output
-    with open(out, newline="") as fh:
-        assert fh.read() == fixture_golden["csv_blast7"]
+    bam = str(tmp_path / "deep.bam")
+    _deep_bam(bam)
+    mode = {"gpu": ["--decode", "gpu"], "host": ["--decode", "host", "--no-stream"],
+            "stream": ["--decode", "host", "--stream"]}[decode]
+    rc = tmp_path / "r.csv"
+    regs = [("amp", "305", "320"), ("bg", "0", "5000"), ("amp", "0", "1200"), ("amp", "301", "299"),
+            ("bg", "100", "101"), ("amp", "455", "470")]
+    rc.write_text("sacc,sstart,send\n" + "".join("%s,%s,%s\n" % r for r in regs))
+    cases = [([], [("amp", 0, 1200), ("bg", 0, 5000)], 8000, False),
+             (["-rc", str(rc)], regs, 8000, False),
+             (["-rc", str(rc), "--max-depth", "0"], regs, None, False),
+             (["-rc", str(rc), "--legacy-endpos"], regs, 8000, True)]
+    for extra, regions, cap, legacy in cases:
+        out = tmp_path / "o.csv"
+        res = CliRunner().invoke(cli_pileup, ["-b", bam, "-o", str(out)] + mode + extra)
+        assert res.exit_code == 0, res.output
+        want = _oracle_csv(bam, regions, cap, legacy)
+        assert open(out, newline="").read() == want, extra
+    # the cap did act, and the exact path differs from it
+    capped = _oracle_csv(bam, [("amp", 0, 1200)], 8000)
+    assert capped != _oracle_csv(bam, [("amp", 0, 1200)], None)
 
+
+def test_classic_defaults_and_cache(lib_built, tmp_path):
+    """pileup.classic: max_depth=8000 by default on every source (path,
+    BamFile, GpuBamFile, StreamedBam), None for exact; a rewritten file at
+    the same path is decoded again (the cache keys on size and mtime)."""
+    from metacov_amd import pileup
+    from metacov_amd.bam import GpuBamFile, StreamedBam
+    from oracle import bamread, htslib_plp
+    from oracle.classic_np import classic_from_vector
+    bam = str(tmp_path / "deep.bam")
+    _deep_bam(bam)
+    names, lengths, recs = bamread.read_bam(bam)
+    iv = bamread.pileup_intervals(recs)
+    tid, pos, span = (np.array([x[i] for x in iv], np.int32) for i in range(3))
+    want = {}
+    for cap in (8000, None):
+        v, _ = htslib_plp.region_depth(tid, pos, span, 0, 250, 600, max_depth=cap or 10 ** 9)
+        want[cap] = classic_from_vector(v.astype(np.float64))
+    assert want[8000] != want[None]
+    for src in (bam, BamFile(bam), GpuBamFile(bam), StreamedBam(bam)):
+        assert pileup.classic(src, "amp", 250, 600) == want[8000]
+        assert pileup.classic(src, "amp", 250, 600, max_depth=None) == want[None]
+    # rewrite the path with other contents: no stale depths
+    shutil_bam = str(tmp_path / "other.bam")
+    synth.write_bam(shutil_bam, ["amp", "bg"], [1200, 5000],
+                    [synth.SynthRecord("x", 0, 10, 0, [(0, 50)], 50)])
+    os.replace(shutil_bam, bam)
+    assert pileup.classic(bam, "amp", 0, 100)["sum"] == 50
+    pileup.close_all()
+
+
+def test_cli_writes_rows_before_a_bad_region(lib_built, golden_dir, tmp_path):
+    """As cli.py:85-108: rows are written one region at a time, so an unknown
+    name (KeyError, cli.py:86), a non-integer coordinate (cli.py:89) or an
+    empty region (classic's ValueError) leaves the rows before it in the CSV
+    and raises."""
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    bam = os.path.join(golden_dir, "bbmap.sorted.bam")
+    good = "ref1,1,425\nref2,1,575\n"
+    for bad, exc in [("nope,1,5\n", KeyError), ("ref1,x,5\n", ValueError),
+                     ("ref2,7,7\n", ValueError)]:
+        rc = tmp_path / "r.csv"
+        rc.write_text("sacc,sstart,send\n" + good + bad + "ref1,3,9\n")
+        out = tmp_path / "o.csv"
+        res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rc", str(rc), "-o", str(out)])
+        assert isinstance(res.exception, exc), (bad, res.exception)
+        lines = open(out, newline="").read().split("\r\n")
+        assert len(lines) == 4 and lines[3] == "", lines            # header + 2 rows
+        assert lines[1].startswith("ref1,1,425,") and lines[2].startswith("ref2,1,575,")
 
 
 def test_fused_device_recompute(lib_built):

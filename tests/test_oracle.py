@@ -92,12 +92,15 @@ def test_stats_cases(stats_golden):
         assert classic_np.classic_from_vector(cols) == case["stats"], case["tag"]
 
 
-def test_synth_goldens(synth_golden, golden_dir):
+@pytest.mark.parametrize("legacy", [False, True])
+def test_synth_goldens(synth_golden, golden_dir, legacy):
     for tag in ("synth_edge", "synth_multi"):
-        g = synth_golden[tag]
+        g = synth_golden[tag]["legacy"] if legacy else synth_golden[tag]
         names, lengths, recs = bamread.read_bam(os.path.join(golden_dir, tag + ".bam"))
         assert len(recs) == g["n_records"]
         tid, pos, span = _iv(g)
+        iv = bamread.pileup_intervals(recs, legacy_endpos=legacy)
+        assert [x[2] for x in iv] == span.tolist()
         d, ext, coff = coracle.depth(lengths, tid, pos, span, method="columnwalk")
         assert ext.tolist() == g["extents"]
         for t in range(len(lengths)):

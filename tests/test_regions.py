@@ -59,3 +59,19 @@ def test_cli_kmer_histogram_without_columns(tmp_path, golden_dir):
     res = CliRunner().invoke(pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
                                       "-k", str(k), "-o", str(tmp_path / "o.csv")])
     assert res.exit_code == 1 and isinstance(res.exception, AttributeError)
+
+
+def test_cli_bad_first_region_writes_nothing(tmp_path, golden_dir, lib_built):
+    """No GPU needed: the first region already fails, so the reference
+    (cli.py:85-91) raises before any row or header is written."""
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup
+    rc = tmp_path / "r.csv"
+    rc.write_text("sacc,sstart,send\nnope,1,5\nref1,1,425\n")
+    out = tmp_path / "o.csv"
+    res = CliRunner().invoke(pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
+                                      "--decode", "host", "--no-stream", "-rc", str(rc),
+                                      "-o", str(out)])
+    assert isinstance(res.exception, KeyError)
+    # click.File('w') opens lazily, in the reference too: no row, no file
+    assert not out.exists() or out.read_text() == ""
