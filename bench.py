@@ -60,6 +60,9 @@ def parse(argv=None):
                     help="steps of the second timed loop, which reuses one explicit prepare's index "
                          "(default: --steps; 0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--dump-rows", default=None, metavar="PATH",
+                    help="rank 0 saves the (gathered) region rows of the last step, in region "
+                         "order, as a .npy (tests compare them with the oracle)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -464,6 +467,8 @@ def main():
         rows = table.cpu().numpy().view(REGION_STAT_DTYPE).reshape(-1)
         if not os.environ.get("MC_BENCH_NOCHECK"):   # set only for deliberately-wrong A/B builds
             assert int(rows["sum"].sum()) == total_bases
+    if args.dump_rows and rank == 0:
+        np.save(args.dump_rows, rows)
 
     # roofline of the dominant kernel of the headline step (K2): it reads the
     # raw (tid, pos, span) tuples on the direct path (12 B/read) or the packed

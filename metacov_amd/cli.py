@@ -79,11 +79,15 @@ def main():
 @click.option('--legacy-endpos', is_flag=True, default=False,
               help="Count a mapped read without reference-consuming CIGAR ops on one column "
                    "(htslib <= 1.9 bam_endpos); default: it adds nothing (current htslib)")
+@click.option('--window-bytes', type=click.IntRange(0), default=0, metavar="B",
+              help="Decode in windows of B inflated bytes (bounded memory); 0: --decode gpu keeps "
+                   "the file resident when it fits in HBM, --stream uses 256 MiB")
 @click.option('--decode', type=click.Choice(['gpu', 'host']), default='gpu',
               help="gpu (default): BGZF inflate and record parse on the device (csrc/bam_gpu.hip); "
                    "host: the C++ decoder on host threads (--stream / --no-stream)")
 def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
-           kmer_histogram, kmer_length, outfile, device, stream, max_depth, legacy_endpos, decode):
+           kmer_histogram, kmer_length, outfile, device, stream, max_depth, legacy_endpos,
+           window_bytes, decode):
     """
     Compute fold coverage values
     """
@@ -95,9 +99,11 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp,
                                   max_depth=max_depth, legacy_endpos=legacy_endpos)
     if decode == 'gpu':
-        bam = GpuBamFile(bamfile.name, device=device, legacy_endpos=legacy_endpos)
+        bam = GpuBamFile(bamfile.name, device=device, window_bytes=window_bytes,
+                         legacy_endpos=legacy_endpos)
     elif stream:
-        bam = StreamedBam(bamfile.name, device=device, legacy_endpos=legacy_endpos)
+        bam = StreamedBam(bamfile.name, device=device, window_bytes=window_bytes,
+                          legacy_endpos=legacy_endpos)
     else:
         bam = BamFile(bamfile.name, legacy_endpos=legacy_endpos)
     regions = _regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam)

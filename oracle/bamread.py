@@ -155,3 +155,59 @@ def depth_vectors(lengths, intervals):
         depth[tid][a] += 1
         depth[tid][b] -= 1
     return [np.cumsum(d)[:-1] for d in depth]
+
+
+def scan_intervals(path, flag_filter=FLAG_FILTER, legacy_endpos=False):
+    """The same restatement over a whole (large) file without building Record
+    objects or decoding bases: returns (names, lengths, (n_records, mapped,
+    unmapped), tid, pos, span) with int32 numpy arrays of the kept records in
+    file order.  Mapped = tid >= 0 and not 0x4 (pysam's mapped count of the
+    index pseudo-bins, as the product reports it).  For the parity tests of
+    multi-window decodes (tests/test_gpu_decode.py): ~2 us per record."""
+    import numpy as np
+    with gzip.open(path, "rb") as fh:
+        data = fh.read()
+    if data[:4] != b"BAM\x01":
+        raise ValueError("not a BAM file: %s" % path)
+    off = 4
+    (l_text,) = struct.unpack_from("<i", data, off)
+    off += 4 + l_text
+    (n_ref,) = struct.unpack_from("<i", data, off)
+    off += 4
+    names, lengths = [], []
+    for _ in range(n_ref):
+        (l_name,) = struct.unpack_from("<i", data, off)
+        off += 4
+        names.append(data[off:off + l_name - 1].decode())
+        off += l_name
+        (l_ref,) = struct.unpack_from("<i", data, off)
+        off += 4
+        lengths.append(l_ref)
+    tid_l, pos_l, span_l = [], [], []
+    n_rec = mapped = 0
+    hdr = struct.Struct("<iiiBBHHHi")
+    end = len(data)
+    while off < end:
+        block_size, tid, pos, l_read_name, _mapq, _bin, n_cigar, flag, l_seq = \
+            hdr.unpack_from(data, off)
+        rec_end = off + 4 + block_size
+        n_rec += 1
+        if tid >= 0 and not flag & 4:
+            mapped += 1
+        if tid >= 0 and not flag & flag_filter:
+            p = off + 36 + l_read_name
+            cig = struct.unpack_from("<%dI" % n_cigar, data, p)
+            if (n_cigar == 2 and cig[0] == ((l_seq << 4) | 4) and cig[1] & 0xF == 3):
+                cg = _find_cg(data, p + 4 * n_cigar + (l_seq + 1) // 2 + l_seq, rec_end)
+                if cg is not None:
+                    cig = [(ln << 4) | op for op, ln in cg]
+            rl = 0
+            for c in cig:
+                if (REF_CONSUMING_MASK >> (c & 0xF)) & 1:
+                    rl += c >> 4
+            tid_l.append(tid)
+            pos_l.append(pos)
+            span_l.append(1 if (rl <= 0 and legacy_endpos) else rl)
+        off = rec_end
+    arr = lambda x: np.array(x, dtype=np.int32)
+    return names, lengths, (n_rec, mapped, n_rec - mapped), arr(tid_l), arr(pos_l), arr(span_l)

@@ -169,6 +169,18 @@ def _assert_same(h, g):
     assert np.array_equal(tid, h.tid) and np.array_equal(pos, h.pos) and np.array_equal(span, h.span)
 
 
+def _assert_oracle(path, g):
+    """The GPU decode against the oracle's own reader (oracle/bamread.py:
+    gzip + struct, the restated 0x704 filter and bam_plp_push span), not
+    against the product's host decoder."""
+    from oracle import bamread
+    names, lengths, counts, tid, pos, span = bamread.scan_intervals(path)
+    assert list(g.references) == names and list(g.lengths) == lengths
+    assert (g.n_records, g.mapped, g.unmapped) == counts
+    gt, gp, gs = g.intervals()
+    assert np.array_equal(gt, tid) and np.array_equal(gp, pos) and np.array_equal(gs, span)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["bbmap.sorted.bam", "synth_edge.bam", "synth_multi.bam",
                                   "synth_longcigar.bam"])
@@ -176,6 +188,7 @@ def _assert_same(h, g):
 def test_gpu_decode_goldens(lib_built, golden_dir, name, window):
     h, g = _host_and_gpu(os.path.join(golden_dir, name), window_bytes=window)
     _assert_same(h, g)
+    _assert_oracle(os.path.join(golden_dir, name), g)
     g.close()
 
 
@@ -190,6 +203,7 @@ def test_gpu_decode_large(lib_built, tmp_path, level, window):
     synth.write_bam_fast(p, ["x", "y", "z"], lengths, *arrs, level=level, n_threads=8)
     h, g = _host_and_gpu(p, window_bytes=window)
     _assert_same(h, g)
+    _assert_oracle(p, g)
     t = g.timings()
     assert t["blocks"] > 100 and t["inflated_bytes"] > 0
     if window:
@@ -213,6 +227,7 @@ def test_gpu_decode_long_records(lib_built, tmp_path):
     for window in (0, 1 << 20):
         h, g = _host_and_gpu(path, window_bytes=window)
         _assert_same(h, g)
+        _assert_oracle(path, g)
         g.close()
 
 
@@ -272,3 +287,48 @@ def test_gpu_decode_feeds_engine(lib_built, golden_dir, fixture_golden):
     for ref, L in zip(h.references, h.lengths):
         assert pileup.classic(g, ref, 0, L) == pileup.classic(h, ref, 0, L)
     g.close()
+
+
+@pytest.mark.gpu
+def test_cli_gpu_decode_windows_vs_oracle(lib_built, tmp_path):
+    """`metacov pileup --decode gpu --window-bytes 1 MiB` over a 200k-record
+    BAM (~60 windows, records cut by window ends): the CSV equals the one
+    built from the oracle alone (bamread intervals -> coracle depth + exact
+    region rows -> classic()'s formatting), for whole contigs and tilings."""
+    import csv
+    import io
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    from metacov_amd.engine import classic_stats
+    from oracle import bamread, coracle
+    lengths = [3_000_000, 1_000, 900_000]
+    arrs = synth.edge_mix_arrays(lengths, 200_000, seed=17)
+    p = str(tmp_path / "w.bam")
+    synth.write_bam_fast(p, ["x", "y", "z"], lengths, *arrs, level=1, n_threads=8)
+    names, lens, _c, tid, pos, span = bamread.scan_intervals(p)
+    d, ext, coff = coracle.depth(lens, tid, pos, span)
+    rng = np.random.default_rng(3)
+    regs = [("x", 0, 3_000_000), ("y", 0, 1_000), ("z", 0, 900_000)]
+    for _ in range(12):
+        t = int(rng.integers(0, 3))
+        a = int(rng.integers(0, lens[t]))
+        regs.append((names[t], a, int(rng.integers(a + 1, lens[t] + 500))))
+    rows = coracle.region_stats(d, ext, coff, np.array([names.index(r[0]) for r in regs], np.int32),
+                                np.array([r[1] for r in regs], np.int64),
+                                np.array([r[2] for r in regs], np.int64))
+    out = io.StringIO()
+    w = None
+    for r, row in zip(regs, rows):
+        res = classic_stats(row)
+        if w is None:
+            w = csv.DictWriter(out, fieldnames=["sacc", "start", "end"] + sorted(res))
+            w.writeheader()
+        res.update({"sacc": r[0], "start": str(r[1]), "end": str(r[2])})
+        w.writerow(res)
+    rc = tmp_path / "r.csv"
+    rc.write_text("sacc,sstart,send\n" + "".join("%s,%d,%d\n" % r for r in regs))
+    o = tmp_path / "o.csv"
+    res = CliRunner().invoke(cli_pileup, ["-b", p, "-rc", str(rc), "-o", str(o), "--decode", "gpu",
+                                          "--window-bytes", str(1 << 20)])
+    assert res.exit_code == 0, res.output
+    assert open(o, newline="").read() == out.getvalue()

@@ -1044,9 +1044,10 @@ def test_bench_gpus_two_launches_ranks(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
+    rows_path = str(tmp_path / "rows.npy")
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
                           "--config", "c3", "--reads", "2000000", "--contigs", "64", "--steps", "2",
-                          "--warmup", "1", "--prepare-steps", "1"],
+                          "--warmup", "1", "--prepare-steps", "1", "--dump-rows", rows_path],
                          capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -1057,6 +1058,22 @@ def test_bench_gpus_two_launches_ranks(tmp_path):
     assert d["allgather_ms"] is not None and d["allgather_ms"] > 0
     assert d["config"]["regions"] == 64
     assert d["value"] > 0
+    # the gathered table, field by field, against the oracle on the same
+    # workload (regenerated here: the bench's GPU generator is seeded)
+    import torch
+    sys.path.insert(0, root)
+    import bench
+    lengths, weights = bench.config_contigs("c3", 2_000_000, 64)
+    tid, pos, span, _ = bench.device_workload(torch, lengths, weights, 2_000_000, 1,
+                                              torch.device("cuda", 0))
+    tid, pos, span = (x.cpu().numpy() for x in (tid, pos, span))
+    dd, ext, coff = coracle.depth(lengths, tid, pos, span)
+    R = len(lengths)
+    want = coracle.region_stats(dd, ext, coff, np.arange(R, dtype=np.int32), np.zeros(R, np.int64),
+                                lengths.astype(np.int64))
+    got = np.load(rows_path)
+    for f in want.dtype.names:
+        assert np.array_equal(got[f], want[f]), f
 
 
 def test_bench_rccl_exchange_one_rank(tmp_path):

@@ -140,3 +140,18 @@ def test_parallel_classic_equals_one_core():
     a, ca = coracle.pileup_classic(*args)
     b, cb = coracle.pileup_classic_parallel(*args, threads=5)
     assert np.array_equal(a, b) and ca == cb
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_scan_intervals_equals_record_reader(golden_dir, legacy):
+    """bamread.scan_intervals (the large-file form the multi-window GPU
+    decode tests use) equals the record reader on every golden BAM."""
+    for f in ("bbmap.sorted.bam", "synth_edge.bam", "synth_multi.bam", "synth_longcigar.bam"):
+        path = os.path.join(golden_dir, f)
+        names, lengths, recs = bamread.read_bam(path)
+        iv = bamread.pileup_intervals(recs, legacy_endpos=legacy)
+        n, l, counts, t, p, s = bamread.scan_intervals(path, legacy_endpos=legacy)
+        assert (n, l, counts[0]) == (names, lengths, len(recs))
+        assert counts[1] == sum(1 for r in recs if r.tid >= 0 and not r.flag & 4)
+        assert t.tolist() == [x[0] for x in iv] and p.tolist() == [x[1] for x in iv]
+        assert s.tolist() == [x[2] for x in iv]
