@@ -76,32 +76,25 @@ enum : int32_t {
     kSegSpan = 5,         // rec_parse 4
 };
 
-// primary Huffman tables per lane in LDS (MC_GZ_LDS) or in the lane's
-// global scratch slot
-#ifndef MC_GZ_LDS
-#define MC_GZ_LDS 1
-#endif
+// One wave per workgroup; a wave inflates kGzLanes blocks at a time, each
+// lane's primary tables and symbol lists in LDS (kGzLdsWords u16 per lane).
+// A lane's symbol loop is a chain of dependent short-latency steps, and a
+// window holds fewer blocks than the chip has lanes, so fewer blocks per wave
+// buys waves to hide that latency (and less divergence per step).  Measured
+// and dropped in round 3 (profiles/r03rc_gz_ab.txt): primary tables in the
+// global scratch (230 vs 198 ms), 9 / 7 table bits (half the lanes per CU).
 #ifndef MC_GZ_WAVES_PER_CU
-#define MC_GZ_WAVES_PER_CU 8
+#define MC_GZ_WAVES_PER_CU 4   // waves (workgroups) per CU the grid is sized for
 #endif
 #ifndef MC_GZ_LANES
-#define MC_GZ_LANES 32     // active lanes (blocks in flight) per wave: 64 100.9, 32 82.6, 16 135.6 ms
+#define MC_GZ_LANES 32         // active lanes (blocks in flight) per wave: 64 100.9, 32 82.6, 16 135.6 ms (r03)
 #endif
-#if MC_GZ_PROFILE
-__device__ unsigned long long g_gz_prof[8];
-#endif
-// One wave per workgroup with LDS tables; a wave inflates kGzLanes blocks at
-// a time.  A lane's symbol loop is a chain of dependent short-latency steps,
-// and a window holds fewer blocks than the chip has lanes, so fewer blocks
-// per wave buys waves to hide that latency (and less divergence per step).
-constexpr int kGzLanes = MC_GZ_LDS ? MC_GZ_LANES : kGzBlock;
-constexpr int kGzThreads = MC_GZ_LDS ? 64 : kGzBlock;
-constexpr int64_t kGzSlotWords = mc::gz::kScratchWords + (MC_GZ_LDS ? 0 : mc::gz::kPrimaryWords);
+constexpr int kGzLanes = MC_GZ_LANES;
+constexpr int kGzThreads = 64;
+constexpr int64_t kGzSlotWords = mc::gz::kScratchWords;
+constexpr int kGzLdsWords = mc::gz::kPrimaryWords + mc::gz::kSymWords;
 
-#ifndef MC_GZ_MIN_WAVES
-#define MC_GZ_MIN_WAVES 1      // __launch_bounds__ waves per SIMD (register budget)
-#endif
-__global__ void __launch_bounds__(kGzThreads, MC_GZ_MIN_WAVES)
+__global__ void __launch_bounds__(kGzThreads)
 gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ blk, int64_t nblk,
                   uint8_t* __restrict__ out, uint16_t* __restrict__ scratch, int* __restrict__ status,
                   int* __restrict__ any_err) {
@@ -109,21 +102,15 @@ gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ 
     const int64_t lane = (int64_t)blockIdx.x * kGzLanes + threadIdx.x;
     const int64_t lanes = (int64_t)gridDim.x * kGzLanes;
     uint16_t* S = scratch + lane * kGzSlotWords;
-#if MC_GZ_LDS
     using lds_u16 = __attribute__((address_space(3))) uint16_t;
-    __shared__ uint16_t tabs[kGzLanes * mc::gz::kPrimaryWords];
-    lds_u16* TL = (lds_u16*)(tabs + threadIdx.x * mc::gz::kPrimaryWords);
-#else
-    uint16_t* TL = S + mc::gz::kScratchWords;
-#endif
-    auto TD = TL + (1 << mc::gz::kLitBits);
+    __shared__ uint16_t tabs[kGzLanes * kGzLdsWords];
+    lds_u16* TL = (lds_u16*)(tabs + threadIdx.x * kGzLdsWords);
+    lds_u16* TD = TL + (1 << mc::gz::kLitBits);
+    lds_u16* SL = TL + mc::gz::kPrimaryWords;
+    lds_u16* SD = SL + mc::gz::kLitSyms;
     for (int64_t b = lane; b < nblk; b += lanes) {
         const GzBlock g = blk[b];
-#if MC_GZ_PROFILE
-        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, g_gz_prof);
-#else
-        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD);
-#endif
+        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, SL, SD);
         status[b] = rc;
         if (rc) atomicOr(any_err, 1);
     }
@@ -785,7 +772,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     // scratch for the inflate lanes
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
-    const int64_t max_lanes = (int64_t)dev_cus * MC_GZ_WAVES_PER_CU * (MC_GZ_LDS ? kGzLanes : 64);
+    const int64_t max_lanes = (int64_t)dev_cus * MC_GZ_WAVES_PER_CU * kGzLanes;
     if (window_bytes <= 0 && !blocks.empty()) {
         // resident when the compressed file, its inflated stream and the
         // scratch take at most half of the free device memory
@@ -966,13 +953,6 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     }
     HIP_TRY(hipStreamSynchronize(st));
     g->t_total = (now_s() - t_start) * 1e3;
-#if MC_GZ_PROFILE
-    unsigned long long pr[8];
-    HIP_TRY(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_gz_prof), sizeof pr));
-    std::fprintf(stderr, "[gz prof] build %.3g cyc  loop %.3g cyc  deflate blocks %llu  symbols %llu  matches %llu  "
-                 "copied %llu B  (per symbol %.1f cyc, build per block %.0f cyc)\n", (double)pr[0], (double)pr[1],
-                 pr[2], pr[3], pr[4], pr[5], pr[3] ? (double)pr[1] / pr[3] : 0.0, pr[2] ? (double)pr[0] / pr[2] : 0.0);
-#endif
     return MC_OK;
 }
 
@@ -1053,10 +1033,11 @@ extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst
     MC_REQUIRE(src && dst && clen >= 0 && isize >= 0, MC_E_INVALID, "bad argument");
     std::vector<uint8_t> padded((size_t)clen + kPad + 32, 0);
     std::memcpy(padded.data(), src, (size_t)clen);
-    std::vector<uint16_t> scratch(mc::gz::kScratchWords + mc::gz::kPrimaryWords);
+    std::vector<uint16_t> scratch(mc::gz::kScratchWords + kGzLdsWords);
     uint16_t* TL = scratch.data() + mc::gz::kScratchWords;
+    uint16_t* SL = TL + mc::gz::kPrimaryWords;
     const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data(), TL,
-                                         TL + (1 << mc::gz::kLitBits));
+                                         TL + (1 << mc::gz::kLitBits), SL, SL + mc::gz::kLitSyms);
     MC_REQUIRE(rc == 0, MC_E_IO, "inflate failed: %s", gz_err_msg(rc));
     return MC_OK;
 }

@@ -1029,7 +1029,11 @@ extern "C" int mc_set_direct_prepare(mc_ctx* ctx, int enable) {
     return MC_OK;
 }
 
-// Resident workgroups of a K2 variant (queried once per ctx and LDS size).
+// Resident workgroups of a K2 variant (queried once per ctx and LDS size),
+// at most MC_K2_PER_CU per CU (0: as many as fit).
+#ifndef MC_K2_PER_CU
+#define MC_K2_PER_CU 0
+#endif
 static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t lds, int64_t work,
                           int* grid) {
     int& cached = ctx->k2_resident[variant];
@@ -1038,6 +1042,7 @@ static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t l
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds));
+        if (MC_K2_PER_CU > 0) per = std::min(per, (int)MC_K2_PER_CU);
         cached = ncu * std::max(1, per);
         ctx->k2_resident_lds[variant] = lds;
     }

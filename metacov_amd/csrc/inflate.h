@@ -5,11 +5,14 @@
 // threads; at 16 threads it is the end-to-end bound of `metacov pileup`
 // (profiles/r03pp_e2e.json: 1.56 s of 1.78 s for a 5.2 GB BAM).  Here every
 // BGZF block (<= 64 KiB out, an independent deflate stream) is one lane's
-// work: a 64-bit bit buffer refilled by aligned 32-bit loads, canonical
-// Huffman codes decoded by a primary lookup table (10 bits literal/length,
-// 8 bits distance; longer codes by the count/symbol walk of RFC 1951 §3.2.2),
-// LZ77 copies from the lane's own output.  The per-lane tables live in a
-// global scratch slab (a lane owns kScratchWords u16).
+// work: a 64-bit bit buffer fed by 16-byte loads, canonical Huffman codes
+// decoded by a primary lookup table (MC_GZ_LIT_BITS = 8 bits literal/length,
+// MC_GZ_DIST_BITS = 6 bits distance; longer codes by the count/symbol walk of
+// RFC 1951 §3.2.2 over counts in registers and the canonical symbol lists),
+// LZ77 copies from the lane's own output, queued per lane.  The kernel keeps
+// the primary tables and the symbol lists of each lane in LDS (bam_gpu.hip);
+// the build's counts and code lengths in a per-lane global scratch slot
+// (kScratchWords u16).
 //
 // Every function is __host__ __device__: mc_gz_inflate_host runs the same
 // code on the CPU for the unit tests (tests/test_gpu_decode.py compares it
@@ -24,9 +27,6 @@ namespace gz {
 
 #define MC_HD __host__ __device__ __forceinline__
 
-#ifndef MC_GZ_PROFILE
-#define MC_GZ_PROFILE 0
-#endif
 #ifndef MC_GZ_QUEUE
 #define MC_GZ_QUEUE 16          // matches a lane defers (0: copy each at once)
 #endif
@@ -45,15 +45,16 @@ constexpr int kLitBits = MC_GZ_LIT_BITS;    // primary table index bits, literal
 constexpr int kDistBits = MC_GZ_DIST_BITS;  // distance alphabet
 static_assert(kLitBits >= 7, "the code length code (<= 7 bits) uses the literal table");
 constexpr int kPrimaryWords = (1 << kLitBits) + (1 << kDistBits);   // both primary tables (u16)
-// per-lane scratch (u16 words): counts, symbols, lengths (the primary tables
-// are separate: global scratch or LDS)
+// per-lane scratch (u16 words): counts, lengths (the primary tables and the
+// symbol lists are separate: LDS in the kernel)
 constexpr int kLitCnt = 0;                        // [16] codes per length
 constexpr int kDistCnt = kLitCnt + 16;            // [16]
-constexpr int kLitSym = kDistCnt + 16;            // [288] symbols in canonical order
-constexpr int kDistSym = kLitSym + 288;           // [32]
-constexpr int kLens = kDistSym + 32;              // [320] code lengths being read
+constexpr int kLens = kDistCnt + 16;              // [320] code lengths being read
 constexpr int kOffs = kLens + 320;                // [16] build temporary
 constexpr int kScratchWords = kOffs + 16;
+constexpr int kLitSyms = 288;                     // symbol lists in canonical order
+constexpr int kDistSyms = 32;
+constexpr int kSymWords = kLitSyms + kDistSyms;
 
 enum : int {
     kOk = 0,
@@ -148,9 +149,8 @@ MC_HD uint32_t bitrev(uint32_t code, int len) {
 // error; incomplete codes are accepted (their missing patterns fail in
 // decode_slow).
 template <class TP>
-MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, int sym_off, const uint16_t* lens, int n) {
+MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint16_t* lens, int n) {
     uint16_t* cnt = S + cnt_off;
-    uint16_t* sym = S + sym_off;
     uint16_t* offs = S + kOffs;
     for (int l = 0; l < 16; ++l) cnt[l] = 0;
     for (int s = 0; s < n; ++s) cnt[lens[s] & 15]++;
@@ -184,7 +184,8 @@ MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, int sym_off, const 
 // counts per length are registers (loaded once per table): walked from
 // memory, each length was a dependent global load, and with the walk
 // divergent some lane of the wave took it at most symbol steps.
-MC_HD int decode_slow(uint64_t bits, const int (&cnt)[16], const uint16_t* sym, int* used) {
+template <class TP>
+MC_HD int decode_slow(uint64_t bits, const int (&cnt)[16], TP sym, int* used) {
     int code = 0, first = 0, index = 0, found = -1, len = 0;
 #pragma unroll
     for (int l = 1; l < 16; ++l) {
@@ -209,14 +210,14 @@ MC_HD void load_counts(const uint16_t* S, int cnt_off, int (&cnt)[16]) {
 }
 
 template <class TP>
-MC_HD int decode_sym(Bits& b, const uint16_t* S, TP T, int tb, const int (&cnt)[16], int sym_off) {
+MC_HD int decode_sym(Bits& b, TP T, int tb, const int (&cnt)[16], TP sym) {
     const uint16_t e = T[(uint32_t)b.buf & ((1u << tb) - 1u)];
     int used, s;
     if (e) {
         used = e & 15;
         s = e >> 4;
     } else {
-        s = decode_slow(b.buf, cnt, S + sym_off, &used);
+        s = decode_slow(b.buf, cnt, sym, &used);
         if (s < 0) return -1;
     }
     b.buf >>= used;
@@ -227,7 +228,7 @@ MC_HD int decode_sym(Bits& b, const uint16_t* S, TP T, int tb, const int (&cnt)[
 // Dynamic block header: code length code, then the literal/length and
 // distance code lengths (RFC 1951 §3.2.7), then both tables.
 template <class TP>
-MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD) {
+MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     bits_refill(b);
     const int nlen = (int)bits_take(b, 5) + 257;
     const int ndist = (int)bits_take(b, 5) + 1;
@@ -241,14 +242,14 @@ MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD) {
         lens[order[i]] = (uint16_t)bits_take(b, 3);
     }
     // the code length code (<= 7 bits) goes through the literal table's slots
-    int rc = build_code(S, TL, 7, kLitCnt, kLitSym, lens, 19);
+    int rc = build_code(S, TL, 7, kLitCnt, SL, lens, 19);
     if (rc) return rc;
     int ccnt[16];
     load_counts(S, kLitCnt, ccnt);
     int idx = 0;
     while (idx < nlen + ndist) {
         bits_refill(b);
-        const int sym = decode_sym(b, S, TL, 7, ccnt, kLitSym);
+        const int sym = decode_sym(b, TL, 7, ccnt, SL);
         if (sym < 0) return kErrCodes;
         if (sym < 16) {
             lens[idx++] = (uint16_t)sym;
@@ -270,19 +271,19 @@ MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD) {
     if (lens[256] == 0) return kErrCodes;
     // the distance lengths follow the literal ones in lens[]; the literal
     // table is built last because its build overwrites nothing of them
-    rc = build_code(S, TD, kDistBits, kDistCnt, kDistSym, lens + nlen, ndist);
+    rc = build_code(S, TD, kDistBits, kDistCnt, SD, lens + nlen, ndist);
     if (rc) return rc;
-    return build_code(S, TL, kLitBits, kLitCnt, kLitSym, lens, nlen);
+    return build_code(S, TL, kLitBits, kLitCnt, SL, lens, nlen);
 }
 
 template <class TP>
-MC_HD int read_fixed(uint16_t* S, TP TL, TP TD) {
+MC_HD int read_fixed(uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     uint16_t* lens = S + kLens;
     for (int s = 0; s < 288; ++s) lens[s] = (uint16_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
-    int rc = build_code(S, TL, kLitBits, kLitCnt, kLitSym, lens, 288);
+    int rc = build_code(S, TL, kLitBits, kLitCnt, SL, lens, 288);
     if (rc) return rc;
     for (int s = 0; s < 30; ++s) lens[s] = 5;
-    return build_code(S, TD, kDistBits, kDistCnt, kDistSym, lens, 30);
+    return build_code(S, TD, kDistBits, kDistCnt, SD, lens, 30);
 }
 
 // LZ77 copy of len bytes from dist back: every source byte precedes the
@@ -311,13 +312,6 @@ MC_HD void lz_copy(uint8_t* q, int len, int dist) {
 #endif
 }
 
-// One raw deflate stream src[0, clen) into dst[0, isize): kOk iff it ends
-// (BFINAL) with exactly isize bytes and without reading past clen.  S: the
-// lane's scratch; TL / TD: its primary tables (1 << kLitBits, 1 << kDistBits).
-// prof (MC_GZ_PROFILE builds, else null): cycles in table builds and in the
-// symbol loops, deflate blocks, symbols, matches, copied bytes
-// TP: the tables' pointer type (uint16_t*, or an LDS-qualified pointer in the
-// kernel so lookups are ds_read, waited on by lgkmcnt alone).
 // A lane's deferred LZ77 copies.  With one lane per BGZF block, a copy
 // waits on its source bytes (global memory); done as decoded, some lane of
 // the wave has one at almost every symbol step (6 % of symbols are matches,
@@ -349,39 +343,22 @@ MC_HD bool wave_any(bool p) {
 #endif
 }
 
+// One raw deflate stream src[0, clen) into dst[0, isize): kOk iff it ends
+// (BFINAL) with exactly isize bytes and without reading past clen.  S: the
+// lane's scratch; TL / TD: its primary tables (1 << kLitBits, 1 << kDistBits);
+// SL / SD: its symbol lists (kLitSyms, kDistSyms).  TP: the pointer type
+// (uint16_t* on the host, an LDS-qualified pointer in the kernel, so every
+// lookup of the symbol loop is a ds_read waited on by lgkmcnt alone: with the
+// symbol lists in the global scratch, a code longer than the primary table,
+// which some lane of the wave meets at almost every step, cost a global round
+// trip whose vmcnt wait also drained the lane's output stores).
 template <class TP>
 MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S, TP TL, TP TD,
-                        unsigned long long* prof = nullptr) {
+                        TP SL, TP SD) {
     if (isize == 0) return kOk;
 #if MC_GZ_QUEUE
     MatchQueue mq;
     mq.n = 0;
-#endif
-#if MC_GZ_PROFILE
-    unsigned long long c_build = 0, c_loop = 0, n_blk = 0, n_sym = 0, n_match = 0, n_copy = 0;
-    auto tick = []() { return (unsigned long long)__builtin_readcyclecounter(); };
-    struct Flush {
-        unsigned long long* p;
-        unsigned long long *a, *b, *c, *d, *e, *f;
-        MC_HD ~Flush() {
-            if (p) {
-                __atomic_fetch_add(p + 0, *a, __ATOMIC_RELAXED);
-                __atomic_fetch_add(p + 1, *b, __ATOMIC_RELAXED);
-                __atomic_fetch_add(p + 2, *c, __ATOMIC_RELAXED);
-                __atomic_fetch_add(p + 3, *d, __ATOMIC_RELAXED);
-                __atomic_fetch_add(p + 4, *e, __ATOMIC_RELAXED);
-                __atomic_fetch_add(p + 5, *f, __ATOMIC_RELAXED);
-            }
-        }
-    } flush{prof, &c_build, &c_loop, &n_blk, &n_sym, &n_match, &n_copy};
-#define MC_GZ_TICK(v) unsigned long long v = tick()
-#define MC_GZ_ADD(dst, v) dst += tick() - v
-#define MC_GZ_CNT(dst, x) dst += (x)
-#else
-    (void)prof;
-#define MC_GZ_TICK(v)
-#define MC_GZ_ADD(dst, v)
-#define MC_GZ_CNT(dst, x)
 #endif
     Bits b;
     bits_init(b, src, 0, clen);
@@ -406,17 +383,12 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
         } else if (type == 3) {
             return kErrBlockType;
         } else {
-            MC_GZ_TICK(t0);
-            const int rc = type == 1 ? read_fixed(S, TL, TD) : read_dynamic(b, S, TL, TD);
-            MC_GZ_ADD(c_build, t0);
-            MC_GZ_CNT(n_blk, 1);
+            const int rc = type == 1 ? read_fixed(S, TL, TD, SL, SD) : read_dynamic(b, S, TL, TD, SL, SD);
             if (rc) return rc;
             int lcnt[16], dcnt[16];
             load_counts(S, kLitCnt, lcnt);
             load_counts(S, kDistCnt, dcnt);
-            MC_GZ_TICK(t1);
             for (;;) {
-                MC_GZ_CNT(n_sym, 1);
 #if MC_GZ_QUEUE
                 // all lanes still in a symbol loop vote: one full queue
                 // flushes every lane's (at most one push per iteration)
@@ -424,7 +396,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
 #endif
                 if (bits_pos(b) > limit_bits) return kErrInput;
                 bits_refill(b);
-                int s = decode_sym(b, S, TL, kLitBits, lcnt, kLitSym);
+                int s = decode_sym(b, TL, kLitBits, lcnt, SL);
                 if (s < 0) return kErrSymbol;
                 if (s < 256) {
                     if (o >= isize) return kErrOutput;
@@ -444,7 +416,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                     len = ((4 + (s & 3)) << e) + 3 + (int)bits_take(b, e);
                 }
                 bits_refill(b);
-                const int d = decode_sym(b, S, TD, kDistBits, dcnt, kDistSym);
+                const int d = decode_sym(b, TD, kDistBits, dcnt, SD);
                 if (d < 0 || d >= 30) return kErrSymbol;
                 int dist;
                 if (d < 4) {
@@ -465,11 +437,8 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
 #else
                 lz_copy(dst + o, len, dist);
 #endif
-                MC_GZ_CNT(n_match, 1);
-                MC_GZ_CNT(n_copy, len);
                 o += len;
             }
-            MC_GZ_ADD(c_loop, t1);
         }
         if (bits_pos(b) > limit_bits) return kErrInput;
         if (final) break;
@@ -478,9 +447,6 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
     mq_flush(mq, dst);
 #endif
     return o == isize ? kOk : kErrSize;
-#undef MC_GZ_TICK
-#undef MC_GZ_ADD
-#undef MC_GZ_CNT
 }
 
 // ---------------------------------------------------------------- BAM records

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--reads", type=int, default=100_000_000)
     ap.add_argument("--contigs", type=int, default=None, help="(c3) contigs, e.g. a strong-scaling shard")
     ap.add_argument("--nocheck", action="store_true", help="deliberately-wrong experiment builds")
-    ap.add_argument("--config", default="c3", choices=["c3", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     a = ap.parse_args()
     import torch
     from bench import CONFIGS, config_contigs, device_workload

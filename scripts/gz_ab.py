@@ -33,9 +33,11 @@ def main():
     print("wrote %s (%.2f GB) in %.1f s" % (path, os.path.getsize(path) / 1e9, time.perf_counter() - t0),
           flush=True)
     out = {}
-    for name in a.variants:
-        lib = _lib.load(os.path.join(ROOT, "metacov_amd", "variants", "lib_%s.so" % name))
-        for rep in range(a.reps):
+    libs = {name: _lib.load(os.path.join(ROOT, "metacov_amd", "variants", "lib_%s.so" % name))
+            for name in a.variants}
+    for rep in range(a.reps):             # interleaved: rep-major, every variant per rep
+        for name in a.variants:
+            lib = libs[name]
             h = ctypes.c_void_p()
             _lib.check(lib.mc_bam_gpu_open(path.encode(), 0, 16, 0x704, a.window, ctypes.byref(h)), lib)
             t = _lib.GpuDecodeTimings()
