@@ -84,7 +84,7 @@ enum : int32_t {
 // and dropped in round 3 (profiles/r03rc_gz_ab.txt): primary tables in the
 // global scratch (230 vs 198 ms), 9 / 7 table bits (half the lanes per CU).
 #ifndef MC_GZ_WAVES_PER_CU
-#define MC_GZ_WAVES_PER_CU 4   // waves (workgroups) per CU the grid is sized for
+#define MC_GZ_WAVES_PER_CU 0   // waves (workgroups) per CU the grid is sized for; 0: as many as the LDS holds
 #endif
 #ifndef MC_GZ_LANES
 #define MC_GZ_LANES 32         // active lanes (blocks in flight) per wave: 64 100.9, 32 82.6, 16 135.6 ms (r03)
@@ -92,7 +92,10 @@ enum : int32_t {
 constexpr int kGzLanes = MC_GZ_LANES;
 constexpr int kGzThreads = 64;
 constexpr int64_t kGzSlotWords = mc::gz::kScratchWords;
-constexpr int kGzLdsWords = mc::gz::kPrimaryWords + mc::gz::kSymWords;
+constexpr int kGzLdsWords = mc::gz::kPrimaryWords + mc::gz::kSymWords + 2 * mc::gz::kRingWords;
+constexpr int kGzWavesPerCu = MC_GZ_WAVES_PER_CU > 0 ? MC_GZ_WAVES_PER_CU
+                                                     : (160 << 10) / (kGzLanes * kGzLdsWords * 2);
+static_assert(kGzWavesPerCu >= 1, "inflate LDS per wave exceeds a CU");
 
 __global__ void __launch_bounds__(kGzThreads)
 gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ blk, int64_t nblk,
@@ -108,9 +111,12 @@ gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ 
     lds_u16* TD = TL + (1 << mc::gz::kLitBits);
     lds_u16* SL = TL + mc::gz::kPrimaryWords;
     lds_u16* SD = SL + mc::gz::kLitSyms;
+    using lds_u32 = __attribute__((address_space(3))) uint32_t;
+    static_assert((mc::gz::kPrimaryWords + mc::gz::kSymWords) % 2 == 0 && kGzLdsWords % 2 == 0, "ring alignment");
+    lds_u32* ring = (lds_u32*)(SD + mc::gz::kDistSyms);
     for (int64_t b = lane; b < nblk; b += lanes) {
         const GzBlock g = blk[b];
-        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, SL, SD);
+        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, SL, SD, ring);
         status[b] = rc;
         if (rc) atomicOr(any_err, 1);
     }
@@ -772,7 +778,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     // scratch for the inflate lanes
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
-    const int64_t max_lanes = (int64_t)dev_cus * MC_GZ_WAVES_PER_CU * kGzLanes;
+    const int64_t max_lanes = (int64_t)dev_cus * kGzWavesPerCu * kGzLanes;
     if (window_bytes <= 0 && !blocks.empty()) {
         // resident when the compressed file, its inflated stream and the
         // scratch take at most half of the free device memory
@@ -1036,8 +1042,9 @@ extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst
     std::vector<uint16_t> scratch(mc::gz::kScratchWords + kGzLdsWords);
     uint16_t* TL = scratch.data() + mc::gz::kScratchWords;
     uint16_t* SL = TL + mc::gz::kPrimaryWords;
+    uint32_t ring[mc::gz::kRingWords];
     const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data(), TL,
-                                         TL + (1 << mc::gz::kLitBits), SL, SL + mc::gz::kLitSyms);
+                                         TL + (1 << mc::gz::kLitBits), SL, SL + mc::gz::kLitSyms, ring);
     MC_REQUIRE(rc == 0, MC_E_IO, "inflate failed: %s", gz_err_msg(rc));
     return MC_OK;
 }

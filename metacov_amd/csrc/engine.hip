@@ -190,6 +190,14 @@ struct mc_ctx {
     DevBuf<int32_t> d_jidx;               // [2 * (n_base + 1)]: J(k w), J(k w - halo)
     DevBuf<int32_t> d_fsamp;              // [nc + 1] first sample of each contig
     DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
+    // K2's constant arguments (K2Consts), a few variants resident at once:
+    // each launch finds its bytes in a slot or uploads them into the next one
+    static constexpr int kK2Slots = 4;
+    DevBuf<K2Consts> d_k2c;
+    Pinned h_k2c;
+    K2Consts k2c[kK2Slots];
+    bool k2c_valid[kK2Slots] = {false, false, false, false};
+    int k2c_next = 0;
     int32_t max_span = 0;
     bool long_hint = false;               // the last full prepare of this contig set had long reads
     bool prep_pending = false;            // the last full prepare's time is not read yet
@@ -352,6 +360,8 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_jidx.release();
     ctx->d_fsamp.release();
     ctx->d_dres.release();
+    ctx->d_k2c.release();
+    ctx->h_k2c.release();
     ctx->d_tile_cnt.release();
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
@@ -1079,6 +1089,29 @@ static DirectWindow direct_window(const mc_ctx* ctx) {
                         (int)((int64_t)kWinBelow * fused_hist_vals(ctx->has_long) / kHistBins)};
 }
 
+// K2's constant arguments in device memory (K2Consts): the slot holding
+// these bytes, else the next slot, uploaded on the ctx stream.  The pinned
+// staging is reused only after the stream has drained the previous upload
+// (uploads happen when buffers are reallocated or the region set changes).
+static int k2_consts(mc_ctx* ctx, const K2Consts& kc, const K2Consts** out) {
+    for (int i = 0; i < mc_ctx::kK2Slots; ++i)
+        if (ctx->k2c_valid[i] && std::memcmp(&ctx->k2c[i], &kc, sizeof kc) == 0) {
+            *out = ctx->d_k2c.p + i;
+            return MC_OK;
+        }
+    HIP_TRY(ctx->d_k2c.reserve(mc_ctx::kK2Slots));
+    HIP_TRY(ctx->h_k2c.reserve(sizeof(K2Consts)));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));   // the staging's previous copy is done
+    const int i = ctx->k2c_next;
+    ctx->k2c_next = (i + 1) % mc_ctx::kK2Slots;
+    std::memcpy(ctx->h_k2c.h, &kc, sizeof kc);
+    HIP_TRY(hipMemcpyAsync(ctx->d_k2c.p + i, ctx->h_k2c.h, sizeof kc, hipMemcpyHostToDevice, ctx->stream));
+    ctx->k2c[i] = kc;
+    ctx->k2c_valid[i] = true;
+    *out = ctx->d_k2c.p + i;
+    return MC_OK;
+}
+
 // K2 launch (plain or with fused region statistics)
 // ea / eb: K2's start / end events (default ev[4] / ev[5], read lazily by
 // mc_get_timings)
@@ -1113,15 +1146,24 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
-    const ReadArrays ra{ctx->d_gpos.p, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p};
     const int64_t n_base = ctx->n_chunks * ctx->cstride;
-    const DirectArgs da{ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_len.p, (int32_t)ctx->len.size(),
-                        ctx->d_dres.p, ctx->direct_gen, direct_window(ctx)};
+    K2Consts kc;
+    std::memset(&kc, 0, sizeof kc);   // (padding too: slots are matched bytewise)
+    kc.A = ReadArrays{ctx->d_gpos.p, ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p};
+    kc.R = fr;
+    DirectWindow w = direct_window(ctx);
+    w.parity = 0;   // (K2 takes this call's parity as an argument)
+    kc.D = DirectArgs{ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_len.p, (int32_t)ctx->len.size(),
+                      ctx->d_dres.p, w};
+    const K2Consts* dk = nullptr;
+    if (int rc = k2_consts(ctx, kc, &dk)) return rc;
+    const int win_parity = (int)(ctx->direct_gen & 1);
 #define MC_LAUNCH_K2(S, L, D)                                                                  \
-    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, ra,            \
+    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, dk,          \
                        ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
-                       toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p, fr, da)
+                       toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p,        \
+                       (unsigned long long)ctx->direct_gen, win_parity)
     if (stats) {
         if (lng) MC_LAUNCH_K2(true, true, false);
         else if (dir) MC_LAUNCH_K2(true, false, true);

@@ -68,72 +68,121 @@ enum : int {
     kErrSize = 8,          // the stream ended before ISIZE bytes
 };
 
-// Bit reader over src[0, clen): 16-byte aligned loads, the next 16 bytes in
-// flight while the current ones are consumed (a lane's refill was a
-// dependent load every ~3 symbols).  The buffer src points into must be
-// readable up to 32 bytes past clen rounded up to 16 (callers pad it).
+MC_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __any(p);
+#else
+    return p;
+#endif
+}
+
+// Bit reader over src[0, clen) through a per-lane ring of kRingWords u32 in
+// LDS (the kernel; a plain array on the host).  The ring is topped up only at
+// wave-uniform points (bits_topup: a vote, then every lane with room loads
+// kRingFill words as 16-byte groups and one wait covers the whole wave).
+// Loading 16 bytes ahead in registers instead (round 3), every lane's refill
+// copied the in-flight group into the loop-carried registers at once: the
+// wave waited a full memory latency, draining every output store in flight
+// too (vmcnt counts stores), at almost every symbol step of some lane.  The
+// buffer src points into must be readable up to 16 bytes past clen rounded up
+// to 16 (callers pad it).
+#ifndef MC_GZ_RING
+#define MC_GZ_RING 16
+#endif
+constexpr int kRingWords = MC_GZ_RING;            // power of two, >= 8
+constexpr int kRingFill = kRingWords / 2;         // words per top-up (a multiple of 4)
+constexpr int kRingLow = 4;                       // a lane below this many words calls the top-up
+static_assert((kRingWords & (kRingWords - 1)) == 0 && kRingWords >= 8, "ring: power of two >= 8 words");
+
+// the ring's pointer type for a table pointer type (LDS-qualified or plain)
+template <class TP> struct RingOf;
+template <> struct RingOf<uint16_t*> { using type = uint32_t*; };
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+template <> struct RingOf<__attribute__((address_space(3))) uint16_t*> {
+    using type = __attribute__((address_space(3))) uint32_t*;
+};
+#endif
+
+template <class RP>
 struct Bits {
     const uint4* p;         // next 16-byte group to load
     const uint4* pend;      // groups at or past it read the last one again (past the payload)
-    uint4 cur, nxt;         // cur: words ci..3 not yet in buf
-    int ci;
+    RP ring;                // kRingWords words: [rpos, rfill) not yet in buf
+    uint32_t rpos, rfill;   // absolute word counters (slot = counter % kRingWords)
     uint64_t buf;
     int cnt;                // valid bits in buf
     int64_t end_bits;       // bits from src[0] to the end of the words moved into buf
 };
 
-// The address is clamped, not the value: a select on the loaded value made
-// the compiler wait for the load at once, defeating the prefetch.  Groups past
-// the payload are never consumed by a valid stream (bits_pos checks).
+// The address is clamped, not the value.  Groups past the payload are never
+// consumed by a valid stream (bits_pos checks).
 MC_HD uint4 ld_group(const uint4* p, const uint4* pend) { return *(p < pend ? p : pend - 1); }
 
-MC_HD uint32_t word_of(const uint4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+template <int kWords, class RP>
+MC_HD void ring_load(Bits<RP>& b) {   // every load issued before the first ring write
+    uint4 v[kWords / 4];
+#pragma unroll
+    for (int g = 0; g < kWords / 4; ++g) v[g] = ld_group(b.p + g, b.pend);
+    b.p += kWords / 4;
+#pragma unroll
+    for (int g = 0; g < kWords / 4; ++g) {
+        const uint32_t s = (b.rfill + 4 * g) & (kRingWords - 1);   // 4-aligned: no wrap inside a group
+        b.ring[s] = v[g].x;
+        b.ring[s + 1] = v[g].y;
+        b.ring[s + 2] = v[g].z;
+        b.ring[s + 3] = v[g].w;
+    }
+    b.rfill += kWords;
+}
+
+// Every lane that may consume input calls it at a point where the whole wave
+// (or the active part of it) does: when some lane is low, each lane with room
+// loads kRingFill words, and the wave waits once.
+template <class RP>
+MC_HD void bits_topup(Bits<RP>& b) {
+    if (wave_any((int)(b.rfill - b.rpos) < kRingLow)) {
+        if ((int)(b.rfill - b.rpos) <= kRingWords - kRingFill) ring_load<kRingFill>(b);
+    }
+}
 
 // (pointer arithmetic only, no integer round trip: the compiler keeps the
-// global address space and issues global loads, not flat ones, whose waits
-// also drain the lane's outstanding output stores)
-MC_HD void bits_init(Bits& b, const uint8_t* src, int64_t byte_off, int64_t clen) {
+// global address space and issues global loads, not flat ones)
+template <class RP>
+MC_HD void bits_init(Bits<RP>& b, const uint8_t* src, int64_t byte_off, int64_t clen) {
     const uint8_t* a = src + byte_off;
     const int mis = (int)((uintptr_t)a & 15);
-    const uint4* g = reinterpret_cast<const uint4*>(a - mis);
     const uint8_t* e = src + clen;
+    b.p = reinterpret_cast<const uint4*>(a - mis);
     b.pend = reinterpret_cast<const uint4*>(e + ((16 - (int)((uintptr_t)e & 15)) & 15)) + 1;
-    b.cur = ld_group(g, b.pend);
-    b.nxt = ld_group(g + 1, b.pend);
-    b.p = g + 2;
+    b.rpos = b.rfill = 0;
+    ring_load<kRingWords>(b);
     const int wi = mis >> 2, bi = mis & 3;
-    b.buf = (uint64_t)word_of(b.cur, wi) >> (8 * bi);
+    b.rpos = wi + 1;
+    b.buf = (uint64_t)b.ring[wi] >> (8 * bi);
     b.cnt = 32 - 8 * bi;
     b.end_bits = (byte_off + 4 - bi) * 8;
-    b.ci = wi + 1;
-    if (b.ci == 4) {
-        b.cur = b.nxt;
-        b.nxt = ld_group(b.p++, b.pend);
-        b.ci = 0;
-    }
 }
 
-MC_HD void bits_refill(Bits& b) {   // afterwards cnt > 32
+template <class RP>
+MC_HD void bits_refill(Bits<RP>& b) {   // afterwards cnt > 32 (rpos < rfill: bits_topup's job)
     if (b.cnt <= 32) {
-        b.buf |= (uint64_t)word_of(b.cur, b.ci) << b.cnt;
+        b.buf |= (uint64_t)b.ring[b.rpos & (kRingWords - 1)] << b.cnt;
+        ++b.rpos;
         b.cnt += 32;
         b.end_bits += 32;
-        if (++b.ci == 4) {
-            b.cur = b.nxt;
-            b.nxt = ld_group(b.p++, b.pend);
-            b.ci = 0;
-        }
     }
 }
 
-MC_HD uint32_t bits_take(Bits& b, int n) {   // n <= cnt, n < 32
+template <class RP>
+MC_HD uint32_t bits_take(Bits<RP>& b, int n) {   // n <= cnt, n < 32
     const uint32_t v = (uint32_t)b.buf & ((1u << n) - 1u);
     b.buf >>= n;
     b.cnt -= n;
     return v;
 }
 
-MC_HD int64_t bits_pos(const Bits& b) { return b.end_bits - b.cnt; }   // next unread bit
+template <class RP>
+MC_HD int64_t bits_pos(const Bits<RP>& b) { return b.end_bits - b.cnt; }   // next unread bit
 
 MC_HD uint32_t bitrev(uint32_t code, int len) {
     uint32_t r = 0;
@@ -209,8 +258,8 @@ MC_HD void load_counts(const uint16_t* S, int cnt_off, int (&cnt)[16]) {
     for (int l = 0; l < 16; ++l) cnt[l] = S[cnt_off + l];
 }
 
-template <class TP>
-MC_HD int decode_sym(Bits& b, TP T, int tb, const int (&cnt)[16], TP sym) {
+template <class TP, class RP>
+MC_HD int decode_sym(Bits<RP>& b, TP T, int tb, const int (&cnt)[16], TP sym) {
     const uint16_t e = T[(uint32_t)b.buf & ((1u << tb) - 1u)];
     int used, s;
     if (e) {
@@ -227,8 +276,9 @@ MC_HD int decode_sym(Bits& b, TP T, int tb, const int (&cnt)[16], TP sym) {
 
 // Dynamic block header: code length code, then the literal/length and
 // distance code lengths (RFC 1951 §3.2.7), then both tables.
-template <class TP>
-MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
+template <class TP, class RP>
+MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
+    bits_topup(b);
     bits_refill(b);
     const int nlen = (int)bits_take(b, 5) + 257;
     const int ndist = (int)bits_take(b, 5) + 1;
@@ -238,6 +288,7 @@ MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
     for (int i = 0; i < 19; ++i) lens[i] = 0;
     for (int i = 0; i < ncode; ++i) {
+        if ((i & 7) == 0) bits_topup(b);   // (8 x 3 bits per top-up at most)
         bits_refill(b);
         lens[order[i]] = (uint16_t)bits_take(b, 3);
     }
@@ -248,6 +299,7 @@ MC_HD int read_dynamic(Bits& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     load_counts(S, kLitCnt, ccnt);
     int idx = 0;
     while (idx < nlen + ndist) {
+        bits_topup(b);
         bits_refill(b);
         const int sym = decode_sym(b, TL, 7, ccnt, SL);
         if (sym < 0) return kErrCodes;
@@ -335,18 +387,11 @@ MC_HD void mq_flush(MatchQueue& q, uint8_t* dst) {
     q.n = 0;
 }
 
-MC_HD bool wave_any(bool p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __any(p);
-#else
-    return p;
-#endif
-}
-
 // One raw deflate stream src[0, clen) into dst[0, isize): kOk iff it ends
 // (BFINAL) with exactly isize bytes and without reading past clen.  S: the
 // lane's scratch; TL / TD: its primary tables (1 << kLitBits, 1 << kDistBits);
-// SL / SD: its symbol lists (kLitSyms, kDistSyms).  TP: the pointer type
+// SL / SD: its symbol lists (kLitSyms, kDistSyms); ring: its input ring
+// (kRingWords u32, see Bits).  TP: the pointer type
 // (uint16_t* on the host, an LDS-qualified pointer in the kernel, so every
 // lookup of the symbol loop is a ds_read waited on by lgkmcnt alone: with the
 // symbol lists in the global scratch, a code longer than the primary table,
@@ -354,17 +399,19 @@ MC_HD bool wave_any(bool p) {
 // trip whose vmcnt wait also drained the lane's output stores).
 template <class TP>
 MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S, TP TL, TP TD,
-                        TP SL, TP SD) {
+                        TP SL, TP SD, typename RingOf<TP>::type ring) {
     if (isize == 0) return kOk;
 #if MC_GZ_QUEUE
     MatchQueue mq;
     mq.n = 0;
 #endif
-    Bits b;
+    Bits<typename RingOf<TP>::type> b;
+    b.ring = ring;
     bits_init(b, src, 0, clen);
     const int64_t limit_bits = clen * 8;
     int64_t o = 0;
     for (;;) {
+        bits_topup(b);
         bits_refill(b);
         const int final = (int)bits_take(b, 1);
         const int type = (int)bits_take(b, 2);
@@ -395,6 +442,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                 if (wave_any(mq.n == MC_GZ_QUEUE)) mq_flush(mq, dst);
 #endif
                 if (bits_pos(b) > limit_bits) return kErrInput;
+                bits_topup(b);   // (a symbol with its distance takes <= 2 words)
                 bits_refill(b);
                 int s = decode_sym(b, TL, kLitBits, lcnt, SL);
                 if (s < 0) return kErrSymbol;

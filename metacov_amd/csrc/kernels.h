@@ -688,10 +688,12 @@ struct DirectWindow {
     int win_below;
 };
 
-__device__ __forceinline__ int direct_window_base(const DirectWindow& W, int t) {
+// (parity: this call's; W.parity is unused by K2, which takes it by value)
+template <class WT>
+__device__ __forceinline__ int direct_window_base(const WT& W, int parity, int t) {
     const long long ns = (long long)uload(W.fsamp, t + 1) - uload(W.fsamp, t);
-    const unsigned long long ssum = uload(W.dres, kDresSpanSum + 2 * W.parity);
-    const unsigned long long scnt = uload(W.dres, kDresSpanCnt + 2 * W.parity);
+    const unsigned long long ssum = uload(W.dres, kDresSpanSum + 2 * parity);
+    const unsigned long long scnt = uload(W.dres, kDresSpanCnt + 2 * parity);
     if (ns <= 0 || scnt == 0) return 0;
     const double mean = (double)ssum / (double)scnt;
     const double bases = (double)ns * (double)kProbeStride * mean;
@@ -1290,8 +1292,8 @@ struct ReadArrays {
 // those are the next chunk's reads, which another workgroup, usually on
 // another XCD, fetches again (PMC: the overshoot was most of K2's 21-39 %
 // fetch excess over its algorithmic bytes).
-template <bool kDirect>
-__device__ __forceinline__ void issue_raw(RawBatch<kDirect>& r, int64_t base, const ReadArrays& A,
+template <bool kDirect, class AT>
+__device__ __forceinline__ void issue_raw(RawBatch<kDirect>& r, int64_t base, const AT& A,
                                           int64_t cend) {
     const int64_t i0 = base + (int64_t)threadIdx.x * kReadsPerThread;
     if constexpr (kDirect) {
@@ -1349,8 +1351,8 @@ struct DirectArgs {
     const int64_t* len;                // [nc] contig lengths (= extents on this path)
     int32_t nc;
     unsigned long long* dres;
-    unsigned long long gen;
-    DirectWindow win;                  // the fused regions' window bases (direct_window_base)
+    DirectWindow win;                  // the fused regions' window bases (direct_window_base; its
+                                       // parity is K2's win_parity argument)
 };
 
 struct DirectChunk {                   // wave-uniform per chunk
@@ -1370,10 +1372,11 @@ struct DirectAcc {                     // per-lane verdict
 // checks of the reads in [vlo, vhi): range, order against the predecessor
 // (the neighbouring lane's last read; lane 0 loads its own by scalar loads),
 // overhang, span.
+template <class DT>
 __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch<true>& r, int64_t base,
                                                     int64_t C0, int64_t chunk_w, const DirectChunk& dc,
-                                                    const ReadArrays& A, const int64_t* __restrict__ coff,
-                                                    const DirectArgs& D, int short_max, DirectAcc& acc) {
+                                                    const int64_t* __restrict__ coff,
+                                                    const DT& D, int short_max, DirectAcc& acc) {
     const int lane4 = (int)threadIdx.x * kReadsPerThread;   // this lane's first read, relative to base
     const int tt[4] = {r.t.x, r.t.y, r.t.z, r.t.w};
     const int pp[4] = {r.p.x, r.p.y, r.p.z, r.p.w};
@@ -1467,7 +1470,8 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
 // read failed a check).  The aligned bases are not counted here: summing
 // the spans cost 0.03 ms of a C3 launch for a figure few callers ask for
 // (span_sum_kernel computes it on request).
-__device__ __forceinline__ void direct_flush(const DirectAcc& a, const DirectArgs& D, int* red) {
+template <class DT>
+__device__ __forceinline__ void direct_flush(const DirectAcc& a, const DT& D, int* red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned f = a.flags;
     int m = a.max_span;
@@ -1734,8 +1738,8 @@ __device__ __forceinline__ void load_events(EvBatch& e, const int32_t* __restric
 // into the region's global accumulator and flushes the LDS histogram.
 // kBarriers = false: the caller has just passed a barrier after the last
 // atomics, and a barrier follows before the histogram is used again.
-template <bool kBarriers, class HC>
-__device__ __forceinline__ void flush_region(const FusedRegions& R, int id, unsigned* h, OvLds* ov) {
+template <bool kBarriers, class HC, class RT>
+__device__ __forceinline__ void flush_region(const RT& R, int id, unsigned* h, OvLds* ov) {
     // id: the region's row, loaded with its other fields (no scalar load on
     // the chunk end's path)
     if (kBarriers) __syncthreads();   // every wave's histogram and overflow atomics are in
@@ -1788,18 +1792,35 @@ __device__ __forceinline__ int take_chunk(unsigned* queue, int64_t n_chunks) {
 // probe's J arrays, the reads are loaded as raw (tid, pos, span), and K2
 // validates them (probe_kernel); otherwise the chunk index and the packed
 // read words of ingest_kernel.
+// K2's pointer arguments that change only when buffers or the region set do,
+// in device memory (engine.hip uploads a copy when they change): read at
+// their uses by scalar loads from constant memory instead of being kernel
+// arguments, which the compiler held in SGPRs for the whole launch and
+// spilled (74 SGPRs into VGPR lanes on the direct fused variant: 34
+// v_readlane per read batch in the apply loop reloading the read array
+// pointers; 35 spills and none in that loop this way).
+struct K2Consts {
+    ReadArrays A;
+    FusedRegions R;
+    DirectArgs D;
+};
+
 template <bool kStats, bool kLong, bool kDirect>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
 __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
                                                  : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
-depth_kernel(ReadArrays A, int64_t n,
+depth_kernel(const K2Consts* __restrict__ K, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
              int cstride, int64_t n_chunks, int tiles_per_chunk, int short_max,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
              const int* __restrict__ chunk_carry,
              int32_t* __restrict__ depth, unsigned* __restrict__ queue,
-             int* __restrict__ max_depth, FusedRegions R, DirectArgs D) {
+             int* __restrict__ max_depth, unsigned long long gen, int win_parity) {
     static_assert(!(kDirect && kLong), "the direct path has no long reads");
+    const auto& KC = *(const __attribute__((address_space(4))) K2Consts*)K;
+    const auto& A = KC.A;
+    const auto& R = KC.R;
+    const auto& D = KC.D;
     extern __shared__ __attribute__((aligned(16))) int lds[];
     // [0] chunk id, [4..7] wave totals, [8..11] wave max, [12..13] block_all votes
     int* hdr = lds;
@@ -1826,7 +1847,7 @@ depth_kernel(ReadArrays A, int64_t n,
     // re-runs this batch through the full prepare; nothing to do here.
     if (kDirect) {
         const unsigned long long f0 = uload(D.dres, kDresBadSample), f1 = uload(D.dres, kDresLongSample);
-        if (f0 == D.gen || f1 == D.gen) return;
+        if (f0 == gen || f1 == gen) return;
     }
     int my_max = 0;
     DirectAcc dacc;            // kDirect: this lane's validation counters
@@ -1894,7 +1915,7 @@ depth_kernel(ReadArrays A, int64_t n,
                 r_gs = uload(R.gs, rcur);
                 r_ge = uload(R.ge, rcur);
                 r_id = uload(R.id, rcur);
-                r_base = kDirect ? direct_window_base(D.win, uload(R.rtid, r_id)) : uload(R.base, rcur);
+                r_base = kDirect ? direct_window_base(D.win, win_parity, uload(R.rtid, r_id)) : uload(R.base, rcur);
             }
         }
         int64_t base = cfirst & ~(int64_t)(kReadsPerThread - 1);
@@ -1904,7 +1925,7 @@ depth_kernel(ReadArrays A, int64_t n,
         b.pending = 0;
         auto finish = [&](const RawBatch<kDirect>& r, int64_t at) {
             if constexpr (kDirect)
-                finish_batch_direct(b, r, at, C0, chunk_w, dc, A, coff, D, short_max, dacc);
+                finish_batch_direct(b, r, at, C0, chunk_w, dc, coff, D, short_max, dacc);
             else
                 finish_batch(b, r, at, cend, C0, cfirst);
         };
@@ -2069,7 +2090,7 @@ depth_kernel(ReadArrays A, int64_t n,
                             r_gs = uload(R.gs, rcur);
                             r_ge = uload(R.ge, rcur);
                             r_id = uload(R.id, rcur);
-                            r_base = kDirect ? direct_window_base(D.win, uload(R.rtid, r_id))
+                            r_base = kDirect ? direct_window_base(D.win, win_parity, uload(R.rtid, r_id))
                                              : uload(R.base, rcur);
                         }
                     } else {
@@ -2572,7 +2593,8 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     const long long n = n_total[r];
     const long long zx = n_zero_extra[r];
     // (direct path: the window K2 used, from the probe's samples)
-    const long long base = rtid ? direct_window_base(dwin, __builtin_amdgcn_readfirstlane(rtid[r])) : base_of[r];
+    const long long base = rtid ? direct_window_base(dwin, dwin.parity, __builtin_amdgcn_readfirstlane(rtid[r]))
+                                : base_of[r];
     const long long zx_bin = base == 0 ? zx : 0;
     const long long low = (long long)low_of[r] + (base == 0 ? 0 : zx);
     const long long r_lo = (n - 1) / 2, r_hi = n / 2;

@@ -1,0 +1,38 @@
+#!/bin/bash
+# One GPU-box session of several steps, each under its own time limit; a
+# fault / abort / time limit ends the session (exit codes 0-1 continue).
+#   STEPS="tests gz k2ab bench prof" TAG=r04d bash scripts/gpu_session.sh
+# tests: pytest -m gpu (PYTEST_SEL narrows it); gz: scripts/gz_ab.py over
+# GZ_VARIANTS; k2ab: scripts/gpu_ab_r04.sh with AB_LIBS / AB_RUNS; bench:
+# bench.py BENCH_ARGS; prof: scripts/profile.sh (PROF_TAG, BENCH_ARGS).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+export PYTHONUNBUFFERED=1
+TAG=${TAG:?set TAG}
+fatal() { case "$1" in 0|1) return 0 ;; *) echo "step $2: fatal status $1, stopping"; exit "$1" ;; esac; }
+faulted() { if grep -qiE "illegal memory access|memory access fault|hipErrorLaunchFailure|gpu hang" "$@" 2>/dev/null; then echo "GPU fault in $*: stopping"; exit 90; fi; }
+for step in ${STEPS:-tests}; do
+  case $step in
+    tests)
+      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_SEL:-tests} -m gpu -v --timeout 300 \
+          --timeout-method thread -p no:cacheprovider > "$O/${TAG}_pytest_gpu.log" 2>&1
+      s=$?; grep -E "passed|failed|error" "$O/${TAG}_pytest_gpu.log" | tail -8; faulted "$O/${TAG}_pytest_gpu.log"; fatal $s tests ;;
+    gz)
+      timeout -k 10 ${GZ_TIMEOUT:-500} python -u scripts/gz_ab.py --reads ${GZ_READS:-10000000} --reps ${GZ_REPS:-3} \
+          ${GZ_VARIANTS:?} > "$O/${TAG}_gz_ab.txt" 2>&1
+      s=$?; grep -v "^{" "$O/${TAG}_gz_ab.txt" | tail -24; faulted "$O/${TAG}_gz_ab.txt"; fatal $s gz ;;
+    k2ab)
+      TAG=${TAG}_k2 bash "$R/scripts/gpu_ab_r04.sh"; s=$?; fatal $s k2ab ;;
+    bench)
+      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > "$O/${TAG}_bench.log" 2>&1
+      s=$?; tail -1 "$O/${TAG}_bench.log" | cut -c1-400; faulted "$O/${TAG}_bench.log"; fatal $s bench ;;
+    smoke)
+      timeout -k 10 240 python __graft_entry__.py smoke > "$O/${TAG}_smoke.log" 2>&1
+      s=$?; tail -2 "$O/${TAG}_smoke.log"; faulted "$O/${TAG}_smoke.log"; fatal $s smoke ;;
+    prof)
+      TAG=${PROF_TAG:?} bash "$R/scripts/profile.sh"; s=$?; fatal $s prof ;;
+  esac
+done
+exit 0
