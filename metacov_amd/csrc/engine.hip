@@ -190,6 +190,7 @@ struct mc_ctx {
     DevBuf<int32_t> d_jidx;               // [2 * (n_base + 1)]: J(k w), J(k w - halo)
     DevBuf<int32_t> d_fsamp;              // [nc + 1] first sample of each contig
     DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
+    DevBuf<uint32_t> d_endw;              // ingest_kernel<true>'s end words (long_fill_words_kernel)
     // K2's constant arguments (K2Consts), a few variants resident at once:
     // each launch finds its bytes in a slot or uploads them into the next one
     static constexpr int kK2Slots = 4;
@@ -360,6 +361,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_jidx.release();
     ctx->d_fsamp.release();
     ctx->d_dres.release();
+    ctx->d_endw.release();
     ctx->d_k2c.release();
     ctx->h_k2c.release();
     ctx->d_tile_cnt.release();
@@ -785,6 +787,8 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
     // they are queued behind ingest before its results are read (speculative:
     // unused if the batch has no long reads, redone if the extents grow), so
     // the host's round trip overlaps them.
+    // end words (ingest's per-read end events) when global ends fit 32 bits
+    bool end_words = false;
     auto launch_long = [&](bool counted) -> int {
         const int64_t alloc_len = ctx->n_chunks * ctx->chunk_w;
         const int64_t n_tiles = ctx->n_chunks * ctx->tiles_per_chunk;
@@ -822,8 +826,12 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(long_scan_final_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
-                           ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        if (counted && end_words)
+            hipLaunchKernelGGL(long_fill_words_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_endw.p, n,
+                               G.per, G.lcw, ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        else
+            hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
+                               ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
         HIP_TRY(hipGetLastError());
         return MC_OK;
     };
@@ -854,9 +862,11 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         }
         if (n) {
             HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kBatch)));   // whole-batch loads
+            end_words = count_long && ctx->n_chunks * ctx->chunk_w < (int64_t)0xffffffffll;
+            if (end_words) HIP_TRY(ctx->d_endw.reserve((size_t)(n + kBatch)));
             IngestIndex ix{ctx->d_coff.p, base_lw(ctx), ctx->short_max, n_base, ctx->d_chunk_first.p,
                            count_long ? ctx->d_tile_cnt.p : nullptr, count_long ? ctx->d_chunk_carry.p : nullptr,
-                           ctx->n_chunks * ctx->chunk_w, lcw};
+                           ctx->n_chunks * ctx->chunk_w, lcw, end_words ? ctx->d_endw.p : nullptr};
             const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 4 * kBlock - 1) / (4 * kBlock),
                                                                       igrid));
             if (count_long)

@@ -775,6 +775,39 @@ def test_invalidate_reprepares_same_reads(eng):
     assert eng.aligned_bases() == int(span.astype(np.int64).sum())
 
 
+def test_long_reads_reprepare_end_words(eng):
+    """Long reads through the full prepare, three times: the first pass counts
+    the end events with long_count_kernel and fills the buckets from the
+    tuples; later passes (the contig set had long reads) count inside ingest
+    and fill from ingest's per-read end words.  Depth and rows equal the
+    oracle's every time, including ends on chunk starts and past the extents."""
+    lengths = [500_000, 300_000, 7, 131_072]
+    rng = np.random.default_rng(91)
+    n = 200_000
+    t = np.sort(rng.choice(4, size=n, p=[0.5, 0.3, 0.0, 0.2])).astype(np.int32)
+    span = rng.integers(4_000, 30_000, size=n)
+    L = np.asarray(lengths)[t]
+    pos = (rng.random(n) * (L + 1000)).astype(np.int64)          # some run past their contig
+    pos = np.minimum(pos, L - 1)
+    span[::97] = (32768 - pos[::97] % 32768)                    # ends exactly on chunk starts
+    span = np.maximum(span, 1).astype(np.int32)
+    pos = pos.astype(np.int32)
+    o = np.lexsort((pos, t))
+    t, pos, span = t[o], pos[o], span[o]
+    d, ext, coff = coracle.depth(lengths, t, pos, span)
+    regs = (np.arange(4, dtype=np.int32), np.zeros(4, np.int64), np.asarray(lengths, np.int64) + 500)
+    want = coracle.region_stats(d, ext, coff, *regs)
+    eng.set_contigs(lengths)
+    eng.add_reads(t, pos, span)
+    for k in range(3):
+        eng.invalidate()
+        got = eng.compute_depth_stats(*regs)
+        for f in want.dtype.names:
+            assert np.array_equal(got[f], want[f]), (k, f)
+        for c in range(4):
+            assert np.array_equal(eng.depth(c, 0, int(ext[c])), d[coff[c]:coff[c] + ext[c]]), (k, c)
+
+
 def test_new_batch_same_layout_moves_windows(eng):
     """A second batch over the same contigs and regions keeps the staged
     region table (same layout) but must move the histogram windows to the
