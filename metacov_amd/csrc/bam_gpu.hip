@@ -428,7 +428,7 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     int64_t first = 0;
     SegRes* R = g->hres.p;
     for (int round = 0;; ++round) {
-        if (round == 16) {   // bounded: the rest becomes one segment walked by one lane
+        if (round == 32) {   // bounded: the rest becomes one segment walked by one lane
             for (int64_t j = first + 1; j < nseg; ++j) seg[j] = n;
         }
         std::memcpy(h, seg.data() + first, (nseg + 1 - first) * 8);
@@ -440,14 +440,19 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
         HIP_TRY(hipMemcpyAsync(R + first, g->res.p + first, (nseg - first) * sizeof(SegRes),
                                hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        // Every inconsistent landing is applied in one round.  Only the chain
-        // up to the first one is verified (`exact`): later walks may have
-        // started at a false sync, so their errors are not reported, and
-        // their landings are hints the next round re-checks.  The verified
-        // prefix grows every round, so the rounds end.
+        // Every inconsistent landing is applied in one round, but only from a
+        // walk whose start this round has not moved (a moved start's walk is
+        // stale: comparing it with its successor cascaded into a "fix" of
+        // every later segment, 390 k resyncs and the one-lane fallback on a
+        // 2.75 GB stream).  Only the chain up to the first fix is verified
+        // (`exact`): later walks may have started at a false sync, so their
+        // errors are not reported, and their landings are hints the next round
+        // re-checks.  The verified prefix grows every round, so the rounds end.
         int64_t redo = -1;
+        int64_t moved_upto = -1;   // segments <= this one had their start moved this round
         bool exact = true;
         for (int64_t i = first; i < nseg; ++i) {
+            if (i <= moved_upto) continue;
             const SegRes& r = R[i];
             const int64_t end = seg[i + 1];
             if (r.err && !exact) break;
@@ -470,11 +475,13 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
                 return MC_E_IO;
             }
             if (r.landing != end) {   // segment i+1's sync was a false positive
+                int64_t j = i + 1;
                 if (r.landing > end) {
-                    for (int64_t j = i + 1; j < nseg && seg[j] < r.landing; ++j) seg[j] = r.landing;
+                    for (; j < nseg && seg[j] < r.landing; ++j) seg[j] = r.landing;
                 } else {
-                    seg[i + 1] = r.landing;   // (only after an unverified walk: the next round checks)
+                    seg[j++] = r.landing;   // (a walk lands at or past its end: not reached)
                 }
+                moved_upto = j - 1;
                 ++g->resyncs;
                 if (redo < 0) redo = i + 1;
                 exact = false;

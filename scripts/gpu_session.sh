@@ -25,9 +25,10 @@ for step in ${STEPS:-tests}; do
       s=$?; grep -v "^{" "$O/${TAG}_gz_ab.txt" | tail -24; faulted "$O/${TAG}_gz_ab.txt"; fatal $s gz ;;
     k2ab)
       TAG=${TAG}_k2 bash "$R/scripts/gpu_ab_r04.sh"; s=$?; fatal $s k2ab ;;
-    bench)
-      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > "$O/${TAG}_bench.log" 2>&1
-      s=$?; tail -1 "$O/${TAG}_bench.log" | cut -c1-400; faulted "$O/${TAG}_bench.log"; fatal $s bench ;;
+    bench|bench_c2|bench_c5)
+      cfg=""; [ $step = bench_c2 ] && cfg="--config c2"; [ $step = bench_c5 ] && cfg="--config c5 --no-cpu-baseline"
+      timeout -k 10 300 python bench.py $cfg ${BENCH_ARGS:-} > "$O/${TAG}_${step}.log" 2>&1
+      s=$?; tail -1 "$O/${TAG}_${step}.log" | cut -c1-300; faulted "$O/${TAG}_${step}.log"; fatal $s $step ;;
     smoke)
       timeout -k 10 240 python __graft_entry__.py smoke > "$O/${TAG}_smoke.log" 2>&1
       s=$?; tail -2 "$O/${TAG}_smoke.log"; faulted "$O/${TAG}_smoke.log"; fatal $s smoke ;;

@@ -208,6 +208,9 @@ def test_gpu_decode_large(lib_built, tmp_path, level, window):
     assert t["blocks"] > 100 and t["inflated_bytes"] > 0
     if window:
         assert t["windows"] > 1
+    # false syncs are rare and each is fixed once (a stale-walk cascade once
+    # made every later segment a "resync" and fell back to a one-lane walk)
+    assert t["resyncs"] <= 64, t["resyncs"]
     g.close()
 
 
