@@ -92,7 +92,7 @@ enum : int32_t {
 constexpr int kGzLanes = MC_GZ_LANES;
 constexpr int kGzThreads = 64;
 constexpr int64_t kGzSlotWords = mc::gz::kScratchWords;
-constexpr int kGzLdsWords = mc::gz::kPrimaryWords + mc::gz::kSymWords + 2 * mc::gz::kRingWords;
+constexpr int kGzLdsWords = mc::gz::kPrimaryWords + mc::gz::kSymWords + 2 * mc::gz::kRingWords + 4 * mc::gz::kQueue;
 constexpr int kGzWavesPerCu = MC_GZ_WAVES_PER_CU > 0 ? MC_GZ_WAVES_PER_CU
                                                      : (160 << 10) / (kGzLanes * kGzLdsWords * 2);
 static_assert(kGzWavesPerCu >= 1, "inflate LDS per wave exceeds a CU");
@@ -114,9 +114,14 @@ gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ 
     using lds_u32 = __attribute__((address_space(3))) uint32_t;
     static_assert((mc::gz::kPrimaryWords + mc::gz::kSymWords) % 2 == 0 && kGzLdsWords % 2 == 0, "ring alignment");
     lds_u32* ring = (lds_u32*)(SD + mc::gz::kDistSyms);
+    using lds_u64 = __attribute__((address_space(3))) uint64_t;
+    static_assert((mc::gz::kPrimaryWords + mc::gz::kSymWords + 2 * mc::gz::kRingWords) % 4 == 0 &&
+                      kGzLdsWords % 4 == 0, "queue alignment");
+    lds_u64* queue = (lds_u64*)(ring + mc::gz::kRingWords);
     for (int64_t b = lane; b < nblk; b += lanes) {
         const GzBlock g = blk[b];
-        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, SL, SD, ring);
+        const int rc = mc::gz::inflate_block(comp + g.cdata, g.clen, out + g.out, g.isize, S, TL, TD, SL, SD, ring,
+                                             queue);
         status[b] = rc;
         if (rc) atomicOr(any_err, 1);
     }
@@ -1050,8 +1055,9 @@ extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst
     uint16_t* TL = scratch.data() + mc::gz::kScratchWords;
     uint16_t* SL = TL + mc::gz::kPrimaryWords;
     uint32_t ring[mc::gz::kRingWords];
+    uint64_t queue[mc::gz::kQueue];
     const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data(), TL,
-                                         TL + (1 << mc::gz::kLitBits), SL, SL + mc::gz::kLitSyms, ring);
+                                         TL + (1 << mc::gz::kLitBits), SL, SL + mc::gz::kLitSyms, ring, queue);
     MC_REQUIRE(rc == 0, MC_E_IO, "inflate failed: %s", gz_err_msg(rc));
     return MC_OK;
 }

@@ -1169,7 +1169,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     if (int rc = k2_consts(ctx, kc, &dk)) return rc;
     const int win_parity = (int)(ctx->direct_gen & 1);
 #define MC_LAUNCH_K2(S, L, D)                                                                  \
-    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, dk,          \
+    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, kc.A, dk,    \
                        ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p,        \

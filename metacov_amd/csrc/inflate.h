@@ -28,7 +28,7 @@ namespace gz {
 #define MC_HD __host__ __device__ __forceinline__
 
 #ifndef MC_GZ_QUEUE
-#define MC_GZ_QUEUE 16          // matches a lane defers (0: copy each at once)
+#define MC_GZ_QUEUE 16          // matches a lane defers (>= 1)
 #endif
 #ifndef MC_GZ_COPY_BATCH
 #define MC_GZ_COPY_BATCH 1
@@ -94,12 +94,17 @@ constexpr int kRingFill = kRingWords / 2;         // words per top-up (a multipl
 constexpr int kRingLow = 4;                       // a lane below this many words calls the top-up
 static_assert((kRingWords & (kRingWords - 1)) == 0 && kRingWords >= 8, "ring: power of two >= 8 words");
 
-// the ring's pointer type for a table pointer type (LDS-qualified or plain)
+// the ring's and the match queue's pointer types for a table pointer type
+// (LDS-qualified or plain)
 template <class TP> struct RingOf;
-template <> struct RingOf<uint16_t*> { using type = uint32_t*; };
+template <> struct RingOf<uint16_t*> {
+    using type = uint32_t*;
+    using queue = uint64_t*;
+};
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
 template <> struct RingOf<__attribute__((address_space(3))) uint16_t*> {
     using type = __attribute__((address_space(3))) uint32_t*;
+    using queue = __attribute__((address_space(3))) uint64_t*;
 };
 #endif
 
@@ -228,45 +233,74 @@ MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint1
     return kOk;
 }
 
-// RFC 1951 §3.2.2 walk over the code lengths (codes longer than the table,
-// and patterns the table does not hold): -1 when the bits are no code.  The
-// counts per length are registers (loaded once per table): walked from
-// memory, each length was a dependent global load, and with the walk
-// divergent some lane of the wave took it at most symbol steps.
-template <class TP>
-MC_HD int decode_slow(uint64_t bits, const int (&cnt)[16], TP sym, int* used) {
-    int code = 0, first = 0, index = 0, found = -1, len = 0;
+// RFC 1951 §3.2.2 walk over the code lengths, for the codes longer than the
+// primary table's TB bits (the table holds every code of up to TB bits, so
+// the walk starts at length TB + 1 from the canonical state there: 15 - TB
+// unrolled steps instead of 15, the whole wave running them whenever one
+// lane meets a long code): -1 when the bits are no code.  The per-length
+// counts and that state are registers (loaded once per table): walked from
+// memory, each length was a dependent global load.
+struct CodeRegs {
+    int cnt[16];
+    int first, index;                  // canonical first code / codes before, at length TB + 1
+};
+
+template <int TB>
+MC_HD void load_code(const uint16_t* S, int cnt_off, CodeRegs& R) {
 #pragma unroll
-    for (int l = 1; l < 16; ++l) {
-        code |= (int)((bits >> (l - 1)) & 1u);
-        const int count = cnt[l];
+    for (int l = 0; l < 16; ++l) R.cnt[l] = S[cnt_off + l];
+    int first = 0, index = 0;
+#pragma unroll
+    for (int l = 1; l <= TB; ++l) {
+        index += R.cnt[l];
+        first = (first + R.cnt[l]) << 1;
+    }
+    R.first = first;
+    R.index = index;
+}
+
+MC_HD uint32_t bitrev32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bitreverse32(x);
+#else
+    x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+    x = ((x >> 8) & 0x00FF00FFu) | ((x & 0x00FF00FFu) << 8);
+    return (x >> 16) | (x << 16);
+#endif
+}
+
+template <int TB, class TP>
+MC_HD int decode_slow(uint64_t bits, const CodeRegs& R, TP sym, int* used) {
+    // the TB-bit prefix as a canonical code (first bit most significant)
+    int code = (int)(bitrev32((uint32_t)bits) >> (32 - TB));
+    int first = R.first, index = R.index, found = -1, len = 0;
+#pragma unroll
+    for (int l = TB + 1; l < 16; ++l) {
+        code = (code << 1) | (int)((bits >> (l - 1)) & 1u);
+        const int count = R.cnt[l];
         if (found < 0 && code - count < first) {
             found = index + (code - first);
             len = l;
         }
         index += count;
         first = (first + count) << 1;
-        code <<= 1;
     }
     if (found < 0) return -1;
     *used = len;
     return sym[found];
 }
 
-MC_HD void load_counts(const uint16_t* S, int cnt_off, int (&cnt)[16]) {
-#pragma unroll
-    for (int l = 0; l < 16; ++l) cnt[l] = S[cnt_off + l];
-}
-
-template <class TP, class RP>
-MC_HD int decode_sym(Bits<RP>& b, TP T, int tb, const int (&cnt)[16], TP sym) {
-    const uint16_t e = T[(uint32_t)b.buf & ((1u << tb) - 1u)];
+template <int TB, class TP, class RP>
+MC_HD int decode_sym(Bits<RP>& b, TP T, const CodeRegs& R, TP sym) {
+    const uint16_t e = T[(uint32_t)b.buf & ((1u << TB) - 1u)];
     int used, s;
     if (e) {
         used = e & 15;
         s = e >> 4;
     } else {
-        s = decode_slow(b.buf, cnt, sym, &used);
+        s = decode_slow<TB>(b.buf, R, sym, &used);
         if (s < 0) return -1;
     }
     b.buf >>= used;
@@ -295,13 +329,13 @@ MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     // the code length code (<= 7 bits) goes through the literal table's slots
     int rc = build_code(S, TL, 7, kLitCnt, SL, lens, 19);
     if (rc) return rc;
-    int ccnt[16];
-    load_counts(S, kLitCnt, ccnt);
+    CodeRegs ccode;
+    load_code<7>(S, kLitCnt, ccode);
     int idx = 0;
     while (idx < nlen + ndist) {
         bits_topup(b);
         bits_refill(b);
-        const int sym = decode_sym(b, TL, 7, ccnt, SL);
+        const int sym = decode_sym<7>(b, TL, ccode, SL);
         if (sym < 0) return kErrCodes;
         if (sym < 16) {
             lens[idx++] = (uint16_t)sym;
@@ -369,20 +403,24 @@ MC_HD void lz_copy(uint8_t* q, int len, int dist) {
 // the wave has one at almost every symbol step (6 % of symbols are matches,
 // 1 - 0.94^64 = 98 %), so every step waited a memory round trip.  Queued, the
 // copies of all lanes run together when some lane's queue is full (a wave
-// vote), then at the block end.  The queue is registers (entries selected
-// by unrolled compares, no dynamic register indexing).
+// vote), then at the block end.  The queue is the lane's kQueue u64 slots in
+// LDS (a push is one ds_write; in registers, an entry selected by unrolled
+// compares cost 3 x kQueue VALU per push, which every step with some lane
+// matching paid), and the flush loops over the entries at run time.
+constexpr int kQueue = MC_GZ_QUEUE;
+static_assert(kQueue >= 1, "match queue: >= 1 entry");
+
+template <class QP>
 struct MatchQueue {
-    uint64_t e[MC_GZ_QUEUE > 0 ? MC_GZ_QUEUE : 1];   // offset << 32 | dist << 9 | len
+    QP e;                              // [kQueue] offset << 32 | dist << 9 | len
     int n;
 };
 
-MC_HD void mq_flush(MatchQueue& q, uint8_t* dst) {
-#pragma unroll
-    for (int j = 0; j < (MC_GZ_QUEUE > 0 ? MC_GZ_QUEUE : 1); ++j) {
-        if (j < q.n) {
-            const uint64_t e = q.e[j];
-            lz_copy(dst + (uint32_t)(e >> 32), (int)(e & 511u), (int)((uint32_t)e >> 9));
-        }
+template <class QP>
+MC_HD void mq_flush(MatchQueue<QP>& q, uint8_t* dst) {
+    for (int j = 0; j < q.n; ++j) {
+        const uint64_t e = q.e[j];
+        lz_copy(dst + (uint32_t)(e >> 32), (int)(e & 511u), (int)((uint32_t)e >> 9));
     }
     q.n = 0;
 }
@@ -399,12 +437,11 @@ MC_HD void mq_flush(MatchQueue& q, uint8_t* dst) {
 // trip whose vmcnt wait also drained the lane's output stores).
 template <class TP>
 MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S, TP TL, TP TD,
-                        TP SL, TP SD, typename RingOf<TP>::type ring) {
+                        TP SL, TP SD, typename RingOf<TP>::type ring, typename RingOf<TP>::queue queue) {
     if (isize == 0) return kOk;
-#if MC_GZ_QUEUE
-    MatchQueue mq;
+    MatchQueue<typename RingOf<TP>::queue> mq;
+    mq.e = queue;
     mq.n = 0;
-#endif
     Bits<typename RingOf<TP>::type> b;
     b.ring = ring;
     bits_init(b, src, 0, clen);
@@ -432,19 +469,17 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
         } else {
             const int rc = type == 1 ? read_fixed(S, TL, TD, SL, SD) : read_dynamic(b, S, TL, TD, SL, SD);
             if (rc) return rc;
-            int lcnt[16], dcnt[16];
-            load_counts(S, kLitCnt, lcnt);
-            load_counts(S, kDistCnt, dcnt);
+            CodeRegs lcode, dcode;
+            load_code<kLitBits>(S, kLitCnt, lcode);
+            load_code<kDistBits>(S, kDistCnt, dcode);
             for (;;) {
-#if MC_GZ_QUEUE
                 // all lanes still in a symbol loop vote: one full queue
                 // flushes every lane's (at most one push per iteration)
-                if (wave_any(mq.n == MC_GZ_QUEUE)) mq_flush(mq, dst);
-#endif
+                if (wave_any(mq.n == kQueue)) mq_flush(mq, dst);
                 if (bits_pos(b) > limit_bits) return kErrInput;
                 bits_topup(b);   // (a symbol with its distance takes <= 2 words)
                 bits_refill(b);
-                int s = decode_sym(b, TL, kLitBits, lcnt, SL);
+                int s = decode_sym<kLitBits>(b, TL, lcode, SL);
                 if (s < 0) return kErrSymbol;
                 if (s < 256) {
                     if (o >= isize) return kErrOutput;
@@ -464,7 +499,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                     len = ((4 + (s & 3)) << e) + 3 + (int)bits_take(b, e);
                 }
                 bits_refill(b);
-                const int d = decode_sym(b, TD, kDistBits, dcnt, SD);
+                const int d = decode_sym<kDistBits>(b, TD, dcode, SD);
                 if (d < 0 || d >= 30) return kErrSymbol;
                 int dist;
                 if (d < 4) {
@@ -475,25 +510,14 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                 }
                 if ((int64_t)dist > o) return kErrDistance;
                 if (o + len > isize) return kErrOutput;
-#if MC_GZ_QUEUE
-                {
-                    const uint64_t e = ((uint64_t)o << 32) | ((uint32_t)dist << 9) | (uint32_t)len;
-#pragma unroll
-                    for (int j = 0; j < MC_GZ_QUEUE; ++j) mq.e[j] = j == mq.n ? e : mq.e[j];
-                    ++mq.n;
-                }
-#else
-                lz_copy(dst + o, len, dist);
-#endif
+                mq.e[mq.n++] = ((uint64_t)o << 32) | ((uint32_t)dist << 9) | (uint32_t)len;
                 o += len;
             }
         }
         if (bits_pos(b) > limit_bits) return kErrInput;
         if (final) break;
     }
-#if MC_GZ_QUEUE
     mq_flush(mq, dst);
-#endif
     return o == isize ? kOk : kErrSize;
 }
 

@@ -1902,7 +1902,7 @@ template <bool kStats, bool kLong, bool kDirect>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
 __global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
                                                  : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
-depth_kernel(const K2Consts* __restrict__ K, int64_t n,
+depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
              int cstride, int64_t n_chunks, int tiles_per_chunk, int short_max,
              const int64_t* __restrict__ tile_ev_off, const int32_t* __restrict__ tile_ev,
@@ -1911,7 +1911,6 @@ depth_kernel(const K2Consts* __restrict__ K, int64_t n,
              int* __restrict__ max_depth, unsigned long long gen, int win_parity) {
     static_assert(!(kDirect && kLong), "the direct path has no long reads");
     const auto& KC = *(const __attribute__((address_space(4))) K2Consts*)K;
-    const auto& A = KC.A;
     const auto& R = KC.R;
     const auto& D = KC.D;
     extern __shared__ __attribute__((aligned(16))) int lds[];
