@@ -233,30 +233,35 @@ MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint1
     return kOk;
 }
 
-// RFC 1951 §3.2.2 walk over the code lengths, for the codes longer than the
-// primary table's TB bits (the table holds every code of up to TB bits, so
-// the walk starts at length TB + 1 from the canonical state there: 15 - TB
-// unrolled steps instead of 15, the whole wave running them whenever one
-// lane meets a long code): -1 when the bits are no code.  The per-length
-// counts and that state are registers (loaded once per table): walked from
-// memory, each length was a dependent global load.
+// Codes longer than the primary table's TB bits.  Canonical codes of length
+// l, left-aligned to 15 bits, fill the interval [lim[l-1], lim[l]) of the
+// 15-bit code space, one length after the other; so for the next 15 bits c
+// (first bit most significant) the length is TB + 1 + the number of l in
+// [TB + 1, 14] with c >= lim[l], the symbol's canonical index is off[len] +
+// (c >> (15 - len)), and c >= lim[15] is no code (an incomplete code).  The
+// bounds and offsets are registers (built once per table); the search is
+// branch-free compares, since the whole wave runs it whenever one lane meets
+// a long code (round 3's 15-step RFC 1951 §3.2.2 count walk was 52 / 65
+// instructions for the literal / distance alphabets, this one about half).
+template <int TB>
 struct CodeRegs {
-    int cnt[16];
-    int first, index;                  // canonical first code / codes before, at length TB + 1
+    int lim[16 - TB];                  // lim[k]: bound of length TB + 1 + k (k = 0 .. 14 - TB)
+    int off[16 - TB];                  // off[k]: canonical index - (code >> shift) base of that length
 };
 
 template <int TB>
-MC_HD void load_code(const uint16_t* S, int cnt_off, CodeRegs& R) {
+MC_HD void load_code(const uint16_t* S, int cnt_off, CodeRegs<TB>& R) {
+    int first = 0, index = 0;          // canonical first code / codes before, at length l
 #pragma unroll
-    for (int l = 0; l < 16; ++l) R.cnt[l] = S[cnt_off + l];
-    int first = 0, index = 0;
-#pragma unroll
-    for (int l = 1; l <= TB; ++l) {
-        index += R.cnt[l];
-        first = (first + R.cnt[l]) << 1;
+    for (int l = 1; l <= 15; ++l) {
+        const int c = S[cnt_off + l];
+        if (l > TB) {
+            R.lim[l - TB - 1] = (first + c) << (15 - l);
+            R.off[l - TB - 1] = index - first;
+        }
+        index += c;
+        first = (first + c) << 1;
     }
-    R.first = first;
-    R.index = index;
 }
 
 MC_HD uint32_t bitrev32(uint32_t x) {
@@ -272,28 +277,23 @@ MC_HD uint32_t bitrev32(uint32_t x) {
 }
 
 template <int TB, class TP>
-MC_HD int decode_slow(uint64_t bits, const CodeRegs& R, TP sym, int* used) {
-    // the TB-bit prefix as a canonical code (first bit most significant)
-    int code = (int)(bitrev32((uint32_t)bits) >> (32 - TB));
-    int first = R.first, index = R.index, found = -1, len = 0;
+MC_HD int decode_slow(uint64_t bits, const CodeRegs<TB>& R, TP sym, int* used) {
+    const int c = (int)(bitrev32((uint32_t)bits) >> 17);   // the next 15 bits, first bit on top
+    int k = 0, off = R.off[0];
 #pragma unroll
-    for (int l = TB + 1; l < 16; ++l) {
-        code = (code << 1) | (int)((bits >> (l - 1)) & 1u);
-        const int count = R.cnt[l];
-        if (found < 0 && code - count < first) {
-            found = index + (code - first);
-            len = l;
-        }
-        index += count;
-        first = (first + count) << 1;
+    for (int j = 0; j < 14 - TB; ++j) {
+        const bool past = c >= R.lim[j];
+        k += past ? 1 : 0;
+        off = past ? R.off[j + 1] : off;
     }
-    if (found < 0) return -1;
+    if (c >= R.lim[14 - TB]) return -1;
+    const int len = TB + 1 + k;
     *used = len;
-    return sym[found];
+    return sym[off + (c >> (15 - len))];
 }
 
 template <int TB, class TP, class RP>
-MC_HD int decode_sym(Bits<RP>& b, TP T, const CodeRegs& R, TP sym) {
+MC_HD int decode_sym(Bits<RP>& b, TP T, const CodeRegs<TB>& R, TP sym) {
     const uint16_t e = T[(uint32_t)b.buf & ((1u << TB) - 1u)];
     int used, s;
     if (e) {
@@ -329,7 +329,7 @@ MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     // the code length code (<= 7 bits) goes through the literal table's slots
     int rc = build_code(S, TL, 7, kLitCnt, SL, lens, 19);
     if (rc) return rc;
-    CodeRegs ccode;
+    CodeRegs<7> ccode;
     load_code<7>(S, kLitCnt, ccode);
     int idx = 0;
     while (idx < nlen + ndist) {
@@ -469,7 +469,8 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
         } else {
             const int rc = type == 1 ? read_fixed(S, TL, TD, SL, SD) : read_dynamic(b, S, TL, TD, SL, SD);
             if (rc) return rc;
-            CodeRegs lcode, dcode;
+            CodeRegs<kLitBits> lcode;
+            CodeRegs<kDistBits> dcode;
             load_code<kLitBits>(S, kLitCnt, lcode);
             load_code<kDistBits>(S, kDistCnt, dcode);
             for (;;) {
