@@ -109,11 +109,12 @@ gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ 
     __shared__ uint16_t tabs[kGzLanes * kGzLdsWords];
     lds_u16* TL = (lds_u16*)(tabs + threadIdx.x * kGzLdsWords);
     lds_u16* TD = TL + (1 << mc::gz::kLitBits);
-    lds_u16* SL = TL + mc::gz::kPrimaryWords;
-    lds_u16* SD = SL + mc::gz::kLitSyms;
+    using lds_u8 = __attribute__((address_space(3))) uint8_t;
+    lds_u8* SL = (lds_u8*)(TL + mc::gz::kPrimaryWords);
+    lds_u8* SD = SL + mc::gz::kLitSyms;
     using lds_u32 = __attribute__((address_space(3))) uint32_t;
     static_assert((mc::gz::kPrimaryWords + mc::gz::kSymWords) % 2 == 0 && kGzLdsWords % 2 == 0, "ring alignment");
-    lds_u32* ring = (lds_u32*)(SD + mc::gz::kDistSyms);
+    lds_u32* ring = (lds_u32*)(TL + mc::gz::kPrimaryWords + mc::gz::kSymWords);
     using lds_u64 = __attribute__((address_space(3))) uint64_t;
     static_assert((mc::gz::kPrimaryWords + mc::gz::kSymWords + 2 * mc::gz::kRingWords) % 4 == 0 &&
                       kGzLdsWords % 4 == 0, "queue alignment");
@@ -1053,7 +1054,7 @@ extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst
     std::memcpy(padded.data(), src, (size_t)clen);
     std::vector<uint16_t> scratch(mc::gz::kScratchWords + kGzLdsWords);
     uint16_t* TL = scratch.data() + mc::gz::kScratchWords;
-    uint16_t* SL = TL + mc::gz::kPrimaryWords;
+    uint8_t* SL = reinterpret_cast<uint8_t*>(TL + mc::gz::kPrimaryWords);
     uint32_t ring[mc::gz::kRingWords];
     uint64_t queue[mc::gz::kQueue];
     const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data(), TL,

@@ -51,10 +51,14 @@ constexpr int kLitCnt = 0;                        // [16] codes per length
 constexpr int kDistCnt = kLitCnt + 16;            // [16]
 constexpr int kLens = kDistCnt + 16;              // [320] code lengths being read
 constexpr int kOffs = kLens + 320;                // [16] build temporary
-constexpr int kScratchWords = kOffs + 16;
-constexpr int kLitSyms = 288;                     // symbol lists in canonical order
+constexpr int kLitHi = kOffs + 16;                // [16] per length: canonical index of its first symbol >= 256
+constexpr int kScratchWords = kLitHi + 16;
+// symbol lists in canonical order, one byte per symbol: within one code
+// length the symbols are in increasing order, so the literal/length symbols
+// >= 256 of a length follow its literals, from the index kLitHi records
+constexpr int kLitSyms = 288;
 constexpr int kDistSyms = 32;
-constexpr int kSymWords = kLitSyms + kDistSyms;
+constexpr int kSymWords = (kLitSyms + kDistSyms) / 2;   // u16 words of both lists
 
 enum : int {
     kOk = 0,
@@ -100,11 +104,13 @@ template <class TP> struct RingOf;
 template <> struct RingOf<uint16_t*> {
     using type = uint32_t*;
     using queue = uint64_t*;
+    using sym = uint8_t*;
 };
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
 template <> struct RingOf<__attribute__((address_space(3))) uint16_t*> {
     using type = __attribute__((address_space(3))) uint32_t*;
     using queue = __attribute__((address_space(3))) uint64_t*;
+    using sym = __attribute__((address_space(3))) uint8_t*;
 };
 #endif
 
@@ -202,8 +208,8 @@ MC_HD uint32_t bitrev(uint32_t code, int len) {
 // the primary table of `tb` index bits.  Over-subscribed lengths are an
 // error; incomplete codes are accepted (their missing patterns fail in
 // decode_slow).
-template <class TP>
-MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint16_t* lens, int n) {
+template <class TP, class SP>
+MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, SP sym, const uint16_t* lens, int n) {
     uint16_t* cnt = S + cnt_off;
     uint16_t* offs = S + kOffs;
     for (int l = 0; l < 16; ++l) cnt[l] = 0;
@@ -215,9 +221,12 @@ MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint1
     }
     offs[1] = 0;
     for (int l = 1; l < 15; ++l) offs[l + 1] = (uint16_t)(offs[l] + cnt[l]);
+    const bool lit = n > 256;   // the literal/length alphabet (symbols >= 256 in a byte list: kLitHi)
     for (int s = 0; s < n; ++s) {
+        if (s == 256)
+            for (int l = 0; l < 16; ++l) S[kLitHi + l] = offs[l];
         const int l = lens[s] & 15;
-        if (l) sym[offs[l]++] = (uint16_t)s;
+        if (l) sym[offs[l]++] = (uint8_t)s;
     }
     const int size = 1 << tb;
     for (int i = 0; i < size; ++i) T[i] = 0;
@@ -225,7 +234,8 @@ MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint1
     int k = 0;
     for (int l = 1; l <= tb; ++l) {
         for (int c = 0; c < cnt[l]; ++c, ++k, ++code) {
-            const uint16_t e = (uint16_t)((sym[k] << 4) | l);
+            const int v = (int)sym[k] | (lit && k >= (int)S[kLitHi + l] ? 256 : 0);
+            const uint16_t e = (uint16_t)((v << 4) | l);
             for (uint32_t r = bitrev(code, l); r < (uint32_t)size; r += 1u << l) T[r] = e;
         }
         code <<= 1;
@@ -243,14 +253,18 @@ MC_HD int build_code(uint16_t* S, TP T, int tb, int cnt_off, TP sym, const uint1
 // branch-free compares, since the whole wave runs it whenever one lane meets
 // a long code (round 3's 15-step RFC 1951 §3.2.2 count walk was 52 / 65
 // instructions for the literal / distance alphabets, this one about half).
-template <int TB>
+// HI: the literal/length alphabet, whose symbols >= 256 are told apart in the
+// byte list by hi[k], the canonical index of the first of them at length
+// TB + 1 + k (kLitHi).
+template <int TB, bool HI>
 struct CodeRegs {
     int lim[16 - TB];                  // lim[k]: bound of length TB + 1 + k (k = 0 .. 14 - TB)
     int off[16 - TB];                  // off[k]: canonical index - (code >> shift) base of that length
+    int hi[HI ? 16 - TB : 1];
 };
 
-template <int TB>
-MC_HD void load_code(const uint16_t* S, int cnt_off, CodeRegs<TB>& R) {
+template <int TB, bool HI>
+MC_HD void load_code(const uint16_t* S, int cnt_off, CodeRegs<TB, HI>& R) {
     int first = 0, index = 0;          // canonical first code / codes before, at length l
 #pragma unroll
     for (int l = 1; l <= 15; ++l) {
@@ -258,6 +272,7 @@ MC_HD void load_code(const uint16_t* S, int cnt_off, CodeRegs<TB>& R) {
         if (l > TB) {
             R.lim[l - TB - 1] = (first + c) << (15 - l);
             R.off[l - TB - 1] = index - first;
+            if (HI) R.hi[l - TB - 1] = S[kLitHi + l];
         }
         index += c;
         first = (first + c) << 1;
@@ -276,31 +291,44 @@ MC_HD uint32_t bitrev32(uint32_t x) {
 #endif
 }
 
-template <int TB, class TP>
-MC_HD int decode_slow(uint64_t bits, const CodeRegs<TB>& R, TP sym, int* used) {
+// Keeps v a register value the compiler cannot fold into an address: a chain
+// of selects over a register array otherwise becomes a select of the array
+// index and one load, and the array moves to scratch (a private-memory round
+// trip whose vmcnt wait drains the lane's output stores too).
+MC_HD int opaque(int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(v));
+#endif
+    return v;
+}
+
+template <int TB, bool HI, class SP>
+MC_HD int decode_slow(uint64_t bits, const CodeRegs<TB, HI>& R, SP sym, int* used) {
     const int c = (int)(bitrev32((uint32_t)bits) >> 17);   // the next 15 bits, first bit on top
-    int k = 0, off = R.off[0];
+    int k = 0, off = R.off[0], hi = R.hi[0];
 #pragma unroll
     for (int j = 0; j < 14 - TB; ++j) {
         const bool past = c >= R.lim[j];
         k += past ? 1 : 0;
-        off = past ? R.off[j + 1] : off;
+        off = opaque(past ? R.off[j + 1] : off);
+        if (HI) hi = opaque(past ? R.hi[j + 1] : hi);
     }
     if (c >= R.lim[14 - TB]) return -1;
     const int len = TB + 1 + k;
     *used = len;
-    return sym[off + (c >> (15 - len))];
+    const int idx = off + (c >> (15 - len));
+    return (int)sym[idx] | (HI && idx >= hi ? 256 : 0);
 }
 
-template <int TB, class TP, class RP>
-MC_HD int decode_sym(Bits<RP>& b, TP T, const CodeRegs<TB>& R, TP sym) {
+template <int TB, bool HI, class TP, class SP, class RP>
+MC_HD int decode_sym(Bits<RP>& b, TP T, const CodeRegs<TB, HI>& R, SP sym) {
     const uint16_t e = T[(uint32_t)b.buf & ((1u << TB) - 1u)];
     int used, s;
     if (e) {
         used = e & 15;
         s = e >> 4;
     } else {
-        s = decode_slow<TB>(b.buf, R, sym, &used);
+        s = decode_slow<TB, HI>(b.buf, R, sym, &used);
         if (s < 0) return -1;
     }
     b.buf >>= used;
@@ -311,7 +339,8 @@ MC_HD int decode_sym(Bits<RP>& b, TP T, const CodeRegs<TB>& R, TP sym) {
 // Dynamic block header: code length code, then the literal/length and
 // distance code lengths (RFC 1951 §3.2.7), then both tables.
 template <class TP, class RP>
-MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
+MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, typename RingOf<TP>::sym SL,
+                       typename RingOf<TP>::sym SD) {
     bits_topup(b);
     bits_refill(b);
     const int nlen = (int)bits_take(b, 5) + 257;
@@ -329,13 +358,13 @@ MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
     // the code length code (<= 7 bits) goes through the literal table's slots
     int rc = build_code(S, TL, 7, kLitCnt, SL, lens, 19);
     if (rc) return rc;
-    CodeRegs<7> ccode;
-    load_code<7>(S, kLitCnt, ccode);
+    CodeRegs<7, false> ccode;
+    load_code<7, false>(S, kLitCnt, ccode);
     int idx = 0;
     while (idx < nlen + ndist) {
         bits_topup(b);
         bits_refill(b);
-        const int sym = decode_sym<7>(b, TL, ccode, SL);
+        const int sym = decode_sym<7, false>(b, TL, ccode, SL);
         if (sym < 0) return kErrCodes;
         if (sym < 16) {
             lens[idx++] = (uint16_t)sym;
@@ -363,7 +392,7 @@ MC_HD int read_dynamic(Bits<RP>& b, uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
 }
 
 template <class TP>
-MC_HD int read_fixed(uint16_t* S, TP TL, TP TD, TP SL, TP SD) {
+MC_HD int read_fixed(uint16_t* S, TP TL, TP TD, typename RingOf<TP>::sym SL, typename RingOf<TP>::sym SD) {
     uint16_t* lens = S + kLens;
     for (int s = 0; s < 288; ++s) lens[s] = (uint16_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
     int rc = build_code(S, TL, kLitBits, kLitCnt, SL, lens, 288);
@@ -437,7 +466,8 @@ MC_HD void mq_flush(MatchQueue<QP>& q, uint8_t* dst) {
 // trip whose vmcnt wait also drained the lane's output stores).
 template <class TP>
 MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize, uint16_t* S, TP TL, TP TD,
-                        TP SL, TP SD, typename RingOf<TP>::type ring, typename RingOf<TP>::queue queue) {
+                        typename RingOf<TP>::sym SL, typename RingOf<TP>::sym SD, typename RingOf<TP>::type ring,
+                        typename RingOf<TP>::queue queue) {
     if (isize == 0) return kOk;
     MatchQueue<typename RingOf<TP>::queue> mq;
     mq.e = queue;
@@ -469,10 +499,10 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
         } else {
             const int rc = type == 1 ? read_fixed(S, TL, TD, SL, SD) : read_dynamic(b, S, TL, TD, SL, SD);
             if (rc) return rc;
-            CodeRegs<kLitBits> lcode;
-            CodeRegs<kDistBits> dcode;
-            load_code<kLitBits>(S, kLitCnt, lcode);
-            load_code<kDistBits>(S, kDistCnt, dcode);
+            CodeRegs<kLitBits, true> lcode;
+            CodeRegs<kDistBits, false> dcode;
+            load_code<kLitBits, true>(S, kLitCnt, lcode);
+            load_code<kDistBits, false>(S, kDistCnt, dcode);
             for (;;) {
                 // all lanes still in a symbol loop vote: one full queue
                 // flushes every lane's (at most one push per iteration)
@@ -480,7 +510,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                 if (bits_pos(b) > limit_bits) return kErrInput;
                 bits_topup(b);   // (a symbol with its distance takes <= 2 words)
                 bits_refill(b);
-                int s = decode_sym<kLitBits>(b, TL, lcode, SL);
+                int s = decode_sym<kLitBits, true>(b, TL, lcode, SL);
                 if (s < 0) return kErrSymbol;
                 if (s < 256) {
                     if (o >= isize) return kErrOutput;
@@ -500,7 +530,7 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                     len = ((4 + (s & 3)) << e) + 3 + (int)bits_take(b, e);
                 }
                 bits_refill(b);
-                const int d = decode_sym<kDistBits>(b, TD, dcode, SD);
+                const int d = decode_sym<kDistBits, false>(b, TD, dcode, SD);
                 if (d < 0 || d >= 30) return kErrSymbol;
                 int dist;
                 if (d < 4) {

@@ -20,7 +20,7 @@ for step in ${STEPS:-tests}; do
           --timeout-method thread -p no:cacheprovider > "$O/${TAG}_pytest_gpu.log" 2>&1
       s=$?; grep -E "passed|failed|error" "$O/${TAG}_pytest_gpu.log" | tail -8; faulted "$O/${TAG}_pytest_gpu.log"; fatal $s tests ;;
     gz)
-      timeout -k 10 ${GZ_TIMEOUT:-500} python -u scripts/gz_ab.py --reads ${GZ_READS:-10000000} --reps ${GZ_REPS:-3} \
+      timeout -k 10 ${GZ_TIMEOUT:-500} python -u scripts/gz_ab.py --reads ${GZ_READS:-10000000} --reps ${GZ_REPS:-3} --window ${GZ_WINDOW:-0} \
           ${GZ_VARIANTS:?} > "$O/${TAG}_gz_ab.txt" 2>&1
       s=$?; grep -v "^{" "$O/${TAG}_gz_ab.txt" | tail -24; faulted "$O/${TAG}_gz_ab.txt"; fatal $s gz ;;
     k2ab)
@@ -34,6 +34,20 @@ for step in ${STEPS:-tests}; do
       s=$?; tail -2 "$O/${TAG}_smoke.log"; faulted "$O/${TAG}_smoke.log"; fatal $s smoke ;;
     prof)
       TAG=${PROF_TAG:?} bash "$R/scripts/profile.sh"; s=$?; fatal $s prof ;;
+    gzpmc)   # kernel trace + SQ counter passes over one GPU decode (variant GZ_PMC_VARIANT)
+      G="$R/scripts/gz_ab.py --reads ${GZ_PMC_READS:-3000000} --reps 1 ${GZ_PMC_VARIANT:-gzopq}"
+      ( cd /tmp && export TMPDIR=/tmp
+        timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$O/prof_${TAG}_gz_trace" -o run \
+            -- python3 $G > "$O/prof_${TAG}_gz_trace.log" 2>&1 || exit 1
+        for p in A B; do
+          case $p in
+            A) C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY" ;;
+            B) C="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SMEM" ;;
+          esac
+          timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$O/prof_${TAG}_gz_sq$p" -o run \
+              -- python3 $G > "$O/prof_${TAG}_gz_sq$p.log" 2>&1 || exit 1
+        done )
+      s=$?; python3 "$R/scripts/sq_summary.py" ${TAG}_gz gz_inflate 2>&1 | tail -20; fatal $s gzpmc ;;
   esac
 done
 exit 0

@@ -56,9 +56,26 @@ def _bgzf_blocks(raw):
     return out
 
 
+def _rare_matches(seed, n=65280):
+    """Skewed literals with rare copies: the end-of-block and length symbols
+    get long codes (10-14 bits, past the primary table), the case of the byte
+    symbol lists' kLitHi split."""
+    rng = np.random.default_rng(seed)
+    out = bytearray(np.minimum(rng.geometric(0.02, n), 255).astype(np.uint8).tobytes())
+    i = 300
+    while i < n - 300:
+        if rng.random() < 0.004:
+            ln, d = int(rng.integers(3, 259)), int(rng.integers(1, min(i, 32768)))
+            for k in range(min(ln, n - i)):
+                out[i + k] = out[i + k - d]
+            i += ln
+        i += 1
+    return bytes(out)
+
+
 def test_inflate_host_matches_zlib(lib_built):
     rng = np.random.default_rng(0)
-    cases = [b"", b"a", b"ab" * 3,
+    cases = [b"", b"a", b"ab" * 3, _rare_matches(1), _rare_matches(2),
              bytes(rng.integers(0, 256, 65280, dtype=np.uint8)),          # incompressible
              bytes(rng.integers(0, 4, 65280, dtype=np.uint8) + 65),
              b"ACGT" * 16000,                                             # long matches
