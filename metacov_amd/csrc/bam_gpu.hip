@@ -29,7 +29,9 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 
 #include "bgzf.h"
 #include "inflate.h"
@@ -309,7 +311,7 @@ struct mc_bam_gpu {
     DBuf<uint16_t> scratch;
     DBuf<int64_t> seg_off, found, out_off;
     DBuf<SegRes> res;
-    PinnedBuf<uint8_t> stage[2];
+    PinnedBuf<uint8_t> stage[3];
     PinnedBuf<int64_t> h64;
     PinnedBuf<SegRes> hres;
     PinnedBuf<GzBlock> hblk;
@@ -351,8 +353,12 @@ const char* gz_err_msg(int e) {
     }
 }
 
-// File bytes [off, off + len) into device memory at dst: pread on threads
-// into a pinned staging slice, copied up while the next slice is read.
+// File bytes [off, off + len) into device memory at dst: reader threads
+// pread each slice into a pinned staging buffer (kStage buffers in rotation),
+// the calling thread copies a slice up as soon as its parts are read, and a
+// buffer is handed back to the readers once its copy is done.  The readers
+// live for the whole range (round 3 started nt threads per slice: ~0.3 ms of
+// thread starts per 64 MiB slice).
 // 32 / 64 / 128 / 256 MiB slices, decode in rounds 1-2 (round 0 includes a cold
 // first run): 271-288 / 273-298 / 304-307 / 323-334 ms
 // (profiles/r03si_upload_slice_ab.txt): larger slices expose a longer first read
@@ -361,45 +367,90 @@ const char* gz_err_msg(int e) {
 #endif
 int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst, hipStream_t st) {
     constexpr size_t kSlice = (size_t)MC_UPLOAD_SLICE_MIB << 20;
+    constexpr int kStage = 3;
+    if (len == 0) return MC_OK;
     for (auto& s : g->stage) HIP_TRY(s.reserve(kSlice));
-    hipEvent_t done[2] = {nullptr, nullptr};
+    hipEvent_t done[kStage] = {};
     for (auto& e : done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     struct Guard {
         hipEvent_t* e;
         ~Guard() {
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < kStage; ++i)
                 if (e[i]) (void)hipEventDestroy(e[i]);
         }
     } guard{done};
-    bool used[2] = {false, false};
-    int k = 0;
-    for (size_t at = 0; at < len; at += kSlice, k ^= 1) {
-        const size_t n = std::min(kSlice, len - at);
-        if (used[k]) HIP_TRY(hipEventSynchronize(done[k]));   // the slice's previous copy is out
-        uint8_t* buf = g->stage[k].p;
-        const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)g->nt, n >> 20));
-        std::atomic<bool> bad{false};
-        auto work = [&](int t) {
+    const int64_t ns = (int64_t)((len + kSlice - 1) / kSlice);
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)g->nt, std::min(len, kSlice) >> 20));
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t free_upto = std::min<int64_t>(ns, kStage);   // slices [0, free_upto) may be read
+    std::vector<int> parts(ns, 0);                     // parts of each slice read
+    bool bad = false, stop = false;
+    auto reader = [&](int t) {
+        for (int64_t k = 0; k < ns; ++k) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return k < free_upto || stop; });
+                if (stop) return;
+            }
+            const size_t at = (size_t)k * kSlice, n = std::min(kSlice, len - at);
             const size_t a = n * t / nt, b = n * (t + 1) / nt;
-            size_t got = a;
-            while (got < b) {
+            uint8_t* buf = g->stage[k % kStage].p;
+            bool ok = true;
+            for (size_t got = a; got < b;) {
                 const ssize_t r = pread(fd, buf + got, b - got, (off_t)(off + at + got));
                 if (r <= 0) {
-                    bad = true;
-                    return;
+                    ok = false;
+                    break;
                 }
                 got += (size_t)r;
             }
-        };
-        std::vector<std::thread> pool;
-        for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
-        work(0);
+            std::lock_guard<std::mutex> lk(mu);
+            if (!ok) bad = true;
+            parts[k] += 1;
+            cv.notify_all();
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back(reader, t);
+    auto finish = [&]() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
         for (auto& th : pool) th.join();
-        MC_REQUIRE(!bad, MC_E_IO, "%s: read failed at offset %zu", g->path.c_str(), off + at);
-        HIP_TRY(hipMemcpyAsync(dst + at, buf, n, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipEventRecord(done[k], st));
-        used[k] = true;
+    };
+    int rc = MC_OK;
+    for (int64_t k = 0; k < ns && rc == MC_OK; ++k) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return parts[k] == nt || bad; });
+            if (bad) {
+                mc::set_error("%s: read failed in [%zu, %zu)", g->path.c_str(), off, off + len);
+                rc = MC_E_IO;
+                break;
+            }
+        }
+        const size_t at = (size_t)k * kSlice, n = std::min(kSlice, len - at);
+        hipError_t e = hipMemcpyAsync(dst + at, g->stage[k % kStage].p, n, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(done[k % kStage], st);
+        // the previous slice's buffer goes back to the readers once its copy
+        // is out (slice j + kStage reuses it): the readers stay a slice ahead
+        const int64_t j = k - 1;
+        if (e == hipSuccess && j >= 0 && j + kStage < ns) {
+            e = hipEventSynchronize(done[j % kStage]);
+            std::lock_guard<std::mutex> lk(mu);
+            free_upto = j + kStage + 1;
+            cv.notify_all();
+        }
+        if (e != hipSuccess) {
+            mc::set_error("HIP error %s in the upload", hipGetErrorString(e));
+            rc = MC_E_HIP;
+        }
     }
+    finish();
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     return MC_OK;
 }

@@ -437,6 +437,16 @@ MC_HD void lz_copy(uint8_t* q, int len, int dist) {
 // compares cost 3 x kQueue VALU per push, which every step with some lane
 // matching paid), and the flush loops over the entries at run time.
 constexpr int kQueue = MC_GZ_QUEUE;
+
+// Literals decoded after a literal in the same symbol step (inflate_block).
+// After bits_refill more than 32 bits are buffered; a first symbol takes at
+// most 15 and each extra literal at most kLitBits <= 8, so two extras never
+// read past the buffered bits.
+#ifndef MC_GZ_LIT_EXTRA
+#define MC_GZ_LIT_EXTRA 2
+#endif
+constexpr int kLitExtra = MC_GZ_LIT_EXTRA;
+static_assert(kLitExtra >= 0 && 32 - 15 - kLitExtra * kLitBits >= 0, "extra literals within the buffered bits");
 static_assert(kQueue >= 1, "match queue: >= 1 entry");
 
 template <class QP>
@@ -515,6 +525,20 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                 if (s < 256) {
                     if (o >= isize) return kErrOutput;
                     dst[o++] = (uint8_t)s;
+                    // up to kLitExtra more literals of primary-table codes
+                    // from the bits already buffered (anything else waits for
+                    // the next iteration): a wave step's fixed cost - votes,
+                    // checks, refill, the other paths some lane takes - is
+                    // paid per iteration, and 72 % of BAM symbols are literals
+#pragma unroll
+                    for (int x = 0; x < kLitExtra; ++x) {
+                        const uint32_t e2 = TL[(uint32_t)b.buf & ((1u << kLitBits) - 1u)];
+                        if (e2 == 0 || e2 >= (256u << 4) || o >= isize) break;
+                        const int u = (int)(e2 & 15u);
+                        b.buf >>= u;
+                        b.cnt -= u;
+                        dst[o++] = (uint8_t)(e2 >> 4);
+                    }
                     continue;
                 }
                 if (s == 256) break;
