@@ -31,7 +31,7 @@ namespace gz {
 #define MC_GZ_QUEUE 16          // matches a lane defers (>= 1)
 #endif
 #ifndef MC_GZ_COPY_BATCH
-#define MC_GZ_COPY_BATCH 1
+#define MC_GZ_COPY_BATCH 2      // lz_copy: 2 = 16-byte chunks (dist >= 16), 1 = byte groups, 0 = byte loop
 #endif
 
 // Tuning knobs (scripts/gz_ab.py): primary table bits, tables in LDS.
@@ -405,7 +405,7 @@ MC_HD int read_fixed(uint16_t* S, TP TL, TP TD, typename RingOf<TP>::sym SL, typ
 // copy's first output byte, so a group's loads are all issued before its
 // stores (one memory round trip per 16 bytes, not per byte); the source
 // index runs modulo dist for overlapping copies.
-MC_HD void lz_copy(uint8_t* q, int len, int dist) {
+MC_HD void lz_copy_bytes(uint8_t* q, int len, int dist) {
 #if MC_GZ_COPY_BATCH
     const uint8_t* s = q - dist;
     int si = 0;
@@ -425,6 +425,61 @@ MC_HD void lz_copy(uint8_t* q, int len, int dist) {
 #else
     for (int k = 0; k < len; ++k) q[k] = q[k - dist];
 #endif
+}
+
+// 16 bytes at p, any alignment (gfx950 runs in unaligned access mode: one
+// global_load / store_dwordx4; memcpy tells the compiler the alignment is 1)
+MC_HD uint4 ld16(const uint8_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+MC_HD void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+
+// A copy whose source ends at least 16 bytes before its destination starts
+// (dist >= 16): whole 16-byte chunks; the last partial one as 8 / 4 / 2 / 1
+// byte stores, since the bytes past the copy may hold literals already
+// written (copies are deferred, literals are not).  Each chunk's source lies
+// before the chunk itself, so a chunk read after earlier chunks' stores sees
+// them (one lane, in order).
+MC_HD void lz_copy_wide(uint8_t* q, int len, int dist) {
+    const uint8_t* s = q - dist;
+    int k = 0;
+    for (; k + 16 <= len; k += 16) st16(q + k, ld16(s + k));
+    const int r = len - k;
+    if (r == 0) return;
+    const uint4 v = ld16(s + k);
+    uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    uint8_t* d = q + k;
+    if (r & 8) {
+        __builtin_memcpy(d, &lo, 8);
+        d += 8;
+        lo = hi;
+    }
+    if (r & 4) {
+        const uint32_t w = (uint32_t)lo;
+        __builtin_memcpy(d, &w, 4);
+        d += 4;
+        lo >>= 32;
+    }
+    if (r & 2) {
+        const uint16_t h = (uint16_t)lo;
+        __builtin_memcpy(d, &h, 2);
+        d += 2;
+        lo >>= 16;
+    }
+    if (r & 1) *d = (uint8_t)lo;
+}
+
+MC_HD void lz_copy(uint8_t* q, int len, int dist) {
+#if MC_GZ_COPY_BATCH == 2
+    if (dist >= 16) {
+        lz_copy_wide(q, len, dist);
+        return;
+    }
+#endif
+    lz_copy_bytes(q, len, dist);
 }
 
 // A lane's deferred LZ77 copies.  With one lane per BGZF block, a copy
