@@ -572,7 +572,9 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
                 // all lanes still in a symbol loop vote: one full queue
                 // flushes every lane's (at most one push per iteration)
                 if (wave_any(mq.n == kQueue)) mq_flush(mq, dst);
-                if (bits_pos(b) > limit_bits) return kErrInput;
+                // (no per-step input bound: loads past the payload are clamped
+                // to its last group, every step but the end of block adds
+                // output, bounded by isize, and the block end checks bits_pos)
                 bits_topup(b);   // (a symbol with its distance takes <= 2 words)
                 bits_refill(b);
                 int s = decode_sym<kLitBits, true>(b, TL, lcode, SL);
