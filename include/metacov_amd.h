@@ -335,6 +335,8 @@ typedef struct mc_bam_gpu_timings {
     int64_t compressed_bytes;
     int64_t inflated_bytes;
     double scan_ms;      /* host: BGZF block header scan */
+    double upload_ms;    /* host: every file read + upload, overlapped or not */
+    double kernel_ms;    /* gz_inflate_kernel launches (HIP events), summed over launches */
 } mc_bam_gpu_timings;
 int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
                     int64_t window_bytes, mc_bam_gpu** out);

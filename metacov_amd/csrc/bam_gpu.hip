@@ -317,6 +317,7 @@ struct mc_bam_gpu {
     PinnedBuf<GzBlock> hblk;
     // timings (ms)
     double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0, t_scan = 0;
+    double t_upload = 0, t_kernel = 0;   // every upload_file_range call; inflate launches (HIP events, summed)
     int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
     ~mc_bam_gpu() {
         for (hipStream_t s : {stream, up_stream, kstream[0], kstream[1], kstream[2]}) {
@@ -369,6 +370,12 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     constexpr size_t kSlice = (size_t)MC_UPLOAD_SLICE_MIB << 20;
     constexpr int kStage = 3;
     if (len == 0) return MC_OK;
+    const double t_begin = now_s();
+    struct Clock {
+        mc_bam_gpu* g;
+        double t0;
+        ~Clock() { g->t_upload += (now_s() - t0) * 1e3; }
+    } clock{g, t_begin};
     for (auto& s : g->stage) HIP_TRY(s.reserve(kSlice));
     hipEvent_t done[kStage] = {};
     for (auto& e : done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -767,6 +774,16 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
     } evg{ev};
     HIP_TRY(hipEventRecord(ev[0], st));   // block table, status flag and pad are set
     for (int k = 1; k < kGzPieceStreams; ++k) HIP_TRY(hipStreamWaitEvent(ks[k], ev[0], 0));
+    // each launch between two timing events (t_kernel: their durations summed)
+    std::vector<hipEvent_t> kev(2 * pcs.size(), nullptr);
+    struct KevGuard {
+        std::vector<hipEvent_t>& e;
+        ~KevGuard() {
+            for (auto x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } kevg{kev};
+    for (auto& e : kev) HIP_TRY(hipEventCreate(&e));
     double t_first = now_s();
     for (size_t p = 0; p < pcs.size(); ++p) {
         const size_t b0 = pcs[p].first, b1 = pcs[p].second;
@@ -781,10 +798,12 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
         const int64_t n = (int64_t)(b1 - b0);
         const int64_t lanes = std::min<int64_t>(max_lanes, (n + kGzLanes - 1) / kGzLanes * kGzLanes);
         const int k = (int)(p % kGzPieceStreams);
+        HIP_TRY(hipEventRecord(kev[2 * p], ks[k]));
         gz_inflate_kernel<<<(int)(lanes / kGzLanes), kGzThreads, 0, ks[k]>>>(
             g->comp[0].p, g->blk.p + b0, n, g->inflated.p, g->scratch.p + k * slot, g->status.p + b0,
             g->status.p + nb);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(kev[2 * p + 1], ks[k]));
     }
     for (int k = 1; k < kGzPieceStreams; ++k) {
         HIP_TRY(hipEventRecord(ev[1], ks[k]));
@@ -795,6 +814,11 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
     HIP_TRY(hipStreamSynchronize(st));
     g->t_inflate = (now_s() - t_first) * 1e3;
     g->windows = (int64_t)pcs.size();
+    for (size_t p = 0; p < pcs.size(); ++p) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, kev[2 * p], kev[2 * p + 1]));
+        g->t_kernel += ms;
+    }
     if (any) {
         std::vector<int> sv(nb);
         HIP_TRY(hipMemcpy(sv.data(), g->status.p, nb * sizeof(int), hipMemcpyDeviceToHost));
@@ -967,6 +991,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         float ms = 0;
         HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
         g->t_inflate += ms;
+        g->t_kernel += ms;
         if (any) {
             std::vector<int> s(nb);
             HIP_TRY(hipMemcpy(s.data(), g->status.p, nb * sizeof(int), hipMemcpyDeviceToHost));
@@ -1089,6 +1114,8 @@ extern "C" int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t) {
     t->compressed_bytes = g->compressed_bytes;
     t->inflated_bytes = g->inflated_bytes;
     t->scan_ms = g->t_scan;
+    t->upload_ms = g->t_upload;
+    t->kernel_ms = g->t_kernel;
     return MC_OK;
 }
 

@@ -97,7 +97,7 @@ def main():
         assert gw.n_kept == n_kept
         gw.close()
         sweep.append({"window_mib": mib, "decode_s": dt, **{k: wt[k] for k in
-                      ("read_ms", "inflate_ms", "parse_ms", "scan_ms", "total_ms", "windows")}})
+                      ("read_ms", "inflate_ms", "parse_ms", "scan_ms", "total_ms", "windows", "upload_ms", "kernel_ms")}})
         print(json.dumps(sweep[-1]), file=sys.stderr, flush=True)
     print(json.dumps({
         "bam_bytes": os.path.getsize(path), "records": n_rec, "kept": n_kept,

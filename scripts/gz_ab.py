@@ -54,8 +54,10 @@ def main():
             r["n_kept"] = n.value
             r["checksum"] = ck
             out.setdefault(name, []).append(r)
-            print(name, rep, "inflate %.1f ms  parse %.1f ms  read %.1f ms  total %.1f ms  resyncs %d  kept %d  ck %d"
-                  % (r["inflate_ms"], r["parse_ms"], r["read_ms"], r["total_ms"], r["resyncs"], n.value, ck),
+            print(name, rep, "inflate %.1f ms (kernels %.1f)  parse %.1f ms  read %.1f ms (uploads %.1f)  total %.1f ms  "
+                  "resyncs %d  kept %d  ck %d"
+                  % (r["inflate_ms"], r.get("kernel_ms", 0), r["parse_ms"], r["read_ms"], r.get("upload_ms", 0),
+                     r["total_ms"], r["resyncs"], n.value, ck),
                   flush=True)
     cks = {v[-1]["checksum"] for v in out.values()}
     print(json.dumps({"agree": len(cks) == 1, "runs": out}))
