@@ -34,6 +34,12 @@ for step in ${STEPS:-tests}; do
       s=$?; tail -2 "$O/${TAG}_smoke.log"; faulted "$O/${TAG}_smoke.log"; fatal $s smoke ;;
     prof)
       TAG=${PROF_TAG:?} bash "$R/scripts/profile.sh"; s=$?; fatal $s prof ;;
+    e2e)     # scripts/e2e.py: CLI end to end, host and GPU decode of one 30 M-record BAM
+      mkdir -p /tmp/e2e
+      timeout -k 10 600 python scripts/e2e.py --reads ${E2E_READS:-30000000} --contigs 1000 --length 1000000 \
+          --dir /tmp/e2e > "$O/${TAG}_e2e.json" 2> "$O/${TAG}_e2e.err"
+      s=$?; tail -3 "$O/${TAG}_e2e.err"; python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['gpu_decode_s'],d['gpu_end_to_end_s'],d['gpu_decode_timings'])" "$O/${TAG}_e2e.json"
+      faulted "$O/${TAG}_e2e.err"; fatal $s e2e ;;
     gzpmc)   # kernel trace + SQ counter passes over one GPU decode (variant GZ_PMC_VARIANT)
       G="$R/scripts/gz_ab.py --reads ${GZ_PMC_READS:-3000000} --reps 1 ${GZ_PMC_VARIANT:-gzopq}"
       ( cd /tmp && export TMPDIR=/tmp
