@@ -147,12 +147,37 @@ MC_HD void ring_load(Bits<RP>& b) {   // every load issued before the first ring
 }
 
 // Every lane that may consume input calls it at a point where the whole wave
-// (or the active part of it) does: when some lane is low, each lane with room
-// loads kRingFill words, and the wave waits once.
+// (or the active part of it) does: when some lane is low, every lane fills its
+// ring (as many 16-byte groups as fit), and the wave waits once.  Filling only
+// the lanes at or below half (round 3) left lanes just above it to trigger
+// the next wait a few steps later; full rings space the waits by at least
+// kRingWords - 3 - kRingLow words of the fastest lane.
+#ifndef MC_GZ_TOPUP_FULL
+#define MC_GZ_TOPUP_FULL 1
+#endif
 template <class RP>
 MC_HD void bits_topup(Bits<RP>& b) {
     if (wave_any((int)(b.rfill - b.rpos) < kRingLow)) {
+#if MC_GZ_TOPUP_FULL
+        const int ng = (kRingWords - (int)(b.rfill - b.rpos)) >> 2;   // free groups
+        uint4 v[kRingWords / 4];
+#pragma unroll
+        for (int g = 0; g < kRingWords / 4; ++g)
+            if (g < ng) v[g] = ld_group(b.p + g, b.pend);
+#pragma unroll
+        for (int g = 0; g < kRingWords / 4; ++g)
+            if (g < ng) {
+                const uint32_t s = (b.rfill + 4 * g) & (kRingWords - 1);
+                b.ring[s] = v[g].x;
+                b.ring[s + 1] = v[g].y;
+                b.ring[s + 2] = v[g].z;
+                b.ring[s + 3] = v[g].w;
+            }
+        b.p += ng;
+        b.rfill += 4 * ng;
+#else
         if ((int)(b.rfill - b.rpos) <= kRingWords - kRingFill) ring_load<kRingFill>(b);
+#endif
     }
 }
 

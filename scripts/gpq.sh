@@ -5,7 +5,7 @@
 out=$1; shift
 for i in $(seq 1 40); do
   timeout 2400 /usr/local/graft/bin/gpurun "$@" > "$out" 2>&1
-  if grep -q "slot(s) on this pod are busy\|status=transient" "$out"; then sleep 60; continue; fi
+  if grep -qE "are busy|status=transient|no free box|backing off" "$out"; then sleep 60; continue; fi
   break
 done
 echo "[gpq] done after $i tries" >> "$out"
