@@ -732,12 +732,18 @@ static_assert(MC_GZ_PIECE_STREAMS >= 1 && MC_GZ_PIECE_STREAMS <= 4, "inflate str
 constexpr int kGzPieceStreams = MC_GZ_PIECE_STREAMS;
 
 int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<Block>& blocks, size_t total,
-                        int64_t max_lanes) {
+                        int64_t max_lanes, size_t pre) {
     const int64_t nb = (int64_t)blocks.size();
     hipStream_t st = g->stream;
     const size_t piece = std::min<size_t>(4ull << 30, std::max<size_t>(256ull << 20, total / MC_GZ_PIECES));
     std::vector<std::pair<size_t, size_t>> pcs;
-    for (size_t b0 = 0; b0 < blocks.size();) {
+    // file bytes [0, pre) are on the device already (uploaded during the
+    // scan): the first piece is the blocks they hold whole
+    auto cend_of = [&](size_t b) { return b + 1 < blocks.size() ? blocks[b + 1].off : mf.size; };
+    size_t first = 0;
+    while (first < blocks.size() && cend_of(first) <= pre) ++first;
+    if (first) pcs.emplace_back(0, first);
+    for (size_t b0 = first; b0 < blocks.size();) {
         size_t b1 = b0, sz = 0;
         while (b1 < blocks.size() && (b1 == b0 || sz + blocks[b1].isize <= piece)) sz += blocks[b1++].isize;
         pcs.emplace_back(b0, b1);
@@ -789,10 +795,12 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
         const size_t b0 = pcs[p].first, b1 = pcs[p].second;
         const size_t coff = blocks[b0].off, cend = b1 < blocks.size() ? blocks[b1].off : mf.size;
         const double t0 = now_s();
-        // returns once the bytes are on the device (its stream synchronised)
-        if (int rc = upload_file_range(g, mf.fd, coff, cend - coff, g->comp[0].p + coff, g->up_stream)) return rc;
+        // returns once the bytes are on the device (its stream synchronised);
+        // bytes below pre are there already
+        const size_t ulo = std::max(coff, std::min(pre, cend));
+        if (int rc = upload_file_range(g, mf.fd, ulo, cend - ulo, g->comp[0].p + ulo, g->up_stream)) return rc;
         if (p == 0) {
-            g->t_read = (now_s() - t0) * 1e3;   // the exposed part: the first piece
+            g->t_read += (now_s() - t0) * 1e3;   // the exposed part: the first piece
             t_first = now_s();
         }
         const int64_t n = (int64_t)(b1 - b0);
@@ -848,8 +856,47 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     if (int rc = mf.open(g->path.c_str())) return rc;
     std::vector<Block> blocks;
     size_t total = 0;
+    // A file likely to decode resident has its first bytes uploaded (the
+    // first piece's worth) while the block headers are scanned: the upload
+    // needs no block list, the scan no device.  (If the file turns out not to
+    // be resident, the windowed decode uploads its windows itself.)
+    size_t pre = 0;
+    struct Spec {
+        std::thread t;
+        int rc = MC_OK;
+        std::string msg;
+        ~Spec() {
+            if (t.joinable()) t.join();
+        }
+    } spec;
+    if (window_bytes <= 0 && mf.size >= (size_t)(256ull << 20)) {
+        size_t free_b = 0, tot_b = 0;
+        HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
+        if (mf.size * 4 <= free_b / 2) {
+            HIP_TRY(g->comp[0].reserve(mf.size + kPad));
+            pre = std::min<size_t>(mf.size / MC_GZ_PIECES, 1536ull << 20);
+            spec.t = std::thread([&]() {
+                if (hipSetDevice(g->device) != hipSuccess) {
+                    spec.rc = MC_E_HIP;
+                    spec.msg = "hipSetDevice failed in the upload thread";
+                    return;
+                }
+                spec.rc = upload_file_range(g, mf.fd, 0, pre, g->comp[0].p, g->up_stream);
+                if (spec.rc) spec.msg = mc::last_error();
+            });
+        }
+    }
     if (int rc = scan_blocks_parallel(mf.data, mf.size, g->nt, blocks, total)) return rc;
     g->t_scan = (now_s() - t_start) * 1e3;
+    if (spec.t.joinable()) {
+        const double t0 = now_s();
+        spec.t.join();
+        g->t_read = (now_s() - t0) * 1e3;   // the part of the first upload not hidden by the scan
+        if (spec.rc) {
+            mc::set_error("%s", spec.msg.c_str());
+            return spec.rc;
+        }
+    }
     g->blocks = (int64_t)blocks.size();
     g->inflated_bytes = (int64_t)total;
     g->compressed_bytes = (int64_t)mf.size;
@@ -875,7 +922,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         const size_t need = mf.size + total + blocks.size() * (sizeof(GzBlock) + sizeof(int)) +
                             (size_t)kGzPieceStreams * (size_t)max_lanes * kGzSlotWords * sizeof(uint16_t);
         if (need <= free_b / 2) {
-            const int rc = gpu_decode_resident(g, mf, blocks, total, max_lanes);
+            const int rc = gpu_decode_resident(g, mf, blocks, total, max_lanes, pre);
             g->t_total = (now_s() - t_start) * 1e3;
             return rc;
         }
