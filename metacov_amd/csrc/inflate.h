@@ -467,13 +467,18 @@ MC_HD void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 // written (copies are deferred, literals are not).  Each chunk's source lies
 // before the chunk itself, so a chunk read after earlier chunks' stores sees
 // them (one lane, in order).
-MC_HD void lz_copy_wide(uint8_t* q, int len, int dist) {
+// v0: the copy's first 16 source bytes, already loaded.
+MC_HD void lz_copy_wide(uint8_t* q, int len, int dist, uint4 v0) {
     const uint8_t* s = q - dist;
     int k = 0;
-    for (; k + 16 <= len; k += 16) st16(q + k, ld16(s + k));
+    uint4 v = v0;
+    if (len >= 16) {
+        st16(q, v0);
+        for (k = 16; k + 16 <= len; k += 16) st16(q + k, ld16(s + k));
+        if (k == len) return;
+        v = ld16(s + k);
+    }
     const int r = len - k;
-    if (r == 0) return;
-    const uint4 v = ld16(s + k);
     uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
     const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
     uint8_t* d = q + k;
@@ -500,7 +505,7 @@ MC_HD void lz_copy_wide(uint8_t* q, int len, int dist) {
 MC_HD void lz_copy(uint8_t* q, int len, int dist) {
 #if MC_GZ_COPY_BATCH == 2
     if (dist >= 16) {
-        lz_copy_wide(q, len, dist);
+        lz_copy_wide(q, len, dist, ld16(q - dist));
         return;
     }
 #endif
@@ -535,9 +540,45 @@ struct MatchQueue {
     int n;
 };
 
+// MC_GZ_FLUSH_BATCH = B > 1: the queue goes in batches of B entries whose
+// first source chunks are loaded together (one memory round trip per batch,
+// not per entry) when they lie before the batch's first destination, which
+// nothing of the batch writes; an entry reading later bytes loads after the
+// stores before it.
+#ifndef MC_GZ_FLUSH_BATCH
+#define MC_GZ_FLUSH_BATCH 1
+#endif
+constexpr int kFlushBatch = MC_GZ_FLUSH_BATCH;
+
 template <class QP>
 MC_HD void mq_flush(MatchQueue<QP>& q, uint8_t* dst) {
-    for (int j = 0; j < q.n; ++j) {
+    int j = 0;
+#if MC_GZ_COPY_BATCH == 2
+    if (kFlushBatch > 1) {
+        for (; j + kFlushBatch <= q.n; j += kFlushBatch) {
+            uint64_t e[kFlushBatch];
+            uint4 v[kFlushBatch];
+            bool early[kFlushBatch];
+#pragma unroll
+            for (int k = 0; k < kFlushBatch; ++k) e[k] = q.e[j + k];
+            const uint32_t o0 = (uint32_t)(e[0] >> 32);
+#pragma unroll
+            for (int k = 0; k < kFlushBatch; ++k) {
+                const uint32_t o = (uint32_t)(e[k] >> 32), d = (uint32_t)e[k] >> 9;
+                early[k] = d >= 16 && o - d + 16 <= o0;
+                v[k] = early[k] ? ld16(dst + (o - d)) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < kFlushBatch; ++k) {
+                const uint32_t o = (uint32_t)(e[k] >> 32), d = (uint32_t)e[k] >> 9;
+                const int len = (int)(e[k] & 511u);
+                if (early[k]) lz_copy_wide(dst + o, len, (int)d, v[k]);
+                else lz_copy(dst + o, len, (int)d);
+            }
+        }
+    }
+#endif
+    for (; j < q.n; ++j) {
         const uint64_t e = q.e[j];
         lz_copy(dst + (uint32_t)(e >> 32), (int)(e & 511u), (int)((uint32_t)e >> 9));
     }
