@@ -337,6 +337,7 @@ typedef struct mc_bam_gpu_timings {
     double scan_ms;      /* host: BGZF block header scan */
     double upload_ms;    /* host: every file read + upload, overlapped or not */
     double kernel_ms;    /* gz_inflate_kernel launches (HIP events), summed over launches */
+    double open_ms;      /* the decode inside mc_bam_gpu_open, teardown of its file mapping included */
 } mc_bam_gpu_timings;
 int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
                     int64_t window_bytes, mc_bam_gpu** out);

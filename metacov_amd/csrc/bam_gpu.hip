@@ -317,7 +317,7 @@ struct mc_bam_gpu {
     PinnedBuf<GzBlock> hblk;
     // timings (ms)
     double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0, t_scan = 0;
-    double t_upload = 0, t_kernel = 0;   // every upload_file_range call; inflate launches (HIP events, summed)
+    double t_upload = 0, t_kernel = 0, t_open = 0;   // every upload_file_range call; inflate launches (HIP events, summed)
     int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
     ~mc_bam_gpu() {
         for (hipStream_t s : {stream, up_stream, kstream[0], kstream[1], kstream[2]}) {
@@ -850,10 +850,20 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
     return MC_OK;
 }
 
+// The header scan's mapping advice (MC_SCAN_ADVICE = random | normal |
+// sequential; A/B knob, default random: no read-around of the pages between
+// two headers, which the scan never reads)
+static int scan_advice() {
+    const char* e = getenv("MC_SCAN_ADVICE");
+    if (e && !strcmp(e, "normal")) return MADV_NORMAL;
+    if (e && !strcmp(e, "sequential")) return MADV_SEQUENTIAL;
+    return MADV_RANDOM;
+}
+
 int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     const double t_start = now_s();
     MappedFile mf;
-    if (int rc = mf.open(g->path.c_str())) return rc;
+    if (int rc = mf.open(g->path.c_str(), scan_advice())) return rc;
     std::vector<Block> blocks;
     size_t total = 0;
     // A file likely to decode resident has its first bytes uploaded (the
@@ -1115,7 +1125,9 @@ extern "C" int mc_bam_gpu_open(const char* path, int device, int n_threads, uint
     g->flag_filter = flag_filter;
     HIP_TRY(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&g->up_stream, hipStreamNonBlocking));
+    const double t0 = now_s();
     if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
+    g->t_open = (now_s() - t0) * 1e3;   // total_ms + the mapping's teardown
     // (the staging and parse buffers go with the handle: a hipFree of the
     // multi-GB windows here sat on the open's critical path)
     *out = g.release();
@@ -1163,6 +1175,7 @@ extern "C" int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t) {
     t->scan_ms = g->t_scan;
     t->upload_ms = g->t_upload;
     t->kernel_ms = g->t_kernel;
+    t->open_ms = g->t_open;
     return MC_OK;
 }
 

@@ -62,7 +62,10 @@ struct MappedFile {
         if (data && size) munmap((void*)data, size);
         if (fd >= 0) close(fd);
     }
-    int open(const char* path) {
+    // advice: MADV_SEQUENTIAL for the host decoder, which reads every byte
+    // through the mapping; the GPU decode's header scan touches two pages per
+    // block (pread feeds its uploads)
+    int open(const char* path, int advice = MADV_SEQUENTIAL) {
         fd = ::open(path, O_RDONLY);
         MC_REQUIRE(fd >= 0, MC_E_IO, "cannot open %s: %s", path, strerror(errno));
         struct stat st;
@@ -72,7 +75,7 @@ struct MappedFile {
         void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
         MC_REQUIRE(m != MAP_FAILED, MC_E_IO, "mmap %s failed", path);
         data = (const uint8_t*)m;
-        (void)madvise(m, size, MADV_SEQUENTIAL);   // read ahead: blocks are visited in order
+        if (advice != MADV_NORMAL) (void)madvise(m, size, advice);
         return MC_OK;
     }
 };

@@ -37,7 +37,7 @@ for step in ${STEPS:-tests}; do
     e2e)     # scripts/e2e.py: CLI end to end, host and GPU decode of one 30 M-record BAM
       mkdir -p /tmp/e2e
       timeout -k 10 600 python scripts/e2e.py --reads ${E2E_READS:-30000000} --contigs 1000 --length 1000000 \
-          --dir /tmp/e2e > "$O/${TAG}_e2e.json" 2> "$O/${TAG}_e2e.err"
+          --dir /tmp/e2e ${E2E_ARGS:-} > "$O/${TAG}_e2e.json" 2> "$O/${TAG}_e2e.err"
       s=$?; tail -3 "$O/${TAG}_e2e.err"; python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['gpu_decode_s'],d['gpu_end_to_end_s'],d['gpu_decode_timings'])" "$O/${TAG}_e2e.json"
       faulted "$O/${TAG}_e2e.err"; fatal $s e2e ;;
     gzpmc)   # kernel trace + SQ counter passes over one GPU decode (variant GZ_PMC_VARIANT)
