@@ -523,15 +523,14 @@ MC_HD void lz_copy(uint8_t* q, int len, int dist) {
 // matching paid), and the flush loops over the entries at run time.
 constexpr int kQueue = MC_GZ_QUEUE;
 
-// Literals decoded after a literal in the same symbol step (inflate_block).
-// After bits_refill more than 32 bits are buffered; a first symbol takes at
-// most 15 and each extra literal at most kLitBits <= 8, so two extras never
-// read past the buffered bits.
+// Literals decoded after a literal in the same symbol step (inflate_block),
+// each while at least kLitBits bits are buffered (after bits_refill more than
+// 32 are; a first symbol takes at most 15, an extra literal at most kLitBits).
 #ifndef MC_GZ_LIT_EXTRA
 #define MC_GZ_LIT_EXTRA 2
 #endif
 constexpr int kLitExtra = MC_GZ_LIT_EXTRA;
-static_assert(kLitExtra >= 0 && 32 - 15 - kLitExtra * kLitBits >= 0, "extra literals within the buffered bits");
+static_assert(kLitExtra >= 0, "extra literals");
 static_assert(kQueue >= 1, "match queue: >= 1 entry");
 
 template <class QP>
@@ -656,7 +655,9 @@ MC_HD int inflate_block(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t 
 #pragma unroll
                     for (int x = 0; x < kLitExtra; ++x) {
                         const uint32_t e2 = TL[(uint32_t)b.buf & ((1u << kLitBits) - 1u)];
-                        if (e2 == 0 || e2 >= (256u << 4) || o >= isize) break;
+                        if (e2 == 0 || e2 >= (256u << 4) || o >= isize ||
+                            (33 - 15 - x * kLitBits < kLitBits && b.cnt < kLitBits))
+                            break;
                         const int u = (int)(e2 & 15u);
                         b.buf >>= u;
                         b.cnt -= u;
