@@ -547,6 +547,9 @@ struct MatchQueue {
 #ifndef MC_GZ_FLUSH_BATCH
 #define MC_GZ_FLUSH_BATCH 1
 #endif
+#ifndef MC_GZ_FLUSH_WAIT
+#define MC_GZ_FLUSH_WAIT 1
+#endif
 constexpr int kFlushBatch = MC_GZ_FLUSH_BATCH;
 
 template <class QP>
@@ -582,6 +585,12 @@ MC_HD void mq_flush(MatchQueue<QP>& q, uint8_t* dst) {
         lz_copy(dst + (uint32_t)(e >> 32), (int)(e & 511u), (int)((uint32_t)e >> 9));
     }
     q.n = 0;
+#if defined(__HIP_DEVICE_COMPILE__) && MC_GZ_FLUSH_WAIT
+    // vmcnt(0) here, once per flush: otherwise the compiler's wait for the
+    // flush's loads lands at the join after it, on the symbol loop's common
+    // path, and every symbol step waited for the output stores in flight
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
 }
 
 // One raw deflate stream src[0, clen) into dst[0, isize): kOk iff it ends
