@@ -356,6 +356,10 @@ int mc_bam_gpu_close(mc_bam_gpu* g);
 int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize);
 int mc_bam_rec_parse_host(const uint8_t* r, int64_t len, int32_t n_ref, uint32_t flag_filter,
                           int32_t* out3);
+/* mc_bgzf_scan_host: the GPU decode's BGZF block scan (pread, n_threads
+ * ranges) -> block count, inflated total, the first cap block offsets. */
+int mc_bgzf_scan_host(const char* path, int n_threads, int64_t* n_blocks, int64_t* inflated,
+                      int64_t* offsets, int64_t cap);
 
 /* ---- synthetic BAM writer ------------------------------------------------
  * Writes coordinate-sorted records from SoA arrays as BGZF-compressed BAM

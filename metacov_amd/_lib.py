@@ -140,6 +140,7 @@ SIGNATURES = {
     "mc_bam_gpu_close": [_P],
     "mc_gz_inflate_host": [_P, _I64, _P, _I64],
     "mc_bam_rec_parse_host": [_P, _I64, _I32, _U32, _P],
+    "mc_bgzf_scan_host": [ctypes.c_char_p, ctypes.c_int, _PI64, _PI64, _PI64, _I64],
     # pileup.experimental: read side (host) and sequence side (GPU)
     "mc_reads_open": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _PP],
     "mc_reads_close": [_P],

@@ -50,7 +50,6 @@ using namespace mc::bgzf;
 
 namespace {
 
-constexpr int kGzBlock = 256;
 constexpr int64_t kSeg = 64 << 10;        // inflated bytes per parse segment
 constexpr int kSyncChain = 8;             // records a sync candidate must chain
 constexpr int kPad = 64;                  // readable bytes past a compressed window
@@ -615,66 +614,139 @@ size_t bgzf_hdr(const uint8_t* d, size_t n, size_t o) {
     return bsize >= (size_t)xlen + 20 && o + bsize <= n ? bsize : 0;
 }
 
-// The block list of the whole file, scanned by nt threads: each byte range
-// starts at the first offset that begins a chain of 4 valid headers (or one
-// reaching the end of the file), and the ranges' hops must meet exactly, else
-// one sequential scan (scan_blocks) decides.  (One thread hopping 126,288
-// headers through the mapping took a minor fault per block.)
-int scan_blocks_parallel(const uint8_t* d, size_t n, int nt, std::vector<Block>& blocks, size_t& total) {
+// BGZF header of the block at file offset o, its first bytes in h[0, hn):
+// the block's total size, 0 if none (bgzf_hdr's rules; n = the file size).
+size_t bgzf_hdr_at(const uint8_t* h, size_t hn, size_t o, size_t n) {
+    if (hn < 18 || o + 18 > n || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return 0;
+    const size_t xlen = rd16(h + 10);
+    size_t bsize = 0;
+    for (size_t x = 12; x + 4 <= 12 + xlen && x + 4 <= hn;) {
+        const uint16_t slen = rd16(h + x + 2);
+        if (h[x] == 66 && h[x + 1] == 67 && slen == 2 && x + 6 <= hn) bsize = (size_t)rd16(h + x + 4) + 1;
+        x += 4 + slen;
+    }
+    return bsize >= xlen + 20 && o + bsize <= n ? bsize : 0;
+}
+
+bool pread_all(int fd, uint8_t* buf, size_t len, size_t off) {
+    for (size_t got = 0; got < len;) {
+        const ssize_t r = pread(fd, buf + got, len - got, (off_t)(off + got));
+        if (r <= 0) return false;
+        got += (size_t)r;
+    }
+    return true;
+}
+
+// The block list of the whole file through pread, by nt threads (the GPU
+// decode's scan; no mapping): each of 4 nt byte ranges starts at the first
+// offset of a window that begins a chain of 4 valid headers (or one reaching
+// the end of the file); then one pread per block takes its ISIZE and the next
+// block's header (adjacent in the file).  The ranges' hops must meet exactly,
+// else one sequential hop from offset 0 decides.
+int scan_blocks_pread(int fd, size_t n, int nt, const char* path, std::vector<Block>& blocks, size_t& total) {
+    constexpr size_t kMaxBlock = 65536, kHdr = 96;
     const size_t nr = n < (64u << 20) ? 1 : (size_t)std::max(1, nt) * 4;
     std::vector<size_t> start(nr + 1, n);
     start[0] = 0;
-    auto sync = [&](size_t from) -> size_t {
-        for (size_t q = from; q < n; ++q) {
+    std::atomic<bool> io_err{false};
+    auto sync = [&](size_t from, std::vector<uint8_t>& w) -> size_t {
+        const size_t wl = std::min(n - from, 5 * kMaxBlock + kHdr);
+        w.resize(wl);
+        if (!pread_all(fd, w.data(), wl, from)) {
+            io_err = true;
+            return n;
+        }
+        const bool to_eof = from + wl == n;
+        for (size_t q = 0; q < std::min(wl, kMaxBlock); ++q) {
             size_t z = q;
             int k = 0;
-            for (; k < 4 && z < n; ++k) {
-                const size_t b = bgzf_hdr(d, n, z);
+            for (; k < 4 && z < wl; ++k) {
+                const size_t b = bgzf_hdr(w.data(), wl, z);
                 if (!b) break;
                 z += b;
             }
-            if (k == 4 || z == n) return q;
+            if (k == 4 || (to_eof && z == wl)) return from + q;
         }
-        return n;
+        return n;   // no chain here: the ranges will not meet, the sequential hop decides
+    };
+    // the blocks of [a, end): false unless the hop lands exactly on end
+    // (*stop: the offset it stopped at)
+    size_t seq_stop = 0;
+    auto hop = [&](size_t a, size_t end, std::vector<Block>& out, size_t* stop) -> bool {
+        *stop = a;
+        if (a >= n) return a == end;
+        uint8_t h[4 + kHdr];   // [0, 4): the previous block's ISIZE; [4, 4 + hn): header bytes at o
+        size_t hn = std::min(kHdr, n - a);
+        if (!pread_all(fd, h + 4, hn, a)) {
+            io_err = true;
+            return false;
+        }
+        size_t o = a;
+        while (o < end) {
+            if (hn < 12) return false;
+            const size_t xlen = rd16(h + 4 + 10);
+            size_t b = bgzf_hdr_at(h + 4, hn, o, n);
+            if (!b && 12 + xlen > hn && o + 12 + xlen <= n) {   // a long extra field: read it whole
+                std::vector<uint8_t> big(12 + xlen);
+                if (!pread_all(fd, big.data(), big.size(), o)) {
+                    io_err = true;
+                    return false;
+                }
+                b = bgzf_hdr_at(big.data(), big.size(), o, n);
+            }
+            if (!b) return false;
+            Block blk;
+            blk.off = o;
+            blk.cdata = o + 12 + xlen;
+            blk.clen = b - xlen - 20;
+            blk.out = 0;
+            const size_t nx = o + b;   // ISIZE is the block's last 4 bytes, the next header follows
+            const size_t rl = std::min(4 + kHdr, n - (nx - 4));
+            if (!pread_all(fd, h, rl, nx - 4)) {
+                io_err = true;
+                return false;
+            }
+            blk.isize = rd32(h);
+            hn = rl - 4;
+            out.push_back(blk);
+            o = nx;
+            *stop = o;
+        }
+        return o == end;
     };
     std::vector<std::vector<Block>> part(nr);
     std::vector<char> ok(nr, 1);
-    std::atomic<size_t> next{1};
-    auto w1 = [&]() {
-        for (size_t i; (i = next.fetch_add(1)) < nr;) start[i] = sync(n / nr * i);
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(w1);
-    w1();
-    for (auto& t : pool) t.join();
-    pool.clear();
-    for (size_t i = nr; i-- > 1;) start[i] = std::min(start[i], start[i + 1]);
-    next = 0;
-    auto w2 = [&]() {
-        for (size_t i; (i = next.fetch_add(1)) < nr;) {
-            size_t o = start[i];
-            while (o < start[i + 1]) {
-                const size_t b = bgzf_hdr(d, n, o);
-                if (!b) break;
-                Block blk;
-                blk.off = o;
-                const uint16_t xlen = rd16(d + o + 10);
-                blk.cdata = o + 12 + xlen;
-                blk.clen = b - xlen - 20;
-                blk.isize = rd32(d + o + b - 4);
-                blk.out = 0;
-                part[i].push_back(blk);
-                o += b;
-            }
-            ok[i] = o == start[i + 1];
-        }
-    };
-    for (int t = 1; t < nt; ++t) pool.emplace_back(w2);
-    w2();
-    for (auto& t : pool) t.join();
+    {
+        std::atomic<size_t> next{1};
+        auto w1 = [&]() {
+            std::vector<uint8_t> w;
+            for (size_t i; (i = next.fetch_add(1)) < nr;) start[i] = sync(n / nr * i, w);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(w1);
+        w1();
+        for (auto& t : pool) t.join();
+    }
+    {
+        std::atomic<size_t> next{0};
+        auto w2 = [&]() {
+            size_t stop;
+            for (size_t i; (i = next.fetch_add(1)) < nr;) ok[i] = hop(start[i], start[i + 1], part[i], &stop);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(w2);
+        w2();
+        for (auto& t : pool) t.join();
+    }
+    MC_REQUIRE(!io_err, MC_E_IO, "%s: read failed while scanning the BGZF blocks", path);
     bool chained = true;
     for (char c : ok) chained &= c != 0;
-    if (!chained) return scan_blocks(d, n, 0, SIZE_MAX, blocks, total);
+    if (!chained) {
+        part.assign(1, {});
+        MC_REQUIRE(hop(0, n, part[0], &seq_stop), MC_E_IO,
+                   "%s: no valid BGZF block at offset %zu (truncated, or not bgzip-compressed BAM)", path, seq_stop);
+        MC_REQUIRE(!io_err, MC_E_IO, "%s: read failed while scanning the BGZF blocks", path);
+    }
     for (auto& p : part)
         for (Block& b : p) {
             b.out = total;
@@ -850,20 +922,10 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
     return MC_OK;
 }
 
-// The header scan's mapping advice (MC_SCAN_ADVICE = random | normal |
-// sequential; A/B knob, default random: no read-around of the pages between
-// two headers, which the scan never reads)
-static int scan_advice() {
-    const char* e = getenv("MC_SCAN_ADVICE");
-    if (e && !strcmp(e, "normal")) return MADV_NORMAL;
-    if (e && !strcmp(e, "sequential")) return MADV_SEQUENTIAL;
-    return MADV_RANDOM;
-}
-
 int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     const double t_start = now_s();
     MappedFile mf;
-    if (int rc = mf.open(g->path.c_str(), scan_advice())) return rc;
+    if (int rc = mf.open(g->path.c_str(), false)) return rc;
     std::vector<Block> blocks;
     size_t total = 0;
     // A file likely to decode resident has its first bytes uploaded (the
@@ -896,7 +958,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
             });
         }
     }
-    if (int rc = scan_blocks_parallel(mf.data, mf.size, g->nt, blocks, total)) return rc;
+    if (int rc = scan_blocks_pread(mf.fd, mf.size, g->nt, g->path.c_str(), blocks, total)) return rc;
     g->t_scan = (now_s() - t_start) * 1e3;
     if (spec.t.joinable()) {
         const double t0 = now_s();
@@ -1198,6 +1260,22 @@ extern "C" int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst
     const int rc = mc::gz::inflate_block(padded.data(), clen, dst, isize, scratch.data(), TL,
                                          TL + (1 << mc::gz::kLitBits), SL, SL + mc::gz::kLitSyms, ring, queue);
     MC_REQUIRE(rc == 0, MC_E_IO, "inflate failed: %s", gz_err_msg(rc));
+    return MC_OK;
+}
+
+// The GPU decode's BGZF block scan on the host (unit tests): block count,
+// inflated total and up to cap block offsets.
+extern "C" int mc_bgzf_scan_host(const char* path, int n_threads, int64_t* n_blocks, int64_t* inflated,
+                                 int64_t* offsets, int64_t cap) {
+    MC_REQUIRE(path && n_blocks && inflated && cap >= 0 && (offsets || cap == 0), MC_E_INVALID, "bad argument");
+    MappedFile f;
+    if (int rc = f.open(path, false)) return rc;
+    std::vector<Block> blocks;
+    size_t total = 0;
+    if (int rc = scan_blocks_pread(f.fd, f.size, std::max(1, n_threads), path, blocks, total)) return rc;
+    *n_blocks = (int64_t)blocks.size();
+    *inflated = (int64_t)total;
+    for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)blocks.size()); ++i) offsets[i] = (int64_t)blocks[i].off;
     return MC_OK;
 }
 

@@ -62,20 +62,21 @@ struct MappedFile {
         if (data && size) munmap((void*)data, size);
         if (fd >= 0) close(fd);
     }
-    // advice: MADV_SEQUENTIAL for the host decoder, which reads every byte
-    // through the mapping; the GPU decode's header scan touches two pages per
-    // block (pread feeds its uploads)
-    int open(const char* path, int advice = MADV_SEQUENTIAL) {
+    // map = false: the descriptor and size only (the GPU decode reads through
+    // pread: unmapping a multi-GB mapping whose header pages the scan had
+    // faulted in cost ~60 ms at the end of its open)
+    int open(const char* path, bool map = true) {
         fd = ::open(path, O_RDONLY);
         MC_REQUIRE(fd >= 0, MC_E_IO, "cannot open %s: %s", path, strerror(errno));
         struct stat st;
         MC_REQUIRE(fstat(fd, &st) == 0, MC_E_IO, "cannot stat %s", path);
         size = (size_t)st.st_size;
         MC_REQUIRE(size > 0, MC_E_IO, "%s is empty", path);
+        if (!map) return MC_OK;
         void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
         MC_REQUIRE(m != MAP_FAILED, MC_E_IO, "mmap %s failed", path);
         data = (const uint8_t*)m;
-        if (advice != MADV_NORMAL) (void)madvise(m, size, advice);
+        (void)madvise(m, size, MADV_SEQUENTIAL);   // read ahead: blocks are visited in order
         return MC_OK;
     }
 };

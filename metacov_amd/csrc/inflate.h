@@ -28,7 +28,7 @@ namespace gz {
 #define MC_HD __host__ __device__ __forceinline__
 
 #ifndef MC_GZ_QUEUE
-#define MC_GZ_QUEUE 8           // matches a lane defers (>= 1)
+#define MC_GZ_QUEUE 16          // matches a lane defers (>= 1)
 #endif
 #ifndef MC_GZ_COPY_BATCH
 #define MC_GZ_COPY_BATCH 2      // lz_copy: 2 = 16-byte chunks (dist >= 16), 1 = byte groups, 0 = byte loop
@@ -36,7 +36,7 @@ namespace gz {
 
 // Tuning knobs (scripts/gz_ab.py): primary table bits, tables in LDS.
 #ifndef MC_GZ_LIT_BITS
-#define MC_GZ_LIT_BITS 7        // primary table index bits (7 / 5 with an 8-entry queue: 6 waves per CU)
+#define MC_GZ_LIT_BITS 7        // primary table index bits (7 / 5-bit tables, 6 waves per CU)
 #endif
 #ifndef MC_GZ_DIST_BITS
 #define MC_GZ_DIST_BITS 5

@@ -352,3 +352,39 @@ def test_cli_gpu_decode_windows_vs_oracle(lib_built, tmp_path):
                                           "--window-bytes", str(1 << 20)])
     assert res.exit_code == 0, res.output
     assert open(o, newline="").read() == out.getvalue()
+
+
+def test_bgzf_scan_host(lib_built, golden_dir, tmp_path):
+    """The GPU decode's pread block scan (no GPU) finds every BGZF block of
+    the golden and synthetic BAMs, with its range split on (many threads on
+    a multi-range file) or off, and fails on a truncated file."""
+    import numpy as np
+    from metacov_amd import synth
+    lib = _lib()
+    paths = [os.path.join(golden_dir, f) for f in sorted(os.listdir(golden_dir)) if f.endswith(".bam")]
+    big = str(tmp_path / "big.bam")
+    lengths = np.full(4, 2_000_000, np.int64)
+    arrs = synth.edge_mix_arrays(lengths, 1_200_000, seed=3)
+    synth.write_bam_fast(big, ["c%d" % i for i in range(4)], lengths, *arrs, level=1, n_threads=8)
+    assert os.path.getsize(big) > 64 << 20     # several scan ranges
+    paths.append(big)
+    for p in paths:
+        raw = open(p, "rb").read()
+        want, o = [], 0
+        for payload, isize in _bgzf_blocks(raw):
+            want.append(isize)
+        offs, o = [], 0
+        while o < len(raw):
+            offs.append(o)
+            o += struct.unpack_from("<H", raw, o + 16)[0] + 1
+        for nt in (1, 3, 16):
+            nb, tot = ctypes.c_int64(), ctypes.c_int64()
+            got = (ctypes.c_int64 * len(offs))()
+            assert lib.mc_bgzf_scan_host(p.encode(), nt, ctypes.byref(nb), ctypes.byref(tot), got, len(offs)) == 0
+            assert nb.value == len(offs) and tot.value == sum(want)
+            assert list(got) == offs, (p, nt)
+    t = tmp_path / "trunc.bam"
+    raw = open(big, "rb").read()
+    t.write_bytes(raw[: len(raw) // 2 + 1000])
+    nb, tot = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.mc_bgzf_scan_host(str(t).encode(), 16, ctypes.byref(nb), ctypes.byref(tot), None, 0) != 0
