@@ -941,7 +941,8 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
             if (t.joinable()) t.join();
         }
     } spec;
-    if (window_bytes <= 0 && mf.size >= (size_t)(256ull << 20)) {
+    const char* spec_env = getenv("MC_SPEC_UPLOAD");   // A/B knob: 0 = scan first, then upload
+    if (window_bytes <= 0 && mf.size >= (size_t)(256ull << 20) && !(spec_env && spec_env[0] == '0')) {
         size_t free_b = 0, tot_b = 0;
         HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
         if (mf.size * 4 <= free_b / 2) {
@@ -958,7 +959,9 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
             });
         }
     }
-    if (int rc = scan_blocks_pread(mf.fd, mf.size, g->nt, g->path.c_str(), blocks, total)) return rc;
+    const char* st_env = getenv("MC_SCAN_THREADS");    // A/B knob (default: the decode's threads)
+    const int scan_nt = st_env && atoi(st_env) > 0 ? atoi(st_env) : g->nt;
+    if (int rc = scan_blocks_pread(mf.fd, mf.size, scan_nt, g->path.c_str(), blocks, total)) return rc;
     g->t_scan = (now_s() - t_start) * 1e3;
     if (spec.t.joinable()) {
         const double t0 = now_s();

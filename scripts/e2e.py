@@ -31,10 +31,10 @@ def main():
     ap.add_argument("--gpu-windows", default="",
                     help="comma-separated inflated window sizes in MiB: extra GPU decodes of the same file, "
                          "timed (window_sweep in the JSON)")
-    ap.add_argument("--advice", default="",
-                    help="comma-separated MC_SCAN_ADVICE values: extra resident GPU decodes per value, in rounds "
-                         "(advice_sweep in the JSON)")
-    ap.add_argument("--advice-rounds", type=int, default=2)
+    ap.add_argument("--env-sweep", default="",
+                    help="';'-separated settings 'K=V[,K=V]' of the decode's environment knobs: extra resident GPU "
+                         "decodes per setting, in rounds (env_sweep in the JSON)")
+    ap.add_argument("--sweep-rounds", type=int, default=2)
     a = ap.parse_args()
     import numpy as np
     from metacov_amd import synth, regions as mreg
@@ -104,18 +104,25 @@ def main():
                       ("read_ms", "inflate_ms", "parse_ms", "scan_ms", "total_ms", "windows", "upload_ms", "kernel_ms", "open_ms")}})
         print(json.dumps(sweep[-1]), file=sys.stderr, flush=True)
     advice = []
-    for r in range(a.advice_rounds if a.advice else 0):
-        for adv in a.advice.split(","):
-            os.environ["MC_SCAN_ADVICE"] = adv
+    settings = [x for x in a.env_sweep.split(";") if x]
+    for r in range(a.sweep_rounds if settings else 0):
+        for st in settings:
+            kv = dict(x.split("=", 1) for x in st.split(","))
+            saved = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
             t0 = time.perf_counter()
             gw = GpuBamFile(path, device=0, n_threads=a.threads)
             dt = time.perf_counter() - t0
             wt = gw.timings()
             assert gw.n_kept == n_kept
             gw.close()
-            advice.append({"advice": adv, "round": r, "decode_s": dt, **wt})
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            advice.append({"env": st, "round": r, "decode_s": dt, **wt})
             print(json.dumps(advice[-1]), file=sys.stderr, flush=True)
-    os.environ.pop("MC_SCAN_ADVICE", None)
     print(json.dumps({
         "bam_bytes": os.path.getsize(path), "records": n_rec, "kept": n_kept,
         "aligned_bases": bases, "host_threads": a.threads,
@@ -129,7 +136,7 @@ def main():
         "gpu_decode_s": t_gdec, "gpu_decode_timings": gtm, "gpu_ingest_s": t_ging,
         "gpudec_stats_csv_s": t_cmp3, "gpu_end_to_end_s": t_gdec + t_ging + t_cmp3,
         "gpu_end_to_end_aligned_bases_per_s": bases / (t_gdec + t_ging + t_cmp3),
-        "window_sweep": sweep, "advice_sweep": advice}))
+        "window_sweep": sweep, "env_sweep": advice}))
     os.remove(path)
 
 

@@ -11,7 +11,7 @@ TAG=${TAG:?set TAG}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
+B="$R/bench.py --steps ${PROF_STEPS:-10} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_${TAG}_trace" -o run \
     -- python3 $B > "$O/prof_${TAG}_trace.log" 2>&1 || { echo "trace pass failed"; tail -5 "$O/prof_${TAG}_trace.log"; exit 1; }
 tail -1 "$O/prof_${TAG}_trace.log"
