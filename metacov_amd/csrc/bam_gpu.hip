@@ -365,7 +365,10 @@ const char* gz_err_msg(int e) {
 #ifndef MC_UPLOAD_SLICE_MIB
 #define MC_UPLOAD_SLICE_MIB 64
 #endif
-int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst, hipStream_t st) {
+// progress (optional): file offset below which every byte is on the device
+// (advanced as copies complete); cancel (optional): stop at the next slice.
+int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst, hipStream_t st,
+                      std::atomic<size_t>* progress = nullptr, const std::atomic<bool>* cancel = nullptr) {
     constexpr size_t kSlice = (size_t)MC_UPLOAD_SLICE_MIB << 20;
     constexpr int kStage = 3;
     if (len == 0) return MC_OK;
@@ -399,6 +402,7 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
                 cv.wait(lk, [&] { return k < free_upto || stop; });
                 if (stop) return;
             }
+            if (cancel && cancel->load(std::memory_order_relaxed)) return;
             const size_t at = (size_t)k * kSlice, n = std::min(kSlice, len - at);
             const size_t a = n * t / nt, b = n * (t + 1) / nt;
             uint8_t* buf = g->stage[k % kStage].p;
@@ -428,7 +432,12 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
         for (auto& th : pool) th.join();
     };
     int rc = MC_OK;
+    bool cancelled = false;
     for (int64_t k = 0; k < ns && rc == MC_OK; ++k) {
+        if (cancel && cancel->load(std::memory_order_relaxed)) {
+            cancelled = true;
+            break;
+        }
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return parts[k] == nt || bad; });
@@ -446,6 +455,7 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
         const int64_t j = k - 1;
         if (e == hipSuccess && j >= 0 && j + kStage < ns) {
             e = hipEventSynchronize(done[j % kStage]);
+            if (e == hipSuccess && progress) progress->store(off + (size_t)(j + 1) * kSlice, std::memory_order_release);
             std::lock_guard<std::mutex> lk(mu);
             free_upto = j + kStage + 1;
             cv.notify_all();
@@ -458,6 +468,7 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     finish();
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(st));
+    if (progress && !cancelled) progress->store(off + len, std::memory_order_release);
     return MC_OK;
 }
 
@@ -803,19 +814,34 @@ int header_from_prefix(mc_bam_gpu* g, size_t n, int64_t* o, bool* ok) {
 static_assert(MC_GZ_PIECE_STREAMS >= 1 && MC_GZ_PIECE_STREAMS <= 4, "inflate streams: stream + kstream[]");
 constexpr int kGzPieceStreams = MC_GZ_PIECE_STREAMS;
 
+// The background upload of a file likely to decode resident: the whole file
+// goes up while its blocks are scanned (the upload needs no block list, the
+// scan no device); the resident pipeline launches each piece once `progress`
+// has passed its bytes.
+struct BgUpload {
+    std::thread t;
+    std::atomic<size_t> progress{0};
+    std::atomic<bool> cancel{false}, finished{false};
+    int rc = MC_OK;
+    std::string msg;
+    int join() {   // the upload's status
+        if (t.joinable()) t.join();
+        if (rc) mc::set_error("%s", msg.c_str());
+        return rc;
+    }
+    ~BgUpload() {
+        cancel = true;
+        if (t.joinable()) t.join();
+    }
+};
+
 int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<Block>& blocks, size_t total,
-                        int64_t max_lanes, size_t pre) {
+                        int64_t max_lanes, BgUpload* bg) {
     const int64_t nb = (int64_t)blocks.size();
     hipStream_t st = g->stream;
     const size_t piece = std::min<size_t>(4ull << 30, std::max<size_t>(256ull << 20, total / MC_GZ_PIECES));
     std::vector<std::pair<size_t, size_t>> pcs;
-    // file bytes [0, pre) are on the device already (uploaded during the
-    // scan): the first piece is the blocks they hold whole
-    auto cend_of = [&](size_t b) { return b + 1 < blocks.size() ? blocks[b + 1].off : mf.size; };
-    size_t first = 0;
-    while (first < blocks.size() && cend_of(first) <= pre) ++first;
-    if (first) pcs.emplace_back(0, first);
-    for (size_t b0 = first; b0 < blocks.size();) {
+    for (size_t b0 = 0; b0 < blocks.size();) {
         size_t b1 = b0, sz = 0;
         while (b1 < blocks.size() && (b1 == b0 || sz + blocks[b1].isize <= piece)) sz += blocks[b1++].isize;
         pcs.emplace_back(b0, b1);
@@ -867,10 +893,22 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
         const size_t b0 = pcs[p].first, b1 = pcs[p].second;
         const size_t coff = blocks[b0].off, cend = b1 < blocks.size() ? blocks[b1].off : mf.size;
         const double t0 = now_s();
-        // returns once the bytes are on the device (its stream synchronised);
-        // bytes below pre are there already
-        const size_t ulo = std::max(coff, std::min(pre, cend));
-        if (int rc = upload_file_range(g, mf.fd, ulo, cend - ulo, g->comp[0].p + ulo, g->up_stream)) return rc;
+        if (bg) {
+            // the background upload has passed the piece (its copies are
+            // complete, so the bytes are visible to any stream)
+            while (bg->progress.load(std::memory_order_acquire) < cend) {
+                if (bg->finished.load(std::memory_order_acquire)) {
+                    if (int rc = bg->join()) return rc;
+                    MC_REQUIRE(bg->progress.load() >= cend, MC_E_IO, "%s: background upload stopped early",
+                               g->path.c_str());
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+        } else {
+            // returns once the bytes are on the device (its stream synchronised)
+            if (int rc = upload_file_range(g, mf.fd, coff, cend - coff, g->comp[0].p + coff, g->up_stream))
+                return rc;
+        }
         if (p == 0) {
             g->t_read += (now_s() - t0) * 1e3;   // the exposed part: the first piece
             t_first = now_s();
@@ -932,30 +970,23 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     // first piece's worth) while the block headers are scanned: the upload
     // needs no block list, the scan no device.  (If the file turns out not to
     // be resident, the windowed decode uploads its windows itself.)
-    size_t pre = 0;
-    struct Spec {
-        std::thread t;
-        int rc = MC_OK;
-        std::string msg;
-        ~Spec() {
-            if (t.joinable()) t.join();
-        }
-    } spec;
-    const char* spec_env = getenv("MC_SPEC_UPLOAD");   // A/B knob: 0 = scan first, then upload
+    BgUpload bg;
+    const char* spec_env = getenv("MC_SPEC_UPLOAD");   // A/B knob: 0 = scan first, then upload per piece
     if (window_bytes <= 0 && mf.size >= (size_t)(256ull << 20) && !(spec_env && spec_env[0] == '0')) {
         size_t free_b = 0, tot_b = 0;
         HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
         if (mf.size * 4 <= free_b / 2) {
             HIP_TRY(g->comp[0].reserve(mf.size + kPad));
-            pre = std::min<size_t>(mf.size / MC_GZ_PIECES, 1536ull << 20);
-            spec.t = std::thread([&]() {
+            bg.t = std::thread([&]() {
                 if (hipSetDevice(g->device) != hipSuccess) {
-                    spec.rc = MC_E_HIP;
-                    spec.msg = "hipSetDevice failed in the upload thread";
-                    return;
+                    bg.rc = MC_E_HIP;
+                    bg.msg = "hipSetDevice failed in the upload thread";
+                } else {
+                    bg.rc = upload_file_range(g, mf.fd, 0, mf.size, g->comp[0].p, g->up_stream, &bg.progress,
+                                              &bg.cancel);
+                    if (bg.rc) bg.msg = mc::last_error();
                 }
-                spec.rc = upload_file_range(g, mf.fd, 0, pre, g->comp[0].p, g->up_stream);
-                if (spec.rc) spec.msg = mc::last_error();
+                bg.finished.store(true, std::memory_order_release);
             });
         }
     }
@@ -963,15 +994,6 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     const int scan_nt = st_env && atoi(st_env) > 0 ? atoi(st_env) : g->nt;
     if (int rc = scan_blocks_pread(mf.fd, mf.size, scan_nt, g->path.c_str(), blocks, total)) return rc;
     g->t_scan = (now_s() - t_start) * 1e3;
-    if (spec.t.joinable()) {
-        const double t0 = now_s();
-        spec.t.join();
-        g->t_read = (now_s() - t0) * 1e3;   // the part of the first upload not hidden by the scan
-        if (spec.rc) {
-            mc::set_error("%s", spec.msg.c_str());
-            return spec.rc;
-        }
-    }
     g->blocks = (int64_t)blocks.size();
     g->inflated_bytes = (int64_t)total;
     g->compressed_bytes = (int64_t)mf.size;
@@ -997,10 +1019,17 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         const size_t need = mf.size + total + blocks.size() * (sizeof(GzBlock) + sizeof(int)) +
                             (size_t)kGzPieceStreams * (size_t)max_lanes * kGzSlotWords * sizeof(uint16_t);
         if (need <= free_b / 2) {
-            const int rc = gpu_decode_resident(g, mf, blocks, total, max_lanes, pre);
+            const int rc = gpu_decode_resident(g, mf, blocks, total, max_lanes, bg.t.joinable() ? &bg : nullptr);
+            if (rc == MC_OK && bg.t.joinable()) {
+                if (int urc = bg.join()) return urc;
+            }
             g->t_total = (now_s() - t_start) * 1e3;
             return rc;
         }
+    }
+    if (bg.t.joinable()) {   // not resident after all: the windows upload their own bytes
+        bg.cancel = true;
+        bg.t.join();
     }
     // windows of blocks (<= win inflated bytes each, at least one block)
     std::vector<std::pair<size_t, size_t>> wins;

@@ -527,7 +527,7 @@ constexpr int kQueue = MC_GZ_QUEUE;
 // each while at least kLitBits bits are buffered (after bits_refill more than
 // 32 are; a first symbol takes at most 15, an extra literal at most kLitBits).
 #ifndef MC_GZ_LIT_EXTRA
-#define MC_GZ_LIT_EXTRA 3
+#define MC_GZ_LIT_EXTRA 4
 #endif
 constexpr int kLitExtra = MC_GZ_LIT_EXTRA;
 static_assert(kLitExtra >= 0, "extra literals");
