@@ -389,7 +389,9 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
         }
     } guard{done};
     const int64_t ns = (int64_t)((len + kSlice - 1) / kSlice);
-    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)g->nt, std::min(len, kSlice) >> 20));
+    const char* ut_env = getenv("MC_UPLOAD_THREADS");   // A/B knob (default: the decode's threads)
+    const size_t unt = ut_env && atoi(ut_env) > 0 ? (size_t)atoi(ut_env) : (size_t)g->nt;
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>(unt, std::min(len, kSlice) >> 20));
     std::mutex mu;
     std::condition_variable cv;
     int64_t free_upto = std::min<int64_t>(ns, kStage);   // slices [0, free_upto) may be read
