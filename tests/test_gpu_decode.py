@@ -232,6 +232,43 @@ def test_gpu_decode_large(lib_built, tmp_path, level, window):
 
 
 @pytest.mark.gpu
+def test_gpu_decode_background_upload(lib_built, tmp_path):
+    """A file >= 256 MiB decodes resident with the whole upload running in the
+    background while its blocks are scanned: equal to the host decoder; a
+    truncated copy (the scan fails while the upload runs) and a copy with a
+    corrupt block near its end (the inflate fails after the upload) raise
+    without hanging."""
+    from metacov_amd.bam import GpuBamFile
+    lengths = [20_000_000, 30_000_000]
+    arrs = synth.edge_mix_arrays(lengths, 2_000_000, seed=5)
+    p = str(tmp_path / "bg.bam")
+    synth.write_bam_fast(p, ["a", "b"], lengths, *arrs, level=1, n_threads=8)
+    size = os.path.getsize(p)
+    assert size >= 256 << 20, size
+    h, g = _host_and_gpu(p)
+    _assert_same(h, g)
+    t = g.timings()
+    assert t["windows"] >= 2 and t["upload_ms"] > 0
+    g.close()
+    raw = open(p, "rb").read()
+    tr = tmp_path / "bg_trunc.bam"
+    tr.write_bytes(raw[: len(raw) * 2 // 3])
+    with pytest.raises(MetacovError):
+        GpuBamFile(str(tr))
+    b = bytearray(raw)
+    off = len(raw) - (1 << 20)
+    while raw[off:off + 4] != b"\x1f\x8b\x08\x04":
+        off += 1
+    for k in range(40, 400):
+        b[off + k] ^= 0x5a
+    cr = tmp_path / "bg_corrupt.bam"
+    cr.write_bytes(bytes(b))
+    del raw, b
+    with pytest.raises(MetacovError, match="inflate|record|CIGAR|BGZF"):
+        GpuBamFile(str(cr))
+
+
+@pytest.mark.gpu
 def test_gpu_decode_long_records(lib_built, tmp_path):
     """Records of 30-200 KB (long reads with their sequence): most 64 KiB
     parse segments hold no record start."""
