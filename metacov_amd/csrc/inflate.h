@@ -5,12 +5,13 @@
 // threads; at 16 threads it is the end-to-end bound of `metacov pileup`
 // (profiles/r03pp_e2e.json: 1.56 s of 1.78 s for a 5.2 GB BAM).  Here every
 // BGZF block (<= 64 KiB out, an independent deflate stream) is one lane's
-// work: a 64-bit bit buffer fed by 16-byte loads, canonical Huffman codes
-// decoded by a primary lookup table (MC_GZ_LIT_BITS = 8 bits literal/length,
-// MC_GZ_DIST_BITS = 6 bits distance; longer codes by the count/symbol walk of
-// RFC 1951 §3.2.2 over counts in registers and the canonical symbol lists),
-// LZ77 copies from the lane's own output, queued per lane.  The kernel keeps
-// the primary tables and the symbol lists of each lane in LDS (bam_gpu.hip);
+// work: a 64-bit bit buffer fed from a per-lane LDS ring of input words,
+// canonical Huffman codes decoded by a primary lookup table (MC_GZ_LIT_BITS =
+// 7 bits literal/length, MC_GZ_DIST_BITS = 5 bits distance; longer codes by
+// branch-free compares against the left-aligned length bounds, held in
+// registers, into byte symbol lists), up to MC_GZ_LIT_EXTRA more literals per
+// step, LZ77 copies from the lane's own output queued per lane.  The kernel
+// keeps each lane's tables, symbol lists, ring and queue in LDS (bam_gpu.hip);
 // the build's counts and code lengths in a per-lane global scratch slot
 // (kScratchWords u16).
 //
