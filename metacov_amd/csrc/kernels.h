@@ -1172,16 +1172,23 @@ long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __re
 
 // The fill pass on the end words ingest_kernel<true> wrote (4 B per read
 // instead of the 12 B tuples long_fill_kernel re-reads: 0.2 instead of 0.6
-// GB at C5).  Same buckets and slots; a round takes kFillSubs sub-ranges
-// (kFillSubs int4 of end words per thread, all loaded before the round's
-// first barrier) and its window starts at the tile of its smallest end (ends
-// are not sorted, starts are).  One sub-range per round paid the five
-// barriers and the global slot reservation (an L2 atomic round trip) per
-// 1024 reads: 0.168 ms at C5, half of HBM speed.
+// GB at C5).  Same buckets and slots.  A round takes kFillSubs sub-ranges
+// (kFillSubs int4 of end words per thread) and its window starts at the tile
+// of its smallest end (ends are not sorted, starts are).  The per-tile counts
+// are split into kFillStripes lane-striped counters whose atomics return each
+// event's rank in its stripe: the lanes of a wave end in few tiles, and one
+// counter per tile serialised their atomics (SQ: LDS bank-conflict cycles 2.5x
+// the LDS-active cycles, waves waiting on LDS 36 % of their cycles), with a
+// second atomic pass for the ranks.
 #ifndef MC_LONG_FILL_SUBS
 #define MC_LONG_FILL_SUBS 4
 #endif
+#ifndef MC_LONG_FILL_STRIPES
+#define MC_LONG_FILL_STRIPES 8
+#endif
 constexpr int kFillSubs = MC_LONG_FILL_SUBS;
+constexpr int kFillStripes = MC_LONG_FILL_STRIPES;
+static_assert((kFillStripes & (kFillStripes - 1)) == 0 && kFillStripes <= 64, "stripes: a power of two <= 64");
 
 __global__ void __launch_bounds__(kBlock)
 long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, int lcw,
@@ -1189,11 +1196,13 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
                        int32_t* __restrict__ ev) {
     static_assert(kLongPer == 4, "one int4 of end words per thread and sub-range");
     constexpr int kE = 4 * kFillSubs;     // end words per thread and round
-    __shared__ int wt[kLongTileWin];      // counts, then ranks
-    __shared__ int wb[kLongTileWin];      // first slot of the round's events per tile
+    constexpr int kW = kLongTileWin * kFillStripes;
+    __shared__ int wt[kW];                // per (tile, stripe): count (ranks come back from the atomics)
+    __shared__ int wb[kW];                // per (tile, stripe): first slot
     __shared__ unsigned red[kWaves];
     const int64_t cmask = ((int64_t)1 << lcw) - 1;
-    for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
+    const int stripe = (int)(threadIdx.x & (kFillStripes - 1));
+    for (int k = threadIdx.x; k < kW; k += kBlock) wt[k] = 0;
     const int64_t r0 = blockIdx.x * per, r1 = min(n, r0 + per);
     for (int64_t sub = r0; sub < r1; sub += (int64_t)kLongSub * kFillSubs) {
         uint32_t e[kE];
@@ -1219,23 +1228,32 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
         __syncthreads();
         m = min(min(red[0], red[1]), min(red[2], red[3]));
         const int64_t TB = m == ~0u ? 0 : (int64_t)(m / kTileW);
-        int te[kE];
+        int te[kE];     // (window tile, stripe) counter index, or -1
+        int rk[kE];     // rank in that counter
 #pragma unroll
         for (int k = 0; k < kE; ++k) {
             te[k] = -1;
+            rk[k] = 0;
             if (e[k] == ~0u) continue;
             const int64_t t = (int64_t)(e[k] / kTileW);
             if (t - TB < kLongTileWin) {
-                te[k] = (int)(t - TB);
-                atomicAdd(&wt[te[k]], 1);
+                te[k] = (int)(t - TB) * kFillStripes + stripe;
+                rk[k] = atomicAdd(&wt[te[k]], 1);
             }
         }
         __syncthreads();
-        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) {
-            const int v = wt[k];
-            if (v) {
-                wb[k] = (int)(tile_off[TB + k] + atomicAdd(&cursor[TB + k], (unsigned)v));
-                wt[k] = 0;
+        for (int t = threadIdx.x; t < kLongTileWin; t += kBlock) {
+            int tot = 0;
+#pragma unroll
+            for (int q = 0; q < kFillStripes; ++q) tot += wt[t * kFillStripes + q];
+            if (tot) {
+                int at = (int)(tile_off[TB + t] + atomicAdd(&cursor[TB + t], (unsigned)tot));
+#pragma unroll
+                for (int q = 0; q < kFillStripes; ++q) {
+                    wb[t * kFillStripes + q] = at;
+                    at += wt[t * kFillStripes + q];
+                    wt[t * kFillStripes + q] = 0;
+                }
             }
         }
         __syncthreads();
@@ -1244,16 +1262,14 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
             if (e[k] == ~0u) continue;
             int64_t slot;
             if (te[k] >= 0) {
-                slot = wb[te[k]] + atomicAdd(&wt[te[k]], 1);
+                slot = wb[te[k]] + rk[k];
             } else {
                 const int64_t t = (int64_t)(e[k] / kTileW);
                 slot = tile_off[t] + atomicAdd(&cursor[t], 1u);
             }
             ev[slot] = (int32_t)((int64_t)e[k] & cmask);   // chunk-relative end
         }
-        __syncthreads();
-        for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
-        __syncthreads();
+        __syncthreads();   // wb is read before the next round's phase 2 rewrites it
     }
 }
 
