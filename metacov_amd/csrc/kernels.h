@@ -1174,17 +1174,17 @@ long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __re
 // instead of the 12 B tuples long_fill_kernel re-reads: 0.2 instead of 0.6
 // GB at C5).  Same buckets and slots.  A round takes kFillSubs sub-ranges
 // (kFillSubs int4 of end words per thread) and its window starts at the tile
-// of its smallest end (ends are not sorted, starts are).  The per-tile counts
-// are split into kFillStripes lane-striped counters whose atomics return each
-// event's rank in its stripe: the lanes of a wave end in few tiles, and one
-// counter per tile serialised their atomics (SQ: LDS bank-conflict cycles 2.5x
-// the LDS-active cycles, waves waiting on LDS 36 % of their cycles), with a
-// second atomic pass for the ranks.
+// of its smallest end (ends are not sorted, starts are).  The count atomics
+// return each event's rank in its tile (round 3 took the ranks in a second
+// atomic pass; SQ: LDS bank-conflict cycles 2.5x the LDS-active cycles, waves
+// waiting on LDS 36 % of their cycles): C5 call 1.670 -> 1.634 ms.  Counters
+// striped over 8 / 16 lanes (kFillStripes) measured 1.680 / 1.686 ms
+// (profiles/r04/r04o_long_fill_ab.txt).
 #ifndef MC_LONG_FILL_SUBS
 #define MC_LONG_FILL_SUBS 4
 #endif
 #ifndef MC_LONG_FILL_STRIPES
-#define MC_LONG_FILL_STRIPES 8
+#define MC_LONG_FILL_STRIPES 1
 #endif
 constexpr int kFillSubs = MC_LONG_FILL_SUBS;
 constexpr int kFillStripes = MC_LONG_FILL_STRIPES;
