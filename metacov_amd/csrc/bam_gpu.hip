@@ -396,7 +396,7 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     std::condition_variable cv;
     int64_t free_upto = std::min<int64_t>(ns, kStage);   // slices [0, free_upto) may be read
     std::vector<int> parts(ns, 0);                     // parts of each slice read
-    bool bad = false, stop = false;
+    bool bad = false, stop = false, quit = false;   // quit: a reader saw cancel
     auto reader = [&](int t) {
         for (int64_t k = 0; k < ns; ++k) {
             {
@@ -404,7 +404,12 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
                 cv.wait(lk, [&] { return k < free_upto || stop; });
                 if (stop) return;
             }
-            if (cancel && cancel->load(std::memory_order_relaxed)) return;
+            if (cancel && cancel->load(std::memory_order_relaxed)) {
+                std::lock_guard<std::mutex> lk(mu);   // the main loop may wait for this slice
+                quit = true;
+                cv.notify_all();
+                return;
+            }
             const size_t at = (size_t)k * kSlice, n = std::min(kSlice, len - at);
             const size_t a = n * t / nt, b = n * (t + 1) / nt;
             uint8_t* buf = g->stage[k % kStage].p;
@@ -442,7 +447,11 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
         }
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return parts[k] == nt || bad; });
+            cv.wait(lk, [&] { return parts[k] == nt || bad || quit; });
+            if (quit && parts[k] != nt && !bad) {
+                cancelled = true;
+                break;
+            }
             if (bad) {
                 mc::set_error("%s: read failed in [%zu, %zu)", g->path.c_str(), off, off + len);
                 rc = MC_E_IO;
