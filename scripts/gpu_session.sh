@@ -34,6 +34,11 @@ for step in ${STEPS:-tests}; do
       s=$?; tail -2 "$O/${TAG}_smoke.log"; faulted "$O/${TAG}_smoke.log"; fatal $s smoke ;;
     prof)
       TAG=${PROF_TAG:?} bash "$R/scripts/profile.sh"; s=$?; fatal $s prof ;;
+    hostreg) # scripts/micro/hostreg_probe: DMA from a registered page-cache mapping vs pread staging
+      head -c $((2048 << 20)) /dev/urandom > /tmp/hostreg.bin && cat /tmp/hostreg.bin > /dev/null
+      timeout -k 10 120 "$R/scripts/micro/hostreg_probe" /tmp/hostreg.bin 256 > "$O/${TAG}_hostreg.txt" 2>&1
+      s=$?; cat "$O/${TAG}_hostreg.txt"; [ $s -eq 0 ] && timeout -k 10 120 "$R/scripts/micro/hostreg_probe" /tmp/hostreg.bin 64 >> "$O/${TAG}_hostreg.txt" 2>&1
+      s=$?; tail -4 "$O/${TAG}_hostreg.txt"; rm -f /tmp/hostreg.bin; faulted "$O/${TAG}_hostreg.txt"; fatal $s hostreg ;;
     e2e)     # scripts/e2e.py: CLI end to end, host and GPU decode of one 30 M-record BAM
       mkdir -p /tmp/e2e
       timeout -k 10 600 python scripts/e2e.py --reads ${E2E_READS:-30000000} --contigs 1000 --length 1000000 \
