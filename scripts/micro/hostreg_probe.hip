@@ -12,6 +12,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 #include <vector>
+#include <atomic>
+#include <thread>
 
 static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -93,6 +95,39 @@ int main(int argc, char** argv) {
         }
     }
     printf("bytes equal\n");
+    // C: registration on nthr threads (a queue of slices), copies in order as
+    // slices become registered, unregistration after each copy
+    for (int nthr : {4, 16}) {
+        CK(hipMemset(d, 0, n));
+        const int64_t ns = (int64_t)((n + slice - 1) / slice);
+        std::vector<std::atomic<int>> ready(ns);
+        for (auto& r : ready) r = 0;
+        std::atomic<int64_t> next{0};
+        const double tc0 = now();
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthr; ++t)
+            th.emplace_back([&]() {
+                hipSetDevice(0);
+                for (int64_t i; (i = next.fetch_add(1)) < ns;) {
+                    const size_t at = (size_t)i * slice, len = std::min(slice, n - at);
+                    ready[i] = hipHostRegister((uint8_t*)m + at, len, hipHostRegisterReadOnly) == hipSuccess ? 1 : -1;
+                }
+            });
+        bool ok = true;
+        for (int64_t i = 0; i < ns; ++i) {
+            while (ready[i].load() == 0) std::this_thread::yield();
+            if (ready[i] < 0) { ok = false; continue; }
+            const size_t at = (size_t)i * slice, len = std::min(slice, n - at);
+            CK(hipMemcpyAsync(d + at, (uint8_t*)m + at, len, hipMemcpyHostToDevice, s));
+        }
+        CK(hipStreamSynchronize(s));
+        const double tc = now() - tc0;
+        for (auto& t : th) t.join();
+        for (int64_t i = 0; i < ns; ++i)
+            if (ready[i] > 0) (void)hipHostUnregister((uint8_t*)m + (size_t)i * slice);
+        printf("%d register threads, copies in order: %.1f ms  %.1f GB/s  %s\n", nthr, tc * 1e3, n / tc / 1e9,
+               ok ? "" : "(some registrations failed)");
+    }
     munmap(m, n);
     close(fd);
     return 0;
