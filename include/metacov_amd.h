@@ -338,7 +338,6 @@ typedef struct mc_bam_gpu_timings {
     double upload_ms;    /* host: every file read + upload, overlapped or not */
     double kernel_ms;    /* gz_inflate_kernel launches (HIP events), summed over launches */
     double open_ms;      /* the decode inside mc_bam_gpu_open, teardown of its file mapping included */
-    int64_t upload_mapped; /* 1: the file went up from the page cache through a registered mapping */
 } mc_bam_gpu_timings;
 int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
                     int64_t window_bytes, mc_bam_gpu** out);

@@ -65,7 +65,7 @@ class GpuDecodeTimings(ctypes.Structure):
                 ("windows", ctypes.c_int64), ("blocks", ctypes.c_int64), ("resyncs", ctypes.c_int64),
                 ("compressed_bytes", ctypes.c_int64), ("inflated_bytes", ctypes.c_int64),
                 ("scan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
-                ("open_ms", ctypes.c_double), ("upload_mapped", ctypes.c_int64)]
+                ("open_ms", ctypes.c_double)]
 
 
 _P = ctypes.c_void_p

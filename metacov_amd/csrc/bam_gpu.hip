@@ -318,11 +318,7 @@ struct mc_bam_gpu {
     double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0, t_scan = 0;
     double t_upload = 0, t_kernel = 0, t_open = 0;   // every upload_file_range call; inflate launches (HIP events, summed)
     int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
-    bool mapped_upload = false;      // the last upload went through a registered mapping
-    int up_fd = -1;                  // the file being decoded (the mapped upload's pread fallback)
-    std::thread unmapper;            // unmaps the registered mapping after the decode (its page tables are large)
     ~mc_bam_gpu() {
-        if (unmapper.joinable()) unmapper.join();
         for (hipStream_t s : {stream, up_stream, kstream[0], kstream[1], kstream[2]}) {
             if (s) {
                 (void)hipStreamSynchronize(s);
@@ -484,131 +480,6 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     if (progress && !cancelled) progress->store(off + len, std::memory_order_release);
-    return MC_OK;
-}
-
-// The same upload from a shared read-only mapping of the file: the GPU copies
-// straight from the page cache, slice by slice, each slice registered
-// (hipHostRegister, read-only) by one of kRegThreads threads ahead of its copy
-// and unregistered once its copy is done (at most kPinned slices pinned).  No
-// host copy: the pread path moves every byte through the CPU into pinned
-// staging (~36 GB/s on 16 threads); here the copies run at the DMA rate
-// (~56 GB/s, scripts/micro/hostreg_probe.hip, profiles/r04/r04r_hostreg.txt).
-// *unsupported: the first registration failed (e.g. a file system whose
-// pages cannot be pinned) and nothing was copied: the caller uses pread.
-int upload_file_range_mapped(mc_bam_gpu* g, const uint8_t* base, size_t off, size_t len, uint8_t* dst,
-                             hipStream_t st, std::atomic<size_t>* progress, const std::atomic<bool>* cancel,
-                             bool* unsupported) {
-    constexpr size_t kSlice = (size_t)64 << 20;
-    constexpr int kPinned = 8, kRegThreads = 4;
-    *unsupported = false;
-    if (len == 0) return MC_OK;
-    const double t_begin = now_s();
-    struct Clock {
-        mc_bam_gpu* g;
-        double t0;
-        ~Clock() { g->t_upload += (now_s() - t0) * 1e3; }
-    } clock{g, t_begin};
-    const int64_t ns = (int64_t)((len + kSlice - 1) / kSlice);
-    hipEvent_t done[kPinned] = {};
-    for (auto& e : done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    struct Guard {
-        hipEvent_t* e;
-        ~Guard() {
-            for (int i = 0; i < kPinned; ++i)
-                if (e[i]) (void)hipEventDestroy(e[i]);
-        }
-    } guard{done};
-    std::mutex mu;
-    std::condition_variable cv;
-    std::vector<int> state(ns, 0);    // 0 pending, 1 registered, -1 failed, 2 unregistered
-    int64_t retired = 0;              // slices [0, retired) copied and unregistered
-    int64_t next = 0;
-    bool stop = false;
-    auto slice_ptr = [&](int64_t i) { return (void*)(base + off + (size_t)i * kSlice); };
-    auto slice_len = [&](int64_t i) { return std::min(kSlice, len - (size_t)i * kSlice); };
-    auto worker = [&]() {
-        if (hipSetDevice(g->device) != hipSuccess) return;
-        for (;;) {
-            int64_t i;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop || next >= ns || next < retired + kPinned; });
-                if (stop || next >= ns) return;
-                i = next++;
-            }
-            const bool cancelled = cancel && cancel->load(std::memory_order_relaxed);
-            const bool ok = !cancelled && hipHostRegister(slice_ptr(i), slice_len(i), hipHostRegisterReadOnly) == hipSuccess;
-            if (!ok) (void)hipGetLastError();
-            std::lock_guard<std::mutex> lk(mu);
-            state[i] = ok ? 1 : -1;
-            cv.notify_all();
-        }
-    };
-    std::vector<std::thread> pool;
-    for (int t = 0; t < kRegThreads; ++t) pool.emplace_back(worker);
-    auto retire = [&](int64_t upto) -> hipError_t {   // copies of slices < upto are done: unregister them
-        hipError_t e = hipSuccess;
-        std::lock_guard<std::mutex> lk(mu);
-        for (; retired < upto; ++retired) {
-            if (state[retired] == 1) (void)hipHostUnregister(slice_ptr(retired));
-            state[retired] = 2;
-        }
-        cv.notify_all();
-        return e;
-    };
-    int rc = MC_OK;
-    int64_t i = 0;
-    for (; i < ns; ++i) {
-        int si;
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return state[i] != 0; });
-            si = state[i];
-        }
-        if (si < 0) break;   // not registered: the rest goes through pread
-        hipError_t e = hipMemcpyAsync(dst + (size_t)i * kSlice, slice_ptr(i), slice_len(i), hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipEventRecord(done[i % kPinned], st);
-        // the oldest copy in flight is waited for before its slot is reused
-        const int64_t j = i - (kPinned - 2);
-        if (e == hipSuccess && j >= 0) {
-            e = hipEventSynchronize(done[j % kPinned]);
-            if (e == hipSuccess) {
-                retire(j + 1);
-                if (progress) progress->store(off + (size_t)(j + 1) * kSlice, std::memory_order_release);
-            }
-        }
-        if (e != hipSuccess) {
-            mc::set_error("HIP error %s in the mapped upload", hipGetErrorString(e));
-            rc = MC_E_HIP;
-            break;
-        }
-    }
-    hipError_t se = hipStreamSynchronize(st);
-    if (se != hipSuccess && rc == MC_OK) {
-        mc::set_error("HIP error %s in the mapped upload", hipGetErrorString(se));
-        rc = MC_E_HIP;
-    }
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        stop = true;
-    }
-    cv.notify_all();
-    for (auto& t : pool) t.join();
-    retire(ns);   // (slices registered ahead of a failure are released too)
-    if (rc) return rc;
-    if (i < ns) {
-        if (i == 0) {
-            *unsupported = true;
-            return MC_OK;
-        }
-        if (cancel && cancel->load()) return MC_OK;
-        // a later registration failed: the rest through pread
-        const size_t at = (size_t)i * kSlice;
-        if (progress) progress->store(off + at, std::memory_order_release);
-        return upload_file_range(g, g->up_fd, off + at, len - at, dst + at, st, progress, cancel);
-    }
-    if (progress) progress->store(off + len, std::memory_order_release);
     return MC_OK;
 }
 
@@ -1117,32 +988,13 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
         if (mf.size * 4 <= free_b / 2) {
             HIP_TRY(g->comp[0].reserve(mf.size + kPad));
-            g->up_fd = mf.fd;
             bg.t = std::thread([&]() {
                 if (hipSetDevice(g->device) != hipSuccess) {
                     bg.rc = MC_E_HIP;
                     bg.msg = "hipSetDevice failed in the upload thread";
                 } else {
-                    // straight from the page cache through a registered mapping
-                    // when the file's pages can be pinned, else pread staging
-                    // (MC_UPLOAD_MAPPED=0: always pread; an A/B knob)
-                    const char* me = getenv("MC_UPLOAD_MAPPED");
-                    bool unsupported = true;
-                    void* m = MAP_FAILED;
-                    if (!(me && me[0] == '0')) m = mmap(nullptr, mf.size, PROT_READ, MAP_SHARED, mf.fd, 0);
-                    if (m != MAP_FAILED) {
-                        bg.rc = upload_file_range_mapped(g, (const uint8_t*)m, 0, mf.size, g->comp[0].p, g->up_stream,
-                                                         &bg.progress, &bg.cancel, &unsupported);
-                        g->mapped_upload = bg.rc == MC_OK && !unsupported;
-                        // the mapping's page tables (filled by the pinning) go
-                        // away off the decode's critical path
-                        const size_t n = mf.size;
-                        if (g->unmapper.joinable()) g->unmapper.join();
-                        g->unmapper = std::thread([m, n]() { munmap(m, n); });
-                    }
-                    if (bg.rc == MC_OK && unsupported)
-                        bg.rc = upload_file_range(g, mf.fd, 0, mf.size, g->comp[0].p, g->up_stream, &bg.progress,
-                                                  &bg.cancel);
+                    bg.rc = upload_file_range(g, mf.fd, 0, mf.size, g->comp[0].p, g->up_stream, &bg.progress,
+                                              &bg.cancel);
                     if (bg.rc) bg.msg = mc::last_error();
                 }
                 bg.finished.store(true, std::memory_order_release);
@@ -1429,7 +1281,6 @@ extern "C" int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t) {
     t->upload_ms = g->t_upload;
     t->kernel_ms = g->t_kernel;
     t->open_ms = g->t_open;
-    t->upload_mapped = g->mapped_upload ? 1 : 0;
     return MC_OK;
 }
 

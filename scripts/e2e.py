@@ -101,7 +101,7 @@ def main():
         assert gw.n_kept == n_kept
         gw.close()
         sweep.append({"window_mib": mib, "decode_s": dt, **{k: wt[k] for k in
-                      ("read_ms", "inflate_ms", "parse_ms", "scan_ms", "total_ms", "windows", "upload_ms", "kernel_ms", "open_ms", "upload_mapped")}})
+                      ("read_ms", "inflate_ms", "parse_ms", "scan_ms", "total_ms", "windows", "upload_ms", "kernel_ms", "open_ms")}})
         print(json.dumps(sweep[-1]), file=sys.stderr, flush=True)
     advice = []
     settings = [x for x in a.env_sweep.split(";") if x]
