@@ -293,8 +293,8 @@ struct mc_ctx {
     unsigned long long done_seq = 0;
     bool stamp_ok = true;
     int ingest_grid[2] = {0, 0};          // resident ingest workgroups (without / with long counting)
-    int k2_resident[7] = {};              // resident K2 workgroups (plain, fused) x (short, long, direct); [6]: deep direct
-    size_t k2_resident_lds[7] = {};
+    int k2_resident[6] = {};              // resident K2 workgroups (plain, fused) x (short, long, direct)
+    size_t k2_resident_lds[6] = {};
     mc_timings t{};
     bool t_cigar = false, t_prep = false, t_depth = false, t_stats = false;
 };
@@ -647,9 +647,6 @@ static void resolve_timings(mc_ctx* ctx, bool all) {
 #endif
 #ifndef MC_K2_MIN_TPC
 #define MC_K2_MIN_TPC 0
-#endif
-#ifndef MC_K2_DEEP
-#define MC_K2_DEEP 1
 #endif
 static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     const int32_t nc = (int32_t)ctx->len.size();
@@ -1155,13 +1152,6 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     int grid = 0;
     if (int rc = occupancy_grid(ctx, (stats ? 1 : 0) + (lng ? 2 : dir ? 4 : 0), kfn, lds, nch, &grid))
         return rc;
-    // fewer chunks than resident workgroups (a small genome): the fused direct
-    // K2 that loads two batches ahead (depth_kernel kDeep; MC_K2_DEEP=0: never)
-    const bool deep = MC_K2_DEEP && stats && dir && !lng && nch <= (int64_t)ctx->k2_resident[5];
-    if (deep) {
-        if (int rc = occupancy_grid(ctx, 6, (const void*)depth_kernel<true, false, true, true>, lds, nch, &grid))
-            return rc;
-    }
     if (!stats) {   // the fused path's fused_init_kernel (or the last K3b) zeroes them
         ctx->fused_clean = false;   // this K2 consumes the queue
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 32, s));
@@ -1183,15 +1173,14 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     const K2Consts* dk = nullptr;
     if (int rc = k2_consts(ctx, kc, &dk)) return rc;
     const int win_parity = (int)(ctx->direct_gen & 1);
-#define MC_LAUNCH_K2(S, L, D, ...)                                                             \
-    hipLaunchKernelGGL((depth_kernel<S, L, D, ##__VA_ARGS__>), dim3(grid), dim3(kBlock), lds, s, kc.A, dk, \
+#define MC_LAUNCH_K2(S, L, D)                                                                  \
+    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, kc.A, dk,    \
                        ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p,        \
                        (unsigned long long)ctx->direct_gen, win_parity)
     if (stats) {
         if (lng) MC_LAUNCH_K2(true, true, false);
-        else if (deep) MC_LAUNCH_K2(true, false, true, true);
         else if (dir) MC_LAUNCH_K2(true, false, true);
         else MC_LAUNCH_K2(true, false, false);
     } else {

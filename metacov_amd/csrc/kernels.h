@@ -1925,15 +1925,10 @@ struct K2Consts {
     DirectArgs D;
 };
 
-// kDeep: the reads are loaded two batches ahead instead of one (ping-pong
-// registers, no copy of loads in flight): for small genomes with deep
-// coverage (C2: 610 chunks of ~16 k reads, fewer chunks than resident
-// workgroups), where each workgroup's chain of batch loads is the bound and
-// the extra VGPRs cost no occupancy that is used.
-template <bool kStats, bool kLong, bool kDirect, bool kDeep = false>
+template <bool kStats, bool kLong, bool kDirect>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
-__global__ void __launch_bounds__(kBlock, kDeep ? 1 : kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
-                                                          : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
+__global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
+                                                 : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
 depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
              int cstride, int64_t n_chunks, int tiles_per_chunk, int short_max,
@@ -2046,8 +2041,6 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
         bool more = base < cend;
         ReadBatch b;
         RawBatch<kDirect> nxt;
-        RawBatch<kDirect> nx2;     // kDeep: nxt holds batch base + kBatch (par 0) or nx2 does (par 1)
-        int par = 0;
         b.pending = 0;
         auto finish = [&](const RawBatch<kDirect>& r, int64_t at) {
             if constexpr (kDirect)
@@ -2058,8 +2051,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
         if (more) {
             RawBatch<kDirect> r0;
             issue_raw<kDirect>(r0, base, A, cend);
-            if ((kPf || kDeep) && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
-            if (kDeep && base + 2 * kBatch < cend) issue_raw<kDirect>(nx2, base + 2 * kBatch, A, cend);
+            if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
             finish(r0, base);
         }
         int carry = kLong ? uload(chunk_carry, c) : 0;
@@ -2135,20 +2127,9 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
                     base += kBatch;
                     more = base < cend;
                     if (more) {
-                        if (kDeep) {   // loaded two batches ago; its registers take the batch after next
-                            if (par == 0) {
-                                finish(nxt, base);
-                                if (base + 2 * kBatch < cend) issue_raw<kDirect>(nxt, base + 2 * kBatch, A, cend);
-                            } else {
-                                finish(nx2, base);
-                                if (base + 2 * kBatch < cend) issue_raw<kDirect>(nx2, base + 2 * kBatch, A, cend);
-                            }
-                            par ^= 1;
-                        } else {
-                            if (!kPf) issue_raw<kDirect>(nxt, base, A, cend);
-                            finish(nxt, base);   // loaded one batch ago
-                            if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
-                        }
+                        if (!kPf) issue_raw<kDirect>(nxt, base, A, cend);
+                        finish(nxt, base);   // loaded one batch ago
+                        if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
                     }
                 }
             }
