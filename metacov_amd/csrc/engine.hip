@@ -645,9 +645,6 @@ static void resolve_timings(mc_ctx* ctx, bool all) {
 #ifndef MC_MIN_CHUNKS
 #define MC_MIN_CHUNKS 4096
 #endif
-#ifndef MC_K2_MIN_TPC
-#define MC_K2_MIN_TPC 0
-#endif
 static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     const int32_t nc = (int32_t)ctx->len.size();
     ctx->extent = ext;
@@ -663,12 +660,11 @@ static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     // the ring divides the chunk) when the genome is too small to fill the GPU
     const int64_t tiles = std::max<int64_t>(1, (off + kTileW - 1) / kTileW);
     const int top = ctx->long_hint ? kTilesPerChunkLong : kTilesPerChunk;
-    // MC_K2_MIN_TPC = 1 (A/B knob): one-tile chunks; a chunk's reads ending
-    // past it land in the ring's other tile, which the chunk end zeroes
-    const int min_tpc = MC_K2_MIN_TPC > 0 ? MC_K2_MIN_TPC : (kRing % kTileW == 0) ? kRing / kTileW : top;
+    // (one-tile chunks for C2 ran K2 at 0.077 vs 0.066 ms: profiles/r04/r04m_*)
+    const int min_tpc = (kRing % kTileW == 0) ? kRing / kTileW : top;
     int tpc = top;
     while (tpc / 2 >= min_tpc && tpc % 2 == 0 && tiles / tpc < MC_MIN_CHUNKS &&
-           (MC_K2_MIN_TPC == 1 || ((int64_t)(tpc / 2) * kTileW) % kRing == 0))
+           ((int64_t)(tpc / 2) * kTileW) % kRing == 0)
         tpc /= 2;
     ctx->tiles_per_chunk = tpc;
     ctx->chunk_w = (int64_t)tpc * kTileW;

@@ -83,8 +83,8 @@ MC_HD bool wave_any(bool p) {
 
 // Bit reader over src[0, clen) through a per-lane ring of kRingWords u32 in
 // LDS (the kernel; a plain array on the host).  The ring is topped up only at
-// wave-uniform points (bits_topup: a vote, then every lane with room loads
-// kRingFill words as 16-byte groups and one wait covers the whole wave).
+// wave-uniform points (bits_topup: a vote, then every lane fills its ring
+// with 16-byte groups and one wait covers the whole wave).
 // Loading 16 bytes ahead in registers instead (round 3), every lane's refill
 // copied the in-flight group into the loop-carried registers at once: the
 // wave waited a full memory latency, draining every output store in flight
@@ -94,8 +94,7 @@ MC_HD bool wave_any(bool p) {
 #ifndef MC_GZ_RING
 #define MC_GZ_RING 16
 #endif
-constexpr int kRingWords = MC_GZ_RING;            // power of two, >= 8
-constexpr int kRingFill = kRingWords / 2;         // words per top-up (a multiple of 4)
+constexpr int kRingWords = MC_GZ_RING;            // power of two, >= 8 (A/B: 8 words 39.4 vs 36.0 ms)
 constexpr int kRingLow = 4;                       // a lane below this many words calls the top-up
 static_assert((kRingWords & (kRingWords - 1)) == 0 && kRingWords >= 8, "ring: power of two >= 8 words");
 
@@ -151,15 +150,11 @@ MC_HD void ring_load(Bits<RP>& b) {   // every load issued before the first ring
 // (or the active part of it) does: when some lane is low, every lane fills its
 // ring (as many 16-byte groups as fit), and the wave waits once.  Filling only
 // the lanes at or below half (round 3) left lanes just above it to trigger
-// the next wait a few steps later; full rings space the waits by at least
-// kRingWords - 3 - kRingLow words of the fastest lane.
-#ifndef MC_GZ_TOPUP_FULL
-#define MC_GZ_TOPUP_FULL 1
-#endif
+// the next wait a few steps later (A/B: 37.5 vs 36.0 ms); full rings space
+// the waits by at least kRingWords - 3 - kRingLow words of the fastest lane.
 template <class RP>
 MC_HD void bits_topup(Bits<RP>& b) {
     if (wave_any((int)(b.rfill - b.rpos) < kRingLow)) {
-#if MC_GZ_TOPUP_FULL
         const int ng = (kRingWords - (int)(b.rfill - b.rpos)) >> 2;   // free groups
         uint4 v[kRingWords / 4];
 #pragma unroll
@@ -176,9 +171,6 @@ MC_HD void bits_topup(Bits<RP>& b) {
             }
         b.p += ng;
         b.rfill += 4 * ng;
-#else
-        if ((int)(b.rfill - b.rpos) <= kRingWords - kRingFill) ring_load<kRingFill>(b);
-#endif
     }
 }
 
@@ -540,56 +532,19 @@ struct MatchQueue {
     int n;
 };
 
-// MC_GZ_FLUSH_BATCH = B > 1: the queue goes in batches of B entries whose
-// first source chunks are loaded together (one memory round trip per batch,
-// not per entry) when they lie before the batch's first destination, which
-// nothing of the batch writes; an entry reading later bytes loads after the
-// stores before it.
-#ifndef MC_GZ_FLUSH_BATCH
-#define MC_GZ_FLUSH_BATCH 1
-#endif
-#ifndef MC_GZ_FLUSH_WAIT
-#define MC_GZ_FLUSH_WAIT 1
-#endif
-constexpr int kFlushBatch = MC_GZ_FLUSH_BATCH;
-
 template <class QP>
 MC_HD void mq_flush(MatchQueue<QP>& q, uint8_t* dst) {
-    int j = 0;
-#if MC_GZ_COPY_BATCH == 2
-    if (kFlushBatch > 1) {
-        for (; j + kFlushBatch <= q.n; j += kFlushBatch) {
-            uint64_t e[kFlushBatch];
-            uint4 v[kFlushBatch];
-            bool early[kFlushBatch];
-#pragma unroll
-            for (int k = 0; k < kFlushBatch; ++k) e[k] = q.e[j + k];
-            const uint32_t o0 = (uint32_t)(e[0] >> 32);
-#pragma unroll
-            for (int k = 0; k < kFlushBatch; ++k) {
-                const uint32_t o = (uint32_t)(e[k] >> 32), d = (uint32_t)e[k] >> 9;
-                early[k] = d >= 16 && o - d + 16 <= o0;
-                v[k] = early[k] ? ld16(dst + (o - d)) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int k = 0; k < kFlushBatch; ++k) {
-                const uint32_t o = (uint32_t)(e[k] >> 32), d = (uint32_t)e[k] >> 9;
-                const int len = (int)(e[k] & 511u);
-                if (early[k]) lz_copy_wide(dst + o, len, (int)d, v[k]);
-                else lz_copy(dst + o, len, (int)d);
-            }
-        }
-    }
-#endif
-    for (; j < q.n; ++j) {
+    for (int j = 0; j < q.n; ++j) {
         const uint64_t e = q.e[j];
         lz_copy(dst + (uint32_t)(e >> 32), (int)(e & 511u), (int)((uint32_t)e >> 9));
     }
     q.n = 0;
-#if defined(__HIP_DEVICE_COMPILE__) && MC_GZ_FLUSH_WAIT
+#if defined(__HIP_DEVICE_COMPILE__)
     // vmcnt(0) here, once per flush: otherwise the compiler's wait for the
     // flush's loads lands at the join after it, on the symbol loop's common
     // path, and every symbol step waited for the output stores in flight
+    // (A/B: 32 vs 33.3 ms).  Loading a batch of four entries' first chunks
+    // together before their stores was slower (38.4 vs 36.0 ms).
     __builtin_amdgcn_s_waitcnt(0x0F70);
 #endif
 }

@@ -1177,18 +1177,10 @@ long_fill_kernel(LongGeo G, const int64_t* __restrict__ tile_off, unsigned* __re
 // of its smallest end (ends are not sorted, starts are).  The count atomics
 // return each event's rank in its tile (round 3 took the ranks in a second
 // atomic pass; SQ: LDS bank-conflict cycles 2.5x the LDS-active cycles, waves
-// waiting on LDS 36 % of their cycles): C5 call 1.670 -> 1.634 ms.  Counters
-// striped over 8 / 16 lanes (kFillStripes) measured 1.680 / 1.686 ms
-// (profiles/r04/r04o_long_fill_ab.txt).
-#ifndef MC_LONG_FILL_SUBS
-#define MC_LONG_FILL_SUBS 4
-#endif
-#ifndef MC_LONG_FILL_STRIPES
-#define MC_LONG_FILL_STRIPES 1
-#endif
-constexpr int kFillSubs = MC_LONG_FILL_SUBS;
-constexpr int kFillStripes = MC_LONG_FILL_STRIPES;
-static_assert((kFillStripes & (kFillStripes - 1)) == 0 && kFillStripes <= 64, "stripes: a power of two <= 64");
+// waiting on LDS 36 % of their cycles): C5 call 1.670 -> 1.634 ms.  Measured
+// and dropped: one or eight sub-ranges per round (no change), counters striped
+// over 8 / 16 lanes (1.680 / 1.686 ms; profiles/r04/r04o_long_fill_ab.txt).
+constexpr int kFillSubs = 4;
 
 __global__ void __launch_bounds__(kBlock)
 long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, int lcw,
@@ -1196,13 +1188,11 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
                        int32_t* __restrict__ ev) {
     static_assert(kLongPer == 4, "one int4 of end words per thread and sub-range");
     constexpr int kE = 4 * kFillSubs;     // end words per thread and round
-    constexpr int kW = kLongTileWin * kFillStripes;
-    __shared__ int wt[kW];                // per (tile, stripe): count (ranks come back from the atomics)
-    __shared__ int wb[kW];                // per (tile, stripe): first slot
+    __shared__ int wt[kLongTileWin];      // per window tile: count (ranks come back from the atomics)
+    __shared__ int wb[kLongTileWin];      // per window tile: first slot
     __shared__ unsigned red[kWaves];
     const int64_t cmask = ((int64_t)1 << lcw) - 1;
-    const int stripe = (int)(threadIdx.x & (kFillStripes - 1));
-    for (int k = threadIdx.x; k < kW; k += kBlock) wt[k] = 0;
+    for (int k = threadIdx.x; k < kLongTileWin; k += kBlock) wt[k] = 0;
     const int64_t r0 = blockIdx.x * per, r1 = min(n, r0 + per);
     for (int64_t sub = r0; sub < r1; sub += (int64_t)kLongSub * kFillSubs) {
         uint32_t e[kE];
@@ -1228,8 +1218,8 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
         __syncthreads();
         m = min(min(red[0], red[1]), min(red[2], red[3]));
         const int64_t TB = m == ~0u ? 0 : (int64_t)(m / kTileW);
-        int te[kE];     // (window tile, stripe) counter index, or -1
-        int rk[kE];     // rank in that counter
+        int te[kE];     // window tile, or -1
+        int rk[kE];     // rank in its tile
 #pragma unroll
         for (int k = 0; k < kE; ++k) {
             te[k] = -1;
@@ -1237,23 +1227,16 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
             if (e[k] == ~0u) continue;
             const int64_t t = (int64_t)(e[k] / kTileW);
             if (t - TB < kLongTileWin) {
-                te[k] = (int)(t - TB) * kFillStripes + stripe;
+                te[k] = (int)(t - TB);
                 rk[k] = atomicAdd(&wt[te[k]], 1);
             }
         }
         __syncthreads();
         for (int t = threadIdx.x; t < kLongTileWin; t += kBlock) {
-            int tot = 0;
-#pragma unroll
-            for (int q = 0; q < kFillStripes; ++q) tot += wt[t * kFillStripes + q];
-            if (tot) {
-                int at = (int)(tile_off[TB + t] + atomicAdd(&cursor[TB + t], (unsigned)tot));
-#pragma unroll
-                for (int q = 0; q < kFillStripes; ++q) {
-                    wb[t * kFillStripes + q] = at;
-                    at += wt[t * kFillStripes + q];
-                    wt[t * kFillStripes + q] = 0;
-                }
+            const int v = wt[t];
+            if (v) {
+                wb[t] = (int)(tile_off[TB + t] + atomicAdd(&cursor[TB + t], (unsigned)v));
+                wt[t] = 0;
             }
         }
         __syncthreads();
