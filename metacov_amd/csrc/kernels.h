@@ -1466,6 +1466,11 @@ struct DirectChunk {                   // wave-uniform per chunk
 struct DirectAcc {                     // per-lane verdict
     unsigned flags = 0;                // kDirectInvalid | kDirectUnfit
     int max_span = 0;                  // over the valid reads loaded for [lo, hi)
+    // the last contig looked up (wave-uniform: its offset and length by
+    // scalar loads; sorted reads meet a new contig rarely, and the loads'
+    // round trip was paid per batch)
+    int ct = -1;
+    int64_t c_off = 0, c_len = 0;
 };
 
 // Raw tuples: chunk-relative starts (contig offsets and lengths by scalar
@@ -1502,7 +1507,12 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         const unsigned long long act = __ballot(cand >= 0);
         if (!act) break;
         const int t0 = __builtin_amdgcn_readlane(cand, __ffsll((long long)act) - 1);
-        const int64_t c = uload(coff, t0) - C0, ln = uload(D.len, t0);
+        if (t0 != acc.ct) {
+            acc.ct = t0;
+            acc.c_off = uload(coff, t0);
+            acc.c_len = uload(D.len, t0);
+        }
+        const int64_t c = acc.c_off - C0, ln = acc.c_len;
         const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
         // rs = clamp(c + pos, -2^30, 2^30) in 32 bits: pos (>= 0 when valid)
         // clamped to [p_lo, p_hi] per contig (scalar), then c + pos wraps
