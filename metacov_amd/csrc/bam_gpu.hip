@@ -378,7 +378,9 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
         double t0;
         ~Clock() { g->t_upload += (now_s() - t0) * 1e3; }
     } clock{g, t_begin};
-    for (auto& s : g->stage) HIP_TRY(s.reserve(kSlice));
+    // the first staging buffer now, the others while the readers fill it
+    // (pinning 64 MiB takes a few ms; a new handle allocates them all)
+    HIP_TRY(g->stage[0].reserve(kSlice));
     hipEvent_t done[kStage] = {};
     for (auto& e : done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     struct Guard {
@@ -393,7 +395,7 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)g->nt, std::min(len, kSlice) >> 20));
     std::mutex mu;
     std::condition_variable cv;
-    int64_t free_upto = std::min<int64_t>(ns, kStage);   // slices [0, free_upto) may be read
+    int64_t free_upto = 1;                            // slices [0, free_upto) may be read
     std::vector<int> parts(ns, 0);                     // parts of each slice read
     bool bad = false, stop = false, quit = false;   // quit: a reader saw cancel
     auto reader = [&](int t) {
@@ -429,6 +431,13 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     };
     std::vector<std::thread> pool;
     for (int t = 0; t < nt; ++t) pool.emplace_back(reader, t);
+    hipError_t stage_err = hipSuccess;
+    for (int k = 1; k < kStage && k < ns && stage_err == hipSuccess; ++k) stage_err = g->stage[k].reserve(kSlice);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (stage_err == hipSuccess) free_upto = std::min<int64_t>(ns, kStage);
+        cv.notify_all();
+    }
     auto finish = [&]() {
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -439,6 +448,10 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     };
     int rc = MC_OK;
     bool cancelled = false;
+    if (stage_err != hipSuccess) {
+        mc::set_error("HIP error %s allocating the upload staging", hipGetErrorString(stage_err));
+        rc = MC_E_HIP;
+    }
     for (int64_t k = 0; k < ns && rc == MC_OK; ++k) {
         if (cancel && cancel->load(std::memory_order_relaxed)) {
             cancelled = true;
