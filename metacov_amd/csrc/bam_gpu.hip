@@ -832,7 +832,7 @@ int header_from_prefix(mc_bam_gpu* g, size_t n, int64_t* o, bool* ok) {
 #define MC_GZ_PIECE_STREAMS 2
 #endif
 #ifndef MC_GZ_PIECES
-#define MC_GZ_PIECES 4                 // pieces per inflated stream (each >= 256 MiB, <= 4 GiB)
+#define MC_GZ_PIECES 3                 // pieces per inflated stream (each >= 256 MiB, <= 4 GiB)
 #endif
 static_assert(MC_GZ_PIECE_STREAMS >= 1 && MC_GZ_PIECE_STREAMS <= 4, "inflate streams: stream + kstream[]");
 constexpr int kGzPieceStreams = MC_GZ_PIECE_STREAMS;
