@@ -815,19 +815,17 @@ int header_from_prefix(mc_bam_gpu* g, size_t n, int64_t* o, bool* ok) {
 }
 
 // Resident decode (the default when the compressed file and its inflated
-// stream fit in HBM): the file goes up in pieces of about a quarter of the
-// inflated stream, and each piece's inflate kernel is launched as soon as its
-// bytes are on the device, on alternating streams, into the piece's final
-// place in one inflated buffer.  A kernel's time has a floor (its slowest
-// lanes decode a whole block serially: ~72 ms for any window of 4 k to 32 k
-// blocks, profiles/r03sd_e2e_window_sweep.json), so successive pieces' kernels
+// stream fit in HBM): the inflated stream is cut into pieces (a third each),
+// and each piece's inflate kernel is launched as soon as its bytes are on the
+// device (uploaded by the background upload of gpu_decode, or here piece by
+// piece for a small file), on alternating streams, into the piece's final
+// place in one inflated buffer.  A kernel lasts at least as long as its
+// slowest lane's serial decode of one block, so successive pieces' kernels
 // overlap each other and the remaining uploads instead of running one window
-// after another; no carry between windows, one parse at the end.
-// A/B on the 30 M-record BAM (profiles/r03sf_gz_pipeline_ab.txt, decode total
-// per build in interleaved rounds 1-2; round 0 includes a cold first run):
-// 2 / 3 / 4 streams with 4 pieces 292-309 / 310-342 / 296-298 ms; 8 pieces
-// 427-433 ms on 2 or 4 streams (the per-launch floor is paid more often than
-// the uploads hide it)
+// after another; no carry between windows, one parse at the end.  Pieces,
+// end to end on the 30 M-record BAM (profiles/r04/r04z*): 8 / 6 /
+// 4 / 3 / 2 pieces 0.227 / 0.211 / 0.192-0.202 / 0.184-0.193 / 0.193 s.
+// Streams (round 3, profiles/r03sf_gz_pipeline_ab.txt): 2 / 3 / 4 alike.
 #ifndef MC_GZ_PIECE_STREAMS
 #define MC_GZ_PIECE_STREAMS 2
 #endif
