@@ -309,6 +309,25 @@ int mc_bam_index_stats(const char* bai_path, int32_t n_ref, int64_t* n_mapped,
 int mc_bam_open_contigs(const char* path, const char* bai_path, int n_threads,
                         uint32_t flag_filter, int keep_cigar, int32_t n_sel,
                         const int32_t* sel, mc_bam** out);
+/* Where each contig's records lie in a coordinate-sorted BAM: what a BAI's
+ * per-reference pseudo-bin holds (htslib hts_idx_finish, bin 37450).
+ * beg_voff / end_voff are the virtual offsets (bgzf_tell: compressed block
+ * offset << 16 | offset inside the inflated block) of the contig's first
+ * record and of the end of its last one; equal when it has no records.
+ * n_kept: records kept under a decode's flag filter (mc_bam_gpu_extents;
+ * 0 when read from an index). */
+typedef struct mc_contig_extent {
+    int64_t beg_voff;
+    int64_t end_voff;
+    int64_t n_mapped;     /* records of this tid without flag 0x4 */
+    int64_t n_unmapped;   /* records of this tid with flag 0x4 */
+    int64_t n_kept;
+} mc_contig_extent;
+/* The extents table of an index (the role of pysam's indexed
+ * AlignmentFile.fetch(ref) at metacov/pileup.py:13 / :90: which bytes hold a
+ * contig's reads); *n_no_coor: records without coordinates. */
+int mc_bam_index_extents(const char* bai_path, int32_t n_ref, mc_contig_extent* ext,
+                         int64_t* n_no_coor);
 
 /* ---- GPU BAM decode ------------------------------------------------------
  * The records mc_bam_open keeps (same intervals in file order, same record /
@@ -338,6 +357,8 @@ typedef struct mc_bam_gpu_timings {
     double upload_ms;    /* host: every file read + upload, overlapped or not */
     double kernel_ms;    /* gz_inflate_kernel launches (HIP events), summed over launches */
     double open_ms;      /* the decode inside mc_bam_gpu_open, teardown of its file mapping included */
+    int64_t parse_rounds;   /* most walk / check rounds of any parsed window (1: no false sync) */
+    int64_t resync_passes;  /* re-syncs with the long chain after repeated false syncs */
 } mc_bam_gpu_timings;
 int mc_bam_gpu_open(const char* path, int device, int n_threads, uint32_t flag_filter,
                     int64_t window_bytes, mc_bam_gpu** out);
@@ -347,6 +368,39 @@ int mc_bam_gpu_intervals_device(const mc_bam_gpu* g, int64_t* n, const int32_t**
 int mc_bam_gpu_intervals(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int32_t* span);
 int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t);
 int mc_bam_gpu_close(mc_bam_gpu* g);
+/* One rank's contig shard decoded on the GPU ("each rank
+ * decodes only its contigs' BGZF chunks, located via BAI virtual offsets";
+ * replaces the per-contig indexed query under pysam's pileup(ref, start,
+ * end), metacov/pileup.py:13).  Only the BGZF blocks holding the selected
+ * contigs' records are read, uploaded and inflated; the kept records are
+ * those mc_bam_open keeps of those contigs, in file order.  Their device
+ * tids are LOCAL ids (the rank of the header tid in the sorted, de-duplicated
+ * selection: the contig ids of a ctx holding just those contigs), in
+ * mc_bam_gpu_intervals_device as in mc_bam_gpu_intervals[_range].  The
+ * header counts are the whole file's, from the extents (as an index reports
+ * them).  mc_bam_gpu_open_contigs reads the extents from the BAI (bai_path
+ * NULL: <path>.bai); mc_bam_gpu_open_extents takes them from the caller
+ * (e.g. mc_bam_gpu_extents of a whole-file decode on another rank, for a BAM
+ * without an index). */
+int mc_bam_gpu_open_contigs(const char* path, const char* bai_path, int device, int n_threads,
+                            uint32_t flag_filter, int32_t n_sel, const int32_t* sel,
+                            mc_bam_gpu** out);
+int mc_bam_gpu_open_extents(const char* path, int device, int n_threads, uint32_t flag_filter,
+                            int32_t n_ref, const mc_contig_extent* ext, int64_t n_no_coor,
+                            int32_t n_sel, const int32_t* sel, mc_bam_gpu** out);
+/* The extents table of a decoded file, computed on the device during the
+ * record walk (per contig: first record, end of the last record, mapped /
+ * unmapped / kept counts).  For a whole-file handle it is the BAI's
+ * pseudo-bin data; MC_E_INVALID if the records of a contig are not
+ * contiguous (the file is not coordinate-sorted).  A contig-subset handle
+ * returns the table it was opened with, with n_kept filled in for its
+ * contigs. */
+int mc_bam_gpu_extents(const mc_bam_gpu* g, int32_t n_ref, mc_contig_extent* ext,
+                       int64_t* n_no_coor);
+/* Kept intervals [first, first + count) of the handle, copied to the host
+ * (the records of chosen contigs: offsets from the extents' n_kept). */
+int mc_bam_gpu_intervals_range(const mc_bam_gpu* g, int64_t first, int64_t count, int32_t* tid,
+                               int32_t* pos, int32_t* span);
 /* Test hooks (no GPU): the lane decoder of the inflate kernel and the record
  * parse of the walk kernels, run on the host.  mc_gz_inflate_host: one raw
  * deflate stream into exactly isize bytes (MC_E_IO otherwise).
@@ -356,6 +410,11 @@ int mc_bam_gpu_close(mc_bam_gpu* g);
 int mc_gz_inflate_host(const uint8_t* src, int64_t clen, uint8_t* dst, int64_t isize);
 int mc_bam_rec_parse_host(const uint8_t* r, int64_t len, int32_t n_ref, uint32_t flag_filter,
                           int32_t* out3);
+/* mc_bam_rec_chain_host: 1 if offset q of the inflated stream d[0, n) starts
+ * `chain` structurally valid records in sort order (mapped records' bin
+ * fields equal to reg2bin of their span), or a shorter such chain ending
+ * exactly at n — the GPU record sync's rule; else 0. */
+int mc_bam_rec_chain_host(const uint8_t* d, int64_t n, int64_t q, int32_t n_ref, int chain);
 /* mc_bgzf_scan_host: the GPU decode's BGZF block scan (pread, n_threads
  * ranges) -> block count, inflated total, the first cap block offsets. */
 int mc_bgzf_scan_host(const char* path, int n_threads, int64_t* n_blocks, int64_t* inflated,

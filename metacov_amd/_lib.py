@@ -65,7 +65,8 @@ class GpuDecodeTimings(ctypes.Structure):
                 ("windows", ctypes.c_int64), ("blocks", ctypes.c_int64), ("resyncs", ctypes.c_int64),
                 ("compressed_bytes", ctypes.c_int64), ("inflated_bytes", ctypes.c_int64),
                 ("scan_ms", ctypes.c_double), ("upload_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
-                ("open_ms", ctypes.c_double)]
+                ("open_ms", ctypes.c_double), ("parse_rounds", ctypes.c_int64),
+                ("resync_passes", ctypes.c_int64)]
 
 
 _P = ctypes.c_void_p
@@ -138,8 +139,16 @@ SIGNATURES = {
     "mc_bam_gpu_intervals": [_P, _P, _P, _P],
     "mc_bam_gpu_stats": [_P, _P],
     "mc_bam_gpu_close": [_P],
+    "mc_bam_index_extents": [ctypes.c_char_p, _I32, _P, _PI64],
+    "mc_bam_gpu_open_contigs": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _U32, _I32, _P,
+                                _PP],
+    "mc_bam_gpu_open_extents": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _U32, _I32, _P, _I64, _I32, _P,
+                                _PP],
+    "mc_bam_gpu_extents": [_P, _I32, _P, _PI64],
+    "mc_bam_gpu_intervals_range": [_P, _I64, _I64, _P, _P, _P],
     "mc_gz_inflate_host": [_P, _I64, _P, _I64],
     "mc_bam_rec_parse_host": [_P, _I64, _I32, _U32, _P],
+    "mc_bam_rec_chain_host": [_P, _I64, _I64, _I32, ctypes.c_int],
     "mc_bgzf_scan_host": [ctypes.c_char_p, ctypes.c_int, _PI64, _PI64, _PI64, _I64],
     # pileup.experimental: read side (host) and sequence side (GPU)
     "mc_reads_open": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _PP],

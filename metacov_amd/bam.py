@@ -260,24 +260,63 @@ def _header_of(lib, hdr):
     return tuple(names), tuple(lengths), (c[0].value, c[2].value, c[3].value)
 
 
+# mc_contig_extent: where a contig's records lie (a BAI pseudo-bin)
+EXTENT_DTYPE = np.dtype([("beg_voff", "<i8"), ("end_voff", "<i8"), ("n_mapped", "<i8"),
+                         ("n_unmapped", "<i8"), ("n_kept", "<i8")])
+
+
+def index_extents(index, n_ref):
+    """The extents table of a BAI (per contig: virtual offsets of its first
+    record and of the end of its last one, mapped / unmapped counts) and its
+    count of records without coordinates."""
+    ext = np.zeros(n_ref, EXTENT_DTYPE)
+    nc = ctypes.c_int64()
+    check(_lib.load().mc_bam_index_extents(os.fspath(index).encode(), int(n_ref), _lib.ptr(ext),
+                                           ctypes.byref(nc)))
+    return ext, nc.value
+
+
 class GpuBamFile:
-    """The whole file decoded on the GPU (mc_bam_gpu_*: BGZF inflate and
-    record parse in HBM).  Same header, counts and kept intervals as
-    BamFile(path); the intervals stay on `device` and go into the engine by
-    a device copy (mc_add_reads_device).  Offers what the CLI uses of
-    BamFile: references, lengths, mapped, unmapped, engine(), local_tid()."""
+    """A BAM decoded on the GPU (mc_bam_gpu_*: BGZF inflate and record parse
+    in HBM).  Same header, counts and kept intervals as BamFile(path); the
+    intervals stay on `device` and go into the engine by a device copy
+    (mc_add_reads_device).  Offers what the CLI uses of BamFile: references,
+    lengths, mapped, unmapped, engine(), local_tid().
+
+    contigs=[...]: one rank's shard: only the BGZF blocks of
+    those contigs are read and inflated, located by the BAI (`index`, default
+    <path>.bai) or by an `extents` table (ext, n_no_coor) of a whole-file
+    decode (GpuBamFile.extents() on another rank, for a BAM without an
+    index).  Its engine holds just those contigs (local_tid maps header ids
+    to them); mapped / unmapped are the whole file's, as an index reports."""
 
     def __init__(self, path, device=0, n_threads=0, flag_filter=FLAG_FILTER, window_bytes=0,
-                 legacy_endpos=False):
+                 legacy_endpos=False, contigs=None, index=None, extents=None):
         self.filename = os.fspath(getattr(path, "filename", path))
-        self.contigs = None
         self.device = device
         self.legacy_endpos = bool(legacy_endpos)
         flag_filter = _filter(flag_filter, legacy_endpos)
         self._lib = _lib.load()
         self._h = ctypes.c_void_p()
-        check(self._lib.mc_bam_gpu_open(self.filename.encode(), int(device), int(n_threads),
-                                        int(flag_filter), int(window_bytes), ctypes.byref(self._h)))
+        self._eng = None
+        self._ext = None
+        if contigs is None:
+            self.contigs = None
+            check(self._lib.mc_bam_gpu_open(self.filename.encode(), int(device), int(n_threads),
+                                            int(flag_filter), int(window_bytes), ctypes.byref(self._h)))
+        else:
+            self.contigs = np.unique(np.asarray(contigs, dtype=np.int32))
+            if extents is None:
+                check(self._lib.mc_bam_gpu_open_contigs(
+                    self.filename.encode(), os.fspath(index).encode() if index else None, int(device),
+                    int(n_threads), int(flag_filter), len(self.contigs), _lib.ptr(self.contigs),
+                    ctypes.byref(self._h)))
+            else:
+                ext = np.ascontiguousarray(extents[0], EXTENT_DTYPE)
+                check(self._lib.mc_bam_gpu_open_extents(
+                    self.filename.encode(), int(device), int(n_threads), int(flag_filter), len(ext),
+                    _lib.ptr(ext), int(extents[1]), len(self.contigs), _lib.ptr(self.contigs),
+                    ctypes.byref(self._h)))
         hdr = ctypes.c_void_p()
         check(self._lib.mc_bam_gpu_header(self._h, ctypes.byref(hdr)))
         self.references, self.lengths, (self.n_records, self.mapped, self.unmapped) = \
@@ -287,7 +326,6 @@ class GpuBamFile:
         check(self._lib.mc_bam_gpu_intervals_device(self._h, ctypes.byref(n),
                                                     *[ctypes.byref(p) for p in self._dptr]))
         self.n_kept = n.value
-        self._eng = None
 
     @property
     def nreferences(self):
@@ -299,15 +337,48 @@ class GpuBamFile:
         except ValueError:
             raise KeyError(name)
 
-    def local_tid(self, tid):
-        return tid
+    local_tid = BamFile.local_tid
 
-    def intervals(self):
-        """(tid, pos, span) copied to host numpy arrays (tests)."""
-        out = tuple(np.empty(self.n_kept, np.int32) for _ in range(3))
-        if self.n_kept:
-            check(self._lib.mc_bam_gpu_intervals(self._h, *[_lib.ptr(a) for a in out]))
+    def extents(self):
+        """(EXTENT_DTYPE table, records without coordinates): per contig the
+        virtual offsets of its first record and of the end of its last one,
+        mapped / unmapped / kept counts — computed on the device during the
+        decode (a whole file), what its BAI would hold."""
+        if self._ext is None:
+            ext = np.zeros(len(self.references), EXTENT_DTYPE)
+            nc = ctypes.c_int64()
+            check(self._lib.mc_bam_gpu_extents(self._h, len(ext), _lib.ptr(ext), ctypes.byref(nc)))
+            self._ext = (ext, nc.value)
+        return self._ext
+
+    def _range(self, first, count):
+        out = tuple(np.empty(count, np.int32) for _ in range(3))
+        if count:
+            check(self._lib.mc_bam_gpu_intervals_range(self._h, int(first), int(count),
+                                                       *[_lib.ptr(a) for a in out]))
         return out
+
+    def intervals(self, contigs=None):
+        """(tid, pos, span) host arrays with header contig ids, in file order:
+        every kept record, or (contigs=[...]) only the records of those
+        contigs, copied back from HBM slice by slice."""
+        if contigs is None:
+            tid, pos, span = self._range(0, self.n_kept)
+        else:
+            ext, _ = self.extents()
+            kept = ext["n_kept"]
+            order = np.argsort(ext["beg_voff"], kind="stable")
+            first = np.zeros(len(kept), np.int64)
+            first[order] = np.cumsum(kept[order]) - kept[order]
+            want = np.unique(np.asarray(contigs, np.int64))
+            want = want[kept[want] > 0]
+            want = want[np.argsort(first[want], kind="stable")]
+            parts = [self._range(first[t], kept[t]) for t in want]
+            tid, pos, span = (np.concatenate([p[i] for p in parts]) if parts else np.zeros(0, np.int32)
+                              for i in range(3))
+        if self.contigs is not None and len(tid):
+            tid = self.contigs[tid]
+        return tid, pos, span
 
     def timings(self):
         t = _lib.GpuDecodeTimings()
@@ -320,7 +391,8 @@ class GpuBamFile:
         if self._eng is None:
             from .engine import CoverageEngine
             eng = CoverageEngine(self.device)
-            eng.set_contigs(np.asarray(self.lengths, dtype=np.int64))
+            lengths = np.asarray(self.lengths, dtype=np.int64)
+            eng.set_contigs(lengths if self.contigs is None else lengths[self.contigs])
             if self.n_kept:
                 eng._check(self._lib.mc_add_reads_device(eng._h, self.n_kept, *self._dptr))
             eng._depth_ready = False

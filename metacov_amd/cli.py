@@ -97,7 +97,7 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     exp = (k_cor, kmer_length, fasta) if k_cor is not None else None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp,
-                                  max_depth=max_depth, legacy_endpos=legacy_endpos)
+                                  max_depth=max_depth, legacy_endpos=legacy_endpos, decode=decode)
     if decode == 'gpu':
         bam = GpuBamFile(bamfile.name, device=device, window_bytes=window_bytes,
                          legacy_endpos=legacy_endpos)
@@ -221,7 +221,7 @@ def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=_depthcap.HT
 
 
 def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=None,
-                       max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False):
+                       max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False, decode="gpu"):
     """One rank of a multi-GPU `pileup` (launched by torch.distributed.run).
     With -k, each rank also computes the experimental columns of the regions
     on its contigs (cli.py:93-95 per region), and rank 0 gathers them with
@@ -242,7 +242,7 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         err = region_err = None
         try:
             table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
-                                       max_depth, legacy_endpos)
+                                       max_depth, legacy_endpos, decode, coll_dev)
             head, regions, tids, starts, ends, rows, mine, r_max, region_err = table_args
             mine_extra = experimental_results(path, exp, head.references, tids[mine], starts[mine],
                                               ends[mine], device)
@@ -269,17 +269,43 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         raise region_err
 
 
+class _Header:
+    """What the ranks of a distributed pileup use of an opened BAM besides
+    its reads: names, lengths and the whole file's record counts."""
+
+    def __init__(self, references, lengths, counts):
+        self.references, self.lengths = tuple(references), tuple(lengths)
+        self.n_records, self.mapped, self.unmapped = counts
+
+
 def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
-                  max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False):
+                  max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False, decode="gpu",
+                  coll_dev=None):
     """This rank's part of a distributed pileup: header and regions (every
     rank; those before the first failing one, and its error), LPT contig
-    shards, and the rows of the regions on its contigs."""
+    shards, and the rows of the regions on its contigs.
+
+    Each rank decodes only its own contigs' BGZF blocks, on
+    its GPU by default, located by the BAI's extents.  Without a .bai, rank 0
+    decodes the whole file on its GPU, which yields the same extents table
+    (mc_bam_gpu_extents: what the index would hold), and broadcasts it; the
+    other ranks then decode their contigs from it.  --decode host: the C++
+    host decoder (whole file without an index)."""
     from . import dist as mdist
     index = path + ".bai"
     have_index = os.path.exists(index)
+    ext = None
     if have_index:       # header + per-contig counts from the index, no decode
         head = BamFile(path, contigs=[])
         reads_per, _, _ = index_stats(index, len(head.lengths))
+    elif decode == "gpu":
+        def whole_file():
+            with GpuBamFile(path, device=device, legacy_endpos=legacy_endpos) as full:
+                return (full.references, full.lengths, (full.n_records, full.mapped, full.unmapped),
+                        full.extents())
+        refs, lens, counts, ext = mdist.broadcast_result(whole_file, rank, device=coll_dev)
+        head = _Header(refs, lens, counts)
+        reads_per = ext[0]["n_mapped"]
     else:
         head = BamFile(path, legacy_endpos=legacy_endpos)
         reads_per = np.bincount(head.tid, minlength=len(head.lengths))
@@ -294,9 +320,18 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
     r_max = max(1, int(np.bincount(region_rank, minlength=world).max()) if len(tids) else 1)
     rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
     if len(mine):
-        bam = (BamFile(path, contigs=shards[rank], legacy_endpos=legacy_endpos) if have_index
-               else head.restrict(shards[rank]))
-        rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
+        if decode == "gpu":
+            bam = GpuBamFile(path, device=device, contigs=shards[rank], extents=ext,
+                             legacy_endpos=legacy_endpos)
+        elif have_index:
+            bam = BamFile(path, contigs=shards[rank], legacy_endpos=legacy_endpos)
+        else:
+            bam = head.restrict(shards[rank])
+        try:
+            rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
+        finally:
+            if decode == "gpu":
+                bam.close()
     return head, regions, tids, starts, ends, rows, mine, r_max, region_err
 
 

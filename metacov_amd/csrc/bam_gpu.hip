@@ -30,6 +30,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 
@@ -129,29 +130,23 @@ gz_inflate_kernel(const uint8_t* __restrict__ comp, const GzBlock* __restrict__ 
     }
 }
 
-// One wave per segment i in [1, nseg): found[i] = the first offset q in
-// [cut_i, min(cut_i + kSeg, n)) that starts kSyncChain plausible records
-// (or a shorter chain ending exactly at n), else n.
+// One wave per segment i in [i0, nseg): found[i] = the first offset q in
+// [cut_i, min(cut_i + kSeg, n)) that starts `chain` plausible records in
+// sort order (or a shorter chain ending exactly at n), else n.
 __global__ void __launch_bounds__(256)
-rec_sync_kernel(const uint8_t* __restrict__ d, int64_t o, int64_t n, int64_t nseg, int32_t n_ref,
-                int64_t* __restrict__ found) {
+rec_sync_kernel(const uint8_t* __restrict__ d, int64_t o, int64_t n, int64_t i0, int64_t nseg, int32_t n_ref,
+                int chain, int64_t* __restrict__ found) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t waves = (int64_t)gridDim.x * 4;
-    for (int64_t i = 1 + wave; i < nseg; i += waves) {
+    for (int64_t i = i0 + wave; i < nseg; i += waves) {
         const int64_t cut = o + i * kSeg;
         const int64_t lim = cut + kSeg < n ? cut + kSeg : n;
         int64_t res = n;
         for (int64_t base = cut; base < lim; base += 64) {
             const int64_t q = base + lane;
             bool ok = false;
-            if (q < lim && mc::gz::rec_plausible(d, q, n, n_ref)) {
-                int64_t z = q;
-                int k = 0;
-                for (; k < kSyncChain && z < n && mc::gz::rec_plausible(d, z, n, n_ref); ++k)
-                    z += 4 + (int64_t)mc::gz::ld_i32(d + z);
-                ok = k == kSyncChain || z == n;
-            }
+            if (q < lim && mc::gz::rec_plausible(d, q, n, n_ref)) ok = mc::gz::rec_chain(d, q, n, n_ref, chain);
             const unsigned long long m = __ballot(ok);
             if (m) {
                 res = base + __ffsll((long long)m) - 1;
@@ -162,15 +157,29 @@ rec_sync_kernel(const uint8_t* __restrict__ d, int64_t o, int64_t n, int64_t nse
     }
 }
 
+// Per contig (index n_ref: the records without coordinates), accumulated by
+// the fill walk: the inflated-stream offsets of its first record (stored
+// complemented, so a zeroed table starts empty under atomicMax) and of the
+// end of its last one, and its mapped / unmapped / kept record counts — a
+// BAI's pseudo-bin once the offsets are turned into virtual offsets.
+struct ExtAcc {
+    unsigned long long nfirst, end, mapped, unmapped, kept;
+};
+
 // One lane per segment: walk [seg_off[i], seg_off[i+1]) (kFill: write the
 // kept intervals at out_off[i]).  The walk of a segment ends at the first
 // record boundary >= seg_off[i+1], at an incomplete record, or at an error.
+// tid_map (optional, a contig-subset decode): a kept record's tid becomes
+// tid_map[tid], and a record whose entry is negative is not kept.  ext
+// (kFill, optional): the per-contig table, offsets plus `base` (the stream
+// offset of d[0]), one set of atomics per run of one contig in a segment.
 template <bool kFill>
 __global__ void __launch_bounds__(256)
 rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restrict__ seg_off, int64_t first,
                 int64_t nseg, int32_t n_ref, uint32_t flag_filter, SegRes* __restrict__ res,
                 const int64_t* __restrict__ out_off, int32_t* __restrict__ tid, int32_t* __restrict__ pos,
-                int32_t* __restrict__ span) {
+                int32_t* __restrict__ span, const int32_t* __restrict__ tid_map, ExtAcc* __restrict__ ext,
+                int64_t base) {
     const int64_t i = first + (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= nseg) return;
     int64_t q = seg_off[i];
@@ -182,6 +191,19 @@ rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restr
         w = out_off[i];
         w_end = w + res[i].kept;
     }
+    // the current run of one contig (ext)
+    int32_t run_t = -2;
+    int64_t run_q0 = 0, run_q1 = 0;
+    unsigned long long run_m = 0, run_u = 0, run_k = 0;
+    auto flush = [&]() {
+        if (run_t < -1) return;
+        ExtAcc* e = ext + (run_t < 0 ? n_ref : run_t);
+        atomicMax(&e->nfirst, ~(unsigned long long)(base + run_q0));
+        atomicMax(&e->end, (unsigned long long)(base + run_q1));
+        if (run_m) atomicAdd(&e->mapped, run_m);
+        if (run_u) atomicAdd(&e->unmapped, run_u);
+        if (run_k) atomicAdd(&e->kept, run_k);
+    };
     while (q < end) {
         if (q + 4 > n) {
             err = kSegIncomplete;
@@ -199,7 +221,8 @@ rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restr
         }
         const uint8_t* r = d + q + 4;
         mc::gz::RecOut ro;
-        const int rc = mc::gz::rec_parse(r, r + bs, n_ref, flag_filter, ro);
+        int rc = mc::gz::rec_parse(r, r + bs, n_ref, flag_filter, ro);
+        const int64_t q0 = q;
         q += 4 + (int64_t)bs;
         ++records;
         mapped += ro.mapped ? 1 : 0;
@@ -207,6 +230,24 @@ rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restr
             err = rc == 2 ? kSegTid : rc == 3 ? kSegCigar : kSegSpan;
             err_at = q;
             break;
+        }
+        const int32_t raw_t = mc::gz::ld_i32(r);
+        if (rc == 1 && tid_map) {
+            const int32_t lt = tid_map[ro.tid];
+            if (lt < 0) rc = 0;
+            ro.tid = lt;
+        }
+        if (kFill && ext && raw_t >= -1 && raw_t < n_ref) {
+            if (raw_t != run_t) {
+                flush();
+                run_t = raw_t;
+                run_q0 = q0;
+                run_m = run_u = run_k = 0;
+            }
+            run_q1 = q;
+            if (raw_t >= 0 && !(mc::gz::ld_u16(r + 14) & 4u)) ++run_m;
+            else ++run_u;
+            if (rc == 1) ++run_k;
         }
         if (rc == 1) {
             if (kFill && w < w_end) {
@@ -218,6 +259,7 @@ rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restr
             ++kept;
         }
     }
+    if (kFill && ext) flush();
     if (!kFill) {
         SegRes s;
         s.landing = q;
@@ -314,10 +356,19 @@ struct mc_bam_gpu {
     PinnedBuf<int64_t> h64;
     PinnedBuf<SegRes> hres;
     PinnedBuf<GzBlock> hblk;
+    DBuf<ExtAcc> ext;                 // per-contig table of the walk (n_ref + 1 entries)
+    DBuf<int32_t> tid_map;            // contig-subset decode: header tid -> local id (or -1)
+    DBuf<uint8_t> raw;                // contig-subset decode: the inflated blocks before compaction
+    std::vector<mc::bgzf::Block> blk_list;   // whole-file decode: the blocks (stream offset -> virtual offset)
+    bool subset = false;
+    std::vector<int32_t> sel;                // contig-subset decode: the selected header tids, sorted
+    std::vector<mc_contig_extent> ext_in;    // contig-subset decode: the extents it was opened with
+    int64_t n_no_coor_in = 0;
     // timings (ms)
     double t_read = 0, t_inflate = 0, t_parse = 0, t_total = 0, t_scan = 0;
     double t_upload = 0, t_kernel = 0, t_open = 0;   // every upload_file_range call; inflate launches (HIP events, summed)
     int64_t windows = 0, blocks = 0, resyncs = 0, inflated_bytes = 0, compressed_bytes = 0;
+    int64_t parse_rounds = 0, resync_passes = 0;
     ~mc_bam_gpu() {
         for (hipStream_t s : {stream, up_stream, kstream[0], kstream[1], kstream[2]}) {
             if (s) {
@@ -365,10 +416,37 @@ const char* gz_err_msg(int e) {
 #ifndef MC_UPLOAD_SLICE_MIB
 #define MC_UPLOAD_SLICE_MIB 64
 #endif
-// progress (optional): file offset below which every byte is on the device
-// (advanced as copies complete); cancel (optional): stop at the next slice.
+// A contig-subset decode uploads only some byte ranges of the file, back to
+// back: a virtual offset v lies in segment k at file offset f + (v - v_k).
+// Without a map (nullptr) virtual offsets are file offsets.
+struct VSeg {
+    size_t v, f, len;
+};
+using VMap = std::vector<VSeg>;
+
+// pread of virtual bytes [v, v + len): the part inside v's segment (the
+// caller's loop continues with the rest); -1 if v is outside the map.
+ssize_t pread_v(int fd, const VMap* vm, uint8_t* buf, size_t len, size_t v) {
+    if (!vm) return pread(fd, buf, len, (off_t)v);
+    auto it = std::upper_bound(vm->begin(), vm->end(), v, [](size_t x, const VSeg& s) { return x < s.v; });
+    if (it == vm->begin()) return -1;
+    --it;
+    if (v >= it->v + it->len) return -1;
+    return pread(fd, buf, std::min(len, it->v + it->len - v), (off_t)(it->f + (v - it->v)));
+}
+
+size_t file_off(const VMap* vm, size_t v) {
+    if (!vm) return v;
+    auto it = std::upper_bound(vm->begin(), vm->end(), v, [](size_t x, const VSeg& s) { return x < s.v; });
+    return it == vm->begin() ? v : std::prev(it)->f + (v - std::prev(it)->v);
+}
+
+// progress (optional): virtual offset below which every byte is on the
+// device (advanced as copies complete); cancel (optional): stop at the next
+// slice.  off, len: a virtual range (vm: the map, nullptr: the file itself).
 int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* dst, hipStream_t st,
-                      std::atomic<size_t>* progress = nullptr, const std::atomic<bool>* cancel = nullptr) {
+                      std::atomic<size_t>* progress = nullptr, const std::atomic<bool>* cancel = nullptr,
+                      const VMap* vm = nullptr) {
     constexpr size_t kSlice = (size_t)MC_UPLOAD_SLICE_MIB << 20;
     constexpr int kStage = 3;
     if (len == 0) return MC_OK;
@@ -416,7 +494,7 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
             uint8_t* buf = g->stage[k % kStage].p;
             bool ok = true;
             for (size_t got = a; got < b;) {
-                const ssize_t r = pread(fd, buf + got, b - got, (off_t)(off + at + got));
+                const ssize_t r = pread_v(fd, vm, buf + got, b - got, off + at + got);
                 if (r <= 0) {
                     ok = false;
                     break;
@@ -495,10 +573,29 @@ int upload_file_range(mc_bam_gpu* g, int fd, size_t off, size_t len, uint8_t* ds
     return MC_OK;
 }
 
+// Segment starts (i0, nseg) of inflated[o, n) from a sync with chains of
+// `chain` records, none before seg[i0] (seg[nseg] = n is kept).
+int sync_segments(mc_bam_gpu* g, int64_t o, int64_t n, int64_t i0, int64_t nseg, int chain,
+                  std::vector<int64_t>& seg) {
+    hipStream_t st = g->stream;
+    const int64_t todo = nseg - (i0 + 1);
+    if (todo <= 0) return MC_OK;
+    int64_t* h = g->h64.p;
+    const int grid = (int)std::min<int64_t>((todo + 3) / 4, 65536);
+    rec_sync_kernel<<<grid, 256, 0, st>>>(g->inflated.p, o, n, i0 + 1, nseg, (int32_t)g->hdr.names.size(), chain,
+                                          g->found.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h + i0 + 1, g->found.p + i0 + 1, todo * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int64_t i = nseg - 1; i > i0; --i) seg[i] = std::max(seg[i0], std::min(std::min(h[i], n), seg[i + 1]));
+    return MC_OK;
+}
+
 // Parses the records in inflated[o, n); partial: the window is not the
 // file's last, so an incomplete last record is carried (*consumed = its
-// offset).  Appends kept intervals to g->tid/pos/span.
-int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* consumed) {
+// offset).  Appends kept intervals to g->tid/pos/span; base: the stream
+// offset of inflated[0] (the per-contig table's offsets).
+int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* consumed, int64_t base = 0) {
     hipStream_t st = g->stream;
     const int32_t n_ref = (int32_t)g->hdr.names.size();
     const uint8_t* d = g->inflated.p;
@@ -510,29 +607,31 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     HIP_TRY(g->h64.reserve(nseg + 1));
     HIP_TRY(g->hres.reserve(nseg));
     int64_t* h = g->h64.p;
-    if (nseg > 1) {
-        const int grid = (int)std::min<int64_t>((nseg - 1 + 3) / 4, 65536);
-        rec_sync_kernel<<<grid, 256, 0, st>>>(d, o, n, nseg, n_ref, g->found.p);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(h, g->found.p, (nseg + 1) * 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
-    std::vector<int64_t> seg(nseg + 1);
+    std::vector<int64_t> seg(nseg + 1, n);
     seg[0] = o;
-    seg[nseg] = n;
-    for (int64_t i = nseg - 1; i >= 1; --i) seg[i] = std::min(std::min(h[i], n), seg[i + 1]);
-    // walk / check rounds: segments before `first` are exact and consistent
+    if (int rc = sync_segments(g, o, n, 0, nseg, kSyncChain, seg)) return rc;
+    // walk / check rounds: segments before `first` are exact and consistent.
+    // Each round verifies at least one more segment.  Repeated false syncs
+    // (a record's bytes holding record-like chains) are re-synced from the
+    // verified prefix with much longer chains instead of walking the rest in
+    // one lane; a stream that still does not settle is refused.
     int64_t first = 0;
     SegRes* R = g->hres.p;
+    bool tail_cut = false;   // a partial window's records ended early: later segments stay empty
     for (int round = 0;; ++round) {
-        if (round == 32) {   // bounded: the rest becomes one segment walked by one lane
-            for (int64_t j = first + 1; j < nseg; ++j) seg[j] = n;
+        g->parse_rounds = std::max<int64_t>(g->parse_rounds, round + 1);
+        if ((round == 3 || round == 8) && !tail_cut) {
+            if (int rc = sync_segments(g, o, n, first, nseg, round == 3 ? 64 : 1024, seg)) return rc;
+            ++g->resync_passes;
         }
+        MC_REQUIRE(round < 16, MC_E_IO, "%s: no consistent record boundaries after %d parse rounds", g->path.c_str(),
+                   round);
         std::memcpy(h, seg.data() + first, (nseg + 1 - first) * 8);
         HIP_TRY(hipMemcpyAsync(g->seg_off.p + first, h, (nseg + 1 - first) * 8, hipMemcpyHostToDevice, st));
         const int grid = (int)((nseg - first + 255) / 256);
         rec_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->flag_filter,
-                                                     g->res.p, nullptr, nullptr, nullptr, nullptr);
+                                                     g->res.p, nullptr, nullptr, nullptr, nullptr,
+                                                     g->tid_map.p, nullptr, 0);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(R + first, g->res.p + first, (nseg - first) * sizeof(SegRes),
                                hipMemcpyDeviceToHost, st));
@@ -556,6 +655,7 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
             if (r.err == kSegIncomplete) {
                 if (partial) {
                     // the window's records end here: later segments are empty
+                    tail_cut = true;
                     if (end != n) {
                         for (int64_t j = i + 1; j < nseg; ++j) seg[j] = n;
                         redo = i + 1;   // (their walks are empty: nothing to redo but the copy)
@@ -621,10 +721,11 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     HIP_TRY(g->tid.reserve(need, st, g->n_kept));
     HIP_TRY(g->pos.reserve(need, st, g->n_kept));
     HIP_TRY(g->span.reserve(need, st, g->n_kept));
-    if (total) {
+    if (total || g->ext.p) {
         const int grid = (int)((nseg + 255) / 256);
         rec_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->flag_filter, g->res.p,
-                                                    g->out_off.p, g->tid.p, g->pos.p, g->span.p);
+                                                    g->out_off.p, g->tid.p, g->pos.p, g->span.p, g->tid_map.p,
+                                                    g->ext.p, base);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipStreamSynchronize(st));
@@ -671,17 +772,25 @@ bool pread_all(int fd, uint8_t* buf, size_t len, size_t off) {
     return true;
 }
 
-// The block list of the whole file through pread, by nt threads (the GPU
-// decode's scan; no mapping): each of 4 nt byte ranges starts at the first
-// offset of a window that begins a chain of 4 valid headers (or one reaching
-// the end of the file); then one pread per block takes its ISIZE and the next
-// block's header (adjacent in the file).  The ranges' hops must meet exactly,
-// else one sequential hop from offset 0 decides.
-int scan_blocks_pread(int fd, size_t n, int nt, const char* path, std::vector<Block>& blocks, size_t& total) {
+// A byte range of the file whose BGZF blocks a decode needs: the blocks from
+// a (a block start) up to f (a block start, or the end of the file), plus the
+// block at f when `extra`.
+struct FileExtent {
+    size_t a, f;
+    bool extra;
+};
+
+// The blocks of the extents, in order, their `out` offsets continuing across
+// extents from *total, through pread by nt threads (the GPU decode's scan; no
+// mapping).  An extent of >= 64 MiB is cut into pieces (up to 4 nt), each
+// starting at the first offset of a window that begins a chain of 4 valid
+// headers (or one reaching the end of the file); one pread per block then
+// takes its ISIZE and the next block's header (adjacent in the file).  The
+// pieces' hops must meet exactly, else one sequential hop of the extent
+// decides.  ex_first (optional): each extent's first block index.
+int scan_extents_pread(int fd, size_t n, int nt, const char* path, const std::vector<FileExtent>& ex,
+                       std::vector<Block>& blocks, size_t& total, std::vector<size_t>* ex_first = nullptr) {
     constexpr size_t kMaxBlock = 65536, kHdr = 96;
-    const size_t nr = n < (64u << 20) ? 1 : (size_t)std::max(1, nt) * 4;
-    std::vector<size_t> start(nr + 1, n);
-    start[0] = 0;
     std::atomic<bool> io_err{false};
     auto sync = [&](size_t from, std::vector<uint8_t>& w) -> size_t {
         const size_t wl = std::min(n - from, 5 * kMaxBlock + kHdr);
@@ -701,11 +810,10 @@ int scan_blocks_pread(int fd, size_t n, int nt, const char* path, std::vector<Bl
             }
             if (k == 4 || (to_eof && z == wl)) return from + q;
         }
-        return n;   // no chain here: the ranges will not meet, the sequential hop decides
+        return n;   // no chain here: the pieces will not meet, the sequential hop decides
     };
     // the blocks of [a, end): false unless the hop lands exactly on end
     // (*stop: the offset it stopped at)
-    size_t seq_stop = 0;
     auto hop = [&](size_t a, size_t end, std::vector<Block>& out, size_t* stop) -> bool {
         *stop = a;
         if (a >= n) return a == end;
@@ -748,46 +856,84 @@ int scan_blocks_pread(int fd, size_t n, int nt, const char* path, std::vector<Bl
         }
         return o == end;
     };
-    std::vector<std::vector<Block>> part(nr);
-    std::vector<char> ok(nr, 1);
-    {
-        std::atomic<size_t> next{1};
-        auto w1 = [&]() {
-            std::vector<uint8_t> w;
-            for (size_t i; (i = next.fetch_add(1)) < nr;) start[i] = sync(n / nr * i, w);
-        };
-        std::vector<std::thread> pool;
-        for (int t = 1; t < nt; ++t) pool.emplace_back(w1);
-        w1();
-        for (auto& t : pool) t.join();
+    // pieces: [start[p], end of piece p) of extent pex[p]; pfirst[k]: extent k's first piece
+    std::vector<size_t> start, pex, pfirst;
+    for (size_t k = 0; k < ex.size(); ++k) {
+        MC_REQUIRE(ex[k].a <= ex[k].f && ex[k].f <= n, MC_E_IO, "%s: block range [%zu, %zu) outside the file", path,
+                   ex[k].a, ex[k].f);
+        const size_t len = ex[k].f - ex[k].a;
+        const size_t np = len < (64u << 20) ? 1
+                                            : std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, nt) * 4,
+                                                                                   len / (4u << 20)));
+        pfirst.push_back(start.size());
+        for (size_t j = 0; j < np; ++j) {
+            start.push_back(ex[k].a + len / np * j);
+            pex.push_back(k);
+        }
     }
+    pfirst.push_back(start.size());
+    const size_t npc = start.size();
+    auto piece_end = [&](size_t p) { return p + 1 < pfirst[pex[p] + 1] ? start[p + 1] : ex[pex[p]].f; };
+    auto pool_run = [&](const std::function<void()>& w) {
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(w);
+        w();
+        for (auto& t : pool) t.join();
+    };
     {
         std::atomic<size_t> next{0};
-        auto w2 = [&]() {
+        pool_run([&]() {
+            std::vector<uint8_t> w;
+            for (size_t p; (p = next.fetch_add(1)) < npc;)
+                if (p != pfirst[pex[p]]) start[p] = std::min(sync(start[p], w), ex[pex[p]].f);
+        });
+    }
+    for (size_t p = 1; p < npc; ++p)
+        if (p != pfirst[pex[p]]) start[p] = std::max(start[p], start[p - 1]);
+    std::vector<std::vector<Block>> part(npc);
+    std::vector<char> ok(npc, 1);
+    {
+        std::atomic<size_t> next{0};
+        pool_run([&]() {
             size_t stop;
-            for (size_t i; (i = next.fetch_add(1)) < nr;) ok[i] = hop(start[i], start[i + 1], part[i], &stop);
-        };
-        std::vector<std::thread> pool;
-        for (int t = 1; t < nt; ++t) pool.emplace_back(w2);
-        w2();
-        for (auto& t : pool) t.join();
+            for (size_t p; (p = next.fetch_add(1)) < npc;) ok[p] = hop(start[p], piece_end(p), part[p], &stop);
+        });
     }
     MC_REQUIRE(!io_err, MC_E_IO, "%s: read failed while scanning the BGZF blocks", path);
-    bool chained = true;
-    for (char c : ok) chained &= c != 0;
-    if (!chained) {
-        part.assign(1, {});
-        MC_REQUIRE(hop(0, n, part[0], &seq_stop), MC_E_IO,
-                   "%s: no valid BGZF block at offset %zu (truncated, or not bgzip-compressed BAM)", path, seq_stop);
-        MC_REQUIRE(!io_err, MC_E_IO, "%s: read failed while scanning the BGZF blocks", path);
-    }
-    for (auto& p : part)
-        for (Block& b : p) {
-            b.out = total;
-            total += b.isize;
-            blocks.push_back(b);
+    for (size_t k = 0; k < ex.size(); ++k) {
+        bool chained = true;
+        for (size_t p = pfirst[k]; p < pfirst[k + 1]; ++p) chained &= ok[p] != 0;
+        if (!chained) {   // one sequential hop of the extent
+            for (size_t p = pfirst[k]; p < pfirst[k + 1]; ++p) part[p].clear();
+            size_t stop = 0;
+            MC_REQUIRE(hop(ex[k].a, ex[k].f, part[pfirst[k]], &stop), MC_E_IO,
+                       "%s: no valid BGZF block at offset %zu (truncated, or not bgzip-compressed BAM)", path, stop);
+            MC_REQUIRE(!io_err, MC_E_IO, "%s: read failed while scanning the BGZF blocks", path);
         }
+        if (ex[k].extra) {   // the block at f
+            std::vector<Block>& last = part[pfirst[k + 1] - 1];
+            const size_t before = last.size();
+            size_t stop = 0;
+            (void)hop(ex[k].f, ex[k].f + 1, last, &stop);
+            MC_REQUIRE(!io_err, MC_E_IO, "%s: read failed while scanning the BGZF blocks", path);
+            MC_REQUIRE(last.size() == before + 1, MC_E_IO, "%s: no valid BGZF block at offset %zu", path, ex[k].f);
+        }
+    }
+    for (size_t k = 0; k < ex.size(); ++k) {
+        if (ex_first) ex_first->push_back(blocks.size());
+        for (size_t p = pfirst[k]; p < pfirst[k + 1]; ++p)
+            for (Block& b : part[p]) {
+                b.out = total;
+                total += b.isize;
+                blocks.push_back(b);
+            }
+    }
     return MC_OK;
+}
+
+// The block list of the whole file (scan_extents_pread over one extent).
+int scan_blocks_pread(int fd, size_t n, int nt, const char* path, std::vector<Block>& blocks, size_t& total) {
+    return scan_extents_pread(fd, n, nt, path, {FileExtent{0, n, false}}, blocks, total);
 }
 
 // Header from a growing prefix of the inflated bytes [0, n): *ok = false if
@@ -856,8 +1002,34 @@ struct BgUpload {
     }
 };
 
-int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<Block>& blocks, size_t total,
-                        int64_t max_lanes, BgUpload* bg) {
+// Inflate lanes the grid is sized for: kGzLanes per wave, as many waves per
+// CU as the kernel's LDS and registers allow on this device (at most
+// kGzWavesPerCu, the count for gfx950's 160 KiB of LDS per CU).
+int64_t gz_max_lanes(int device) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    int per_cu = kGzWavesPerCu;
+    int nb = 0;
+    if (MC_GZ_WAVES_PER_CU == 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gz_inflate_kernel, kGzThreads, 0) == hipSuccess && nb > 0)
+        per_cu = std::min(per_cu, nb);
+    return (int64_t)cus * per_cu * kGzLanes;
+}
+
+// The resident decode's device memory (compressed bytes, inflated stream,
+// block table, lane scratch; `extra`: more, e.g. a compaction buffer) fits
+// in half of `free_b`.
+bool resident_fits(size_t comp, size_t total, size_t nblocks, int64_t max_lanes, size_t free_b, size_t extra = 0) {
+    const size_t need = comp + total + extra + nblocks * (sizeof(GzBlock) + sizeof(int)) +
+                        (size_t)kGzPieceStreams * (size_t)max_lanes * kGzSlotWords * sizeof(uint16_t);
+    return need <= free_b / 2;
+}
+
+// The pieces' uploads and inflate launches of the resident decode: blocks
+// (offsets in the virtual layout of vm, nullptr: the file) inflate into
+// dst[0, total); vsize: the virtual bytes (the compressed buffer's size).
+int inflate_resident(mc_bam_gpu* g, int fd, const VMap* vm, size_t vsize, const std::vector<Block>& blocks,
+                     size_t total, int64_t max_lanes, BgUpload* bg, uint8_t* dst) {
     const int64_t nb = (int64_t)blocks.size();
     hipStream_t st = g->stream;
     const size_t piece = std::min<size_t>(4ull << 30, std::max<size_t>(256ull << 20, total / MC_GZ_PIECES));
@@ -868,8 +1040,7 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
         pcs.emplace_back(b0, b1);
         b0 = b1;
     }
-    HIP_TRY(g->comp[0].reserve(mf.size + kPad));
-    HIP_TRY(g->inflated.reserve(total + 8));
+    HIP_TRY(g->comp[0].reserve(vsize + kPad));
     HIP_TRY(g->hblk.reserve(nb));
     for (int64_t i = 0; i < nb; ++i) {
         const Block& b = blocks[i];
@@ -881,7 +1052,7 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
     HIP_TRY(g->scratch.reserve((size_t)(kGzPieceStreams * slot)));
     HIP_TRY(hipMemcpyAsync(g->blk.p, g->hblk.p, nb * sizeof(GzBlock), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(g->status.p + nb, 0, sizeof(int), st));
-    HIP_TRY(hipMemsetAsync(g->comp[0].p + mf.size, 0, kPad, st));
+    HIP_TRY(hipMemsetAsync(g->comp[0].p + vsize, 0, kPad, st));
     hipStream_t ks[kGzPieceStreams];
     ks[0] = st;
     for (int k = 1; k < kGzPieceStreams; ++k) {
@@ -912,7 +1083,7 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
     double t_first = now_s();
     for (size_t p = 0; p < pcs.size(); ++p) {
         const size_t b0 = pcs[p].first, b1 = pcs[p].second;
-        const size_t coff = blocks[b0].off, cend = b1 < blocks.size() ? blocks[b1].off : mf.size;
+        const size_t coff = blocks[b0].off, cend = b1 < blocks.size() ? blocks[b1].off : vsize;
         const double t0 = now_s();
         if (bg) {
             // the background upload has passed the piece (its copies are
@@ -927,7 +1098,8 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
             }
         } else {
             // returns once the bytes are on the device (its stream synchronised)
-            if (int rc = upload_file_range(g, mf.fd, coff, cend - coff, g->comp[0].p + coff, g->up_stream))
+            if (int rc = upload_file_range(g, fd, coff, cend - coff, g->comp[0].p + coff, g->up_stream, nullptr,
+                                               nullptr, vm))
                 return rc;
         }
         if (p == 0) {
@@ -939,7 +1111,7 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
         const int k = (int)(p % kGzPieceStreams);
         HIP_TRY(hipEventRecord(kev[2 * p], ks[k]));
         gz_inflate_kernel<<<(int)(lanes / kGzLanes), kGzThreads, 0, ks[k]>>>(
-            g->comp[0].p, g->blk.p + b0, n, g->inflated.p, g->scratch.p + k * slot, g->status.p + b0,
+            g->comp[0].p, g->blk.p + b0, n, dst, g->scratch.p + k * slot, g->status.p + b0,
             g->status.p + nb);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(kev[2 * p + 1], ks[k]));
@@ -964,14 +1136,31 @@ int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<B
         for (int64_t i = 0; i < nb; ++i)
             if (sv[i]) {
                 mc::set_error("BGZF inflate failed in %s (block at file offset %zu: %s)", g->path.c_str(),
-                              blocks[i].off, gz_err_msg(sv[i]));
+                              file_off(vm, blocks[i].off), gz_err_msg(sv[i]));
                 return MC_E_IO;
             }
     }
+    return MC_OK;
+}
+
+// The per-contig table of the record walk, zeroed (n_ref + 1 entries).
+int init_ext(mc_bam_gpu* g) {
+    const size_t m = g->hdr.names.size() + 1;
+    HIP_TRY(g->ext.reserve(m));
+    HIP_TRY(hipMemsetAsync(g->ext.p, 0, m * sizeof(ExtAcc), g->stream));
+    return MC_OK;
+}
+
+int gpu_decode_resident(mc_bam_gpu* g, const MappedFile& mf, const std::vector<Block>& blocks, size_t total,
+                        int64_t max_lanes, BgUpload* bg) {
+    HIP_TRY(g->inflated.reserve(total + 8));
+    if (int rc = inflate_resident(g, mf.fd, nullptr, mf.size, blocks, total, max_lanes, bg, g->inflated.p))
+        return rc;
     int64_t o = 0;
     bool ok = false;
     if (int rc = header_from_prefix(g, total, &o, &ok)) return rc;
     MC_REQUIRE(ok, MC_E_IO, "%s: no valid BAM header", g->path.c_str());
+    if (int rc = init_ext(g)) return rc;
     const double t1 = now_s();
     int64_t consumed = 0;
     if (int rc = parse_window(g, o, (int64_t)total, false, &consumed)) return rc;
@@ -1026,22 +1215,21 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
             for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
         }
     } evg{ev};
-    // scratch for the inflate lanes
-    int dev_cus = 256;
-    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g->device);
-    const int64_t max_lanes = (int64_t)dev_cus * kGzWavesPerCu * kGzLanes;
+    const int64_t max_lanes = gz_max_lanes(g->device);
     if (window_bytes <= 0 && !blocks.empty()) {
         // resident when the compressed file, its inflated stream and the
-        // scratch take at most half of the free device memory
+        // scratch take at most half of the device memory free before the
+        // decode (the background upload's buffer, already allocated, counts
+        // as free: it is the compressed file of `need`)
         size_t free_b = 0, tot_b = 0;
         HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
-        const size_t need = mf.size + total + blocks.size() * (sizeof(GzBlock) + sizeof(int)) +
-                            (size_t)kGzPieceStreams * (size_t)max_lanes * kGzSlotWords * sizeof(uint16_t);
-        if (need <= free_b / 2) {
+        if (bg.t.joinable()) free_b += g->comp[0].cap;
+        if (resident_fits(mf.size, total, blocks.size(), max_lanes, free_b)) {
             const int rc = gpu_decode_resident(g, mf, blocks, total, max_lanes, bg.t.joinable() ? &bg : nullptr);
             if (rc == MC_OK && bg.t.joinable()) {
                 if (int urc = bg.join()) return urc;
             }
+            g->blk_list = std::move(blocks);
             g->t_total = (now_s() - t_start) * 1e3;
             return rc;
         }
@@ -1049,6 +1237,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
     if (bg.t.joinable()) {   // not resident after all: the windows upload their own bytes
         bg.cancel = true;
         bg.t.join();
+        g->comp[0].release();   // (the windows size their own buffers)
     }
     // windows of blocks (<= win inflated bytes each, at least one block)
     std::vector<std::pair<size_t, size_t>> wins;
@@ -1187,6 +1376,7 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
                     g->hdr.lens = std::move(lens);
                     o = (int64_t)ho;
                     have_header = true;
+                    if (int rc = init_ext(g)) return rc;
                     break;
                 }
                 if (p >= n) break;
@@ -1202,7 +1392,8 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         }
         const double t1 = now_s();
         int64_t consumed = 0;
-        if (int rc = parse_window(g, o, (int64_t)n, !last, &consumed)) return rc;
+        if (int rc = parse_window(g, o, (int64_t)n, !last, &consumed, (int64_t)(blocks[b0].out - carry)))
+            return rc;
         g->t_parse += (now_s() - t1) * 1e3;
         carry = n - (size_t)consumed;
         if (last) {
@@ -1217,7 +1408,263 @@ int gpu_decode(mc_bam_gpu* g, int64_t window_bytes) {
         ++g->windows;
     }
     HIP_TRY(hipStreamSynchronize(st));
+    g->blk_list = std::move(blocks);
     g->t_total = (now_s() - t_start) * 1e3;
+    return MC_OK;
+}
+
+// The BAM header through pread of the leading blocks (inflated on the host).
+int read_header_pread(int fd, size_t n, const char* path, std::vector<std::string>& names,
+                      std::vector<int64_t>& lens) {
+    std::vector<uint8_t> buf, blk(65536);
+    size_t off = 0;
+    for (;;) {
+        MC_REQUIRE(off < n, MC_E_IO, "%s: truncated BAM header", path);
+        const size_t hn = std::min<size_t>(n - off, blk.size());
+        MC_REQUIRE(pread_all(fd, blk.data(), hn, off), MC_E_IO, "%s: read failed", path);
+        const size_t b = bgzf_hdr(blk.data(), hn, 0);
+        MC_REQUIRE(b, MC_E_IO, "%s: no valid BGZF block at offset %zu", path, off);
+        const size_t xlen = rd16(blk.data() + 10), isize = rd32(blk.data() + b - 4);
+        const size_t at = buf.size();
+        buf.resize(at + isize);
+        MC_REQUIRE(isize == 0 || inflate_block(blk.data() + 12 + xlen, b - xlen - 20, buf.data() + at, isize), MC_E_IO,
+                   "BGZF inflate failed in %s", path);
+        off += b;
+        names.clear();
+        lens.clear();
+        size_t o = 0;
+        if (buf.size() >= 12 && parse_header(buf.data(), buf.size(), path, names, lens, &o) == MC_OK) return MC_OK;
+        MC_REQUIRE(buf.size() < (size_t(1) << 31), MC_E_IO, "%s: no valid BAM header", path);
+    }
+}
+
+// Size of the BGZF block at file offset o (0 if none).
+size_t block_size_at(int fd, size_t n, size_t o) {
+    uint8_t h[96];
+    const size_t hn = std::min<size_t>(sizeof h, n - std::min(n, o));
+    if (hn < 18 || !pread_all(fd, h, hn, o)) return 0;
+    return bgzf_hdr_at(h, hn, o, n);
+}
+
+// Block i of `blocks` (file offsets, sorted) in [b0, b1) at file offset off.
+int64_t block_at(const std::vector<Block>& blocks, size_t b0, size_t b1, size_t off) {
+    auto it = std::lower_bound(blocks.begin() + b0, blocks.begin() + b1, off,
+                               [](const Block& b, size_t x) { return b.off < x; });
+    return it != blocks.begin() + b1 && it->off == off ? (int64_t)(it - blocks.begin()) : -1;
+}
+
+// One rank's contigs (sel) decoded on the GPU from the extents table: only
+// the BGZF blocks holding their records are read (the extents' byte ranges,
+// back to back in a virtual layout), uploaded and inflated; each contig's
+// inflated range [first record, end of the last) is copied into one compact
+// record stream, which one parse walks with a tid map (header tid -> local
+// id).  The header counts are the whole file's, from the table.
+int gpu_decode_extents(mc_bam_gpu* g, int32_t n_ref_in, const mc_contig_extent* ext, int64_t n_no_coor,
+                       int32_t n_sel, const int32_t* sel_in) {
+    const double t_start = now_s();
+    const char* path = g->path.c_str();
+    MappedFile mf;
+    if (int rc = mf.open(path, false)) return rc;
+    if (int rc = read_header_pread(mf.fd, mf.size, path, g->hdr.names, g->hdr.lens)) return rc;
+    const int32_t n_ref = (int32_t)g->hdr.names.size();
+    MC_REQUIRE(n_ref_in == n_ref, MC_E_INVALID, "%s: the extents table has %d contigs, the BAM header %d", path,
+               n_ref_in, n_ref);
+    g->subset = true;
+    g->sel.assign(sel_in, sel_in + n_sel);
+    std::sort(g->sel.begin(), g->sel.end());
+    g->sel.erase(std::unique(g->sel.begin(), g->sel.end()), g->sel.end());
+    for (int32_t t : g->sel) MC_REQUIRE(t >= 0 && t < n_ref, MC_E_INVALID, "contig %d out of range", t);
+    g->ext_in.assign(ext, ext + n_ref);
+    g->n_no_coor_in = n_no_coor;
+    for (const mc_contig_extent& e : g->ext_in) {
+        g->hdr.n_mapped += e.n_mapped;
+        g->hdr.n_unmapped += e.n_unmapped;
+    }
+    g->hdr.n_unmapped += n_no_coor;
+    g->hdr.n_records = g->hdr.n_mapped + g->hdr.n_unmapped;
+    // the selected contigs with records, in file order, and their file extents
+    struct Cr {
+        int32_t tid;
+        uint64_t beg, end;
+        size_t ext = 0;
+        int64_t q0 = 0, q1 = 0;
+    };
+    std::vector<Cr> crs;
+    for (int32_t t : g->sel) {
+        const mc_contig_extent& e = ext[t];
+        if ((uint64_t)e.end_voff <= (uint64_t)e.beg_voff) continue;
+        MC_REQUIRE(((uint64_t)e.beg_voff >> 16) < mf.size && ((uint64_t)e.end_voff >> 16) <= mf.size, MC_E_IO,
+                   "%s: the extent of contig %d lies outside the file", path, t);
+        crs.push_back(Cr{t, (uint64_t)e.beg_voff, (uint64_t)e.end_voff});
+    }
+    std::sort(crs.begin(), crs.end(), [](const Cr& a, const Cr& b) { return a.beg < b.beg; });
+    std::vector<FileExtent> fx;
+    for (Cr& c : crs) {
+        const size_t a = c.beg >> 16, f = c.end >> 16;
+        const bool extra = (c.end & 0xffff) != 0;
+        if (!fx.empty() && a <= fx.back().f) {   // shares (or starts at) the previous extent's last block
+            FileExtent& b = fx.back();
+            if (f > b.f) {
+                b.f = f;
+                b.extra = extra;
+            } else if (f == b.f) {
+                b.extra |= extra;
+            }
+        } else {
+            fx.push_back(FileExtent{a, f, extra});
+        }
+        c.ext = fx.size() - 1;
+    }
+    // the virtual layout: the extents' bytes back to back
+    VMap vm;
+    size_t vsize = 0;
+    for (const FileExtent& x : fx) {
+        size_t e = x.f;
+        if (x.extra) {
+            const size_t b = block_size_at(mf.fd, mf.size, x.f);
+            MC_REQUIRE(b, MC_E_IO, "%s: no valid BGZF block at offset %zu (index offsets do not match the BAM)", path,
+                       x.f);
+            e += b;
+        }
+        vm.push_back(VSeg{vsize, x.a, e - x.a});
+        vsize += e - x.a;
+    }
+    // the upload runs beside the block scan
+    BgUpload bg;
+    if (vsize >= (size_t)(64ull << 20)) {
+        size_t free_b = 0, tot_b = 0;
+        HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
+        if (vsize * 4 <= free_b / 2) {
+            HIP_TRY(g->comp[0].reserve(vsize + kPad));
+            bg.t = std::thread([&]() {
+                if (hipSetDevice(g->device) != hipSuccess) {
+                    bg.rc = MC_E_HIP;
+                    bg.msg = "hipSetDevice failed in the upload thread";
+                } else {
+                    bg.rc = upload_file_range(g, mf.fd, 0, vsize, g->comp[0].p, g->up_stream, &bg.progress,
+                                              &bg.cancel, &vm);
+                    if (bg.rc) bg.msg = mc::last_error();
+                }
+                bg.finished.store(true, std::memory_order_release);
+            });
+        }
+    }
+    std::vector<Block> blocks;
+    std::vector<size_t> ex_first;
+    size_t total = 0;
+    if (int rc = scan_extents_pread(mf.fd, mf.size, g->nt, path, fx, blocks, total, &ex_first)) return rc;
+    ex_first.push_back(blocks.size());
+    g->t_scan = (now_s() - t_start) * 1e3;
+    g->blocks = (int64_t)blocks.size();
+    g->inflated_bytes = (int64_t)total;
+    g->compressed_bytes = (int64_t)vsize;
+    // each contig's range of the inflated stream
+    for (Cr& c : crs) {
+        const size_t k = c.ext, b0 = ex_first[k], b1 = ex_first[k + 1];
+        const int64_t i0 = block_at(blocks, b0, b1, c.beg >> 16);
+        MC_REQUIRE(i0 >= 0 && (c.beg & 0xffff) <= blocks[i0].isize, MC_E_IO,
+                   "%s: the index's first offset of contig %d does not match the BAM blocks", path, c.tid);
+        c.q0 = (int64_t)(blocks[i0].out + (c.beg & 0xffff));
+        const int64_t i1 = block_at(blocks, b0, b1, c.end >> 16);
+        if (i1 >= 0) {
+            MC_REQUIRE((c.end & 0xffff) <= blocks[i1].isize, MC_E_IO,
+                       "%s: the index's end offset of contig %d does not match the BAM blocks", path, c.tid);
+            c.q1 = (int64_t)(blocks[i1].out + (c.end & 0xffff));
+        } else {   // the end is the start of the block after the extent
+            MC_REQUIRE((c.end & 0xffff) == 0 && (c.end >> 16) == fx[k].f && b1 > b0, MC_E_IO,
+                       "%s: the index's end offset of contig %d does not match the BAM blocks", path, c.tid);
+            c.q1 = (int64_t)(blocks[b1 - 1].out + blocks[b1 - 1].isize);
+        }
+        MC_REQUIRE(c.q0 <= c.q1, MC_E_IO, "%s: contig %d's index offsets are reversed", path, c.tid);
+    }
+    // blocks into the virtual layout
+    for (size_t k = 0; k < fx.size(); ++k)
+        for (size_t i = ex_first[k]; i < ex_first[k + 1]; ++i) {
+            blocks[i].off = vm[k].v + (blocks[i].off - fx[k].a);
+            blocks[i].cdata = vm[k].v + (blocks[i].cdata - fx[k].a);
+        }
+    // compact ranges (neighbours merged)
+    std::vector<std::pair<int64_t, int64_t>> cpy;
+    int64_t n_comp = 0;
+    for (const Cr& c : crs) {
+        if (c.q1 == c.q0) continue;
+        if (!cpy.empty() && cpy.back().second == c.q0) cpy.back().second = c.q1;
+        else cpy.emplace_back(c.q0, c.q1);
+        n_comp += c.q1 - c.q0;
+    }
+    const int64_t max_lanes = gz_max_lanes(g->device);
+    {
+        size_t free_b = 0, tot_b = 0;
+        HIP_TRY(hipMemGetInfo(&free_b, &tot_b));
+        if (bg.t.joinable()) free_b += g->comp[0].cap;
+        MC_REQUIRE(resident_fits(vsize, total, blocks.size(), max_lanes, free_b, (size_t)n_comp), MC_E_RANGE,
+                   "%s: the selected contigs' %zu inflated bytes do not fit in device memory (decode them on the "
+                   "host: mc_bam_open_contigs)", path, total);
+    }
+    hipStream_t st = g->stream;
+    HIP_TRY(g->raw.reserve(total + 8));
+    HIP_TRY(g->inflated.reserve((size_t)n_comp + 8));
+    if (!blocks.empty()) {
+        const int rc = inflate_resident(g, mf.fd, &vm, vsize, blocks, total, max_lanes,
+                                        bg.t.joinable() ? &bg : nullptr, g->raw.p);
+        if (rc) return rc;
+        if (bg.t.joinable())
+            if (int urc = bg.join()) return urc;
+    }
+    int64_t at = 0;
+    for (const auto& c : cpy) {
+        HIP_TRY(hipMemcpyAsync(g->inflated.p + at, g->raw.p + c.first, c.second - c.first, hipMemcpyDeviceToDevice,
+                               st));
+        at += c.second - c.first;
+    }
+    std::vector<int32_t> map(n_ref, -1);
+    for (size_t i = 0; i < g->sel.size(); ++i) map[g->sel[i]] = (int32_t)i;
+    HIP_TRY(g->tid_map.reserve(std::max<size_t>(1, map.size())));
+    if (!map.empty()) HIP_TRY(hipMemcpyAsync(g->tid_map.p, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    if (int rc = init_ext(g)) return rc;
+    HIP_TRY(hipStreamSynchronize(st));   // (map is a host temporary)
+    const int64_t rec = g->hdr.n_records, m = g->hdr.n_mapped, u = g->hdr.n_unmapped;
+    if (n_comp > 0) {
+        const double t1 = now_s();
+        int64_t consumed = 0;
+        if (int rc = parse_window(g, 0, n_comp, false, &consumed)) return rc;
+        g->t_parse += (now_s() - t1) * 1e3;
+        MC_REQUIRE(consumed == n_comp, MC_E_IO, "%s: truncated record at byte %lld of the selected ranges", path,
+                   (long long)consumed);
+    }
+    g->hdr.n_records = rec;   // the whole file's counts, not the parsed ranges'
+    g->hdr.n_mapped = m;
+    g->hdr.n_unmapped = u;
+    g->t_total = (now_s() - t_start) * 1e3;
+    return MC_OK;
+}
+
+// Virtual offset (bgzf_tell) of inflated-stream offset q of a whole-file
+// decode, as the index builder's VoffWalker (bam_index.cpp) and htslib give
+// it: inside the first non-empty block that ends at or after q, or, when q
+// is that block's end, at the start of the next block (htslib moves on once
+// a block is used up; the file's end when there is none).  nz: the indices
+// of the non-empty blocks.
+uint64_t voff_of(const std::vector<Block>& b, const std::vector<size_t>& nz, size_t q, size_t file_size) {
+    auto it = std::partition_point(nz.begin(), nz.end(), [&](size_t k) { return b[k].out + b[k].isize < q; });
+    const size_t k = it != nz.end() ? *it : b.size() - 1;
+    if (q >= b[k].out && q < b[k].out + b[k].isize) return ((uint64_t)b[k].off << 16) | (uint64_t)(q - b[k].out);
+    return k + 1 < b.size() ? (uint64_t)b[k + 1].off << 16 : (uint64_t)file_size << 16;
+}
+
+int open_common(const char* path, int device, int n_threads, uint32_t flag_filter,
+                std::unique_ptr<mc_bam_gpu>& g) {
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    MC_REQUIRE(device >= 0 && device < ndev, MC_E_INVALID, "no HIP device %d", device);
+    HIP_TRY(hipSetDevice(device));
+    g.reset(new mc_bam_gpu());
+    g->path = path;
+    g->device = device;
+    g->nt = n_threads > 0 ? n_threads : std::min(16, n_threads_or_all(0));   // file reads only
+    g->flag_filter = flag_filter;
+    HIP_TRY(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&g->up_stream, hipStreamNonBlocking));
     return MC_OK;
 }
 
@@ -1227,17 +1674,8 @@ extern "C" int mc_bam_gpu_open(const char* path, int device, int n_threads, uint
                                int64_t window_bytes, mc_bam_gpu** out) {
     MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
     *out = nullptr;
-    int ndev = 0;
-    HIP_TRY(hipGetDeviceCount(&ndev));
-    MC_REQUIRE(device >= 0 && device < ndev, MC_E_INVALID, "no HIP device %d", device);
-    HIP_TRY(hipSetDevice(device));
-    std::unique_ptr<mc_bam_gpu> g(new mc_bam_gpu());
-    g->path = path;
-    g->device = device;
-    g->nt = n_threads > 0 ? n_threads : std::min(16, n_threads_or_all(0));   // file reads only
-    g->flag_filter = flag_filter;
-    HIP_TRY(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&g->up_stream, hipStreamNonBlocking));
+    std::unique_ptr<mc_bam_gpu> g;
+    if (int rc = open_common(path, device, n_threads, flag_filter, g)) return rc;
     const double t0 = now_s();
     if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
     g->t_open = (now_s() - t0) * 1e3;   // total_ms + the mapping's teardown
@@ -1289,11 +1727,109 @@ extern "C" int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t) {
     t->upload_ms = g->t_upload;
     t->kernel_ms = g->t_kernel;
     t->open_ms = g->t_open;
+    t->parse_rounds = g->parse_rounds;
+    t->resync_passes = g->resync_passes;
     return MC_OK;
 }
 
 extern "C" int mc_bam_gpu_close(mc_bam_gpu* g) {
     delete g;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_open_extents(const char* path, int device, int n_threads, uint32_t flag_filter,
+                                       int32_t n_ref, const mc_contig_extent* ext, int64_t n_no_coor, int32_t n_sel,
+                                       const int32_t* sel, mc_bam_gpu** out) {
+    MC_REQUIRE(path && out && (ext || n_ref == 0) && n_ref >= 0 && n_sel >= 0 && (sel || n_sel == 0) &&
+                   n_no_coor >= 0,
+               MC_E_INVALID, "bad argument");
+    *out = nullptr;
+    std::unique_ptr<mc_bam_gpu> g;
+    if (int rc = open_common(path, device, n_threads, flag_filter, g)) return rc;
+    const double t0 = now_s();
+    if (int rc = gpu_decode_extents(g.get(), n_ref, ext, n_no_coor, n_sel, sel)) return rc;
+    g->t_open = (now_s() - t0) * 1e3;
+    *out = g.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_open_contigs(const char* path, const char* bai_path, int device, int n_threads,
+                                       uint32_t flag_filter, int32_t n_sel, const int32_t* sel, mc_bam_gpu** out) {
+    MC_REQUIRE(path && out && n_sel >= 0 && (sel || n_sel == 0), MC_E_INVALID, "bad argument");
+    *out = nullptr;
+    int n_ref = 0;
+    {
+        MappedFile mf;
+        if (int rc = mf.open(path, false)) return rc;
+        std::vector<std::string> names;
+        std::vector<int64_t> lens;
+        if (int rc = read_header_pread(mf.fd, mf.size, path, names, lens)) return rc;
+        n_ref = (int)names.size();
+    }
+    const std::string bai = bai_path && *bai_path ? std::string(bai_path) : std::string(path) + ".bai";
+    std::vector<mc_contig_extent> ext((size_t)n_ref);
+    int64_t n_no_coor = 0;
+    if (int rc = mc_bam_index_extents(bai.c_str(), n_ref, ext.data(), &n_no_coor)) return rc;
+    return mc_bam_gpu_open_extents(path, device, n_threads, flag_filter, n_ref, ext.data(), n_no_coor, n_sel, sel,
+                                   out);
+}
+
+extern "C" int mc_bam_gpu_extents(const mc_bam_gpu* g, int32_t n_ref, mc_contig_extent* ext, int64_t* n_no_coor) {
+    MC_REQUIRE(g && (ext || n_ref == 0) && n_no_coor, MC_E_INVALID, "null argument");
+    MC_REQUIRE(n_ref == (int32_t)g->hdr.names.size(), MC_E_INVALID, "the file has %zu contigs, not %d",
+               g->hdr.names.size(), n_ref);
+    HIP_TRY(hipSetDevice(g->device));
+    std::vector<ExtAcc> acc((size_t)n_ref + 1);
+    if (g->ext.p) HIP_TRY(hipMemcpy(acc.data(), g->ext.p, acc.size() * sizeof(ExtAcc), hipMemcpyDeviceToHost));
+    if (g->subset) {
+        for (int32_t t = 0; t < n_ref; ++t) {
+            ext[t] = g->ext_in[t];
+            ext[t].n_kept = (int64_t)acc[t].kept;
+        }
+        *n_no_coor = g->n_no_coor_in;
+        return MC_OK;
+    }
+    std::vector<std::pair<uint64_t, uint64_t>> spans;   // (first, end) stream offsets of contigs with records
+    std::vector<size_t> nz;
+    for (size_t k = 0; k < g->blk_list.size(); ++k)
+        if (g->blk_list[k].isize) nz.push_back(k);
+    for (int32_t t = 0; t < n_ref; ++t) {
+        const ExtAcc& a = acc[t];
+        mc_contig_extent& e = ext[t];
+        e.n_mapped = (int64_t)a.mapped;
+        e.n_unmapped = (int64_t)a.unmapped;
+        e.n_kept = (int64_t)a.kept;
+        e.beg_voff = e.end_voff = 0;
+        if (a.nfirst == 0) continue;
+        const uint64_t q0 = ~a.nfirst, q1 = a.end;
+        spans.emplace_back(q0, q1);
+        e.beg_voff = (int64_t)voff_of(g->blk_list, nz, (size_t)q0, (size_t)g->compressed_bytes);
+        e.end_voff = (int64_t)voff_of(g->blk_list, nz, (size_t)q1, (size_t)g->compressed_bytes);
+    }
+    std::sort(spans.begin(), spans.end());
+    for (size_t i = 1; i < spans.size(); ++i)
+        MC_REQUIRE(spans[i - 1].second <= spans[i].first, MC_E_INVALID,
+                   "%s: a contig's records are not contiguous (the BAM is not coordinate-sorted)", g->path.c_str());
+    const ExtAcc& nc = acc[n_ref];
+    if (nc.nfirst && !spans.empty())
+        MC_REQUIRE(spans.back().second <= ~nc.nfirst, MC_E_INVALID,
+                   "%s: records without coordinates are not all at the end of the file", g->path.c_str());
+    *n_no_coor = (int64_t)(nc.mapped + nc.unmapped);
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_intervals_range(const mc_bam_gpu* g, int64_t first, int64_t count, int32_t* tid,
+                                          int32_t* pos, int32_t* span) {
+    MC_REQUIRE(g && tid && pos && span, MC_E_INVALID, "null argument");
+    MC_REQUIRE(first >= 0 && count >= 0 && first + count <= g->n_kept, MC_E_RANGE,
+               "intervals [%lld, %lld) outside the %lld kept", (long long)first, (long long)(first + count),
+               (long long)g->n_kept);
+    HIP_TRY(hipSetDevice(g->device));
+    if (count) {
+        HIP_TRY(hipMemcpy(tid, g->tid.p + first, count * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pos, g->pos.p + first, count * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(span, g->span.p + first, count * 4, hipMemcpyDeviceToHost));
+    }
     return MC_OK;
 }
 
@@ -1328,6 +1864,13 @@ extern "C" int mc_bgzf_scan_host(const char* path, int n_threads, int64_t* n_blo
     *inflated = (int64_t)total;
     for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)blocks.size()); ++i) offsets[i] = (int64_t)blocks[i].off;
     return MC_OK;
+}
+
+// rec_chain on the host: q of d[0, n) starts `chain` plausible records in
+// sort order (the record sync's rule; unit tests)
+extern "C" int mc_bam_rec_chain_host(const uint8_t* d, int64_t n, int64_t q, int32_t n_ref, int chain) {
+    MC_REQUIRE(d && n >= 0 && q >= 0 && chain >= 1, MC_E_INVALID, "bad argument");
+    return mc::gz::rec_chain(d, q, n, n_ref, chain) ? 1 : 0;
 }
 
 // rec_parse on the host for one record body (unit tests)

@@ -331,6 +331,26 @@ extern "C" int mc_bam_index_stats(const char* bai_path, int32_t n_ref, int64_t* 
     return MC_OK;
 }
 
+extern "C" int mc_bam_index_extents(const char* bai_path, int32_t n_ref, mc_contig_extent* ext,
+                                    int64_t* n_no_coor) {
+    MC_REQUIRE(bai_path && (ext || n_ref == 0) && n_no_coor && n_ref >= 0, MC_E_INVALID, "bad argument");
+    Bai bai;
+    if (int rc = read_bai(bai_path, bai)) return rc;
+    MC_REQUIRE((int32_t)bai.refs.size() == n_ref, MC_E_INVALID,
+               "%s indexes %zu references, the BAM header has %d", bai_path, bai.refs.size(), n_ref);
+    for (int32_t t = 0; t < n_ref; ++t) {
+        const Bai::Ref& r = bai.refs[t];
+        const bool has = (r.has_meta || r.has_bins) && r.end > r.beg;
+        ext[t].beg_voff = has ? (int64_t)r.beg : 0;
+        ext[t].end_voff = has ? (int64_t)r.end : 0;
+        ext[t].n_mapped = (int64_t)r.n_mapped;
+        ext[t].n_unmapped = (int64_t)r.n_unmapped;
+        ext[t].n_kept = 0;
+    }
+    *n_no_coor = (int64_t)bai.n_no_coor;
+    return MC_OK;
+}
+
 extern "C" int mc_bam_open_contigs(const char* path, const char* bai_path, int n_threads,
                                    uint32_t flag_filter, int keep_cigar, int32_t n_sel,
                                    const int32_t* sel, mc_bam** out) {

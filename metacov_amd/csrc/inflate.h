@@ -674,8 +674,24 @@ MC_HD uint32_t ld_u32(const uint8_t* p) {
 }
 MC_HD int32_t ld_i32(const uint8_t* p) { return (int32_t)ld_u32(p); }
 
-// a structurally valid record starts at q of d[0, n)
-MC_HD bool rec_plausible(const uint8_t* d, int64_t q, int64_t n, int32_t n_ref) {
+// hts_reg2bin(beg, end, 14, 5): the bin field of a record spanning [beg, end)
+MC_HD uint32_t reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (uint32_t)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (uint32_t)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (uint32_t)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (uint32_t)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (uint32_t)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+// A structurally valid record starts at q of d[0, n): sizes that fit, ids
+// in range, a NUL-terminated name and, for a mapped record, the bin field
+// equal to reg2bin over its bam_endpos span (SAMv1 §4.2.1; the CG:B,I
+// placeholder `<l_seq>S<rlen>N` has the real reference length).  Unmapped
+// records' bins are not checked (writers differ on them).  *key (optional):
+// the record's sort key (tid as unsigned, so tid -1 sorts last; pos + 1).
+MC_HD bool rec_plausible(const uint8_t* d, int64_t q, int64_t n, int32_t n_ref, uint64_t* key = nullptr) {
     if (q + 36 > n) return false;
     const int32_t bs = ld_i32(d + q);
     if (bs < 32 || q + 4 + (int64_t)bs > n) return false;
@@ -687,7 +703,34 @@ MC_HD bool rec_plausible(const uint8_t* d, int64_t q, int64_t n, int32_t n_ref) 
         return false;
     const uint64_t need = 32 + (uint64_t)lrn + 4ull * ncig + ((uint64_t)lseq + 1) / 2 + (uint64_t)lseq;
     if (need > (uint64_t)bs) return false;
-    return d[q + 36 + lrn - 1] == 0;
+    if (d[q + 36 + lrn - 1] != 0) return false;
+    const uint32_t flag = ld_u16(d + q + 18);
+    if (tid >= 0 && pos >= 0 && !(flag & 4u)) {
+        const uint8_t* cig = d + q + 36 + lrn;
+        int64_t rlen = 0;
+        for (uint32_t k = 0; k < ncig; ++k) {
+            const uint32_t cw = ld_u32(cig + 4ull * k);
+            if ((0x18Du >> (cw & 0xFu)) & 1u) rlen += cw >> 4;
+        }
+        if (ld_u16(d + q + 14) != reg2bin(pos, pos + (rlen > 0 ? rlen : 1))) return false;
+    }
+    if (key) *key = ((uint64_t)(uint32_t)tid << 32) | (uint32_t)(pos + 1);
+    return true;
+}
+
+// q starts a chain of `chain` plausible records in sort order, or a shorter
+// chain ending exactly at n (the host decoder's sync rule, with the bin and
+// order checks: a false start inside a record's bytes rarely chains).
+MC_HD bool rec_chain(const uint8_t* d, int64_t q, int64_t n, int32_t n_ref, int chain) {
+    uint64_t prev = 0, key = 0;
+    int64_t z = q;
+    int k = 0;
+    for (; k < chain && z < n; ++k) {
+        if (!rec_plausible(d, z, n, n_ref, &key) || key < prev) return false;
+        prev = key;
+        z += 4 + (int64_t)ld_i32(d + z);
+    }
+    return k == chain || z == n;
 }
 
 // CG:B,I in the aux data [p, end) (SAMv1 §4.2.2)

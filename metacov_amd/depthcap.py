@@ -42,14 +42,22 @@ def cap_mask(tid, pos, span, max_depth=HTSLIB_MAX_DEPTH, n_threads=0):
     return keep.view(bool), dropped.value
 
 
-def region_reads(tid, pos, span, t, start, end):
+def region_reads(tid, pos, span, t, start, end, max_span=None):
     """Indices of the records of contig t overlapping [start, end) — what
     htslib's region iterator hands the pileup (hts_itr_next tests overlap
-    with bam_endpos, at least pos + 1, in every htslib version)."""
+    with bam_endpos, at least pos + 1, in every htslib version).  The
+    records are coordinate-sorted, so only those starting in
+    [start - max_span, end) are examined (max_span: the longest span, at
+    least 1; None: computed here)."""
     lo, hi = np.searchsorted(tid, t, "left"), np.searchsorted(tid, t, "right")
-    p = pos[lo:hi].astype(np.int64)
-    e = p + np.maximum(span[lo:hi], 1)
-    return lo + np.nonzero((p < end) & (e > start))[0]
+    if max_span is None:
+        max_span = int(span[lo:hi].max()) if hi > lo else 1
+    p = pos[lo:hi]
+    a = lo + int(np.searchsorted(p, start - max(int(max_span), 1), "left"))
+    b = lo + int(np.searchsorted(p, end, "left"))
+    pp = pos[a:b].astype(np.int64)
+    e = pp + np.maximum(span[a:b], 1)
+    return a + np.nonzero(e > start)[0]
 
 
 def may_cap(rows, max_depth):
@@ -60,21 +68,32 @@ def may_cap(rows, max_depth):
 def host_intervals(src, contigs):
     """(tid, pos, span) host arrays (header contig ids) holding at least the
     records of `contigs`, from any of the library's BAM sources: a decoded
-    BamFile keeps them; a GpuBamFile copies them back from HBM; a StreamedBam
-    (intervals never kept on the host) decodes those contigs again, through
-    the BAI when there is one."""
+    BamFile keeps them; a GpuBamFile copies just those contigs' records back
+    from HBM; a StreamedBam (intervals never kept on the host) decodes those
+    contigs again, through the BAI when there is one, else in bounded
+    windows keeping only their records."""
     if hasattr(src, "tid") and getattr(src, "tid", None) is not None:
         return src.tid, src.pos, src.span
     if hasattr(src, "intervals"):
-        return src.intervals()
-    from .bam import BamFile
+        return src.intervals(contigs)
+    from .bam import BamFile, BamStream
     path = src.filename
     legacy = getattr(src, "legacy_endpos", False)
+    want = np.unique(np.asarray(contigs, np.int64))
     if os.path.exists(path + ".bai"):
-        bf = BamFile(path, contigs=np.unique(contigs), legacy_endpos=legacy)
-    else:
-        bf = BamFile(path, legacy_endpos=legacy)
-    return bf.tid, bf.pos, bf.span
+        bf = BamFile(path, contigs=want, legacy_endpos=legacy)
+        return bf.tid, bf.pos, bf.span
+    parts = []
+    with BamStream(path, legacy_endpos=legacy) as st:
+        while True:
+            k, (t, p, sp) = st.read(1 << 22)
+            if k == 0:
+                break
+            keep = np.isin(t[:k], want)
+            parts.append((t[:k][keep], p[:k][keep], sp[:k][keep]))
+    if not parts:
+        return tuple(np.zeros(0, np.int32) for _ in range(3))
+    return tuple(np.concatenate([q[i] for q in parts]) for i in range(3))
 
 
 def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0):
@@ -90,7 +109,8 @@ def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, de
     if len(tids) == 0:
         return np.zeros(0, dtype=REGION_STAT_DTYPE), 0
     tid, pos, span = host_intervals(src, tids)
-    idx = [region_reads(tid, pos, span, int(t), int(s), int(e))
+    max_span = int(span.max()) if len(span) else 1
+    idx = [region_reads(tid, pos, span, int(t), int(s), int(e), max_span)
            for t, s, e in zip(tids, starts, ends)]
     counts = np.array([len(i) for i in idx], np.int64)
     sel = np.concatenate(idx) if len(idx) else np.zeros(0, np.int64)

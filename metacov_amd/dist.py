@@ -113,3 +113,25 @@ def agree_on_error(err, group=None, device=None):
         raise err
     if failed:
         raise PeerRankError("%d rank(s) failed; see their logs" % failed)
+
+
+def broadcast_result(fn, rank, src=0, group=None, device=None):
+    """Runs fn() on rank `src` and hands its (picklable) result to every rank
+    in one broadcast.  An exception on `src` is raised there and as
+    PeerRankError on the other ranks, so no rank waits on a failed root."""
+    import torch.distributed as dist
+    obj = [None]
+    err = None
+    if rank == src:
+        try:
+            obj = [("ok", fn())]
+        except BaseException as e:   # every rank learns of it
+            err = e
+            obj = [("err", "%s: %s" % (type(e).__name__, e))]
+    dist.broadcast_object_list(obj, src=src, group=group, device=device)
+    if err is not None:
+        raise err
+    tag, val = obj[0]
+    if tag == "err":
+        raise PeerRankError("rank %d failed: %s" % (src, val))
+    return val

@@ -3,9 +3,10 @@
     classic(bam, ref, start, end) -> {min, max, med, std, avg, q23, sum}
 
 `bam` may be a path, a `metacov_amd.bam.BamFile` / `GpuBamFile`, or a `pysam.AlignmentFile`
-(its `.filename` is decoded by this library).  The depth of every contig is
-computed once per file on the GPU (K2) and each call reduces one region
-(K3); `classic_batch` reduces many regions in one launch.  Semantics match
+(its `.filename` is decoded by this library, on the GPU: `GpuBamFile`).  The
+depth of every contig is computed once per file on the GPU (K2) and each
+call reduces one region (K3); `classic_batch` reduces many regions in one
+launch.  Semantics match
 classic(): positions are 0-based half-open [start, end); positions the reads
 do not cover (or past the contig end) count as 0 (pileup.py:11-16); an empty
 region raises ValueError (pileup.py:19 on a zero-size vector); an unknown
@@ -26,16 +27,20 @@ import os
 import numpy as np
 
 from . import depthcap
-from .bam import BamFile
+from .bam import BamFile, GpuBamFile
 from .engine import classic_stats
 from .experimental import experimental, load_kmerhist  # noqa: F401  (pileup.py:29-173)
 
 HTSLIB_MAX_DEPTH = depthcap.HTSLIB_MAX_DEPTH
 _OPEN_MAX = 2                              # decoded files kept between calls
-_open_files = collections.OrderedDict()    # (path, size, mtime_ns, legacy) -> BamFile
+_open_files = collections.OrderedDict()    # (path, size, mtime_ns, legacy, device) -> GpuBamFile
 
 
-def _as_bamfile(bam, legacy_endpos=False):
+def _as_bamfile(bam, legacy_endpos=False, device=0):
+    """An open decoded file for `bam`: the library's own handles as given; a
+    path (or a pysam.AlignmentFile's .filename) is decoded on the GPU
+    (GpuBamFile: BGZF inflate and record parse in HBM, the reads handed to
+    the engine by a device copy) and kept for later calls."""
     if isinstance(bam, BamFile) or hasattr(bam, "engine"):   # BamFile, GpuBamFile, StreamedBam
         return bam
     path = getattr(bam, "filename", bam)
@@ -43,10 +48,10 @@ def _as_bamfile(bam, legacy_endpos=False):
         path = path.decode()
     path = os.fspath(path)
     st = os.stat(path)
-    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns, bool(legacy_endpos))
+    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns, bool(legacy_endpos), int(device))
     f = _open_files.pop(key, None)
     if f is None:
-        f = BamFile(path, legacy_endpos=legacy_endpos)
+        f = GpuBamFile(path, device=device, legacy_endpos=legacy_endpos)
     _open_files[key] = f                   # most recently used last
     while len(_open_files) > _OPEN_MAX:
         _open_files.popitem(last=False)[1].close()
@@ -79,7 +84,7 @@ def classic_batch(bam, regions, device=0, max_depth=HTSLIB_MAX_DEPTH, legacy_end
     query, applied where it can act (metacov_amd.depthcap); None: exact.
     legacy_endpos applies when `bam` is a path (an open file keeps the rule
     it was decoded with)."""
-    bf = _as_bamfile(bam, legacy_endpos)
+    bf = _as_bamfile(bam, legacy_endpos, device)
     regions = list(regions)
     if not regions:
         return []
@@ -104,6 +109,6 @@ def classic_batch(bam, regions, device=0, max_depth=HTSLIB_MAX_DEPTH, legacy_end
 def depth(bam, ref, start=0, end=None, device=0):
     """The exact (uncapped) per-position depth vector (int32) of [start, end)
     of `ref`."""
-    bf = _as_bamfile(bam)
+    bf = _as_bamfile(bam, device=device)
     t = _resolve(bf, ref)
     return bf.engine(device).depth(t, start, bf.lengths[t] if end is None else end)

@@ -126,3 +126,46 @@ def test_gloo_error_agreement_world2():
             p.join(timeout=60)
         want = [(0, "peer"), (1, "own")] if bad == 1 else [(0, "none"), (1, "none")]
         assert res == want
+
+
+def _bcast_worker(rank, world, port, fail, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def root_work():   # rank 0 only (the whole-file decode of cli._pileup_shard)
+            if fail:
+                raise OSError("no valid BGZF block")
+            return {"ext": np.arange(5, dtype=np.int64), "names": ("a", "b")}
+        try:
+            got = mdist.broadcast_result(root_work, rank)
+            q.put((rank, "ok", got["ext"].tolist(), got["names"]))
+        except mdist.PeerRankError:
+            q.put((rank, "peer", None, None))
+        except OSError:
+            q.put((rank, "own", None, None))
+        # still in step afterwards
+        mdist.agree_on_error(None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_broadcast_result_world2():
+    """The root's result (the extents table of a BAM without an index)
+    reaches every rank; a failure on the root raises there and as
+    PeerRankError on the other rank, and nobody blocks."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    for fail in (False, True):
+        q = ctx.Queue()
+        port = _free_port()
+        ps = [ctx.Process(target=_bcast_worker, args=(r, 2, port, fail, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        res = sorted(q.get(timeout=120) for _ in ps)
+        for p in ps:
+            p.join(timeout=60)
+        if fail:
+            assert res == [(0, "own", None, None), (1, "peer", None, None)]
+        else:
+            assert res == [(r, "ok", [0, 1, 2, 3, 4], ("a", "b")) for r in (0, 1)]

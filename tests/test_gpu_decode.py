@@ -425,3 +425,223 @@ def test_bgzf_scan_host(lib_built, golden_dir, tmp_path):
     t.write_bytes(raw[: len(raw) // 2 + 1000])
     nb, tot = ctypes.c_int64(), ctypes.c_int64()
     assert lib.mc_bgzf_scan_host(str(t).encode(), 16, ctypes.byref(nb), ctypes.byref(tot), None, 0) != 0
+
+
+# ------------------------------------------------ record sync: bins and order
+
+def _inflated(path):
+    """The BAM's inflated stream, its first record offset and n_ref."""
+    data = b"".join(zlib.decompress(p, -15) for p, _ in _bgzf_blocks(open(path, "rb").read()))
+    l_text, = struct.unpack_from("<i", data, 4)
+    o = 8 + l_text
+    n_ref, = struct.unpack_from("<i", data, o)
+    o += 4
+    for _ in range(n_ref):
+        ln, = struct.unpack_from("<i", data, o)
+        o += 8 + ln
+    return data, o, n_ref
+
+
+def _record_starts(data, o):
+    out = []
+    while o < len(data):
+        out.append(o)
+        o += 4 + struct.unpack_from("<i", data, o)[0]
+    return out
+
+
+def _chain(data, q, n_ref, chain=8):
+    return _lib().mc_bam_rec_chain_host(data, len(data), q, n_ref, chain)
+
+
+def test_rec_chain_accepts_every_record_start(lib_built, golden_dir):
+    """The GPU record sync's rule (structure, the bin field of mapped
+    records, sort order along the chain) holds at every record of the
+    samtools-written fixture and of the synthetic BAMs, whose mapped
+    records' bins were computed by their writers."""
+    for name in ("bbmap.sorted.bam", "synth_edge.bam", "synth_multi.bam", "synth_longcigar.bam"):
+        data, o, n_ref = _inflated(os.path.join(golden_dir, name))
+        starts = _record_starts(data, o)
+        assert len(starts) >= 2
+        for q in starts:
+            assert _chain(data, q, n_ref) == 1, (name, q)
+
+
+def _fake_records(k, tid, pos0, good_bins, ascending=True):
+    """k back-to-back minimal records (37 bytes each: no CIGAR, no bases, a
+    1-byte name) that pass the old structural sync test."""
+    out = b""
+    for j in range(k):
+        pos = pos0 + (j if ascending else k - j)
+        bin_ = synth._reg2bin(pos, pos + 1) if good_bins else 1234
+        out += struct.pack("<i", 33) + struct.pack("<iiBBHHHiiii", tid, pos, 1, 0, bin_, 0, 0, 0, tid,
+                                                   pos, 0) + b"\0"
+    return out
+
+
+def _near_valid_bam(path, n, good_bins, ascending, fakes=12, seed=4):
+    """Records whose aux data (an XB:B:C byte array) holds a chain of fake
+    records: a sync landing in a record's bytes meets them first."""
+    rng = np.random.default_rng(seed)
+    names, lengths = ["a", "b"], [4_000_000, 3_000_000]
+    recs = []
+    for t, L in enumerate(lengths):
+        for p in np.sort(rng.integers(0, L - 200, n // 2)):
+            r = synth.SynthRecord("r%d" % len(recs), t, int(p), 0, [(0, 100)], 100)
+            body = synth.encode_record(r)[4:]
+            payload = _fake_records(fakes, t, int(p), good_bins, ascending)
+            body += b"XBBC" + struct.pack("<i", len(payload)) + payload
+            recs.append(struct.pack("<i", len(body)) + body)
+    text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join("@SQ\tSN:%s\tLN:%d\n" % x for x in zip(names, lengths))
+    hdr = bytearray(b"BAM\x01") + struct.pack("<i", len(text)) + text.encode() + struct.pack("<i", 2)
+    for nm, L in zip(names, lengths):
+        hdr += struct.pack("<i", len(nm) + 1) + nm.encode() + b"\0" + struct.pack("<i", L)
+    with open(path, "wb") as fh:
+        fh.write(synth._bgzf(bytes(hdr) + b"".join(recs)))
+
+
+def test_rec_chain_rejects_near_valid_fakes(lib_built, tmp_path):
+    """Fake record chains inside aux bytes: wrong bins, or right bins in
+    descending order, never start a sync chain; the real records do.  (The
+    last of the descending fakes does chain into the real records after it:
+    a walk from it lands on the next real record, and the previous
+    segment's walk corrects it.)"""
+    for good_bins, ascending in ((False, True), (True, False)):
+        p = str(tmp_path / "nv.bam")
+        _near_valid_bam(p, 200, good_bins, ascending)
+        data, o, n_ref = _inflated(p)
+        starts = _record_starts(data, o)
+        for q in starts:
+            assert _chain(data, q, n_ref) == 1
+            fake0 = q + 4 + struct.unpack_from("<i", data, q)[0] - 12 * 37
+            for f in range(fake0, fake0 + (12 if not good_bins else 11) * 37, 37):
+                assert _chain(data, f, n_ref) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("good_bins,ascending", [(False, True), (True, False), (True, True)])
+def test_gpu_decode_near_valid_records(lib_built, tmp_path, good_bins, ascending):
+    """40k records of ~500 B, most of each a chain of fake records: the
+    decode equals the oracle's reader.  Fakes the bin check rejects cost no
+    resync at all; fakes that pass the checks (right bins: the last of a
+    descending run, or a whole ascending run) are corrected from the
+    verified prefix, re-synced with long chains if they persist, in a few
+    rounds, never by one lane walking the rest."""
+    p = str(tmp_path / "nv.bam")
+    _near_valid_bam(p, 40_000, good_bins, ascending, fakes=12)
+    from metacov_amd.bam import GpuBamFile
+    with GpuBamFile(p) as g:
+        _assert_oracle(p, g)
+        t = g.timings()
+    if not good_bins:
+        assert t["resyncs"] == 0 and t["parse_rounds"] == 1, t
+    else:
+        assert t["parse_rounds"] <= 6, t
+
+
+# ------------------------------------------------ contig shards (SURVEY §8e)
+
+def _multi_contig_bam(tmp_path, n_reads=300_000, seed=21):
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(20_000, 400_000, 40).astype(np.int64)
+    lengths[[3, 17]] = [1, 64]                      # tiny contigs (few or no reads)
+    arrs = synth.edge_mix_arrays(lengths, n_reads, seed=seed)
+    p = str(tmp_path / "mc.bam")
+    synth.write_bam_fast(p, ["c%d" % i for i in range(len(lengths))], lengths, *arrs, level=1, n_threads=8)
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [0, 1 << 20])
+def test_gpu_extents_equal_the_index(lib_built, tmp_path, golden_dir, window):
+    """A whole-file GPU decode's extents table (computed in the record walk)
+    is the BAI's pseudo-bin data: the same first / end virtual offsets and
+    mapped / unmapped counts as mc_bam_index_build writes, resident and
+    windowed; its kept counts are the decoded records per contig."""
+    from metacov_amd.bam import BamFile, GpuBamFile, build_index, index_extents
+    import shutil
+    paths = [_multi_contig_bam(tmp_path)]
+    for name in ("bbmap.sorted.bam", "synth_multi.bam", "synth_edge.bam"):
+        q = str(tmp_path / name)
+        shutil.copy(os.path.join(golden_dir, name), q)
+        paths.append(q)
+    for p in paths:
+        build_index(p)
+        with GpuBamFile(p, window_bytes=window) as g:
+            ext, nc = g.extents()
+            want, wnc = index_extents(p + ".bai", len(g.references))
+            for f in ("beg_voff", "end_voff", "n_mapped", "n_unmapped"):
+                assert np.array_equal(ext[f], want[f]), (p, f)
+            assert nc == wnc
+            h = BamFile(p)
+            assert np.array_equal(ext["n_kept"], np.bincount(h.tid, minlength=len(h.lengths)))
+
+
+@pytest.mark.gpu
+def test_gpu_decode_contig_shards(lib_built, tmp_path, golden_dir):
+    """One rank's contigs decoded on the GPU, only their BGZF blocks read:
+    through the BAI and through the extents of a whole-file decode, equal to
+    the host's indexed decode (BamFile(contigs=...)) and to the oracle's
+    reader restricted to those contigs, for first / last / scattered /
+    neighbouring / empty / tiny selections; the engine holds just those
+    contigs and reproduces the oracle's rows."""
+    from metacov_amd.bam import BamFile, GpuBamFile, build_index
+    from oracle import bamread, coracle
+    import shutil
+    p = _multi_contig_bam(tmp_path)
+    q = str(tmp_path / "sm.bam")
+    shutil.copy(os.path.join(golden_dir, "synth_multi.bam"), q)
+    for path in (p, q):
+        build_index(path)
+        names, lens, counts, otid, opos, ospan = bamread.scan_intervals(path)
+        n = len(names)
+        with GpuBamFile(path) as whole:
+            ext = whole.extents()
+            sels = [[0], [n - 1], [0, n - 1], list(range(0, n, 3)), [1, 2], list(range(n)), [],
+                    [3] if n > 3 else [0], [17 % n, 18 % n]]
+            for sel in sels:
+                h = BamFile(path, contigs=sel)
+                keep = np.isin(otid, sel)
+                for g in (GpuBamFile(path, contigs=sel), GpuBamFile(path, contigs=sel, extents=ext)):
+                    with g:
+                        t, ps, sp = g.intervals()
+                        assert np.array_equal(t, otid[keep]) and np.array_equal(ps, opos[keep])
+                        assert np.array_equal(sp, ospan[keep])
+                        assert np.array_equal(t, h.tid) and np.array_equal(ps, h.pos)
+                        assert (g.n_records, g.mapped, g.unmapped) == (h.n_records, h.mapped, h.unmapped)
+                        assert g.references == h.references and g.lengths == h.lengths
+                        if not len(sel):
+                            continue
+                        # the shard's engine against the oracle's exact rows
+                        su = np.unique(sel)
+                        rt = su.astype(np.int32)
+                        rs = np.zeros(len(su), np.int64)
+                        re_ = np.asarray(lens, np.int64)[su] + 5
+                        d, e, c = coracle.depth(lens, otid, opos, ospan)
+                        want = coracle.region_stats(d, e, c, rt, rs, re_)
+                        got = g.engine(0, compute=False).compute_depth_stats(g.local_tid(rt), rs, re_)
+                        for f in want.dtype.names:
+                            assert np.array_equal(got[f], want[f]), f
+            # bounded copies of chosen contigs from the whole-file decode
+            sel = [1, n - 1]
+            t, ps, sp = whole.intervals(sel)
+            keep = np.isin(otid, sel)
+            assert np.array_equal(t, otid[keep]) and np.array_equal(ps, opos[keep])
+
+
+@pytest.mark.gpu
+def test_classic_path_decodes_on_the_gpu(lib_built, golden_dir, fixture_golden):
+    """pileup.classic(path) — INTEGRATION.md's drop-in — opens the BAM with
+    the GPU decoder and returns the real classic()'s goldens."""
+    from metacov_amd import pileup
+    from metacov_amd.bam import GpuBamFile
+    path = os.path.join(golden_dir, "bbmap.sorted.bam")
+    pileup.close_all()
+    try:
+        got = pileup.classic(path, "ref1", 1, 425)
+        assert all(isinstance(f, GpuBamFile) for f in pileup._open_files.values())
+        assert len(pileup._open_files) == 1
+    finally:
+        pileup.close_all()
+    assert got == {"min": 7, "max": 526, "med": 344, "std": 134.03, "avg": 342.53, "q23": 353.25,
+                   "sum": 145231}

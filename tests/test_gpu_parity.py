@@ -534,12 +534,14 @@ def test_external_stream(lib_built):
     eng.close()
 
 
-@pytest.mark.parametrize("indexed", [True, False])
-def test_cli_two_ranks(lib_built, golden_dir, tmp_path, indexed):
+@pytest.mark.parametrize("decode,indexed", [("gpu", True), ("gpu", False), ("host", True)])
+def test_cli_two_ranks(lib_built, golden_dir, tmp_path, decode, indexed):
     """`metacov pileup` on 2 ranks (torch.distributed.run, contig shards,
     region-table all-gather; gloo so both ranks can share the box's one GPU)
-    writes byte-for-byte the CSV of one process — with the index (each rank
-    decodes only its contigs) and without (decode all, keep the shard)."""
+    writes byte-for-byte the CSV built from the oracle alone (bamread +
+    coracle) and the CSV of one process.  --decode gpu: each rank decodes
+    only its contigs' BGZF blocks on the GPU, located by the BAI, or without
+    one by the extents table of rank 0's whole-file GPU decode."""
     import shutil
     import socket
     import subprocess
@@ -547,16 +549,21 @@ def test_cli_two_ranks(lib_built, golden_dir, tmp_path, indexed):
     from click.testing import CliRunner
     from metacov_amd.bam import build_index
     from metacov_amd.cli import pileup as cli_pileup
+    from tests.oracle_csv import oracle_csv
     bam = str(tmp_path / "m.bam")
     shutil.copy(os.path.join(golden_dir, "synth_multi.bam"), bam)
     if indexed:
         build_index(bam)
+    regs = [("contig_5", "100", "39000"), ("contig_0", "0", "5000"), ("contig_6", "7000", "10"),
+            ("contig_2", "5", "6"), ("contig_3", "0", "1"), ("contig_5", "0", "40000"),
+            ("contig_1", "0", "300"), ("contig_4", "3", "2000"), ("contig_4", "0", "20000")]
     rc = tmp_path / "r.csv"
-    rc.write_text("sequence_id,start,stop\ncontig_5,100,39000\ncontig_0,0,5000\ncontig_6,7000,10\n"
-                  "contig_2,5,6\ncontig_3,0,1\ncontig_5,0,40000\ncontig_1,0,300\n")
+    rc.write_text("sequence_id,start,stop\n" + "".join("%s,%s,%s\n" % r for r in regs))
+    want = oracle_csv(bam, regs)
     one = tmp_path / "one.csv"
-    res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rc", str(rc), "-o", str(one)])
+    res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rc", str(rc), "-o", str(one), "--decode", decode])
     assert res.exit_code == 0, res.output
+    assert open(one, newline="").read() == want
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -566,10 +573,10 @@ def test_cli_two_ranks(lib_built, golden_dir, tmp_path, indexed):
                PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", "--master-port=%d" % port, "-m", "metacov_amd.cli", "pileup",
-           "-b", bam, "-rc", str(rc), "-o", str(two)]
+           "-b", bam, "-rc", str(rc), "-o", str(two), "--decode", decode]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
-    assert open(two, newline="").read() == open(one, newline="").read()
+    assert open(two, newline="").read() == want
 
 
 def test_cigar_device_batches(lib_built):
