@@ -397,6 +397,13 @@ int mc_bam_gpu_open_extents(const char* path, int device, int n_threads, uint32_
  * contigs. */
 int mc_bam_gpu_extents(const mc_bam_gpu* g, int32_t n_ref, mc_contig_extent* ext,
                        int64_t* n_no_coor);
+/* A whole-file handle turned into a contig-subset one in place: only the
+ * kept intervals of the selected contigs remain, in file order, with local
+ * tids (as mc_bam_gpu_open_contigs gives them); the header counts stay the
+ * whole file's.  (Rank 0 of a multi-GPU run without an index decodes the
+ * whole file for the extents table and keeps its own shard this way.)
+ * MC_E_INVALID if the file is not coordinate-sorted. */
+int mc_bam_gpu_restrict(mc_bam_gpu* g, int32_t n_sel, const int32_t* sel);
 /* Kept intervals [first, first + count) of the handle, copied to the host
  * (the records of chosen contigs: offsets from the extents' n_kept). */
 int mc_bam_gpu_intervals_range(const mc_bam_gpu* g, int64_t first, int64_t count, int32_t* tid,

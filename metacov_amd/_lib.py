@@ -145,6 +145,7 @@ SIGNATURES = {
     "mc_bam_gpu_open_extents": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _U32, _I32, _P, _I64, _I32, _P,
                                 _PP],
     "mc_bam_gpu_extents": [_P, _I32, _P, _PI64],
+    "mc_bam_gpu_restrict": [_P, _I32, _P],
     "mc_bam_gpu_intervals_range": [_P, _I64, _I64, _P, _P, _P],
     "mc_gz_inflate_host": [_P, _I64, _P, _I64],
     "mc_bam_rec_parse_host": [_P, _I64, _I32, _U32, _P],

@@ -351,6 +351,26 @@ class GpuBamFile:
             self._ext = (ext, nc.value)
         return self._ext
 
+    def restrict(self, contigs):
+        """Keeps only `contigs`' records (a rank's shard of this whole-file
+        decode), in place on the device; returns self, now a contig-subset
+        file (local_tid, engine over those contigs)."""
+        if self.contigs is not None:
+            raise ValueError("already a contig subset")
+        sel = np.unique(np.asarray(contigs, dtype=np.int32))
+        self.extents()                  # the whole file's table, before the subset
+        if self._eng is not None:
+            self._eng.close()
+            self._eng = None
+        check(self._lib.mc_bam_gpu_restrict(self._h, len(sel), _lib.ptr(sel)))
+        self.contigs = sel
+        self._ext = None
+        n = ctypes.c_int64()
+        check(self._lib.mc_bam_gpu_intervals_device(self._h, ctypes.byref(n),
+                                                    *[ctypes.byref(p) for p in self._dptr]))
+        self.n_kept = n.value
+        return self
+
     def _range(self, first, count):
         out = tuple(np.empty(count, np.int32) for _ in range(3))
         if count:

@@ -26,9 +26,11 @@ all-gather of the region table (RCCL; MC_DIST_BACKEND=gloo for a CPU
 rehearsal) brings the rows to rank 0, which writes the same CSV.
 """
 import csv
+import json
 import logging
 import os
 import sys
+import time
 
 import click
 import numpy as np
@@ -238,18 +240,22 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         torch.cuda.set_device(device)
     dist.init_process_group(backend)
     coll_dev = torch.device("cuda", device) if backend == "nccl" else None
+    times = {}
+    t_start = time.perf_counter()
     try:
         err = region_err = None
         try:
             table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
-                                       max_depth, legacy_endpos, decode, coll_dev)
+                                       max_depth, legacy_endpos, decode, coll_dev, times)
             head, regions, tids, starts, ends, rows, mine, r_max, region_err = table_args
             mine_extra = experimental_results(path, exp, head.references, tids[mine], starts[mine],
                                               ends[mine], device)
         except BaseException as e:   # every rank learns of it before the table gather
             err = e
         mdist.agree_on_error(err, device=coll_dev)
+        t0 = time.perf_counter()
         table = mdist.all_gather_table(mdist.pack_rows(rows, mine), r_max, device=coll_dev)
+        times["gather_s"] = time.perf_counter() - t0
         extra = None
         if exp is not None:          # each rank's experimental results (our own objects) to rank 0
             parts = [None] * world if rank == 0 else None
@@ -263,6 +269,8 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
             log_counts(head)
             write_csv(regions, mdist.unpack_rows(table, len(regions), REGION_STAT_DTYPE), outfile,
                       extra)
+        times["total_s"] = time.perf_counter() - t_start
+        log.info("rank %d/%d phases: %s", rank, world, json.dumps(times))
     finally:
         dist.destroy_process_group()
     if region_err is not None:       # every rank resolved the same regions
@@ -280,7 +288,7 @@ class _Header:
 
 def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
                   max_depth=_depthcap.HTSLIB_MAX_DEPTH, legacy_endpos=False, decode="gpu",
-                  coll_dev=None):
+                  coll_dev=None, times=None):
     """This rank's part of a distributed pileup: header and regions (every
     rank; those before the first failing one, and its error), LPT contig
     shards, and the rows of the regions on its contigs.
@@ -292,6 +300,9 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
     other ranks then decode their contigs from it.  --decode host: the C++
     host decoder (whole file without an index)."""
     from . import dist as mdist
+    full = None          # rank 0 without an index: the whole-file GPU decode
+    times = {} if times is None else times
+    t0 = time.perf_counter()
     index = path + ".bai"
     have_index = os.path.exists(index)
     ext = None
@@ -300,15 +311,22 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
         reads_per, _, _ = index_stats(index, len(head.lengths))
     elif decode == "gpu":
         def whole_file():
-            with GpuBamFile(path, device=device, legacy_endpos=legacy_endpos) as full:
-                return (full.references, full.lengths, (full.n_records, full.mapped, full.unmapped),
-                        full.extents())
-        refs, lens, counts, ext = mdist.broadcast_result(whole_file, rank, device=coll_dev)
+            nonlocal full
+            full = GpuBamFile(path, device=device, legacy_endpos=legacy_endpos)
+            return (full.references, full.lengths, (full.n_records, full.mapped, full.unmapped),
+                    full.extents())
+        try:
+            refs, lens, counts, ext = mdist.broadcast_result(whole_file, rank, device=coll_dev)
+        except BaseException:
+            if full is not None:
+                full.close()
+            raise
         head = _Header(refs, lens, counts)
         reads_per = ext[0]["n_mapped"]
     else:
         head = BamFile(path, legacy_endpos=legacy_endpos)
         reads_per = np.bincount(head.tid, minlength=len(head.lengths))
+    times["head_s"] = time.perf_counter() - t0
     regions, tids, starts, ends, region_err = resolve_regions(
         head, _regions.make_region_iterator(regionfile_blast7, regionfile_csv, head))
     shards = mdist.lpt_shard(mdist.contig_costs(head.lengths, reads_per), world)
@@ -320,18 +338,29 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
     r_max = max(1, int(np.bincount(region_rank, minlength=world).max()) if len(tids) else 1)
     rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
     if len(mine):
-        if decode == "gpu":
+        t0 = time.perf_counter()
+        if full is not None:      # rank 0 keeps its shard of the whole file
+            bam, full = full.restrict(shards[rank]), None
+            times["decode_timings"] = {}
+        elif decode == "gpu":
             bam = GpuBamFile(path, device=device, contigs=shards[rank], extents=ext,
                              legacy_endpos=legacy_endpos)
+            times["decode_timings"] = {k: round(v, 3) if isinstance(v, float) else v
+                                       for k, v in bam.timings().items()}
         elif have_index:
             bam = BamFile(path, contigs=shards[rank], legacy_endpos=legacy_endpos)
         else:
             bam = head.restrict(shards[rank])
+        times["decode_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
         try:
             rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
         finally:
             if decode == "gpu":
                 bam.close()
+        times["rows_s"] = time.perf_counter() - t0
+    if full is not None:
+        full.close()
     return head, regions, tids, starts, ends, rows, mine, r_max, region_err
 
 

@@ -1784,7 +1784,7 @@ extern "C" int mc_bam_gpu_extents(const mc_bam_gpu* g, int32_t n_ref, mc_contig_
     if (g->subset) {
         for (int32_t t = 0; t < n_ref; ++t) {
             ext[t] = g->ext_in[t];
-            ext[t].n_kept = (int64_t)acc[t].kept;
+            ext[t].n_kept = std::binary_search(g->sel.begin(), g->sel.end(), t) ? (int64_t)acc[t].kept : 0;
         }
         *n_no_coor = g->n_no_coor_in;
         return MC_OK;
@@ -1815,6 +1815,67 @@ extern "C" int mc_bam_gpu_extents(const mc_bam_gpu* g, int32_t n_ref, mc_contig_
         MC_REQUIRE(spans.back().second <= ~nc.nfirst, MC_E_INVALID,
                    "%s: records without coordinates are not all at the end of the file", g->path.c_str());
     *n_no_coor = (int64_t)(nc.mapped + nc.unmapped);
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_restrict(mc_bam_gpu* g, int32_t n_sel, const int32_t* sel) {
+    MC_REQUIRE(g && n_sel >= 0 && (sel || n_sel == 0), MC_E_INVALID, "bad argument");
+    MC_REQUIRE(!g->subset, MC_E_STATE, "the handle already holds a contig subset");
+    const int32_t n_ref = (int32_t)g->hdr.names.size();
+    std::vector<mc_contig_extent> ext((size_t)n_ref);
+    int64_t n_no_coor = 0;
+    if (int rc = mc_bam_gpu_extents(g, n_ref, ext.data(), &n_no_coor)) return rc;   // (checks contiguity)
+    std::vector<int32_t> keep(sel, sel + n_sel);
+    std::sort(keep.begin(), keep.end());
+    keep.erase(std::unique(keep.begin(), keep.end()), keep.end());
+    for (int32_t t : keep) MC_REQUIRE(t >= 0 && t < n_ref, MC_E_INVALID, "contig %d out of range", t);
+    // each contig's slice of the kept intervals (file order = order of first offsets)
+    std::vector<int32_t> order;
+    for (int32_t t = 0; t < n_ref; ++t)
+        if (ext[t].n_kept) order.push_back(t);
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return ext[a].beg_voff < ext[b].beg_voff; });
+    std::vector<int64_t> first((size_t)n_ref, 0);
+    int64_t at = 0;
+    for (int32_t t : order) {
+        first[t] = at;
+        at += ext[t].n_kept;
+    }
+    MC_REQUIRE(at == g->n_kept, MC_E_STATE, "kept counts per contig (%lld) differ from the kept records (%lld)",
+               (long long)at, (long long)g->n_kept);
+    std::vector<int32_t> picked;   // selected contigs with records, in file order
+    for (int32_t t : order)
+        if (std::binary_search(keep.begin(), keep.end(), t)) picked.push_back(t);
+    int64_t n = 0;
+    for (int32_t t : picked) n += ext[t].n_kept;
+    HIP_TRY(hipSetDevice(g->device));
+    hipStream_t st = g->stream;
+    DBuf<int32_t> tid, pos, span;
+    HIP_TRY(tid.reserve((size_t)n + 4));
+    HIP_TRY(pos.reserve((size_t)n + 4));
+    HIP_TRY(span.reserve((size_t)n + 4));
+    int64_t w = 0;
+    for (int32_t t : picked) {
+        const int64_t k = ext[t].n_kept, f = first[t];
+        const int32_t local = (int32_t)(std::lower_bound(keep.begin(), keep.end(), t) - keep.begin());
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(tid.p + w), local, (size_t)k, st));
+        HIP_TRY(hipMemcpyAsync(pos.p + w, g->pos.p + f, k * 4, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(span.p + w, g->span.p + f, k * 4, hipMemcpyDeviceToDevice, st));
+        w += k;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    std::swap(g->tid.p, tid.p);
+    std::swap(g->tid.cap, tid.cap);
+    std::swap(g->pos.p, pos.p);
+    std::swap(g->pos.cap, pos.cap);
+    std::swap(g->span.p, span.p);
+    std::swap(g->span.cap, span.cap);
+    g->n_kept = n;
+    // the per-contig table keeps the whole file's extents; kept counts only for the subset
+    g->subset = true;
+    g->sel = keep;
+    g->ext_in = ext;
+    for (mc_contig_extent& e : g->ext_in) e.n_kept = 0;
+    g->n_no_coor_in = n_no_coor;
     return MC_OK;
 }
 

@@ -627,6 +627,26 @@ def test_gpu_decode_contig_shards(lib_built, tmp_path, golden_dir):
             t, ps, sp = whole.intervals(sel)
             keep = np.isin(otid, sel)
             assert np.array_equal(t, otid[keep]) and np.array_equal(ps, opos[keep])
+        # a whole-file decode restricted in place (rank 0 without an index)
+        for sel in ([n - 1, 0], list(range(1, n, 2)), []):
+            with GpuBamFile(path) as g:
+                ext_before = g.extents()
+                g.restrict(sel)
+                keep = np.isin(otid, sel)
+                t, ps, sp = g.intervals()
+                assert np.array_equal(t, otid[keep]) and np.array_equal(ps, opos[keep])
+                assert np.array_equal(sp, ospan[keep])
+                ext_after, _ = g.extents()
+                assert np.array_equal(ext_after["beg_voff"], ext_before[0]["beg_voff"])
+                assert int(ext_after["n_kept"].sum()) == int(keep.sum()) == g.n_kept
+                if len(sel):
+                    su = np.unique(sel).astype(np.int32)
+                    d, e, c = coracle.depth(lens, otid, opos, ospan)
+                    rs = np.zeros(len(su), np.int64)
+                    re_ = np.asarray(lens, np.int64)[su]
+                    want = coracle.region_stats(d, e, c, su, rs, re_)
+                    got = g.engine(0, compute=False).compute_depth_stats(g.local_tid(su), rs, re_)
+                    assert all(np.array_equal(got[f], want[f]) for f in want.dtype.names)
 
 
 @pytest.mark.gpu
