@@ -704,14 +704,25 @@ MC_HD bool rec_plausible(const uint8_t* d, int64_t q, int64_t n, int32_t n_ref, 
     const uint64_t need = 32 + (uint64_t)lrn + 4ull * ncig + ((uint64_t)lseq + 1) / 2 + (uint64_t)lseq;
     if (need > (uint64_t)bs) return false;
     if (d[q + 36 + lrn - 1] != 0) return false;
+    // QNAME: 1-254 printable characters (SAMv1 §1.4: "*" when absent; some
+    // aligners, BBMap among them, write spaces too)
+    if (lrn < 2) return false;
+    for (uint32_t k = 0; k + 1 < lrn; ++k)
+        if ((uint32_t)(d[q + 36 + k] - 0x20) > 0x7e - 0x20) return false;
     const uint32_t flag = ld_u16(d + q + 18);
+    if (flag >> 12) return false;   // no flag bits beyond 0x800 are defined
     if (tid >= 0 && pos >= 0 && !(flag & 4u)) {
+        // ops 0-8 only; the query length of the CIGAR is l_seq (or no
+        // sequence stored); the bin field is reg2bin of the span
         const uint8_t* cig = d + q + 36 + lrn;
-        int64_t rlen = 0;
+        int64_t rlen = 0, qlen = 0;
         for (uint32_t k = 0; k < ncig; ++k) {
-            const uint32_t cw = ld_u32(cig + 4ull * k);
-            if ((0x18Du >> (cw & 0xFu)) & 1u) rlen += cw >> 4;
+            const uint32_t cw = ld_u32(cig + 4ull * k), op = cw & 0xFu;
+            if (op > 8) return false;
+            if ((0x18Du >> op) & 1u) rlen += cw >> 4;
+            if ((0x193u >> op) & 1u) qlen += cw >> 4;
         }
+        if (ncig && lseq && qlen != lseq) return false;
         if (ld_u16(d + q + 14) != reg2bin(pos, pos + (rlen > 0 ? rlen : 1))) return false;
     }
     if (key) *key = ((uint64_t)(uint32_t)tid << 32) | (uint32_t)(pos + 1);

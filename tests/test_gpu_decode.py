@@ -467,15 +467,18 @@ def test_rec_chain_accepts_every_record_start(lib_built, golden_dir):
             assert _chain(data, q, n_ref) == 1, (name, q)
 
 
+FAKE = 38   # bytes per fake record
+
+
 def _fake_records(k, tid, pos0, good_bins, ascending=True):
-    """k back-to-back minimal records (37 bytes each: no CIGAR, no bases, a
-    1-byte name) that pass the old structural sync test."""
+    """k back-to-back minimal records (38 bytes each: no CIGAR, no bases, a
+    1-character name) that pass the old structural sync test."""
     out = b""
     for j in range(k):
         pos = pos0 + (j if ascending else k - j)
         bin_ = synth._reg2bin(pos, pos + 1) if good_bins else 1234
-        out += struct.pack("<i", 33) + struct.pack("<iiBBHHHiiii", tid, pos, 1, 0, bin_, 0, 0, 0, tid,
-                                                   pos, 0) + b"\0"
+        out += struct.pack("<i", 34) + struct.pack("<iiBBHHHiiii", tid, pos, 2, 0, bin_, 0, 0, 0, tid,
+                                                   pos, 0) + b"f\0"
     return out
 
 
@@ -513,8 +516,8 @@ def test_rec_chain_rejects_near_valid_fakes(lib_built, tmp_path):
         starts = _record_starts(data, o)
         for q in starts:
             assert _chain(data, q, n_ref) == 1
-            fake0 = q + 4 + struct.unpack_from("<i", data, q)[0] - 12 * 37
-            for f in range(fake0, fake0 + (12 if not good_bins else 11) * 37, 37):
+            fake0 = q + 4 + struct.unpack_from("<i", data, q)[0] - 12 * FAKE
+            for f in range(fake0, fake0 + (12 if not good_bins else 11) * FAKE, FAKE):
                 assert _chain(data, f, n_ref) == 0
 
 
