@@ -94,6 +94,8 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     Compute fold coverage values
     """
     fasta = reference_fasta.name if reference_fasta else None
+    if fasta:            # cli.py:59: pysam.FastaFile(...) for every run with -f
+        _experimental.check_faidx(fasta)
     # cli.py:81: the histogram is read with load_kmerhist's default k_len (7)
     k_cor = _experimental.load_kmerhist(kmer_histogram) if kmer_histogram else None
     exp = (k_cor, kmer_length, fasta) if k_cor is not None else None

@@ -73,6 +73,47 @@ def load_kmerhist(f, k_len=7):
 
 # ------------------------------------------------------------------ inputs
 
+def check_faidx(path):
+    """Raises OSError where pysam.FastaFile(path) fails to open a reference
+    (metacov/cli.py:59 opens one for every `pileup -f`): htslib's faidx needs
+    plain text or BGZF (not plain gzip: "Cannot index files compressed with
+    gzip, please use bgzip"), '>' headers, and within a sequence every line
+    but the last of one length ("Different line length in sequence")."""
+    def fail(why):
+        raise OSError("error when opening file `%s`: %s" % (path, why))
+    with open(path, "rb") as fh:
+        head = fh.read(18)
+    if head[:2] == b"\x1f\x8b":
+        bgzf = len(head) >= 16 and head[3] & 4 and head[12:14] == b"BC"
+        if not bgzf:
+            fail("Cannot index files compressed with gzip, please use bgzip")
+        with gzip.open(path, "rb") as fh:
+            data = fh.read()
+    else:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    name, width, short = None, None, False
+    for no, line in enumerate(data.split(b"\n"), 1):
+        line = line.rstrip(b"\r")
+        if line.startswith(b">"):
+            name, width, short = line[1:].split()[0].decode() if line[1:].split() else "", None, False
+            continue
+        if not line:
+            if name is not None:
+                short = short or width is not None
+            continue
+        if name is None:
+            fail("Format error, unexpected \"%s\" at line %d" % (chr(line[0]), no))
+        if short:
+            fail("Different line length in sequence '%s'" % name)
+        if width is None:
+            width = len(line)
+        elif len(line) > width:
+            fail("Different line length in sequence '%s'" % name)
+        elif len(line) < width:
+            short = True
+
+
 class FastaFile:
     """pysam.FastaFile.fetch over a plain or gzip FASTA, held as one byte
     buffer (the sequence the GPU reads).  Names are the first word of each

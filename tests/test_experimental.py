@@ -313,7 +313,12 @@ def test_cli_kmer_histogram_gpu(golden_dir, fixture_golden, lib_built, tmp_path)
     rows.append("NNNNNNN,1,1,1,R1,Mapped")
     hist = tmp_path / "k.csv"
     hist.write_text("\n".join(rows) + "\n")
-    fasta = os.path.join(golden_dir, "reference_1K.fa.gz")
+    # pysam.FastaFile needs plain text or bgzip (cli.py:59): the plain-gzip
+    # fixture goes in decompressed
+    import gzip as _gz
+    fasta = str(tmp_path / "reference_1K.fa")
+    with _gz.open(os.path.join(golden_dir, "reference_1K.fa.gz"), "rb") as fh:
+        open(fasta, "wb").write(fh.read())
     bam = os.path.join(golden_dir, "bbmap.sorted.bam")
     out = tmp_path / "o.csv"
     res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"),
@@ -379,3 +384,43 @@ def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path):
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     assert open(two, newline="").read() == open(one, newline="").read()
+
+
+def test_check_faidx_follows_pysam_open(tmp_path):
+    """`pileup -f` opens the reference like pysam.FastaFile (cli.py:59):
+    plain and BGZF FASTA with equal-length lines open; plain gzip, ragged
+    lines inside a sequence and text before the first header fail."""
+    import gzip as _gz
+    import subprocess
+    ok = tmp_path / "ok.fa"
+    ok.write_text(">a desc\nACGTACGT\nACGTACGT\nACG\n>b\nAC\n")
+    mx.check_faidx(str(ok))
+    crlf = tmp_path / "crlf.fa"
+    crlf.write_bytes(b">a\r\nACGT\r\nAC\r\n")
+    mx.check_faidx(str(crlf))
+    gz = tmp_path / "plain.fa.gz"
+    gz.write_bytes(_gz.compress(ok.read_bytes()))
+    with pytest.raises(OSError, match="bgzip"):
+        mx.check_faidx(str(gz))
+    from metacov_amd import synth
+    bg = tmp_path / "bg.fa.gz"
+    bg.write_bytes(synth._bgzf(ok.read_bytes()))
+    mx.check_faidx(str(bg))
+    for bad in (">a\nACGT\nAC\nACGT\n", ">a\nACG\nACGTA\n", "ACGT\n>a\nAC\n", ">a\nACGT\n\nACGT\n"):
+        f = tmp_path / "bad.fa"
+        f.write_text(bad)
+        with pytest.raises(OSError):
+            mx.check_faidx(str(f))
+
+
+def test_cli_rejects_unopenable_fasta_without_k(lib_built, golden_dir, tmp_path):
+    """Without -k the reference still opens -f (cli.py:59): a plain-gzip
+    FASTA fails before any row is written."""
+    from click.testing import CliRunner
+    from metacov_amd.cli import pileup as cli_pileup
+    out = tmp_path / "o.csv"
+    res = CliRunner().invoke(cli_pileup, ["-b", os.path.join(golden_dir, "bbmap.sorted.bam"),
+                                          "-f", os.path.join(golden_dir, "reference_1K.fa.gz"),
+                                          "-o", str(out)])
+    assert res.exit_code != 0 and isinstance(res.exception, OSError)
+    assert not out.exists() or out.read_text() == ""
