@@ -313,12 +313,16 @@ def test_cli_kmer_histogram_gpu(golden_dir, fixture_golden, lib_built, tmp_path)
     rows.append("NNNNNNN,1,1,1,R1,Mapped")
     hist = tmp_path / "k.csv"
     hist.write_text("\n".join(rows) + "\n")
-    # pysam.FastaFile needs plain text or bgzip (cli.py:59): the plain-gzip
-    # fixture goes in decompressed
-    import gzip as _gz
+    # pysam.FastaFile (cli.py:59) needs plain text or bgzip and faidx's line
+    # rule; the fixture is plain gzip and its ref2 starts with a 65-base line:
+    # the same sequences go in re-wrapped at 70 bases
     fasta = str(tmp_path / "reference_1K.fa")
-    with _gz.open(os.path.join(golden_dir, "reference_1K.fa.gz"), "rb") as fh:
-        open(fasta, "wb").write(fh.read())
+    src = mx.FastaFile(os.path.join(golden_dir, "reference_1K.fa.gz"))
+    with open(fasta, "w") as fh:
+        for name, L in zip(src.references, src.lengths):
+            seq = src.fetch(name, 0, L)
+            fh.write(">%s\n" % name + "".join(seq[i:i + 70] + "\n" for i in range(0, L, 70)))
+    mx.check_faidx(fasta)
     bam = os.path.join(golden_dir, "bbmap.sorted.bam")
     out = tmp_path / "o.csv"
     res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"),
