@@ -35,6 +35,15 @@ namespace mc {
 #ifndef MC_PREFETCH_STATS
 #define MC_PREFETCH_STATS 1            // the same for the fused-statistics K2
 #endif
+#ifndef MC_APPLY_SHORT
+#define MC_APPLY_SHORT 1               // K2 without long reads: one branch per read in the apply loop
+                                       // (A/B, profiles/r05/r05ab1: direct C3 1.019 -> 1.002 ms, C2 0.0653 ->
+                                       // 0.0611; 2 = no branch, zero adds: 1.004 vs 0.990 ms, r05ab2)
+#endif
+#ifndef MC_DIRECT_ONE_CONTIG
+#define MC_DIRECT_ONE_CONTIG 1         // direct K2: a batch on the cached contig skips the contig lookup loop
+                                       // (C3 1.019 -> 1.007 ms, C2 0.0653 -> 0.0615; both: 0.988 / 0.0558)
+#endif
 #ifndef MC_NT_STORE
 #define MC_NT_STORE 1                  // non-temporal depth stores (written once, not re-read soon)
 #endif
@@ -1501,7 +1510,49 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
     int rs[4] = {0, 0, 0, 0};
     unsigned L[4] = {0, 0, 0, 0};          // contig length (positions fit 32 bits)
     unsigned todo = valid;
-    for (;;) {
+    // 4-bit masks of this lane's reads: in [lo, hi) (applied) and in [vlo,
+    // vhi) (checked here); the bounds relative to the batch are scalar
+    auto range4 = [&](int64_t lo, int64_t hi) -> unsigned {
+        const int la = (int)(lo - base < -8 ? -8 : lo - base > kBatch + 8 ? kBatch + 8 : lo - base);
+        const int ha = (int)(hi - base < -8 ? -8 : hi - base > kBatch + 8 ? kBatch + 8 : hi - base);
+        const int ka = min(max(la - lane4, 0), 4), kz = min(max(ha - lane4, 0), 4);
+        return ((1u << kz) - 1u) & ~((1u << ka) - 1u);
+    };
+    const unsigned inr = range4(dc.lo, dc.hi);
+    const unsigned own = range4(dc.vlo, dc.vhi);
+    bool fast = false;   // wave-uniform
+    if (MC_DIRECT_ONE_CONTIG && acc.ct >= 0) {
+        // every read this batch applies or checks is on the contig of the
+        // previous batch (sorted reads: almost every batch): one vote instead
+        // of the lookup loop's two and its per-read selects
+        const unsigned use = (inr | own) & valid;
+        bool other = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) other |= ((use >> k) & 1u) && tt[k] != acc.ct;
+        if (!__ballot(other)) {
+            const int64_t c = acc.c_off - C0, ln = acc.c_len;
+            const unsigned l32 = ln > 0xffffffffll ? 0xffffffffu : (unsigned)ln;
+            int c32, p_lo, p_hi;
+            if (c > kClamp) {
+                c32 = (int)kClamp;
+                p_lo = p_hi = 0;
+            } else if (c < -kClamp - (int64_t)INT32_MAX) {
+                c32 = -(int)kClamp;
+                p_lo = p_hi = 0;
+            } else {
+                c32 = (int)(uint32_t)(uint64_t)c;
+                p_lo = (int)(c < -kClamp ? -kClamp - c : 0);
+                p_hi = (int)(kClamp - c > (int64_t)INT32_MAX ? (int64_t)INT32_MAX : kClamp - c);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                rs[k] = (int)((unsigned)c32 + (unsigned)min(max(pp[k], p_lo), p_hi));
+                L[k] = l32;
+            }
+            fast = true;   // (reads outside use: their rs / L are never used)
+        }
+    }
+    for (; !fast;) {
         const int cand = (todo & 1u) ? tt[0] : (todo & 2u) ? tt[1] : (todo & 4u) ? tt[2]
                        : (todo & 8u) ? tt[3] : -1;
         const unsigned long long act = __ballot(cand >= 0);
@@ -1542,14 +1593,6 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
     // permute); lane 0 keeps its own, which came with the batch
     const int pt = __builtin_amdgcn_update_dpp(r.pt, tt[3], 0x138, 0xf, 0xf, false);
     const int ppv = __builtin_amdgcn_update_dpp(r.pp, pp[3], 0x138, 0xf, 0xf, false);
-    // 4-bit masks of this lane's reads: in [lo, hi) (applied) and in [vlo,
-    // vhi) (checked here); the bounds relative to the batch are scalar
-    auto range4 = [&](int64_t lo, int64_t hi) -> unsigned {
-        const int la = (int)(lo - base < -8 ? -8 : lo - base > kBatch + 8 ? kBatch + 8 : lo - base);
-        const int ha = (int)(hi - base < -8 ? -8 : hi - base > kBatch + 8 ? kBatch + 8 : hi - base);
-        const int ka = min(max(la - lane4, 0), 4), kz = min(max(ha - lane4, 0), 4);
-        return ((1u << kz) - 1u) & ~((1u << ka) - 1u);
-    };
     unsigned pend = 0, bad = 0, unfit = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1567,7 +1610,6 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
         bad |= (!ok | uns) ? 1u << k : 0u;
         unfit |= ((unsigned)pp[k] + (unsigned)sp[k] > L[k]) ? 1u << k : 0u;
     }
-    const unsigned inr = range4(dc.lo, dc.hi);
     b.pending = pend & inr;
     // the batch's maximum span (every read is loaded by the chunk it belongs
     // to, so the maximum over the workgroups is exact): the host takes long
@@ -1575,7 +1617,6 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
     const unsigned mm = valid & inr;
     acc.max_span = max(acc.max_span, max(max((mm & 1u) ? sp[0] : 0, (mm & 2u) ? sp[1] : 0),
                                          max((mm & 4u) ? sp[2] : 0, (mm & 8u) ? sp[3] : 0)));
-    const unsigned own = range4(dc.vlo, dc.vhi);
     acc.flags |= (bad & own) ? kDirectInvalid : (unfit & own) ? kDirectUnfit : 0u;
 }
 
@@ -2088,6 +2129,30 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
                             eb.pending &= ~(1u << k);
                         }
                 }
+                if (MC_APPLY_SHORT && !kLong) {
+                    // every pending read is short here (the direct path's masks;
+                    // a packed batch without long reads): one branch per read
+                    unsigned done = 0;
+#pragma unroll
+                    for (int k = 0; k < kReadsPerThread; ++k) {
+                        const bool go = ((b.pending >> k) & 1u) && b.rs[k] < tend_rel;
+                        done |= go ? 1u << k : 0u;
+                        const int s = b.rs[k] > 0 ? b.rs[k] : 0, e = b.rs[k] + b.sp[k];
+                        if (MC_APPLY_SHORT == 2) {
+                            // no branch: a read that applies nothing adds 0 to
+                            // its slots (a wave-uniform skip when no lane applies)
+                            const bool ap = go && e > s;
+                            if (__ballot(ap)) {
+                                atomicAdd(&ring[ring_slot(s)], ap ? 1 : 0);
+                                atomicAdd(&ring[ring_slot(e)], ap ? -1 : 0);
+                            }
+                        } else if (go && e > s) {
+                            atomicAdd(&ring[ring_slot(s)], 1);
+                            atomicAdd(&ring[ring_slot(e)], -1);
+                        }
+                    }
+                    b.pending &= ~done;
+                } else
 #pragma unroll
                 for (int k = 0; k < kReadsPerThread; ++k) {
                     if (((b.pending >> k) & 1u) && b.rs[k] < tend_rel) {
