@@ -313,16 +313,7 @@ def test_cli_kmer_histogram_gpu(golden_dir, fixture_golden, lib_built, tmp_path)
     rows.append("NNNNNNN,1,1,1,R1,Mapped")
     hist = tmp_path / "k.csv"
     hist.write_text("\n".join(rows) + "\n")
-    # pysam.FastaFile (cli.py:59) needs plain text or bgzip and faidx's line
-    # rule; the fixture is plain gzip and its ref2 starts with a 65-base line:
-    # the same sequences go in re-wrapped at 70 bases
-    fasta = str(tmp_path / "reference_1K.fa")
-    src = mx.FastaFile(os.path.join(golden_dir, "reference_1K.fa.gz"))
-    with open(fasta, "w") as fh:
-        for name, L in zip(src.references, src.lengths):
-            seq = src.fetch(name, 0, L)
-            fh.write(">%s\n" % name + "".join(seq[i:i + 70] + "\n" for i in range(0, L, 70)))
-    mx.check_faidx(fasta)
+    fasta = _indexable_fasta(golden_dir, tmp_path)
     bam = os.path.join(golden_dir, "bbmap.sorted.bam")
     out = tmp_path / "o.csv"
     res = CliRunner().invoke(cli_pileup, ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"),
@@ -348,6 +339,20 @@ def test_cli_kmer_histogram_gpu(golden_dir, fixture_golden, lib_built, tmp_path)
                 assert g[key] == str(v), (key, g[key], v)
 
 
+def _indexable_fasta(golden_dir, tmp_path):
+    """The reference's FASTA fixture as pysam.FastaFile (cli.py:59) can open
+    it: the fixture is plain gzip and its ref2 starts with a 65-base line
+    (faidx refuses both), so the same sequences go in re-wrapped at 70."""
+    fasta = str(tmp_path / "reference_1K.fa")
+    src = mx.FastaFile(os.path.join(golden_dir, "reference_1K.fa.gz"))
+    with open(fasta, "w") as fh:
+        for name, L in zip(src.references, src.lengths):
+            seq = src.fetch(name, 0, L)
+            fh.write(">%s\n" % name + "".join(seq[i:i + 70] + "\n" for i in range(0, L, 70)))
+    mx.check_faidx(fasta)
+    return fasta
+
+
 @pytest.mark.gpu
 def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path):
     """`metacov pileup -k` under torch.distributed.run with 2 ranks: each rank
@@ -369,7 +374,7 @@ def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path):
                                                        rng.integers(1, 50), r))
     hist = tmp_path / "k.csv"
     hist.write_text("\n".join(rows) + "\n")
-    fasta = os.path.join(golden_dir, "reference_1K.fa.gz")
+    fasta = _indexable_fasta(golden_dir, tmp_path)
     bam = os.path.join(golden_dir, "bbmap.sorted.bam")
     args = ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"), "-k", str(hist), "-f", fasta]
     one = tmp_path / "one.csv"
