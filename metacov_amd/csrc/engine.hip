@@ -195,9 +195,11 @@ struct mc_ctx {
     // each launch finds its bytes in a slot or uploads them into the next one
     static constexpr int kK2Slots = 4;
     DevBuf<K2Consts> d_k2c;
+    DevBuf<unsigned long long> d_bases_part;   // span_sum_kernel's per-workgroup partials
     Pinned h_k2c;
     K2Consts k2c[kK2Slots];
     bool k2c_valid[kK2Slots] = {false, false, false, false};
+    hipEvent_t k2c_ev[kK2Slots] = {};   // slot i's staging copy is done
     int k2c_next = 0;
     int32_t max_span = 0;
     bool long_hint = false;               // the last full prepare of this contig set had long reads
@@ -363,7 +365,13 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_dres.release();
     ctx->d_endw.release();
     ctx->d_k2c.release();
+    ctx->d_bases_part.release();
     ctx->h_k2c.release();
+    for (hipEvent_t& e : ctx->k2c_ev)
+        if (e) {
+            (void)hipEventDestroy(e);
+            e = nullptr;
+        }
     ctx->d_tile_cnt.release();
     ctx->d_tile_off.release();
     ctx->d_tile_ev.release();
@@ -1101,9 +1109,16 @@ static DirectWindow direct_window(const mc_ctx* ctx) {
 }
 
 // K2's constant arguments in device memory (K2Consts): the slot holding
-// these bytes, else the next slot, uploaded on the ctx stream.  The pinned
-// staging is reused only after the stream has drained the previous upload
-// (uploads happen when buffers are reallocated or the region set changes).
+// these bytes, else the next slot, uploaded on the ctx stream (uploads happen
+// when buffers are reallocated or the region set changes).  Each slot has
+// its own pinned staging; it is rewritten only once that slot's previous
+// copy is done (its event), not after a drain of the whole stream.  The
+// slots are matched bytewise: K2Consts has no padding but DirectArgs' one
+// hole, which launch_depth keeps zeroed (memberwise stores into a zeroed
+// struct).
+static_assert(sizeof(DirectArgs) == 4 * 8 + 8 + sizeof(DirectWindow) && sizeof(DirectWindow) == 32 &&
+                  sizeof(FusedRegions) == 10 * 8 && sizeof(ReadArrays) == 4 * 8,
+              "K2Consts: padding beyond DirectArgs' 4 bytes after nc");
 static int k2_consts(mc_ctx* ctx, const K2Consts& kc, const K2Consts** out) {
     for (int i = 0; i < mc_ctx::kK2Slots; ++i)
         if (ctx->k2c_valid[i] && std::memcmp(&ctx->k2c[i], &kc, sizeof kc) == 0) {
@@ -1111,12 +1126,15 @@ static int k2_consts(mc_ctx* ctx, const K2Consts& kc, const K2Consts** out) {
             return MC_OK;
         }
     HIP_TRY(ctx->d_k2c.reserve(mc_ctx::kK2Slots));
-    HIP_TRY(ctx->h_k2c.reserve(sizeof(K2Consts)));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));   // the staging's previous copy is done
+    HIP_TRY(ctx->h_k2c.reserve(sizeof(K2Consts) * mc_ctx::kK2Slots));
     const int i = ctx->k2c_next;
     ctx->k2c_next = (i + 1) % mc_ctx::kK2Slots;
-    std::memcpy(ctx->h_k2c.h, &kc, sizeof kc);
-    HIP_TRY(hipMemcpyAsync(ctx->d_k2c.p + i, ctx->h_k2c.h, sizeof kc, hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->k2c_ev[i]) HIP_TRY(hipEventSynchronize(ctx->k2c_ev[i]));   // the slot's previous copy is done
+    else HIP_TRY(hipEventCreateWithFlags(&ctx->k2c_ev[i], hipEventDisableTiming));
+    K2Consts* stage = reinterpret_cast<K2Consts*>(ctx->h_k2c.h) + i;
+    std::memcpy(stage, &kc, sizeof kc);
+    HIP_TRY(hipMemcpyAsync(ctx->d_k2c.p + i, stage, sizeof kc, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->k2c_ev[i], ctx->stream));
     ctx->k2c[i] = kc;
     ctx->k2c_valid[i] = true;
     *out = ctx->d_k2c.p + i;
@@ -1164,8 +1182,12 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     kc.R = fr;
     DirectWindow w = direct_window(ctx);
     w.parity = 0;   // (K2 takes this call's parity as an argument)
-    kc.D = DirectArgs{ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_len.p, (int32_t)ctx->len.size(),
-                      ctx->d_dres.p, w};
+    kc.D.j0 = ctx->d_jidx.p;   // (memberwise: the struct's padding stays zero)
+    kc.D.jh = ctx->d_jidx.p + (n_base + 1);
+    kc.D.len = ctx->d_len.p;
+    kc.D.nc = (int32_t)ctx->len.size();
+    kc.D.dres = ctx->d_dres.p;
+    kc.D.win = w;
     const K2Consts* dk = nullptr;
     if (int rc = k2_consts(ctx, kc, &dk)) return rc;
     const int win_parity = (int)(ctx->direct_gen & 1);
@@ -1816,9 +1838,12 @@ extern "C" int mc_region_stats(mc_ctx* ctx, int64_t R, const int32_t* tid, const
 static int direct_bases(mc_ctx* ctx) {
     hipStream_t s = ctx->stream;
     const int64_t n = ctx->n_reads;
-    HIP_TRY(hipMemsetAsync(ctx->d_dres.p + kDresBases, 0, 8, s));
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>(2048, (n / 4 + kBlock - 1) / kBlock));
+    HIP_TRY(ctx->d_bases_part.reserve((size_t)g));
     hipLaunchKernelGGL(span_sum_kernel, dim3((unsigned)g), dim3(kBlock), 0, s, ctx->d_span.p, n,
+                       ctx->d_bases_part.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(span_sum_final_kernel, dim3(1), dim3(kBlock), 0, s, ctx->d_bases_part.p, (int)g,
                        ctx->d_dres.p + kDresBases);
     HIP_TRY(hipGetLastError());
     unsigned long long v = 0;
