@@ -504,6 +504,10 @@ int mc_ecor_run(mc_ecor* e, int64_t R, const int64_t* base, const int64_t* n_ava
 typedef struct mc_scan_src mc_scan_src;
 int mc_scan_src_open_bam(const char* path, int n_threads, mc_scan_src** out);
 int mc_scan_src_open_fastq(const char* path1, const char* path2, mc_scan_src** out);
+/* SAM text (plain, gzip or BGZF), the records as htslib's sam_parse1 stores
+ * them (pysam opens a .sam for `metacov scan x.sam`: cli.py:171-173,
+ * scan.pyx:188-216): @SQ order for the tids, POS - 1, nt16 bases. */
+int mc_scan_src_open_sam(const char* path, mc_scan_src** out);
 int mc_scan_src_close(mc_scan_src* s);
 int mc_scan_src_n_targets(const mc_scan_src* s, int32_t* n);
 int mc_scan_src_target(const mc_scan_src* s, int32_t i, const char** name, int64_t* length);

@@ -167,6 +167,7 @@ SIGNATURES = {
     # metacov scan: read sources (host) and histograms (GPU)
     "mc_scan_src_open_bam": [ctypes.c_char_p, ctypes.c_int, _PP],
     "mc_scan_src_open_fastq": [ctypes.c_char_p, ctypes.c_char_p, _PP],
+    "mc_scan_src_open_sam": [ctypes.c_char_p, _PP],
     "mc_scan_src_close": [_P],
     "mc_scan_src_n_targets": [_P, _PI32],
     "mc_scan_src_target": [_P, _I32, ctypes.POINTER(ctypes.c_char_p), _PI64],

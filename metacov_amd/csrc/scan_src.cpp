@@ -30,6 +30,7 @@
 // (FastQFile.cnext, pyfq.pyx:166-175).
 #include <zlib.h>
 
+#include <cctype>
 #include <memory>
 
 #include "bgzf.h"
@@ -50,6 +51,21 @@ struct Ascii16 {
     }
 };
 const Ascii16 kAscii16;
+
+// SAM SEQ byte -> nt16 code as htslib's seq_nt16_table stores it in a BAM
+// record ("=ACMGRSVTWYHKDBN", either case; anything else N = 15)
+struct SamNt16 {
+    uint8_t t[256];
+    SamNt16() {
+        std::memset(t, 15, sizeof t);
+        const char* code = "=ACMGRSVTWYHKDBN";
+        for (int i = 0; i < 16; ++i) {
+            t[(uint8_t)code[i]] = (uint8_t)i;
+            t[(uint8_t)std::tolower(code[i])] = (uint8_t)i;
+        }
+    }
+};
+const SamNt16 kSamNt16;
 
 // Buffered getline over a zlib stream (gzread reads plain files as-is).
 struct LineReader {
@@ -107,7 +123,7 @@ struct LineReader {
 }  // namespace
 
 struct mc_scan_src {
-    int kind = 0;   // 0 = BAM, 1 = FASTQ
+    int kind = 0;   // 0 = BAM, 1 = FASTQ, 2 = SAM text
     std::string path;
     int64_t n_records = 0;
     // BAM
@@ -118,10 +134,12 @@ struct mc_scan_src {
     std::unique_ptr<uint8_t[]> buf;
     size_t cap = 0, n = 0, o = 0, next_off = 0;
     bool have_header = false, last = false, done = false;
-    // FASTQ
+    // FASTQ (SAM: fq[0], the pending first record in line[0])
     LineReader fq[2];
     int n_fq = 0, cur = 0;
     std::string line[4];
+    bool sam_pending = false;
+    int64_t sam_line = 0;
     // the batch handed out by mc_scan_src_next
     std::vector<int32_t> rlen, flag, gpos, gisize, tid;
     std::vector<int64_t> seq_off;
@@ -262,7 +280,148 @@ int fq_next(mc_scan_src* s, int64_t max_reads, int64_t max_bytes) {
     return MC_OK;
 }
 
+// SAM text (plain, gzip or BGZF): the record fields scan reads, as htslib's
+// sam_parse1 stores them in a bam1_t (pysam AlignmentFile over a .sam, what
+// the reference opens for `scan x.sam`: metacov/cli.py:171-173,
+// scan.pyx:188-216): FLAG, RNAME -> tid (the @SQ order; "*" = -1), POS - 1,
+// TLEN, SEQ as nt16 ("*" = no bases).
+int sam_fields(mc_scan_src* s, const std::string& ln, const char* f[11], size_t fl[11]) {
+    size_t a = 0;
+    int k = 0;
+    for (; k < 11; ++k) {
+        const size_t b = ln.find('\t', a);
+        const size_t e = b == std::string::npos ? ln.size() : b;
+        f[k] = ln.data() + a;
+        fl[k] = e - a;
+        if (b == std::string::npos) {
+            ++k;
+            break;
+        }
+        a = b + 1;
+    }
+    MC_REQUIRE(k >= 11, MC_E_IO, "%s: line %lld: a SAM record needs 11 fields, found %d", s->path.c_str(),
+               (long long)s->sam_line, k);
+    return MC_OK;
+}
+
+int sam_int(mc_scan_src* s, const char* p, size_t n, int base, int64_t* out) {
+    std::string t(p, n);
+    char* end = nullptr;
+    errno = 0;
+    const long long v = std::strtoll(t.c_str(), &end, base);
+    MC_REQUIRE(n && end == t.c_str() + n && errno == 0, MC_E_IO, "%s: line %lld: bad number '%s'",
+               s->path.c_str(), (long long)s->sam_line, t.c_str());
+    *out = v;
+    return MC_OK;
+}
+
+// Next non-empty line without its line end into line[0]; *got false at the end.
+int sam_getline(mc_scan_src* s, bool* got) {
+    for (;;) {
+        if (int rc = s->fq[0].getline(s->line[0], got)) return rc;
+        if (!*got) return MC_OK;
+        ++s->sam_line;
+        std::string& l = s->line[0];
+        while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+        if (!l.empty()) return MC_OK;
+    }
+}
+
+int sam_header(mc_scan_src* s) {
+    for (;;) {
+        bool got = false;
+        if (int rc = sam_getline(s, &got)) return rc;
+        if (!got) return MC_OK;
+        const std::string& l = s->line[0];
+        if (l[0] != '@') {
+            s->sam_pending = true;
+            return MC_OK;
+        }
+        if (l.compare(0, 4, "@SQ\t") != 0) continue;
+        std::string name;
+        int64_t len = -1;
+        for (size_t a = 4; a < l.size();) {
+            size_t b = l.find('\t', a);
+            if (b == std::string::npos) b = l.size();
+            const std::string tag = l.substr(a, b - a);
+            if (tag.compare(0, 3, "SN:") == 0) name = tag.substr(3);
+            if (tag.compare(0, 3, "LN:") == 0 && sam_int(s, tag.data() + 3, tag.size() - 3, 10, &len)) return MC_E_IO;
+            a = b + 1;
+        }
+        MC_REQUIRE(!name.empty() && len >= 0, MC_E_IO, "%s: line %lld: @SQ needs SN and LN", s->path.c_str(),
+                   (long long)s->sam_line);
+        s->names.push_back(name);
+        s->lens.push_back(len);
+    }
+}
+
+int sam_next(mc_scan_src* s, int64_t max_reads, int64_t max_bytes) {
+    const char* f[11];
+    size_t fl[11];
+    while ((int64_t)s->rlen.size() < max_reads && (int64_t)s->seq.size() < max_bytes) {
+        if (!s->sam_pending) {
+            bool got = false;
+            if (int rc = sam_getline(s, &got)) return rc;
+            if (!got) {
+                s->done = true;
+                return MC_OK;
+            }
+        }
+        s->sam_pending = false;
+        const std::string& ln = s->line[0];
+        MC_REQUIRE(ln[0] != '@', MC_E_IO, "%s: line %lld: header line after the records", s->path.c_str(),
+                   (long long)s->sam_line);
+        if (int rc = sam_fields(s, ln, f, fl)) return rc;
+        int64_t flag = 0, pos = 0, tlen = 0;
+        if (int rc = sam_int(s, f[1], fl[1], 0, &flag)) return rc;
+        if (int rc = sam_int(s, f[3], fl[3], 10, &pos)) return rc;
+        if (int rc = sam_int(s, f[8], fl[8], 10, &tlen)) return rc;
+        MC_REQUIRE(flag >= 0 && flag <= 0xffff && pos >= 0 && pos <= (int64_t)INT32_MAX + 1 &&
+                       tlen >= INT32_MIN && tlen <= INT32_MAX,
+                   MC_E_IO, "%s: line %lld: FLAG, POS or TLEN out of range", s->path.c_str(), (long long)s->sam_line);
+        int32_t tid = -1;
+        if (!(fl[2] == 1 && f[2][0] == '*')) {
+            const std::string rn(f[2], fl[2]);
+            auto it = std::find(s->names.begin(), s->names.end(), rn);
+            MC_REQUIRE(it != s->names.end(), MC_E_IO, "%s: line %lld: reference '%s' is not in the header",
+                       s->path.c_str(), (long long)s->sam_line, rn.c_str());
+            tid = (int32_t)(it - s->names.begin());
+        }
+        const bool no_seq = fl[9] == 1 && f[9][0] == '*';
+        const size_t L = no_seq ? 0 : fl[9];
+        MC_REQUIRE(L <= (size_t)INT32_MAX, MC_E_RANGE, "SAM sequence too long");
+        const int32_t l_seq = (int32_t)L, p0 = (int32_t)(pos - 1);
+        s->rlen.push_back(l_seq);
+        s->flag.push_back((int32_t)flag);
+        s->gpos.push_back((flag & 0x10) ? p0 + l_seq : p0);
+        s->gisize.push_back((flag & 0x2) ? (int32_t)tlen : 0);
+        s->tid.push_back(tid);
+        const size_t at = s->seq.size();
+        s->seq.resize(at + (((L + 1) / 2 + 3) & ~size_t(3)), 0);   // 4-byte aligned starts
+        uint8_t* o = s->seq.data() + at;
+        const uint8_t* c = reinterpret_cast<const uint8_t*>(f[9]);
+        for (size_t i = 0; i + 1 < L; i += 2) o[i >> 1] = (uint8_t)(kSamNt16.t[c[i]] << 4 | kSamNt16.t[c[i + 1]]);
+        if (L & 1) o[L >> 1] = (uint8_t)(kSamNt16.t[c[L - 1]] << 4);
+        s->seq_off.push_back((int64_t)s->seq.size());
+        ++s->n_records;
+    }
+    return MC_OK;
+}
+
 }  // namespace
+
+extern "C" int mc_scan_src_open_sam(const char* path, mc_scan_src** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<mc_scan_src> s(new mc_scan_src());
+    s->kind = 2;
+    s->path = path;
+    if (int rc = s->fq[0].open(path)) return rc;
+    if (int rc = sam_header(s.get())) return rc;
+    s->clear_batch();
+    *out = s.release();
+    return MC_OK;
+}
 
 extern "C" int mc_scan_src_open_bam(const char* path, int n_threads, mc_scan_src** out) {
     MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
@@ -320,8 +479,9 @@ extern "C" int mc_scan_src_next(mc_scan_src* s, int64_t max_reads, int64_t max_s
     MC_REQUIRE(s && n_out && max_reads > 0 && max_seq_bytes > 0, MC_E_INVALID, "bad argument");
     s->clear_batch();
     if (!s->done) {
-        if (int rc = s->kind == 0 ? bam_next(s, max_reads, max_seq_bytes)
-                                  : fq_next(s, max_reads, max_seq_bytes))
+        if (int rc = s->kind == 0   ? bam_next(s, max_reads, max_seq_bytes)
+                     : s->kind == 2 ? sam_next(s, max_reads, max_seq_bytes)
+                                    : fq_next(s, max_reads, max_seq_bytes))
             return rc;
     }
     *n_out = (int64_t)s->rlen.size();

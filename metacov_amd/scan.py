@@ -294,10 +294,26 @@ def _source(lib, infile, n_threads):
     if path.endswith((".fq", ".fq.gz", ".fastq", ".fastq.gz")):
         _lib.check(lib.mc_scan_src_open_fastq(path.encode(), None, ctypes.byref(h)), lib)
         return h, "fq"
-    if path.endswith(".sam"):
-        raise NotImplementedError("SAM text input is not supported; convert it to BAM")
+    if is_sam(path):   # pysam tells SAM from BAM by content, whatever the name
+        _lib.check(lib.mc_scan_src_open_sam(path.encode(), ctypes.byref(h)), lib)
+        return h, "bam"
     _lib.check(lib.mc_scan_src_open_bam(path.encode(), n_threads, ctypes.byref(h)), lib)
     return h, "bam"
+
+
+def is_sam(path):
+    """True for SAM text (plain, gzip or BGZF), False for BAM: htslib's
+    format detection looks at the (inflated) first bytes, "BAM\\1" or text."""
+    import gzip
+    with open(path, "rb") as fh:
+        head = fh.read(2)
+    if head == b"\x1f\x8b":
+        try:
+            with gzip.open(path, "rb") as fh:
+                return fh.read(4) != b"BAM\x01"
+        except (OSError, EOFError):
+            return False
+    return True
 
 
 def _fasta(fasta):

@@ -212,6 +212,67 @@ def test_cpp_bam_source_matches_oracle(mix, golden_dir, lib_built):
         assert rows == want
 
 
+def _source_rows(lib, h):
+    rows = []
+    for (rlen, flag, gpos, gisize, tid), off, seq in _src_batches(lib, h, cap=301):
+        codes = []
+        for i in range(len(rlen)):
+            b = seq[off[i]:off[i + 1]]
+            nib = np.empty(2 * len(b), np.uint8)
+            nib[0::2], nib[1::2] = b >> 4, b & 15
+            codes.append("".join(bamread.NT16[c] for c in nib[:rlen[i]]))
+        rows += list(zip(rlen.tolist(), flag.tolist(), gpos.tolist(), gisize.tolist(),
+                         tid.tolist(), codes))
+    return rows
+
+
+def test_cpp_sam_source_matches_bam_source(mix, golden_dir, lib_built, tmp_path):
+    """SAM text (`metacov scan x.sam`, cli.py:171-173: pysam reads it like a
+    BAM) gives the records of the BAM it was converted from: the same
+    accessor values and bases, plain and gzip-compressed; pysam's content
+    detection picks SAM or BAM whatever the file name."""
+    from metacov_amd import _lib, scan as mscan
+    from tests.sam_convert import bam_to_sam
+    lib = _lib.load()
+    for k, path in enumerate((mix[0], os.path.join(golden_dir, "bbmap.sorted.bam"),
+                              os.path.join(golden_dir, "synth_edge.bam"))):
+        names, lengths, recs = bamread.read_bam(path)
+        want = [(r.l_seq, r.flag, r.pos + r.l_seq if r.flag & 0x10 else r.pos,
+                 r.tlen if r.flag & 2 else 0, r.tid, r.seq) for r in recs]
+        for gz in (False, True):
+            sam = bam_to_sam(path, str(tmp_path / ("s%d%s.sam" % (k, ".gz" if gz else ""))), gz)
+            assert mscan.is_sam(sam) and not mscan.is_sam(path)
+            h = ctypes.c_void_p()
+            _lib.check(lib.mc_scan_src_open_sam(sam.encode(), ctypes.byref(h)), lib)
+            nt = ctypes.c_int32()
+            lib.mc_scan_src_n_targets(h, ctypes.byref(nt))
+            assert nt.value == len(names)
+            rows = _source_rows(lib, h)
+            n = ctypes.c_int64()
+            lib.mc_scan_src_records(h, ctypes.byref(n))
+            lib.mc_scan_src_close(h)
+            assert n.value == len(recs) and rows == want
+
+
+def test_cpp_sam_source_errors(tmp_path, lib_built):
+    from metacov_amd import _lib
+    lib = _lib.load()
+    head = "@SQ\tSN:a\tLN:100\n"
+    good = "r1\t0\ta\t5\t60\t4M\t*\t0\t0\tACGT\t*\n"
+    for body, msg in ((good.replace("\ta\t", "\tzz\t"), "not in the header"),
+                      ("r1\t0\ta\t5\n", "11 fields"),
+                      (good.replace("\t5\t", "\tx5\t"), "bad number"),
+                      (good + "@SQ\tSN:b\tLN:5\n", "header line after")):
+        p = tmp_path / "bad.sam"
+        p.write_text(head + body)
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_src_open_sam(str(p).encode(), ctypes.byref(h)), lib)
+        n = ctypes.c_int64()
+        rc = lib.mc_scan_src_next(h, 100, 1 << 20, ctypes.byref(n))
+        lib.mc_scan_src_close(h)
+        assert rc != 0 and msg in lib.mc_last_error().decode()
+
+
 # ----------------------------------------------------- processors (no GPU)
 
 def test_byflag_rows_layout():
@@ -323,6 +384,26 @@ def test_scan_bam_cli_vs_oracle_gpu(case, mix, golden_dir, lib_built, tmp_path):
     want = oscan.scan_csv([bam], out, **_oracle_kwargs(extra))
     for name in out:
         assert got[name] == want[name], name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [0, 3, 4])
+def test_scan_sam_cli_vs_bam_and_oracle_gpu(case, mix, golden_dir, lib_built, tmp_path):
+    """`metacov scan x.sam` (the SAM conversion of the BAM) writes the CSV
+    bytes of the BAM run and of the oracle (oracle/scan.py on the BAM)."""
+    from tests.sam_convert import bam_to_sam
+    which, out, extra = BAM_CASES[case]
+    bam = mix[0] if which == "mix" else os.path.join(golden_dir, "bbmap.sorted.bam")
+    subst = {"@fa": os.path.join(golden_dir, "reference_1K.fa.gz"), "@mixfa": mix[1]}
+    extra = [subst.get(a, a) for a in extra]
+    sam = bam_to_sam(bam, str(tmp_path / "x.sam"))
+    (tmp_path / "sam").mkdir()
+    (tmp_path / "bam").mkdir()
+    got = _cli_scan(tmp_path / "sam", [sam], out, extra)
+    from_bam = _cli_scan(tmp_path / "bam", [bam], out, extra)
+    want = oscan.scan_csv([bam], out, **_oracle_kwargs(extra))
+    for name in out:
+        assert got[name] == from_bam[name] == want[name], name
 
 
 FQ_CASES = [
