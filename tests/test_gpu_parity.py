@@ -1073,11 +1073,14 @@ def test_bench_json_contract(tmp_path):
     assert c["value"] > 0 and c["kind"] in ("port", "reference")
 
 
-def test_bench_gpus_two_launches_ranks(tmp_path):
+@pytest.mark.parametrize("cfg,reads,contigs", [("c3", 2_000_000, 64), ("c5", 2_000_000, 400)])
+def test_bench_gpus_two_launches_ranks(tmp_path, cfg, reads, contigs):
     """`bench.py --gpus 2` (no torchrun around it) starts two ranks through a
     child torch.distributed.run and prints rank 0's line: n_gpus == 2, the
     contig-sharded (strong) layout, the all-gather timed apart.  gloo lets
-    both ranks share the box's one GPU."""
+    both ranks share the box's one GPU.  C3's layout and C5's (long reads:
+    the full prepare, long-read K2, device recomputes) rehearse C4 / the
+    8-GPU C5 run; the gathered rows equal the oracle's."""
     import json
     import subprocess
     import sys
@@ -1086,7 +1089,7 @@ def test_bench_gpus_two_launches_ranks(tmp_path):
     env.pop("WORLD_SIZE", None)
     rows_path = str(tmp_path / "rows.npy")
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                          "--config", "c3", "--reads", "2000000", "--contigs", "64", "--steps", "2",
+                          "--config", cfg, "--reads", str(reads), "--contigs", str(contigs), "--steps", "2",
                           "--warmup", "1", "--prepare-steps", "1", "--dump-rows", rows_path],
                          capture_output=True, text=True, timeout=600, cwd=str(tmp_path), env=env)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -1096,16 +1099,16 @@ def test_bench_gpus_two_launches_ranks(tmp_path):
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["ranks_seen"] == 2
     assert d["scaling"] == "strong" and d["backend"] == "gloo"
     assert d["allgather_ms"] is not None and d["allgather_ms"] > 0
-    assert d["config"]["regions"] == 64
+    assert d["config"]["regions"] == contigs
     assert d["value"] > 0
     # the gathered table, field by field, against the oracle on the same
     # workload (regenerated here: the bench's GPU generator is seeded)
     import torch
     sys.path.insert(0, root)
     import bench
-    lengths, weights = bench.config_contigs("c3", 2_000_000, 64)
-    tid, pos, span, _ = bench.device_workload(torch, lengths, weights, 2_000_000, 1,
-                                              torch.device("cuda", 0))
+    lengths, weights = bench.config_contigs(cfg, reads, contigs)
+    tid, pos, span, _ = bench.device_workload(torch, lengths, weights, reads, 1,
+                                              torch.device("cuda", 0), long_reads=cfg == "c5")
     tid, pos, span = (x.cpu().numpy() for x in (tid, pos, span))
     dd, ext, coff = coracle.depth(lengths, tid, pos, span)
     R = len(lengths)
