@@ -119,6 +119,60 @@ __global__ void __launch_bounds__(256, 4) k2shape(Args a) {
     if (acc == 0x7fedcba9) a.sink[0] = acc;
 }
 
+// 512-thread workgroups (8 waves) on the same chunks: 2 per CU keep K2's 16
+// waves per CU with half as many concurrent chunk streams (the g512 rows
+// above run 2 x 256-thread workgroups per CU: 8 waves).
+template <int MODE>
+__global__ void __launch_bounds__(512, 2) k2shape512(Args a) {
+    __shared__ unsigned c_s[2];
+    __shared__ int pad[20480];
+    if (threadIdx.x == 0) pad[0] = 0;
+    int acc = 0;
+    for (;;) {
+        if (threadIdx.x == 0) c_s[0] = atomicAdd(a.q, 1u);
+        __syncthreads();
+        const int64_t c = c_s[0];
+        __syncthreads();
+        if (c >= a.n_chunks) break;
+        const int64_t r0 = read_lo(a, c), r1 = read_lo(a, c + 1);
+        constexpr int kB2 = 2048;
+        const int nb = (int)((r1 - r0 + kB2 - 1) / kB2);
+        auto load2 = [&](int64_t q0) {
+            const int64_t r = (q0 & ~3ll) + 4 * threadIdx.x;
+            int v = 0;
+            if (r < r1) {
+                const i32x4 t = a.tid[r >> 2], p = a.pos[r >> 2], s = a.span[r >> 2];
+                v = t.x + p.y + s.z + t.w;
+            }
+            return v;
+        };
+        auto store2 = [&](int t, int v) {
+            i32x4* base = a.depth + c * kChunk4 + t * kTile4 + threadIdx.x;
+            __builtin_nontemporal_store(i32x4{v, 0, t, 3}, base);
+            __builtin_nontemporal_store(i32x4{v, 1, t, 3}, base + 512);
+        };
+        if (MODE == 2) {
+            int v = 0;
+            for (int b = 0; b < nb; ++b) v += load2(r0 + (int64_t)b * kB2);
+            for (int t = 0; t < 8; ++t) store2(t, v + t);
+        } else {
+            int b = 1, v = load2(r0);
+            int nextv = b < nb ? load2(r0 + (int64_t)b * kB2) : 0;
+            for (int t = 0; t < 8; ++t) {
+                const int need = ((t + 1) * nb + 7) / 8;
+                while (b < need) {
+                    v += nextv;
+                    ++b;
+                    nextv = b < nb ? load2(r0 + (int64_t)b * kB2) : 0;
+                }
+                store2(t, v + t);
+            }
+            acc += nextv;
+        }
+    }
+    if (acc == 0x7fedcba9) a.sink[0] = acc;
+}
+
 int main() {
     const int64_t n_chunks = 1005000000LL / 32768;          // 30,670 chunks (C3 genome)
     const int64_t n_reads = 100000000LL;
@@ -131,12 +185,12 @@ int main() {
     a.tid = t; a.pos = p; a.span = s; a.depth = d; a.n_chunks = n_chunks; a.n_reads = n_reads; a.q = q; a.sink = o;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     printf("C3 shape: %lld chunks, %.3f GB written, %.3f GB read\n", (long long)n_chunks, wbytes / 1e9, rbytes / 1e9);
-    auto run = [&](const char* nm, int g, auto kern, double bytes) {
+    auto run = [&](const char* nm, int g, auto kern, double bytes, int bt = 256) {
         float ms[8];
         for (int rep = 0; rep < 9; ++rep) {
             hipMemsetAsync(q, 0, 4);
             hipEventRecord(e0);
-            hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, a);
+            hipLaunchKernelGGL(kern, dim3(g), dim3(bt), 0, 0, a);
             hipEventRecord(e1); hipEventSynchronize(e1);
             float x; hipEventElapsedTime(&x, e0, e1);
             if (rep) ms[rep - 1] = x;
@@ -146,7 +200,11 @@ int main() {
                bytes / (sum / 8 * 1e-3) / 1e12, bytes / (best * 1e-3) / 1e12);
     };
     const double mix = (double)wbytes + rbytes;
-    for (int g : {512, 1024, 2048}) {
+    for (int g : {512, 256}) {
+        run("seq 512thr", g, k2shape512<2>, mix, 512);
+        run("inter 512thr", g, k2shape512<3>, mix, 512);
+    }
+    for (int g : {512, 1024}) {
         run("wr", g, k2shape<0, true>, wbytes);
         run("rd", g, k2shape<1, true>, rbytes);
         run("seq", g, k2shape<2, true>, mix);
