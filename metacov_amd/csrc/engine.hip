@@ -449,10 +449,10 @@ extern "C" int mc_set_contigs(mc_ctx* ctx, int32_t n, const int64_t* lengths) {
 
 // grow the read arrays to hold `n_total` reads (+ one batch of padding)
 static int reserve_reads(mc_ctx* ctx, int64_t n_total, bool cigar_mode) {
-    const size_t cap = (size_t)round_up(n_total + kBatch, kBatch);
+    const size_t cap = (size_t)round_up(n_total + kPadBatch, kPadBatch);
     if (cap > ctx->d_tid.cap) {
         size_t ncap = std::max(cap, ctx->d_tid.cap * 3 / 2);
-        ncap = (size_t)round_up((int64_t)ncap, kBatch);
+        ncap = (size_t)round_up((int64_t)ncap, kPadBatch);
         DevBuf<int32_t> t2, p2, s2;
         HIP_TRY(t2.reserve(ncap));
         HIP_TRY(p2.reserve(ncap));
@@ -804,7 +804,7 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         HIP_TRY(ctx->d_tile_cnt.reserve(n_tiles + 1));
         HIP_TRY(ctx->d_chunk_carry.reserve(ctx->n_chunks + 1));
         HIP_TRY(ctx->d_tile_off.reserve(n_tiles + 1));
-        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(n + kBatch)));   // K2 loads whole int4 batches
+        HIP_TRY(ctx->d_tile_ev.reserve((size_t)(n + kPadBatch)));   // K2 loads whole int4 batches
         if (!counted) {
             HIP_TRY(hipMemsetAsync(ctx->d_tile_cnt.p, 0, (n_tiles + 1) * 4, s));
             HIP_TRY(hipMemsetAsync(ctx->d_chunk_carry.p, 0, (ctx->n_chunks + 1) * 4, s));
@@ -870,9 +870,9 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             HIP_TRY(hipGetLastError());
         }
         if (n) {
-            HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kBatch)));   // whole-batch loads
+            HIP_TRY(ctx->d_gpos.reserve((size_t)(n + kPadBatch)));   // whole-batch loads
             end_words = count_long && ctx->n_chunks * ctx->chunk_w < (int64_t)0xffffffffll;
-            if (end_words) HIP_TRY(ctx->d_endw.reserve((size_t)(n + kBatch)));
+            if (end_words) HIP_TRY(ctx->d_endw.reserve((size_t)(n + kPadBatch)));
             IngestIndex ix{ctx->d_coff.p, base_lw(ctx), ctx->short_max, n_base, ctx->d_chunk_first.p,
                            count_long ? ctx->d_tile_cnt.p : nullptr, count_long ? ctx->d_chunk_carry.p : nullptr,
                            ctx->n_chunks * ctx->chunk_w, lcw, end_words ? ctx->d_endw.p : nullptr};
@@ -1070,7 +1070,7 @@ static int occupancy_grid(mc_ctx* ctx, int variant, const void* kernel, size_t l
         int dev = 0, ncu = 0, per = 0;
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kK2Block, lds));
         if (MC_K2_PER_CU > 0) per = std::min(per, (int)MC_K2_PER_CU);
         cached = ncu * std::max(1, per);
         ctx->k2_resident_lds[variant] = lds;
@@ -1192,7 +1192,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     if (int rc = k2_consts(ctx, kc, &dk)) return rc;
     const int win_parity = (int)(ctx->direct_gen & 1);
 #define MC_LAUNCH_K2(S, L, D)                                                                  \
-    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kBlock), lds, s, kc.A, dk,    \
+    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kK2Block), lds, s, kc.A, dk,  \
                        ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p,        \

@@ -44,6 +44,12 @@ namespace mc {
 #define MC_DIRECT_ONE_CONTIG 1         // direct K2: a batch on the cached contig skips the contig lookup loop
                                        // (C3 1.019 -> 1.007 ms, C2 0.0653 -> 0.0615; both: 0.988 / 0.0558)
 #endif
+#ifndef MC_K2_WAVE_ADVANCE
+#define MC_K2_WAVE_ADVANCE 0           // K2's read batches advance per wave (no block vote in the apply loop)
+#endif
+#ifndef MC_FILL_WAVE_COUNTS
+#define MC_FILL_WAVE_COUNTS 0          // long_fill_words_kernel: one count atomic per distinct tile of a wave
+#endif
 #ifndef MC_NT_STORE
 #define MC_NT_STORE 1                  // non-temporal depth stores (written once, not re-read soon)
 #endif
@@ -85,7 +91,22 @@ constexpr int kTilesPerChunk = MC_TILES_PER_CHUNK;
 constexpr int kTilesPerChunkLong = MC_TILES_PER_CHUNK_LONG;
 constexpr int kReadsPerThread = 4;     // int4 loads of tid/pos/span
 constexpr int kBatch = kBlock * kReadsPerThread;
-constexpr int kLdsHeader = 20;         // ints reserved in front of the ring (K2: see depth_kernel)
+// K2's workgroup (depth_kernel alone): MC_K2_WAVES waves.  The K2-shape
+// micro (profiles/r05/r05g_micro_k2_shape.txt) moves K2's byte mix in 0.79-0.80
+// ms with 2 x 512-thread workgroups per CU against 0.92 ms with 4 x 256 at
+// the same 16 waves per CU: half as many concurrent chunk streams, each with
+// twice the bytes in flight.
+#ifndef MC_K2_WAVES
+#define MC_K2_WAVES 4
+#endif
+constexpr int kK2Waves = MC_K2_WAVES;
+constexpr int kK2Block = 64 * kK2Waves;
+constexpr int kK2Batch = kK2Block * kReadsPerThread;   // reads per K2 batch
+constexpr int kPadBatch = kK2Batch > kBatch ? kK2Batch : kBatch;   // read arrays' padding past n
+static_assert(kK2Waves == 4 || kK2Waves == 8, "K2 workgroups of 4 or 8 waves");
+// K2's LDS header (ints): [0] chunk id, [4, 4 + W) wave totals, [4 + W, 4 +
+// 2W) wave maxima, then block_all2's two 8-byte vote words
+constexpr int kLdsHeader = (4 + 2 * kK2Waves + 4 + 3) / 4 * 4 > 20 ? (4 + 2 * kK2Waves + 4 + 3) / 4 * 4 : 20;
 constexpr int kSeg = 65536;            // K3 segment length (positions)
 constexpr int kLdsBins = 16384;        // K3 LDS histogram bins (64 KiB)
 
@@ -1229,14 +1250,31 @@ long_fill_words_kernel(const uint32_t* __restrict__ ew, int64_t n, int64_t per, 
         const int64_t TB = m == ~0u ? 0 : (int64_t)(m / kTileW);
         int te[kE];     // window tile, or -1
         int rk[kE];     // rank in its tile
+        const int lane = threadIdx.x & 63;
+        const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
         for (int k = 0; k < kE; ++k) {
             te[k] = -1;
             rk[k] = 0;
-            if (e[k] == ~0u) continue;
-            const int64_t t = (int64_t)(e[k] / kTileW);
-            if (t - TB < kLongTileWin) {
-                te[k] = (int)(t - TB);
+            if (e[k] != ~0u) {
+                const int64_t t = (int64_t)(e[k] / kTileW);
+                if (t - TB < kLongTileWin) te[k] = (int)(t - TB);
+            }
+            if (MC_FILL_WAVE_COUNTS) {
+                // one LDS atomic per distinct tile of the wave (the lanes of
+                // a tile take consecutive ranks after the leader's add)
+                unsigned long long todo = __ballot(te[k] >= 0);
+                while (todo) {
+                    const int leader = __ffsll((long long)todo) - 1;
+                    const int tt = __builtin_amdgcn_readlane(te[k], leader);
+                    const unsigned long long m = __ballot(te[k] == tt);
+                    int base = 0;
+                    if (lane == leader) base = atomicAdd(&wt[tt], (int)__popcll(m));
+                    base = __builtin_amdgcn_readlane(base, leader);
+                    if (te[k] == tt) rk[k] = base + (int)__popcll(m & below);
+                    todo &= ~m;
+                }
+            } else if (te[k] >= 0) {
                 rk[k] = atomicAdd(&wt[te[k]], 1);
             }
         }
@@ -1513,8 +1551,8 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
     // 4-bit masks of this lane's reads: in [lo, hi) (applied) and in [vlo,
     // vhi) (checked here); the bounds relative to the batch are scalar
     auto range4 = [&](int64_t lo, int64_t hi) -> unsigned {
-        const int la = (int)(lo - base < -8 ? -8 : lo - base > kBatch + 8 ? kBatch + 8 : lo - base);
-        const int ha = (int)(hi - base < -8 ? -8 : hi - base > kBatch + 8 ? kBatch + 8 : hi - base);
+        const int la = (int)(lo - base < -8 ? -8 : lo - base > kK2Batch + 8 ? kK2Batch + 8 : lo - base);
+        const int ha = (int)(hi - base < -8 ? -8 : hi - base > kK2Batch + 8 ? kK2Batch + 8 : hi - base);
         const int ka = min(max(la - lane4, 0), 4), kz = min(max(ha - lane4, 0), 4);
         return ((1u << kz) - 1u) & ~((1u << ka) - 1u);
     };
@@ -1637,16 +1675,16 @@ __device__ __forceinline__ void direct_flush(const DirectAcc& a, const DT& D, in
     __syncthreads();
     if (lane == 0) {
         red[wave] = (int)f;
-        red[kWaves + wave] = m;
+        red[kK2Waves + wave] = m;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned ff = 0;
         int mm = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
+        for (int w = 0; w < kK2Waves; ++w) {
             ff |= (unsigned)red[w];
-            mm = max(mm, red[kWaves + w]);
+            mm = max(mm, red[kK2Waves + w]);
         }
         if (ff) atomicOr(&D.dres[kDresFlags], (unsigned long long)ff);
         if (mm > 0) atomicMax(&D.dres[kDresMaxSpan], (unsigned long long)mm);
@@ -1890,15 +1928,21 @@ __device__ __forceinline__ void hist_int4(unsigned* h, int dummy, OvReg& ovr, in
 // next call uses the other, so a wave running ahead never overwrites a word
 // another wave still reads).  __syncthreads_and compiled to three barriers
 // and an LDS atomic for one predicate.
-static_assert(kWaves == 4, "block_all2 packs one byte per wave into a word");
+// (words: two 8-byte words; one byte per wave, up to 8 waves)
 __device__ __forceinline__ void block_all2(int* words, int& flip, bool p0, bool p1, int wave, int lane,
                                            bool& all0, bool& all1) {
     const int v = (__all(p0) ? 1 : 0) | (__all(p1) ? 2 : 0);
-    if (lane == 0) reinterpret_cast<unsigned char*>(words + flip)[wave] = (unsigned char)v;
+    if (lane == 0) reinterpret_cast<unsigned char*>(words + 2 * flip)[wave] = (unsigned char)v;
     __syncthreads();
-    const int w = words[flip];
-    all0 = (w & 0x01010101) == 0x01010101;
-    all1 = (w & 0x02020202) == 0x02020202;
+    if (kK2Waves == 4) {
+        const int w = words[2 * flip];
+        all0 = (w & 0x01010101) == 0x01010101;
+        all1 = (w & 0x02020202) == 0x02020202;
+    } else {
+        const unsigned long long w = *reinterpret_cast<const unsigned long long*>(words + 2 * flip);
+        all0 = (w & 0x0101010101010101ull) == 0x0101010101010101ull;
+        all1 = (w & 0x0202020202020202ull) == 0x0202020202020202ull;
+    }
     flip ^= 1;
 }
 
@@ -1946,7 +1990,7 @@ __device__ __forceinline__ void flush_region(const RT& R, int id, unsigned* h, O
         }
     }
     unsigned* g = R.hist + (int64_t)id * HC::kBins;
-    for (int k = threadIdx.x; k < HC::kBins; k += kBlock) {
+    for (int k = threadIdx.x; k < HC::kBins; k += kK2Block) {
         unsigned cnt = 0;
 #pragma unroll
         for (int c = 0; c < HC::kCopies; ++c) cnt += h[c * HC::kStride + k];
@@ -1998,7 +2042,7 @@ struct K2Consts {
 
 template <bool kStats, bool kLong, bool kDirect>
 // waves/SIMD minimum per variant (0 = unconstrained -> 1)
-__global__ void __launch_bounds__(kBlock, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
+__global__ void __launch_bounds__(kK2Block, kStats ? (MC_WAVES_STATS ? MC_WAVES_STATS : 1)
                                                  : (MC_WAVES_PLAIN ? MC_WAVES_PLAIN : 1))
 depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
              const int64_t* __restrict__ coff, const int64_t* __restrict__ chunk_first,
@@ -2012,7 +2056,8 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
     const auto& R = KC.R;
     const auto& D = KC.D;
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    // [0] chunk id, [4..7] wave totals, [8..11] wave max, [12..13] block_all votes
+    // [0] chunk id, [4, 4 + W) wave totals, [4 + W, 4 + 2W) wave max, then the
+    // block_all2 votes (kLdsHeader)
     int* hdr = lds;
     int and_flip = 0;
     int* ring = lds + kLdsHeader;
@@ -2025,7 +2070,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
     const int hist_dummy = HC::kBins + (lane / HC::kCopies) % HC::kPad;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform per wave
     const int64_t chunk_w = (int64_t)tiles_per_chunk * kTileW;
-    constexpr int kWaveSpan = kTileW / kWaves;       // 1024 positions per wave
+    constexpr int kWaveSpan = kTileW / kK2Waves;       // 1024 positions per wave
     constexpr int kChunks = kWaveSpan / (64 * 4);    // int4 per lane -> 4
     // Deferred tile stores (a tile's stores issued after the next tile's
     // apply loop), plain K2 only: with 12 B/read they gained plain C3 -2.4 %,
@@ -2044,7 +2089,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
     OvReg ovr;                 // kStats: this lane's out-of-window runs of the open region
     ov_reg_reset(ovr);
     if (kStats) {
-        for (int k = threadIdx.x; k < HC::kLds; k += kBlock) hist[k] = 0;
+        for (int k = threadIdx.x; k < HC::kLds; k += kK2Block) hist[k] = 0;
         if (threadIdx.x < kOvRecs) ov_reset(ovf + threadIdx.x);   // ordered by the first barrier
     }
 
@@ -2062,7 +2107,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
     // chunk (at most short_max = one tile) landed: every tile's own slots are
     // zeroed by its scan
     const int ring_tail = (int)(((int64_t)tiles_per_chunk * kTileW) % kRing);
-    for (int k = threadIdx.x * 4; k < kRing; k += kBlock * 4)
+    for (int k = threadIdx.x * 4; k < kRing; k += kK2Block * 4)
         *reinterpret_cast<i32x4*>(ring + k) = i32x4{0, 0, 0, 0};
     for (;;) {
         // (the barrier also orders the hdr write before the reads)
@@ -2122,7 +2167,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
         if (more) {
             RawBatch<kDirect> r0;
             issue_raw<kDirect>(r0, base, A, cend);
-            if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
+            if (kPf && base + kK2Batch < cend) issue_raw<kDirect>(nxt, base + kK2Batch, A, cend);
             finish(r0, base);
         }
         int carry = kLong ? uload(chunk_carry, c) : 0;
@@ -2208,23 +2253,31 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
                     }
                 }
                 bool all_done, ev_done;
-                block_all2(hdr + 12, and_flip, b.pending == 0, eb.pending == 0, wave, lane, all_done,
-                           ev_done);
+                if (MC_K2_WAVE_ADVANCE) {
+                    // each wave streams its own quarter of every batch (reads
+                    // base + 256 w ..): it advances as soon as its lanes are
+                    // done, no barrier; the tile scan's barrier orders the ring
+                    all_done = __all(b.pending == 0);
+                    ev_done = __all(eb.pending == 0);
+                } else {
+                    block_all2(hdr + 4 + 2 * kK2Waves, and_flip, b.pending == 0, eb.pending == 0, wave, lane,
+                               all_done, ev_done);
+                }
                 const bool adv_reads = all_done && more;
                 const bool adv_events = ev_done && ev_more;
                 if (!adv_reads && !adv_events) break;
                 if (adv_events) {
-                    ev_base += kBatch;
+                    ev_base += kK2Batch;
                     ev_more = ev_base < ev_hi;
                     if (ev_more) load_events(eb, tile_ev, ev_base, ev_lo, ev_hi);
                 }
                 if (adv_reads) {
-                    base += kBatch;
+                    base += kK2Batch;
                     more = base < cend;
                     if (more) {
                         if (!kPf) issue_raw<kDirect>(nxt, base, A, cend);
                         finish(nxt, base);   // loaded one batch ago
-                        if (kPf && base + kBatch < cend) issue_raw<kDirect>(nxt, base + kBatch, A, cend);
+                        if (kPf && base + kK2Batch < cend) issue_raw<kDirect>(nxt, base + kK2Batch, A, cend);
                     }
                 }
             }
@@ -2256,7 +2309,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
             __syncthreads();
             int off = carry, tile_total = 0;
 #pragma unroll
-            for (int w = 0; w < kWaves; ++w) {
+            for (int w = 0; w < kK2Waves; ++w) {
                 const int tw = hdr[4 + w];
                 if (w < wave) off += tw;
                 tile_total += tw;
@@ -2322,16 +2375,18 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
             if (rcur < R.n && r_gs < C0 + chunk_w) flush_region<false, HC>(R, r_id, hist, ovf);
         }
         if (threadIdx.x == 0) hdr[0] = kAhead ? ticket : take_chunk(queue, n_chunks);
-        for (int k = threadIdx.x * 4; k < kTileW; k += kBlock * 4)
+        for (int k = threadIdx.x * 4; k < kTileW; k += kK2Block * 4)
             *reinterpret_cast<i32x4*>(ring + ring_tail + k) = i32x4{0, 0, 0, 0};
     }
     // one atomic per workgroup (same-address atomics of every wave at the end of
     // the launch serialise); hdr[8..11] are free once the queue is drained
     my_max = wave_max(my_max);
-    if (lane == 0) hdr[8 + wave] = my_max;
+    if (lane == 0) hdr[4 + kK2Waves + wave] = my_max;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int m = max(max(hdr[8], hdr[9]), max(hdr[10], hdr[11]));
+        int m = 0;
+#pragma unroll
+        for (int w = 0; w < kK2Waves; ++w) m = max(m, hdr[4 + kK2Waves + w]);
         if (m > 0) atomicMax(max_depth, m);
     }
     if (kDirect) direct_flush(dacc, D, ring);   // (ring: free now)
