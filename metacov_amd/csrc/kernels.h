@@ -2281,6 +2281,9 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
                     }
                 }
             }
+            // (per-wave advance: every wave's ring adds for this tile are in
+            // before any wave reads its span of the tile)
+            if (MC_K2_WAVE_ADVANCE) __syncthreads();
             // the previous tile's depth, held in v since its scan: its stores go
             // out only now, so a vmcnt wait in the apply loop above (batch
             // advance) found them a whole tile phase old instead of just issued
