@@ -266,6 +266,7 @@ struct mc_ctx {
     DevBuf<RegionAcc> d_fb_acc;           // [kFbSlots]
     DevBuf<int32_t> d_fb_list;            // [kFbSlots]
     DevBuf<unsigned> d_fb_cnt;            // [2] (by call parity)
+    DevBuf<unsigned> d_kdone;             // [1] K3b's finished-workgroup count (0 between calls)
     int64_t fb_calls = 0;
     bool fb_recent = false;               // the last fused call had out-of-window regions
     int64_t device_recomputes = 0;
@@ -288,9 +289,10 @@ struct mc_ctx {
     static constexpr int kTimingSets = 4;
     TimingSet ts[kTimingSets];
     int ts_cur = 0;
-    // completion stamp: the stream writes done_seq into mapped host memory
-    // after a fused call's last kernel, and the host spins on it (a stream
-    // synchronize woke ~10 us after the last kernel's end)
+    // completion stamp: a fused call's K3b writes done_seq into mapped host
+    // memory when its last workgroup is done, and the host spins on it (a
+    // stream synchronize woke ~10 us after the last kernel's end; a stream
+    // write command after K3b cost ~13 us more)
     HostMapped<unsigned long long> h_done;
     unsigned long long done_seq = 0;
     bool stamp_ok = true;
@@ -397,6 +399,7 @@ extern "C" int mc_ctx_destroy(mc_ctx* ctx) {
     ctx->d_fb_acc.release();
     ctx->d_fb_list.release();
     ctx->d_fb_cnt.release();
+    ctx->d_kdone.release();
     for (auto ev : ctx->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto& T : ctx->ts)
@@ -602,9 +605,17 @@ extern "C" int mc_clear_reads(mc_ctx* ctx) {
     return MC_OK;
 }
 
+// MC_STEP_EVENTS 0: a fused call records no timing events (A/B of their
+// cost only: its kernel times then read 0)
+#ifndef MC_STEP_EVENTS
+#define MC_STEP_EVENTS 1
+#endif
 static float elapsed(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();   // (not a stream error: keep it out of the next launch check)
+        return 0.f;
+    }
     return ms;
 }
 
@@ -950,7 +961,7 @@ static int prepare_direct(mc_ctx* ctx) {
     if (int rc = run_k1(ctx)) return rc;
     // the prepare's span: this event to K2's start event (probe + window)
     auto& T = ctx->ts[ctx->ts_cur];
-    HIP_TRY(hipEventRecord(T.e[0], s));
+    if (MC_STEP_EVENTS) HIP_TRY(hipEventRecord(T.e[0], s));
     T.prep = true;
     ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
@@ -1171,7 +1182,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 32, s));
         HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
     }
-    HIP_TRY(hipEventRecord(ea ? ea : ctx->ev[4], s));
+    if (MC_STEP_EVENTS || !ea) HIP_TRY(hipEventRecord(ea ? ea : ctx->ev[4], s));
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
@@ -1208,7 +1219,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     }
 #undef MC_LAUNCH_K2
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(eb ? eb : ctx->ev[5], s));
+    if (MC_STEP_EVENTS || !eb) HIP_TRY(hipEventRecord(eb ? eb : ctx->ev[5], s));
     ctx->t_depth = ea == nullptr;   // else the caller's set carries the time
     ctx->t.depth_launches += 1;
     ctx->depth_valid = true;
@@ -1456,6 +1467,22 @@ static int direct_verdict_sync(mc_ctx* ctx) {
 // Waits until the stream has written stamp `seq` (spinning on mapped host
 // memory; a stream query every ~1k spins reports a failed stream), or, where
 // the stream cannot write stamps, for the stream to drain.
+// How a fused call learns that its last kernel is done (MC_DONE_MODE):
+// 0 a stream write command after it writes the stamp; 1 K3b's last
+// workgroup writes the stamp (grid_done_stamp) when K3b is the call's last
+// kernel, else as 0; 2 the host polls the event recorded after it.
+#ifndef MC_DONE_MODE
+#define MC_DONE_MODE 1
+#endif
+static int wait_event_spin(hipEvent_t ev) {
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return MC_OK;
+        if (e != hipErrorNotReady) HIP_TRY(e);
+        __builtin_ia32_pause();
+    }
+}
+
 static int wait_stamp(mc_ctx* ctx, unsigned long long seq) {
     if (!ctx->stamp_ok) {
         HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1532,6 +1559,21 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     if (nf == 0) fr.n = 0;
     auto& T = ctx->ts[ctx->ts_cur];
     if (int rc = launch_depth(ctx, fr, T.e[1], T.e[2])) return rc;
+    // the completion stamp (MC_DONE_MODE 0 / 1)
+    const unsigned long long seq = ++ctx->done_seq;
+    unsigned long long* stamp = nullptr;
+    if (ctx->stamp_ok) {
+        if (!ctx->h_done.h) {
+            if (ctx->h_done.reserve(1) != hipSuccess || ctx->d_kdone.reserve(1) != hipSuccess ||
+                hipMemsetAsync(ctx->d_kdone.p, 0, sizeof(unsigned), s) != hipSuccess) {
+                (void)hipGetLastError();
+                ctx->stamp_ok = false;
+            } else {
+                __atomic_store_n(ctx->h_done.h, 0ull, __ATOMIC_RELEASE);
+            }
+        }
+        if (ctx->stamp_ok && MC_DONE_MODE == 1) stamp = ctx->h_done.d;
+    }
     // K3b: its span is timed from K2's end event (one event fewer per call)
     // the device-side recompute of out-of-window regions: on for long reads
     // (deep contigs with long end ramps) and after a call that had them
@@ -1577,7 +1619,8 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
                        verdict ? ctx->d_dres.p : nullptr, verdict ? fflag_dres(ctx->h_fflag.d, R) : nullptr, \
                        devfb ? F.cnt + F.parity : nullptr, devfb ? F.list : nullptr,                \
                        ctx->direct ? direct_window(ctx) : DirectWindow{},                          \
-                       ctx->direct ? reinterpret_cast<const int32_t*>(d + L.rtid) : nullptr)
+                       ctx->direct ? reinterpret_cast<const int32_t*>(d + L.rtid) : nullptr,           \
+                       ctx->d_kdone.p, devfb ? nullptr : stamp, seq)
     if (vals == HistCfg<false>::kBins) MC_LAUNCH_K3B(HistCfg<false>::kBins);
     else MC_LAUNCH_K3B(HistCfg<true>::kBins);
 #undef MC_LAUNCH_K3B
@@ -1588,25 +1631,17 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         hipLaunchKernelGGL(fb_final_kernel, dim3(kFbSlots), dim3(kBlock), 0, s, F);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(T.e[3], s));
+    if (MC_STEP_EVENTS) HIP_TRY(hipEventRecord(T.e[3], s));
+    if ((MC_DONE_MODE == 0 || (MC_DONE_MODE == 1 && devfb)) && ctx->stamp_ok && hipStreamWriteValue64(s, ctx->h_done.d, seq, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->stamp_ok = false;
+    }
     ctx->t_stats = false;
     ctx->t.stats_launches += 1;
-    // the flags are in host memory once the stream has passed K3b (no copy
-    // command): the completion stamp after it, while the previous call's
-    // event times are read
-    const unsigned long long seq = ++ctx->done_seq;
-    if (ctx->stamp_ok) {
-        if (!ctx->h_done.h) {
-            HIP_TRY(ctx->h_done.reserve(1));
-            __atomic_store_n(ctx->h_done.h, 0ull, __ATOMIC_RELEASE);
-        }
-        if (hipStreamWriteValue64(s, ctx->h_done.d, seq, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            ctx->stamp_ok = false;
-        }
-    }
+    // the flags are in host memory once K3b's stamp is (no copy command);
+    // the previous call's event times are read meanwhile
     resolve_timings(ctx, false);
-    if (int rc = wait_stamp(ctx, seq)) return rc;
+    if (int rc = MC_DONE_MODE == 2 ? wait_event_spin(T.e[3]) : wait_stamp(ctx, seq)) return rc;
     const int* flags = ctx->h_fflag.h;
     if (verdict && !check_direct(ctx, fflag_dres(ctx->h_fflag.h, R), true)) {
         direct_fallback(ctx, fflag_dres(ctx->h_fflag.h, R));

@@ -2761,6 +2761,35 @@ struct FbArgs {
     RegionOut* out;                    // the call's rows
 };
 
+// The last workgroup of the grid to get here writes seq to *stamp (mapped
+// host memory): the host learns that a call's last kernel is done without a
+// stream write command after it (~13 us per call: the command's own dispatch
+// and the gap before it, C2 trace r05i).  The kernel's results that others
+// read (rows, host flags) are written through to memory with system-scope
+// stores (store_sys), so each wave only waits for its own stores: no L2
+// write-back per workgroup (a system-scope fence per workgroup cost K3b
+// +1 us at C2's one workgroup and +20 us at C3's 250).  done_cnt: a device
+// counter, 0 between launches (the last workgroup resets it).  Every thread
+// of every workgroup calls this.
+__device__ __forceinline__ void grid_done_stamp(unsigned* done_cnt, unsigned long long* stamp,
+                                                unsigned long long seq) {
+    if (stamp == nullptr) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(done_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(done_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(stamp, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+template <class T>
+__device__ __forceinline__ void store_sys(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(kBlock)
 fb_seg_kernel(FbArgs F) {
     extern __shared__ __attribute__((aligned(16))) unsigned hb[];
@@ -2807,8 +2836,7 @@ fb_seg_kernel(FbArgs F) {
     }
 }
 
-__global__ void __launch_bounds__(kBlock)
-fb_final_kernel(FbArgs F) {
+__device__ __forceinline__ void fb_final_row(const FbArgs& F) {
     if (blockIdx.x == 0 && threadIdx.x == 0) F.cnt[F.parity ^ 1] = 0;   // the next call's counter
     const int n = (int)min(F.cnt[F.parity], (unsigned)kFbSlots);
     const int maxd = *F.max_depth;
@@ -2826,6 +2854,11 @@ fb_final_kernel(FbArgs F) {
     }
 }
 
+__global__ void __launch_bounds__(kBlock)
+fb_final_kernel(FbArgs F) {
+    fb_final_row(F);
+}
+
 // The fused path's finalize: one wave per region (4 per workgroup) over its
 // kHistBins-bin window, the same rules as region_final_kernel with base_of,
 // low_of and hist_stats set and no row scatter.  A 256-thread block per
@@ -2834,26 +2867,26 @@ fb_final_kernel(FbArgs F) {
 // also copies K2's max depth to max_out (mapped host memory: the fallback
 // path needs it without a device-to-host copy).
 template <int kVals>
-__global__ void __launch_bounds__(kBlock)
-region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
-                         RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
-                         const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
-                         int* __restrict__ fallback, const int32_t* __restrict__ base_of,
-                         unsigned* __restrict__ low_of, int* __restrict__ max_depth,
-                         int* __restrict__ max_out, unsigned* __restrict__ queue,
-                         const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out,
-                         unsigned* __restrict__ fb_cnt, int32_t* __restrict__ fb_list,
-                         DirectWindow dwin, const int32_t* __restrict__ rtid) {
+__device__ __forceinline__ void
+final_wave_row(unsigned* __restrict__ hist, int64_t R,
+               RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
+               const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
+               int* __restrict__ fallback, const int32_t* __restrict__ base_of,
+               unsigned* __restrict__ low_of, int* __restrict__ max_depth,
+               int* __restrict__ max_out, unsigned* __restrict__ queue,
+               const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out,
+               unsigned* __restrict__ fb_cnt, int32_t* __restrict__ fb_list,
+               DirectWindow dwin, const int32_t* __restrict__ rtid, bool wt) {
     constexpr int kFinPer = (kVals + 63) / 64;
     const int lane = threadIdx.x & 63;
     // dres_out (mapped host memory): the direct K2's validation counters, so
     // the host reads its verdict with the flags, without a copy command
-    if (blockIdx.x == 0 && dres_out && threadIdx.x < kDresWords) dres_out[threadIdx.x] = dres_in[threadIdx.x];
+    if (blockIdx.x == 0 && dres_out && threadIdx.x < kDresWords) store_sys(dres_out + threadIdx.x, dres_in[threadIdx.x]);
     // queue != null: leave the fused buffers as fused_init_kernel does (zero
     // histograms and below-window counts, initial accumulators, K2's queue
     // and max depth), so a repeated call on the same regions skips that launch
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (max_out) *max_out = *max_depth;
+        if (max_out) store_sys(max_out, *max_depth);
         if (queue) {
             for (int k = 0; k < 4; ++k) max_depth[k] = 0;
             for (int k = 0; k < 8; ++k) queue[k] = 0;
@@ -2933,7 +2966,7 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
     if (lane != 0) return;
     const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
     const bool fb = n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi);
-    fallback[r] = fb ? 1 : 0;
+    store_sys(fallback + r, fb ? 1 : 0);
     if (fb && fb_cnt) {   // listed for the device-side recompute (fb_seg_kernel)
         const unsigned slot = atomicAdd(fb_cnt, 1u);
         if (slot < (unsigned)kFbSlots) fb_list[slot] = (int32_t)r;
@@ -2969,7 +3002,34 @@ region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
         o.sum = 0;
         o.sumsq = 0;
     }
-    out[r] = o;
+    if (wt) {   // written through: visible to the host and other streams once stored
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(out + r);
+        const unsigned long long* v = reinterpret_cast<const unsigned long long*>(&o);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(RegionOut) / 8); ++k) store_sys(w + k, v[k]);
+    } else {
+        out[r] = o;
+    }
+}
+
+// stamp != null (the call's last kernel): grid_done_stamp after the rows,
+// flags, K2's max depth and verdict copy.
+template <int kVals>
+__global__ void __launch_bounds__(kBlock)
+region_final_wave_kernel(unsigned* __restrict__ hist, int64_t R,
+                         RegionAcc* __restrict__ acc, const int64_t* __restrict__ n_total,
+                         const int64_t* __restrict__ n_zero_extra, RegionOut* __restrict__ out,
+                         int* __restrict__ fallback, const int32_t* __restrict__ base_of,
+                         unsigned* __restrict__ low_of, int* __restrict__ max_depth,
+                         int* __restrict__ max_out, unsigned* __restrict__ queue,
+                         const unsigned long long* __restrict__ dres_in, unsigned long long* __restrict__ dres_out,
+                         unsigned* __restrict__ fb_cnt, int32_t* __restrict__ fb_list,
+                         DirectWindow dwin, const int32_t* __restrict__ rtid,
+                         unsigned* __restrict__ done_cnt, unsigned long long* __restrict__ stamp,
+                         unsigned long long seq) {
+    final_wave_row<kVals>(hist, R, acc, n_total, n_zero_extra, out, fallback, base_of, low_of, max_depth,
+                          max_out, queue, dres_in, dres_out, fb_cnt, fb_list, dwin, rtid, stamp != nullptr);
+    grid_done_stamp(done_cnt, stamp, seq);
 }
 
 }  // namespace mc

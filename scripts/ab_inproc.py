@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--reads", type=int, default=100_000_000)
     ap.add_argument("--contigs", type=int, default=None, help="(c3) contigs, e.g. a strong-scaling shard")
     ap.add_argument("--nocheck", action="store_true", help="deliberately-wrong experiment builds")
+    ap.add_argument("--loop", action="store_true", help="direct mode: also time back-to-back calls into a device table")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     a = ap.parse_args()
     import torch
@@ -76,6 +77,25 @@ def main():
                 elif not a.nocheck:
                     for f in rows.dtype.names:
                         assert np.array_equal(rows[f], ref_rows[f]), (lib, f)
+        if mode == "direct" and a.loop:
+            # bench-like: back-to-back fresh-batch calls into a device table,
+            # one synchronize per round (host gaps between calls included)
+            import torch
+            tbl = torch.empty((len(rt), 9), dtype=torch.int64, device="cuda")
+            loops = {lib: [] for lib in a.libs}
+            for _ in range(a.rounds):
+                for lib, e in zip(a.libs, engines):
+                    e.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(a.steps):
+                        e.invalidate()
+                        e.compute_depth_stats_device(rt, rs, re_, tbl.data_ptr())
+                    e.synchronize()
+                    loops[lib].append((time.perf_counter() - t0) * 1e3 / a.steps)
+            for lib in a.libs:
+                l = np.array(loops[lib])
+                print("loop   %-48s per call median %.4f ms  min %.4f ms  (rounds %d x %d calls)"
+                      % (os.path.basename(lib), np.median(l), l.min(), len(l), a.steps), flush=True)
         for lib in a.libs:
             t = np.array(times[lib])
             w = np.array(walls[lib])
