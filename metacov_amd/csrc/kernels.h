@@ -2881,12 +2881,21 @@ final_wave_row(unsigned* __restrict__ hist, int64_t R,
     const int lane = threadIdx.x & 63;
     // dres_out (mapped host memory): the direct K2's validation counters, so
     // the host reads its verdict with the flags, without a copy command
-    if (blockIdx.x == 0 && dres_out && threadIdx.x < kDresWords) store_sys(dres_out + threadIdx.x, dres_in[threadIdx.x]);
+    // (wt: the call's last kernel, stamping: its host-visible results are
+    // written through with system-scope stores; those cost K3b 3x at C5's
+    // 10 k regions, so only then)
+    if (blockIdx.x == 0 && dres_out && threadIdx.x < kDresWords) {
+        if (wt) store_sys(dres_out + threadIdx.x, dres_in[threadIdx.x]);
+        else dres_out[threadIdx.x] = dres_in[threadIdx.x];
+    }
     // queue != null: leave the fused buffers as fused_init_kernel does (zero
     // histograms and below-window counts, initial accumulators, K2's queue
     // and max depth), so a repeated call on the same regions skips that launch
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (max_out) store_sys(max_out, *max_depth);
+        if (max_out) {
+            if (wt) store_sys(max_out, *max_depth);
+            else *max_out = *max_depth;
+        }
         if (queue) {
             for (int k = 0; k < 4; ++k) max_depth[k] = 0;
             for (int k = 0; k < 8; ++k) queue[k] = 0;
@@ -2966,7 +2975,8 @@ final_wave_row(unsigned* __restrict__ hist, int64_t R,
     if (lane != 0) return;
     const long long win_lo = low, win_hi = low + in_hist;   // ranks held by the window
     const bool fb = n > 0 && (r_lo < win_lo || r_hi >= win_hi || q_lo < win_lo || q_hi - 1 >= win_hi);
-    store_sys(fallback + r, fb ? 1 : 0);
+    if (wt) store_sys(fallback + r, fb ? 1 : 0);
+    else fallback[r] = fb ? 1 : 0;
     if (fb && fb_cnt) {   // listed for the device-side recompute (fb_seg_kernel)
         const unsigned slot = atomicAdd(fb_cnt, 1u);
         if (slot < (unsigned)kFbSlots) fb_list[slot] = (int32_t)r;
