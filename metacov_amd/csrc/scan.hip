@@ -63,6 +63,28 @@
 
 namespace {
 
+#ifndef MC_SCAN_CUT
+#define MC_SCAN_CUT 1
+#endif
+#ifndef MC_SCAN_PAIRS
+#define MC_SCAN_PAIRS 1
+#endif
+#ifndef MC_SCAN_DYN
+#define MC_SCAN_DYN 1
+#endif
+#ifndef MC_SCAN_SLICE
+#define MC_SCAN_SLICE 256
+#endif
+constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SCAN_DYN)
+#ifndef MC_SCAN_NOL0
+#define MC_SCAN_NOL0 0
+#endif
+// A/B of the scan kernel's parts (wrong results): 1 no BaseHist counting,
+// 2 no mismatch test on the staged path
+#ifndef MC_SCAN_EXP
+#define MC_SCAN_EXP 0
+#endif
+
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kLdsWords = 8192;     // histogram arena: 32 KiB
@@ -82,7 +104,8 @@ struct ScanArgs {
     const int64_t* seq_off;
     const uint8_t* seq;
     int64_t n;
-    int64_t per_wave;         // reads per wave (a multiple of 64)
+    int64_t per_wave;         // reads per slice (a multiple of 64)
+    unsigned* work;           // the slice queue (0 at launch), or null: one static slice per wave
     const uint8_t* ref;       // nt4 codes, all sequences back to back (padded both ends)
     const int64_t* ref_off;
     const int64_t* ref_len;
@@ -245,7 +268,8 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
         // the exit the staged-window loop has no loop-carried branch and its
         // LDS reads of several words are in flight together.
         int mism = 0;
-        if (fast) {
+        if (fast && MC_SCAN_EXP == 2) {
+        } else if (fast) {
 #pragma unroll 4
             for (int k = 0; k < nw; ++k) {
                 const uint32_t w = s32[k];
@@ -303,6 +327,26 @@ typedef __attribute__((address_space(3))) const uint64_t lds_cu64;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 constexpr int kIncTabWords = 64;   // 32 u64: nibble -> packed-counter increment, forward then reverse
 
+// A batch whose passing reads are in several groups (or with BaseHist in
+// global memory): each lane counts its own read.
+__device__ __forceinline__ void count_bases_lanes(const ScanArgs& a, bool pending, int rlen, int fl, int g,
+                                                  int soff, lds_u32* sseq, lds_u32* lds) {
+    if (!pending) return;
+    const int rowstride = a.G * 5;
+    lds_cu8* s = (lds_cu8*)(sseq + soff);
+    const bool rev = (fl & 0x10) != 0;
+    for (int j = 0; j < rlen; ++j) {
+        const uint32_t byte = s[j >> 1];
+        int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
+        int x = j;
+        if (rev) {
+            v = comp4(v);
+            x = rlen - 1 - j;
+        }
+        inc(lds + a.lds_base, a.base, (int64_t)(x + a.base_start) * rowstride + g * 5 + v, a.base_lds);
+    }
+}
+
 __device__ __forceinline__ void count_bases(lds_cu64* inc_tab, const ScanArgs& a, int64_t r, bool pending, bool act,
                                             int soff, lds_u32* sseq, lds_u32* lds, int lane) {
     uint64_t pend = __ballot(pending);
@@ -315,21 +359,7 @@ __device__ __forceinline__ void count_bases(lds_cu64* inc_tab, const ScanArgs& a
     const int g0 = __builtin_amdgcn_readlane(g, first);
     const int rowstride = a.G * 5;
     if (!a.base_lds || __ballot(pending && g != g0)) {
-        if (pending) {
-            lds_cu8* s = (lds_cu8*)(sseq + soff);
-            const bool rev = (fl & 0x10) != 0;
-            for (int j = 0; j < rlen; ++j) {
-                const uint32_t byte = s[j >> 1];
-                int v = nt4_of((j & 1) ? (byte & 15u) : (byte >> 4));
-                int x = j;
-                if (rev) {
-                    v = comp4(v);
-                    x = rlen - 1 - j;
-                }
-                inc(lds + a.lds_base, a.base, (int64_t)(x + a.base_start) * rowstride + g * 5 + v,
-                    a.base_lds);
-            }
-        }
+        count_bases_lanes(a, pending, rlen, fl, g, soff, sseq, lds);
         return;
     }
     uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
@@ -401,6 +431,123 @@ __device__ __forceinline__ void count_bases(lds_cu64* inc_tab, const ScanArgs& a
     }
 }
 
+// BaseHist counts, two positions per lane (MC_SCAN_PAIRS).  Lane L owns the
+// read-position pairs P = L and P = 64 + L: one LDS byte holds a pair's two
+// bases, and one 8-byte table entry (pair_tab) both positions' increments as
+// 8-bit A/C/G/T counters in a dword each; N is the position's coverage less
+// the four.  The reads are counted in BAM orientation: a read set of one
+// group is walked forward strand first (position x = base j), then per
+// length L the reverse-strand reads of that length, whose counts land at x =
+// L-1-j, complemented, when the set's counters are flushed.  So every read
+// costs a byte load, a table load and a 64-bit add per 128 positions, with no
+// per-read strand arithmetic (the one-position-per-lane walk, count_bases,
+// spent ~100 instructions per read).  A batch has at most 64 reads: no 8-bit
+// counter overflows before its flush.
+constexpr int kPairTabWords = 256 * 2;   // 256 u64
+
+__device__ __forceinline__ uint32_t inc8(int v) { return v < 4 ? 1u << (8 * v) : 0u; }
+
+__device__ __forceinline__ void pair_tab_init(lds_u64* tab) {
+    for (int i = threadIdx.x; i < 256; i += kThreads) {
+        // the high nibble is the even base
+        tab[i] = (uint64_t)inc8(nt4_of((uint32_t)i >> 4)) | ((uint64_t)inc8(nt4_of((uint32_t)i & 15u)) << 32);
+    }
+}
+
+// Counts of the reads in `set` (lane mask; each read's length in rlen, its
+// first staged dword in soff) at base pairs P = lane (acc0) and 64 + lane
+// (acc1), two reads per step so their loads are in flight together.
+__device__ __forceinline__ void count_set(lds_cu64* tab, uint64_t set, int rlen, int soff, lds_u32* sseq, int lane,
+                                          uint64_t& acc0, uint32_t& cov0, uint64_t& acc1, uint32_t& cov1) {
+    auto one = [&](int len, lds_cu8* sp, int P, uint64_t& acc, uint32_t& cov) {
+        const bool ok0 = 2 * P < len, ok1 = 2 * P + 1 < len;
+        const uint64_t v = tab[sp[ok0 ? P : 0]];
+        acc += v & (ok0 ? (ok1 ? ~0ull : 0xffffffffull) : 0ull);
+        cov += (ok0 ? 1u : 0u) + (ok1 ? 0x10000u : 0u);
+    };
+    while (set) {
+        const int l = __builtin_ctzll(set);
+        set &= set - 1;
+        const bool two = set != 0;
+        const int l2 = two ? __builtin_ctzll(set) : l;
+        if (two) set &= set - 1;
+        const int len = __builtin_amdgcn_readlane(rlen, l);
+        const int len2 = two ? __builtin_amdgcn_readlane(rlen, l2) : 0;
+        lds_cu8* s = (lds_cu8*)(sseq + __builtin_amdgcn_readlane(soff, l));
+        lds_cu8* s2 = (lds_cu8*)(sseq + __builtin_amdgcn_readlane(soff, l2));
+        one(len, s, lane, acc0, cov0);
+        one(len2, s2, lane, acc0, cov0);
+        if (max(len, len2) > 128) {
+            one(len, s, 64 + lane, acc1, cov1);
+            one(len2, s2, 64 + lane, acc1, cov1);
+        }
+    }
+}
+
+// Adds base pair P's counts (c, cov) to the rows of group g0: forward
+// (rlen_rev < 0) at positions 2P, 2P+1; reverse at rlen_rev-1-2P and
+// rlen_rev-2-2P, complemented.  Zeroes (c, cov).
+__device__ __forceinline__ void flush_pair(const ScanArgs& a, lds_u32* lds, int g0, int P, int rlen_rev,
+                                           uint64_t& c, uint32_t& cov) {
+    if (cov) {
+        const int rowstride = a.G * 5;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t n = (cov >> (16 * h)) & 0xFFFFu;
+            if (!n) continue;
+            const uint32_t w = (uint32_t)(c >> (32 * h));
+            const int j = 2 * P + h;
+            const int x = rlen_rev < 0 ? j : rlen_rev - 1 - j;
+            lds_u32* row = lds + a.lds_base + (x + a.base_start) * rowstride + g0 * 5;
+            uint32_t sum = 0;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint32_t k = (w >> (8 * v)) & 0xFFu;
+                sum += k;
+                if (k) __hip_atomic_fetch_add(row + (rlen_rev < 0 ? v : 3 - v), k, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (n > sum) __hip_atomic_fetch_add(row + 4, n - sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    c = 0;
+    cov = 0;
+}
+
+__device__ __forceinline__ void count_bases_pairs(lds_cu64* tab, const ScanArgs& a, int64_t r, bool pending,
+                                                  bool act, int soff, lds_u32* sseq, lds_u32* lds, int lane) {
+    uint64_t pend = __ballot(pending);
+    if (!pend) return;
+    const int32_t rlen = act ? a.rlen[r] : 0;
+    const int32_t fl = act ? a.flag[r] : 0;
+    int g = 0;
+    for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
+    if (!a.base_lds || __ballot(pending && rlen > 256)) {   // BaseHist in global memory, or long reads
+        count_bases_lanes(a, pending, rlen, fl, g, soff, sseq, lds);
+        return;
+    }
+    const uint64_t rev = __ballot((fl & 0x10) != 0);
+    uint64_t c0 = 0, c1 = 0;
+    uint32_t v0 = 0, v1 = 0;
+    while (pend) {   // per group of the batch's passing reads (one, normally)
+        const int g0 = __builtin_amdgcn_readlane(g, __builtin_ctzll(pend));
+        const uint64_t set = pend & __ballot(g == g0);
+        pend &= ~set;
+        count_set(tab, set & ~rev, rlen, soff, sseq, lane, c0, v0, c1, v1);
+        flush_pair(a, lds, g0, lane, -1, c0, v0);
+        flush_pair(a, lds, g0, 64 + lane, -1, c1, v1);
+        uint64_t rs = set & rev;
+        while (rs) {   // reverse strand, per read length (one, normally)
+            const int L = __builtin_amdgcn_readlane(rlen, __builtin_ctzll(rs));
+            const uint64_t same = rs & __ballot(rlen == L);
+            rs &= ~same;
+            count_set(tab, same, rlen, soff, sseq, lane, c0, v0, c1, v1);
+            flush_pair(a, lds, g0, lane, L, c0, v0);
+            flush_pair(a, lds, g0, 64 + lane, L, c1, v1);
+        }
+    }
+}
+
 // Reference positions a read's BaseHist / MirrorHist may read: [lo, hi).
 __device__ __forceinline__ void ref_span(const ScanArgs& a, int64_t r, int64_t& lo, int64_t& hi) {
     const int32_t rlen = a.rlen[r], gpos = a.gpos[r];
@@ -425,10 +572,6 @@ __device__ __forceinline__ void ref_span(const ScanArgs& a, int64_t r, int64_t& 
     }
 }
 
-__device__ __forceinline__ int64_t wave_min(int64_t v) {
-    for (int d = 32; d > 0; d >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, d, 64));
-    return v;
-}
 __device__ __forceinline__ int64_t wave_max(int64_t v) {
     for (int d = 32; d > 0; d >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, d, 64));
     return v;
@@ -451,98 +594,139 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
         const int v = nt4_of(threadIdx.x & 15u);
         inc_tab[threadIdx.x] = 1ull << (12 * (threadIdx.x < 16 ? v : comp4(v)));
     }
+    lds_u64* pair_tab = inc_tab + kIncTabWords / 2;
+    if (MC_SCAN_PAIRS) pair_tab_init(pair_tab);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     lds_u32* sseq = lds + a.stage_off + wave * (kStageBytes / 4);
     lds_u32* sref = sseq + (kSeqStage + kStagePad) / 4;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
-    int64_t r0 = gw * a.per_wave;
-    const int64_t rend = min(a.n, r0 + a.per_wave);
-    while (r0 < rend) {
-        const int64_t r = r0 + lane;
-        const bool valid = r < rend;
-        const int64_t so = valid ? a.seq_off[r] : 0, se = valid ? a.seq_off[r + 1] : 0;
-        if (valid && (so & 3)) atomicOr(a.error, 1);
-        const int64_t base = __shfl((long long)so, 0, 64);
-        const uint64_t fit = __ballot(valid && se - base <= kSeqStage);
-        const int m = fit == ~0ull ? 64 : __builtin_ctzll(~fit);
-        if (m == 0) {   // the first read alone exceeds the stage: global path
-            if (lane == 0) {
-                const int32_t rid = a.ref_id[r];
-                RefWin rw{nullptr, 0, nullptr, 0, 0};
-                if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
-                process_read(a, r, a.seq + so, reinterpret_cast<const uint32_t*>(a.seq + so), rw,
-                             lds, false, false);
-            }
-            r0 += 1;
-            continue;
+    // work != null: each wave takes slices of per_wave reads from a queue
+    // (a static slice per wave left the kernel waiting on the waves whose
+    // slices cover sparse stretches: many short batches); else slice gw
+    for (int64_t c = gw;;) {
+        if (a.work) {
+            unsigned t = 0;
+            if (lane == 0) t = atomicAdd(a.work, 1u);
+            c = __shfl((int)t, 0, 64);
         }
-        const bool act = lane < m;
-        const int64_t end = __shfl((long long)se, m - 1, 64);
-        // stage the batch's bases
-        const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.seq + (base & ~int64_t(3)));
-        const int nwd = (int)((end - (base & ~int64_t(3)) + 3) >> 2);
-        for (int i = lane; i < nwd; i += 64) sseq[i] = g32[i];
-        // the reference window, when the batch shares one sequence
-        const int32_t rid = act ? a.ref_id[r] : -1;
-        const int32_t rid0 = __shfl(rid, 0, 64);
-        const bool one_ref = __ballot(act && rid != rid0) == 0 && rid0 >= 0 && rid0 < a.n_ref;
-        RefWin rw{nullptr, 0, nullptr, 0, 0};
-        if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
-        if (one_ref) {
-            int64_t lo, hi;
+        int64_t r0 = c * a.per_wave;
+        if (r0 >= a.n) break;
+        const int64_t rend = min(a.n, r0 + a.per_wave);
+        while (r0 < rend) {
+            const int64_t r = r0 + lane;
+            const bool valid = r < rend;
+            const int64_t so = valid ? a.seq_off[r] : 0, se = valid ? a.seq_off[r + 1] : 0;
+            if (valid && (so & 3)) atomicOr(a.error, 1);
+            const int64_t base = __shfl((long long)so, 0, 64);
+            const uint64_t fit = __ballot(valid && se - base <= kSeqStage);
+            const int m_seq = fit == ~0ull ? 64 : __builtin_ctzll(~fit);
+            // the batch also ends where its reads leave lane 0's sequence or the
+            // reference window they touch outgrows kRefStage (inclusive prefix
+            // min / max of the reads' spans): a batch over a sparse stretch of a
+            // contig used to leave the window unstaged and every base of its
+            // reads to global loads (scan C3: 1/3 of the launch)
+            const int32_t ridv = valid ? a.ref_id[r] : -1;
+            const int32_t rid0 = __shfl(ridv, 0, 64);
+            const bool rid0_ok = rid0 >= 0 && rid0 < a.n_ref;
+            int64_t plo = INT64_MAX, phi = INT64_MIN;
+            if (valid && rid0_ok) ref_span(a, r, plo, phi);
+    #pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t ol = __shfl_up((long long)plo, d, 64), oh = __shfl_up((long long)phi, d, 64);
+                if (lane >= d) {
+                    plo = min(plo, ol);
+                    phi = max(phi, oh);
+                }
+            }
+    #if MC_SCAN_NOL0
+            const int64_t L0 = INT64_MAX;
+    #else
+            const int64_t L0 = rid0_ok ? a.ref_len[rid0] : 0;
+    #endif
+            const int64_t cwlo = max<int64_t>(plo, 0), cwhi = min<int64_t>(phi, L0);
+            const bool wfit = rid0_ok ? ridv == rid0 && (cwhi <= cwlo || cwhi - cwlo <= kRefStage)
+                                      : (ridv < 0 || ridv >= a.n_ref);
+            const uint64_t wf = __ballot(valid && wfit);
+            const int m_ref = wf == ~0ull ? 64 : __builtin_ctzll(~wf);
+            int m = m_seq == 0 ? 0 : MC_SCAN_CUT == 1 ? min(m_seq, max(m_ref, 1)) : m_seq;
+            if (MC_SCAN_CUT == 2 && m_ref == 0 && phi == 12345 && m > 1) m = 1;   // (A/B: computed, not applied)
+            if (m == 0) {   // the first read alone exceeds the stage: global path
+                if (lane == 0) {
+                    const int32_t rid = a.ref_id[r];
+                    RefWin rw{nullptr, 0, nullptr, 0, 0};
+                    if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
+                    process_read(a, r, a.seq + so, reinterpret_cast<const uint32_t*>(a.seq + so), rw,
+                                 lds, false, false);
+                }
+                r0 += 1;
+                continue;
+            }
+            const bool act = lane < m;
+            const int64_t end = __shfl((long long)se, m - 1, 64);
+            // stage the batch's bases
+            const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.seq + (base & ~int64_t(3)));
+            const int nwd = (int)((end - (base & ~int64_t(3)) + 3) >> 2);
+            for (int i = lane; i < nwd; i += 64) sseq[i] = g32[i];
+            // the reference window, when the batch shares one sequence (the
+            // prefix span at its last read)
+            const int32_t rid = act ? ridv : -1;
+            const bool one_ref = __ballot(act && rid != rid0) == 0 && rid0_ok;
+            RefWin rw{nullptr, 0, nullptr, 0, 0};
+            if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
+            if (one_ref) {
+                const int64_t L = a.ref_len[rid0];
+                const int64_t wlo = max<int64_t>(__shfl((long long)plo, m - 1, 64), 0);
+                const int64_t whi = min<int64_t>(__shfl((long long)phi, m - 1, 64), L);
+                if (whi > wlo && whi - wlo <= kRefStage) {
+                    const uint8_t* gref = a.ref + a.ref_off[rid0];
+                    const uintptr_t ga = reinterpret_cast<uintptr_t>(gref + wlo);
+                    const uint32_t* q = reinterpret_cast<const uint32_t*>(ga & ~uintptr_t(3));
+                    const int nrw = (int)((whi - wlo + (int64_t)(ga & 3) + 3) >> 2);
+                    for (int i = lane; i < nrw; i += 64) sref[i] = q[i];
+                    rw.w = (lds_cu8*)sref + (ga & 3);
+                    rw.wlo = wlo;
+                    rw.whi = whi;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // IsizeHist max, aggregated when the batch is one group
+            bool isize_done = false;
+            if (a.isz_on && a.isz_lds) {
+                int g = 0;
+                const int32_t fl = act ? a.flag[r] : 0;
+                for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
+                const int g0 = __shfl(g, 0, 64);
+                if (__ballot(act && g != g0) == 0) {
+                    int32_t v = act ? a.gisize[r] : 0;
+                    v = v < 0 ? -v : v;
+                    if (act)
+                        __hip_atomic_fetch_add(lds + a.lds_isz + (int64_t)v * a.G + g, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const int64_t mx = wave_max(act ? (int64_t)v : 0);
+                    if (lane == 0)
+                        __hip_atomic_fetch_max((__attribute__((address_space(3))) int32_t*)(lds + a.lds_isz_max) + g0,
+                                               (int32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    isize_done = true;
+                }
+            }
+            const int soff = (int)((so - (base & ~int64_t(3))) >> 2);   // the read's first dword
+            bool pending = false;
             if (act) {
-                ref_span(a, r, lo, hi);
-            } else {
-                lo = INT64_MAX;
-                hi = INT64_MIN;
+                lds_cu32* rs32 = sseq + soff;
+                pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done);
             }
-            const int64_t L = a.ref_len[rid0];
-            int64_t wlo = max<int64_t>(wave_min(lo), 0), whi = min<int64_t>(wave_max(hi), L);
-            if (whi > wlo && whi - wlo <= kRefStage) {
-                const uint8_t* gref = a.ref + a.ref_off[rid0];
-                const uintptr_t ga = reinterpret_cast<uintptr_t>(gref + wlo);
-                const uint32_t* q = reinterpret_cast<const uint32_t*>(ga & ~uintptr_t(3));
-                const int nrw = (int)((whi - wlo + (int64_t)(ga & 3) + 3) >> 2);
-                for (int i = lane; i < nrw; i += 64) sref[i] = q[i];
-                rw.w = (lds_cu8*)sref + (ga & 3);
-                rw.wlo = wlo;
-                rw.whi = whi;
+            if (a.base_on && MC_SCAN_EXP != 1) {
+                if (MC_SCAN_PAIRS) count_bases_pairs(pair_tab, a, r, pending, act, soff, sseq, lds, lane);
+                else count_bases(inc_tab, a, r, pending, act, soff, sseq, lds, lane);
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            r0 += m;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // IsizeHist max, aggregated when the batch is one group
-        bool isize_done = false;
-        if (a.isz_on && a.isz_lds) {
-            int g = 0;
-            const int32_t fl = act ? a.flag[r] : 0;
-            for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
-            const int g0 = __shfl(g, 0, 64);
-            if (__ballot(act && g != g0) == 0) {
-                int32_t v = act ? a.gisize[r] : 0;
-                v = v < 0 ? -v : v;
-                if (act)
-                    __hip_atomic_fetch_add(lds + a.lds_isz + (int64_t)v * a.G + g, 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int64_t mx = wave_max(act ? (int64_t)v : 0);
-                if (lane == 0)
-                    __hip_atomic_fetch_max((__attribute__((address_space(3))) int32_t*)(lds + a.lds_isz_max) + g0,
-                                           (int32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                isize_done = true;
-            }
-        }
-        const int soff = (int)((so - (base & ~int64_t(3))) >> 2);   // the read's first dword
-        bool pending = false;
-        if (act) {
-            lds_cu32* rs32 = sseq + soff;
-            pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done);
-        }
-        if (a.base_on) count_bases(inc_tab, a, r, pending, act, soff, sseq, lds, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        r0 += m;
+        if (!a.work) break;
     }
     __syncthreads();
     // flush the workgroup's private bins
@@ -667,6 +851,7 @@ struct mc_scan {
     Dev<uint8_t> ref;
     Dev<int64_t> ref_off, ref_len;
     Dev<int32_t> error;
+    Dev<uint32_t> work;         // scan_kernel's slice queue
     Dev<uint16_t> kcodes, kgroup;
     int cus = 1;
     int32_t n_ref = 0;
@@ -800,7 +985,14 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
                                                                   s->grid));
     const int64_t waves = (int64_t)grid * kWaves;
     a.per_wave = (batches + waves - 1) / waves * 64;
-    const size_t lds_bytes = (size_t)a.stage_off * 4 + (size_t)kWaves * kStageBytes + kIncTabWords * 4;
+    if (MC_SCAN_DYN && a.per_wave > 64) {
+        a.per_wave = std::min<int64_t>(a.per_wave, kScanSlice);
+        HIP_TRY(s->work.reserve(1));
+        HIP_TRY(hipMemsetAsync(s->work.p, 0, 4, s->stream));
+        a.work = s->work.p;
+    }
+    const size_t lds_bytes = (size_t)a.stage_off * 4 + (size_t)kWaves * kStageBytes + kIncTabWords * 4 +
+                             (MC_SCAN_PAIRS ? kPairTabWords * 4 : 0);
     hipLaunchKernelGGL(scan_kernel, dim3(grid), dim3(kThreads), lds_bytes, s->stream, a);
     HIP_TRY(hipGetLastError());
     if (a.kcodes) {
