@@ -32,15 +32,15 @@
 //   * k-mer bases outside [0, rlen) (negative OFFSET, K > STEP) read as N
 //     (the reference reads stale bytes of earlier reads).
 //
-// Layout: one lane per read (grid-stride).  A 150 bp read is ~1 KB of LDS
-// atomics for BaseHist: with a lane per read a wave's 64 reads do 64
-// distinct-address atomics per instruction when each lane starts its walk
-// at a different offset (lane-rotated order), where a wave per read would
-// leave 3/4 of its lanes idle on short reads.  BaseHist, MirrorHist and
-// IsizeHist are privatised per workgroup in LDS when they fit (every read
-// hits the same few hundred bins) and flushed once per workgroup; KmerHist
-// (4^K+1 x NK bins per group) takes global atomics, which spread over
-// its 131 K bins at K = 7.
+// Layout: one lane per read.  Waves take slices of kScanSlice reads from a
+// queue and walk them in batches of up to 64 consecutive reads whose bases
+// (and, when they share a reference sequence, the reference window they
+// touch) are staged in LDS; every per-read access after that is LDS.
+// BaseHist, MirrorHist and IsizeHist are privatised per workgroup in LDS
+// when they fit (every read hits the same few hundred bins) and flushed once
+// per workgroup; BaseHist's per-position counts are taken position-parallel
+// (count_bases_pairs).  KmerHist codes go to HBM and kmer_count_kernel counts
+// them in LDS tables (global atomics for K >= 8).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -63,6 +63,12 @@
 
 namespace {
 
+// Build knobs (A/B of the round-5 changes, profiles/r05/r05s-r05z):
+//   MC_SCAN_CUT    a batch ends where its reference window outgrows the stage
+//   MC_SCAN_PAIRS  BaseHist by strand/length sets, two positions per lane
+//                  (0: count_bases, one position per lane)
+//   MC_SCAN_DYN    slices from a queue (0: one static slice per wave)
+//   MC_SCAN_SLICE  reads per queued slice
 #ifndef MC_SCAN_CUT
 #define MC_SCAN_CUT 1
 #endif
@@ -76,14 +82,6 @@ namespace {
 #define MC_SCAN_SLICE 256
 #endif
 constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SCAN_DYN)
-#ifndef MC_SCAN_NOL0
-#define MC_SCAN_NOL0 0
-#endif
-// A/B of the scan kernel's parts (wrong results): 1 no BaseHist counting,
-// 2 no mismatch test on the staged path
-#ifndef MC_SCAN_EXP
-#define MC_SCAN_EXP 0
-#endif
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
@@ -268,8 +266,7 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
         // the exit the staged-window loop has no loop-carried branch and its
         // LDS reads of several words are in flight together.
         int mism = 0;
-        if (fast && MC_SCAN_EXP == 2) {
-        } else if (fast) {
+        if (fast) {
 #pragma unroll 4
             for (int k = 0; k < nw; ++k) {
                 const uint32_t w = s32[k];
@@ -639,19 +636,14 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
                     phi = max(phi, oh);
                 }
             }
-    #if MC_SCAN_NOL0
-            const int64_t L0 = INT64_MAX;
-    #else
             const int64_t L0 = rid0_ok ? a.ref_len[rid0] : 0;
-    #endif
             const int64_t cwlo = max<int64_t>(plo, 0), cwhi = min<int64_t>(phi, L0);
             const bool wfit = rid0_ok ? ridv == rid0 && (cwhi <= cwlo || cwhi - cwlo <= kRefStage)
                                       : (ridv < 0 || ridv >= a.n_ref);
             const uint64_t wf = __ballot(valid && wfit);
             const int m_ref = wf == ~0ull ? 64 : __builtin_ctzll(~wf);
-            int m = m_seq == 0 ? 0 : MC_SCAN_CUT == 1 ? min(m_seq, max(m_ref, 1)) : m_seq;
-            if (MC_SCAN_CUT == 2 && m_ref == 0 && phi == 12345 && m > 1) m = 1;   // (A/B: computed, not applied)
-            if (m == 0) {   // the first read alone exceeds the stage: global path
+            const int m = m_seq == 0 ? 0 : MC_SCAN_CUT ? min(m_seq, max(m_ref, 1)) : m_seq;
+                if (m == 0) {   // the first read alone exceeds the stage: global path
                 if (lane == 0) {
                     const int32_t rid = a.ref_id[r];
                     RefWin rw{nullptr, 0, nullptr, 0, 0};
@@ -718,7 +710,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
                 lds_cu32* rs32 = sseq + soff;
                 pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done);
             }
-            if (a.base_on && MC_SCAN_EXP != 1) {
+            if (a.base_on) {
                 if (MC_SCAN_PAIRS) count_bases_pairs(pair_tab, a, r, pending, act, soff, sseq, lds, lane);
                 else count_bases(inc_tab, a, r, pending, act, soff, sseq, lds, lane);
             }
