@@ -68,6 +68,7 @@ namespace {
 //   MC_SCAN_PAIRS  BaseHist by strand/length sets, two positions per lane
 //                  (0: count_bases, one position per lane)
 //   MC_SCAN_DYN    slices from a queue (0: one static slice per wave)
+//   MC_SCAN_PREFETCH  the next batch's accessor columns load during this one
 //   MC_SCAN_SLICE  reads per queued slice
 #ifndef MC_SCAN_CUT
 #define MC_SCAN_CUT 1
@@ -77,6 +78,9 @@ namespace {
 #endif
 #ifndef MC_SCAN_DYN
 #define MC_SCAN_DYN 1
+#endif
+#ifndef MC_SCAN_PREFETCH
+#define MC_SCAN_PREFETCH 1
 #endif
 #ifndef MC_SCAN_SLICE
 #define MC_SCAN_SLICE 256
@@ -546,9 +550,9 @@ __device__ __forceinline__ void count_bases_pairs(lds_cu64* tab, const ScanArgs&
 }
 
 // Reference positions a read's BaseHist / MirrorHist may read: [lo, hi).
-__device__ __forceinline__ void ref_span(const ScanArgs& a, int64_t r, int64_t& lo, int64_t& hi) {
-    const int32_t rlen = a.rlen[r], gpos = a.gpos[r];
-    const bool rev = (a.flag[r] & 0x10) != 0;
+__device__ __forceinline__ void ref_span(const ScanArgs& a, int32_t rlen, int32_t gpos, int32_t flag, int64_t& lo,
+                                         int64_t& hi) {
+    const bool rev = (flag & 0x10) != 0;
     lo = INT64_MAX;
     hi = INT64_MIN;
     if (a.base_on && gpos >= a.base_start) {
@@ -567,6 +571,26 @@ __device__ __forceinline__ void ref_span(const ScanArgs& a, int64_t r, int64_t& 
             hi = max(hi, p + a.MN + 1);
         }
     }
+}
+
+// A batch's accessor columns at read r (the first read of the batch plus
+// the lane): loaded for the next batch while the current one is processed
+// (MC_SCAN_PREFETCH), so a batch starts without a global round trip.
+struct Cols {
+    int64_t so = 0, se = 0;
+    int32_t rid = -1, rlen = 0, gpos = 0, flag = 0;
+};
+__device__ __forceinline__ Cols load_cols(const ScanArgs& a, int64_t r, bool valid) {
+    Cols c;
+    if (valid) {
+        c.so = a.seq_off[r];
+        c.se = a.seq_off[r + 1];
+        c.rid = a.ref_id[r];
+        c.rlen = a.rlen[r];
+        c.gpos = a.gpos[r];
+        c.flag = a.flag[r];
+    }
+    return c;
 }
 
 __device__ __forceinline__ int64_t wave_max(int64_t v) {
@@ -610,10 +634,12 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
         int64_t r0 = c * a.per_wave;
         if (r0 >= a.n) break;
         const int64_t rend = min(a.n, r0 + a.per_wave);
+        Cols nx = load_cols(a, r0 + lane, r0 + lane < rend);
         while (r0 < rend) {
             const int64_t r = r0 + lane;
             const bool valid = r < rend;
-            const int64_t so = valid ? a.seq_off[r] : 0, se = valid ? a.seq_off[r + 1] : 0;
+            const Cols cc = nx;
+            const int64_t so = cc.so, se = cc.se;
             if (valid && (so & 3)) atomicOr(a.error, 1);
             const int64_t base = __shfl((long long)so, 0, 64);
             const uint64_t fit = __ballot(valid && se - base <= kSeqStage);
@@ -623,12 +649,12 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
             // min / max of the reads' spans): a batch over a sparse stretch of a
             // contig used to leave the window unstaged and every base of its
             // reads to global loads (scan C3: 1/3 of the launch)
-            const int32_t ridv = valid ? a.ref_id[r] : -1;
+            const int32_t ridv = cc.rid;
             const int32_t rid0 = __shfl(ridv, 0, 64);
             const bool rid0_ok = rid0 >= 0 && rid0 < a.n_ref;
             int64_t plo = INT64_MAX, phi = INT64_MIN;
-            if (valid && rid0_ok) ref_span(a, r, plo, phi);
-    #pragma unroll
+            if (valid && rid0_ok) ref_span(a, cc.rlen, cc.gpos, cc.flag, plo, phi);
+#pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const int64_t ol = __shfl_up((long long)plo, d, 64), oh = __shfl_up((long long)phi, d, 64);
                 if (lane >= d) {
@@ -643,7 +669,12 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
             const uint64_t wf = __ballot(valid && wfit);
             const int m_ref = wf == ~0ull ? 64 : __builtin_ctzll(~wf);
             const int m = m_seq == 0 ? 0 : MC_SCAN_CUT ? min(m_seq, max(m_ref, 1)) : m_seq;
-                if (m == 0) {   // the first read alone exceeds the stage: global path
+            {   // the next batch's columns, in flight while this one is processed
+                const int64_t rn = r0 + max(m, 1) + lane;
+                if (MC_SCAN_PREFETCH) nx = load_cols(a, rn, rn < rend);
+                else nx = load_cols(a, rn, false);
+            }
+            if (m == 0) {   // the first read alone exceeds the stage: global path
                 if (lane == 0) {
                     const int32_t rid = a.ref_id[r];
                     RefWin rw{nullptr, 0, nullptr, 0, 0};
@@ -652,6 +683,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
                                  lds, false, false);
                 }
                 r0 += 1;
+                if (!MC_SCAN_PREFETCH) nx = load_cols(a, r0 + lane, r0 + lane < rend);
                 continue;
             }
             const bool act = lane < m;
@@ -717,6 +749,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             r0 += m;
+            if (!MC_SCAN_PREFETCH) nx = load_cols(a, r0 + lane, r0 + lane < rend);
         }
         if (!a.work) break;
     }
