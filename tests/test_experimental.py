@@ -185,6 +185,24 @@ def test_read_side_long_regions_vs_oracle(tmp_path, lib_built):
         check_result(case, res)
 
 
+def test_read_table_threads_agree(tmp_path, lib_built):
+    """The record walk splits a window's placed records over threads (each
+    with its own name arena): 1 and 8 threads give the same results."""
+    path = str(tmp_path / "many.bam")
+    _long_bam(path, 9, L=200_000, pairs=20_000)
+    k = 4
+    rng = np.random.default_rng(3)
+    keys = ["".join(p) for p in __import__("itertools").product("ACGT", repeat=k)]
+    kc = [{x: float(rng.uniform(0.3, 3)) for x in keys} for _ in range(2)]
+    regions = [("chr", 0, 200_000), ("chr", 50_000, 51_000), ("chr", 123_457, 190_001)]
+    outs = []
+    for nt in (1, 8):
+        with mx.ReadTable(path, k, nt) as table:
+            res = mx.experimental_batch(table, kc, k, None, regions, n_threads=nt)
+            outs.append([repr((r.row, r.error, r.zero_lines)) for r in res])
+    assert outs[0] == outs[1]
+
+
 def test_unsorted_bam_rejected(tmp_path, lib_built):
     from metacov_amd._lib import MetacovError
     path = str(tmp_path / "u.bam")
