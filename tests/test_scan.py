@@ -635,3 +635,86 @@ def test_scan_kernel_vs_c_port_gpu(mix, lib_built):
         want, _ = coracle.scan(cfg, batch, ref, roff, rlen_ref, rows.value, cap.value)
         for a, b in zip(got, want):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_scan_kernel_queue_and_cuts_vs_c_port_gpu(lib_built):
+    """A batch large enough for the slice queue, sorted like a coordinate-
+    sorted BAM, on a dense and a sparse contig (batches cut at the reference
+    window), with odd / even / > 256-base reads on both strands and two
+    groups: equal to the C port."""
+    from metacov_amd import _lib
+    from oracle import coracle
+    lib = _lib.load()
+    rng = np.random.default_rng(17)
+    lens_ref = np.array([300_000, 2_000_000, 40_000], np.int64)
+    counts = [250_000, 45_000, 60_000]
+    roff = np.zeros(3, np.int64)
+    roff[1:] = np.cumsum(lens_ref)[:-1]
+    ref_ascii = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(lens_ref.sum()))].copy()
+    ref_ascii[rng.random(ref_ascii.size) < 0.001] = ord("N")
+    choices = np.array([36, 75, 100, 101, 150, 151, 251, 300], np.int32)
+    p = np.array([0.05, 0.1, 0.1, 0.1, 0.3, 0.3, 0.04, 0.01])
+    rlen, flag, gpos, rid = [], [], [], []
+    for t, (L, c) in enumerate(zip(lens_ref, counts)):
+        rl = rng.choice(choices, size=c, p=p)
+        pos = np.sort(rng.integers(0, int(L) - 301, c))
+        rev = rng.random(c) < 0.5
+        rlen.append(rl)
+        flag.append((0x1 | np.where(rng.random(c) < 0.5, 0x40, 0x80) | (rng.random(c) < 0.9) * 0x2 |
+                     rev * 0x10).astype(np.int32))
+        gpos.append((pos + rev * rl).astype(np.int32))
+        rid.append(np.full(c, t, np.int32))
+    rlen, flag, gpos, rid = (np.concatenate(x) for x in (rlen, flag, gpos, rid))
+    n = rlen.size
+    gisize = np.where(flag & 0x2, rng.integers(-900, 900, n), 0).astype(np.int32)
+    code = np.zeros(256, np.uint8)
+    for ch, v in zip(b"ACGTN", (1, 2, 4, 8, 15)):
+        code[ch] = v
+    nbytes = (rlen + 1) // 2
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(nbytes)
+    seq = np.zeros(int(off[-1]), np.uint8)
+    start = roff[rid] + np.where(flag & 0x10, gpos - rlen, gpos)
+    for i in range(0, n, 50_000):   # bases from the reference, 1 % substitutions, some random reads
+        j = np.arange(i, min(n, i + 50_000))
+        for L in np.unique(rlen[j]):
+            sel = j[rlen[j] == L]
+            b = code[ref_ascii[start[sel, None] + np.arange(L)[None, :]]]
+            mut = rng.random(b.shape) < 0.01
+            b = np.where(mut, np.array([1, 2, 4, 8, 3], np.uint8)[rng.integers(0, 5, b.shape)], b)
+            junk = rng.random(sel.size) < 0.05
+            b[junk] = np.array([1, 2, 4, 8], np.uint8)[rng.integers(0, 4, (int(junk.sum()), int(L)))]
+            if L % 2:
+                b = np.concatenate([b, np.zeros((b.shape[0], 1), np.uint8)], axis=1)
+            packed = (b[:, 0::2] << 4) | b[:, 1::2]
+            for k, r in enumerate(sel):
+                seq[off[r]:off[r + 1]] = packed[k]
+    t4 = np.full(256, 4, np.uint8)
+    for ch, v in zip(b"ACGT", (0, 1, 2, 3)):
+        t4[ch] = v
+    batch = [rlen, flag, gpos, gisize, rid, off, seq]
+    cfg = _lib.ScanConfig()
+    cfg.n_flags = 1
+    cfg.flags[0] = 0x80
+    cfg.base_on, cfg.base_start = 1, 3
+    cfg.kmer_on, cfg.kmer_k, cfg.kmer_nk, cfg.kmer_step, cfg.kmer_offset = 1, 7, 8, 7, 0
+    cfg.mirror_on, cfg.mirror_offset, cfg.mirror_n = 1, 4, 10
+    cfg.isize_on = 1
+    h = ctypes.c_void_p()
+    _lib.check(lib.mc_scan_create(0, ctypes.byref(cfg), ctypes.byref(h)), lib)
+    _lib.check(lib.mc_scan_set_reference(h, 3, _lib.ptr(roff), _lib.ptr(lens_ref), ref_ascii.size,
+                                         _lib.ptr(ref_ascii)), lib)
+    _lib.check(lib.mc_scan_add_batch(h, n, *[_lib.ptr(a) for a in batch]), lib)
+    G, rows, cap = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+    lib.mc_scan_dims(h, ctypes.byref(G), ctypes.byref(rows), ctypes.byref(cap), None, None)
+    got = (np.zeros((G.value, rows.value, 5), np.uint32), np.zeros((G.value, 4 ** 7 + 1, 8), np.uint32),
+           np.zeros((G.value, 11, 2), np.uint32), np.zeros((G.value, cap.value), np.uint32),
+           np.zeros(G.value, np.int32))
+    _lib.check(lib.mc_scan_results(h, *[_lib.ptr(x) for x in got]), lib)
+    lib.mc_scan_destroy(h)
+    want, done = coracle.scan(cfg, batch, t4[ref_ascii], roff, lens_ref, rows.value, cap.value)
+    assert done == n
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b)
+    assert got[0][:, :, :4].sum() > 0.5 * (rlen.sum())   # most reads passed BaseHist's test
