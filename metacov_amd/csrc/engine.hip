@@ -187,7 +187,7 @@ struct mc_ctx {
     // that far before it instead of short_max (C3: 4096 -> ~2400 positions)
     int direct_halo = 0;
     int direct_halo_used = 0;
-    DevBuf<int32_t> d_jidx;               // [2 * (n_base + 1)]: J(k w), J(k w - halo)
+    DevBuf<int32_t> d_jidx;               // [3 * (n_base + 1)]: J(k w), J(k w - halo), J(k w - kNearHalo)
     DevBuf<int32_t> d_fsamp;              // [nc + 1] first sample of each contig
     DevBuf<unsigned long long> d_dres;    // [kDresWords] probe flags + K2's counters
     DevBuf<uint32_t> d_endw;              // ingest_kernel<true>'s end words (long_fill_words_kernel)
@@ -971,7 +971,7 @@ static int prepare_direct(mc_ctx* ctx) {
     set_layout(ctx, ctx->len);
     if (int rc = upload_coff(ctx, coff_up)) return rc;
     const int64_t n_base = ctx->n_chunks * ctx->cstride;
-    HIP_TRY(ctx->d_jidx.reserve(2 * (n_base + 1)));
+    HIP_TRY(ctx->d_jidx.reserve(3 * (n_base + 1)));
     HIP_TRY(ctx->d_fsamp.reserve(nc + 1));
     if (!ctx->d_dres.p) {
         HIP_TRY(ctx->d_dres.reserve(kDresWords));
@@ -981,7 +981,8 @@ static int prepare_direct(mc_ctx* ctx) {
     // direct K2 neither applies nor checks reads at or past n)
     ctx->direct_halo_used = ctx->direct_halo > 0 ? std::min(ctx->direct_halo, ctx->short_max) : ctx->short_max;
     ProbeArgs P{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, nc, ctx->d_coff.p, base_lw(ctx),
-                ctx->short_max, ctx->direct_halo_used, n_base, ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1), ctx->d_fsamp.p,
+                ctx->short_max, ctx->direct_halo_used, n_base, ctx->d_jidx.p, ctx->d_jidx.p + (n_base + 1),
+                ctx->d_jidx.p + 2 * (n_base + 1), ctx->d_fsamp.p,
                 ctx->d_dres.p, ++ctx->direct_gen};
     const int64_t M = (n + kProbeStride - 1) >> kProbeShift;
     hipLaunchKernelGGL(probe_kernel, dim3((unsigned)std::max<int64_t>(1, (M + kBlock - 1) / kBlock)),
@@ -1127,7 +1128,7 @@ static DirectWindow direct_window(const mc_ctx* ctx) {
 // slots are matched bytewise: K2Consts has no padding but DirectArgs' one
 // hole, which launch_depth keeps zeroed (memberwise stores into a zeroed
 // struct).
-static_assert(sizeof(DirectArgs) == 4 * 8 + 8 + sizeof(DirectWindow) && sizeof(DirectWindow) == 32 &&
+static_assert(sizeof(DirectArgs) == 5 * 8 + 8 + sizeof(DirectWindow) && sizeof(DirectWindow) == 32 &&
                   sizeof(FusedRegions) == 10 * 8 && sizeof(ReadArrays) == 4 * 8,
               "K2Consts: padding beyond DirectArgs' 4 bytes after nc");
 static int k2_consts(mc_ctx* ctx, const K2Consts& kc, const K2Consts** out) {
@@ -1195,6 +1196,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     w.parity = 0;   // (K2 takes this call's parity as an argument)
     kc.D.j0 = ctx->d_jidx.p;   // (memberwise: the struct's padding stays zero)
     kc.D.jh = ctx->d_jidx.p + (n_base + 1);
+    kc.D.jn = ctx->d_jidx.p + 2 * (n_base + 1);
     kc.D.len = ctx->d_len.p;
     kc.D.nc = (int32_t)ctx->len.size();
     kc.D.dres = ctx->d_dres.p;

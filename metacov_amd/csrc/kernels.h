@@ -40,6 +40,12 @@ namespace mc {
                                        // (A/B, profiles/r05/r05ab1: direct C3 1.019 -> 1.002 ms, C2 0.0653 ->
                                        // 0.0611; 2 = no branch, zero adds: 1.004 vs 0.990 ms, r05ab2)
 #endif
+#ifndef MC_FAR_HALO
+#define MC_FAR_HALO 1                  // direct K2: the chunk halo's far part by spans only (far_halo)
+#endif
+#ifndef MC_FAR_HALO_MIN
+#define MC_FAR_HALO_MIN 4096
+#endif
 #ifndef MC_DIRECT_ONE_CONTIG
 #define MC_DIRECT_ONE_CONTIG 1         // direct K2: a batch on the cached contig skips the contig lookup loop
                                        // (C3 1.019 -> 1.007 ms, C2 0.0653 -> 0.0615; both: 0.988 / 0.0558)
@@ -685,6 +691,11 @@ ingest_kernel(const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
 // then re-runs the batch through the full prepare, which raises the exact
 // errors or builds the extents and long-read buckets.
 constexpr int kProbeShift = 8;                 // sample stride S = 256 reads
+// Reads starting more than kNearHalo positions before a chunk reach into it
+// only with a span above kNearHalo: K2 takes that far part of the chunk's
+// halo by spans alone (far_halo), the rest as whole tuples.
+constexpr int kNearHalo = 256;
+constexpr int kFarHaloMin = MC_FAR_HALO_MIN;   // reads
 constexpr int kProbeStride = 1 << kProbeShift;
 
 // dres[]: probe flags (the call's generation stamp, so they need no reset)
@@ -715,6 +726,7 @@ struct ProbeArgs {
     int64_t n_base;                    // grid targets k = 0 .. n_base
     int32_t* j0;                       // [n_base + 1] J(k * w)
     int32_t* jh;                       // [n_base + 1] J(k * w - halo)
+    int32_t* jn;                       // [n_base + 1] J(k * w - kNearHalo) (MC_FAR_HALO)
     int32_t* fsamp;                    // [nc + 1] first sample of contig t
     unsigned long long* dres;
     unsigned long long gen;
@@ -833,6 +845,7 @@ probe_kernel(ProbeArgs A) {
     const bool first = j == 0;
     probe_fill(A.j0, A.n_base, A.lw, 0, key, key_next, first, last, (int32_t)(j + 1));
     probe_fill(A.jh, A.n_base, A.lw, A.halo, key, key_next, first, last, (int32_t)(j + 1));
+    if (MC_FAR_HALO) probe_fill(A.jn, A.n_base, A.lw, kNearHalo, key, key_next, first, last, (int32_t)(j + 1));
     // contigs (tid_j, tid_next] start after sample j
     const int ct = t < 0 ? 0 : t >= A.nc ? A.nc - 1 : t;
     const int cn = last ? A.nc : (t_next < 0 ? 0 : t_next >= A.nc ? A.nc - 1 : t_next);
@@ -1498,6 +1511,7 @@ __device__ __forceinline__ void finish_batch(ReadBatch& b, const RawBatch<false>
 struct DirectArgs {
     const int32_t* j0;                 // [n_base + 1] J(k * w)       (probe_kernel)
     const int32_t* jh;                 // [n_base + 1] J(k * w - halo)
+    const int32_t* jn;                 // [n_base + 1] J(k * w - kNearHalo)
     const int64_t* len;                // [nc] contig lengths (= extents on this path)
     int32_t nc;
     unsigned long long* dres;
@@ -1656,6 +1670,36 @@ __device__ __forceinline__ void finish_batch_direct(ReadBatch& b, const RawBatch
     acc.max_span = max(acc.max_span, max(max((mm & 1u) ? sp[0] : 0, (mm & 2u) ? sp[1] : 0),
                                          max((mm & 4u) ? sp[2] : 0, (mm & 8u) ? sp[3] : 0)));
     acc.flags |= (bad & own) ? kDirectInvalid : (unfit & own) ? kDirectUnfit : 0u;
+}
+
+// The far part of a direct chunk's halo, reads [lo, hi) that start more
+// than kNearHalo positions before the chunk (C0): only those with a span
+// above kNearHalo can reach it, so their spans are read (4 B per read, int4
+// per lane) and only such reads' (tid, pos) (rare: the span mix's spliced
+// reads).  A read reaching past C0 adds +1 at the chunk's first slot and -1
+// at its end, as the batch loop applies a halo read.  The reads are checked
+// by their own chunk.  At C2 depth this is ~45 % of the reads a chunk loads.
+template <class DT>
+__device__ __forceinline__ void far_halo(const ReadArrays& A, const DT& D, const int64_t* __restrict__ coff,
+                                         int64_t lo, int64_t hi, int64_t C0, int short_max, int* ring) {
+    // (one int4 of spans per thread and step: keeping 8 in flight raised the
+    // kernel's VGPRs and cost C3 +10 %, r05/r05ab13_*)
+    for (int64_t i0 = (lo & ~(int64_t)3) + (int64_t)threadIdx.x * 4; i0 < hi; i0 += (int64_t)kK2Block * 4) {
+        const i32x4 s4 = *reinterpret_cast<const i32x4*>(A.span + i0);
+        const int sp[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = i0 + k;
+            if (i < lo || i >= hi || sp[k] <= kNearHalo || sp[k] > short_max) continue;
+            const int t = A.tid[i], p = A.pos[i];
+            if ((unsigned)t >= (unsigned)D.nc || p < 0) continue;
+            const int64_t e = coff[t] + p + sp[k] - C0;
+            if (e > 0 && e <= short_max) {   // (sorted input: e <= short_max - kNearHalo)
+                atomicAdd(&ring[ring_slot(0)], 1);
+                atomicAdd(&ring[ring_slot((int)e)], -1);
+            }
+        }
+    }
 }
 
 // K2 direct: the per-workgroup verdict into dres (one atomic, only when a
@@ -2119,6 +2163,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
         const int64_t b0 = c * cstride;
         int64_t cfirst, cend;
         DirectChunk dc{0, 0, 0, 0};
+        int64_t far_lo = 0, far_hi = 0;
         if (kDirect) {
             // read ranges from the probe's sample counts J: lb(P) lies in
             // ((J - 1) * S, J * S]; the first chunk starts at 0, the last ends at n
@@ -2132,6 +2177,16 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
             dc.vhi = last ? n : lower(uload(D.j0, b1));
             dc.lo = min(dc.lo, dc.vlo);   // (apart only on unsorted input, which is reported)
             dc.hi = max(dc.hi, dc.vhi);
+            if (MC_FAR_HALO && c) {   // [lo, lower(J(C0 - kNearHalo))): by spans (far_halo)
+                const int64_t fh = min(max(lower(uload(D.jn, b0)), dc.lo), dc.vlo);
+                // (a far part under kFarHaloMin reads costs more than it saves:
+                // C3 +1.4 % at 1024, neutral at 4096; C2 K2 -3 %, r05/r05ab12_*)
+                if (fh - dc.lo >= kFarHaloMin) {
+                    far_lo = dc.lo;
+                    far_hi = fh;
+                    dc.lo = fh;
+                }
+            }
             cfirst = dc.lo;
             cend = dc.hi;
         } else {
@@ -2164,12 +2219,14 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
             else
                 finish_batch(b, r, at, cend, C0, cfirst);
         };
+        RawBatch<kDirect> r0;
         if (more) {
-            RawBatch<kDirect> r0;
             issue_raw<kDirect>(r0, base, A, cend);
             if (kPf && base + kK2Batch < cend) issue_raw<kDirect>(nxt, base + kK2Batch, A, cend);
-            finish(r0, base);
         }
+        // (after the first batches' loads are issued: one round trip for both)
+        if (kDirect && MC_FAR_HALO && far_hi > far_lo) far_halo(A, D, coff, far_lo, far_hi, C0, short_max, ring);
+        if (more) finish(r0, base);
         int carry = kLong ? uload(chunk_carry, c) : 0;
         // -1 end events of long reads (chunk-relative, in tile order): a
         // second stream of 1024-event batches, applied like the reads while
