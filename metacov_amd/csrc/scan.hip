@@ -125,6 +125,7 @@ struct ScanArgs {
     uint32_t* kmer;
     uint16_t* kcodes;
     uint16_t* kgroup;         // per read group (G > 1 with kcodes)
+    int64_t kstride;          // kcodes row stride: n rounded up to 8 (16-byte rows)
     // MirrorHist: [G][N + 1][2]
     int32_t mir_on, MOFF, MN, mir_lds;
     uint32_t* mir;
@@ -238,7 +239,7 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
                 }
             }
             if (a.kcodes)
-                a.kcodes[(int64_t)i * a.n + r] = (uint16_t)k;
+                a.kcodes[(int64_t)i * a.kstride + r] = (uint16_t)k;
             else if (ok)
                 atomicAdd(a.kmer + ((int64_t)g * a.NK + i) * (nbucket + 1) + k, 1u);
         }
@@ -780,7 +781,7 @@ constexpr int kKmerThreads = 512;
 constexpr int kKmerLdsBytes = 160 * 1024;
 
 __global__ __launch_bounds__(kKmerThreads) void kmer_count_kernel(
-    const uint16_t* __restrict__ kcodes, const uint16_t* __restrict__ kgroup, int64_t n, int NK,
+    const uint16_t* __restrict__ kcodes, const uint16_t* __restrict__ kgroup, int64_t n, int64_t kstride, int NK,
     int nbins, int spp, int G, uint32_t* __restrict__ kmer) {
     extern __shared__ uint32_t t_[];
     lds_u32* t = (lds_u32*)t_;
@@ -788,14 +789,35 @@ __global__ __launch_bounds__(kKmerThreads) void kmer_count_kernel(
     const int words = ns * nbins;
     for (int i = threadIdx.x; i < words; i += kKmerThreads) t[i] = 0;
     __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * kKmerThreads;
-    for (int64_t r = (int64_t)blockIdx.x * kKmerThreads + threadIdx.x; r < n; r += stride) {
-        if (G > 1 && kgroup[r] != g) continue;
-        for (int q = 0; q < ns; ++q) {
-            const uint32_t c = kcodes[(int64_t)(s0 + q) * n + r];
-            if (c != 0xFFFFu)
-                __hip_atomic_fetch_add(t + q * nbins + c, 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    // 8 reads' codes per 16-byte load (rows are kstride = n rounded up to 8
+    // apart); two steps' loads in flight (one u16 per thread and step was
+    // latency-bound: ~3 ms of 100 M reads x 8 slots)
+    const int64_t stride = (int64_t)gridDim.x * kKmerThreads * 8;
+    auto count8 = [&](lds_u32* tq, int64_t r8, uint4 v, uint4 gr) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t gw[4] = {gr.x, gr.y, gr.z, gr.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const uint32_t c = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+            const uint32_t gg = (gw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+            if (r8 + e < n && c != 0xFFFFu && (G == 1 || (int)gg == g))
+                __hip_atomic_fetch_add(tq + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    for (int q = 0; q < ns; ++q) {
+        const uint16_t* row = kcodes + (int64_t)(s0 + q) * kstride;
+        lds_u32* tq = t + q * nbins;
+        for (int64_t r8 = ((int64_t)blockIdx.x * kKmerThreads + threadIdx.x) * 8; r8 < n; r8 += 2 * stride) {
+            const int64_t r8b = r8 + stride;
+            const uint4 va = *reinterpret_cast<const uint4*>(row + r8);
+            const uint4 vb = r8b < n ? *reinterpret_cast<const uint4*>(row + r8b) : uint4{};
+            uint4 ga{}, gb{};
+            if (G > 1) {
+                ga = *reinterpret_cast<const uint4*>(kgroup + r8);
+                if (r8b < n) gb = *reinterpret_cast<const uint4*>(kgroup + r8b);
+            }
+            count8(tq, r8, va, ga);
+            if (r8b < n) count8(tq, r8b, vb, gb);
         }
     }
     __syncthreads();
@@ -993,10 +1015,11 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
     const int nbins = (1 << (2 * c.kmer_k)) + 1;
     const int spp = c.kmer_on ? std::min(c.kmer_nk, kKmerLdsBytes / (nbins * 4)) : 0;
     if (c.kmer_on && spp >= 1) {       // K <= 7: codes + LDS counting kernel
-        HIP_TRY(s->kcodes.reserve((size_t)(n * c.kmer_nk)));
+        a.kstride = (n + 7) & ~int64_t(7);
+        HIP_TRY(s->kcodes.reserve((size_t)(a.kstride * c.kmer_nk)));
         a.kcodes = s->kcodes.p;
         if (s->G > 1) {
-            HIP_TRY(s->kgroup.reserve((size_t)n));
+            HIP_TRY(s->kgroup.reserve((size_t)a.kstride));
             a.kgroup = s->kgroup.p;
         }
     }
@@ -1022,10 +1045,10 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
     HIP_TRY(hipGetLastError());
     if (a.kcodes) {
         const int passes = (c.kmer_nk + spp - 1) / spp;
-        const int64_t wantb = (n + kKmerThreads - 1) / kKmerThreads;
+        const int64_t wantb = (n + 8 * kKmerThreads - 1) / (8 * kKmerThreads);
         const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(wantb, s->cus));
         hipLaunchKernelGGL(kmer_count_kernel, dim3(gx, passes, s->G), dim3(kKmerThreads),
-                           (size_t)spp * nbins * 4, s->stream, a.kcodes, a.kgroup, n, c.kmer_nk,
+                           (size_t)spp * nbins * 4, s->stream, a.kcodes, a.kgroup, n, a.kstride, c.kmer_nk,
                            nbins, spp, s->G, s->kmer.p);
         HIP_TRY(hipGetLastError());
     }
