@@ -90,8 +90,22 @@ constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SC
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kLdsWords = 8192;     // histogram arena: 32 KiB
-constexpr int kSeqStage = 6144;     // per wave: packed bases of the batch
-constexpr int kRefStage = 2048;     // per wave: reference window of the batch
+// scan_kernel residency: 4 workgroups per CU (launch bounds: VGPRs <= 128)
+// with 5 KB of read stage and 1.5 KB of reference window per wave (whole
+// 64-read batches of 150 bp, a window of ~0.8 kbp at C3 density): C3 scan
+// 20.5 -> 17.9 ms against 3 per CU with 6 + 2 KB; 5 per CU with 3 + 1.5 KB
+// 24.4 ms (short batches) (profiles/r05/r05zh_scan_occupancy.txt)
+#ifndef MC_SCAN_OCC
+#define MC_SCAN_OCC 4
+#endif
+#ifndef MC_SCAN_SEQ
+#define MC_SCAN_SEQ (MC_SCAN_OCC >= 4 ? 5120 : 6144)
+#endif
+#ifndef MC_SCAN_REF
+#define MC_SCAN_REF (MC_SCAN_OCC >= 4 ? 1536 : 2048)
+#endif
+constexpr int kSeqStage = MC_SCAN_SEQ;   // per wave: packed bases of the batch
+constexpr int kRefStage = MC_SCAN_REF;   // per wave: reference window of the batch
 constexpr int kStagePad = 16;
 constexpr int kStageBytes = kSeqStage + kRefStage + 2 * kStagePad;
 constexpr int kMaxFlags = 16;
@@ -605,7 +619,7 @@ __device__ __forceinline__ int64_t wave_max(int64_t v) {
 // reference sequence, the reference window it touches are copied to LDS
 // with coalesced dword loads; every per-read access after that is LDS.
 // A read too long to stage is processed from global memory.
-__global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs a) {
+__global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a) {
     extern __shared__ uint32_t lds_[];
     lds_u32* lds = (lds_u32*)lds_;
     for (int i = threadIdx.x; i < a.lds_words; i += kThreads) lds[i] = 0;
@@ -1088,7 +1102,7 @@ extern "C" int mc_scan_create(int device, const mc_scan_config* cfg, mc_scan** o
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     s->cus = std::max(1, cus);
-    s->grid = s->cus * 3;
+    s->grid = s->cus * MC_SCAN_OCC;
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(kmer_count_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kKmerLdsBytes));
     HIP_TRY(s->error.reserve(1));
