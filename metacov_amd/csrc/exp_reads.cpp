@@ -35,12 +35,15 @@
 //   wnf   the pair terms in pairing order                          (exact)
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <string_view>
 #include <thread>
 #include <unordered_map>
 
 #include "bgzf.h"
+#include "common.h"
 
 using namespace mc::bgzf;
 
@@ -132,6 +135,7 @@ int walk_records(mc_reads* r, const uint8_t* d, size_t o, size_t n, size_t* cons
         const int32_t bs = rdi32(d + o);
         MC_REQUIRE(bs >= 32, MC_E_IO, "%s: bad record size at inflated byte %zu", path, o);
         if (o + 4 + (size_t)bs > n) break;
+        __builtin_prefetch(d + std::min(n - 1, o + 4096));   // (the size chain is a serial walk)
         const uint8_t* b = d + o + 4;
         const int32_t tid = rdi32(b), pos = rdi32(b + 4);
         const uint8_t l_read_name = b[8];
@@ -211,7 +215,7 @@ int walk_records(mc_reads* r, const uint8_t* d, size_t o, size_t n, size_t* cons
     }
     size_t names = r->arena.size();   // join the arenas
     for (int t = 0; t < T; ++t) names += arenas[t].size();
-    r->arena.reserve(std::max(names, r->arena.capacity() + r->arena.capacity() / 2));
+    if (names > r->arena.capacity()) r->arena.reserve(std::max(names, r->arena.capacity() + r->arena.capacity() / 2));
     for (int t = 0; t < T; ++t) {
         const size_t i0 = m * t / T, i1 = m * (t + 1) / T, shift = r->arena.size();
         for (size_t i = i0; i < i1; ++i) r->name_off[base + i] += shift;
@@ -227,43 +231,106 @@ int walk_records(mc_reads* r, const uint8_t* d, size_t o, size_t n, size_t* cons
     return MC_OK;
 }
 
+// One window of the file: its BGZF blocks inflated after kCarryRoom bytes of
+// room, where the previous window's unfinished record is copied in front.
+struct Window {
+    std::unique_ptr<uint8_t[]> buf;
+    size_t cap = 0, total = 0;
+    bool last = false;
+};
+constexpr size_t kCarryRoom = 1 << 20;
+
+// Finds the blocks of up to `window` inflated bytes from *next_off and
+// inflates them into w (after kCarryRoom).  Runs on a background thread for
+// the next window while the current one is walked: the walk's serial parts
+// (the record-size chain, the joins) overlap the inflate.
+int produce_window(const MappedFile& mf, size_t* next_off, size_t window, int nt, const char* path, Window& w,
+                   std::string* err) {
+    std::vector<Block> blocks;
+    size_t total = 0;
+    while (*next_off < mf.size && total < window) {
+        const size_t b0 = blocks.size();
+        if (int rc = scan_blocks(mf.data, mf.size, *next_off, *next_off, blocks, total)) {
+            *err = mc::last_error();
+            return rc;
+        }
+        *next_off = blocks[b0].cdata + blocks[b0].clen + 8;
+    }
+    w.last = *next_off >= mf.size;
+    w.total = total;
+    if (kCarryRoom + total + 8 > w.cap) {
+        w.cap = kCarryRoom + total + 8;
+        w.buf.reset(new (std::nothrow) uint8_t[w.cap]);
+        if (!w.buf) {
+            *err = "cannot allocate the read window for " + std::string(path);
+            w.cap = 0;
+            return MC_E_IO;
+        }
+    }
+    if (!blocks.empty() && !inflate_blocks(mf.data, blocks, w.buf.get() + kCarryRoom, nt)) {
+        *err = "BGZF inflate failed in " + std::string(path);
+        return MC_E_IO;
+    }
+    return MC_OK;
+}
+
 int reads_open(const char* path, int n_threads, int k, mc_reads* r) {
     MappedFile mf;
     if (int rc = mf.open(path)) return rc;
     const int nt = n_threads_or_all(n_threads);
-    const size_t window = 256ull << 20;
-    std::unique_ptr<uint8_t[]> buf;
-    size_t cap = 0, carry = 0, next_off = 0;
+    size_t window = 256ull << 20;
+    if (const char* e = std::getenv("MC_READS_WINDOW")) window = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+    const char* pe = std::getenv("MC_READS_PIPELINE");
+    const bool pipeline = !(pe && pe[0] == '0');
+    size_t next_off = 0;
     bool have_header = false;
-    size_t o = 0;
     int32_t last_tid = -1, last_pos = -1;
+    std::vector<uint8_t> carry;   // the previous window's unfinished bytes
+    Window cur, nxt;
+    std::string perr;
+    if (int rc = produce_window(mf, &next_off, window, nt, path, cur, &perr)) {
+        mc::set_error("%s", perr.c_str());
+        return rc;
+    }
     for (;;) {
-        std::vector<Block> blocks;
-        size_t total = 0;
-        while (next_off < mf.size && total < window) {
-            const size_t b0 = blocks.size();
-            if (int rc = scan_blocks(mf.data, mf.size, next_off, next_off, blocks, total)) return rc;
-            next_off = blocks[b0].cdata + blocks[b0].clen + 8;
+        int prc = MC_OK;
+        std::thread producer;
+        if (!cur.last) {
+            if (pipeline)
+                producer = std::thread([&] { prc = produce_window(mf, &next_off, window, nt, path, nxt, &perr); });
+            else
+                prc = produce_window(mf, &next_off, window, nt, path, nxt, &perr);
         }
-        const bool last = next_off >= mf.size;
-        if (carry + total + 8 > cap) {
-            const size_t ncap = std::max(carry + total + 8, cap + cap / 4);
-            std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[ncap]);
-            MC_REQUIRE(nb, MC_E_IO, "cannot allocate %zu bytes for %s", ncap, path);
-            if (carry) std::memcpy(nb.get(), buf.get(), carry);
-            buf = std::move(nb);
-            cap = ncap;
+        auto join = [&] {
+            if (producer.joinable()) producer.join();
+        };
+        // the window's bytes with the carry in front
+        uint8_t* d;
+        std::unique_ptr<uint8_t[]> big;   // (a carry larger than the room)
+        if (carry.size() <= kCarryRoom) {
+            d = cur.buf.get() + kCarryRoom - carry.size();
+            if (!carry.empty()) std::memcpy(d, carry.data(), carry.size());
+        } else {
+            big.reset(new (std::nothrow) uint8_t[carry.size() + cur.total + 8]);
+            if (!big) {
+                join();
+                MC_REQUIRE(false, MC_E_IO, "cannot allocate %zu bytes for %s", carry.size() + cur.total, path);
+            }
+            std::memcpy(big.get(), carry.data(), carry.size());
+            std::memcpy(big.get() + carry.size(), cur.buf.get() + kCarryRoom, cur.total);
+            d = big.get();
         }
-        MC_REQUIRE(blocks.empty() || inflate_blocks(mf.data, blocks, buf.get() + carry, nt), MC_E_IO,
-                   "BGZF inflate failed in %s", path);
-        const size_t n = carry + total;
-        o = 0;
+        const size_t n = carry.size() + cur.total;
+        size_t o = 0;
         if (!have_header) {
             std::vector<std::string> names;
             std::vector<int64_t> lens;
-            if (parse_header(buf.get(), n, path, names, lens, &o) != MC_OK) {
-                MC_REQUIRE(!last, MC_E_IO, "%s: no valid BAM header", path);
-                carry = n;
+            if (parse_header(d, n, path, names, lens, &o) != MC_OK) {
+                join();
+                MC_REQUIRE(!cur.last, MC_E_IO, "%s: no valid BAM header", path);
+                MC_REQUIRE(prc == MC_OK, prc, "%s", perr.c_str());
+                carry.assign(d, d + n);
+                std::swap(cur, nxt);
                 continue;
             }
             have_header = true;
@@ -272,14 +339,16 @@ int reads_open(const char* path, int n_threads, int k, mc_reads* r) {
             r->max_span.assign(r->names.size(), 0);
         }
         size_t consumed = o;
-        if (int rc = walk_records(r, buf.get(), o, n, &consumed, &last_tid, &last_pos, path, nt))
-            return rc;
-        carry = n - consumed;
-        if (carry) std::memmove(buf.get(), buf.get() + consumed, carry);
-        if (last) {
-            MC_REQUIRE(carry == 0, MC_E_IO, "%s: truncated record at the end of the file", path);
+        const int wrc = walk_records(r, d, o, n, &consumed, &last_tid, &last_pos, path, nt);
+        join();
+        if (wrc) return wrc;
+        carry.assign(d + consumed, d + n);
+        if (cur.last) {
+            MC_REQUIRE(carry.empty(), MC_E_IO, "%s: truncated record at the end of the file", path);
             break;
         }
+        MC_REQUIRE(prc == MC_OK, prc, "%s", perr.c_str());
+        std::swap(cur, nxt);
     }
     r->first.resize(r->names.size() + 1, (int64_t)r->pos.size());
     return MC_OK;

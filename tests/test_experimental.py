@@ -185,9 +185,10 @@ def test_read_side_long_regions_vs_oracle(tmp_path, lib_built):
         check_result(case, res)
 
 
-def test_read_table_threads_agree(tmp_path, lib_built):
+def test_read_table_threads_agree(tmp_path, lib_built, monkeypatch):
     """The record walk splits a window's placed records over threads (each
-    with its own name arena): 1 and 8 threads give the same results."""
+    with its own name arena): 1 and 8 threads, and many small windows, give
+    the same results."""
     path = str(tmp_path / "many.bam")
     _long_bam(path, 9, L=200_000, pairs=20_000)
     k = 4
@@ -196,11 +197,15 @@ def test_read_table_threads_agree(tmp_path, lib_built):
     kc = [{x: float(rng.uniform(0.3, 3)) for x in keys} for _ in range(2)]
     regions = [("chr", 0, 200_000), ("chr", 50_000, 51_000), ("chr", 123_457, 190_001)]
     outs = []
-    for nt in (1, 8):
+    for nt, window in ((1, None), (8, None), (8, "65536")):
+        # (a 64 KiB window: the file in ~40 windows, records cut at every
+        # window end, each window inflated while the previous one is walked)
+        if window:
+            monkeypatch.setenv("MC_READS_WINDOW", window)
         with mx.ReadTable(path, k, nt) as table:
             res = mx.experimental_batch(table, kc, k, None, regions, n_threads=nt)
             outs.append([repr((r.row, r.error, r.zero_lines)) for r in res])
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
 
 
 def test_unsorted_bam_rejected(tmp_path, lib_built):
