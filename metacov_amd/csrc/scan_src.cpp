@@ -31,9 +31,13 @@
 #include <zlib.h>
 
 #include <cctype>
+#include <cstdlib>
 #include <memory>
+#include <string>
+#include <thread>
 
 #include "bgzf.h"
+#include "common.h"
 
 using namespace mc::bgzf;
 
@@ -140,6 +144,18 @@ struct mc_scan_src {
     std::string line[4];
     bool sam_pending = false;
     int64_t sam_line = 0;
+    // the next window, inflated on a background thread while the current
+    // one is walked (bam_fill)
+    std::unique_ptr<uint8_t[]> nbuf;
+    size_t window = 256ull << 20;   // inflated bytes per window (MC_SCAN_WINDOW for tests)
+    size_t ncap = 0, ntotal = 0;
+    bool nlast = false;
+    std::thread prod;
+    int prc = 0;
+    std::string perr;
+    ~mc_scan_src() {
+        if (prod.joinable()) prod.join();
+    }
     // the batch handed out by mc_scan_src_next
     std::vector<int32_t> rlen, flag, gpos, gisize, tid;
     std::vector<int64_t> seq_off;
@@ -157,40 +173,73 @@ struct mc_scan_src {
 
 namespace {
 
-constexpr size_t kWindow = 256ull << 20;
+constexpr size_t kCarryRoom = 1 << 20;   // room before a window for the previous one's unfinished record
 
-// Inflates the next window of BGZF blocks after the unparsed tail.
-int bam_fill(mc_scan_src* s) {
-    const size_t carry = s->n - s->o;
+// Inflates the window of BGZF blocks after s->next_off into s->nbuf (after
+// kCarryRoom).  Runs on s->prod while the current window is walked.
+int bam_produce(mc_scan_src* s) {
     std::vector<Block> blocks;
     size_t total = 0;
-    while (s->next_off < s->mf.size && total < kWindow) {
+    while (s->next_off < s->mf.size && total < s->window) {
         const size_t b0 = blocks.size();
-        if (int rc = scan_blocks(s->mf.data, s->mf.size, s->next_off, s->next_off, blocks, total))
+        if (int rc = scan_blocks(s->mf.data, s->mf.size, s->next_off, s->next_off, blocks, total)) {
+            s->perr = mc::last_error();
             return rc;
+        }
         s->next_off = blocks[b0].cdata + blocks[b0].clen + 8;
     }
-    s->last = s->next_off >= s->mf.size;
-    if (carry + total + 8 > s->cap) {
-        const size_t ncap = std::max(carry + total + 8, s->cap + s->cap / 4);
-        std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[ncap]);
-        MC_REQUIRE(nb, MC_E_IO, "cannot allocate %zu bytes for %s", ncap, s->path.c_str());
-        if (carry) std::memcpy(nb.get(), s->buf.get() + s->o, carry);
-        s->buf = std::move(nb);
-        s->cap = ncap;
-    } else if (carry && s->o) {
-        std::memmove(s->buf.get(), s->buf.get() + s->o, carry);
+    s->nlast = s->next_off >= s->mf.size;
+    s->ntotal = total;
+    if (kCarryRoom + total + 8 > s->ncap) {
+        s->nbuf.reset(new (std::nothrow) uint8_t[kCarryRoom + total + 8]);
+        if (!s->nbuf) {
+            s->ncap = 0;
+            s->perr = "cannot allocate the read window for " + s->path;
+            return MC_E_IO;
+        }
+        s->ncap = kCarryRoom + total + 8;
     }
-    s->o = 0;
-    s->n = carry;
-    MC_REQUIRE(blocks.empty() || inflate_blocks(s->mf.data, blocks, s->buf.get() + carry, s->nt),
-               MC_E_IO, "BGZF inflate failed in %s", s->path.c_str());
-    s->n = carry + total;
+    if (!blocks.empty() && !inflate_blocks(s->mf.data, blocks, s->nbuf.get() + kCarryRoom, s->nt)) {
+        s->perr = "BGZF inflate failed in " + s->path;
+        return MC_E_IO;
+    }
+    return MC_OK;
+}
+
+// Moves to the next window: the unparsed tail of the current one goes in
+// front of it, and the window after it starts inflating in the background.
+int bam_fill(mc_scan_src* s) {
+    if (s->prod.joinable()) {
+        s->prod.join();
+    } else {
+        s->prc = bam_produce(s);
+    }
+    MC_REQUIRE(s->prc == MC_OK, s->prc, "%s", s->perr.c_str());
+    const size_t carry = s->n - s->o;
+    if (carry <= kCarryRoom) {
+        if (carry) std::memcpy(s->nbuf.get() + kCarryRoom - carry, s->buf.get() + s->o, carry);
+        std::swap(s->buf, s->nbuf);
+        std::swap(s->cap, s->ncap);
+        s->o = kCarryRoom - carry;
+        s->n = kCarryRoom + s->ntotal;
+    } else {   // (a carry longer than the room: one buffer with both)
+        const size_t need = carry + s->ntotal + 8;
+        std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[need]);
+        MC_REQUIRE(nb, MC_E_IO, "cannot allocate %zu bytes for %s", need, s->path.c_str());
+        std::memcpy(nb.get(), s->buf.get() + s->o, carry);
+        std::memcpy(nb.get() + carry, s->nbuf.get() + kCarryRoom, s->ntotal);
+        s->buf = std::move(nb);
+        s->cap = need;
+        s->o = 0;
+        s->n = carry + s->ntotal;
+    }
+    s->last = s->nlast;
+    if (!s->last) s->prod = std::thread([s] { s->prc = bam_produce(s); });
     if (!s->have_header) {
         size_t o = 0;
-        if (parse_header(s->buf.get(), s->n, s->path.c_str(), s->names, s->lens, &o) == MC_OK) {
+        if (parse_header(s->buf.get() + s->o, s->n - s->o, s->path.c_str(), s->names, s->lens, &o) == MC_OK) {
             s->have_header = true;
-            s->o = o;
+            s->o += o;
         } else {
             MC_REQUIRE(!s->last, MC_E_IO, "%s: no valid BAM header", s->path.c_str());
         }
@@ -430,6 +479,7 @@ extern "C" int mc_scan_src_open_bam(const char* path, int n_threads, mc_scan_src
     s->kind = 0;
     s->path = path;
     s->nt = n_threads_or_all(n_threads);
+    if (const char* e = std::getenv("MC_SCAN_WINDOW")) s->window = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
     if (int rc = s->mf.open(path)) return rc;
     while (!s->have_header) {
         if (int rc = bam_fill(s.get())) return rc;

@@ -184,9 +184,15 @@ def test_cpp_fastq_source_truncated_and_plain(tmp_path, lib_built):
         assert got == want
 
 
-def test_cpp_bam_source_matches_oracle(mix, golden_dir, lib_built):
-    """Every record in file order, with the ReadIterator accessor values."""
+@pytest.mark.parametrize("window", [None, "4096", "65536"])
+def test_cpp_bam_source_matches_oracle(mix, golden_dir, lib_built, window, monkeypatch):
+    """Every record in file order, with the ReadIterator accessor values; with
+    small windows (MC_SCAN_WINDOW) records straddle windows, each window is
+    inflated while the previous one is walked, and a 4 KiB window is smaller
+    than some headers (the unfinished header carried over)."""
     from metacov_amd import _lib
+    if window:
+        monkeypatch.setenv("MC_SCAN_WINDOW", window)
     lib = _lib.load()
     for path in (mix[0], os.path.join(golden_dir, "bbmap.sorted.bam"),
                  os.path.join(golden_dir, "synth_edge.bam")):
