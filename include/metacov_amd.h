@@ -368,6 +368,16 @@ int mc_bam_gpu_intervals_device(const mc_bam_gpu* g, int64_t* n, const int32_t**
 int mc_bam_gpu_intervals(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int32_t* span);
 int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t);
 int mc_bam_gpu_close(mc_bam_gpu* g);
+/* `metacov scan` input decoded on the GPU (the BAM half of scan.pyx:188-216,
+ * IteratorRowAll: every record in file order; replaces mc_scan_src_open_bam's
+ * host walk): the whole file as the SoA batch mc_scan_add_batch_device takes
+ * (rlen = l_seq, flag, gpos = pos [+ l_seq on the reverse strand], gisize =
+ * tlen when properly paired else 0, tid, packed nt16 bases at 4-byte aligned
+ * offsets seq_off[0..n]), left in device memory owned by the handle. */
+int mc_bam_gpu_open_scan(const char* path, int device, int n_threads, int64_t window_bytes, mc_bam_gpu** out);
+int mc_bam_gpu_scan_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_rlen, const int32_t** d_flag,
+                           const int32_t** d_gpos, const int32_t** d_gisize, const int32_t** d_tid,
+                           const int64_t** d_seq_off, const uint8_t** d_seq, int64_t* seq_bytes);
 /* One rank's contig shard decoded on the GPU ("each rank
  * decodes only its contigs' BGZF chunks, located via BAI virtual offsets";
  * replaces the per-contig indexed query under pysam's pileup(ref, start,
@@ -550,6 +560,10 @@ int mc_scan_add_batch_device(mc_scan* s, int64_t n, const int32_t* rlen, const i
                              int64_t max_abs_isize, float* kernel_ms);
 int mc_scan_run(mc_scan* s, mc_scan_src* src, int32_t n_map, const int32_t* tid_to_ref,
                 int64_t max_reads, int64_t batch_reads, int64_t* n_done);
+/* mc_scan_run over a BAM decoded on the GPU (mc_bam_gpu_open_scan): the same
+ * reads and reference-id rule, the whole file as one device batch. */
+int mc_scan_run_gpu(mc_scan* s, const mc_bam_gpu* g, int32_t n_map, const int32_t* tid_to_ref,
+                    int64_t max_reads, int64_t* n_done);
 int mc_scan_dims(mc_scan* s, int32_t* groups, int64_t* base_rows, int64_t* isize_cap,
                  int32_t* max_rlen, int64_t* n_reads);
 int mc_scan_results(mc_scan* s, uint32_t* base, uint32_t* kmer, uint32_t* mirror,

@@ -139,6 +139,8 @@ SIGNATURES = {
     "mc_bam_gpu_intervals": [_P, _P, _P, _P],
     "mc_bam_gpu_stats": [_P, _P],
     "mc_bam_gpu_close": [_P],
+    "mc_bam_gpu_open_scan": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _I64, _PP],
+    "mc_bam_gpu_scan_device": [_P, _PI64, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PI64],
     "mc_bam_index_extents": [ctypes.c_char_p, _I32, _P, _PI64],
     "mc_bam_gpu_open_contigs": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _U32, _I32, _P,
                                 _PP],
@@ -181,6 +183,7 @@ SIGNATURES = {
     "mc_scan_add_batch_device": [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _I64,
                                  ctypes.POINTER(ctypes.c_float)],
     "mc_scan_run": [_P, _P, _I32, _P, _I64, _I64, _PI64],
+    "mc_scan_run_gpu": [_P, _P, _I32, _P, _I64, _PI64],
     "mc_scan_dims": [_P, _PI32, _PI64, _PI64, _PI32, _PI64],
     "mc_scan_results": [_P, _P, _P, _P, _P, _P],
     "mc_scan_timing": [_P, ctypes.POINTER(ctypes.c_float), _PI64],

@@ -66,6 +66,7 @@ struct SegRes {
     int64_t landing;  // first record boundary at or past the next segment's start (or where the walk stopped)
     int64_t records, mapped, kept;
     int64_t err_at;
+    int64_t bytes;    // scan mode: the kept records' sequence bytes, each record's rounded up to 4
     int32_t err;      // 0, kSegIncomplete, or an error class
     int32_t pad;
 };
@@ -76,6 +77,7 @@ enum : int32_t {
     kSegTid = 3,          // rec_parse 2
     kSegCigar = 4,        // rec_parse 3
     kSegSpan = 5,         // rec_parse 4
+    kSegMalformed = 6,    // scan mode: l_seq < 0, SEQ past the record, or tid out of range
 };
 
 // One wave per workgroup; a wave inflates kGzLanes blocks at a time, each
@@ -267,6 +269,98 @@ rec_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restr
         s.mapped = mapped;
         s.kept = kept;
         s.err_at = err_at;
+        s.bytes = 0;
+        s.err = err;
+        s.pad = 0;
+        res[i] = s;
+    }
+}
+
+// Scan mode (`metacov scan` on BAM input, scan_src.cpp's bam_next on the
+// device): every record is kept, in file order, as the SoA batch the scan
+// kernels take: rlen (l_seq), flag, gpos (pos + l_seq on the reverse strand),
+// gisize (tlen when properly paired, else 0), tid, and its packed nt16 bases
+// at a 4-byte aligned offset (seq_off[k + 1] = the aligned end of record k).
+// One lane per segment, as rec_walk_kernel.
+template <bool kFill>
+__global__ void __launch_bounds__(256)
+scan_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restrict__ seg_off, int64_t first,
+                 int64_t nseg, int32_t n_ref, SegRes* __restrict__ res, const int64_t* __restrict__ out_off,
+                 const int64_t* __restrict__ byte_off, int32_t* __restrict__ rlen, int32_t* __restrict__ flag,
+                 int32_t* __restrict__ gpos, int32_t* __restrict__ gisize, int32_t* __restrict__ tid,
+                 int64_t* __restrict__ seq_off, uint8_t* __restrict__ seq) {
+    const int64_t i = first + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nseg) return;
+    int64_t q = seg_off[i];
+    const int64_t end = seg_off[i + 1];
+    int64_t records = 0, mapped = 0, bytes = 0, err_at = 0;
+    int32_t err = 0;
+    int64_t w = 0, w_end = 0, b = 0;
+    if (kFill) {
+        w = out_off[i];
+        w_end = w + res[i].kept;
+        b = byte_off[i];
+    }
+    while (q < end) {
+        if (q + 4 > n) {
+            err = kSegIncomplete;
+            break;
+        }
+        const int32_t bs = mc::gz::ld_i32(d + q);
+        if (bs < 32) {
+            err = kSegBadSize;
+            err_at = q;
+            break;
+        }
+        if (q + 4 + (int64_t)bs > n) {
+            err = kSegIncomplete;
+            break;
+        }
+        const uint8_t* r = d + q + 4;
+        const int32_t t = mc::gz::ld_i32(r), pos = mc::gz::ld_i32(r + 4);
+        const uint32_t l_name = r[8], n_cigar = mc::gz::ld_u16(r + 12), fl = mc::gz::ld_u16(r + 14);
+        const int32_t l_seq = mc::gz::ld_i32(r + 16), tlen = mc::gz::ld_i32(r + 28);
+        const int64_t seq_at = 32 + (int64_t)l_name + 4 * (int64_t)n_cigar;
+        const int64_t nbytes = ((int64_t)(l_seq > 0 ? l_seq : 0) + 1) / 2;
+        if (l_seq < 0 || seq_at + nbytes > bs || t < -1 || t >= n_ref) {
+            err = kSegMalformed;
+            err_at = q;
+            break;
+        }
+        q += 4 + (int64_t)bs;
+        ++records;
+        mapped += (t >= 0 && !(fl & 4u)) ? 1 : 0;
+        const int64_t al = (nbytes + 3) & ~(int64_t)3;
+        bytes += al;
+        if (kFill && w < w_end) {
+            rlen[w] = l_seq;
+            flag[w] = (int32_t)fl;
+            gpos[w] = (fl & 0x10u) ? pos + l_seq : pos;
+            gisize[w] = (fl & 0x2u) ? tlen : 0;
+            tid[w] = t;
+            // the bases, dword by dword (the source is byte-aligned)
+            const uint8_t* src = r + seq_at;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(seq + b);
+            for (int64_t k = 0; k < al; k += 4) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (k + e < nbytes) v |= (uint32_t)src[k + e] << (8 * e);
+                dst[k >> 2] = v;
+            }
+            b += al;
+            seq_off[w + 1] = b;
+            ++w;
+        }
+    }
+    if (!kFill) {
+        SegRes s;
+        s.landing = q;
+        s.records = records;
+        s.mapped = mapped;
+        s.kept = records;
+        s.err_at = err_at;
+        s.bytes = bytes;
         s.err = err;
         s.pad = 0;
         res[i] = s;
@@ -342,8 +436,14 @@ struct mc_bam_gpu {
     hipStream_t stream = nullptr;
     int nt = 16;
     uint32_t flag_filter = 0;
-    DBuf<int32_t> tid, pos, span;     // kept intervals, file order
+    DBuf<int32_t> tid, pos, span;     // kept intervals, file order (scan mode: tid, gpos, rlen)
     int64_t n_kept = 0;
+    bool scan_mode = false;           // every record as scan's SoA batch (scan_walk_kernel)
+    DBuf<int32_t> sflag, sgisize;     // scan mode: flag, gisize
+    DBuf<int64_t> soff;               // scan mode: [n_kept + 1] aligned sequence offsets
+    DBuf<uint8_t> sseq;               // scan mode: packed nt16 bases
+    DBuf<int64_t> boff;               // scan mode: per-segment byte offsets of the fill
+    int64_t n_bytes = 0;
     DBuf<uint8_t> comp[2], inflated, tail;   // comp: window k's compressed bytes in comp[k & 1]
     hipStream_t up_stream = nullptr;          // uploads of the next window (overlap the current one's kernels)
     hipStream_t kstream[3] = {};              // resident decode: inflate streams besides `stream`
@@ -387,6 +487,7 @@ const char* seg_err_msg(int32_t e) {
         case kSegBadSize: return "bad record size";
         case kSegTid: return "record tid beyond the reference list";
         case kSegCigar: return "CIGAR overruns record";
+        case kSegMalformed: return "malformed record";
         default: return "reference span exceeds int32";
     }
 }
@@ -604,7 +705,7 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     HIP_TRY(g->found.reserve(nseg + 1));
     HIP_TRY(g->out_off.reserve(nseg + 1));
     HIP_TRY(g->res.reserve(nseg));
-    HIP_TRY(g->h64.reserve(nseg + 1));
+    HIP_TRY(g->h64.reserve(2 * (nseg + 1)));   // (scan mode: the byte offsets after the record offsets)
     HIP_TRY(g->hres.reserve(nseg));
     int64_t* h = g->h64.p;
     std::vector<int64_t> seg(nseg + 1, n);
@@ -629,9 +730,14 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
         std::memcpy(h, seg.data() + first, (nseg + 1 - first) * 8);
         HIP_TRY(hipMemcpyAsync(g->seg_off.p + first, h, (nseg + 1 - first) * 8, hipMemcpyHostToDevice, st));
         const int grid = (int)((nseg - first + 255) / 256);
-        rec_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->flag_filter,
-                                                     g->res.p, nullptr, nullptr, nullptr, nullptr,
-                                                     g->tid_map.p, nullptr, 0);
+        if (g->scan_mode)
+            scan_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->res.p, nullptr,
+                                                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                          nullptr, nullptr);
+        else
+            rec_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->flag_filter,
+                                                         g->res.p, nullptr, nullptr, nullptr, nullptr,
+                                                         g->tid_map.p, nullptr, 0);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(R + first, g->res.p + first, (nseg - first) * sizeof(SegRes),
                                hipMemcpyDeviceToHost, st));
@@ -692,22 +798,25 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
         }
     }
     // segments after an incomplete stop are empty; their results may be stale
-    int64_t total = 0, records = 0, mapped = 0, tail = n;
-    std::vector<int64_t> koff(nseg + 1);
+    int64_t total = 0, records = 0, mapped = 0, tail = n, bytes = 0;
+    std::vector<int64_t> koff(nseg + 1), bo(nseg + 1);
     for (int64_t i = 0; i < nseg; ++i) {
         SegRes& r = R[i];
         if (seg[i] >= seg[i + 1] && seg[i] == n) {   // empty tail segment
-            r.kept = r.records = r.mapped = 0;
+            r.kept = r.records = r.mapped = r.bytes = 0;
         }
         koff[i] = g->n_kept + total;
+        bo[i] = g->n_bytes + bytes;
         total += r.kept;
+        bytes += r.bytes;
         records += r.records;
         mapped += r.mapped;
         if (r.err == kSegIncomplete) {
             tail = r.landing;
             for (int64_t j = i + 1; j < nseg; ++j) {
                 koff[j] = g->n_kept + total;
-                R[j].kept = R[j].records = R[j].mapped = 0;
+                bo[j] = g->n_bytes + bytes;
+                R[j].kept = R[j].records = R[j].mapped = R[j].bytes = 0;
             }
             break;
         }
@@ -721,7 +830,23 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     HIP_TRY(g->tid.reserve(need, st, g->n_kept));
     HIP_TRY(g->pos.reserve(need, st, g->n_kept));
     HIP_TRY(g->span.reserve(need, st, g->n_kept));
-    if (total || g->ext.p) {
+    if (g->scan_mode) {
+        HIP_TRY(g->sflag.reserve(need, st, g->n_kept));
+        HIP_TRY(g->sgisize.reserve(need, st, g->n_kept));
+        HIP_TRY(g->soff.reserve(need + 1, st, g->n_kept + 1));
+        HIP_TRY(g->sseq.reserve((size_t)(g->n_bytes + bytes) + 16, st, (size_t)g->n_bytes));
+        HIP_TRY(g->boff.reserve(nseg + 1));
+        if (g->n_kept == 0) HIP_TRY(hipMemsetAsync(g->soff.p, 0, 8, st));
+        std::memcpy(h + nseg + 1, bo.data(), nseg * 8);
+        HIP_TRY(hipMemcpyAsync(g->boff.p, h + nseg + 1, nseg * 8, hipMemcpyHostToDevice, st));
+        if (total) {
+            const int grid = (int)((nseg + 255) / 256);
+            scan_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->res.p, g->out_off.p,
+                                                         g->boff.p, g->span.p, g->sflag.p, g->pos.p, g->sgisize.p,
+                                                         g->tid.p, g->soff.p, g->sseq.p);
+            HIP_TRY(hipGetLastError());
+        }
+    } else if (total || g->ext.p) {
         const int grid = (int)((nseg + 255) / 256);
         rec_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->flag_filter, g->res.p,
                                                     g->out_off.p, g->tid.p, g->pos.p, g->span.p, g->tid_map.p,
@@ -730,6 +855,7 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     }
     HIP_TRY(hipStreamSynchronize(st));
     g->n_kept += total;
+    g->n_bytes += bytes;
     g->hdr.n_records += records;
     g->hdr.n_mapped += mapped;
     g->hdr.n_unmapped += records - mapped;
@@ -1145,6 +1271,7 @@ int inflate_resident(mc_bam_gpu* g, int fd, const VMap* vm, size_t vsize, const 
 
 // The per-contig table of the record walk, zeroed (n_ref + 1 entries).
 int init_ext(mc_bam_gpu* g) {
+    if (g->scan_mode) return MC_OK;   // (no extents table: every record is kept)
     const size_t m = g->hdr.names.size() + 1;
     HIP_TRY(g->ext.reserve(m));
     HIP_TRY(hipMemsetAsync(g->ext.p, 0, m * sizeof(ExtAcc), g->stream));
@@ -1682,6 +1809,39 @@ extern "C" int mc_bam_gpu_open(const char* path, int device, int n_threads, uint
     // (the staging and parse buffers go with the handle: a hipFree of the
     // multi-GB windows here sat on the open's critical path)
     *out = g.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_open_scan(const char* path, int device, int n_threads, int64_t window_bytes,
+                                    mc_bam_gpu** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<mc_bam_gpu> g;
+    if (int rc = open_common(path, device, n_threads, 0, g)) return rc;
+    g->scan_mode = true;
+    const double t0 = now_s();
+    if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
+    g->t_open = (now_s() - t0) * 1e3;
+    *out = g.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_scan_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_rlen,
+                                      const int32_t** d_flag, const int32_t** d_gpos, const int32_t** d_gisize,
+                                      const int32_t** d_tid, const int64_t** d_seq_off, const uint8_t** d_seq,
+                                      int64_t* seq_bytes) {
+    MC_REQUIRE(g && n && d_rlen && d_flag && d_gpos && d_gisize && d_tid && d_seq_off && d_seq && seq_bytes,
+               MC_E_INVALID, "null argument");
+    MC_REQUIRE(g->scan_mode, MC_E_STATE, "not a scan-mode decode (mc_bam_gpu_open_scan)");
+    *n = g->n_kept;
+    *d_rlen = g->span.p;
+    *d_flag = g->sflag.p;
+    *d_gpos = g->pos.p;
+    *d_gisize = g->sgisize.p;
+    *d_tid = g->tid.p;
+    *d_seq_off = g->soff.p;
+    *d_seq = g->sseq.p;
+    *seq_bytes = g->n_bytes;
     return MC_OK;
 }
 

@@ -42,6 +42,7 @@
 // (count_bases_pairs).  KmerHist codes go to HBM and kmer_count_kernel counts
 // them in LDS tables (global atomics for K >= 8).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -842,6 +843,38 @@ __global__ __launch_bounds__(kKmerThreads) void kmer_count_kernel(
     }
 }
 
+// mc_scan_run_gpu: idx[i] = i when read i's tid maps to a loaded sequence,
+// else -1 (then an inclusive max-scan gives each read the latest such read at
+// or before it), and the batch's longest read / largest |insert size|.
+__global__ void ref_idx_kernel(const int32_t* __restrict__ tid, int64_t n, const int32_t* __restrict__ map,
+                               int32_t n_map, int64_t* __restrict__ idx, const int32_t* __restrict__ rlen,
+                               const int32_t* __restrict__ gisize, int* __restrict__ maxes) {
+    int mr = 0, mi = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t t = tid[i];
+        idx[i] = (t >= 0 && t < n_map && map[t] >= 0) ? i : -1;
+        mr = max(mr, rlen[i]);
+        const int32_t v = gisize[i];
+        mi = max(mi, v < 0 ? -v : v);   // (|INT_MIN| overflows: such a read is out of range anyway)
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        mr = max(mr, __shfl_xor(mr, d, 64));
+        mi = max(mi, __shfl_xor(mi, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(maxes, mr);
+        atomicMax(maxes + 1, mi);
+    }
+}
+
+__global__ void ref_fill_kernel(const int64_t* __restrict__ last, const int32_t* __restrict__ tid, int64_t n,
+                                const int32_t* __restrict__ map, int32_t* __restrict__ ref_id) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = last[i];
+        ref_id[i] = j >= 0 ? map[tid[j]] : -1;
+    }
+}
+
 // nt4 of FASTA bytes (iupac_to_nt4, scan.pyx:37-60)
 __global__ void ascii_nt4_kernel(uint8_t* p, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -913,6 +946,9 @@ struct mc_scan {
     Dev<int64_t> ref_off, ref_len;
     Dev<int32_t> error;
     Dev<uint32_t> work;         // scan_kernel's slice queue
+    Dev<int64_t> ridx;          // mc_scan_run_gpu: the forward-fill scan
+    Dev<int32_t> rid, rmap, rmax;
+    Dev<uint8_t> rtemp;
     Dev<uint16_t> kcodes, kgroup;
     int cus = 1;
     int32_t n_ref = 0;
@@ -1314,6 +1350,53 @@ extern "C" int mc_scan_run(mc_scan* s, mc_scan_src* src, int32_t n_map, const in
         *n_done += n;
     }
     HIP_TRY(hipStreamSynchronize(s->stream));
+    return MC_OK;
+}
+
+// The same run over a BAM decoded on the GPU (mc_bam_gpu_open_scan): the
+// whole file is one device-resident batch; the reference ids are forward-
+// filled on the device (an inclusive max-scan of "latest read whose tid has
+// a sequence"), as mc_scan_run does on the host.
+extern "C" int mc_scan_run_gpu(mc_scan* s, const mc_bam_gpu* g, int32_t n_map, const int32_t* tid_to_ref,
+                               int64_t max_reads, int64_t* n_done) {
+    MC_REQUIRE(s && g && n_done && n_map >= 0 && (n_map == 0 || tid_to_ref), MC_E_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(s->device));
+    *n_done = 0;
+    int64_t n = 0, nbytes = 0;
+    const int32_t *rlen, *flag, *gpos, *gisize, *tid;
+    const int64_t* seq_off;
+    const uint8_t* seq;
+    if (int rc = mc_bam_gpu_scan_device(g, &n, &rlen, &flag, &gpos, &gisize, &tid, &seq_off, &seq, &nbytes))
+        return rc;
+    if (max_reads > 0) n = std::min(n, max_reads);
+    if (n == 0) return MC_OK;
+    MC_REQUIRE(n < INT32_MAX, MC_E_RANGE, "%lld records in one GPU-decoded batch (the scan takes int32 counts)",
+               (long long)n);
+    hipStream_t st = s->stream;
+    HIP_TRY(s->ridx.reserve((size_t)n));
+    HIP_TRY(s->rid.reserve((size_t)n));
+    HIP_TRY(s->rmap.reserve((size_t)std::max(n_map, 1)));
+    HIP_TRY(s->rmax.reserve(2));
+    if (n_map) HIP_TRY(hipMemcpyAsync(s->rmap.p, tid_to_ref, (size_t)n_map * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(s->rmax.p, 0, 8, st));
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)s->cus * 8);
+    hipLaunchKernelGGL(ref_idx_kernel, dim3(grid), dim3(256), 0, st, tid, n, s->rmap.p, n_map, s->ridx.p, rlen,
+                       gisize, s->rmax.p);
+    HIP_TRY(hipGetLastError());
+    size_t temp = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, temp, s->ridx.p, s->ridx.p, hipcub::Max(), (int)n, st));
+    HIP_TRY(s->rtemp.reserve(temp + 16));
+    HIP_TRY(hipcub::DeviceScan::InclusiveScan(s->rtemp.p, temp, s->ridx.p, s->ridx.p, hipcub::Max(), (int)n, st));
+    hipLaunchKernelGGL(ref_fill_kernel, dim3(grid), dim3(256), 0, st, s->ridx.p, tid, n, s->rmap.p, s->rid.p);
+    HIP_TRY(hipGetLastError());
+    int mx[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(mx, s->rmax.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = mc_scan_add_batch_device(s, n, rlen, flag, gpos, gisize, s->rid.p, seq_off, seq, mx[0], mx[1],
+                                          nullptr))
+        return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    *n_done = n;
     return MC_OK;
 }
 

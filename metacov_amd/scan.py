@@ -273,9 +273,10 @@ def _groups(counters):
     return flags, out
 
 
-def _source(lib, infile, n_threads):
-    """(mc_scan_src handle, kind) for a path, a pyfq FastQFile / FastQFilePair
-    or an object with .filename (pysam AlignmentFile)."""
+def _source(lib, infile, n_threads, decode="host", device=0):
+    """(handle, kind) for a path, a pyfq FastQFile / FastQFilePair or an
+    object with .filename (pysam AlignmentFile): an mc_scan_src, or for a BAM
+    with decode="gpu" an mc_bam_gpu decoded on `device` (kind "gbam")."""
     from . import pyfq
     h = ctypes.c_void_p()
     if isinstance(infile, pyfq.FastQFilePair):
@@ -297,6 +298,11 @@ def _source(lib, infile, n_threads):
     if is_sam(path):   # pysam tells SAM from BAM by content, whatever the name
         _lib.check(lib.mc_scan_src_open_sam(path.encode(), ctypes.byref(h)), lib)
         return h, "bam"
+    if decode == "gpu":
+        window = int(os.environ.get("MC_SCAN_GPU_WINDOW", "0"))   # (tests: force the windowed decode)
+        _lib.check(lib.mc_bam_gpu_open_scan(path.encode(), int(device), int(n_threads), window, ctypes.byref(h)),
+                   lib)
+        return h, "gbam"
     _lib.check(lib.mc_scan_src_open_bam(path.encode(), n_threads, ctypes.byref(h)), lib)
     return h, "bam"
 
@@ -344,13 +350,18 @@ def _config(flags, leaves):
 
 
 def scan_reads(infile, fasta, counters, progress_interval=10000000, progress_cb=None,
-               maxreads=0, device=0, n_threads=0, batch_reads=1 << 21):
+               maxreads=0, device=0, n_threads=0, batch_reads=1 << 21, decode=None):
     """scan.pyx:623-672: runs `counters` over every read of `infile` (a BAM
     path / pysam-like object with .filename, a FASTQ path, or a pyfq
     FastQFile / FastQFilePair) and returns the number of reads processed.
     `fasta` (path or experimental.FastaFile) supplies the reference for
     BaseHist / MirrorHist.  progress_cb is called once per progress_interval
-    reads, after the GPU pass."""
+    reads, after the GPU pass.  decode: "gpu" (default; MC_SCAN_DECODE
+    overrides) inflates and walks a BAM on the GPU, "host" with the C++
+    source (SAM and FASTQ always take the host source)."""
+    decode = decode or os.environ.get("MC_SCAN_DECODE", "gpu")
+    if decode not in ("gpu", "host"):
+        raise ValueError("decode must be 'gpu' or 'host'")
     lib = _lib.load()
     flags, groups = _groups(counters)
     if len(flags) > 11:
@@ -374,29 +385,42 @@ def scan_reads(infile, fasta, counters, progress_interval=10000000, progress_cb=
                     sel.append(p)
             per_group.append(sel)
         nreads = _run_layer(lib, infile, fa, flags, per_group, maxreads, device, n_threads,
-                            batch_reads)
+                            batch_reads, decode)
     if progress_cb and progress_interval > 0:
         for _ in range(nreads // progress_interval):
             progress_cb()
     return nreads
 
 
-def _run_layer(lib, infile, fa, flags, per_group, maxreads, device, n_threads, batch_reads):
-    src, kind = _source(lib, infile, n_threads)
+def _target_names(lib, src, kind):
+    if kind == "gbam":
+        from .bam import _header_of
+        hdr = ctypes.c_void_p()
+        _lib.check(lib.mc_bam_gpu_header(src, ctypes.byref(hdr)), lib)
+        return list(_header_of(lib, hdr)[0])
+    n_t = ctypes.c_int32()
+    _lib.check(lib.mc_scan_src_n_targets(src, ctypes.byref(n_t)), lib)
+    name = ctypes.c_char_p()
+    ln = ctypes.c_int64()
+    names = []
+    for t in range(n_t.value):
+        _lib.check(lib.mc_scan_src_target(src, t, ctypes.byref(name), ctypes.byref(ln)), lib)
+        names.append(name.value.decode())
+    return names
+
+
+def _run_layer(lib, infile, fa, flags, per_group, maxreads, device, n_threads, batch_reads, decode="host"):
+    src, kind = _source(lib, infile, n_threads, decode, device)
     scan = ctypes.c_void_p()
     try:
         cfg = _config(flags, per_group[0])
         _lib.check(lib.mc_scan_create(device, ctypes.byref(cfg), ctypes.byref(scan)), lib)
         tid_map = np.zeros(0, np.int32)
-        if fa is not None and kind == "bam":
-            n_t = ctypes.c_int32()
-            _lib.check(lib.mc_scan_src_n_targets(src, ctypes.byref(n_t)), lib)
-            tid_map = np.full(n_t.value, -1, np.int32)
-            name = ctypes.c_char_p()
-            ln = ctypes.c_int64()
-            for t in range(n_t.value):
-                _lib.check(lib.mc_scan_src_target(src, t, ctypes.byref(name), ctypes.byref(ln)), lib)
-                i = fa._index.get(name.value.decode())
+        if fa is not None and kind in ("bam", "gbam"):
+            names = _target_names(lib, src, kind)
+            tid_map = np.full(len(names), -1, np.int32)
+            for t, nm in enumerate(names):
+                i = fa._index.get(nm)
                 if i is not None and fa.lengths[i] > 0:
                     tid_map[t] = i
             off = np.ascontiguousarray(fa._off, np.int64)
@@ -405,14 +429,21 @@ def _run_layer(lib, infile, fa, flags, per_group, maxreads, device, n_threads, b
             _lib.check(lib.mc_scan_set_reference(scan, len(lens), _lib.ptr(off), _lib.ptr(lens),
                                                  buf.size, _lib.ptr(buf)), lib)
         done = ctypes.c_int64()
-        _lib.check(lib.mc_scan_run(scan, src, tid_map.size, _lib.ptr(tid_map), int(maxreads or 0),
-                                   int(batch_reads), ctypes.byref(done)), lib)
+        if kind == "gbam":
+            _lib.check(lib.mc_scan_run_gpu(scan, src, tid_map.size, _lib.ptr(tid_map), int(maxreads or 0),
+                                           ctypes.byref(done)), lib)
+        else:
+            _lib.check(lib.mc_scan_run(scan, src, tid_map.size, _lib.ptr(tid_map), int(maxreads or 0),
+                                       int(batch_reads), ctypes.byref(done)), lib)
         _collect(lib, scan, cfg, per_group)
         return done.value
     finally:
         if scan:
             lib.mc_scan_destroy(scan)
-        lib.mc_scan_src_close(src)
+        if kind == "gbam":
+            lib.mc_bam_gpu_close(src)
+        else:
+            lib.mc_scan_src_close(src)
 
 
 def _collect(lib, scan, cfg, per_group):

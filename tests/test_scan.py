@@ -724,3 +724,39 @@ def test_scan_kernel_queue_and_cuts_vs_c_port_gpu(lib_built):
     for a, b in zip(got, want):
         assert np.array_equal(a, b)
     assert got[0][:, :, :4].sum() > 0.5 * (rlen.sum())   # most reads passed BaseHist's test
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [None, "65536"])
+def test_scan_gpu_decode_equals_host_source_gpu(mix, golden_dir, lib_built, tmp_path, window, monkeypatch):
+    """scan_reads with the BAM decoded on the GPU (mc_bam_gpu_open_scan +
+    mc_scan_run_gpu: every record, the reference ids forward-filled on the
+    device) gives the host source's tables; a 64 KiB decode window takes the
+    windowed path (records cut at every window end).  The BAMs: the mix (with
+    a FASTA), the reference's bbmap BAM, the edge-case BAM, and a 355 K-read
+    sorted BAM on three contigs."""
+    from metacov_amd import scan as mscan
+    if window:
+        monkeypatch.setenv("MC_SCAN_GPU_WINDOW", window)
+    bam, fa = mix
+    big = str(tmp_path / "big.bam")
+    rng = np.random.default_rng(8)
+    lens = [300_000, 2_000_000, 40_000]
+    arrs = synth.edge_mix_arrays(np.array(lens, np.int64), 120_000, seed=8,
+                                 weights=np.array([5.0, 1.0, 2.0]))
+    synth.write_bam_fast(big, ["a", "b", "c"], np.array(lens, np.int64), *arrs, level=1, n_threads=4)
+    big_fa = str(tmp_path / "big.fa")
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    synth.write_fasta(big_fa, {n: acgt[rng.integers(0, 4, L)].tobytes().decode() for n, L in zip("ab", lens)})
+    cases = [(bam, fa), (os.path.join(golden_dir, "bbmap.sorted.bam"), None),
+             (os.path.join(golden_dir, "synth_edge.bam"), None), (big, big_fa)]
+    for path, fasta in cases:
+        outs = []
+        for decode in ("host", "gpu"):
+            c = mscan.ByFlag([mscan.BaseHist(2), mscan.KmerHist(5, 6, 4, 1), mscan.MirrorHist(4, 10),
+                              mscan.IsizeHist()], [mscan.Flags["IsRead1"], mscan.Flags["Readdir"]])
+            n = mscan.scan_reads(path, fasta, c, decode=decode)
+            rows = [[list(map(str, r)) for r in q.get_rows()] for g in c.processors for q in g.processors]
+            outs.append((n, rows))
+        assert outs[0][0] == outs[1][0] and outs[0][0] > 0, path
+        assert outs[0][1] == outs[1][1], path
