@@ -45,6 +45,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -867,11 +868,12 @@ __global__ void ref_idx_kernel(const int32_t* __restrict__ tid, int64_t n, const
     }
 }
 
+// carry: the reference id in force before this chunk of reads (-1: none)
 __global__ void ref_fill_kernel(const int64_t* __restrict__ last, const int32_t* __restrict__ tid, int64_t n,
-                                const int32_t* __restrict__ map, int32_t* __restrict__ ref_id) {
+                                const int32_t* __restrict__ map, int32_t carry, int32_t* __restrict__ ref_id) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = last[i];
-        ref_id[i] = j >= 0 ? map[tid[j]] : -1;
+        ref_id[i] = j >= 0 ? map[tid[j]] : carry;
     }
 }
 
@@ -1369,34 +1371,44 @@ extern "C" int mc_scan_run_gpu(mc_scan* s, const mc_bam_gpu* g, int32_t n_map, c
     if (int rc = mc_bam_gpu_scan_device(g, &n, &rlen, &flag, &gpos, &gisize, &tid, &seq_off, &seq, &nbytes))
         return rc;
     if (max_reads > 0) n = std::min(n, max_reads);
-    if (n == 0) return MC_OK;
-    MC_REQUIRE(n < INT32_MAX, MC_E_RANGE, "%lld records in one GPU-decoded batch (the scan takes int32 counts)",
-               (long long)n);
     hipStream_t st = s->stream;
-    HIP_TRY(s->ridx.reserve((size_t)n));
-    HIP_TRY(s->rid.reserve((size_t)n));
-    HIP_TRY(s->rmap.reserve((size_t)std::max(n_map, 1)));
-    HIP_TRY(s->rmax.reserve(2));
-    if (n_map) HIP_TRY(hipMemcpyAsync(s->rmap.p, tid_to_ref, (size_t)n_map * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(s->rmax.p, 0, 8, st));
-    const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)s->cus * 8);
-    hipLaunchKernelGGL(ref_idx_kernel, dim3(grid), dim3(256), 0, st, tid, n, s->rmap.p, n_map, s->ridx.p, rlen,
-                       gisize, s->rmax.p);
-    HIP_TRY(hipGetLastError());
-    size_t temp = 0;
-    HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, temp, s->ridx.p, s->ridx.p, hipcub::Max(), (int)n, st));
-    HIP_TRY(s->rtemp.reserve(temp + 16));
-    HIP_TRY(hipcub::DeviceScan::InclusiveScan(s->rtemp.p, temp, s->ridx.p, s->ridx.p, hipcub::Max(), (int)n, st));
-    hipLaunchKernelGGL(ref_fill_kernel, dim3(grid), dim3(256), 0, st, s->ridx.p, tid, n, s->rmap.p, s->rid.p);
-    HIP_TRY(hipGetLastError());
-    int mx[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(mx, s->rmax.p, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (int rc = mc_scan_add_batch_device(s, n, rlen, flag, gpos, gisize, s->rid.p, seq_off, seq, mx[0], mx[1],
-                                          nullptr))
-        return rc;
-    HIP_TRY(hipStreamSynchronize(st));
-    *n_done = n;
+    // in chunks of up to 2^30 reads (the scan's counts are int32); the
+    // forward fill carries the reference id in force across chunks
+    int64_t kChunk = int64_t(1) << 30;
+    if (const char* e = std::getenv("MC_SCAN_RUN_CHUNK")) kChunk = std::max<int64_t>(1, std::atoll(e));   // (tests)
+    const int64_t cmax = std::min(n, kChunk);
+    if (n > 0) {
+        HIP_TRY(s->ridx.reserve((size_t)cmax));
+        HIP_TRY(s->rid.reserve((size_t)cmax));
+        HIP_TRY(s->rmap.reserve((size_t)std::max(n_map, 1)));
+        HIP_TRY(s->rmax.reserve(2));
+        if (n_map) HIP_TRY(hipMemcpyAsync(s->rmap.p, tid_to_ref, (size_t)n_map * 4, hipMemcpyHostToDevice, st));
+    }
+    int32_t carry = -1;
+    for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
+        const int64_t m = std::min(kChunk, n - c0);
+        HIP_TRY(hipMemsetAsync(s->rmax.p, 0, 8, st));
+        const int grid = (int)std::min<int64_t>((m + 255) / 256, (int64_t)s->cus * 8);
+        hipLaunchKernelGGL(ref_idx_kernel, dim3(grid), dim3(256), 0, st, tid + c0, m, s->rmap.p, n_map, s->ridx.p,
+                           rlen + c0, gisize + c0, s->rmax.p);
+        HIP_TRY(hipGetLastError());
+        size_t temp = 0;
+        HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, temp, s->ridx.p, s->ridx.p, hipcub::Max(), (int)m, st));
+        HIP_TRY(s->rtemp.reserve(temp + 16));
+        HIP_TRY(hipcub::DeviceScan::InclusiveScan(s->rtemp.p, temp, s->ridx.p, s->ridx.p, hipcub::Max(), (int)m, st));
+        hipLaunchKernelGGL(ref_fill_kernel, dim3(grid), dim3(256), 0, st, s->ridx.p, tid + c0, m, s->rmap.p, carry,
+                           s->rid.p);
+        HIP_TRY(hipGetLastError());
+        int mx[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(mx, s->rmax.p, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&carry, s->rid.p + (m - 1), 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = mc_scan_add_batch_device(s, m, rlen + c0, flag + c0, gpos + c0, gisize + c0, s->rid.p,
+                                              seq_off + c0, seq, mx[0], mx[1], nullptr))
+            return rc;
+        HIP_TRY(hipStreamSynchronize(st));   // (ridx / rid are reused by the next chunk)
+        *n_done += m;
+    }
     return MC_OK;
 }
 

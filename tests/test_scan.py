@@ -727,8 +727,8 @@ def test_scan_kernel_queue_and_cuts_vs_c_port_gpu(lib_built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("window", [None, "65536"])
-def test_scan_gpu_decode_equals_host_source_gpu(mix, golden_dir, lib_built, tmp_path, window, monkeypatch):
+@pytest.mark.parametrize("window, chunk", [(None, None), ("65536", None), (None, "9999")])
+def test_scan_gpu_decode_equals_host_source_gpu(mix, golden_dir, lib_built, tmp_path, window, chunk, monkeypatch):
     """scan_reads with the BAM decoded on the GPU (mc_bam_gpu_open_scan +
     mc_scan_run_gpu: every record, the reference ids forward-filled on the
     device) gives the host source's tables; a 64 KiB decode window takes the
@@ -738,6 +738,8 @@ def test_scan_gpu_decode_equals_host_source_gpu(mix, golden_dir, lib_built, tmp_
     from metacov_amd import scan as mscan
     if window:
         monkeypatch.setenv("MC_SCAN_GPU_WINDOW", window)
+    if chunk:   # the device run in chunks of 9999 reads (the reference id carried across them)
+        monkeypatch.setenv("MC_SCAN_RUN_CHUNK", chunk)
     bam, fa = mix
     big = str(tmp_path / "big.bam")
     rng = np.random.default_rng(8)
