@@ -378,6 +378,23 @@ int mc_bam_gpu_open_scan(const char* path, int device, int n_threads, int64_t wi
 int mc_bam_gpu_scan_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_rlen, const int32_t** d_flag,
                            const int32_t** d_gpos, const int32_t** d_gisize, const int32_t** d_tid,
                            const int64_t** d_seq_off, const uint8_t** d_seq, int64_t* seq_bytes);
+/* pileup.experimental's read table decoded on the GPU (the device form of
+ * mc_reads_open's walk, exp_reads.cpp; replaces bam.fetch at
+ * metacov/pileup.py:101): every placed record (tid >= 0) in file order, with
+ * tid, pos, end (pos + reference length; pos + 1 when unmapped or 0), flag,
+ * bits (1 no SEQ, 2 no reference length), the 2-bit code of the first k_len
+ * bases of query_alignment_sequence (0xFFFFFFFF: none) and the query name
+ * (name_len bytes at name_off in the names arena), left in device memory owned
+ * by the handle.  mc_bam_gpu_reads_copy copies them to caller buffers of
+ * n entries (names: name_bytes). */
+int mc_bam_gpu_open_reads(const char* path, int device, int n_threads, int k_len, int64_t window_bytes,
+                          mc_bam_gpu** out);
+int mc_bam_gpu_reads_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_tid, const int32_t** d_pos,
+                            const int64_t** d_end, const int32_t** d_flag, const uint8_t** d_bits,
+                            const uint32_t** d_kmer, const uint8_t** d_name_len, const int64_t** d_name_off,
+                            const uint8_t** d_names, int64_t* name_bytes);
+int mc_bam_gpu_reads_copy(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int64_t* end, int32_t* flag,
+                          uint8_t* bits, uint32_t* kmer, uint8_t* name_len, int64_t* name_off, uint8_t* names);
 /* One rank's contig shard decoded on the GPU ("each rank
  * decodes only its contigs' BGZF chunks, located via BAI virtual offsets";
  * replaces the per-contig indexed query under pysam's pileup(ref, start,
@@ -469,9 +486,19 @@ int mc_bam_write(const char* path, int32_t n_ref, const char* const* names,
  * mc_experimental_events. */
 typedef struct mc_reads mc_reads;
 int mc_reads_open(const char* path, int n_threads, int k_len, mc_reads** out);
+/* The same table with the BAM decoded on GPU `device` (mc_bam_gpu_open_reads)
+ * and copied to the host; the same checks and errors. */
+int mc_reads_open_gpu(const char* path, int device, int n_threads, int k_len, mc_reads** out);
 int mc_reads_close(mc_reads* r);
 int mc_reads_header(const mc_reads* r, int32_t* n_ref, int64_t* n_records, int64_t* n_placed);
 int mc_reads_target(const mc_reads* r, int32_t i, const char** name, int64_t* length);
+/* The table itself (views into the handle, n_placed entries; first: n_ref + 1
+ * per-contig record offsets, max_span: n_ref) -- for tests and bindings that
+ * read the placed records directly. */
+int mc_reads_fields(const mc_reads* r, const int32_t** pos, const int64_t** end, const uint16_t** flag,
+                    const uint8_t** bits, const uint32_t** kmer, const uint64_t** name_off,
+                    const uint8_t** name_len, const char** names, int64_t* name_bytes,
+                    const int64_t** first, const int64_t** max_span);
 int mc_experimental_reads(mc_reads* r, int k_len, const double* val1, const uint8_t* has1,
                           const double* val2, const uint8_t* has2, int64_t R,
                           const int32_t* tid, const int64_t* start, const int64_t* end,

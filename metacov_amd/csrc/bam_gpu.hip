@@ -367,6 +367,156 @@ scan_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __rest
     }
 }
 
+// Reads mode (pileup.experimental's read table, exp_reads.cpp's walk on the
+// device): every placed record (tid >= 0) in file order with what
+// experimental() reads of it: tid, pos, end (pos + bam_cigar2rlen, pos + 1
+// when unmapped or 0), flag, bits (1: no SEQ, 2: no reference length), the
+// 2-bit code of the first k bases of query_alignment_sequence (0xFFFFFFFF:
+// none), and its name (NUL-free bytes, name_off[w] into the names arena).
+// One lane per segment, as rec_walk_kernel.
+__device__ __forceinline__ uint32_t exp_kmer(const uint8_t* cig, uint32_t n_cigar, const uint8_t* seq, int32_t l_seq,
+                                             int k) {
+    int64_t qs = 0, qe = l_seq;
+    for (uint32_t i = 0; i < n_cigar; ++i) {   // getQueryStart
+        const uint32_t cw = mc::gz::ld_u32(cig + 4ull * i), op = cw & 0xFu;
+        if (op == 5) continue;
+        if (op == 4) {
+            qs += cw >> 4;
+            continue;
+        }
+        break;
+    }
+    for (uint32_t i = n_cigar; i-- > 1;) {      // getQueryEnd (stops at op 1)
+        const uint32_t cw = mc::gz::ld_u32(cig + 4ull * i), op = cw & 0xFu;
+        if (op == 5) continue;
+        if (op == 4) {
+            qe -= cw >> 4;
+            continue;
+        }
+        break;
+    }
+    if (qe - qs < k) return 0xFFFFFFFFu;
+    uint32_t code = 0;
+    for (int m = 0; m < k; ++m) {
+        const int64_t q = qs + m;
+        const uint32_t nib = (seq[q >> 1] >> ((~q & 1) << 2)) & 0xFu;
+        const uint32_t b = nib == 1 ? 0u : nib == 2 ? 1u : nib == 4 ? 2u : nib == 8 ? 3u : 4u;
+        if (b > 3) return 0xFFFFFFFFu;
+        code = (code << 2) | b;
+    }
+    return code;
+}
+
+template <bool kFill>
+__global__ void __launch_bounds__(256)
+reads_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __restrict__ seg_off, int64_t first,
+                  int64_t nseg, int32_t n_ref, int k, SegRes* __restrict__ res, const int64_t* __restrict__ out_off,
+                  const int64_t* __restrict__ byte_off, int32_t* __restrict__ tid, int32_t* __restrict__ pos,
+                  int64_t* __restrict__ end_pos, int32_t* __restrict__ flag, uint8_t* __restrict__ bits,
+                  uint32_t* __restrict__ kmer, uint8_t* __restrict__ name_len, int64_t* __restrict__ name_off,
+                  uint8_t* __restrict__ names) {
+    const int64_t i = first + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nseg) return;
+    int64_t q = seg_off[i];
+    const int64_t end = seg_off[i + 1];
+    int64_t records = 0, mapped = 0, placed = 0, bytes = 0, err_at = 0;
+    int32_t err = 0;
+    int64_t w = 0, w_end = 0, b = 0;
+    if (kFill) {
+        w = out_off[i];
+        w_end = w + res[i].kept;
+        b = byte_off[i];
+    }
+    while (q < end) {
+        if (q + 4 > n) {
+            err = kSegIncomplete;
+            break;
+        }
+        const int32_t bs = mc::gz::ld_i32(d + q);
+        if (bs < 32) {
+            err = kSegBadSize;
+            err_at = q;
+            break;
+        }
+        if (q + 4 + (int64_t)bs > n) {
+            err = kSegIncomplete;
+            break;
+        }
+        const uint8_t* r = d + q + 4;
+        const uint8_t* rend = r + bs;
+        const int32_t t = mc::gz::ld_i32(r);
+        const uint32_t l_name = r[8], fl = mc::gz::ld_u16(r + 14);
+        const int32_t l_seq = mc::gz::ld_i32(r + 16);
+        if (t < -1 || t >= n_ref || l_name == 0 || l_seq < 0) {
+            err = kSegMalformed;
+            err_at = q;
+            break;
+        }
+        if (t >= 0) {
+            uint32_t n_cigar = mc::gz::ld_u16(r + 12);
+            const uint8_t* cig = r + 32 + l_name;
+            const uint8_t* seq = cig + 4ull * n_cigar;
+            bool ok = cig + 4ull * n_cigar <= rend && seq + ((uint64_t)l_seq + 1) / 2 <= rend;
+            if (ok && n_cigar == 2 && mc::gz::ld_u32(cig) == (((uint32_t)l_seq << 4) | 4u) &&
+                (mc::gz::ld_u32(cig + 4) & 0xFu) == 3u) {   // the CG:B,I placeholder
+                const uint8_t* aux = seq + ((uint64_t)l_seq + 1) / 2 + (uint64_t)l_seq;
+                const uint8_t* words = nullptr;
+                uint32_t cnt = 0;
+                if (aux <= rend && mc::gz::find_cg(aux, rend, &words, &cnt) && words) {
+                    cig = words;
+                    n_cigar = cnt;
+                }
+            }
+            if (!ok) {
+                err = kSegMalformed;
+                err_at = q;
+                break;
+            }
+            uint32_t nl = 0;
+            while (nl < l_name && r[32 + nl]) ++nl;
+            if (kFill && w < w_end) {
+                const bool unmapped = fl & 4u;
+                int64_t rlen = 0;
+                if (!unmapped)
+                    for (uint32_t c = 0; c < n_cigar; ++c) {
+                        const uint32_t cw = mc::gz::ld_u32(cig + 4ull * c);
+                        if ((0x18Du >> (cw & 0xFu)) & 1u) rlen += cw >> 4;
+                    }
+                if (rlen == 0) rlen = 1;
+                const int32_t p = mc::gz::ld_i32(r + 4);
+                tid[w] = t;
+                pos[w] = p;
+                end_pos[w] = (int64_t)p + rlen;
+                flag[w] = (int32_t)fl;
+                bits[w] = (uint8_t)((l_seq == 0 ? 1 : 0) | ((unmapped || n_cigar == 0) ? 2 : 0));
+                kmer[w] = l_seq ? exp_kmer(cig, n_cigar, seq, l_seq, k) : 0xFFFFFFFFu;
+                name_len[w] = (uint8_t)nl;
+                name_off[w] = b;
+                for (uint32_t c = 0; c < nl; ++c) names[b + c] = r[32 + c];
+                b += nl;
+                ++w;
+            }
+            ++placed;
+            bytes += nl;
+            mapped += (fl & 4u) ? 0 : 1;
+        }
+        q += 4 + (int64_t)bs;
+        ++records;
+    }
+    if (!kFill) {
+        SegRes s;
+        s.landing = q;
+        s.records = records;
+        s.mapped = mapped;
+        s.kept = placed;
+        s.err_at = err_at;
+        s.bytes = bytes;
+        s.err = err;
+        s.pad = 0;
+        res[i] = s;
+    }
+}
+
 template <typename T>
 struct DBuf {
     T* p = nullptr;
@@ -439,6 +589,11 @@ struct mc_bam_gpu {
     DBuf<int32_t> tid, pos, span;     // kept intervals, file order (scan mode: tid, gpos, rlen)
     int64_t n_kept = 0;
     bool scan_mode = false;           // every record as scan's SoA batch (scan_walk_kernel)
+    bool reads_mode = false;          // the placed records as experimental()'s read table (reads_walk_kernel)
+    int reads_k = 0;
+    DBuf<int64_t> rend_pos;           // reads mode: end (pos + reference length)
+    DBuf<uint8_t> rbits, rnlen;       // reads mode: bits, name length
+    DBuf<uint32_t> rkmer;             // reads mode: k-mer prefix code
     DBuf<int32_t> sflag, sgisize;     // scan mode: flag, gisize
     DBuf<int64_t> soff;               // scan mode: [n_kept + 1] aligned sequence offsets
     DBuf<uint8_t> sseq;               // scan mode: packed nt16 bases
@@ -734,6 +889,10 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
             scan_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->res.p, nullptr,
                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                                           nullptr, nullptr);
+        else if (g->reads_mode)
+            reads_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->reads_k,
+                                                           g->res.p, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         else
             rec_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->flag_filter,
                                                          g->res.p, nullptr, nullptr, nullptr, nullptr,
@@ -830,21 +989,35 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
     HIP_TRY(g->tid.reserve(need, st, g->n_kept));
     HIP_TRY(g->pos.reserve(need, st, g->n_kept));
     HIP_TRY(g->span.reserve(need, st, g->n_kept));
-    if (g->scan_mode) {
+    if (g->scan_mode || g->reads_mode) {
         HIP_TRY(g->sflag.reserve(need, st, g->n_kept));
-        HIP_TRY(g->sgisize.reserve(need, st, g->n_kept));
         HIP_TRY(g->soff.reserve(need + 1, st, g->n_kept + 1));
         HIP_TRY(g->sseq.reserve((size_t)(g->n_bytes + bytes) + 16, st, (size_t)g->n_bytes));
         HIP_TRY(g->boff.reserve(nseg + 1));
-        if (g->n_kept == 0) HIP_TRY(hipMemsetAsync(g->soff.p, 0, 8, st));
         std::memcpy(h + nseg + 1, bo.data(), nseg * 8);
         HIP_TRY(hipMemcpyAsync(g->boff.p, h + nseg + 1, nseg * 8, hipMemcpyHostToDevice, st));
-        if (total) {
-            const int grid = (int)((nseg + 255) / 256);
-            scan_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->res.p, g->out_off.p,
-                                                         g->boff.p, g->span.p, g->sflag.p, g->pos.p, g->sgisize.p,
-                                                         g->tid.p, g->soff.p, g->sseq.p);
-            HIP_TRY(hipGetLastError());
+        const int grid = (int)((nseg + 255) / 256);
+        if (g->scan_mode) {
+            HIP_TRY(g->sgisize.reserve(need, st, g->n_kept));
+            if (g->n_kept == 0) HIP_TRY(hipMemsetAsync(g->soff.p, 0, 8, st));
+            if (total) {
+                scan_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->res.p,
+                                                             g->out_off.p, g->boff.p, g->span.p, g->sflag.p, g->pos.p,
+                                                             g->sgisize.p, g->tid.p, g->soff.p, g->sseq.p);
+                HIP_TRY(hipGetLastError());
+            }
+        } else {
+            HIP_TRY(g->rend_pos.reserve(need, st, g->n_kept));
+            HIP_TRY(g->rbits.reserve(need, st, g->n_kept));
+            HIP_TRY(g->rkmer.reserve(need, st, g->n_kept));
+            HIP_TRY(g->rnlen.reserve(need, st, g->n_kept));
+            if (total) {
+                reads_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->reads_k,
+                                                              g->res.p, g->out_off.p, g->boff.p, g->tid.p, g->pos.p,
+                                                              g->rend_pos.p, g->sflag.p, g->rbits.p, g->rkmer.p,
+                                                              g->rnlen.p, g->soff.p, g->sseq.p);
+                HIP_TRY(hipGetLastError());
+            }
         }
     } else if (total || g->ext.p) {
         const int grid = (int)((nseg + 255) / 256);
@@ -1271,7 +1444,7 @@ int inflate_resident(mc_bam_gpu* g, int fd, const VMap* vm, size_t vsize, const 
 
 // The per-contig table of the record walk, zeroed (n_ref + 1 entries).
 int init_ext(mc_bam_gpu* g) {
-    if (g->scan_mode) return MC_OK;   // (no extents table: every record is kept)
+    if (g->scan_mode || g->reads_mode) return MC_OK;   // (no extents table)
     const size_t m = g->hdr.names.size() + 1;
     HIP_TRY(g->ext.reserve(m));
     HIP_TRY(hipMemsetAsync(g->ext.p, 0, m * sizeof(ExtAcc), g->stream));
@@ -1842,6 +2015,68 @@ extern "C" int mc_bam_gpu_scan_device(const mc_bam_gpu* g, int64_t* n, const int
     *d_seq_off = g->soff.p;
     *d_seq = g->sseq.p;
     *seq_bytes = g->n_bytes;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_open_reads(const char* path, int device, int n_threads, int k, int64_t window_bytes,
+                                     mc_bam_gpu** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    MC_REQUIRE(k >= 1 && k <= 16, MC_E_INVALID, "k-mer length %d outside [1, 16]", k);
+    *out = nullptr;
+    std::unique_ptr<mc_bam_gpu> g;
+    if (int rc = open_common(path, device, n_threads, 0, g)) return rc;
+    g->reads_mode = true;
+    g->reads_k = k;
+    const double t0 = now_s();
+    if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
+    g->t_open = (now_s() - t0) * 1e3;
+    *out = g.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_reads_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_tid,
+                                       const int32_t** d_pos, const int64_t** d_end, const int32_t** d_flag,
+                                       const uint8_t** d_bits, const uint32_t** d_kmer, const uint8_t** d_name_len,
+                                       const int64_t** d_name_off, const uint8_t** d_names, int64_t* name_bytes) {
+    MC_REQUIRE(g && n && d_tid && d_pos && d_end && d_flag && d_bits && d_kmer && d_name_len && d_name_off &&
+                   d_names && name_bytes,
+               MC_E_INVALID, "null argument");
+    MC_REQUIRE(g->reads_mode, MC_E_STATE, "not a reads-mode decode (mc_bam_gpu_open_reads)");
+    *n = g->n_kept;
+    *d_tid = g->tid.p;
+    *d_pos = g->pos.p;
+    *d_end = g->rend_pos.p;
+    *d_flag = g->sflag.p;
+    *d_bits = g->rbits.p;
+    *d_kmer = g->rkmer.p;
+    *d_name_len = g->rnlen.p;
+    *d_name_off = g->soff.p;
+    *d_names = g->sseq.p;
+    *name_bytes = g->n_bytes;
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_reads_copy(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int64_t* end, int32_t* flag,
+                                     uint8_t* bits, uint32_t* kmer, uint8_t* name_len, int64_t* name_off,
+                                     uint8_t* names) {
+    MC_REQUIRE(g && tid && pos && end && flag && bits && kmer && name_len && name_off && (names || !g->n_bytes),
+               MC_E_INVALID, "null argument");
+    MC_REQUIRE(g->reads_mode, MC_E_STATE, "not a reads-mode decode (mc_bam_gpu_open_reads)");
+    HIP_TRY(hipSetDevice(g->device));
+    const size_t n = (size_t)g->n_kept;
+    hipStream_t st = g->stream;
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(tid, g->tid.p, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(pos, g->pos.p, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(end, g->rend_pos.p, n * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(flag, g->sflag.p, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(bits, g->rbits.p, n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(kmer, g->rkmer.p, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(name_len, g->rnlen.p, n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(name_off, g->soff.p, n * 8, hipMemcpyDeviceToHost, st));
+    }
+    if (g->n_bytes) HIP_TRY(hipMemcpyAsync(names, g->sseq.p, (size_t)g->n_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return MC_OK;
 }
 

@@ -622,6 +622,77 @@ extern "C" int mc_reads_open(const char* path, int n_threads, int k_len, mc_read
     return MC_OK;
 }
 
+namespace {
+
+// mc_reads_open_gpu's table from a reads-mode GPU decode: the device fields
+// copied back, the names joined, then reads_open's order check and the per
+// contig first record / maximum span.
+int reads_from_gpu(const mc_bam_gpu* g, const char* path, mc_reads* r) {
+    const mc_bam* h = nullptr;
+    if (int rc = mc_bam_gpu_header(g, &h)) return rc;
+    int64_t m = 0, nb = 0;
+    const int32_t *dt, *dp, *df;
+    const int64_t *de, *dno;
+    const uint8_t *db, *dnl, *dn;
+    const uint32_t* dk;
+    if (int rc = mc_bam_gpu_reads_device(g, &m, &dt, &dp, &de, &df, &db, &dk, &dnl, &dno, &dn, &nb)) return rc;
+    r->names = h->names;
+    r->lens = h->lens;
+    r->n_records = h->n_records;
+    r->n_unplaced = h->n_records - m;
+    std::vector<int32_t> tid((size_t)m), flag((size_t)m);
+    std::vector<int64_t> name_off((size_t)m);
+    r->pos.resize((size_t)m);
+    r->end.resize((size_t)m);
+    r->flag.resize((size_t)m);
+    r->bits.resize((size_t)m);
+    r->kmer.resize((size_t)m);
+    r->name_off.resize((size_t)m);
+    r->name_len.resize((size_t)m);
+    r->arena.resize((size_t)nb);
+    if (int rc = mc_bam_gpu_reads_copy(g, tid.data(), r->pos.data(), r->end.data(), flag.data(), r->bits.data(),
+                                       r->kmer.data(), r->name_len.data(), name_off.data(),
+                                       (uint8_t*)r->arena.data()))
+        return rc;
+    r->max_span.assign(r->names.size(), 0);
+    int32_t last_tid = -1, last_pos = -1;
+    for (int64_t i = 0; i < m; ++i) {
+        const size_t k = (size_t)i;
+        const int32_t t = tid[k], p = r->pos[k];
+        MC_REQUIRE(t > last_tid || (t == last_tid && p >= last_pos), MC_E_INVALID,
+                   "%s is not coordinate-sorted (placed record %lld); experimental() fetches "
+                   "regions of a sorted, indexed BAM", path, (long long)i);
+        last_tid = t;
+        last_pos = p;
+        r->flag[k] = (uint16_t)flag[k];
+        r->name_off[k] = (uint64_t)name_off[k];
+        if (r->first.size() <= (size_t)t) r->first.resize((size_t)t + 1, i);
+        int64_t& ms = r->max_span[(size_t)t];
+        ms = std::max<int64_t>(ms, r->end[k] - p);
+    }
+    r->first.resize(r->names.size() + 1, m);
+    return MC_OK;
+}
+
+}  // namespace
+
+extern "C" int mc_reads_open_gpu(const char* path, int device, int n_threads, int k_len, mc_reads** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    MC_REQUIRE(k_len >= 1 && k_len <= 13, MC_E_RANGE, "k-mer length %d outside 1..13", k_len);
+    *out = nullptr;
+    std::unique_ptr<mc_reads> r(new mc_reads());
+    r->k = k_len;
+    mc_bam_gpu* g = nullptr;
+    int64_t window = 0;   // (tests: MC_READS_GPU_WINDOW forces the windowed decode)
+    if (const char* e = std::getenv("MC_READS_GPU_WINDOW")) window = std::strtoll(e, nullptr, 10);
+    if (int rc = mc_bam_gpu_open_reads(path, device, n_threads, k_len, window, &g)) return rc;
+    const int rc = reads_from_gpu(g, path, r.get());
+    mc_bam_gpu_close(g);
+    if (rc) return rc;
+    *out = r.release();
+    return MC_OK;
+}
+
 extern "C" int mc_reads_close(mc_reads* r) {
     delete r;
     return MC_OK;
@@ -633,6 +704,27 @@ extern "C" int mc_reads_header(const mc_reads* r, int32_t* n_ref, int64_t* n_rec
     if (n_ref) *n_ref = (int32_t)r->names.size();
     if (n_records) *n_records = r->n_records;
     if (n_placed) *n_placed = (int64_t)r->pos.size();
+    return MC_OK;
+}
+
+extern "C" int mc_reads_fields(const mc_reads* r, const int32_t** pos, const int64_t** end, const uint16_t** flag,
+                               const uint8_t** bits, const uint32_t** kmer, const uint64_t** name_off,
+                               const uint8_t** name_len, const char** names, int64_t* name_bytes,
+                               const int64_t** first, const int64_t** max_span) {
+    MC_REQUIRE(r && pos && end && flag && bits && kmer && name_off && name_len && names && name_bytes && first &&
+                   max_span,
+               MC_E_INVALID, "null argument");
+    *pos = r->pos.data();
+    *end = r->end.data();
+    *flag = r->flag.data();
+    *bits = r->bits.data();
+    *kmer = r->kmer.data();
+    *name_off = r->name_off.data();
+    *name_len = r->name_len.data();
+    *names = r->arena.data();
+    *name_bytes = (int64_t)r->arena.size();
+    *first = r->first.data();
+    *max_span = r->max_span.data();
     return MC_OK;
 }
 

@@ -158,14 +158,25 @@ class FastaFile:
 
 class ReadTable:
     """The placed records of a coordinate-sorted BAM as experimental() reads
-    them (mc_reads_open); plays the role of the reference's indexed
-    pysam.AlignmentFile for bam.fetch (pileup.py:101)."""
+    them; plays the role of the reference's indexed pysam.AlignmentFile for
+    bam.fetch (pileup.py:101).  decode: "host" (mc_reads_open: BGZF inflate
+    and record walk on n_threads host threads) or "gpu" (mc_reads_open_gpu:
+    the file inflated and walked on GPU `device`, the table copied back);
+    None: MC_READS_DECODE, else "host"."""
 
-    def __init__(self, path, k_len=7, n_threads=0):
+    def __init__(self, path, k_len=7, n_threads=0, decode=None, device=0):
         self._lib = _lib.load()
+        decode = decode or os.environ.get("MC_READS_DECODE", "host")
+        if decode not in ("gpu", "host"):
+            raise ValueError("decode must be 'gpu' or 'host'")
         h = _lib.ctypes.c_void_p()
-        _lib.check(self._lib.mc_reads_open(str(path).encode(), n_threads, k_len,
-                                           _lib.ctypes.byref(h)), self._lib)
+        if decode == "gpu":
+            rc = self._lib.mc_reads_open_gpu(str(path).encode(), int(device), n_threads, k_len,
+                                             _lib.ctypes.byref(h))
+        else:
+            rc = self._lib.mc_reads_open(str(path).encode(), n_threads, k_len, _lib.ctypes.byref(h))
+        _lib.check(rc, self._lib)
+        self.decode = decode
         self._h = h
         self.k_len = k_len
         self.filename = str(path)
@@ -187,6 +198,32 @@ class ReadTable:
         self.n_records = n_rec.value
         self.n_placed = n_placed.value
         self._tid = {n: i for i, n in enumerate(names)}
+
+    def fields(self):
+        """The placed records as numpy copies: pos, end, flag, bits, kmer,
+        name (bytes), plus per contig first (n_ref + 1) and max_span."""
+        c = _lib.ctypes
+        ptrs = [c.c_void_p() for _ in range(8)]
+        nb = c.c_int64()
+        first, span = c.c_void_p(), c.c_void_p()
+        _lib.check(self._lib.mc_reads_fields(self._h, *[c.byref(p) for p in ptrs], c.byref(nb),
+                                             c.byref(first), c.byref(span)), self._lib)
+        n, n_ref = self.n_placed, len(self.references)
+
+        def arr(p, dt, count):
+            if count == 0 or not p.value:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(c.cast(p, c.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         (count,)).copy()
+        out = {k: arr(p, dt, n) for k, p, dt in zip(
+            ("pos", "end", "flag", "bits", "kmer", "name_off", "name_len"), ptrs[:7],
+            (np.int32, np.int64, np.uint16, np.uint8, np.uint32, np.uint64, np.uint8))}
+        arena = c.string_at(ptrs[7], nb.value) if nb.value else b""
+        out["name"] = [arena[o:o + ln] for o, ln in zip(out.pop("name_off").tolist(),
+                                                         out.pop("name_len").tolist())]
+        out["first"] = arr(first, np.int64, n_ref + 1)
+        out["max_span"] = arr(span, np.int64, n_ref)
+        return out
 
     def get_tid(self, ref):
         if ref not in self._tid:
@@ -294,7 +331,7 @@ class EcorEngine:
 
 # ------------------------------------------------------------------ estimator
 
-def _as_reads(bam, k_len, n_threads):
+def _as_reads(bam, k_len, n_threads, decode=None, device=0):
     if isinstance(bam, ReadTable):
         if bam.k_len != k_len:
             raise ValueError("ReadTable was opened for k=%d, not %d" % (bam.k_len, k_len))
@@ -303,7 +340,7 @@ def _as_reads(bam, k_len, n_threads):
     if isinstance(path, bytes):
         path = path.decode()
     if isinstance(path, (str, os.PathLike)):
-        return ReadTable(path, k_len, n_threads), True
+        return ReadTable(path, k_len, n_threads, decode, device), True
     raise TypeError("bam must be a BAM path or a metacov_amd.experimental.ReadTable")
 
 
@@ -374,8 +411,11 @@ class RegionResult:
 def experimental_batch(bam, k_cor, k_len, fasta, regions, device=0, n_threads=0, timings=None):
     """pileup.experimental for every (ref, start, end) in `regions`; a list
     of RegionResult in input order.  Reads: one host pass per region on
-    n_threads threads; sequence: one GPU launch for all regions."""
-    reads, own_reads = _as_reads(bam, k_len, n_threads)
+    n_threads threads; sequence: one GPU launch for all regions.  A BAM
+    path is decoded on the GPU when there is a FASTA (the run uses `device`
+    anyway; MC_READS_DECODE overrides), else on the host."""
+    decode = os.environ.get("MC_READS_DECODE") or ("gpu" if fasta is not None else "host")
+    reads, own_reads = _as_reads(bam, k_len, n_threads, decode, device)
     fasta = _as_fasta(fasta)
     try:
         return _batch(reads, k_cor, k_len, fasta, list(regions), device, n_threads, timings)

@@ -5,8 +5,10 @@ random reference FASTA, a random 7-mer correction table.
 
     python scripts/bench_experimental.py [--contigs 40 --reps 3]
 
-Times, per whole-contig region set: the host read pass (mc_reads_open +
-mc_experimental_reads), the GPU k-mer correlation (ecor_kernel, HIP events)
+Times, per whole-contig region set: the read table opened with the host
+decode (mc_reads_open) and with the GPU decode (mc_reads_open_gpu; the two
+tables compared field for field), the batch's host read pass
+(mc_experimental_reads), the GPU k-mer correlation (ecor_kernel, HIP events)
 against the MI355X FP64 vector peak, the whole experimental_batch call, and
 the CPU restatement of the reference's sequence side (oracle/experimental.py
 raw_ecor: the reference's per-position np.inner loop, pileup.py:63-88) on a
@@ -59,8 +61,17 @@ def main():
     runs = []
     for rep in range(a.reps):
         t0 = time.perf_counter()
-        reads = mx.ReadTable(bam, 7, a.threads)
+        reads_h = mx.ReadTable(bam, 7, a.threads, decode="host")
         t_open = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        reads = mx.ReadTable(bam, 7, a.threads, decode="gpu", device=0)
+        t_open_gpu = time.perf_counter() - t0
+        if rep == 0:   # the two decodes' tables, field for field
+            fh, fg = reads_h.fields(), reads.fields()
+            for key in fh:
+                same = fh[key] == fg[key] if isinstance(fh[key], list) else np.array_equal(fh[key], fg[key])
+                assert same, "GPU-decoded read table differs from the host's in " + key
+        reads_h.close()
         fa = mx.FastaFile(fasta)
         tm = {}
         t0 = time.perf_counter()
@@ -71,7 +82,7 @@ def main():
         assert all(r.error is None for r in res)
         ecor_ms = tm["ecor_kernel_ms"]
         flop = 2.0 * TAPS * positions
-        runs.append({"reads_open_s": t_open, "batch_s": t_batch, "ecor_kernel_ms": ecor_ms,
+        runs.append({"reads_open_s": t_open, "reads_open_gpu_s": t_open_gpu, "batch_s": t_batch, "ecor_kernel_ms": ecor_ms,
                      "ecor_tflops": flop / (ecor_ms * 1e-3) / 1e12,
                      "ecor_frac_fp64_peak": flop / (ecor_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFLOPS})
         print(json.dumps(runs[-1]), file=sys.stderr, flush=True)

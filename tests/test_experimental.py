@@ -218,6 +218,55 @@ def test_unsorted_bam_rejected(tmp_path, lib_built):
         mx.ReadTable(path, 4)
 
 
+def _mixed_reads_bam(path, seed=11, n=12_000):
+    """Placed records of every kind the read table distinguishes: soft and
+    hard clips at both ends (query_alignment_sequence bounds), insertions at
+    the end (getQueryEnd stops there), N bases, no SEQ, placed but unmapped
+    (no CIGAR: reference_length None), CIGARs over 8 ops stored as CG:B,I
+    tags, three contigs, and unplaced records at the end."""
+    rng = np.random.default_rng(seed)
+    lengths = [40_000, 25_000, 60_000]
+    recs = []
+    for i in range(n):
+        tid = int(rng.integers(0, 3))
+        u = rng.random()
+        l = int(rng.integers(20, 120))
+        if u < 0.04:                                   # placed, unmapped, no CIGAR
+            cig, flag = [], 0x4
+        elif u < 0.12:                                 # long CIGAR (CG tag)
+            parts = [(0, 5)] * 10
+            cig, l, flag = [(4, 3)] + parts + [(1, 2), (4, 4)], 3 + 50 + 2 + 4, 0x10
+        else:
+            a, b = int(rng.integers(0, 6)), int(rng.integers(0, 6))
+            m = max(1, l - a - b)
+            cig = ([(5, 2)] if rng.random() < 0.2 else []) + ([(4, a)] if a else []) + [(0, m)]
+            cig += ([(1, 2)] if rng.random() < 0.1 else []) + ([(4, b)] if b else [])
+            cig += [(5, 3)] if rng.random() < 0.2 else []
+            l = sum(n_ for op, n_ in cig if op in (0, 1, 4))
+            flag = int(rng.choice([0x1 | 0x2 | 0x40, 0x1 | 0x80 | 0x10, 0x100, 0]))
+        seq = "".join(rng.choice(list("ACGTN"), size=l, p=[0.24, 0.24, 0.24, 0.24, 0.04]))
+        if rng.random() < 0.03:
+            l, seq = 0, None                           # no SEQ
+        pos = int(rng.integers(0, lengths[tid] - 200))
+        recs.append(synth.SynthRecord("q%d%s" % (i, "x" * int(rng.integers(0, 40))), tid, pos, flag, cig, l, seq))
+    recs.sort(key=lambda r: (r.tid, r.pos))
+    recs += [synth.SynthRecord("u%d" % j, -1, -1, 0x4, [], 30, "ACGT" * 7 + "AC") for j in range(40)]
+    synth.write_bam(path, ["c0", "c1", "c2"], lengths, recs, long_cigar_threshold=8)
+
+
+def test_read_table_fields(tmp_path, lib_built):
+    path = str(tmp_path / "mixed.bam")
+    _mixed_reads_bam(path, n=3000)
+    with mx.ReadTable(path, 6) as t:
+        f = t.fields()
+        assert t.n_records == 3040 and t.n_placed == 3000
+    assert len(f["name"]) == 3000 and all(nm.startswith(b"q") for nm in f["name"])
+    assert f["first"][0] == 0 and f["first"][-1] == 3000 and np.all(np.diff(f["first"]) >= 0)
+    assert np.all(f["end"] > f["pos"])
+    assert np.all((f["bits"] & 2) == ((f["flag"] & 4) != 0) * 2)
+    assert np.all(f["max_span"] >= 1)
+
+
 def test_region_errors_without_gpu(golden_dir, lib_built):
     bam = os.path.join(golden_dir, "bbmap.sorted.bam")
     res = mx.experimental_batch(bam, [{}, {}], 7, None,
@@ -236,6 +285,45 @@ def test_region_errors_without_gpu(golden_dir, lib_built):
 
 
 # ------------------------------------------------------------------ GPU
+
+def _same_tables(a, b):
+    for key in a:
+        if isinstance(a[key], list):
+            assert a[key] == b[key], key
+        else:
+            np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [None, "1048576"])
+def test_read_table_gpu_decode_equals_host(golden_dir, tmp_path, lib_built, monkeypatch, window):
+    """mc_reads_open_gpu (inflate + record walk on the GPU) gives the host
+    walk's table field for field, on every golden BAM and on a mixed BAM
+    (clips, CG-tag CIGARs, no SEQ, placed-unmapped, unplaced records), whole
+    and in 1 MiB windows (records cut at window ends)."""
+    mixed = str(tmp_path / "mixed.bam")
+    _mixed_reads_bam(mixed)
+    if window:
+        monkeypatch.setenv("MC_READS_GPU_WINDOW", window)
+    paths = [os.path.join(golden_dir, f) for f in sorted(os.listdir(golden_dir)) if f.endswith(".bam")]
+    for path in paths + [mixed]:
+        for k in (4, 7):
+            with mx.ReadTable(path, k, decode="host") as h, mx.ReadTable(path, k, decode="gpu") as g:
+                assert (h.references, h.lengths, h.n_records, h.n_placed) == \
+                    (g.references, g.lengths, g.n_records, g.n_placed), path
+                _same_tables(h.fields(), g.fields())
+
+
+@pytest.mark.gpu
+def test_read_table_gpu_unsorted_rejected(tmp_path, lib_built):
+    from metacov_amd._lib import MetacovError
+    path = str(tmp_path / "u.bam")
+    synth.write_bam(path, ["c"], [1000], [
+        synth.SynthRecord("a", 0, 500, 0x3, [(0, 10)], 10, "ACGTACGTAC"),
+        synth.SynthRecord("b", 0, 100, 0x3, [(0, 10)], 10, "ACGTACGTAC")])
+    with pytest.raises(MetacovError, match="coordinate-sorted"):
+        mx.ReadTable(path, 4, decode="gpu")
+
 
 @pytest.mark.gpu
 def test_goldens_with_fasta_gpu(gold, golden_dir, lib_built):
