@@ -2059,8 +2059,9 @@ extern "C" int mc_bam_gpu_reads_device(const mc_bam_gpu* g, int64_t* n, const in
 extern "C" int mc_bam_gpu_reads_copy(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int64_t* end, int32_t* flag,
                                      uint8_t* bits, uint32_t* kmer, uint8_t* name_len, int64_t* name_off,
                                      uint8_t* names) {
-    MC_REQUIRE(g && tid && pos && end && flag && bits && kmer && name_len && name_off && (names || !g->n_bytes),
-               MC_E_INVALID, "null argument");
+    MC_REQUIRE(g && ((tid && pos && end && flag && bits && kmer && name_len && name_off) || !g->n_kept) &&
+                   (names || !g->n_bytes),
+               MC_E_INVALID, "null argument");   // (an empty table: no buffers needed)
     MC_REQUIRE(g->reads_mode, MC_E_STATE, "not a reads-mode decode (mc_bam_gpu_open_reads)");
     HIP_TRY(hipSetDevice(g->device));
     const size_t n = (size_t)g->n_kept;

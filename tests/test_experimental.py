@@ -315,6 +315,30 @@ def test_read_table_gpu_decode_equals_host(golden_dir, tmp_path, lib_built, monk
 
 
 @pytest.mark.gpu
+def test_read_table_gpu_decode_edge_files(tmp_path, lib_built):
+    """Header-only and unplaced-only BAMs give the host walk's (empty) tables;
+    a BAM cut inside a record is refused by both decodes."""
+    from metacov_amd._lib import MetacovError
+    empty, unpl, cut = (str(tmp_path / n) for n in ("empty.bam", "unplaced.bam", "cut.bam"))
+    synth.write_bam(empty, ["c0", "c1"], [100, 200], [])
+    synth.write_bam(unpl, ["c0"], [100], [synth.SynthRecord("u%d" % j, -1, -1, 0x4, [], 12, "ACGTACGTACGT")
+                                          for j in range(50)])
+    for path in (empty, unpl):
+        with mx.ReadTable(path, 5, decode="host") as h, mx.ReadTable(path, 5, decode="gpu") as g:
+            assert (h.references, h.lengths, h.n_records, h.n_placed) == \
+                (g.references, g.lengths, g.n_records, g.n_placed)
+            _same_tables(h.fields(), g.fields())
+    _mixed_reads_bam(cut, n=400)
+    import gzip
+    raw = gzip.decompress(open(cut, "rb").read())
+    with open(cut, "wb") as fh:              # the same stream re-blocked, cut mid-record
+        fh.write(synth._bgzf(raw[:len(raw) - 37]))
+    for decode in ("host", "gpu"):
+        with pytest.raises(MetacovError):
+            mx.ReadTable(cut, 5, decode=decode)
+
+
+@pytest.mark.gpu
 def test_read_table_gpu_unsorted_rejected(tmp_path, lib_built):
     from metacov_amd._lib import MetacovError
     path = str(tmp_path / "u.bam")
