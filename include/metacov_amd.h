@@ -395,6 +395,12 @@ int mc_bam_gpu_reads_device(const mc_bam_gpu* g, int64_t* n, const int32_t** d_t
                             const uint8_t** d_names, int64_t* name_bytes);
 int mc_bam_gpu_reads_copy(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int64_t* end, int32_t* flag,
                           uint8_t* bits, uint32_t* kmer, uint8_t* name_len, int64_t* name_off, uint8_t* names);
+/* The same for one rank's contigs (mc_bam_gpu_open_extents' blocks and
+ * extents table: only the selected contigs' BGZF blocks are read and
+ * inflated); tids stay the header's.  The header counts are the table's. */
+int mc_bam_gpu_open_reads_extents(const char* path, int device, int n_threads, int k_len, int32_t n_ref,
+                                  const mc_contig_extent* ext, int64_t n_no_coor, int32_t n_sel, const int32_t* sel,
+                                  mc_bam_gpu** out);
 /* One rank's contig shard decoded on the GPU ("each rank
  * decodes only its contigs' BGZF chunks, located via BAI virtual offsets";
  * replaces the per-contig indexed query under pysam's pileup(ref, start,
@@ -489,6 +495,12 @@ int mc_reads_open(const char* path, int n_threads, int k_len, mc_reads** out);
 /* The same table with the BAM decoded on GPU `device` (mc_bam_gpu_open_reads)
  * and copied to the host; the same checks and errors. */
 int mc_reads_open_gpu(const char* path, int device, int n_threads, int k_len, mc_reads** out);
+/* One rank's read table: the placed records of contigs sel[0..n_sel) only,
+ * decoded from their BGZF blocks (extents: a BAI's, mc_bam_index_extents, or
+ * a whole-file decode's, mc_bam_gpu_extents). */
+int mc_reads_open_gpu_extents(const char* path, int device, int n_threads, int k_len, int32_t n_ref,
+                              const mc_contig_extent* ext, int64_t n_no_coor, int32_t n_sel, const int32_t* sel,
+                              mc_reads** out);
 int mc_reads_close(mc_reads* r);
 int mc_reads_header(const mc_reads* r, int32_t* n_ref, int64_t* n_records, int64_t* n_placed);
 int mc_reads_target(const mc_reads* r, int32_t i, const char** name, int64_t* length);

@@ -144,6 +144,8 @@ SIGNATURES = {
     "mc_bam_gpu_open_reads": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _PP],
     "mc_bam_gpu_reads_device": [_P, _PI64, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PI64],
     "mc_bam_gpu_reads_copy": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "mc_bam_gpu_open_reads_extents": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I32, _P, _I64,
+                                      _I32, _P, _PP],
     "mc_bam_index_extents": [ctypes.c_char_p, _I32, _P, _PI64],
     "mc_bam_gpu_open_contigs": [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _U32, _I32, _P,
                                 _PP],
@@ -159,6 +161,8 @@ SIGNATURES = {
     # pileup.experimental: read side (host) and sequence side (GPU)
     "mc_reads_open": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _PP],
     "mc_reads_open_gpu": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _PP],
+    "mc_reads_open_gpu_extents": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I32, _P, _I64, _I32,
+                                  _P, _PP],
     "mc_reads_fields": [_P, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PI64, _PP, _PP],
     "mc_reads_close": [_P],
     "mc_reads_header": [_P, _PI32, _PI64, _PI64],

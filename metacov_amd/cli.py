@@ -187,13 +187,18 @@ def compute_rows(bam, tids, starts, ends, device=0, max_depth=_depthcap.HTSLIB_M
     return rows
 
 
-def experimental_results(path, exp, references, tids, starts, ends, device=0):
-    """pileup.experimental for every region (cli.py:93-95), or None without -k."""
+def experimental_results(path, exp, references, tids, starts, ends, device=0, contigs=None, extents=None):
+    """pileup.experimental for every region (cli.py:93-95), or None without -k.
+    contigs / extents: a distributed rank's shard, whose read table is decoded
+    from those contigs' BGZF blocks only (experimental_batch)."""
     if exp is None:
         return None
     k_cor, k_len, fasta = exp
     regs = [(references[t], int(a), int(b)) for t, a, b in zip(tids, starts, ends)]
-    return _experimental.experimental_batch(path, k_cor, k_len, fasta, regs, device=device)
+    if not regs:
+        return []
+    return _experimental.experimental_batch(path, k_cor, k_len, fasta, regs, device=device, contigs=contigs,
+                                            extents=extents)
 
 
 def write_csv(regions, rows, outfile, extra=None):
@@ -249,9 +254,11 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         try:
             table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
                                        max_depth, legacy_endpos, decode, coll_dev, times)
-            head, regions, tids, starts, ends, rows, mine, r_max, region_err = table_args
+            head, regions, tids, starts, ends, rows, mine, r_max, region_err, shard = table_args
+            # -k: the read table of this rank's contigs only (their BGZF blocks, by
+            # the BAI or rank 0's extents table), when the GPU decodes
             mine_extra = experimental_results(path, exp, head.references, tids[mine], starts[mine],
-                                              ends[mine], device)
+                                              ends[mine], device, *shard)
         except BaseException as e:   # every rank learns of it before the table gather
             err = e
         mdist.agree_on_error(err, device=coll_dev)
@@ -293,7 +300,8 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
                   coll_dev=None, times=None):
     """This rank's part of a distributed pileup: header and regions (every
     rank; those before the first failing one, and its error), LPT contig
-    shards, and the rows of the regions on its contigs.
+    shards, the rows of the regions on its contigs, and (contigs, extents)
+    for its -k read table.
 
     Each rank decodes only its own contigs' BGZF blocks, on
     its GPU by default, located by the BAI's extents.  Without a .bai, rank 0
@@ -363,7 +371,9 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
         times["rows_s"] = time.perf_counter() - t0
     if full is not None:
         full.close()
-    return head, regions, tids, starts, ends, rows, mine, r_max, region_err
+    # (contigs, extents) for this rank's -k read table: a contig-subset GPU decode
+    shard = (shards[rank], ext) if decode == "gpu" and (have_index or ext is not None) else (None, None)
+    return head, regions, tids, starts, ends, rows, mine, r_max, region_err, shard
 
 
 @main.command()

@@ -373,7 +373,8 @@ scan_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __rest
 // when unmapped or 0), flag, bits (1: no SEQ, 2: no reference length), the
 // 2-bit code of the first k bases of query_alignment_sequence (0xFFFFFFFF:
 // none), and its name (NUL-free bytes, name_off[w] into the names arena).
-// One lane per segment, as rec_walk_kernel.
+// One lane per segment, as rec_walk_kernel.  tid_map (a contig-subset
+// decode): only records whose entry is >= 0 are taken; tids stay the header's.
 __device__ __forceinline__ uint32_t exp_kmer(const uint8_t* cig, uint32_t n_cigar, const uint8_t* seq, int32_t l_seq,
                                              int k) {
     int64_t qs = 0, qe = l_seq;
@@ -414,7 +415,7 @@ reads_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __res
                   const int64_t* __restrict__ byte_off, int32_t* __restrict__ tid, int32_t* __restrict__ pos,
                   int64_t* __restrict__ end_pos, int32_t* __restrict__ flag, uint8_t* __restrict__ bits,
                   uint32_t* __restrict__ kmer, uint8_t* __restrict__ name_len, int64_t* __restrict__ name_off,
-                  uint8_t* __restrict__ names) {
+                  uint8_t* __restrict__ names, const int32_t* __restrict__ tid_map) {
     const int64_t i = first + (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= nseg) return;
     int64_t q = seg_off[i];
@@ -452,7 +453,7 @@ reads_walk_kernel(const uint8_t* __restrict__ d, int64_t n, const int64_t* __res
             err_at = q;
             break;
         }
-        if (t >= 0) {
+        if (t >= 0 && (!tid_map || tid_map[t] >= 0)) {   // (a contig-subset decode: the selected contigs)
             uint32_t n_cigar = mc::gz::ld_u16(r + 12);
             const uint8_t* cig = r + 32 + l_name;
             const uint8_t* seq = cig + 4ull * n_cigar;
@@ -892,7 +893,8 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
         else if (g->reads_mode)
             reads_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->reads_k,
                                                            g->res.p, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                           g->subset ? g->tid_map.p : nullptr);
         else
             rec_walk_kernel<false><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, first, nseg, n_ref, g->flag_filter,
                                                          g->res.p, nullptr, nullptr, nullptr, nullptr,
@@ -1015,7 +1017,8 @@ int parse_window(mc_bam_gpu* g, int64_t o, int64_t n, bool partial, int64_t* con
                 reads_walk_kernel<true><<<grid, 256, 0, st>>>(d, n, g->seg_off.p, 0, nseg, n_ref, g->reads_k,
                                                               g->res.p, g->out_off.p, g->boff.p, g->tid.p, g->pos.p,
                                                               g->rend_pos.p, g->sflag.p, g->rbits.p, g->rkmer.p,
-                                                              g->rnlen.p, g->soff.p, g->sseq.p);
+                                                              g->rnlen.p, g->soff.p, g->sseq.p,
+                                                              g->subset ? g->tid_map.p : nullptr);
                 HIP_TRY(hipGetLastError());
             }
         }
@@ -2029,6 +2032,25 @@ extern "C" int mc_bam_gpu_open_reads(const char* path, int device, int n_threads
     g->reads_k = k;
     const double t0 = now_s();
     if (int rc = gpu_decode(g.get(), window_bytes)) return rc;
+    g->t_open = (now_s() - t0) * 1e3;
+    *out = g.release();
+    return MC_OK;
+}
+
+extern "C" int mc_bam_gpu_open_reads_extents(const char* path, int device, int n_threads, int k, int32_t n_ref,
+                                             const mc_contig_extent* ext, int64_t n_no_coor, int32_t n_sel,
+                                             const int32_t* sel, mc_bam_gpu** out) {
+    MC_REQUIRE(path && out && (ext || n_ref == 0) && n_ref >= 0 && n_sel >= 0 && (sel || n_sel == 0) &&
+                   n_no_coor >= 0,
+               MC_E_INVALID, "bad argument");
+    MC_REQUIRE(k >= 1 && k <= 16, MC_E_INVALID, "k-mer length %d outside [1, 16]", k);
+    *out = nullptr;
+    std::unique_ptr<mc_bam_gpu> g;
+    if (int rc = open_common(path, device, n_threads, 0, g)) return rc;
+    g->reads_mode = true;
+    g->reads_k = k;
+    const double t0 = now_s();
+    if (int rc = gpu_decode_extents(g.get(), n_ref, ext, n_no_coor, n_sel, sel)) return rc;
     g->t_open = (now_s() - t0) * 1e3;
     *out = g.release();
     return MC_OK;

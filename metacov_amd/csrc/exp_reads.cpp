@@ -676,6 +676,24 @@ int reads_from_gpu(const mc_bam_gpu* g, const char* path, mc_reads* r) {
 
 }  // namespace
 
+extern "C" int mc_reads_open_gpu_extents(const char* path, int device, int n_threads, int k_len, int32_t n_ref,
+                                         const mc_contig_extent* ext, int64_t n_no_coor, int32_t n_sel,
+                                         const int32_t* sel, mc_reads** out) {
+    MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
+    MC_REQUIRE(k_len >= 1 && k_len <= 13, MC_E_RANGE, "k-mer length %d outside 1..13", k_len);
+    *out = nullptr;
+    std::unique_ptr<mc_reads> r(new mc_reads());
+    r->k = k_len;
+    mc_bam_gpu* g = nullptr;
+    if (int rc = mc_bam_gpu_open_reads_extents(path, device, n_threads, k_len, n_ref, ext, n_no_coor, n_sel, sel, &g))
+        return rc;
+    const int rc = reads_from_gpu(g, path, r.get());
+    mc_bam_gpu_close(g);
+    if (rc) return rc;
+    *out = r.release();
+    return MC_OK;
+}
+
 extern "C" int mc_reads_open_gpu(const char* path, int device, int n_threads, int k_len, mc_reads** out) {
     MC_REQUIRE(path && out, MC_E_INVALID, "null argument");
     MC_REQUIRE(k_len >= 1 && k_len <= 13, MC_E_RANGE, "k-mer length %d outside 1..13", k_len);

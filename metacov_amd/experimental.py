@@ -162,15 +162,33 @@ class ReadTable:
     bam.fetch (pileup.py:101).  decode: "host" (mc_reads_open: BGZF inflate
     and record walk on n_threads host threads) or "gpu" (mc_reads_open_gpu:
     the file inflated and walked on GPU `device`, the table copied back);
-    None: MC_READS_DECODE, else "host"."""
+    None: MC_READS_DECODE, else "host".
 
-    def __init__(self, path, k_len=7, n_threads=0, decode=None, device=0):
+    contigs=[...] (GPU decode): one rank's shard -- only the
+    placed records of those header contigs, decoded from their BGZF blocks
+    alone, located by the BAI (`index`, default <path>.bai) or an `extents`
+    table (ext, n_no_coor) as GpuBamFile takes it."""
+
+    def __init__(self, path, k_len=7, n_threads=0, decode=None, device=0, contigs=None, index=None,
+                 extents=None):
         self._lib = _lib.load()
         decode = decode or os.environ.get("MC_READS_DECODE", "host")
         if decode not in ("gpu", "host"):
             raise ValueError("decode must be 'gpu' or 'host'")
+        if contigs is not None and decode != "gpu":
+            raise ValueError("a contig subset is read with decode='gpu'")
         h = _lib.ctypes.c_void_p()
-        if decode == "gpu":
+        if contigs is not None:
+            from . import bam as _bam
+            sel = np.unique(np.asarray(contigs, dtype=np.int32))
+            if extents is None:
+                n_ref = len(_bam.BamFile(path, contigs=[], index=index).lengths)
+                extents = _bam.index_extents(index or str(path) + ".bai", n_ref)
+            ext = np.ascontiguousarray(extents[0], _bam.EXTENT_DTYPE)
+            rc = self._lib.mc_reads_open_gpu_extents(str(path).encode(), int(device), n_threads, k_len, len(ext),
+                                                     _lib.ptr(ext), int(extents[1]), len(sel), _lib.ptr(sel),
+                                                     _lib.ctypes.byref(h))
+        elif decode == "gpu":
             rc = self._lib.mc_reads_open_gpu(str(path).encode(), int(device), n_threads, k_len,
                                              _lib.ctypes.byref(h))
         else:
@@ -331,7 +349,7 @@ class EcorEngine:
 
 # ------------------------------------------------------------------ estimator
 
-def _as_reads(bam, k_len, n_threads, decode=None, device=0):
+def _as_reads(bam, k_len, n_threads, decode=None, device=0, contigs=None, extents=None):
     if isinstance(bam, ReadTable):
         if bam.k_len != k_len:
             raise ValueError("ReadTable was opened for k=%d, not %d" % (bam.k_len, k_len))
@@ -340,6 +358,8 @@ def _as_reads(bam, k_len, n_threads, decode=None, device=0):
     if isinstance(path, bytes):
         path = path.decode()
     if isinstance(path, (str, os.PathLike)):
+        if contigs is not None and decode == "gpu":
+            return ReadTable(path, k_len, n_threads, decode, device, contigs=contigs, extents=extents), True
         return ReadTable(path, k_len, n_threads, decode, device), True
     raise TypeError("bam must be a BAM path or a metacov_amd.experimental.ReadTable")
 
@@ -408,14 +428,17 @@ class RegionResult:
         return self.row
 
 
-def experimental_batch(bam, k_cor, k_len, fasta, regions, device=0, n_threads=0, timings=None):
+def experimental_batch(bam, k_cor, k_len, fasta, regions, device=0, n_threads=0, timings=None, contigs=None,
+                       extents=None):
     """pileup.experimental for every (ref, start, end) in `regions`; a list
     of RegionResult in input order.  Reads: one host pass per region on
     n_threads threads; sequence: one GPU launch for all regions.  A BAM
     path is decoded on the GPU when there is a FASTA (the run uses `device`
-    anyway; MC_READS_DECODE overrides), else on the host."""
+    anyway; MC_READS_DECODE overrides), else on the host.  contigs /
+    extents (a GPU decode): only those header contigs' records are decoded
+    (a distributed rank's shard; every region must lie on one of them)."""
     decode = os.environ.get("MC_READS_DECODE") or ("gpu" if fasta is not None else "host")
-    reads, own_reads = _as_reads(bam, k_len, n_threads, decode, device)
+    reads, own_reads = _as_reads(bam, k_len, n_threads, decode, device, contigs, extents)
     fasta = _as_fasta(fasta)
     try:
         return _batch(reads, k_cor, k_len, fasta, list(regions), device, n_threads, timings)

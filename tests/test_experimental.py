@@ -339,6 +339,42 @@ def test_read_table_gpu_decode_edge_files(tmp_path, lib_built):
 
 
 @pytest.mark.gpu
+def test_read_table_gpu_contig_subset(tmp_path, lib_built, golden_dir):
+    """A rank's read table (contigs=[...]): only those contigs' BGZF blocks
+    decoded, located by the BAI or by a whole-file decode's extents table;
+    its records are the host table's records of those contigs."""
+    from metacov_amd.bam import GpuBamFile, build_index
+    mixed = str(tmp_path / "mixed.bam")
+    _mixed_reads_bam(mixed, n=30_000)
+    multi = str(tmp_path / "multi.bam")
+    import shutil
+    shutil.copy(os.path.join(golden_dir, "synth_multi.bam"), multi)
+    for path in (mixed, multi):
+        build_index(path)
+        with mx.ReadTable(path, 6, decode="host") as h:
+            fh, first = h.fields(), None
+            n_ref = len(h.references)
+        first = fh["first"]
+        with GpuBamFile(path) as whole:
+            ext = whole.extents()
+        for sel in ([0], [n_ref - 1], list(range(0, n_ref, 2)), []):
+            for extents in (None, ext):
+                with mx.ReadTable(path, 6, decode="gpu", contigs=sel, extents=extents) as g:
+                    fg = g.fields()
+                keep = np.zeros(len(fh["pos"]), bool)
+                for t in sel:
+                    keep[first[t]:first[t + 1]] = True
+                for key in ("pos", "end", "flag", "bits", "kmer"):
+                    np.testing.assert_array_equal(fh[key][keep], fg[key], err_msg=key)
+                assert [nm for nm, k in zip(fh["name"], keep) if k] == fg["name"]
+                for t in range(n_ref):
+                    want = first[t + 1] - first[t] if t in sel else 0
+                    assert fg["first"][t + 1] - fg["first"][t] == want
+                    if t in sel:
+                        assert fg["max_span"][t] == fh["max_span"][t]
+
+
+@pytest.mark.gpu
 def test_read_table_gpu_unsorted_rejected(tmp_path, lib_built):
     from metacov_amd._lib import MetacovError
     path = str(tmp_path / "u.bam")
@@ -489,11 +525,14 @@ def _indexable_fasta(golden_dir, tmp_path):
 
 
 @pytest.mark.gpu
-def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path):
+@pytest.mark.parametrize("indexed", [True, False])
+def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path, indexed):
     """`metacov pileup -k` under torch.distributed.run with 2 ranks: each rank
-    computes the experimental columns of the regions on its own contigs and
-    rank 0 gathers them with the region table; the CSV equals one process's
-    byte for byte (gloo: both ranks share the box's one GPU)."""
+    computes the experimental columns of the regions on its own contigs (its
+    read table decoded from those contigs' BGZF blocks, found by the BAI or
+    by rank 0's extents table) and rank 0 gathers them with the region table;
+    the CSV equals one process's byte for byte (gloo: both ranks share the
+    box's one GPU)."""
     import socket
     import subprocess
     import sys
@@ -511,6 +550,9 @@ def test_cli_kmer_histogram_two_ranks(golden_dir, lib_built, tmp_path):
     hist.write_text("\n".join(rows) + "\n")
     fasta = _indexable_fasta(golden_dir, tmp_path)
     bam = os.path.join(golden_dir, "bbmap.sorted.bam")
+    if not indexed:
+        import shutil
+        bam = shutil.copy(bam, str(tmp_path / "noindex.bam"))
     args = ["-b", bam, "-rb", os.path.join(golden_dir, "regions.blast7"), "-k", str(hist), "-f", fasta]
     one = tmp_path / "one.csv"
     res = CliRunner().invoke(cli_pileup, args + ["-o", str(one)])
