@@ -88,6 +88,21 @@ namespace {
 #define MC_SCAN_SLICE 256
 #endif
 constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SCAN_DYN)
+//   MC_SCAN_STAGE16  a batch's bases and reference window staged with 16-byte
+//                  loads all issued before the first wait (0: dword loop,
+//                  one round trip per 4 dwords per lane)
+#ifndef MC_SCAN_STAGE16
+#define MC_SCAN_STAGE16 1
+#endif
+//   MC_SCAN_REGCOLS  the per-read columns (rlen, flag, gpos, gisize) taken
+//                  from the prefetched registers (0: reloaded from global
+//                  memory where they are used, an L2 round trip each)
+#ifndef MC_SCAN_REGCOLS
+#define MC_SCAN_REGCOLS 1
+#endif
+#ifndef MC_SCAN_STAGE_REGS
+#define MC_SCAN_STAGE_REGS 3      // 16-byte units per lane in flight (VGPRs: 4 each)
+#endif
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
@@ -158,6 +173,8 @@ struct ScanArgs {
 // LDS compile to flat instructions (vector-memory path, several times
 // slower than ds_* for the atomics and byte reads this kernel lives on).
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
 
@@ -213,14 +230,14 @@ __device__ __forceinline__ void inc(lds_u32* lds_base, uint32_t* g, int64_t i, b
 template <typename P8, typename P32>
 __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s, P32 s32,
                                              const RefWin& rw, lds_u32* lds, bool defer,
-                                             bool isize_done) {
-    const int32_t rlen = a.rlen[r], flag = a.flag[r], gpos = a.gpos[r];
+                                             bool isize_done, int32_t rlen, int32_t flag, int32_t gpos,
+                                             int32_t isz) {
     const bool rev = (flag & 0x10) != 0;
     int g = 0;
     for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((flag & a.fmask[f]) ? 1 : 0);
 
     if (a.isz_on && !isize_done) {
-        int32_t v = a.gisize[r];
+        int32_t v = isz;
         v = v < 0 ? -v : v;
         inc(lds + a.lds_isz, a.isz, (int64_t)v * a.G + g, a.isz_lds);
         if (a.isz_lds)
@@ -366,11 +383,12 @@ __device__ __forceinline__ void count_bases_lanes(const ScanArgs& a, bool pendin
 }
 
 __device__ __forceinline__ void count_bases(lds_cu64* inc_tab, const ScanArgs& a, int64_t r, bool pending, bool act,
-                                            int soff, lds_u32* sseq, lds_u32* lds, int lane) {
+                                            int soff, lds_u32* sseq, lds_u32* lds, int lane, int32_t rlen_r,
+                                            int32_t flag_r) {
     uint64_t pend = __ballot(pending);
     if (!pend) return;
-    const int32_t rlen = act ? a.rlen[r] : 0;
-    const int32_t fl = act ? a.flag[r] : 0;
+    const int32_t rlen = act ? rlen_r : 0;
+    const int32_t fl = act ? flag_r : 0;
     int g = 0;
     for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
     const int first = __builtin_ctzll(pend);
@@ -533,11 +551,12 @@ __device__ __forceinline__ void flush_pair(const ScanArgs& a, lds_u32* lds, int 
 }
 
 __device__ __forceinline__ void count_bases_pairs(lds_cu64* tab, const ScanArgs& a, int64_t r, bool pending,
-                                                  bool act, int soff, lds_u32* sseq, lds_u32* lds, int lane) {
+                                                  bool act, int soff, lds_u32* sseq, lds_u32* lds, int lane,
+                                                  int32_t rlen_r, int32_t flag_r) {
     uint64_t pend = __ballot(pending);
     if (!pend) return;
-    const int32_t rlen = act ? a.rlen[r] : 0;
-    const int32_t fl = act ? a.flag[r] : 0;
+    const int32_t rlen = act ? rlen_r : 0;
+    const int32_t fl = act ? flag_r : 0;
     int g = 0;
     for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
     if (!a.base_lds || __ballot(pending && rlen > 256)) {   // BaseHist in global memory, or long reads
@@ -595,7 +614,7 @@ __device__ __forceinline__ void ref_span(const ScanArgs& a, int32_t rlen, int32_
 // (MC_SCAN_PREFETCH), so a batch starts without a global round trip.
 struct Cols {
     int64_t so = 0, se = 0;
-    int32_t rid = -1, rlen = 0, gpos = 0, flag = 0;
+    int32_t rid = -1, rlen = 0, gpos = 0, flag = 0, isz = 0;
 };
 __device__ __forceinline__ Cols load_cols(const ScanArgs& a, int64_t r, bool valid) {
     Cols c;
@@ -606,6 +625,7 @@ __device__ __forceinline__ Cols load_cols(const ScanArgs& a, int64_t r, bool val
         c.rlen = a.rlen[r];
         c.gpos = a.gpos[r];
         c.flag = a.flag[r];
+        if (a.isz_on) c.isz = a.gisize[r];
     }
     return c;
 }
@@ -613,6 +633,30 @@ __device__ __forceinline__ Cols load_cols(const ScanArgs& a, int64_t r, bool val
 __device__ __forceinline__ int64_t wave_max(int64_t v) {
     for (int d = 32; d > 0; d >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, d, 64));
     return v;
+}
+
+// Copies the 16-byte units [0, nq) of src (16-byte aligned) to dst (LDS,
+// 16-byte aligned): every lane's loads issued before the first wait, one
+// round trip per batch.  An aligned 16-byte unit never crosses a page, so the
+// bytes around a buffer's first and last valid ones are safe to read.
+template <int kMaxUnits>
+__device__ __forceinline__ void stage16(lds_u32* dst, const u32x4* __restrict__ src, int nq, int lane) {
+    constexpr int kPer = (kMaxUnits + 63) / 64;
+    constexpr int kRound = kPer < MC_SCAN_STAGE_REGS ? kPer : MC_SCAN_STAGE_REGS;   // units per lane in flight
+#pragma unroll 1
+    for (int k0 = 0; k0 < kPer && 64 * k0 < nq; k0 += kRound) {
+        u32x4 v[kRound];
+#pragma unroll
+        for (int k = 0; k < kRound; ++k) {
+            const int i = lane + 64 * (k0 + k);
+            if (i < nq) v[k] = __builtin_nontemporal_load(src + i);
+        }
+#pragma unroll
+        for (int k = 0; k < kRound; ++k) {
+            const int i = lane + 64 * (k0 + k);
+            if (i < nq) *((lds_u32x4*)dst + i) = v[k];
+        }
+    }
 }
 
 // One wave walks its slice of reads in batches of up to 64 consecutive
@@ -697,7 +741,7 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
                     RefWin rw{nullptr, 0, nullptr, 0, 0};
                     if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
                     process_read(a, r, a.seq + so, reinterpret_cast<const uint32_t*>(a.seq + so), rw,
-                                 lds, false, false);
+                                 lds, false, false, a.rlen[r], a.flag[r], a.gpos[r], a.isz_on ? a.gisize[r] : 0);
                 }
                 r0 += 1;
                 if (!MC_SCAN_PREFETCH) nx = load_cols(a, r0 + lane, r0 + lane < rend);
@@ -705,10 +749,19 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             }
             const bool act = lane < m;
             const int64_t end = __shfl((long long)se, m - 1, 64);
-            // stage the batch's bases
-            const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.seq + (base & ~int64_t(3)));
-            const int nwd = (int)((end - (base & ~int64_t(3)) + 3) >> 2);
-            for (int i = lane; i < nwd; i += 64) sseq[i] = g32[i];
+            // stage the batch's bases (sdl: dwords between the staged origin
+            // and the batch's first base)
+            int sdl = 0;
+            if (MC_SCAN_STAGE16) {
+                const uintptr_t g0 = reinterpret_cast<uintptr_t>(a.seq + base), g16 = g0 & ~uintptr_t(15);
+                const int nq = (int)((reinterpret_cast<uintptr_t>(a.seq + end) - g16 + 15) >> 4);
+                stage16<(kSeqStage + kStagePad) / 16>(sseq, reinterpret_cast<const u32x4*>(g16), nq, lane);
+                sdl = (int)(g0 - g16) >> 2;
+            } else {
+                const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.seq + (base & ~int64_t(3)));
+                const int nwd = (int)((end - (base & ~int64_t(3)) + 3) >> 2);
+                for (int i = lane; i < nwd; i += 64) sseq[i] = g32[i];
+            }
             // the reference window, when the batch shares one sequence (the
             // prefix span at its last read)
             const int32_t rid = act ? ridv : -1;
@@ -722,10 +775,17 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
                 if (whi > wlo && whi - wlo <= kRefStage) {
                     const uint8_t* gref = a.ref + a.ref_off[rid0];
                     const uintptr_t ga = reinterpret_cast<uintptr_t>(gref + wlo);
-                    const uint32_t* q = reinterpret_cast<const uint32_t*>(ga & ~uintptr_t(3));
-                    const int nrw = (int)((whi - wlo + (int64_t)(ga & 3) + 3) >> 2);
-                    for (int i = lane; i < nrw; i += 64) sref[i] = q[i];
-                    rw.w = (lds_cu8*)sref + (ga & 3);
+                    if (MC_SCAN_STAGE16) {
+                        const uintptr_t g16 = ga & ~uintptr_t(15);
+                        const int nq = (int)((whi - wlo + (int64_t)(ga - g16) + 15) >> 4);
+                        stage16<(kRefStage + kStagePad) / 16>(sref, reinterpret_cast<const u32x4*>(g16), nq, lane);
+                        rw.w = (lds_cu8*)sref + (ga - g16);
+                    } else {
+                        const uint32_t* q = reinterpret_cast<const uint32_t*>(ga & ~uintptr_t(3));
+                        const int nrw = (int)((whi - wlo + (int64_t)(ga & 3) + 3) >> 2);
+                        for (int i = lane; i < nrw; i += 64) sref[i] = q[i];
+                        rw.w = (lds_cu8*)sref + (ga & 3);
+                    }
                     rw.wlo = wlo;
                     rw.whi = whi;
                 }
@@ -737,11 +797,11 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             bool isize_done = false;
             if (a.isz_on && a.isz_lds) {
                 int g = 0;
-                const int32_t fl = act ? a.flag[r] : 0;
+                const int32_t fl = act ? (MC_SCAN_REGCOLS ? cc.flag : a.flag[r]) : 0;
                 for (int f = 0; f < a.n_flags; ++f) g = (g << 1) | ((fl & a.fmask[f]) ? 1 : 0);
                 const int g0 = __shfl(g, 0, 64);
                 if (__ballot(act && g != g0) == 0) {
-                    int32_t v = act ? a.gisize[r] : 0;
+                    int32_t v = act ? (MC_SCAN_REGCOLS ? cc.isz : a.gisize[r]) : 0;
                     v = v < 0 ? -v : v;
                     if (act)
                         __hip_atomic_fetch_add(lds + a.lds_isz + (int64_t)v * a.G + g, 1u, __ATOMIC_RELAXED,
@@ -753,15 +813,20 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
                     isize_done = true;
                 }
             }
-            const int soff = (int)((so - (base & ~int64_t(3))) >> 2);   // the read's first dword
+            const int soff = (int)((so - (base & ~int64_t(3))) >> 2) + sdl;   // the read's first dword
             bool pending = false;
             if (act) {
                 lds_cu32* rs32 = sseq + soff;
-                pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done);
+                pending = process_read(a, r, (lds_cu8*)rs32, rs32, rw, lds, true, isize_done,
+                                       MC_SCAN_REGCOLS ? cc.rlen : a.rlen[r], MC_SCAN_REGCOLS ? cc.flag : a.flag[r],
+                                       MC_SCAN_REGCOLS ? cc.gpos : a.gpos[r],
+                                       a.isz_on ? (MC_SCAN_REGCOLS ? cc.isz : a.gisize[r]) : 0);
             }
             if (a.base_on) {
-                if (MC_SCAN_PAIRS) count_bases_pairs(pair_tab, a, r, pending, act, soff, sseq, lds, lane);
-                else count_bases(inc_tab, a, r, pending, act, soff, sseq, lds, lane);
+                const int32_t rl = MC_SCAN_REGCOLS ? cc.rlen : act ? a.rlen[r] : 0;
+                const int32_t fl = MC_SCAN_REGCOLS ? cc.flag : act ? a.flag[r] : 0;
+                if (MC_SCAN_PAIRS) count_bases_pairs(pair_tab, a, r, pending, act, soff, sseq, lds, lane, rl, fl);
+                else count_bases(inc_tab, a, r, pending, act, soff, sseq, lds, lane, rl, fl);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
