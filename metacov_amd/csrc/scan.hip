@@ -100,6 +100,10 @@ constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SC
 #ifndef MC_SCAN_REGCOLS
 #define MC_SCAN_REGCOLS 1
 #endif
+//   MC_SCAN_NEED   stage / cut a batch only for what its tables read
+#ifndef MC_SCAN_NEED
+#define MC_SCAN_NEED 1
+#endif
 #ifndef MC_SCAN_STAGE_REGS
 #define MC_SCAN_STAGE_REGS 3      // 16-byte units per lane in flight (VGPRs: 4 each)
 #endif
@@ -683,6 +687,10 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
     lds_u32* sseq = lds + a.stage_off + wave * (kStageBytes / 4);
     lds_u32* sref = sseq + (kSeqStage + kStagePad) / 4;
     const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
+    // which tables read the bases / the reference: a batch stages (and is cut
+    // for) only what they read (kmer-only and isize-only runs skip the window)
+    const bool need_seq = MC_SCAN_NEED ? (a.base_on || a.kmer_on) : true;
+    const bool need_ref = MC_SCAN_NEED ? (a.base_on || a.mir_on) : true;
     // work != null: each wave takes slices of per_wave reads from a queue
     // (a static slice per wave left the kernel waiting on the waves whose
     // slices cover sparse stretches: many short batches); else slice gw
@@ -703,7 +711,7 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             const int64_t so = cc.so, se = cc.se;
             if (valid && (so & 3)) atomicOr(a.error, 1);
             const int64_t base = __shfl((long long)so, 0, 64);
-            const uint64_t fit = __ballot(valid && se - base <= kSeqStage);
+            const uint64_t fit = __ballot(valid && (!need_seq || se - base <= kSeqStage));
             const int m_seq = fit == ~0ull ? 64 : __builtin_ctzll(~fit);
             // the batch also ends where its reads leave lane 0's sequence or the
             // reference window they touch outgrows kRefStage (inclusive prefix
@@ -714,21 +722,24 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             const int32_t rid0 = __shfl(ridv, 0, 64);
             const bool rid0_ok = rid0 >= 0 && rid0 < a.n_ref;
             int64_t plo = INT64_MAX, phi = INT64_MIN;
-            if (valid && rid0_ok) ref_span(a, cc.rlen, cc.gpos, cc.flag, plo, phi);
+            int m_ref = 64;
+            if (need_ref) {
+                if (valid && rid0_ok) ref_span(a, cc.rlen, cc.gpos, cc.flag, plo, phi);
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int64_t ol = __shfl_up((long long)plo, d, 64), oh = __shfl_up((long long)phi, d, 64);
-                if (lane >= d) {
-                    plo = min(plo, ol);
-                    phi = max(phi, oh);
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int64_t ol = __shfl_up((long long)plo, d, 64), oh = __shfl_up((long long)phi, d, 64);
+                    if (lane >= d) {
+                        plo = min(plo, ol);
+                        phi = max(phi, oh);
+                    }
                 }
+                const int64_t L0 = rid0_ok ? a.ref_len[rid0] : 0;
+                const int64_t cwlo = max<int64_t>(plo, 0), cwhi = min<int64_t>(phi, L0);
+                const bool wfit = rid0_ok ? ridv == rid0 && (cwhi <= cwlo || cwhi - cwlo <= kRefStage)
+                                          : (ridv < 0 || ridv >= a.n_ref);
+                const uint64_t wf = __ballot(valid && wfit);
+                m_ref = wf == ~0ull ? 64 : __builtin_ctzll(~wf);
             }
-            const int64_t L0 = rid0_ok ? a.ref_len[rid0] : 0;
-            const int64_t cwlo = max<int64_t>(plo, 0), cwhi = min<int64_t>(phi, L0);
-            const bool wfit = rid0_ok ? ridv == rid0 && (cwhi <= cwlo || cwhi - cwlo <= kRefStage)
-                                      : (ridv < 0 || ridv >= a.n_ref);
-            const uint64_t wf = __ballot(valid && wfit);
-            const int m_ref = wf == ~0ull ? 64 : __builtin_ctzll(~wf);
             const int m = m_seq == 0 ? 0 : MC_SCAN_CUT ? min(m_seq, max(m_ref, 1)) : m_seq;
             {   // the next batch's columns, in flight while this one is processed
                 const int64_t rn = r0 + max(m, 1) + lane;
@@ -752,7 +763,9 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             // stage the batch's bases (sdl: dwords between the staged origin
             // and the batch's first base)
             int sdl = 0;
-            if (MC_SCAN_STAGE16) {
+            if (!need_seq) {
+                // (no table reads the bases: nothing staged)
+            } else if (MC_SCAN_STAGE16) {
                 const uintptr_t g0 = reinterpret_cast<uintptr_t>(a.seq + base), g16 = g0 & ~uintptr_t(15);
                 const int nq = (int)((reinterpret_cast<uintptr_t>(a.seq + end) - g16 + 15) >> 4);
                 stage16<(kSeqStage + kStagePad) / 16>(sseq, reinterpret_cast<const u32x4*>(g16), nq, lane);
@@ -768,7 +781,7 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             const bool one_ref = __ballot(act && rid != rid0) == 0 && rid0_ok;
             RefWin rw{nullptr, 0, nullptr, 0, 0};
             if (rid >= 0 && rid < a.n_ref) rw = RefWin{a.ref + a.ref_off[rid], a.ref_len[rid], nullptr, 0, 0};
-            if (one_ref) {
+            if (one_ref && need_ref) {
                 const int64_t L = a.ref_len[rid0];
                 const int64_t wlo = max<int64_t>(__shfl((long long)plo, m - 1, 64), 0);
                 const int64_t whi = min<int64_t>(__shfl((long long)phi, m - 1, 64), L);
