@@ -104,6 +104,10 @@ constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SC
 #ifndef MC_SCAN_NEED
 #define MC_SCAN_NEED 1
 #endif
+//   MC_SCAN_PF2    a second batch of accessor columns in flight (see scan_kernel)
+#ifndef MC_SCAN_PF2
+#define MC_SCAN_PF2 1
+#endif
 #ifndef MC_SCAN_STAGE_REGS
 #define MC_SCAN_STAGE_REGS 3      // 16-byte units per lane in flight (VGPRs: 4 each)
 #endif
@@ -704,6 +708,15 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
         if (r0 >= a.n) break;
         const int64_t rend = min(a.n, r0 + a.per_wave);
         Cols nx = load_cols(a, r0 + lane, r0 + lane < rend);
+        // MC_SCAN_PF2: the columns of the 64 reads after the next batch, loaded
+        // one batch early; used when the next batch is a whole 64 reads (most
+        // batches), so two batches' loads are in flight
+        Cols nx2;
+        int64_t spec = -1;   // first read of nx2 (-1: none)
+        if (MC_SCAN_PF2) {
+            nx2 = load_cols(a, r0 + 64 + lane, r0 + 64 + lane < rend);
+            spec = r0 + 64;
+        }
         while (r0 < rend) {
             const int64_t r = r0 + lane;
             const bool valid = r < rend;
@@ -742,9 +755,17 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
             }
             const int m = m_seq == 0 ? 0 : MC_SCAN_CUT ? min(m_seq, max(m_ref, 1)) : m_seq;
             {   // the next batch's columns, in flight while this one is processed
-                const int64_t rn = r0 + max(m, 1) + lane;
-                if (MC_SCAN_PREFETCH) nx = load_cols(a, rn, rn < rend);
-                else nx = load_cols(a, rn, false);
+                const int64_t s1 = r0 + max(m, 1), rn = s1 + lane;
+                if (MC_SCAN_PF2) {
+                    if (spec == s1) nx = nx2;
+                    else nx = load_cols(a, rn, rn < rend);
+                    nx2 = load_cols(a, rn + 64, rn + 64 < rend);
+                    spec = s1 + 64;
+                } else if (MC_SCAN_PREFETCH) {
+                    nx = load_cols(a, rn, rn < rend);
+                } else {
+                    nx = load_cols(a, rn, false);
+                }
             }
             if (m == 0) {   // the first read alone exceeds the stage: global path
                 if (lane == 0) {
