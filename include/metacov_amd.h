@@ -205,6 +205,19 @@ int mc_region_stats_device(mc_ctx* ctx, int64_t R, const int32_t* tid,
                            const int64_t* start, const int64_t* end,
                            mc_region_stat* d_out);
 
+/* numpy's float64 sum of squared deviations of each region's column vector,
+ * in numpy's own order, from the depth vector in HBM: with m = mean[r]
+ * (= fl(sum / n), what np.mean returns), out[r] = the sum np.std forms over
+ * fl(fl(v - m)^2): pairwise_sum within each 8192-element reduction buffer,
+ * the buffers added in turn.  sqrt(fl(out[r] / n)) is then np.std(columns)
+ * bit for bit (pileup.py:22).  classic() rounds it to two decimals; the
+ * exact variance rounds the same way except within numpy's rounding noise of
+ * a .xx5 boundary, and only such regions need this (metacov_amd.engine).
+ * Regions must be non-empty; positions past the extent count as 0. */
+int mc_region_np_sqdev(mc_ctx* ctx, int64_t R, const int32_t* tid,
+                       const int64_t* start, const int64_t* end,
+                       const double* mean, double* out);
+
 /* Depth AND region statistics in one pass: K2 folds every tile into the
  * regions covering it while the depth values are still in registers, so the
  * depth vector is written once and never re-read.  Regions must not overlap
@@ -368,6 +381,12 @@ int mc_bam_gpu_intervals_device(const mc_bam_gpu* g, int64_t* n, const int32_t**
 int mc_bam_gpu_intervals(const mc_bam_gpu* g, int32_t* tid, int32_t* pos, int32_t* span);
 int mc_bam_gpu_stats(const mc_bam_gpu* g, mc_bam_gpu_timings* t);
 int mc_bam_gpu_close(mc_bam_gpu* g);
+/* Releases the decode's staging buffers (compressed bytes, inflated stream,
+ * block and segment tables) of an open handle; its results (intervals, read
+ * table or scan columns, the per-contig extents) stay valid.  For handles
+ * kept between calls (metacov_amd.pileup's path cache).  freed (optional):
+ * device bytes released. */
+int mc_bam_gpu_trim(mc_bam_gpu* g, int64_t* freed);
 /* `metacov scan` input decoded on the GPU (the BAM half of scan.pyx:188-216,
  * IteratorRowAll: every record in file order; replaces mc_scan_src_open_bam's
  * host walk): the whole file as the SoA batch mc_scan_add_batch_device takes

@@ -106,6 +106,7 @@ SIGNATURES = {
     "mc_contig_offset": [_P, _I32, _PI64, _PI64],
     "mc_region_stats": [_P, _I64, _P, _P, _P, _P],
     "mc_region_stats_device": [_P, _I64, _P, _P, _P, _P],
+    "mc_region_np_sqdev": [_P, _I64, _P, _P, _P, _P, _P],
     "mc_compute_depth_stats": [_P, _I64, _P, _P, _P, _P],
     "mc_compute_depth_stats_device": [_P, _I64, _P, _P, _P, _P],
     "mc_fused_fallbacks": [_P, _PI64],
@@ -139,6 +140,7 @@ SIGNATURES = {
     "mc_bam_gpu_intervals": [_P, _P, _P, _P],
     "mc_bam_gpu_stats": [_P, _P],
     "mc_bam_gpu_close": [_P],
+    "mc_bam_gpu_trim": [_P, _PI64],
     "mc_bam_gpu_open_scan": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, _I64, _PP],
     "mc_bam_gpu_scan_device": [_P, _PI64, _PP, _PP, _PP, _PP, _PP, _PP, _PP, _PI64],
     "mc_bam_gpu_open_reads": [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _PP],

@@ -400,6 +400,14 @@ class GpuBamFile:
             tid = self.contigs[tid]
         return tid, pos, span
 
+    def trim(self):
+        """Releases the decode's staging buffers in HBM (compressed file,
+        inflated stream, block and segment tables); the intervals, the
+        extents table and the engine stay.  Returns the bytes released."""
+        freed = ctypes.c_int64()
+        check(self._lib.mc_bam_gpu_trim(self._h, ctypes.byref(freed)))
+        return freed.value
+
     def timings(self):
         t = _lib.GpuDecodeTimings()
         check(self._lib.mc_bam_gpu_stats(self._h, ctypes.byref(t)))

@@ -40,7 +40,7 @@ from . import experimental as _experimental
 from . import regions as _regions
 from . import scan as _scan
 from .bam import BamFile, GpuBamFile, StreamedBam, index_stats
-from .engine import REGION_STAT_DTYPE, classic_stats
+from .engine import REGION_STAT_DTYPE, classic_stats, numpy_std
 
 logging.basicConfig(level=logging.INFO,
                     format="[%(relativeCreated)6.1f %(funcName)s]  %(message)s",
@@ -172,19 +172,22 @@ def compute_rows(bam, tids, starts, ends, device=0, max_depth=_depthcap.HTSLIB_M
     the library falls back to K2 + K3 otherwise.  max_depth: htslib's read
     cap per region query; only regions whose exact maximum could reach it
     are recomputed, together in one more engine call (metacov_amd.depthcap);
-    0 / None: exact depths."""
+    0 / None: exact depths.  Returns (rows, std): std is numpy's own np.std
+    value for the rows near a rounding tie, NaN elsewhere (engine.numpy_std)."""
     if len(tids) == 0:
-        return np.zeros(0, dtype=REGION_STAT_DTYPE)
+        return np.zeros(0, dtype=REGION_STAT_DTYPE), np.zeros(0)
     eng = bam.engine(device, compute=False)
-    rows = eng.compute_depth_stats(np.asarray(bam.local_tid(tids), np.int32), starts, ends)
+    local = np.asarray(bam.local_tid(tids), np.int32)
+    rows = eng.compute_depth_stats(local, starts, ends)
     eng._depth_ready = True
+    std = numpy_std(eng, rows, local, starts, ends)
     if max_depth:
         rows, n_cap, dropped = _depthcap.apply_cap(bam, rows, tids, starts, ends, bam.lengths,
-                                                   max_depth, device)
+                                                   max_depth, device, std=std)
         if n_cap:
             log.info("max_depth %d: %d regions deep enough for the pileup cap, %d reads dropped",
                      max_depth, n_cap, dropped)
-    return rows
+    return rows, std
 
 
 def experimental_results(path, exp, references, tids, starts, ends, device=0, contigs=None, extents=None):
@@ -201,13 +204,14 @@ def experimental_results(path, exp, references, tids, starts, ends, device=0, co
                                             extents=extents)
 
 
-def write_csv(regions, rows, outfile, extra=None):
+def write_csv(regions, rows, outfile, extra=None, std=None):
     """Rows in input order exactly as cli.py:97-108 writes them; `extra`
     (experimental_batch results) adds the -k columns, its "RCOR is ZERO"
-    lines and its errors at the region where the reference meets them."""
+    lines and its errors at the region where the reference meets them.
+    std: numpy's std per row where given (engine.numpy_std; NaN: none)."""
     writer = None
     for i, (hit, row) in enumerate(zip(regions, rows)):
-        result = classic_stats(row)
+        result = classic_stats(row, None if std is None else std[i])
         if extra is not None:
             result.update(extra[i].emit(out=sys.stdout))
         if writer is None:
@@ -222,9 +226,9 @@ def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=_depthcap.HT
     then writes rows in input order exactly as cli.py:97-108 does; the rows
     before a failing region are written before its error is raised."""
     hits, tids, starts, ends, err = resolve_regions(bam, regions)
-    rows = compute_rows(bam, tids, starts, ends, device, max_depth)
+    rows, std = compute_rows(bam, tids, starts, ends, device, max_depth)
     extra = experimental_results(bam.filename, exp, bam.references, tids, starts, ends, device)
-    write_csv(hits, rows, outfile, extra)
+    write_csv(hits, rows, outfile, extra, std)
     if err is not None:
         raise err
 
@@ -254,7 +258,7 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         try:
             table_args = _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
                                        max_depth, legacy_endpos, decode, coll_dev, times)
-            head, regions, tids, starts, ends, rows, mine, r_max, region_err, shard = table_args
+            head, regions, tids, starts, ends, rows, std, mine, r_max, region_err, shard = table_args
             # -k: the read table of this rank's contigs only (their BGZF blocks, by
             # the BAI or rank 0's extents table), when the GPU decodes
             mine_extra = experimental_results(path, exp, head.references, tids[mine], starts[mine],
@@ -263,7 +267,7 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
             err = e
         mdist.agree_on_error(err, device=coll_dev)
         t0 = time.perf_counter()
-        table = mdist.all_gather_table(mdist.pack_rows(rows, mine), r_max, device=coll_dev)
+        table = mdist.all_gather_table(mdist.pack_rows(rows, mine, std), r_max, device=coll_dev)
         times["gather_s"] = time.perf_counter() - t0
         extra = None
         if exp is not None:          # each rank's experimental results (our own objects) to rank 0
@@ -277,7 +281,7 @@ def pileup_distributed(path, regionfile_blast7, regionfile_csv, outfile, exp=Non
         if rank == 0:
             log_counts(head)
             write_csv(regions, mdist.unpack_rows(table, len(regions), REGION_STAT_DTYPE), outfile,
-                      extra)
+                      extra, mdist.unpack_std(table, len(regions)))
         times["total_s"] = time.perf_counter() - t_start
         log.info("rank %d/%d phases: %s", rank, world, json.dumps(times))
     finally:
@@ -346,7 +350,7 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
     region_rank = owner[tids] if len(tids) else np.zeros(0, np.int64)
     mine = np.nonzero(region_rank == rank)[0]
     r_max = max(1, int(np.bincount(region_rank, minlength=world).max()) if len(tids) else 1)
-    rows = np.zeros(0, dtype=REGION_STAT_DTYPE)
+    rows, std = np.zeros(0, dtype=REGION_STAT_DTYPE), np.zeros(0)
     if len(mine):
         t0 = time.perf_counter()
         if full is not None:      # rank 0 keeps its shard of the whole file
@@ -364,7 +368,7 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
         times["decode_s"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         try:
-            rows = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
+            rows, std = compute_rows(bam, tids[mine], starts[mine], ends[mine], device, max_depth)
         finally:
             if decode == "gpu":
                 bam.close()
@@ -373,7 +377,7 @@ def _pileup_shard(path, regionfile_blast7, regionfile_csv, rank, world, device,
         full.close()
     # (contigs, extents) for this rank's -k read table: a contig-subset GPU decode
     shard = (shards[rank], ext) if decode == "gpu" and (have_index or ext is not None) else (None, None)
-    return head, regions, tids, starts, ends, rows, mine, r_max, region_err, shard
+    return head, regions, tids, starts, ends, rows, std, mine, r_max, region_err, shard
 
 
 @main.command()

@@ -2155,6 +2155,36 @@ extern "C" int mc_bam_gpu_close(mc_bam_gpu* g) {
     return MC_OK;
 }
 
+extern "C" int mc_bam_gpu_trim(mc_bam_gpu* g, int64_t* freed) {
+    MC_REQUIRE(g, MC_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(g->device));
+    for (hipStream_t s : {g->stream, g->up_stream, g->kstream[0], g->kstream[1], g->kstream[2]})
+        if (s) HIP_TRY(hipStreamSynchronize(s));
+    int64_t bytes = 0;
+    auto drop = [&](auto& b) {
+        bytes += (int64_t)(b.cap * sizeof(*b.p));
+        b.release();
+    };
+    // the decode's staging: compressed bytes, inflated stream, raw blocks,
+    // block / segment tables, scan-mode fill offsets; the results (the kept
+    // intervals, reads / scan columns, the per-contig table) stay
+    drop(g->comp[0]);
+    drop(g->comp[1]);
+    drop(g->inflated);
+    drop(g->tail);
+    drop(g->raw);
+    drop(g->blk);
+    drop(g->status);
+    drop(g->scratch);
+    drop(g->seg_off);
+    drop(g->found);
+    drop(g->out_off);
+    drop(g->res);
+    drop(g->boff);
+    if (freed) *freed = bytes;
+    return MC_OK;
+}
+
 extern "C" int mc_bam_gpu_open_extents(const char* path, int device, int n_threads, uint32_t flag_filter,
                                        int32_t n_ref, const mc_contig_extent* ext, int64_t n_no_coor, int32_t n_sel,
                                        const int32_t* sel, mc_bam_gpu** out) {

@@ -18,6 +18,7 @@
 #include "../../include/metacov_amd.h"
 #include "common.h"
 #include "kernels.h"
+#include "npstd.h"
 
 using namespace mc;
 
@@ -1867,6 +1868,61 @@ extern "C" int mc_region_stats(mc_ctx* ctx, int64_t R, const int32_t* tid, const
     HIP_TRY(hipMemcpyAsync(out, ctx->d_out.p, R * sizeof(mc_region_stat), hipMemcpyDeviceToHost,
                            ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MC_OK;
+}
+
+extern "C" int mc_region_np_sqdev(mc_ctx* ctx, int64_t R, const int32_t* tid, const int64_t* start,
+                                  const int64_t* end, const double* mean, double* out) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(ctx->depth_valid, MC_E_STATE, "depth not computed (call mc_compute_depth)");
+    MC_REQUIRE(R >= 0 && (R == 0 || (tid && start && end && mean && out)), MC_E_INVALID,
+               "bad region arrays");
+    if (R == 0) return MC_OK;
+    const int32_t nc = (int32_t)ctx->len.size();
+    std::vector<NpBlock> blk;
+    std::vector<int32_t> first((size_t)R + 1, 0);
+    for (int64_t r = 0; r < R; ++r) {
+        MC_REQUIRE(tid[r] >= 0 && tid[r] < nc, MC_E_INVALID, "region %lld: tid %d out of range",
+                   (long long)r, tid[r]);
+        MC_REQUIRE(start[r] >= 0 && end[r] > start[r], MC_E_INVALID,
+                   "region %lld: bad range [%lld, %lld)", (long long)r, (long long)start[r],
+                   (long long)end[r]);
+        const int64_t ext = ctx->extent[tid[r]];
+        for (int64_t p = start[r]; p < end[r]; p += kNpBuf) {
+            NpBlock b{};
+            b.n = (int32_t)std::min<int64_t>(kNpBuf, end[r] - p);
+            b.n_data = (int32_t)std::max<int64_t>(0, std::min<int64_t>(b.n, ext - p));
+            b.gpos = ctx->coff[tid[r]] + std::min(p, ext);
+            b.region = (int32_t)r;
+            blk.push_back(b);
+        }
+        MC_REQUIRE(blk.size() < (size_t(1) << 30), MC_E_RANGE, "regions too long");
+        first[(size_t)r + 1] = (int32_t)blk.size();
+    }
+    const int64_t nb = (int64_t)blk.size();
+    const size_t o_blk = 0, o_first = stage_align(nb * sizeof(NpBlock)),
+                 o_mean = o_first + stage_align((R + 1) * 4), o_bsum = o_mean + stage_align(R * 8),
+                 o_out = o_bsum + stage_align(nb * 8), total = o_out + stage_align(R * 8);
+    HIP_TRY(ctx->k3_stage.reserve(total));
+    unsigned char* h = ctx->k3_stage.host();
+    std::memcpy(h + o_blk, blk.data(), nb * sizeof(NpBlock));
+    std::memcpy(h + o_first, first.data(), (R + 1) * 4);
+    std::memcpy(h + o_mean, mean, R * 8);
+    unsigned char* d = ctx->k3_stage.d.p;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(d, h, o_bsum, hipMemcpyHostToDevice, s));
+    constexpr int kWaves = kBlock / 64;
+    hipLaunchKernelGGL(np_block_kernel, dim3((unsigned)((nb + kWaves - 1) / kWaves)), dim3(kBlock), 0, s,
+                       ctx->d_depth.p, reinterpret_cast<const NpBlock*>(d + o_blk), (int)nb,
+                       reinterpret_cast<const double*>(d + o_mean), reinterpret_cast<double*>(d + o_bsum));
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(np_region_kernel, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const double*>(d + o_bsum), reinterpret_cast<const int32_t*>(d + o_first),
+                       (int)R, reinterpret_cast<double*>(d + o_out));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h + o_out, d + o_out, R * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(out, h + o_out, R * 8);
     return MC_OK;
 }
 

@@ -2828,6 +2828,17 @@ struct FbArgs {
 // +1 us at C2's one workgroup and +20 us at C3's 250).  done_cnt: a device
 // counter, 0 between launches (the last workgroup resets it).  Every thread
 // of every workgroup calls this.
+//
+// The host reads, once the stamp is seen and without any stream sync:
+//   RegionOut rows (out[r]), the fallback flags (fallback[r]), K2's max depth
+//   copy (max_out) and the direct-path verdict copy (dres_out)
+// and each of them MUST be written with store_sys when `stamp` is set (the
+// `wt` paths of final_wave_row); a plain store of any of them would sit in
+// its XCD's L2 and race the host's spin.  The per-wave s_waitcnt vmcnt(0)
+// orders those system-scope stores before this workgroup's counter
+// increment; the last workgroup then releases at system scope (one fence per
+// launch, not per workgroup) before publishing the stamp, which also covers
+// its own writes.
 __device__ __forceinline__ void grid_done_stamp(unsigned* done_cnt, unsigned long long* stamp,
                                                 unsigned long long seq) {
     if (stamp == nullptr) return;
@@ -2837,6 +2848,7 @@ __device__ __forceinline__ void grid_done_stamp(unsigned* done_cnt, unsigned lon
         const unsigned prev = __hip_atomic_fetch_add(done_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == gridDim.x - 1) {
             __hip_atomic_store(done_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope, last workgroup only
             __hip_atomic_store(stamp, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }

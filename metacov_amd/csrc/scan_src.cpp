@@ -31,9 +31,11 @@
 #include <zlib.h>
 
 #include <cctype>
+#include <cstring>
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <thread>
 
 #include "bgzf.h"
@@ -135,6 +137,9 @@ struct mc_scan_src {
     int nt = 1;
     std::vector<std::string> names;
     std::vector<int64_t> lens;
+    std::unordered_map<std::string, int32_t> name_tid;   // SAM: RNAME -> tid (the first @SQ of a name)
+    std::string last_rname;                               // SAM: the previous record's RNAME and tid
+    int32_t last_tid = -1;
     std::unique_ptr<uint8_t[]> buf;
     size_t cap = 0, n = 0, o = 0, next_off = 0;
     bool have_header = false, last = false, done = false;
@@ -399,6 +404,7 @@ int sam_header(mc_scan_src* s) {
         }
         MC_REQUIRE(!name.empty() && len >= 0, MC_E_IO, "%s: line %lld: @SQ needs SN and LN", s->path.c_str(),
                    (long long)s->sam_line);
+        s->name_tid.emplace(name, (int32_t)s->names.size());
         s->names.push_back(name);
         s->lens.push_back(len);
     }
@@ -430,11 +436,18 @@ int sam_next(mc_scan_src* s, int64_t max_reads, int64_t max_bytes) {
                    MC_E_IO, "%s: line %lld: FLAG, POS or TLEN out of range", s->path.c_str(), (long long)s->sam_line);
         int32_t tid = -1;
         if (!(fl[2] == 1 && f[2][0] == '*')) {
-            const std::string rn(f[2], fl[2]);
-            auto it = std::find(s->names.begin(), s->names.end(), rn);
-            MC_REQUIRE(it != s->names.end(), MC_E_IO, "%s: line %lld: reference '%s' is not in the header",
-                       s->path.c_str(), (long long)s->sam_line, rn.c_str());
-            tid = (int32_t)(it - s->names.begin());
+            if (s->last_tid >= 0 && s->last_rname.size() == fl[2] &&
+                std::memcmp(s->last_rname.data(), f[2], fl[2]) == 0) {
+                tid = s->last_tid;   // sorted SAM: runs of one RNAME
+            } else {
+                const std::string rn(f[2], fl[2]);
+                auto it = s->name_tid.find(rn);
+                MC_REQUIRE(it != s->name_tid.end(), MC_E_IO, "%s: line %lld: reference '%s' is not in the header",
+                           s->path.c_str(), (long long)s->sam_line, rn.c_str());
+                tid = it->second;
+                s->last_rname = rn;
+                s->last_tid = tid;
+            }
         }
         const bool no_seq = fl[9] == 1 && f[9][0] == '*';
         const size_t L = no_seq ? 0 : fl[9];

@@ -96,18 +96,20 @@ def host_intervals(src, contigs):
     return tuple(np.concatenate([q[i] for q in parts]) for i in range(3))
 
 
-def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0):
+def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0, with_std=False):
     """Exact stat rows of regions (header contig ids) as pysam's capped
     pileup would fill classic()'s column vector: per region the overlapping
     records and the cap; then ONE engine call over all of them, each region
     its own contig of the batch (the same contig's reads repeated when
-    regions share it).  Returns (rows, reads dropped)."""
-    from .engine import CoverageEngine, REGION_STAT_DTYPE
+    regions share it).  Returns (rows, reads dropped), and with_std:
+    engine.numpy_std of the rows on that batch's depth as a third value."""
+    from .engine import CoverageEngine, REGION_STAT_DTYPE, numpy_std
     tids = np.asarray(tids, np.int64)
     starts = np.asarray(starts, np.int64)
     ends = np.asarray(ends, np.int64)
     if len(tids) == 0:
-        return np.zeros(0, dtype=REGION_STAT_DTYPE), 0
+        empty = np.zeros(0, dtype=REGION_STAT_DTYPE)
+        return (empty, 0, np.zeros(0)) if with_std else (empty, 0)
     tid, pos, span = host_intervals(src, tids)
     max_span = int(span.max()) if len(span) else 1
     idx = [region_reads(tid, pos, span, int(t), int(s), int(e), max_span)
@@ -121,23 +123,29 @@ def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, de
     try:
         eng.set_contigs(np.asarray(lengths, np.int64)[tids])
         eng.add_reads(vt[keep], vpos[keep], vspan[keep])
-        rows = eng.compute_depth_stats(np.arange(len(tids), dtype=np.int32), starts, ends)
+        local = np.arange(len(tids), dtype=np.int32)
+        rows = eng.compute_depth_stats(local, starts, ends)
+        std = numpy_std(eng, rows, local, starts, ends) if with_std else None
     finally:
         eng.close()
-    return rows, dropped
+    return (rows, dropped, std) if with_std else (rows, dropped)
 
 
-def apply_cap(src, rows, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0):
+def apply_cap(src, rows, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0, std=None):
     """Rows of the same regions under the cap: the exact `rows` where the cap
     cannot act (may_cap), the capped recompute elsewhere.  Returns (rows,
-    regions recomputed, reads dropped)."""
+    regions recomputed, reads dropped).  std (optional, engine.numpy_std of
+    `rows`): its recomputed regions' entries are replaced in place by those
+    of the capped rows."""
     if not max_depth or len(rows) == 0:
         return rows, 0, 0
     need = np.nonzero(may_cap(rows, max_depth))[0]
     if len(need) == 0:
         return rows, 0, 0
-    sub, dropped = capped_rows(src, np.asarray(tids)[need], np.asarray(starts)[need],
-                               np.asarray(ends)[need], lengths, max_depth, device)
+    sub, dropped, sub_std = capped_rows(src, np.asarray(tids)[need], np.asarray(starts)[need],
+                                        np.asarray(ends)[need], lengths, max_depth, device, with_std=True)
     out = rows.copy()
     out[need] = sub
+    if std is not None:
+        std[need] = sub_std
     return out, len(need), dropped

@@ -14,7 +14,11 @@ import heapq
 import numpy as np
 
 STAT_FIELDS = ("n", "sum", "sumsq", "min", "max", "med_lo", "med_hi", "q23_sum", "q23_cnt")
-ROW_WIDTH = len(STAT_FIELDS) + 1      # + original region index
+# + numpy's std near a rounding tie (float64 bits, NaN: none; engine.numpy_std)
+# + original region index.  unpack_rows also takes tables without the std
+# column (the bench's device rows).
+ROW_WIDTH = len(STAT_FIELDS) + 2
+_NAN_BITS = np.array([np.nan]).view(np.int64)[0]
 
 
 def lpt_shard(costs, world):
@@ -48,28 +52,47 @@ def select_reads(tid, owned):
     return mask, remap
 
 
-def pack_rows(rows, index):
-    """structured stat rows + original region index -> int64 [R, ROW_WIDTH]."""
+def pack_rows(rows, index, std=None):
+    """structured stat rows (+ numpy std per row, NaN / None: none) +
+    original region index -> int64 [R, ROW_WIDTH]."""
     out = np.empty((len(rows), ROW_WIDTH), dtype=np.int64)
     for k, f in enumerate(STAT_FIELDS):
         out[:, k] = rows[f].astype(np.int64) if f != "sumsq" else rows[f].view(np.int64)
+    if std is None:
+        out[:, -2] = _NAN_BITS
+    else:
+        out[:, -2] = np.ascontiguousarray(std, np.float64).view(np.int64)
     out[:, -1] = index
     return out
+
+
+def _live(table, n_regions):
+    table = np.asarray(table)
+    table = table[table[:, -1] >= 0]
+    idx = table[:, -1]
+    if len(np.unique(idx)) != len(idx) or len(idx) != n_regions:
+        raise RuntimeError("region table gather lost or duplicated rows (%d of %d)"
+                           % (len(idx), n_regions))
+    return table, idx
 
 
 def unpack_rows(table, n_regions, dtype):
     """int64 [*, ROW_WIDTH] (rows with index < 0 are padding) -> structured
     rows in original region order."""
-    table = np.asarray(table)
-    table = table[table[:, -1] >= 0]
+    table, idx = _live(table, n_regions)
     out = np.zeros(n_regions, dtype=dtype)
-    idx = table[:, -1]
-    if len(np.unique(idx)) != len(idx) or len(idx) != n_regions:
-        raise RuntimeError("region table gather lost or duplicated rows (%d of %d)"
-                           % (len(idx), n_regions))
     for k, f in enumerate(STAT_FIELDS):
         col = table[:, k]
         out[f][idx] = col.view(np.uint64) if f == "sumsq" else col
+    return out
+
+
+def unpack_std(table, n_regions):
+    """The numpy-std column of a packed table in original region order
+    (float64, NaN where none)."""
+    table, idx = _live(table, n_regions)
+    out = np.full(n_regions, np.nan)
+    out[idx] = np.ascontiguousarray(table[:, -2]).view(np.float64)
     return out
 
 

@@ -33,7 +33,48 @@ def _np_round2(x):
     return float(np.round(np.float64(x), 2))
 
 
-def classic_stats(row):
+STD_TIE_REL = 1e-9   # |100 std - (k + 1/2)| below this (relative): numpy's own value decides
+
+
+def std_near_tie(rows, rel=None):
+    """bool mask of the rows whose round(np.std, 2) could differ from the
+    rounding of the exact standard deviation: 100 * std within `rel`
+    (relative) of a k + 1/2 boundary.  numpy's float64 std is within a few
+    ulps times log2(n) of the exact value (~1e-14 relative), so outside this
+    window both round alike; inside it, numpy_std() computes numpy's value.
+    rel None: STD_TIE_REL (read at call time)."""
+    rel = STD_TIE_REL if rel is None else rel
+    out = np.zeros(len(rows), bool)
+    for i, r in enumerate(rows):
+        n = int(r["n"])
+        if n <= 0:
+            continue
+        s = int(r["sum"])
+        num = n * int(r["sumsq"]) - s * s
+        if num <= 0:
+            continue
+        x = 100.0 * math.sqrt(num / (n * n))
+        out[i] = abs(x - math.floor(x) - 0.5) <= rel * max(x, 1.0)
+    return out
+
+
+def numpy_std(eng, rows, tids, starts, ends, rel=None):
+    """float64 per row: np.std(columns) bit for bit (pileup.py:22) for the
+    rows near a rounding tie (std_near_tie), NaN elsewhere.  `eng` holds the
+    depth vector the rows came from; tids are its contig ids.  numpy's
+    summation order runs on the device (mc_region_np_sqdev)."""
+    out = np.full(len(rows), np.nan)
+    need = np.nonzero(std_near_tie(rows, rel))[0]
+    if len(need) == 0:
+        return out
+    n = rows["n"][need].astype(np.float64)
+    means = rows["sum"][need].astype(np.float64) / n          # np.mean (exact sum, one division)
+    t = eng.np_sqdev(np.asarray(tids)[need], np.asarray(starts)[need], np.asarray(ends)[need], means)
+    out[need] = np.sqrt(t / n)                                # ret / rcount, then sqrt
+    return out
+
+
+def classic_stats(row, np_std=None):
     """dict(min, max, med, std, avg, q23, sum) from one exact stat row.
 
     Mirrors metacov/pileup.py:18-26 on the float64 column vector:
@@ -42,7 +83,9 @@ def classic_stats(row):
       avg          round(np.mean, 2): float64(sum)/n is what np.mean returns
                    for integer-valued float64 data (its pairwise sum is exact)
       q23          round(np.mean(sorted(c)[n//4 : n-n//4]), 2), likewise exact
-      std          round(np.std, 2) (ddof=0), from the exact variance
+      std          round(np.std, 2) (ddof=0): numpy's own float64 value when
+                   given (`np_std`, from numpy_std() for rows near a rounding
+                   tie), else from the exact variance
     Raises ValueError for an empty region as classic does (zero-size
     reduction in np.amin).
     """
@@ -51,8 +94,11 @@ def classic_stats(row):
         raise ValueError("zero-size array to reduction operation minimum which has no identity")
     s = int(row["sum"])
     sq = int(row["sumsq"])
-    var = Fraction(n * sq - s * s, n * n)
-    std = math.sqrt(float(var)) if var > 0 else 0.0
+    if np_std is not None and not math.isnan(np_std):
+        std = float(np_std)
+    else:
+        var = Fraction(n * sq - s * s, n * n)
+        std = math.sqrt(float(var)) if var > 0 else 0.0
     avg = float(np.float64(s) / np.float64(n))
     q23 = float(np.float64(int(row["q23_sum"])) / np.float64(int(row["q23_cnt"])))
     med = (int(row["med_lo"]) + int(row["med_hi"])) // 2
@@ -229,6 +275,18 @@ class CoverageEngine:
         ends = np.ascontiguousarray(ends, dtype=np.int64)
         self._check(self._lib.mc_region_stats_device(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
                                                ctypes.c_void_p(d_out_ptr)))
+
+    def np_sqdev(self, tids, starts, ends, means):
+        """numpy's float64 sum of squared deviations from `means` of each
+        region's column vector, in numpy's summation order (float64 array)."""
+        tids = np.ascontiguousarray(tids, dtype=np.int32)
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        means = np.ascontiguousarray(means, dtype=np.float64)
+        out = np.zeros(len(tids), dtype=np.float64)
+        self._check(self._lib.mc_region_np_sqdev(self._h, len(tids), ptr(tids), ptr(starts), ptr(ends),
+                                                 ptr(means), ptr(out)))
+        return out
 
     def compute_depth_stats(self, tids, starts, ends):
         """K2 with the region statistics fused in (non-overlapping regions),

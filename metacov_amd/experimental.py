@@ -75,43 +75,65 @@ def load_kmerhist(f, k_len=7):
 
 def check_faidx(path):
     """Raises OSError where pysam.FastaFile(path) fails to open a reference
-    (metacov/cli.py:59 opens one for every `pileup -f`): htslib's faidx needs
+    (metacov/cli.py:59 opens one for every `pileup -f`).  With an existing
+    `<path>.fai` (and `.gzi` for BGZF) htslib's fai_load takes the index as
+    it is, so nothing is checked.  Otherwise it builds one, and faidx needs
     plain text or BGZF (not plain gzip: "Cannot index files compressed with
     gzip, please use bgzip"), '>' headers, and within a sequence every line
-    but the last of one length ("Different line length in sequence")."""
+    but the last of one length ("Different line length in sequence").  The
+    lines are checked as numpy arrays of their bounds, not one by one."""
     def fail(why):
         raise OSError("error when opening file `%s`: %s" % (path, why))
     with open(path, "rb") as fh:
         head = fh.read(18)
-    if head[:2] == b"\x1f\x8b":
+    gz = head[:2] == b"\x1f\x8b"
+    if gz:
         bgzf = len(head) >= 16 and head[3] & 4 and head[12:14] == b"BC"
         if not bgzf:
             fail("Cannot index files compressed with gzip, please use bgzip")
+    if os.path.exists(path + ".fai") and (not gz or os.path.exists(path + ".gzi")):
+        return
+    if gz:
         with gzip.open(path, "rb") as fh:
             data = fh.read()
     else:
         with open(path, "rb") as fh:
             data = fh.read()
-    name, width, short = None, None, False
-    for no, line in enumerate(data.split(b"\n"), 1):
-        line = line.rstrip(b"\r")
-        if line.startswith(b">"):
-            name, width, short = line[1:].split()[0].decode() if line[1:].split() else "", None, False
-            continue
-        if not line:
-            if name is not None:
-                short = short or width is not None
-            continue
-        if name is None:
-            fail("Format error, unexpected \"%s\" at line %d" % (chr(line[0]), no))
-        if short:
-            fail("Different line length in sequence '%s'" % name)
-        if width is None:
-            width = len(line)
-        elif len(line) > width:
-            fail("Different line length in sequence '%s'" % name)
-        elif len(line) < width:
-            short = True
+    buf = np.frombuffer(data, np.uint8)
+    nl = np.flatnonzero(buf == 10)
+    starts = np.concatenate([[0], nl + 1])
+    ends = np.concatenate([nl, [len(buf)]])
+    lens = ends - starts
+    cr = np.zeros(len(lens), bool)
+    has = lens > 0
+    cr[has] = buf[ends[has] - 1] == 13
+    lens = lens - cr
+    nonempty = lens > 0
+    first = np.zeros(len(lens), np.uint8)
+    first[nonempty] = buf[starts[nonempty]]
+    is_head = nonempty & (first == ord(">"))
+    grp = np.cumsum(is_head)
+    seq = np.flatnonzero(nonempty & ~is_head)
+    bad = []                                   # (line index, message)
+    orphan = seq[grp[seq] == 0]
+    if len(orphan):
+        i = int(orphan[0])
+        bad.append((i, "Format error, unexpected \"%s\" at line %d" % (chr(first[i]), i + 1)))
+    seq = seq[grp[seq] > 0]
+    if len(seq) > 1:
+        g = grp[seq]
+        new_grp = np.concatenate([[True], g[1:] != g[:-1]])
+        w1 = lens[seq[new_grp]][np.cumsum(new_grp) - 1]      # each group's first line width
+        cont = ~new_grp[1:]                                   # line k+1 continues line k's sequence
+        prev, cur = seq[:-1], seq[1:]
+        broken = cont & ((cur - prev > 1) | (lens[prev] < w1[1:]) | (lens[cur] > w1[1:]))
+        if broken.any():
+            i = int(cur[np.flatnonzero(broken)[0]])
+            h = int(np.flatnonzero(is_head[:i])[-1])
+            words = data[starts[h] + 1:ends[h] - cr[h]].split()
+            bad.append((i, "Different line length in sequence '%s'" % (words[0].decode() if words else "")))
+    if bad:
+        fail(min(bad)[1])
 
 
 class FastaFile:

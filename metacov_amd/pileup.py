@@ -28,7 +28,7 @@ import numpy as np
 
 from . import depthcap
 from .bam import BamFile, GpuBamFile
-from .engine import classic_stats
+from .engine import classic_stats, numpy_std
 from .experimental import experimental, load_kmerhist  # noqa: F401  (pileup.py:29-173)
 
 HTSLIB_MAX_DEPTH = depthcap.HTSLIB_MAX_DEPTH
@@ -52,6 +52,7 @@ def _as_bamfile(bam, legacy_endpos=False, device=0):
     f = _open_files.pop(key, None)
     if f is None:
         f = GpuBamFile(path, device=device, legacy_endpos=legacy_endpos)
+        f.trim()                           # kept between calls: only its results stay in HBM
     _open_files[key] = f                   # most recently used last
     while len(_open_files) > _OPEN_MAX:
         _open_files.popitem(last=False)[1].close()
@@ -99,11 +100,14 @@ def classic_batch(bam, regions, device=0, max_depth=HTSLIB_MAX_DEPTH, legacy_end
         if s < 0:
             raise ValueError("region start %d < 0" % s)
         starts[i], ends[i] = s, e
-    rows = bf.engine(device).region_stats(bf.local_tid(tids), starts, ends)
+    eng = bf.engine(device)
+    local = bf.local_tid(tids)
+    rows = eng.region_stats(local, starts, ends)
+    std = numpy_std(eng, rows, local, starts, ends)   # numpy's own std near rounding ties
     if max_depth:
         rows, _, _ = depthcap.apply_cap(bf, rows, tids, starts, ends, bf.lengths, int(max_depth),
-                                        device)
-    return [classic_stats(r) for r in rows]
+                                        device, std=std)
+    return [classic_stats(r, s) for r, s in zip(rows, std)]
 
 
 def depth(bam, ref, start=0, end=None, device=0):

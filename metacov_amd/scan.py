@@ -358,7 +358,9 @@ def scan_reads(infile, fasta, counters, progress_interval=10000000, progress_cb=
     BaseHist / MirrorHist.  progress_cb is called once per progress_interval
     reads, after the GPU pass.  decode: "gpu" (default; MC_SCAN_DECODE
     overrides) inflates and walks a BAM on the GPU, "host" with the C++
-    source (SAM and FASTQ always take the host source)."""
+    source (SAM and FASTQ always take the host source).  With maxreads the
+    host source streams and stops there; a GPU decode that does not fit in
+    device memory falls back to it."""
     decode = decode or os.environ.get("MC_SCAN_DECODE", "gpu")
     if decode not in ("gpu", "host"):
         raise ValueError("decode must be 'gpu' or 'host'")
@@ -410,6 +412,25 @@ def _target_names(lib, src, kind):
 
 
 def _run_layer(lib, infile, fa, flags, per_group, maxreads, device, n_threads, batch_reads, decode="host"):
+    if maxreads:
+        # the GPU decode inflates and walks the whole file into HBM before
+        # the first batch; the host source streams and stops at maxreads
+        decode = "host"
+    try:
+        return _run_layer_on(lib, infile, fa, flags, per_group, maxreads, device, n_threads, batch_reads,
+                             decode)
+    except _lib.MetacovError as e:
+        # a BAM whose whole-file SoA batch does not fit in HBM (allocation
+        # failure or a batch past the engine's range): the streaming host
+        # source, in bounded windows, feeds the same GPU histograms
+        if decode != "gpu" or e.code not in (_lib.MC_E_HIP, _lib.MC_E_RANGE):
+            raise
+        log.warning("GPU BAM decode for scan failed (%s); reading on the host instead", e)
+        return _run_layer_on(lib, infile, fa, flags, per_group, maxreads, device, n_threads, batch_reads,
+                             "host")
+
+
+def _run_layer_on(lib, infile, fa, flags, per_group, maxreads, device, n_threads, batch_reads, decode):
     src, kind = _source(lib, infile, n_threads, decode, device)
     scan = ctypes.c_void_p()
     try:

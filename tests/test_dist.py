@@ -47,6 +47,14 @@ def test_pack_unpack_roundtrip():
         assert np.array_equal(back[f][idx], rows[f])
     with pytest.raises(RuntimeError):
         mdist.unpack_rows(t[:5], 7, REGION_STAT_DTYPE)
+    assert np.isnan(mdist.unpack_std(t, 7)).all()
+    # numpy's std column (engine.numpy_std) travels with its row
+    std = np.array([np.nan, 0.285, np.nan, 1e-300, 3.0, np.nan, 0.2849999999999999])
+    t = mdist.pack_rows(rows, idx, std)
+    got = mdist.unpack_std(np.concatenate([pad, t]), 7)
+    assert np.array_equal(got[idx], std, equal_nan=True)
+    # the bench's tables carry no std column
+    assert np.array_equal(mdist.unpack_rows(np.delete(t, -2, axis=1), 7, REGION_STAT_DTYPE), back)
 
 
 def _free_port():

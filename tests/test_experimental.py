@@ -597,6 +597,61 @@ def test_check_faidx_follows_pysam_open(tmp_path):
         f.write_text(bad)
         with pytest.raises(OSError):
             mx.check_faidx(str(f))
+    # an existing index is taken as it is (htslib fai_load), whatever the lines
+    (tmp_path / "bad.fa.fai").write_text("a\t6\t3\t4\t5\n")
+    mx.check_faidx(str(tmp_path / "bad.fa"))
+
+
+def _faidx_lines(data):
+    """The per-line form of faidx's build checks (the first failing line's
+    message, or None), against which check_faidx's array form is fuzzed."""
+    name, width, short = None, None, False
+    for no, line in enumerate(data.split(b"\n"), 1):
+        line = line.rstrip(b"\r")
+        if line.startswith(b">"):
+            name, width, short = line[1:].split()[0].decode() if line[1:].split() else "", None, False
+            continue
+        if not line:
+            if name is not None:
+                short = short or width is not None
+            continue
+        if name is None:
+            return "Format error, unexpected \"%s\" at line %d" % (chr(line[0]), no)
+        if short or (width is not None and len(line) > width):
+            return "Different line length in sequence '%s'" % name
+        if width is None:
+            width = len(line)
+        elif len(line) < width:
+            short = True
+    return None
+
+
+def test_check_faidx_fuzz(tmp_path):
+    rng = np.random.default_rng(4)
+    f = tmp_path / "r.fa"
+    kinds = 0
+    for it in range(400):
+        parts = []
+        if rng.random() < 0.1:
+            parts.append(b"AC")
+        for s in range(int(rng.integers(0, 4))):
+            parts.append(b">s%d x" % s if rng.random() < 0.9 else b">")
+            w = int(rng.integers(1, 9))
+            for k in range(int(rng.integers(0, 5))):
+                r = rng.random()
+                ln = w if r < 0.7 else int(rng.integers(0, 2 * w + 1))
+                parts.append(b"A" * ln + (b"\r" if rng.random() < 0.1 else b""))
+        data = b"\n".join(parts) + (b"\n" if rng.random() < 0.7 else b"")
+        f.write_bytes(data)
+        want = _faidx_lines(data)
+        if want is None:
+            mx.check_faidx(str(f))
+        else:
+            kinds += 1
+            with pytest.raises(OSError) as e:
+                mx.check_faidx(str(f))
+            assert str(e.value).endswith(want), (data, want, str(e.value))
+    assert 50 < kinds < 350
 
 
 def test_cli_rejects_unopenable_fasta_without_k(lib_built, golden_dir, tmp_path):

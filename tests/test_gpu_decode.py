@@ -228,6 +228,18 @@ def test_gpu_decode_large(lib_built, tmp_path, level, window):
     # false syncs are rare and each is fixed once (a stale-walk cascade once
     # made every later segment a "resync" and fell back to a one-lane walk)
     assert t["resyncs"] <= 64, t["resyncs"]
+    # trim() drops the decode's staging (compressed file, inflated
+    # stream, tables); intervals, extents, the engine and restrict still work
+    ext = g.extents()
+    freed = g.trim()
+    assert freed >= t["inflated_bytes"] if not window else freed > window
+    assert g.trim() == 0
+    _assert_same(h, g)
+    assert np.array_equal(g.extents()[0], ext[0])
+    tid, pos, span = g.intervals([2])
+    assert np.array_equal(pos, h.pos[h.tid == 2])
+    g.restrict([0, 2])
+    assert g.n_kept == int(np.sum(h.tid != 1))
     g.close()
 
 

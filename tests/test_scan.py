@@ -762,3 +762,40 @@ def test_scan_gpu_decode_equals_host_source_gpu(mix, golden_dir, lib_built, tmp_
             outs.append((n, rows))
         assert outs[0][0] == outs[1][0] and outs[0][0] > 0, path
         assert outs[0][1] == outs[1][1], path
+
+
+@pytest.mark.gpu
+def test_scan_gpu_decode_bounded(mix, lib_built, monkeypatch):
+    """`scan --max-reads N` streams from the host source (the
+    GPU decode would inflate the whole file first), and a GPU decode that
+    runs out of device memory falls back to the host source; the tables are
+    the host source's either way."""
+    from metacov_amd import _lib
+    from metacov_amd import scan as mscan
+    bam, fa = mix
+
+    def tables(**kw):
+        c = mscan.ByFlag([mscan.BaseHist(2), mscan.KmerHist(5, 6, 4, 1), mscan.IsizeHist()], [])
+        n = mscan.scan_reads(bam, fa, c, **kw)
+        return n, [[list(map(str, r)) for r in q.get_rows()] for g in c.processors for q in g.processors]
+
+    seen = []
+    real = mscan._run_layer_on
+
+    def spy(lib, infile, fa_, flags, per_group, maxreads, device, n_threads, batch_reads, decode):
+        seen.append(decode)
+        return real(lib, infile, fa_, flags, per_group, maxreads, device, n_threads, batch_reads, decode)
+    monkeypatch.setattr(mscan, "_run_layer_on", spy)
+    assert tables(maxreads=57, decode="gpu") == tables(maxreads=57, decode="host")
+    assert seen == ["host", "host"]
+    want = tables(decode="host")
+    seen.clear()
+
+    def oom(lib, infile, fa_, flags, per_group, maxreads, device, n_threads, batch_reads, decode):
+        seen.append(decode)
+        if decode == "gpu":
+            raise _lib.MetacovError(_lib.MC_E_HIP, "hipMalloc failed: out of memory")
+        return real(lib, infile, fa_, flags, per_group, maxreads, device, n_threads, batch_reads, decode)
+    monkeypatch.setattr(mscan, "_run_layer_on", oom)
+    assert tables(decode="gpu") == want
+    assert seen == ["gpu", "host"]

@@ -15,9 +15,10 @@ this file checks:
   * med: (med_lo + med_hi) // 2 is int(np.median) for non-negative data.
 With a non-integer mean np.std's value depends on its summation order (its
 rounding errors are position-dependent), so a vector whose exact std lies
-within ~1e-13 of a .xx5 boundary is decided by float noise in the
-reference itself: those are covered by the random vectors only (parity
-unpinned at such ties).
+within ~1e-13 of a .xx5 boundary can round the other way in numpy.  Those
+rows are flagged (engine.std_near_tie) and given numpy's own value,
+computed on the device in numpy's order: tests/test_npstd.py pins them
+against the real classic() on constructed ties (tests/golden/std_ties.json).
 """
 import numpy as np
 import pytest
