@@ -42,6 +42,8 @@ from . import scan as _scan
 from .bam import BamFile, GpuBamFile, StreamedBam, index_stats
 from .engine import REGION_STAT_DTYPE, classic_stats, numpy_std
 
+_T_IMPORTED = time.time()    # (MC_CLI_TIMES: the end of the module imports)
+
 logging.basicConfig(level=logging.INFO,
                     format="[%(relativeCreated)6.1f %(funcName)s]  %(message)s",
                     datefmt="%I:%M:%S")
@@ -102,6 +104,7 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return pileup_distributed(bamfile.name, regionfile_blast7, regionfile_csv, outfile, exp,
                                   max_depth=max_depth, legacy_endpos=legacy_endpos, decode=decode)
+    times = _PhaseTimes.start(device)
     if decode == 'gpu':
         bam = GpuBamFile(bamfile.name, device=device, window_bytes=window_bytes,
                          legacy_endpos=legacy_endpos)
@@ -110,9 +113,74 @@ def pileup(bamfile, reference_fasta, regionfile_blast7, regionfile_csv,
                           legacy_endpos=legacy_endpos)
     else:
         bam = BamFile(bamfile.name, legacy_endpos=legacy_endpos)
+    times.mark("decode")
     regions = _regions.make_region_iterator(regionfile_blast7, regionfile_csv, bam)
     log_counts(bam)
-    write_rows(bam, regions, outfile, device=device, exp=exp, max_depth=max_depth)
+    write_rows(bam, regions, outfile, device=device, exp=exp, max_depth=max_depth, times=times)
+    times.finish(outfile, bam)
+
+
+class _PhaseTimes:
+    """MC_CLI_TIMES=<path>: the single-process `pileup`'s wall-clock phases as
+    JSON (scripts/cold_cli.py): process start (MC_CLI_T0, the launcher's
+    clock, else the OS's process start) to the end of the imports, HIP
+    runtime and device init (one ctx created and destroyed up front, so the
+    decode phase holds the decode alone), decode, rows (depth, statistics,
+    cap), write.  Without the variable every call is a no-op."""
+
+    def __init__(self, path):
+        self.path = path
+        self.t = {}
+        self.last = time.time()
+
+    @classmethod
+    def start(cls, device=0):
+        path = os.environ.get("MC_CLI_TIMES")
+        if not path:
+            return _NoTimes()
+        t0 = os.environ.get("MC_CLI_T0")
+        if t0:
+            t0 = float(t0)
+        else:
+            import psutil
+            t0 = psutil.Process().create_time()
+        self = cls(path)
+        self.t["interpreter_and_imports_s"] = _T_IMPORTED - t0
+        self.t["cli_parse_s"] = time.time() - _T_IMPORTED
+        self.t0 = t0
+        self.last = time.time()
+        from . import _lib as L
+        import ctypes
+        lib = L.load()
+        self.mark("library_load")
+        h = ctypes.c_void_p()
+        L.check(lib.mc_ctx_create(int(device), ctypes.byref(h)), lib)
+        lib.mc_ctx_destroy(h)
+        self.mark("hip_init")
+        return self
+
+    def mark(self, name):
+        now = time.time()
+        self.t[name + "_s"] = now - self.last
+        self.last = now
+
+    def finish(self, outfile, bam):
+        outfile.flush()
+        self.mark("write")
+        self.t["total_s"] = time.time() - self.t0
+        tm = getattr(bam, "timings", None)
+        if tm is not None:
+            self.t["decode_timings"] = {k: round(v, 3) if isinstance(v, float) else v for k, v in tm().items()}
+        with open(self.path, "w") as fh:
+            json.dump(self.t, fh, indent=1)
+
+
+class _NoTimes:
+    def mark(self, name):
+        pass
+
+    def finish(self, outfile, bam):
+        pass
 
 
 def log_counts(bam):
@@ -221,13 +289,18 @@ def write_csv(regions, rows, outfile, extra=None, std=None):
         writer.writerow(result)
 
 
-def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=_depthcap.HTSLIB_MAX_DEPTH):
+def write_rows(bam, regions, outfile, device=0, exp=None, max_depth=_depthcap.HTSLIB_MAX_DEPTH, times=None):
     """Resolves names like cli.py:80-91, reduces the regions in one GPU call,
     then writes rows in input order exactly as cli.py:97-108 does; the rows
     before a failing region are written before its error is raised."""
+    times = times or _NoTimes()
     hits, tids, starts, ends, err = resolve_regions(bam, regions)
+    times.mark("regions")
     rows, std = compute_rows(bam, tids, starts, ends, device, max_depth)
+    times.mark("rows")
     extra = experimental_results(bam.filename, exp, bam.references, tids, starts, ends, device)
+    if exp is not None:
+        times.mark("experimental")
     write_csv(hits, rows, outfile, extra, std)
     if err is not None:
         raise err
