@@ -260,6 +260,28 @@ int mc_synchronize(mc_ctx* ctx);
 int mc_depth_cap_mask(int64_t n, const int32_t* tid, const int32_t* pos, const int32_t* span,
                       int32_t max_depth, int n_threads, uint8_t* keep, int64_t* n_dropped);
 
+/* The same mask on the device (csrc/capmask.h: one wave per query walks its
+ * start groups in order; a chunk of 64 reads that cannot reach the cap is
+ * applied in bulk).  d_*: device arrays; each distinct tid is one query.
+ * MC_E_INVALID for unsorted reads, MC_E_RANGE for a span >= 32704 (the
+ * wave's LDS ring of read ends; mc_depth_cap_mask takes those). */
+int mc_depth_cap_mask_device(int device, int64_t n, const int32_t* d_tid, const int32_t* d_pos,
+                             const int32_t* d_span, int32_t max_depth, uint8_t* d_keep,
+                             int64_t* n_dropped);
+
+/* The capped recompute's batch, built on the device (metacov_amd.depthcap):
+ * from coordinate-sorted device intervals (e.g. mc_bam_gpu_intervals_device),
+ * region r's query — the reads of contig qtid[r] overlapping [qstart[r],
+ * qend[r]) by bam_endpos, what pysam's pileup(ref, start, end) hands htslib
+ * (pileup.py:13) — with the cap applied, becomes contig r of the ctx's
+ * batch.  The ctx must hold R contigs (mc_set_contigs: the regions' contig
+ * lengths) and no reads.  Dropped reads (and reads of the gathered range
+ * outside the query) stay in the batch with span 0, so they add no depth.
+ * n_dropped: reads the cap dropped.  MC_E_RANGE for a span >= 32704. */
+int mc_add_reads_capped(mc_ctx* ctx, int64_t n, const int32_t* d_tid, const int32_t* d_pos,
+                        const int32_t* d_span, int64_t R, const int32_t* qtid, const int64_t* qstart,
+                        const int64_t* qend, int32_t max_depth, int64_t* n_dropped);
+
 /* ---- host BAM decoder (C++, multi-threaded BGZF inflate) ----------------
  * Replaces the pysam/htslib read path the reference uses: AlignmentFile
  * header (bam.references / bam.lengths, cli.py:80, util.py:64-69),

@@ -116,6 +116,8 @@ SIGNATURES = {
     "mc_get_timings": [_P, ctypes.POINTER(Timings)],
     "mc_synchronize": [_P],
     "mc_depth_cap_mask": [_I64, _P, _P, _P, _I32, ctypes.c_int, _P, _PI64],
+    "mc_depth_cap_mask_device": [ctypes.c_int, _I64, _P, _P, _P, _I32, _P, _PI64],
+    "mc_add_reads_capped": [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, _I32, _PI64],
     "mc_bam_open": [ctypes.c_char_p, ctypes.c_int, _U32, ctypes.c_int, _PP],
     "mc_bam_close": [_P],
     "mc_bam_n_targets": [_P, _PI32],

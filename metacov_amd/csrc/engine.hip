@@ -19,6 +19,9 @@
 #include "common.h"
 #include "kernels.h"
 #include "npstd.h"
+#include "capmask.h"
+
+#include <hipcub/hipcub.hpp>
 
 using namespace mc;
 
@@ -1923,6 +1926,166 @@ extern "C" int mc_region_np_sqdev(mc_ctx* ctx, int64_t R, const int32_t* tid, co
     HIP_TRY(hipMemcpyAsync(h + o_out, d + o_out, R * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::memcpy(out, h + o_out, R * 8);
+    return MC_OK;
+}
+
+// ---- htslib's max_depth cap on the device (csrc/capmask.h) ----------------
+
+static int cap_max_span(hipStream_t s, const int32_t* span, int64_t n, int* d_tmp, int* out) {
+    HIP_TRY(hipMemsetAsync(d_tmp, 0, 4, s));
+    if (n) {
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 255) / 256));
+        hipLaunchKernelGGL(cap_max_span_kernel, dim3(g), dim3(256), 0, s, span, n, d_tmp);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(out, d_tmp, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MC_OK;
+}
+
+static int cap_walk(hipStream_t s, const int32_t* pos, int32_t* span, const uint8_t* inq, const int64_t* d_seg,
+                    int64_t n_seg, int max_depth, int max_span, uint8_t* keep, int zero,
+                    unsigned long long* d_dropped) {
+    static bool attr = false;
+    if (!attr) {
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(cap_walk_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kCapRing * 4));
+        attr = true;
+    }
+    if (n_seg <= 0) return MC_OK;
+    hipLaunchKernelGGL(cap_walk_kernel, dim3((unsigned)n_seg), dim3(64), (size_t)kCapRing * 4, s, pos, span, inq,
+                       d_seg, max_depth, max_span, keep, zero, d_dropped);
+    HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_depth_cap_mask_device(int device, int64_t n, const int32_t* d_tid, const int32_t* d_pos,
+                                        const int32_t* d_span, int32_t max_depth, uint8_t* d_keep,
+                                        int64_t* n_dropped) {
+    MC_REQUIRE(n >= 0 && (n == 0 || (d_tid && d_pos && d_span && d_keep)), MC_E_INVALID, "bad read arrays");
+    MC_REQUIRE(max_depth >= 1, MC_E_INVALID, "max_depth must be >= 1 (got %d)", max_depth);
+    HIP_TRY(hipSetDevice(device));
+    if (n_dropped) *n_dropped = 0;
+    if (n == 0) return MC_OK;
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    struct StreamGuard {
+        hipStream_t s;
+        ~StreamGuard() {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    } sg{s};
+    DevBuf<uint8_t> flags;
+    DevBuf<int64_t> segs;
+    DevBuf<unsigned long long> cnt;   // [0] dropped, [1] bad (as unsigned), [2] segments, [3] max span
+    DevBuf<unsigned char> temp;
+    HIP_TRY(flags.reserve((size_t)n));
+    HIP_TRY(segs.reserve((size_t)n + 1));
+    HIP_TRY(cnt.reserve(4));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 32, s));
+    unsigned* d_bad = reinterpret_cast<unsigned*>(cnt.p + 1);
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+    hipLaunchKernelGGL(cap_seg_flags_kernel, dim3(g), dim3(256), 0, s, d_tid, d_pos, n, flags.p, d_bad);
+    HIP_TRY(hipGetLastError());
+    hipcub::CountingInputIterator<int64_t> idx(0);
+    int64_t* d_nsel = reinterpret_cast<int64_t*>(cnt.p + 2);
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, idx, flags.p, segs.p, d_nsel, (int)n, s));
+    HIP_TRY(temp.reserve(std::max<size_t>(tb, 1)));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(temp.p, tb, idx, flags.p, segs.p, d_nsel, (int)n, s));
+    unsigned long long h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(h, cnt.p, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    MC_REQUIRE((unsigned)h[1] == 0, MC_E_INVALID, "reads are not coordinate-sorted");
+    const int64_t n_seg = (int64_t)h[2];
+    HIP_TRY(hipMemcpyAsync(segs.p + n_seg, &n, 8, hipMemcpyHostToDevice, s));
+    int max_span = 0;
+    if (int rc = cap_max_span(s, d_span, n, reinterpret_cast<int*>(cnt.p + 3), &max_span)) return rc;
+    MC_REQUIRE(max_span < kCapRing - 64, MC_E_RANGE,
+               "a span of %d is beyond the device cap's ring (%d); use mc_depth_cap_mask", max_span, kCapRing - 64);
+    if (int rc = cap_walk(s, d_pos, const_cast<int32_t*>(d_span), nullptr, segs.p, n_seg, max_depth, max_span,
+                          d_keep, 0, cnt.p))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(h, cnt.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (n_dropped) *n_dropped = (int64_t)h[0];
+    return MC_OK;
+}
+
+extern "C" int mc_add_reads_capped(mc_ctx* ctx, int64_t n, const int32_t* d_tid, const int32_t* d_pos,
+                                   const int32_t* d_span, int64_t R, const int32_t* qtid, const int64_t* qstart,
+                                   const int64_t* qend, int32_t max_depth, int64_t* n_dropped) {
+    if (int rc = ctx_use(ctx)) return rc;
+    MC_REQUIRE(n >= 0 && (n == 0 || (d_tid && d_pos && d_span)), MC_E_INVALID, "bad read arrays");
+    MC_REQUIRE(R >= 0 && (R == 0 || (qtid && qstart && qend)), MC_E_INVALID, "bad region arrays");
+    MC_REQUIRE(max_depth >= 1, MC_E_INVALID, "max_depth must be >= 1 (got %d)", max_depth);
+    MC_REQUIRE((int64_t)ctx->len.size() == R, MC_E_STATE, "the ctx needs one contig per region (%lld, has %zu)",
+               (long long)R, ctx->len.size());
+    MC_REQUIRE(ctx->n_reads == 0 && !ctx->spans_pending, MC_E_STATE, "mc_add_reads_capped needs an empty batch");
+    MC_REQUIRE(R < (int64_t(1) << 16), MC_E_RANGE, "at most 65535 regions per capped batch");
+    for (int64_t r = 0; r < R; ++r)
+        MC_REQUIRE(qstart[r] >= 0 && qend[r] >= qstart[r] && qend[r] < (int64_t(1) << 31), MC_E_INVALID,
+                   "region %lld: bad range", (long long)r);
+    if (n_dropped) *n_dropped = 0;
+    if (R == 0) return MC_OK;
+    hipStream_t s = ctx->stream;
+    // staged queries: qt (int32), qs, qe, lo, hi, off (int64 each; off has R + 1)
+    const size_t o_qt = 0, o_qs = stage_align(R * 4), o_qe = o_qs + stage_align(R * 8),
+                 o_lo = o_qe + stage_align(R * 8), o_hi = o_lo + stage_align(R * 8),
+                 o_off = o_hi + stage_align(R * 8), o_cnt = o_off + stage_align((R + 1) * 8),
+                 total = o_cnt + 64;
+    HIP_TRY(ctx->k3_stage.reserve(total));
+    unsigned char* h = ctx->k3_stage.host();
+    unsigned char* d = ctx->k3_stage.d.p;
+    std::memcpy(h + o_qt, qtid, R * 4);
+    std::memcpy(h + o_qs, qstart, R * 8);
+    std::memcpy(h + o_qe, qend, R * 8);
+    HIP_TRY(hipMemcpyAsync(d, h, o_lo, hipMemcpyHostToDevice, s));
+    int* d_ms = reinterpret_cast<int*>(d + o_cnt);
+    unsigned long long* d_dropped = reinterpret_cast<unsigned long long*>(d + o_cnt + 8);
+    int max_span = 0;
+    if (int rc = cap_max_span(s, d_span, n, d_ms, &max_span)) return rc;
+    MC_REQUIRE(max_span < kCapRing - 64, MC_E_RANGE,
+               "a span of %d is beyond the device cap's ring (%d)", max_span, kCapRing - 64);
+    int64_t* d_lo = reinterpret_cast<int64_t*>(d + o_lo);
+    int64_t* d_hi = reinterpret_cast<int64_t*>(d + o_hi);
+    hipLaunchKernelGGL(cap_ranges_kernel, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, s, d_tid, d_pos, n,
+                       reinterpret_cast<const int32_t*>(d + o_qt), reinterpret_cast<const int64_t*>(d + o_qs),
+                       reinterpret_cast<const int64_t*>(d + o_qe), (int)R, max_span, d_lo, d_hi);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h + o_lo, d_lo, o_off - o_lo, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int64_t* lo = reinterpret_cast<const int64_t*>(h + o_lo);
+    const int64_t* hi = reinterpret_cast<const int64_t*>(h + o_hi);
+    int64_t* off = reinterpret_cast<int64_t*>(h + o_off);
+    off[0] = 0;
+    for (int64_t r = 0; r < R; ++r) off[r + 1] = off[r] + std::max<int64_t>(0, hi[r] - lo[r]);
+    const int64_t N = off[R];
+    MC_REQUIRE(N < (int64_t(1) << 31), MC_E_RANGE, "capped batch of %lld reads", (long long)N);
+    HIP_TRY(hipMemcpyAsync(d + o_off, h + o_off, (R + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_dropped, 0, 8, s));
+    if (int rc = reserve_reads(ctx, N, false)) return rc;
+    DevBuf<uint8_t> inq;
+    HIP_TRY(inq.reserve((size_t)std::max<int64_t>(N, 1)));
+    if (N) {
+        const int64_t per = (N + R - 1) / R;
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (per + 255) / 256));
+        hipLaunchKernelGGL(cap_gather_kernel, dim3(gx, (unsigned)R), dim3(256), 0, s, d_pos, d_span, d_lo,
+                           reinterpret_cast<const int64_t*>(d + o_off), reinterpret_cast<const int64_t*>(d + o_qs),
+                           ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, inq.p);
+        HIP_TRY(hipGetLastError());
+        if (int rc = cap_walk(s, ctx->d_pos.p, ctx->d_span.p, inq.p, reinterpret_cast<const int64_t*>(d + o_off), R,
+                              max_depth, max_span, nullptr, 1, d_dropped))
+            return rc;
+    }
+    unsigned long long dropped = 0;
+    HIP_TRY(hipMemcpyAsync(&dropped, d_dropped, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));   // (inq and the staging buffer are reused / freed next)
+    ctx->n_reads = N;
+    ctx->t_cigar = false;
+    invalidate(ctx);
+    if (n_dropped) *n_dropped = (int64_t)dropped;
     return MC_OK;
 }
 

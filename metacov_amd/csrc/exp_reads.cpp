@@ -44,6 +44,7 @@
 
 #include "bgzf.h"
 #include "common.h"
+#include "exp_gpu.h"
 
 using namespace mc::bgzf;
 
@@ -78,6 +79,16 @@ struct mc_reads {
     std::vector<int64_t> first;     // per contig [first[t], first[t+1])
     std::vector<int64_t> max_span;  // per contig max(end - pos)
     std::vector<std::vector<uint64_t>> events;   // per region of the last call: (readno << 32) | kmer
+    // a GPU decode's table stays in HBM (mc_reads_open_gpu*): the read pass
+    // runs on the device (csrc/exp_gpu.hip); the host vectors above are
+    // filled only when mc_reads_fields asks for them
+    mc_bam_gpu* g = nullptr;
+    ExpDevTable dev;
+    bool host_ready = true;
+    double pass_ms = 0;             // the last mc_experimental_reads call
+    ~mc_reads() {
+        if (g) mc_bam_gpu_close(g);
+    }
 };
 
 namespace {
@@ -624,10 +635,10 @@ extern "C" int mc_reads_open(const char* path, int n_threads, int k_len, mc_read
 
 namespace {
 
-// mc_reads_open_gpu's table from a reads-mode GPU decode: the device fields
-// copied back, the names joined, then reads_open's order check and the per
-// contig first record / maximum span.
-int reads_from_gpu(const mc_bam_gpu* g, const char* path, mc_reads* r) {
+// mc_reads_open_gpu's table: the reads-mode GPU decode stays open and its
+// fields in HBM; the order check and the per contig first record / maximum
+// span run on the device (exp_gpu_index).
+int reads_keep_gpu(mc_bam_gpu* g, const char* path, int device, int k, mc_reads* r) {
     const mc_bam* h = nullptr;
     if (int rc = mc_bam_gpu_header(g, &h)) return rc;
     int64_t m = 0, nb = 0;
@@ -640,6 +651,35 @@ int reads_from_gpu(const mc_bam_gpu* g, const char* path, mc_reads* r) {
     r->lens = h->lens;
     r->n_records = h->n_records;
     r->n_unplaced = h->n_records - m;
+    r->dev = ExpDevTable{device, k, m, dt, dp, de, df, db, dk, dnl, dno, dn};
+    const int32_t n_ref = (int32_t)r->names.size();
+    r->first.assign((size_t)n_ref + 1, m);
+    r->max_span.assign((size_t)n_ref, 0);
+    int64_t bad = -1;
+    if (int rc = exp_gpu_index(r->dev, n_ref, r->first.data(), r->max_span.data(), &bad)) return rc;
+    MC_REQUIRE(bad < 0, MC_E_INVALID,
+               "%s is not coordinate-sorted (placed record %lld); experimental() fetches "
+               "regions of a sorted, indexed BAM", path, (long long)bad);
+    r->g = g;
+    r->host_ready = false;
+    (void)nb;
+    return MC_OK;
+}
+
+// the device table's fields copied back (mc_reads_fields on a GPU table)
+int reads_to_host(mc_reads* r) {
+    if (r->host_ready) return MC_OK;
+    const int64_t m = r->dev.n;
+    int64_t nb = 0;
+    {
+        int64_t m2 = 0;
+        const int32_t *dt, *dp, *df;
+        const int64_t *de, *dno;
+        const uint8_t *db, *dnl, *dn;
+        const uint32_t* dk;
+        if (int rc = mc_bam_gpu_reads_device(r->g, &m2, &dt, &dp, &de, &df, &db, &dk, &dnl, &dno, &dn, &nb))
+            return rc;
+    }
     std::vector<int32_t> tid((size_t)m), flag((size_t)m);
     std::vector<int64_t> name_off((size_t)m);
     r->pos.resize((size_t)m);
@@ -650,27 +690,15 @@ int reads_from_gpu(const mc_bam_gpu* g, const char* path, mc_reads* r) {
     r->name_off.resize((size_t)m);
     r->name_len.resize((size_t)m);
     r->arena.resize((size_t)nb);
-    if (int rc = mc_bam_gpu_reads_copy(g, tid.data(), r->pos.data(), r->end.data(), flag.data(), r->bits.data(),
+    if (int rc = mc_bam_gpu_reads_copy(r->g, tid.data(), r->pos.data(), r->end.data(), flag.data(), r->bits.data(),
                                        r->kmer.data(), r->name_len.data(), name_off.data(),
                                        (uint8_t*)r->arena.data()))
         return rc;
-    r->max_span.assign(r->names.size(), 0);
-    int32_t last_tid = -1, last_pos = -1;
     for (int64_t i = 0; i < m; ++i) {
-        const size_t k = (size_t)i;
-        const int32_t t = tid[k], p = r->pos[k];
-        MC_REQUIRE(t > last_tid || (t == last_tid && p >= last_pos), MC_E_INVALID,
-                   "%s is not coordinate-sorted (placed record %lld); experimental() fetches "
-                   "regions of a sorted, indexed BAM", path, (long long)i);
-        last_tid = t;
-        last_pos = p;
-        r->flag[k] = (uint16_t)flag[k];
-        r->name_off[k] = (uint64_t)name_off[k];
-        if (r->first.size() <= (size_t)t) r->first.resize((size_t)t + 1, i);
-        int64_t& ms = r->max_span[(size_t)t];
-        ms = std::max<int64_t>(ms, r->end[k] - p);
+        r->flag[(size_t)i] = (uint16_t)flag[(size_t)i];
+        r->name_off[(size_t)i] = (uint64_t)name_off[(size_t)i];
     }
-    r->first.resize(r->names.size() + 1, m);
+    r->host_ready = true;
     return MC_OK;
 }
 
@@ -687,9 +715,10 @@ extern "C" int mc_reads_open_gpu_extents(const char* path, int device, int n_thr
     mc_bam_gpu* g = nullptr;
     if (int rc = mc_bam_gpu_open_reads_extents(path, device, n_threads, k_len, n_ref, ext, n_no_coor, n_sel, sel, &g))
         return rc;
-    const int rc = reads_from_gpu(g, path, r.get());
-    mc_bam_gpu_close(g);
-    if (rc) return rc;
+    if (int rc = reads_keep_gpu(g, path, device, k_len, r.get())) {
+        if (!r->g) mc_bam_gpu_close(g);
+        return rc;
+    }
     *out = r.release();
     return MC_OK;
 }
@@ -704,9 +733,10 @@ extern "C" int mc_reads_open_gpu(const char* path, int device, int n_threads, in
     int64_t window = 0;   // (tests: MC_READS_GPU_WINDOW forces the windowed decode)
     if (const char* e = std::getenv("MC_READS_GPU_WINDOW")) window = std::strtoll(e, nullptr, 10);
     if (int rc = mc_bam_gpu_open_reads(path, device, n_threads, k_len, window, &g)) return rc;
-    const int rc = reads_from_gpu(g, path, r.get());
-    mc_bam_gpu_close(g);
-    if (rc) return rc;
+    if (int rc = reads_keep_gpu(g, path, device, k_len, r.get())) {
+        if (!r->g) mc_bam_gpu_close(g);
+        return rc;
+    }
     *out = r.release();
     return MC_OK;
 }
@@ -732,6 +762,7 @@ extern "C" int mc_reads_fields(const mc_reads* r, const int32_t** pos, const int
     MC_REQUIRE(r && pos && end && flag && bits && kmer && name_off && name_len && names && name_bytes && first &&
                    max_span,
                MC_E_INVALID, "null argument");
+    if (int rc = reads_to_host(const_cast<mc_reads*>(r))) return rc;
     *pos = r->pos.data();
     *end = r->end.data();
     *flag = r->flag.data();
@@ -766,6 +797,11 @@ extern "C" int mc_experimental_reads(mc_reads* r, int k_len, const double* val1,
                    "region %lld: bad contig id %d", (long long)q, tid[q]);
         MC_REQUIRE(end[q] > start[q], MC_E_INVALID, "region %lld: length must be > 0", (long long)q);
     }
+    if (r->g && !(std::getenv("MC_EXP_READS") && std::strcmp(std::getenv("MC_EXP_READS"), "host") == 0))
+        return exp_gpu_reads(r->dev, r->first.data(), r->max_span.data(), none ? nullptr : val1, none ? nullptr : has1,
+                             none ? nullptr : val2, none ? nullptr : has2, R, tid, start, end, counts, sums, r->events,
+                             &r->pass_ms);
+    if (int rc = reads_to_host(r)) return rc;   // (MC_EXP_READS=host on a GPU table: the host pass)
     Tables tab{{val1, val2}, {has1, has2}, none};
     r->events.assign((size_t)R, {});
     const int nt = std::max(1, std::min<int>(n_threads_or_all(n_threads), (int)std::max<int64_t>(R, 1)));

@@ -42,6 +42,22 @@ def cap_mask(tid, pos, span, max_depth=HTSLIB_MAX_DEPTH, n_threads=0):
     return keep.view(bool), dropped.value
 
 
+def cap_mask_device(tid, pos, span, max_depth=HTSLIB_MAX_DEPTH):
+    """cap_mask on the device (mc_depth_cap_mask_device) for int32 torch
+    tensors on one GPU: (uint8 keep tensor, reads dropped)."""
+    import torch
+    ts = [t.contiguous().to(torch.int32) for t in (tid, pos, span)]
+    n = ts[0].numel()
+    keep = torch.empty(n, dtype=torch.uint8, device=ts[0].device)
+    torch.cuda.current_stream(ts[0].device).synchronize()
+    dropped = ctypes.c_int64()
+    check(_lib.load().mc_depth_cap_mask_device(ts[0].device.index or 0, n, *[ctypes.c_void_p(t.data_ptr())
+                                                                           for t in ts],
+                                               int(max_depth), ctypes.c_void_p(keep.data_ptr()),
+                                               ctypes.byref(dropped)))
+    return keep, dropped.value
+
+
 def region_reads(tid, pos, span, t, start, end, max_span=None):
     """Indices of the records of contig t overlapping [start, end) — what
     htslib's region iterator hands the pileup (hts_itr_next tests overlap
@@ -96,6 +112,15 @@ def host_intervals(src, contigs):
     return tuple(np.concatenate([q[i] for q in parts]) for i in range(3))
 
 
+def device_intervals(src):
+    """(n, (tid, pos, span) device addresses) of a GPU-decoded source's kept
+    intervals (GpuBamFile), else None."""
+    dptr = getattr(src, "_dptr", None)
+    if dptr is None or getattr(src, "_h", None) is None:
+        return None
+    return int(src.n_kept), tuple(int(p.value or 0) for p in dptr)
+
+
 def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, device=0, with_std=False):
     """Exact stat rows of regions (header contig ids) as pysam's capped
     pileup would fill classic()'s column vector: per region the overlapping
@@ -110,6 +135,26 @@ def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, de
     if len(tids) == 0:
         empty = np.zeros(0, dtype=REGION_STAT_DTYPE)
         return (empty, 0, np.zeros(0)) if with_std else (empty, 0)
+    local = np.arange(len(tids), dtype=np.int32)
+    dev = device_intervals(src)
+    if dev is not None:
+        # the GPU decode's intervals stay in HBM: query gather, cap and the
+        # batch on the device (mc_add_reads_capped)
+        eng = CoverageEngine(device)
+        try:
+            eng.set_contigs(np.asarray(lengths, np.int64)[tids])
+            try:
+                dropped = eng.add_reads_capped(dev[0], *dev[1], src.local_tid(tids), starts, ends, max_depth)
+            except _lib.MetacovError as e:
+                if e.code != _lib.MC_E_RANGE:
+                    raise
+                dev = None   # a span beyond the device walk's ring: the host sweep below
+            if dev is not None:
+                rows = eng.compute_depth_stats(local, starts, ends)
+                std = numpy_std(eng, rows, local, starts, ends) if with_std else None
+                return (rows, dropped, std) if with_std else (rows, dropped)
+        finally:
+            eng.close()
     tid, pos, span = host_intervals(src, tids)
     max_span = int(span.max()) if len(span) else 1
     idx = [region_reads(tid, pos, span, int(t), int(s), int(e), max_span)
@@ -123,7 +168,6 @@ def capped_rows(src, tids, starts, ends, lengths, max_depth=HTSLIB_MAX_DEPTH, de
     try:
         eng.set_contigs(np.asarray(lengths, np.int64)[tids])
         eng.add_reads(vt[keep], vpos[keep], vspan[keep])
-        local = np.arange(len(tids), dtype=np.int32)
         rows = eng.compute_depth_stats(local, starts, ends)
         std = numpy_std(eng, rows, local, starts, ends) if with_std else None
     finally:

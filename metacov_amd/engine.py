@@ -215,6 +215,20 @@ class CoverageEngine:
             self._h, n, ctypes.c_void_p(tid.data_ptr()), ctypes.c_void_p(pos.data_ptr()),
             ctypes.c_void_p(cig_off.data_ptr()), ctypes.c_void_p(cigar.data_ptr())))
 
+    def add_reads_capped(self, n, d_tid, d_pos, d_span, qtid, qstart, qend, max_depth):
+        """The capped recompute's batch from device intervals (addresses of
+        n coordinate-sorted int32 tid / pos / span): region r's pileup query,
+        capped, as contig r (mc_add_reads_capped).  Returns the reads
+        dropped."""
+        qtid = np.ascontiguousarray(qtid, dtype=np.int32)
+        qstart = np.ascontiguousarray(qstart, dtype=np.int64)
+        qend = np.ascontiguousarray(qend, dtype=np.int64)
+        dropped = ctypes.c_int64()
+        self._check(self._lib.mc_add_reads_capped(
+            self._h, int(n), ctypes.c_void_p(d_tid), ctypes.c_void_p(d_pos), ctypes.c_void_p(d_span), len(qtid),
+            ptr(qtid), ptr(qstart), ptr(qend), int(max_depth), ctypes.byref(dropped)))
+        return dropped.value
+
     def clear_reads(self):
         """Drop the reads (contigs stay): the next batch starts empty."""
         self._check(self._lib.mc_clear_reads(self._h))

@@ -137,3 +137,120 @@ def test_zero_span_reads_and_the_pool():
         keep, d2 = depthcap.cap_mask(tid, pos, span, cap)
         assert d2 == dropped, cap
         assert np.array_equal(kept_depth(pos, span, keep, 0, 40), want), cap
+
+
+# ---- the device walk (csrc/capmask.h) --------------------------------------
+
+def _model_case(rng, cap, pile, bg, L, smin, inq_frac=0.0):
+    pos, span = piles(rng, int(rng.integers(1, 12)), pile, bg, L, (smin, 300))
+    if smin == 0:
+        span[rng.random(len(span)) < 0.15] = 0
+    inq = np.ones(len(pos), np.uint8)
+    if inq_frac:
+        inq[rng.random(len(pos)) < inq_frac] = 0
+    return pos, span, inq
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_device_walk_model_matches_host_closed_form(seed):
+    """tests/cap_model.py (cap_walk_kernel lane for lane: bulk chunks, groups
+    in lane order, the ring of ends) against mc_depth_cap_mask on the reads
+    of the query; reads outside the query are invisible to the walk and keep
+    0; small rings take the wrap-around and gap paths."""
+    from tests import cap_model
+    rng = np.random.default_rng(100 + seed)
+    cap = int(rng.choice([1, 2, 3, 5, 20, 64, 100, 300]))
+    pile = int(rng.choice([3, 12, 40, 70, 150, 400]))
+    pos, span, inq = _model_case(rng, cap, pile, int(rng.integers(0, 600)), 5000, int(rng.integers(0, 2)),
+                                 inq_frac=0.2 if seed % 3 == 0 else 0.0)
+    ring = int(rng.choice([512, 1024, 32768]))
+    keep, out_span, dropped = cap_model.cap_walk(list(pos), list(span), list(inq), cap, int(span.max(initial=0)),
+                                                 ring=ring)
+    sel = np.nonzero(inq)[0]
+    want, wd = depthcap.cap_mask(np.zeros(len(sel), np.int32), pos[sel], span[sel], cap)
+    assert dropped == wd
+    got = np.array(keep, bool)
+    assert not got[inq == 0].any()
+    assert np.array_equal(got[sel], want)
+    assert np.array_equal(np.array(out_span), np.where(got, span, 0))
+
+
+def test_device_walk_model_deep_pile():
+    """A 20,000x pile at the 8000 cap: groups larger than a chunk, bulk
+    stretches before and after."""
+    from tests import cap_model
+    rng = np.random.default_rng(9)
+    pos = np.sort(np.concatenate([rng.integers(0, 3000, 600), rng.integers(1000, 1150, 20000)])).astype(np.int32)
+    span = rng.integers(0, 200, len(pos)).astype(np.int32)
+    keep, _, dropped = cap_model.cap_walk(list(pos), list(span), [1] * len(pos), 8000, 200)
+    want, wd = depthcap.cap_mask(np.zeros(len(pos), np.int32), pos, span, 8000)
+    assert dropped == wd > 0
+    assert np.array_equal(np.array(keep, bool), want)
+
+
+@pytest.mark.gpu
+def test_device_cap_mask_matches_host(lib_built):
+    """mc_depth_cap_mask_device against mc_depth_cap_mask and the literal
+    htslib restatement: many queries (tids) in one call, span-0 reads,
+    8000-cap amplicon piles, unsorted input refused."""
+    import torch
+    rng = np.random.default_rng(21)
+    tids, poss, spans = [], [], []
+    for t in range(40):
+        cap_case = t % 4
+        pos, span = piles(rng, int(rng.integers(1, 8)), [12, 60, 150, 2500][cap_case], int(rng.integers(0, 800)),
+                          6000, (0 if t % 2 else 1, 300))
+        if t % 2:
+            span[rng.random(len(span)) < 0.15] = 0
+        tids.append(np.full(len(pos), t, np.int32))
+        poss.append(pos)
+        spans.append(span)
+    tid, pos, span = (np.concatenate(x) for x in (tids, poss, spans))
+    for cap in (3, 40, 8000, 1):
+        want, wd = depthcap.cap_mask(tid, pos, span, cap)
+        got, gd = depthcap.cap_mask_device(*(torch.from_numpy(a).cuda() for a in (tid, pos, span)), cap)
+        assert gd == wd
+        assert np.array_equal(got.cpu().numpy().astype(bool), want)
+    # one query against the literal pileup loop
+    t0 = tid == 3
+    idx = np.nonzero(t0)[0]
+    got, gd = depthcap.cap_mask_device(*(torch.from_numpy(a[idx]).cuda() for a in (tid, pos, span)), 40)
+    v, dropped = htslib_plp.region_depth(tid[idx], pos[idx], span[idx], 3, 0, 6000, max_depth=40)
+    assert gd == dropped
+    assert np.array_equal(kept_depth(pos[idx], span[idx], got.cpu().numpy().astype(bool), 0, 6000), v)
+    bad = pos.copy()
+    bad[5], bad[6] = bad[6] + 1, bad[5]
+    with pytest.raises(Exception, match="sorted"):
+        depthcap.cap_mask_device(*(torch.from_numpy(a).cuda() for a in (tid, bad, span)), 40)
+
+
+@pytest.mark.gpu
+def test_capped_rows_device_equals_host(lib_built, tmp_path):
+    """capped_rows on a GPU decode (mc_add_reads_capped: gather, cap and
+    batch in HBM) equals the host sweep on the same file's host decode, on
+    8000-cap piles with span-0 reads, for regions that share a contig, start
+    before / inside piles, run past the contig end, and on a contig shard."""
+    from metacov_amd import synth
+    from metacov_amd.bam import BamFile, GpuBamFile
+    rng = np.random.default_rng(5)
+    names, lengths, recs = ["a", "b", "c"], [6000, 3000, 9000], []
+    for t, L in enumerate(lengths):
+        pos, span = piles(rng, 3, [9000, 4100, 12000][t], 3000, L, (0, 300))
+        span[rng.random(len(span)) < 0.05] = 0
+        recs += [synth.SynthRecord("r%d_%d" % (t, i), t, int(p), 0, [(0, int(s))] if s else [(4, 20)], 0)
+                 for i, (p, s) in enumerate(zip(pos, span))]
+    bam = str(tmp_path / "deep.bam")
+    synth.write_bam(bam, names, lengths, recs)
+    regs = [(0, 0, 6000), (0, 1000, 2500), (2, 0, 9500), (1, 100, 2900), (2, 4000, 4100), (0, 5990, 6000)]
+    t, s, e = (np.array([r[i] for r in regs], np.int64) for i in range(3))
+    want, wd = depthcap.capped_rows(BamFile(bam), t, s, e, lengths)
+    g = GpuBamFile(bam)
+    got, gd = depthcap.capped_rows(g, t, s, e, lengths)
+    assert gd == wd > 0
+    assert np.array_equal(got, want)
+    g.restrict([0, 2])
+    sel = t != 1
+    got2, gd2 = depthcap.capped_rows(g, t[sel], s[sel], e[sel], lengths)
+    want2, wd2 = depthcap.capped_rows(BamFile(bam), t[sel], s[sel], e[sel], lengths)
+    assert gd2 == wd2 and np.array_equal(got2, want2)
+    g.close()

@@ -665,3 +665,66 @@ def test_cli_rejects_unopenable_fasta_without_k(lib_built, golden_dir, tmp_path)
                                           "-o", str(out)])
     assert res.exit_code != 0 and isinstance(res.exception, OSError)
     assert not out.exists() or out.read_text() == ""
+
+
+def _dup_names_bam(path, seed=13, L=30_000, n=6_000):
+    """Names repeated 1-5 times (supplementary-like copies), some across
+    strands and contigs: the reference's dict pairs occurrences 1-2, 3-4,
+    ... of a name in read order, and a region query sees only its reads."""
+    rng = np.random.default_rng(seed)
+    ref = "".join(rng.choice(list("ACGT"), size=L))
+    recs = []
+    for q in range(n // 3):
+        for c in range(int(rng.integers(1, 6))):
+            tid = int(rng.integers(0, 2))
+            rl = int(rng.integers(30, 120))
+            p = int(rng.integers(0, L - rl))
+            flag = 0x1 | 0x2 | (0x40 if c % 2 == 0 else 0x80) | (0x10 if rng.random() < 0.5 else 0)
+            if rng.random() < 0.05:
+                flag |= 0x100
+            recs.append(synth.SynthRecord("d%d" % q, tid, p, flag, [(0, rl)], rl, ref[p:p + rl]))
+    recs.sort(key=lambda r: (r.tid, r.pos))
+    synth.write_bam(path, ["a", "b"], [L, L], recs)
+
+
+@pytest.mark.gpu
+def test_device_read_pass_equals_host_pass(tmp_path, lib_built, monkeypatch):
+    """The read pass on the device (exp_gpu.hip, the GPU decode's table in
+    HBM) against the host pass over the same table (MC_EXP_READS=host):
+    rows, errors and "RCOR is ZERO" lines identical, for k_cor with zeros,
+    NaN and missing keys, k_cor None (the pair error), reads without SEQ or
+    reference length (errors after and before events), duplicate names,
+    regions past the contig end, one position long, and whole contigs."""
+    import itertools
+    paths = {"long": str(tmp_path / "long.bam"), "mixed": str(tmp_path / "mixed.bam"),
+             "dup": str(tmp_path / "dup.bam")}
+    _long_bam(paths["long"], 21, L=70_000, pairs=8_000)
+    _mixed_reads_bam(paths["mixed"], n=8_000)
+    _dup_names_bam(paths["dup"])
+    rng = np.random.default_rng(8)
+    for k in (4, 6):
+        keys = ["".join(p) for p in itertools.product("ACGT", repeat=k)]
+        kc = [{x: float(rng.uniform(0.3, 3)) for x in keys if rng.random() < 0.85} for _ in range(2)]
+        kc[0][keys[5]] = 0.0
+        kc[1][keys[9]] = 0.0
+        kc[1][keys[11]] = float("nan")
+        ones = [{x: 1.0 for x in keys}, {x: 1.0 for x in keys}]
+        for name, path in paths.items():
+            with mx.ReadTable(path, k, decode="gpu") as t:
+                refs, lens = t.references, t.lengths
+                regions = []
+                for ref, L in zip(refs, lens):
+                    regions += [(ref, 0, L), (ref, 1234, 9000), (ref, 8191, 8192 * 3 + 5), (ref, L - 500, L + 800),
+                                (ref, 17, 18), (ref, 5000, 5001 + 8192)]
+                for kcor in (kc, ones, None):
+                    outs = []
+                    for mode in ("gpu", "host"):
+                        if mode == "host":
+                            monkeypatch.setenv("MC_EXP_READS", "host")
+                        else:
+                            monkeypatch.delenv("MC_EXP_READS", raising=False)
+                        res = mx.experimental_batch(t, kcor, k, None, regions)
+                        outs.append([(r.row, repr(r.error), r.zero_lines) for r in res])
+                    monkeypatch.delenv("MC_EXP_READS", raising=False)
+                    for a, b, reg in zip(outs[0], outs[1], regions):
+                        assert repr(a) == repr(b), (name, k, kcor is None, reg)
