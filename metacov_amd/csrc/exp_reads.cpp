@@ -751,7 +751,7 @@ extern "C" int mc_reads_header(const mc_reads* r, int32_t* n_ref, int64_t* n_rec
     MC_REQUIRE(r, MC_E_INVALID, "null handle");
     if (n_ref) *n_ref = (int32_t)r->names.size();
     if (n_records) *n_records = r->n_records;
-    if (n_placed) *n_placed = (int64_t)r->pos.size();
+    if (n_placed) *n_placed = r->g ? r->dev.n : (int64_t)r->pos.size();
     return MC_OK;
 }
 

@@ -163,6 +163,36 @@ def ref_nt4(w):
     return t[w["ref"].cpu().numpy()]
 
 
+# MI355X issue peaks (MI355X_MICROARCH.md): a wave64 VALU instruction issues
+# over 2 cycles on a SIMD-32 (4 SIMDs per CU); the LDS array takes one
+# 64-lane dword instruction per 2 cycles per CU; 256 CUs at 2.4 GHz.
+VALU_PEAK = 256 * 4 * 0.5 * 2.4e9      # wave-instructions / s
+LDS_PEAK = 256 * 0.5 * 2.4e9
+
+
+def issue_roofline(kern_ms):
+    """The launch's VALU and LDS issue rates against the chip's, from the SQ
+    counters of profiles/sq_scan_kernel.json (scripts/sq_scan_summary.py)
+    when they were taken on the current csrc/scan.hip, else None."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from sq_scan_summary import scan_source_id
+    p = os.path.join(ROOT, "profiles", "sq_scan_kernel.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        d = json.load(fh)
+    if d.get("source_id") != scan_source_id(ROOT):
+        return None
+    k = d["kernels"]
+    valu = sum(v.get("SQ_INSTS_VALU", 0) for v in k.values())
+    lds = sum(v.get("SQ_INSTS_LDS", 0) for v in k.values())
+    t = kern_ms * 1e-3
+    return {"bound": "issue", "unit": "wave-instructions/s",
+            "valu": {"achieved": valu / t, "peak": VALU_PEAK, "frac": valu / t / VALU_PEAK, "insts": valu},
+            "lds": {"achieved": lds / t, "peak": LDS_PEAK, "frac": lds / t / LDS_PEAK, "insts": lds},
+            "per_kernel": k, "record": "profiles/sq_scan_kernel.json (%s)" % d.get("tag")}
+
+
 def main(argv=None):
     args = parse(argv)
     import torch
@@ -237,6 +267,9 @@ def main(argv=None):
                              "(BaseHist: ~10 VALU ops per base)"},
         "checked_reads_vs_c_port": args.check if check else 0,
     }
+    issue = issue_roofline(kern_ms)
+    if issue is not None:
+        line["roofline_issue"] = issue
     if not args.no_cpu_baseline:
         m = min(args.cpu_sample, n)
         if nt4 is None:

@@ -17,3 +17,6 @@ timeout -k 10 500 python -u scripts/cold_cli.py --runs 3 > "$O/${T}_cold_cli.jso
 cat "$O/${T}_cold_cli.json"
 # scan: SQ counters of the final scan kernels (all four tables)
 TAG=${T}_scan SCAN_PROCS=${SCAN_PROCS:-base,kmer,mirror,isize} bash scripts/gpu_scan_sq.sh || exit 1
+python3 scripts/sq_scan_summary.py ${T}_scan libmetacov_amd > "$O/${T}_sq_scan.json" || exit 1
+timeout -k 10 300 python scripts/bench_scan.py > "$O/${T}_scan_bench.log" 2>&1 || { echo "scan bench failed"; tail -5 "$O/${T}_scan_bench.log"; exit 1; }
+tail -1 "$O/${T}_scan_bench.log"
