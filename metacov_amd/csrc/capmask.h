@@ -26,6 +26,9 @@ namespace mc {
 
 constexpr int kCapRing = 32768;               // LDS ints (128 KiB): max span must stay below it
 constexpr int kCapRingMask = kCapRing - 1;
+constexpr int kCapStage = 1024;               // reads per staged batch
+constexpr int kCapPer = kCapStage / 64;
+constexpr int kCapLdsBytes = (kCapRing + 6 * kCapStage) * 4;   // ring + two staged batches
 
 struct CapWave {
     int* E;
@@ -43,6 +46,17 @@ struct CapWave {
         }
         if (s <= ptr) return;
         const long long n = (long long)s - ptr;
+        if (n <= 8) {   // the usual step in a pile: a few slots, read by every lane alike (no reduction)
+            int acc = 0;
+            for (int x = 0; x < (int)n; ++x) {
+                const int k = (ptr + x) & kCapRingMask;
+                acc += E[k];
+            }
+            for (int x = lane; x < (int)n; x += 64) E[(ptr + x) & kCapRingMask] = 0;
+            removed += __builtin_amdgcn_readfirstlane(acc);
+            ptr = s;
+            return;
+        }
         int acc = 0;
         if (n >= kCapRing) {   // every live end lies before s
             for (int k = lane; k < kCapRing; k += 64) {
@@ -89,23 +103,44 @@ cap_walk_kernel(const int32_t* __restrict__ pos, int32_t* __restrict__ span, con
     int last_pos = 0;
     bool have_last = false;
     unsigned long long dropped = 0;
-    // one chunk of loads in flight ahead of the walk
-    int p_n = 0, s_n = 0, q_n = 0;
-    if (i0 + lane < i1) {
-        p_n = pos[i0 + lane];
-        s_n = span[i0 + lane];
-        q_n = inq ? inq[i0 + lane] : 1;
+    // reads staged through LDS in batches of kCapStage (16 chunks), the next
+    // batch's loads in flight while the current one is walked (a chunk's
+    // loads waited on one at a time left the walk latency-bound)
+    int* st_pos = cap_lds + kCapRing;                 // [2][kCapStage]
+    int* st_span = st_pos + 2 * kCapStage;            // [2][kCapStage]
+    int* st_q = st_span + 2 * kCapStage;              // [2][kCapStage]
+    int rp[kCapPer], rs[kCapPer], rq[kCapPer];
+    auto load_batch = [&](int64_t b0) {
+#pragma unroll
+        for (int j = 0; j < kCapPer; ++j) {
+            const int64_t i = b0 + j * 64 + lane;
+            const bool ok = i < i1;
+            rp[j] = ok ? pos[i] : 0;
+            rs[j] = ok ? span[i] : 0;
+            rq[j] = ok ? (inq ? (int)inq[i] : 1) : 0;
+        }
+    };
+    auto stage_batch = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < kCapPer; ++j) {
+            st_pos[buf * kCapStage + j * 64 + lane] = rp[j];
+            st_span[buf * kCapStage + j * 64 + lane] = rs[j];
+            st_q[buf * kCapStage + j * 64 + lane] = rq[j];
+        }
+    };
+    if (i0 < i1) {
+        load_batch(i0);
+        stage_batch(0);
     }
     for (int64_t c0 = i0; c0 < i1; c0 += 64) {
         const int64_t i = c0 + lane;
         const bool valid = i < i1;
-        const int p = p_n, sp = s_n;
-        const bool q = valid && q_n != 0;
-        if (c0 + 64 + lane < i1) {
-            p_n = pos[i + 64];
-            s_n = span[i + 64];
-            q_n = inq ? inq[i + 64] : 1;
-        }
+        const int64_t rel = c0 - i0;
+        const int buf = (int)((rel / kCapStage) & 1);
+        const int at = (int)(rel % kCapStage);
+        if (at == 0 && c0 + kCapStage < i1) load_batch(c0 + kCapStage);   // the next batch, in flight
+        const int p = st_pos[buf * kCapStage + at + lane], sp = st_span[buf * kCapStage + at + lane];
+        const bool q = valid && st_q[buf * kCapStage + at + lane] != 0;
         const unsigned long long qm = __ballot(q);
         bool kept = false;
         if (qm) {
@@ -119,13 +154,15 @@ cap_walk_kernel(const int32_t* __restrict__ pos, int32_t* __restrict__ span, con
             const unsigned long long gm = __ballot(gstart);
             const int f_lane = gm ? __builtin_ctzll(gm) : 0;
             const int l_lane = gm ? 63 - __builtin_clzll(gm) : 0;
-            const int s_first = __shfl(p, f_lane, 64), s_last = __shfl(p, l_lane, 64);
+            const int s_first = __builtin_amdgcn_readlane(p, f_lane), s_last = __builtin_amdgcn_readlane(p, l_lane);
             const long long live = W.total - W.removed;
-            const bool bulk = live + 64 <= maxcnt &&
-                              (!gm || (long long)s_last - (W.have_ptr ? (s_first > W.ptr ? s_first : W.ptr)
-                                                                       : s_first) + max_span + 64 < kCapRing);
+            // bulk: every end inserted first, then the pointer moved to the last
+            // start (ends before it would have left by then anyway); the ring
+            // must hold [ptr, s_last + max span] meanwhile
+            const long long base = W.have_ptr ? W.ptr : s_first;
+            const bool bulk = live + 64 <= maxcnt && (!gm || (long long)s_last - base + max_span + 64 < kCapRing);
             if (bulk) {
-                if (gm) W.advance(s_first);
+                if (gm && !W.have_ptr) W.advance(s_first);   // (the walk's first start: sets the pointer)
                 const bool u = q && (gstart || sp > 0);
                 if (u) atomicAdd(&cap_lds[(p + sp) & kCapRingMask], 1);
                 W.total += __popcll(__ballot(u));
@@ -166,19 +203,20 @@ cap_walk_kernel(const int32_t* __restrict__ pos, int32_t* __restrict__ span, con
                     todo ^= low;
                     const unsigned long long next = todo & (~todo + 1);
                     part = qm & ~(low - 1ull) & (next ? next - 1ull : ~0ull);
-                    W.advance(__shfl(p, first, 64));
+                    W.advance(__builtin_amdgcn_readlane(p, first));
                     C = W.total - W.removed;
                     b = 0;
                 }
             }
             const int hl = 63 - __builtin_clzll(qm);
-            last_pos = __shfl(p, hl, 64);
+            last_pos = __builtin_amdgcn_readlane(p, hl);
             have_last = true;
         }
         if (valid) {
             if (keep) keep[i] = kept ? 1 : 0;
             if (zero_dropped && !kept && sp != 0) span[i] = 0;
         }
+        if (at + 64 == kCapStage && c0 + 64 < i1) stage_batch(buf ^ 1);
     }
     if (lane == 0 && dropped) atomicAdd(dropped_out, dropped);
 }

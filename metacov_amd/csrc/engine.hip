@@ -1949,11 +1949,11 @@ static int cap_walk(hipStream_t s, const int32_t* pos, int32_t* span, const uint
     static bool attr = false;
     if (!attr) {
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(cap_walk_kernel),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kCapRing * 4));
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kCapLdsBytes));
         attr = true;
     }
     if (n_seg <= 0) return MC_OK;
-    hipLaunchKernelGGL(cap_walk_kernel, dim3((unsigned)n_seg), dim3(64), (size_t)kCapRing * 4, s, pos, span, inq,
+    hipLaunchKernelGGL(cap_walk_kernel, dim3((unsigned)n_seg), dim3(64), (size_t)kCapLdsBytes, s, pos, span, inq,
                        d_seg, max_depth, max_span, keep, zero, d_dropped);
     HIP_TRY(hipGetLastError());
     return MC_OK;

@@ -28,6 +28,7 @@ key is dropped with a warning.
 import gzip
 import logging
 import os
+import time
 import warnings
 
 import numpy as np
@@ -523,9 +524,12 @@ def _batch(reads, k_cor, k_len, fasta, regions, device, n_threads, timings):
         t_ = np.ascontiguousarray(tids[idx])
         a_ = np.ascontiguousarray(starts[idx])
         b_ = np.ascontiguousarray(ends[idx])
+        t_pass = time.perf_counter()
         _lib.check(lib.mc_experimental_reads(reads._h, k_len, *ptrs, idx.size, t_.ctypes.data,
                                              a_.ctypes.data, b_.ctypes.data, n_threads,
                                              c_.ctypes.data, s_.ctypes.data), lib)
+        if timings is not None:
+            timings["reads_pass_ms"] = (time.perf_counter() - t_pass) * 1e3
         counts[idx], sums[idx] = c_, s_
         events = []
         for j in range(idx.size):

@@ -254,3 +254,40 @@ def test_capped_rows_device_equals_host(lib_built, tmp_path):
     want2, wd2 = depthcap.capped_rows(BamFile(bam), t[sel], s[sel], e[sel], lengths)
     assert gd2 == wd2 and np.array_equal(got2, want2)
     g.close()
+
+
+def _continuation_pile():
+    """Start groups of 70 reads (longer than a 64-read chunk) whose tails are
+    1 bp and span-0 reads, 3 positions apart, below the cap, then a pile
+    at the cap: a bulk chunk must insert the open group's ends before it
+    moves its pointer, or they linger and inflate the later pool count."""
+    pos, span = [], []
+    for s in range(0, 12000, 3):
+        for j in range(70):
+            pos.append(s)
+            span.append((0 if j % 2 else 1) if j >= 60 else 1 + (j % 3))
+    for j in range(400):
+        pos.append(12100)
+        span.append(50)
+    return np.array(pos, np.int32), np.array(span, np.int32)
+
+
+def test_device_walk_model_continuation_groups():
+    from tests import cap_model
+    pos, span = _continuation_pile()
+    for cap in (120, 75, 300):
+        keep, _, dropped = cap_model.cap_walk(list(pos), list(span), [1] * len(pos), cap, 3, ring=1024)
+        want, wd = depthcap.cap_mask(np.zeros(len(pos), np.int32), pos, span, cap)
+        assert dropped == wd and np.array_equal(np.array(keep, bool), want)
+
+
+@pytest.mark.gpu
+def test_device_cap_mask_continuation_groups(lib_built):
+    import torch
+    pos, span = _continuation_pile()
+    tid = np.zeros(len(pos), np.int32)
+    for cap in (120, 75, 300):
+        want, wd = depthcap.cap_mask(tid, pos, span, cap)
+        got, gd = depthcap.cap_mask_device(*(torch.from_numpy(a).cuda() for a in (tid, pos, span)), cap)
+        assert gd == wd
+        assert np.array_equal(got.cpu().numpy().astype(bool), want)
