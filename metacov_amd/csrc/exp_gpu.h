@@ -27,10 +27,14 @@ struct ExpDevTable {
 // unsorted_at: the first record out of (tid, pos) order, or -1.
 int exp_gpu_index(const ExpDevTable& t, int32_t n_ref, int64_t* first, int64_t* max_span, int64_t* unsorted_at);
 
+// Device buffers kept between calls (one per mc_reads table).
+struct ExpScratch;
+void exp_gpu_scratch_free(ExpScratch* s);
+
 // mc_experimental_reads on the device: the same counts[8 R] / sums[4 R] and
 // per-region "RCOR is ZERO" events as the host pass (csrc/exp_reads.cpp).
 // val / has: the two k-mer tables (null: k_cor is None).
 int exp_gpu_reads(const ExpDevTable& t, const int64_t* first, const int64_t* max_span, const double* val1,
                   const uint8_t* has1, const double* val2, const uint8_t* has2, int64_t R, const int32_t* tid,
                   const int64_t* start, const int64_t* end, int64_t* counts, double* sums,
-                  std::vector<std::vector<uint64_t>>& events, double* kernel_ms);
+                  std::vector<std::vector<uint64_t>>& events, double* kernel_ms, ExpScratch** scratch);

@@ -721,7 +721,53 @@ int exp_gpu_index(const ExpDevTable& t, int32_t n_ref, int64_t* first, int64_t* 
     return MC_OK;
 }
 
-static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t* max_span, const double* val1,
+struct ExpScratch {
+    Buf<int64_t> d_first;
+    Buf<unsigned long long> d_ms;
+    Buf<double> d_val;
+    Buf<uint8_t> d_has;
+    Buf<int32_t> d_t;
+    Buf<uint8_t> cls;
+    Buf<uint8_t> open;
+    Buf<uint8_t> err;
+    Buf<uint8_t> ev;
+    Buf<uint8_t> pflag;
+    Buf<uint8_t> rflag;
+    Buf<int64_t> ridx;
+    Buf<int64_t> c2;
+    Buf<int64_t> rs;
+    Buf<int64_t> re;
+    Buf<int32_t> sreg;
+    Buf<int32_t> mate;
+    Buf<uint64_t> key;
+    Buf<uint64_t> key2;
+    Buf<uint64_t> skey;
+    Buf<uint64_t> skey2;
+    Buf<uint32_t> sidx;
+    Buf<uint32_t> sidx2;
+    Buf<uint32_t> sval2;
+    Buf<double> term;
+    Buf<double> inv;
+    Buf<unsigned long long> cnt;
+    Buf<unsigned long long> err_at;
+    Buf<unsigned long long> n_ev;
+    Buf<Event> evs;
+    Buf<unsigned char> temp;
+    Buf<double> cterm;
+    Buf<double> seq_out;
+    Buf<int64_t> poff;
+    Buf<int64_t> d_nsel;
+    Buf<int64_t> runs_at;
+    Buf<int64_t> srs;
+    Buf<int64_t> soff;
+    Buf<double> sinv;
+    Buf<int64_t> boff;
+    Buf<double> bsum;
+    Buf<double> tot;
+    Buf<uint8_t> d_want;
+};
+
+static int reads_chunk(ExpScratch& X, const ExpDevTable& t, const int64_t* first, const int64_t* max_span, const double* val1,
                        const uint8_t* has1, const double* val2, const uint8_t* has2, int64_t R, const int32_t* tid,
                        const int64_t* start, const int64_t* end, int64_t* counts, double* sums,
                        std::vector<std::vector<uint64_t>>& events) {
@@ -734,8 +780,8 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     // per-contig index on the device (first record, max span)
     int32_t n_all = 0;
     for (int64_t q = 0; q < R; ++q) n_all = std::max(n_all, tid[q] + 1);
-    Buf<int64_t> d_first;
-    Buf<unsigned long long> d_ms;
+    auto& d_first = X.d_first;
+    auto& d_ms = X.d_ms;
     {
         // the caller's tables cover every contig of the header; copy what the regions index
         std::vector<unsigned long long> ms((size_t)n_all);
@@ -748,8 +794,8 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     // k-mer tables
     const bool none = !val1 || !has1 || !val2 || !has2;
     const size_t nk = (size_t)1 << (2 * t.k);
-    Buf<double> d_val;
-    Buf<uint8_t> d_has;
+    auto& d_val = X.d_val;
+    auto& d_has = X.d_has;
     Tab tab{{nullptr, nullptr}, {nullptr, nullptr}, none ? 1 : 0};
     if (!none) {
         HIP_TRY(d_val.reserve(2 * nk));
@@ -763,7 +809,7 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     // regions
     std::vector<int64_t> hL((size_t)R);
     for (int64_t q = 0; q < R; ++q) hL[(size_t)q] = end[q] - start[q];
-    Buf<int32_t> d_t;
+    auto& d_t = X.d_t;
     Buf<int64_t> d_s, d_L, d_lo, d_hi, d_off;
     HIP_TRY(d_t.reserve((size_t)R));
     HIP_TRY(d_s.reserve((size_t)R));
@@ -791,12 +837,27 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     MC_REQUIRE(N < (int64_t(1) << 31), MC_E_RANGE, "%lld candidate reads", (long long)N);
     HIP_TRY(hipMemcpy(d_off.p, off.data(), (R + 1) * 8, hipMemcpyHostToDevice));
     // slots
-    Buf<uint8_t> cls, open, err, ev, pflag, rflag;
-    Buf<int64_t> ridx, c2, rs, re;
-    Buf<int32_t> sreg, mate;
-    Buf<uint64_t> key, key2, skey, skey2;
-    Buf<uint32_t> sidx, sidx2, sval2;
-    Buf<double> term, inv;
+    auto& cls = X.cls;
+    auto& open = X.open;
+    auto& err = X.err;
+    auto& ev = X.ev;
+    auto& pflag = X.pflag;
+    auto& rflag = X.rflag;
+    auto& ridx = X.ridx;
+    auto& c2 = X.c2;
+    auto& rs = X.rs;
+    auto& re = X.re;
+    auto& sreg = X.sreg;
+    auto& mate = X.mate;
+    auto& key = X.key;
+    auto& key2 = X.key2;
+    auto& skey = X.skey;
+    auto& skey2 = X.skey2;
+    auto& sidx = X.sidx;
+    auto& sidx2 = X.sidx2;
+    auto& sval2 = X.sval2;
+    auto& term = X.term;
+    auto& inv = X.inv;
     const size_t Nz = (size_t)std::max<int64_t>(N, 1);
     for (auto* b : {&cls, &open, &err, &ev, &pflag, &rflag}) HIP_TRY(b->reserve(Nz));
     for (auto* b : {&ridx, &c2, &rs, &re}) HIP_TRY(b->reserve(Nz));
@@ -805,7 +866,9 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     for (auto* b : {&sidx, &sidx2, &sval2}) HIP_TRY(b->reserve(Nz));
     for (auto* b : {&term, &inv}) HIP_TRY(b->reserve(Nz));
     Slots S{cls.p, ridx.p, sreg.p, key.p, sidx.p, mate.p, open.p, err.p, ev.p, term.p, c2.p, inv.p, rs.p, re.p};
-    Buf<unsigned long long> cnt, err_at, n_ev;
+    auto& cnt = X.cnt;
+    auto& err_at = X.err_at;
+    auto& n_ev = X.n_ev;
     HIP_TRY(cnt.reserve((size_t)R * kC));
     HIP_TRY(err_at.reserve((size_t)R));
     HIP_TRY(n_ev.reserve(1));
@@ -814,10 +877,10 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     HIP_TRY(hipMemset(n_ev.p, 0, 8));
     HIP_TRY(hipMemset(pflag.p, 0, Nz));
     HIP_TRY(hipMemset(skey.p, 0xFF, Nz * 8));
-    Buf<Event> evs;
+    auto& evs = X.evs;
     HIP_TRY(evs.reserve(Nz));
     const unsigned gx = grid_for(max_q, 256, 512);
-    Buf<unsigned char> temp;
+    auto& temp = X.temp;
     auto sort_pairs = [&](const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout) -> int {
         size_t tb = 0;
         HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, (int)N, 0, 64, st));
@@ -842,8 +905,10 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     HIP_TRY(hipMemcpy(he.data(), err_at.p, R * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&hn, n_ev.p, 8, hipMemcpyDeviceToHost));
     // wnf: the pair terms in read order of the second mate
-    Buf<double> cterm, seq_out;
-    Buf<int64_t> poff, d_nsel;
+    auto& cterm = X.cterm;
+    auto& seq_out = X.seq_out;
+    auto& poff = X.poff;
+    auto& d_nsel = X.d_nsel;
     HIP_TRY(cterm.reserve(Nz));
     HIP_TRY(seq_out.reserve((size_t)R));
     HIP_TRY(poff.reserve((size_t)R + 1));
@@ -857,8 +922,10 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
         HIP_TRY(hipcub::DeviceSelect::Flagged(temp.p, tb, term.p, pflag.p, cterm.p, d_nsel.p, (int)N, st));
     }
     // the starts: (region, rstart) sorted, the last read of each kept
-    Buf<int64_t> runs_at, srs, soff;
-    Buf<double> sinv;
+    auto& runs_at = X.runs_at;
+    auto& srs = X.srs;
+    auto& soff = X.soff;
+    auto& sinv = X.sinv;
     if (N) {
         if (int rc = sort_pairs(skey.p, skey2.p, sidx.p, sval2.p)) return rc;
         hipLaunchKernelGGL(start_runs_kernel, dim3(grid_for(N, 256, 1 << 30)), dim3(256), 0, st, skey2.p, N, rflag.p,
@@ -887,15 +954,14 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
     std::vector<int64_t> hbo((size_t)R + 1, 0);
     for (int64_t q = 0; q < R; ++q) hbo[(size_t)q + 1] = hbo[(size_t)q] + (hL[(size_t)q] + kBuf - 1) / kBuf;
     const int64_t NB = hbo[(size_t)R];
-    Buf<int64_t> boff;
-    Buf<double> bsum, tot;
+    auto& boff = X.boff;
+    auto& bsum = X.bsum;
+    auto& tot = X.tot;
     HIP_TRY(boff.reserve((size_t)R + 1));
     HIP_TRY(bsum.reserve((size_t)std::max<int64_t>(NB, 1)));
     HIP_TRY(tot.reserve((size_t)R));
     HIP_TRY(hipMemcpy(boff.p, hbo.data(), (R + 1) * 8, hipMemcpyHostToDevice));
     if (M) {
-        Buf<int64_t> iota;
-        HIP_TRY(iota.reserve(Nz));
         {
             size_t tb = 0;
             hipcub::CountingInputIterator<int64_t> ci(0);
@@ -926,7 +992,7 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
         any |= want[(size_t)q] != 0;
     }
     if (any && NB) {
-        Buf<uint8_t> d_want;
+        auto& d_want = X.d_want;
         HIP_TRY(d_want.reserve((size_t)R));
         HIP_TRY(hipMemcpy(d_want.p, want.data(), R, hipMemcpyHostToDevice));
         HIP_TRY(hipMemset(bsum.p, 0, (size_t)NB * 8));
@@ -972,15 +1038,16 @@ static int reads_chunk(const ExpDevTable& t, const int64_t* first, const int64_t
 int exp_gpu_reads(const ExpDevTable& t, const int64_t* first, const int64_t* max_span, const double* val1,
                   const uint8_t* has1, const double* val2, const uint8_t* has2, int64_t R, const int32_t* tid,
                   const int64_t* start, const int64_t* end, int64_t* counts, double* sums,
-                  std::vector<std::vector<uint64_t>>& events, double* kernel_ms) {
+                  std::vector<std::vector<uint64_t>>& events, double* kernel_ms, ExpScratch** scratch) {
     const auto t_start = std::chrono::steady_clock::now();
+    if (!*scratch) *scratch = new ExpScratch();
     HIP_TRY(hipSetDevice(t.device));
     events.assign((size_t)R, {});
     constexpr int64_t kChunkRegions = 32768;   // (regions are the grids' y dimension)
     for (int64_t r0 = 0; r0 < R; r0 += kChunkRegions) {
         const int64_t nr = std::min(kChunkRegions, R - r0);
         std::vector<std::vector<uint64_t>> ev;
-        if (int rc = reads_chunk(t, first, max_span, val1, has1, val2, has2, nr, tid + r0, start + r0, end + r0,
+        if (int rc = reads_chunk(**scratch, t, first, max_span, val1, has1, val2, has2, nr, tid + r0, start + r0, end + r0,
                                  counts + 8 * r0, sums + 4 * r0, ev))
             return rc;
         for (int64_t q = 0; q < nr; ++q) events[(size_t)(r0 + q)] = std::move(ev[(size_t)q]);
@@ -988,4 +1055,8 @@ int exp_gpu_reads(const ExpDevTable& t, const int64_t* first, const int64_t* max
     if (kernel_ms)
         *kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return MC_OK;
+}
+
+void exp_gpu_scratch_free(ExpScratch* s) {
+    delete s;
 }

@@ -86,7 +86,9 @@ struct mc_reads {
     ExpDevTable dev;
     bool host_ready = true;
     double pass_ms = 0;             // the last mc_experimental_reads call
+    ExpScratch* scratch = nullptr;  // the device pass's buffers, kept between calls
     ~mc_reads() {
+        if (scratch) exp_gpu_scratch_free(scratch);
         if (g) mc_bam_gpu_close(g);
     }
 };
@@ -800,7 +802,7 @@ extern "C" int mc_experimental_reads(mc_reads* r, int k_len, const double* val1,
     if (r->g && !(std::getenv("MC_EXP_READS") && std::strcmp(std::getenv("MC_EXP_READS"), "host") == 0))
         return exp_gpu_reads(r->dev, r->first.data(), r->max_span.data(), none ? nullptr : val1, none ? nullptr : has1,
                              none ? nullptr : val2, none ? nullptr : has2, R, tid, start, end, counts, sums, r->events,
-                             &r->pass_ms);
+                             &r->pass_ms, &r->scratch);
     if (int rc = reads_to_host(r)) return rc;   // (MC_EXP_READS=host on a GPU table: the host pass)
     Tables tab{{val1, val2}, {has1, has2}, none};
     r->events.assign((size_t)R, {});
