@@ -227,6 +227,7 @@ struct mc_ctx {
     DevBuf<int> d_chunk_carry;
     DevBuf<long long> d_scan_part;        // long_scan partial sums
     int long_grid = 0;                    // resident long_count / long_fill workgroups
+    int long_grid_words = 0;              // resident long_fill_words workgroups
     DevBuf<int32_t> d_depth;
     bool depth_valid = false;
     int32_t max_depth = -1;
@@ -830,6 +831,8 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
             HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)long_fill_kernel, kBlock, 0));
             ctx->long_grid = ncu * std::max(1, per);
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)long_fill_words_kernel, kBlock, 0));
+            ctx->long_grid_words = ncu * std::max(1, per);
         }
         LongGeo G{ctx->d_tid.p, ctx->d_pos.p, ctx->d_span.p, n, ctx->d_coff.p, ctx->short_max, alloc_len, 0, 0};
         while (((int64_t)1 << G.lcw) < ctx->chunk_w) ++G.lcw;
@@ -850,10 +853,14 @@ extern "C" int mc_prepare(mc_ctx* ctx) {
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(long_scan_final_kernel, dim3(bt + bc), dim3(kBlock), 0, s, A);
         HIP_TRY(hipGetLastError());
-        if (counted && end_words)
-            hipLaunchKernelGGL(long_fill_words_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, ctx->d_endw.p, n,
-                               G.per, G.lcw, ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
-        else
+        if (counted && end_words) {
+            // its own resident grid (the LDS event buffer of MC_FILL_SORTED
+            // lowers its occupancy); counts and fill need not share sub-ranges
+            const int64_t nbw = std::max<int64_t>(1, std::min<int64_t>(subs, ctx->long_grid_words));
+            const int64_t perw = (subs + nbw - 1) / nbw * kLongSub;
+            hipLaunchKernelGGL(long_fill_words_kernel, dim3((unsigned)nbw), dim3(kBlock), 0, s, ctx->d_endw.p, n,
+                               perw, G.lcw, ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
+        } else
             hipLaunchKernelGGL(long_fill_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, G,
                                ctx->d_tile_off.p, ctx->d_tile_cnt.p, ctx->d_tile_ev.p);
         HIP_TRY(hipGetLastError());
