@@ -61,6 +61,11 @@ namespace mc {
                                        // (measured at C5: 0.114 -> 0.128 ms, prepare 0.410 -> 0.421 ms; the 32 KB
                                        // buffer halves the resident workgroups: profiles/r06/r06h_*)
 #endif
+#ifndef MC_DEFER_LONG
+#define MC_DEFER_LONG 1                // the fused long-read K2 defers its tile stores too (in-process A/B,
+                                       // C5 K2 median 1.087 -> 1.070 and 1.081 -> 1.072 ms: profiles/r06/r06j_*, r06k_*;
+                                       // the fused short-read K2 has no long-read registers to trade and loses 1.6 %)
+#endif
 #ifndef MC_NT_STORE
 #define MC_NT_STORE 1                  // non-temporal depth stores (written once, not re-read soon)
 #endif
@@ -2172,7 +2177,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
     // apply loop), plain K2 only: with 12 B/read they gained plain C3 -2.4 %,
     // C5 -4.9 %; with the packed read words the fused C3 K2 runs 1.6 % faster
     // without them (profiles/r02zz_knobs_ab.txt).
-    constexpr bool kDefer = !kStats;
+    constexpr bool kDefer = !kStats || (kLong && MC_DEFER_LONG);
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     // The probe saw an unsorted / invalid sample or a long span: the host
     // re-runs this batch through the full prepare; nothing to do here.
