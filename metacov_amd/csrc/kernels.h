@@ -66,6 +66,10 @@ namespace mc {
                                        // C5 K2 median 1.087 -> 1.070 and 1.081 -> 1.072 ms: profiles/r06/r06j_*, r06k_*;
                                        // the fused short-read K2 has no long-read registers to trade and loses 1.6 %)
 #endif
+#ifndef MC_DEFER_DIRECT
+#define MC_DEFER_DIRECT 0              // the fused direct K2 defers its tile stores too (in-process A/B: C3 K2
+                                       // 0.990 -> 1.009 ms, C2 0.0527 -> 0.0534: profiles/r06/r06l_*)
+#endif
 #ifndef MC_NT_STORE
 #define MC_NT_STORE 1                  // non-temporal depth stores (written once, not re-read soon)
 #endif
@@ -1741,7 +1745,12 @@ __device__ __forceinline__ void far_halo(const ReadArrays& A, const DT& D, const
                                          int64_t lo, int64_t hi, int64_t C0, int short_max, int* ring) {
     // (one int4 of spans per thread and step: keeping 8 in flight raised the
     // kernel's VGPRs and cost C3 +10 %, r05/r05ab13_*)
-    for (int64_t i0 = (lo & ~(int64_t)3) + (int64_t)threadIdx.x * 4; i0 < hi; i0 += (int64_t)kK2Block * 4) {
+    // the lane offset is opaque to the optimiser: hoisted out of the chunk
+    // loop, the three per-lane array addresses were the fused direct K2's
+    // VGPR spills (6), reloaded from scratch with a vmcnt(0) each per chunk
+    int lane_off = (int)threadIdx.x * 4;
+    asm volatile("" : "+v"(lane_off));
+    for (int64_t i0 = (lo & ~(int64_t)3) + lane_off; i0 < hi; i0 += (int64_t)kK2Block * 4) {
         const i32x4 s4 = *reinterpret_cast<const i32x4*>(A.span + i0);
         const int sp[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
@@ -2177,7 +2186,7 @@ depth_kernel(ReadArrays A, const K2Consts* __restrict__ K, int64_t n,
     // apply loop), plain K2 only: with 12 B/read they gained plain C3 -2.4 %,
     // C5 -4.9 %; with the packed read words the fused C3 K2 runs 1.6 % faster
     // without them (profiles/r02zz_knobs_ab.txt).
-    constexpr bool kDefer = !kStats || (kLong && MC_DEFER_LONG);
+    constexpr bool kDefer = !kStats || (kLong && MC_DEFER_LONG) || (kDirect && MC_DEFER_DIRECT);
     constexpr bool kPf = kStats ? MC_PREFETCH_STATS : MC_PREFETCH;
     // The probe saw an unsorted / invalid sample or a long span: the host
     // re-runs this batch through the full prepare; nothing to do here.
