@@ -108,6 +108,11 @@ constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SC
 #ifndef MC_SCAN_PF2
 #define MC_SCAN_PF2 1
 #endif
+//   MC_SCAN_KMER8  KmerHist codes (K <= 8) from one 8-base window each (kmer8;
+//                  0: base by base)
+#ifndef MC_SCAN_KMER8
+#define MC_SCAN_KMER8 1
+#endif
 #ifndef MC_SCAN_STAGE_REGS
 #define MC_SCAN_STAGE_REGS 3      // 16-byte units per lane in flight (VGPRs: 4 each)
 #endif
@@ -224,6 +229,38 @@ struct RefWin {
     }
 };
 
+// KmerHist's code of the K <= 8 bases b .. b+K-1 of a read (forward), or of
+// comp(b+K-1) .. comp(b) (reverse strand: base j of the k-mer is the read's
+// base b+K-1-j, complemented), from one 8-base window: two dwords of packed
+// bases (the pair is clamped to the read's last dwords, ndw = dwords of its
+// bases, so nothing past it is read), the nibbles of each byte swapped into
+// base order, then per nibble n (nt16): nt4 = (bit1 | bit3) | (bit2 | bit3) << 1
+// for n in {1, 2, 4, 8}; any other n (one bit set is the test) puts the k-mer
+// in the N bucket 4^K.  Base j of the code at bits 2j (scan.pyx:480-501).
+template <typename P32>
+__device__ __forceinline__ uint32_t kmer8(P32 s32, int b, int ndw, int K, bool rev) {
+    const int byte = b >> 1;
+    const int q = min(byte >> 2, ndw - 2);
+    uint64_t w = (uint64_t)s32[q] | ((uint64_t)s32[q + 1] << 32);
+    w >>= 8 * (byte - 4 * q);   // (0..7 bytes: the window ends inside the pair)
+    w = ((w >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((w & 0x0F0F0F0F0F0F0F0Full) << 4);
+    const uint32_t n = (uint32_t)(w >> (4 * (b & 1)));   // base b + j at nibble j
+    constexpr uint32_t M1 = 0x11111111u;
+    const uint32_t t0 = n & M1, t1 = (n >> 1) & M1, t2 = (n >> 2) & M1, t3 = (n >> 3) & M1;
+    const uint32_t nib = K == 8 ? 0xFFFFFFFFu : (1u << (4 * K)) - 1u;
+    if (((t0 + t1 + t2 + t3) ^ M1) & nib) return 1u << (2 * K);   // a base other than A/C/G/T
+    uint32_t c = (t1 | t3) | ((t2 | t3) << 1);   // nt4 in the low 2 bits of each nibble
+    c = (c | (c >> 2)) & 0x0F0F0F0Fu;
+    c = (c | (c >> 4)) & 0x00FF00FFu;
+    c = (c | (c >> 8)) & 0x0000FFFFu;            // base b + j at bits 2j
+    const uint32_t km = (1u << (2 * K)) - 1u;
+    if (!rev) return c & km;
+    c = ((c & 0x3333u) << 2) | ((c >> 2) & 0x3333u);   // the eight 2-bit fields reversed
+    c = ((c & 0x0F0Fu) << 4) | ((c >> 4) & 0x0F0Fu);
+    c = ((c & 0x00FFu) << 8) | ((c >> 8) & 0x00FFu);
+    return (c >> (2 * (8 - K))) ^ km;                  // comp(n) = 3 - n
+}
+
 __device__ __forceinline__ void inc(lds_u32* lds_base, uint32_t* g, int64_t i, bool in_lds) {
     if (in_lds)
         __hip_atomic_fetch_add(lds_base + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -259,9 +296,16 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
         const uint32_t nbucket = 1u << (2 * a.K);
         const bool ok = rlen >= a.OFF + a.STEP * a.NK;
         if (a.kcodes && a.G > 1) a.kgroup[r] = (uint16_t)g;
+        // every k-mer's bases inside the read (and K <= 8, two dwords of
+        // bases): each code from one 8-base window (kmer8), not base by base
+        const bool fast = MC_SCAN_KMER8 && ok && a.K <= 8 && a.OFF >= 0 && rlen >= 9 &&
+                          a.OFF + (a.NK - 1) * a.STEP + a.K <= rlen;
         for (int i = 0; i < a.NK; ++i) {
             uint32_t k = 0xFFFFu;
-            if (ok) {
+            if (fast) {
+                const int x0 = a.OFF + i * a.STEP;
+                k = kmer8(s32, rev ? rlen - a.K - x0 : x0, (rlen + 7) >> 3, a.K, rev);
+            } else if (ok) {
                 k = 0;
                 for (int j = 0; j < a.K; ++j) {
                     const int x = a.OFF + i * a.STEP + j;

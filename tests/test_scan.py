@@ -727,6 +727,52 @@ def test_scan_kernel_queue_and_cuts_vs_c_port_gpu(lib_built):
 
 
 @pytest.mark.gpu
+def test_kmer_codes_vs_c_port_gpu(lib_built):
+    """KmerHist alone over reads of random nt16 nibbles (mostly A/C/G/T, some
+    N and invalid codes), both strands, 1-300 bases plus two reads longer
+    than the LDS stage (the global-memory path), under k-mer geometries that
+    take the 8-base-window codes (K <= 8, every base inside the read: odd and
+    even first bases, windows ending in the read's last dword) and the
+    base-by-base loop (K > 8, a negative offset, K > STEP running past the
+    read): equal to the C port in every bin."""
+    from metacov_amd import _lib
+    from oracle import coracle
+    lib = _lib.load()
+    rng = np.random.default_rng(29)
+    rlen = np.concatenate([rng.integers(1, 301, 6000), [12001, 15000]]).astype(np.int32)
+    n = rlen.size
+    flag = np.where(rng.random(n) < 0.5, 0x10, 0).astype(np.int32) | np.where(rng.random(n) < 0.5, 0x40, 0x80)
+    gpos = rng.integers(0, 1000, n).astype(np.int32)
+    nbytes = (rlen + 1) // 2
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum((nbytes + 3) // 4 * 4)
+    nib = np.array([1, 2, 4, 8], np.uint8)[rng.integers(0, 4, int(2 * off[-1]))]
+    odd = rng.random(nib.size)
+    nib[odd < 0.01] = 15
+    nib[(odd >= 0.01) & (odd < 0.015)] = rng.integers(0, 16, int(((odd >= 0.01) & (odd < 0.015)).sum()))
+    seq = ((nib[0::2] << 4) | nib[1::2]).astype(np.uint8)
+    batch = [rlen, flag, gpos, np.zeros(n, np.int32), np.full(n, -1, np.int32), off, seq]
+    for K, NK, STEP, OFF in ((7, 8, 7, 0), (8, 5, 3, 4), (1, 20, 1, 0), (5, 10, 2, 3), (3, 4, 9, 1),
+                             (8, 1, 1, 0), (2, 30, 9, 7), (12, 3, 12, 0), (6, 9, 5, -2), (8, 6, 4, 0)):
+        cfg = _lib.ScanConfig()
+        cfg.n_flags = 1
+        cfg.flags[0] = 0x40
+        cfg.kmer_on, cfg.kmer_k, cfg.kmer_nk, cfg.kmer_step, cfg.kmer_offset = 1, K, NK, STEP, OFF
+        h = ctypes.c_void_p()
+        _lib.check(lib.mc_scan_create(0, ctypes.byref(cfg), ctypes.byref(h)), lib)
+        _lib.check(lib.mc_scan_add_batch(h, n, *[_lib.ptr(a) for a in batch]), lib)
+        G, rows, cap = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        lib.mc_scan_dims(h, ctypes.byref(G), ctypes.byref(rows), ctypes.byref(cap), None, None)
+        kmer = np.zeros((G.value, 4 ** K + 1, NK), np.uint32)
+        _lib.check(lib.mc_scan_results(h, None, _lib.ptr(kmer), None, None, None), lib)
+        lib.mc_scan_destroy(h)
+        want, done = coracle.scan(cfg, batch, None, None, None, 0, 128)
+        assert done == n
+        assert np.array_equal(kmer, want[1]), (K, NK, STEP, OFF)
+        assert kmer[:, :4 ** K].sum() > 0 and kmer[:, 4 ** K].sum() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("window, chunk", [(None, None), ("65536", None), (None, "9999")])
 def test_scan_gpu_decode_equals_host_source_gpu(mix, golden_dir, lib_built, tmp_path, window, chunk, monkeypatch):
     """scan_reads with the BAM decoded on the GPU (mc_bam_gpu_open_scan +
