@@ -662,12 +662,15 @@ static void resolve_timings(mc_ctx* ctx, bool all) {
 // (its chunk-end flushes double) and reads its chunk c as base chunks
 // [c*s, c*s + s).  Long reads' end buckets and carries are per full
 // chunk, so with long reads the plain K2 runs on full chunks too.
-// chunks are halved while a layout would have fewer than this many: a
+// chunks are halved while a layout would have fewer than this many.  The
 // strong-scaling shard (C3 / 8: 3.8 k chunks of 8 tiles for 1024 resident
-// workgroups) runs K2 2.5 % faster on 4-tile chunks; 8192 was 33 % slower
-// (profiles/r03ii_min_chunks_ab.txt)
+// workgroups) ran K2 2.5 % faster on 4-tile chunks in round 3
+// (profiles/r03ii_min_chunks_ab.txt); on the round-6 kernel it runs 3.7 %
+// faster on 8-tile chunks (floor 2048: 0.147 -> 0.142 ms; 8192 / 16384, two-
+// tile chunks: 0.210 ms; profiles/r06/r06n_*, r06o_*).  C2 and C3 take the
+// same chunks either way.
 #ifndef MC_MIN_CHUNKS
-#define MC_MIN_CHUNKS 4096
+#define MC_MIN_CHUNKS 2048
 #endif
 static void set_layout(mc_ctx* ctx, const std::vector<int64_t>& ext) {
     const int32_t nc = (int32_t)ctx->len.size();
