@@ -113,6 +113,17 @@ constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SC
 #ifndef MC_SCAN_KMER8
 #define MC_SCAN_KMER8 1
 #endif
+//   MC_SCAN_QUEUES slice queues (take_slice).  100 M reads, ms for IsizeHist
+//                  alone / KmerHist alone / all four: 1 queue 4.53 / 5.29 /
+//                  14.22, 2: 2.37 / 3.58 / 14.11, 4: 1.32 / 3.54 / 14.05,
+//                  8 (one per XCD): 1.02 / 3.52 / 14.30
+//                  (profiles/r06/r06s_scan_queues_ab.txt)
+#ifndef MC_SCAN_QUEUES
+#define MC_SCAN_QUEUES 4
+#endif
+#ifndef MC_SCAN_QPEEK
+#define MC_SCAN_QPEEK 0             // take_slice reads a queue's counter before its atomic
+#endif
 #ifndef MC_SCAN_STAGE_REGS
 #define MC_SCAN_STAGE_REGS 3      // 16-byte units per lane in flight (VGPRs: 4 each)
 #endif
@@ -151,7 +162,9 @@ struct ScanArgs {
     const uint8_t* seq;
     int64_t n;
     int64_t per_wave;         // reads per slice (a multiple of 64)
-    unsigned* work;           // the slice queue (0 at launch), or null: one static slice per wave
+    unsigned* work;           // the slice queues (0 at launch, kQueueStride apart), or null: one static slice per wave
+    int32_t nq;               // queues: queue q hands out slices [q * per_q, (q + 1) * per_q) of n_slices
+    uint32_t per_q, n_slices;
     const uint8_t* ref;       // nt4 codes, all sequences back to back (padded both ends)
     const int64_t* ref_off;
     const int64_t* ref_len;
@@ -717,6 +730,28 @@ __device__ __forceinline__ void stage16(lds_u32* dst, const u32x4* __restrict__ 
 // reference sequence, the reference window it touches are copied to LDS
 // with coalesced dword loads; every per-read access after that is LDS.
 // A read too long to stage is processed from global memory.
+// The next slice for a wave of workgroup queue `home` (blockIdx % nq; with
+// nq dividing the 8 XCDs, the workgroups of one XCD share a queue over a
+// contiguous stretch of the reads), else the first queue after it with slices
+// left; n_slices when none is.  One queue for all waves made its counter the
+// launch's serialisation point: ~11 ns per grab, 4.5 ms of a 100 M-read launch
+// with IsizeHist alone (profiles/r06/r06s_scan_queues_ab.txt).  Reading a
+// counter before its atomic (MC_SCAN_QPEEK) cost a round trip per grab.
+constexpr int kQueueStride = 32;   // counters 128 bytes apart
+__device__ __forceinline__ unsigned take_slice(const ScanArgs& a, int home) {
+    for (int k = 0; k < a.nq; ++k) {
+        const int q = home + k < a.nq ? home + k : home + k - a.nq;
+        const unsigned lo = (unsigned)q * a.per_q;
+        if (lo >= a.n_slices) continue;
+        const unsigned cnt = min(a.per_q, a.n_slices - lo);
+        unsigned* ctr = a.work + q * kQueueStride;
+        if (MC_SCAN_QPEEK && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cnt) continue;
+        const unsigned t = atomicAdd(ctr, 1u);
+        if (t < cnt) return lo + t;
+    }
+    return a.n_slices;
+}
+
 __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a) {
     extern __shared__ uint32_t lds_[];
     lds_u32* lds = (lds_u32*)lds_;
@@ -745,7 +780,7 @@ __global__ __launch_bounds__(kThreads, MC_SCAN_OCC) void scan_kernel(ScanArgs a)
     for (int64_t c = gw;;) {
         if (a.work) {
             unsigned t = 0;
-            if (lane == 0) t = atomicAdd(a.work, 1u);
+            if (lane == 0) t = take_slice(a, (int)(blockIdx.x % (unsigned)a.nq));
             c = __shfl((int)t, 0, 64);
         }
         int64_t r0 = c * a.per_wave;
@@ -1230,8 +1265,12 @@ int launch(mc_scan* s, int64_t n, const int32_t* rlen, const int32_t* flag, cons
     a.per_wave = (batches + waves - 1) / waves * 64;
     if (MC_SCAN_DYN && a.per_wave > 64) {
         a.per_wave = std::min<int64_t>(a.per_wave, kScanSlice);
-        HIP_TRY(s->work.reserve(1));
-        HIP_TRY(hipMemsetAsync(s->work.p, 0, 4, s->stream));
+        const int64_t slices = (n + a.per_wave - 1) / a.per_wave;
+        a.nq = (int32_t)std::max<int64_t>(1, std::min<int64_t>(MC_SCAN_QUEUES, slices));
+        a.n_slices = (uint32_t)slices;
+        a.per_q = (uint32_t)((slices + a.nq - 1) / a.nq);
+        HIP_TRY(s->work.reserve((size_t)a.nq * kQueueStride));
+        HIP_TRY(hipMemsetAsync(s->work.p, 0, (size_t)a.nq * kQueueStride * 4, s->stream));
         a.work = s->work.p;
     }
     const size_t lds_bytes = (size_t)a.stage_off * 4 + (size_t)kWaves * kStageBytes + kIncTabWords * 4 +
