@@ -728,3 +728,16 @@ def test_device_read_pass_equals_host_pass(tmp_path, lib_built, monkeypatch):
                     monkeypatch.delenv("MC_EXP_READS", raising=False)
                     for a, b, reg in zip(outs[0], outs[1], regions):
                         assert repr(a) == repr(b), (name, k, kcor is None, reg)
+                # the device pass keeps its buffers with the table: region sets
+                # that shrink and grow between calls on it
+                for sub in (regions[:2], regions, regions[3:5], regions[::-1]):
+                    outs = []
+                    for mode in ("gpu", "host"):
+                        if mode == "host":
+                            monkeypatch.setenv("MC_EXP_READS", "host")
+                        else:
+                            monkeypatch.delenv("MC_EXP_READS", raising=False)
+                        res = mx.experimental_batch(t, kc, k, None, sub)
+                        outs.append([(r.row, repr(r.error), r.zero_lines) for r in res])
+                    monkeypatch.delenv("MC_EXP_READS", raising=False)
+                    assert repr(outs[0]) == repr(outs[1]), (name, k, len(sub))
