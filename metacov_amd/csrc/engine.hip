@@ -7,6 +7,7 @@
 //           64 positions)
 //   depth   int32[n_chunks * chunk_w]    all contigs back to back
 //   index   int64 chunk_first[n_chunks]  first read of each chunk (with halo)
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -615,6 +616,15 @@ extern "C" int mc_clear_reads(mc_ctx* ctx) {
 #ifndef MC_STEP_EVENTS
 #define MC_STEP_EVENTS 1
 #endif
+// MC_EXT_EVENTS 1: a fused call's timing events ride on its launches
+// (hipExtLaunchKernel's start / stop events) instead of four hipEventRecord
+// calls (the one before the probe sits between a call's entry and its first
+// launch).  Back-to-back calls ran slower that way: C2 0.0821 -> 0.0870 ms,
+// C3 1.0549 -> 1.0588, one N = 8 share 0.1827 -> 0.1858
+// (profiles/r06/r06w_ab_*).
+#ifndef MC_EXT_EVENTS
+#define MC_EXT_EVENTS 0
+#endif
 static float elapsed(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
@@ -975,7 +985,7 @@ static int prepare_direct(mc_ctx* ctx) {
     if (int rc = run_k1(ctx)) return rc;
     // the prepare's span: this event to K2's start event (probe + window)
     auto& T = ctx->ts[ctx->ts_cur];
-    if (MC_STEP_EVENTS) HIP_TRY(hipEventRecord(T.e[0], s));
+    if (MC_STEP_EVENTS && !MC_EXT_EVENTS) HIP_TRY(hipEventRecord(T.e[0], s));
     T.prep = true;
     ctx->ring = kRing;
     ctx->short_max = ctx->ring - kTileW;
@@ -999,8 +1009,8 @@ static int prepare_direct(mc_ctx* ctx) {
                 ctx->d_jidx.p + 2 * (n_base + 1), ctx->d_fsamp.p,
                 ctx->d_dres.p, ++ctx->direct_gen};
     const int64_t M = (n + kProbeStride - 1) >> kProbeShift;
-    hipLaunchKernelGGL(probe_kernel, dim3((unsigned)std::max<int64_t>(1, (M + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, s, P);
+    hipExtLaunchKernelGGL(probe_kernel, dim3((unsigned)std::max<int64_t>(1, (M + kBlock - 1) / kBlock)),
+                          dim3(kBlock), 0, s, MC_STEP_EVENTS && MC_EXT_EVENTS ? T.e[0] : nullptr, nullptr, 0, P);
     HIP_TRY(hipGetLastError());
     HIP_TRY(ctx->d_depth.reserve((size_t)(ctx->n_chunks * ctx->chunk_w)));
     ctx->has_long = false;
@@ -1197,7 +1207,9 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
         HIP_TRY(hipMemsetAsync(ctx->d_queue.p, 0, 32, s));
         HIP_TRY(hipMemsetAsync(ctx->d_maxdepth.p, 0, 16, s));
     }
-    if (MC_STEP_EVENTS || !ea) HIP_TRY(hipEventRecord(ea ? ea : ctx->ev[4], s));
+    hipEvent_t k2_start = MC_STEP_EVENTS || !ea ? (ea ? ea : ctx->ev[4]) : nullptr;
+    hipEvent_t k2_stop = MC_STEP_EVENTS || !eb ? (eb ? eb : ctx->ev[5]) : nullptr;
+    if (!MC_EXT_EVENTS && k2_start) HIP_TRY(hipEventRecord(k2_start, s));
     const int64_t* toff = ctx->has_long ? ctx->d_tile_off.p : nullptr;
     const int32_t* tev = ctx->has_long ? ctx->d_tile_ev.p : nullptr;
     const int* ccar = ctx->has_long ? ctx->d_chunk_carry.p : nullptr;
@@ -1219,7 +1231,8 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     if (int rc = k2_consts(ctx, kc, &dk)) return rc;
     const int win_parity = (int)(ctx->direct_gen & 1);
 #define MC_LAUNCH_K2(S, L, D)                                                                  \
-    hipLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kK2Block), lds, s, kc.A, dk,  \
+    hipExtLaunchKernelGGL((depth_kernel<S, L, D>), dim3(grid), dim3(kK2Block), (uint32_t)lds, s,        \
+                          MC_EXT_EVENTS ? k2_start : nullptr, MC_EXT_EVENTS ? k2_stop : nullptr, 0u, kc.A, dk, \
                        ctx->n_reads, ctx->d_coff.p,                                               \
                        cfirst, cstride, nch, tpc, ctx->short_max,                                \
                        toff, tev, ccar, ctx->d_depth.p, ctx->d_queue.p, ctx->d_maxdepth.p,        \
@@ -1235,7 +1248,7 @@ static int launch_depth(mc_ctx* ctx, const FusedRegions& fr, hipEvent_t ea = nul
     }
 #undef MC_LAUNCH_K2
     HIP_TRY(hipGetLastError());
-    if (MC_STEP_EVENTS || !eb) HIP_TRY(hipEventRecord(eb ? eb : ctx->ev[5], s));
+    if (!MC_EXT_EVENTS && k2_stop) HIP_TRY(hipEventRecord(k2_stop, s));
     ctx->t_depth = ea == nullptr;   // else the caller's set carries the time
     ctx->t.depth_launches += 1;
     ctx->depth_valid = true;
@@ -1625,9 +1638,12 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
         ctx->fb_calls += 1;
     }
     // one wave per region; flags [0, R) and K2's max depth [R] land in mapped host memory
+    // the call's end event: on its last kernel (MC_EXT_EVENTS)
+    hipEvent_t k3_stop = MC_STEP_EVENTS && MC_EXT_EVENTS ? T.e[3] : nullptr;
 #define MC_LAUNCH_K3B(V)                                                                           \
-    hipLaunchKernelGGL(region_final_wave_kernel<V>, dim3((unsigned)((R + kWaves - 1) / kWaves)),        \
-                       dim3(kBlock), 0, s, ctx->d_fhist.p, R, ctx->d_acc.p,                          \
+    hipExtLaunchKernelGGL(region_final_wave_kernel<V>, dim3((unsigned)((R + kWaves - 1) / kWaves)),     \
+                          dim3(kBlock), 0u, s, nullptr, devfb ? nullptr : k3_stop, 0u,                   \
+                          ctx->d_fhist.p, R, ctx->d_acc.p,                                              \
                        reinterpret_cast<const int64_t*>(d + o_ntot),                                \
                        reinterpret_cast<const int64_t*>(d + o_nzx), d_out, ctx->h_fflag.d,           \
                        reinterpret_cast<const int32_t*>(d + o_brow), ctx->d_flow.p,                 \
@@ -1644,10 +1660,10 @@ static int depth_stats_launch(mc_ctx* ctx, int64_t R, const int32_t* tid, const 
     if (devfb) {
         hipLaunchKernelGGL(fb_seg_kernel, dim3(1024), dim3(kBlock), (size_t)kLdsBins * 4, s, F);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(fb_final_kernel, dim3(kFbSlots), dim3(kBlock), 0, s, F);
+        hipExtLaunchKernelGGL(fb_final_kernel, dim3(kFbSlots), dim3(kBlock), 0u, s, nullptr, k3_stop, 0u, F);
         HIP_TRY(hipGetLastError());
     }
-    if (MC_STEP_EVENTS) HIP_TRY(hipEventRecord(T.e[3], s));
+    if (MC_STEP_EVENTS && !MC_EXT_EVENTS) HIP_TRY(hipEventRecord(T.e[3], s));
     if ((MC_DONE_MODE == 0 || (MC_DONE_MODE == 1 && devfb)) && ctx->stamp_ok && hipStreamWriteValue64(s, ctx->h_done.d, seq, 0) != hipSuccess) {
         (void)hipGetLastError();
         ctx->stamp_ok = false;
