@@ -113,6 +113,13 @@ constexpr int64_t kScanSlice = MC_SCAN_SLICE;   // reads per queued slice (MC_SC
 #ifndef MC_SCAN_KMER8
 #define MC_SCAN_KMER8 1
 #endif
+//   MC_SCAN_MISM8  BaseHist's mismatch test 8 bases at a time (mism8; 0: per
+//                  base, the compiler's unrolled byte compares).  Slower: all
+//                  four 14.09 -> 14.19 ms, BaseHist alone 10.65 -> 10.77
+//                  (profiles/r06/r06x_scan_mism8_ab.txt)
+#ifndef MC_SCAN_MISM8
+#define MC_SCAN_MISM8 0
+#endif
 //   MC_SCAN_QUEUES slice queues (take_slice).  100 M reads, ms for IsizeHist
 //                  alone / KmerHist alone / all four: 1 queue 4.53 / 5.29 /
 //                  14.22, 2: 2.37 / 3.58 / 14.11, 4: 1.32 / 3.54 / 14.05,
@@ -241,6 +248,29 @@ struct RefWin {
         hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
     }
 };
+
+// BaseHist's mismatches of 8 packed bases (w, BAM order) against the
+// reference's nt4 bytes lo (positions 0-3) / hi (4-7), the first n8 only:
+// nt4 of every nibble at once (the kmer8 arithmetic; a nibble that is not
+// A/C/G/T becomes 4, the reference's N code), spread to bytes, compared by
+// XOR, the non-zero bytes counted.
+__device__ __forceinline__ int mism8(uint32_t w, uint32_t lo, uint32_t hi, int n8) {
+    constexpr uint32_t M1 = 0x11111111u, B1 = 0x01010101u;
+    w = ((w >> 4) & 0x0F0F0F0Fu) | ((w & 0x0F0F0F0Fu) << 4);   // base j at nibble j
+    const uint32_t t0 = w & M1, t1 = (w >> 1) & M1, t2 = (w >> 2) & M1, t3 = (w >> 3) & M1;
+    const uint32_t f = (t0 + t1 + t2 + t3) ^ M1;                // non-zero: not one bit set
+    const uint32_t fb = (f | (f >> 1) | (f >> 2)) & M1;
+    const uint32_t n = (((t1 | t3) | ((t2 | t3) << 1)) & ~(fb * 3u)) | (fb << 2);
+    auto spread = [](uint32_t x) {   // nibbles 0-3 -> bytes 0-3
+        x &= 0xFFFFu;
+        x = (x | (x << 8)) & 0x00FF00FFu;
+        return (x | (x << 4)) & 0x0F0F0F0Fu;
+    };
+    const uint32_t dl = spread(n) ^ lo, dh = spread(n >> 16) ^ hi;
+    const uint32_t ml = n8 >= 4 ? B1 : ((1u << (8 * n8)) - 1u) & B1;
+    const uint32_t mh = n8 >= 8 ? B1 : n8 <= 4 ? 0u : ((1u << (8 * (n8 - 4))) - 1u) & B1;
+    return __builtin_popcount((dl | (dl >> 1) | (dl >> 2)) & ml) + __builtin_popcount((dh | (dh >> 1) | (dh >> 2)) & mh);
+}
 
 // KmerHist's code of the K <= 8 bases b .. b+K-1 of a read (forward), or of
 // comp(b+K-1) .. comp(b) (reverse strand: base j of the k-mer is the read's
@@ -376,10 +406,14 @@ __device__ __forceinline__ bool process_read(const ScanArgs& a, int64_t r, P8 s,
                 const int n8 = min(8, rlen - 8 * k);
                 uint32_t lo, hi;
                 rw.at8(b0 + 8 * k, lo, hi);
+                if (MC_SCAN_MISM8) {
+                    mism += mism8(w, lo, hi, n8);
+                } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int rv = (int)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 255u);
-                    mism += (j < n8) & (nt4_of(nib8(w, j)) != rv);
+                    for (int j = 0; j < 8; ++j) {
+                        const int rv = (int)(((j < 4 ? lo : hi) >> (8 * (j & 3))) & 255u);
+                        mism += (j < n8) & (nt4_of(nib8(w, j)) != rv);
+                    }
                 }
             }
         } else {
