@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -1972,11 +1973,11 @@ static int cap_max_span(hipStream_t s, const int32_t* span, int64_t n, int* d_tm
 static int cap_walk(hipStream_t s, const int32_t* pos, int32_t* span, const uint8_t* inq, const int64_t* d_seg,
                     int64_t n_seg, int max_depth, int max_span, uint8_t* keep, int zero,
                     unsigned long long* d_dropped) {
-    static bool attr = false;
-    if (!attr) {
+    static std::atomic<bool> attr{false};   // (engines on several host threads)
+    if (!attr.load(std::memory_order_acquire)) {
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(cap_walk_kernel),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kCapLdsBytes));
-        attr = true;
+        attr.store(true, std::memory_order_release);
     }
     if (n_seg <= 0) return MC_OK;
     hipLaunchKernelGGL(cap_walk_kernel, dim3((unsigned)n_seg), dim3(64), (size_t)kCapLdsBytes, s, pos, span, inq,
