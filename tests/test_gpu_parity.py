@@ -683,6 +683,49 @@ def test_fused_repeated_calls_reuse_and_invalidate(eng):
     check(whole, d2, ext2, coff2)
 
 
+def test_engines_on_two_threads(lib_built):
+    """Two contexts driven from two host threads at once (their own streams
+    and buffers; the calls release the GIL), each over a different batch
+    with the direct step repeated (invalidate + fused call): every row equals
+    the oracle's (scripts/bench_streams.py measures what it buys)."""
+    import threading
+    from metacov_amd.engine import CoverageEngine
+    cases = [make_case([80_000, 50_000, 120_000], 60_000, (1, 300), 31),
+             make_case([200_000, 7_000], 90_000, (1, 700), 32)]
+    engines, wants, regs = [], [], []
+    for lengths, tid, pos, span in cases:
+        e = CoverageEngine(0)
+        e.set_contigs(lengths)
+        e.add_reads(tid, pos, span)
+        engines.append(e)
+        d, ext, coff = coracle.depth(lengths, tid, pos, span)
+        r = _tiling(np.random.default_rng(len(lengths)), lengths, 7)
+        regs.append(r)
+        wants.append(coracle.region_stats(d, ext, coff, *r))
+    got = [[], []]
+    errors = []
+
+    def loop(i):
+        try:
+            for _ in range(12):
+                engines[i].invalidate()
+                got[i].append(engines[i].compute_depth_stats(*regs[i]))
+        except Exception as ex:   # noqa: BLE001 (reported below)
+            errors.append(ex)
+
+    ths = [threading.Thread(target=loop, args=(i,)) for i in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    for i in range(2):
+        assert len(got[i]) == 12
+        for g in got[i]:
+            for f in wants[i].dtype.names:
+                assert np.array_equal(g[f], wants[i][f]), (i, f)
+
+
 def test_fused_timing_totals(eng):
     """mc_timings.fused_*_total: each fused call adds its K2 and K3b event
     times (what bench.py averages over the timed steps)."""
