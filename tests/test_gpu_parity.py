@@ -1429,10 +1429,11 @@ def test_direct_and_full_fuzz(lib_built):
     """Random batches through one ctx (the direct path with its halo carried
     from batch to batch, the full prepare for long reads and overhangs):
     depth, whole-contig fused rows and random-region rows equal the oracle."""
-    rng = np.random.default_rng(2024)
+    # (MC_FUZZ_ITERS / MC_FUZZ_SEED: longer soak runs, profiles/r06/r06soak_*)
+    rng = np.random.default_rng(int(os.environ.get("MC_FUZZ_SEED", "2024")))
     e = _fresh(lib_built)
     try:
-        for k in range(24):
+        for k in range(int(os.environ.get("MC_FUZZ_ITERS", "24"))):
             lengths, tid, pos, span = _fuzz_batch(rng)
             e.set_contigs(lengths)
             e.add_reads(tid, pos, span)
