@@ -4,6 +4,8 @@ bam_plp_push / bam_plp_next loop (oracle/htslib_plp.py), per region query
 the way pysam's AlignmentFile.pileup(ref, start, end) runs it
 (metacov/pileup.py:13).  Parity with htslib itself is unpinned (htslib is
 absent here and the cap is version-dependent)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -222,6 +224,31 @@ def test_device_cap_mask_matches_host(lib_built):
     bad[5], bad[6] = bad[6] + 1, bad[5]
     with pytest.raises(Exception, match="sorted"):
         depthcap.cap_mask_device(*(torch.from_numpy(a).cuda() for a in (tid, bad, span)), 40)
+
+
+@pytest.mark.gpu
+def test_device_cap_mask_random_sets(lib_built):
+    """Random query sets (1-30 contigs of random piles, background depth,
+    span-0 share and cap from 1 to 9000): the device mask and drop count
+    equal mc_depth_cap_mask's.  MC_CAP_SOAK_ITERS / MC_CAP_SOAK_SEED: soak
+    runs (profiles/r06/r06soak_cap.txt)."""
+    import torch
+    rng = np.random.default_rng(int(os.environ.get("MC_CAP_SOAK_SEED", "77")))
+    for _ in range(int(os.environ.get("MC_CAP_SOAK_ITERS", "4"))):
+        tids, poss, spans = [], [], []
+        for t in range(int(rng.integers(1, 31))):
+            pos, span = piles(rng, int(rng.integers(1, 6)), int(rng.integers(5, 3000)), int(rng.integers(0, 400)),
+                              int(rng.integers(800, 9000)), (int(rng.integers(0, 2)), int(rng.integers(2, 400))))
+            span[rng.random(len(span)) < rng.random() * 0.3] = 0
+            tids.append(np.full(len(pos), t, np.int32))
+            poss.append(pos)
+            spans.append(span)
+        tid, pos, span = (np.concatenate(x) for x in (tids, poss, spans))
+        cap = int(rng.choice([1, 2, 7, 50, 300, 2000, 8000, 9000]))
+        want, wd = depthcap.cap_mask(tid, pos, span, cap)
+        got, gd = depthcap.cap_mask_device(*(torch.from_numpy(a).cuda() for a in (tid, pos, span)), cap)
+        assert gd == wd, cap
+        assert np.array_equal(got.cpu().numpy().astype(bool), want), cap
 
 
 @pytest.mark.gpu
