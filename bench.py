@@ -63,6 +63,10 @@ def parse(argv=None):
     ap.add_argument("--dump-rows", default=None, metavar="PATH",
                     help="rank 0 saves the (gathered) region rows of the last step, in region "
                          "order, as a .npy (tests compare them with the oracle)")
+    ap.add_argument("--exchange-every", type=int, default=8, metavar="G",
+                    help="N > 1: the region tables of G consecutive steps leave in one all-gather "
+                         "(one collective per step cost the N = 8 share ~20 us of host time per "
+                         "step: profiles/r06/r06zg_exchange_cost.txt)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -379,19 +383,22 @@ def main():
     xbufs = coll_bufs = gouts = gidx = None
     works = [None, None]   # in-flight all-gathers, one per exchange buffer
     n_calls = [0]
+    G = max(1, args.exchange_every)   # steps per all-gather
+    last = [None]          # (buffer, slot) the last step wrote; ungathered[0]: its group is not sent yet
+    ungathered = [False]
     if ex:
         # two exchange buffers, allocated once: [r_max, 9 stats]; the engine
         # writes a batch's rows straight into the first R of one (no copy per
         # step) while the previous batch's all-gather may still read the other,
         # and the rows' original region indices are gathered once here
-        xbufs = [torch.full((r_max, 9), -1, dtype=torch.int64, device=dev) for _ in range(2)]
+        xbufs = [torch.full((G * r_max, 9), -1, dtype=torch.int64, device=dev) for _ in range(2)]
         ibuf = torch.full((r_max, 1), -1, dtype=torch.int64, device=coll_dev)
         ibuf[:R, 0] = torch.from_numpy(np.asarray(region_index, np.int64)).to(coll_dev)
         gidx = torch.empty((world * r_max, 1), dtype=torch.int64, device=coll_dev)
         dist.all_gather_into_tensor(gidx, ibuf)
-        coll_bufs = [x if coll_dev == dev else torch.empty((r_max, 9), dtype=torch.int64, device=coll_dev)
+        coll_bufs = [x if coll_dev == dev else torch.empty((G * r_max, 9), dtype=torch.int64, device=coll_dev)
                      for x in xbufs]
-        gouts = [torch.empty((world * r_max, 9), dtype=torch.int64, device=coll_dev) for _ in range(2)]
+        gouts = [torch.empty((world * G * r_max, 9), dtype=torch.int64, device=coll_dev) for _ in range(2)]
 
     def step(fresh):
         """One pass of the hot path over the resident batch.  fresh: the
@@ -400,21 +407,21 @@ def main():
         K3b; otherwise K2 reuses the index an explicit prepare() built.
         For N > 1 the batch's rows leave in an asynchronous all-gather that
         runs under the next batch's kernels; drain() waits for the last."""
-        nonlocal gathered
-        i = n_calls[0] & 1
+        k = n_calls[0]
         n_calls[0] += 1
+        i, slot = (k // G) & 1, k % G
         tbl = table
         if ex:
-            if works[i] is not None:   # this buffer's previous gather must be done
+            if slot == 0 and works[i] is not None:   # this buffer's previous gather must be done
                 works[i].wait()
                 # RCCL: wait() only orders torch's current stream after the
                 # gather; the engine writes the buffer on its own stream, so
-                # the host waits for the gather itself (done two steps ago,
+                # the host waits for the gather itself (done two groups ago,
                 # normally: one event query)
                 while coll_dev.type == "cuda" and not works[i].is_completed():
                     time.sleep(0)
                 works[i] = None
-            tbl = xbufs[i][:R]
+            tbl = xbufs[i][slot * r_max:slot * r_max + R]
         if args.cigar:   # a fresh raw-CIGAR batch: K1 + prepare run inside this step
             eng.clear_reads()
             eng.add_reads_cigar_device(tid, pos, cig_off, cigar)
@@ -425,13 +432,23 @@ def main():
             eng.region_stats_device(rt, rs, re_, tbl.data_ptr())
         else:
             eng.compute_depth_stats_device(rt, rs, re_, tbl.data_ptr())
-        if ex:   # the rows are in the exchange buffer already: one all-gather
-            if coll_bufs[i] is not xbufs[i]:   # (gloo: through host memory)
-                coll_bufs[i].copy_(xbufs[i])
-            works[i] = dist.all_gather_into_tensor(gouts[i], coll_bufs[i], async_op=True)
-            gathered = gouts[i]
+        if ex:   # the rows are in the exchange buffer already: one all-gather per G steps
+            last[0] = (i, slot)
+            ungathered[0] = True
+            if slot == G - 1:
+                send(i)
+
+    def send(i):
+        nonlocal gathered
+        if coll_bufs[i] is not xbufs[i]:   # (gloo: through host memory)
+            coll_bufs[i].copy_(xbufs[i])
+        works[i] = dist.all_gather_into_tensor(gouts[i], coll_bufs[i], async_op=True)
+        gathered = gouts[i]
+        ungathered[0] = False
 
     def drain():
+        if ex and ungathered[0]:   # a partly filled group (its other slots: an older group's rows)
+            send(last[0][0])
         for j, w in enumerate(works):
             if w is not None:
                 w.wait()
@@ -512,7 +529,9 @@ def main():
         b = torch.tensor([bases], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(b)
         total_bases = int(b.item())
-        full = torch.cat([gathered, gidx], dim=1)   # [world * r_max, 9 stats + region index]
+        # the last step's rows: slot s of every rank's G-step block
+        mine = gathered.view(world, G, r_max, 9)[:, last[0][1]].reshape(world * r_max, 9)
+        full = torch.cat([mine, gidx], dim=1)   # [world * r_max, 9 stats + region index]
         rows = mdist.unpack_rows(full.cpu().numpy(), n_regions_total, REGION_STAT_DTYPE)
         assert int(rows["sum"].sum()) == total_bases, "gathered region table lost bases"
     else:
@@ -630,7 +649,8 @@ def main():
             "world_size": world,
             "ranks_seen": dist.get_world_size() if ex else 1,
             "backend": (args.backend if ex else None),
-            "allgather_ms": allgather_ms,
+            "allgather_ms": allgather_ms,   # one all-gather of a G-step group of region tables
+            "exchange_every": (G if ex else None),
         }
         if t_max_re is not None:
             line["reused_index"] = {
