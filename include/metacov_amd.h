@@ -94,6 +94,13 @@ const char* mc_version(void);
  * (metacov_amd/build.py rebuilds when the tree's hash differs). */
 const char* mc_build_id(void);
 
+/* The HIP runtime and device `device`'s context, initialised ahead of the
+ * first mc_ctx_create (which does it anyway): the CLI calls it on a thread
+ * while Python imports its modules, so the two start-up costs overlap
+ * (nothing in the reference; pysam has no device to initialise).  A device
+ * out of range initialises the runtime only. */
+int mc_runtime_init(int device);
+
 /* ---- context ------------------------------------------------------------ */
 int mc_ctx_create(int device, mc_ctx** out);
 int mc_ctx_destroy(mc_ctx* ctx);

@@ -83,6 +83,7 @@ SIGNATURES = {
     "mc_last_error": [],
     "mc_version": [],
     "mc_build_id": [],
+    "mc_runtime_init": [ctypes.c_int],
     "mc_ctx_create": [ctypes.c_int, _PP],
     "mc_ctx_destroy": [_P],
     "mc_ctx_set_stream": [_P, _P],

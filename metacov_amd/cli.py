@@ -25,17 +25,48 @@ keeps its shard).  Each rank reduces the regions on its contigs; one
 all-gather of the region table (RCCL; MC_DIST_BACKEND=gloo for a CPU
 rehearsal) brings the rows to rank 0, which writes the same CSV.
 """
-import csv
-import json
-import logging
 import os
 import sys
 import time
 
-import click
-import numpy as np
 
-from . import depthcap as _depthcap
+def _prewarm_hip():
+    """`python -m metacov_amd.cli` (one process): the HIP runtime and the
+    device context are initialised on a thread while the imports below run
+    (the library's calls release the GIL); mc_ctx_create then finds them
+    done.  MC_CLI_PREWARM=0 turns it off."""
+    if os.environ.get("MC_CLI_PREWARM", "1") == "0" or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return
+    argv = sys.argv[1:]
+    device = 0
+    if "--device" in argv[:-1]:
+        try:
+            device = int(argv[argv.index("--device") + 1])
+        except ValueError:
+            pass
+
+    def run():
+        try:
+            from metacov_amd import _lib
+            _lib.load().mc_runtime_init(device)
+        except Exception:   # noqa: BLE001 (the real calls report it)
+            pass
+
+    import threading
+    threading.Thread(target=run, name="hip-prewarm", daemon=True).start()
+
+
+if __name__ == "__main__":
+    _prewarm_hip()
+
+import csv  # noqa: E402
+import json  # noqa: E402
+import logging  # noqa: E402
+
+import click  # noqa: E402
+import numpy as np  # noqa: E402
+
+from . import depthcap as _depthcap  # noqa: E402
 from . import experimental as _experimental
 from . import regions as _regions
 from . import scan as _scan
