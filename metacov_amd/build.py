@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmetacov_amd.so")
 SOURCES = ["engine.hip", "ecor.hip", "scan.hip", "bam_gpu.hip", "exp_gpu.hip", "bam_decode.cpp", "bam_index.cpp",
-           "bam_write.cpp", "exp_reads.cpp", "scan_src.cpp", "depth_cap.cpp", "common.cpp"]
+           "bam_write.cpp", "exp_reads.cpp", "scan_src.cpp", "depth_cap.cpp", "common.cpp", "runtime.cpp"]
 HEADERS = ["kernels.h", "npstd.h", "capmask.h", "exp_gpu.h", "common.h", "bgzf.h", "inflate.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",

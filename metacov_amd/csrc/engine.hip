@@ -324,18 +324,6 @@ static void invalidate(mc_ctx* ctx) {
     ctx->max_depth = -1;
 }
 
-extern "C" int mc_runtime_init(int device) {
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    MC_REQUIRE(e == hipSuccess && n > 0, MC_E_HIP, "no HIP device available (hipGetDeviceCount: %s)",
-               hipGetErrorString(e));
-    if (device >= 0 && device < n) {   // the device's context (the first call on a device creates it)
-        HIP_TRY(hipSetDevice(device));
-        HIP_TRY(hipFree(nullptr));
-    }
-    return MC_OK;
-}
-
 extern "C" int mc_ctx_create(int device, mc_ctx** out) {
     MC_REQUIRE(out, MC_E_INVALID, "null out");
     *out = nullptr;
